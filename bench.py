@@ -1,0 +1,253 @@
+"""Benchmark: radar frames/s of the MI355X-native hot path (BASELINE.json metric).
+
+One step = one batch of synthetic RadarScenes-shaped frames, raw measurements
+already resident in HBM, through the whole hot path: kNN graph build + ball
+query, node / edge input features, node and edge encoders, L message-passing
+layers, the four task heads (graph_features.py:58-164 + gnn_detector.py:141-201).
+
+Default workload = BASELINE config 2: 64 frames x 3000 nodes per GPU, k = 32,
+L = 6, bf16 compute (fp32 accumulation / normalisation statistics), random-init
+weights of the yml architecture (no checkpoint is needed for throughput).
+Multi-GPU (torchrun, one process per GPU): every rank owns its own 64 frames
+(frame-parallel, weak scaling, no collective in the timed region; barrier +
+max-over-ranks timing only).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from graph_neural_network_for_radar_perception_amd import synthetic  # noqa: E402
+from graph_neural_network_for_radar_perception_amd.config import default_config  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, 'BASELINE.json')))['metric']
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}   # dense MFMA peaks (same doc)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--frames', type=int, default=64, help='frames per GPU')
+    p.add_argument('--nodes', type=int, default=3000)
+    p.add_argument('--k', type=int, default=32)
+    p.add_argument('--layers', type=int, default=6)
+    p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    p.add_argument('--cpu-frames', type=int, default=2, help='CPU baseline sample (frames)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--seed', type=int, default=synthetic.SEED0)
+    return p.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64,
+                     device='cuda' if torch.cuda.is_available() else 'cpu')
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64,
+                     device='cuda' if torch.cuda.is_available() else 'cpu')
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def rank_frame_seeds(rank: int, frames: int, seed0: int):
+    """Frames owned by a rank (weak scaling): seeds seed0 + rank*frames + f."""
+    return [seed0 + rank * frames + f for f in range(frames)]
+
+
+def make_model(cfg, device):
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    torch.manual_seed(1234)
+    m = Model_Training(cfg, device).to(device)
+    return m.pred.eval().requires_grad_(False)
+
+
+def event_durations(events):
+    """(name:start, name:end) event pairs -> {name: [ms, ...]}"""
+    out, open_ = {}, {}
+    for name, ev in events:
+        base, which = name.rsplit(':', 1)
+        if which == 'start':
+            open_[base] = ev
+        else:
+            out.setdefault(base, []).append(open_.pop(base).elapsed_time(ev))
+    return out
+
+
+def cpu_baseline(args, cfg):
+    """The oracle (numpy dense graph build + op-for-op torch fp32 forward, i.e. the
+    reference's own CPU algorithm) on a bounded sample of the same workload."""
+    from oracle import gnn_forward_ref, graph_features_ref as gref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = None
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    torch.manual_seed(1234)
+    model = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach() for k, v in model.state_dict().items()}
+    frames = [synthetic.make_frame(args.nodes, args.seed + 10**6 + i)
+              for i in range(args.cpu_frames + 1)]
+    times = []
+    gmax = float(np.sqrt(np.float64(cfg.max_x ** 2 + cfg.max_y ** 2)))
+    for i, fr in enumerate(frames):
+        t0 = time.perf_counter()
+        g = gref.build_frame_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points, gmax)
+        cl = [torch.from_numpy(c) for c in synthetic.cluster_lists(args.nodes)]
+        with torch.no_grad():
+            gnn_forward_ref.forward(sd, cfg, torch.from_numpy(g['node_features']),
+                                    torch.from_numpy(g['edge_features']),
+                                    torch.from_numpy(g['edge_index']),
+                                    torch.from_numpy(g['adj_matrix']), cl)
+        if i > 0:  # first frame = warm-up
+            times.append(time.perf_counter() - t0)
+    sec = float(np.median(times))
+    return {'value': round(1.0 / sec, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{len(times)} frame(s) of {args.nodes} nodes, k={args.k}, L={args.layers} '
+                      f'after 1 warm-up frame: oracle graph build (dense numpy, '
+                      f'graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
+                      f'{sec * 1e3:.0f} ms/frame, torch threads={threads}'}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    if not torch.cuda.is_available():
+        raise SystemExit('bench.py needs a HIP device')
+    dev = torch.device('cuda', local)
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+
+    cfg = default_config(graph_convolution_stem_channels=[64] * args.layers,
+                         k_number_nearest_points=args.k)
+    model = make_model(cfg, dev)
+    seeds = rank_frame_seeds(rank, args.frames, args.seed)
+    frames = [synthetic.make_frame(args.nodes, s) for s in seeds]
+    clusters = [synthetic.cluster_lists(args.nodes) for _ in seeds]
+    batch = FrameBatch.from_frames(frames, clusters, device=dev)
+    pipe = RadarGNNPipeline(model, cfg, args.dtype)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            gb, out = pipe.step(batch)
+        torch.cuda.synchronize()
+        E = int(gb.n_edges_dev.item())
+        # ---- timed region: K full steps -----------------------------------------
+        events = []
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            gb, out = pipe.step(batch, events=events)
+        torch.cuda.synchronize()
+        barrier(world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, world)
+        durs = event_durations(events)
+        # ---- forward only (graph + features already built) -----------------------
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            pipe.forward(batch, gb)
+        torch.cuda.synchronize()
+        fwd_elapsed = max_over_ranks(time.perf_counter() - t1, world)
+
+    frames_total = sum_over_ranks(args.frames * args.steps, world)
+    value = frames_total / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    N = args.frames * args.nodes
+    s = 2 if args.dtype == 'bf16' else 4
+    C = 64
+    kern = {}
+    for name, ms in durs.items():
+        kern[name] = {'avg_ms': round(float(np.mean(ms)), 4), 'launches_per_step':
+                      len(ms) // args.steps}
+    # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
+    msg_ms = float(np.mean(durs['message_chain']))
+    msg_flops = 65536.0 * E                              # 2*(192*128+128*64) per edge
+    msg_bytes = E * (3 * C * s + C * s + 8)              # x_i, x_j, e read; msg write; 2 int32 idx
+    msg_tf = msg_flops / (msg_ms * 1e-3) / 1e12
+    msg_gbs = msg_bytes / (msg_ms * 1e-3) / 1e9
+    agg_ms = float(np.mean(durs['segment_reduce']))
+    agg_bytes = E * C * s + N * C * s + (N + 1) * 4     # SURVEY §8(d) B_agg
+    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    enc_ms = float(np.mean(durs['edge_encoder']))
+    enc_flops = 118272.0 * E
+    kern['message_chain'].update(algorithmic_tflops=round(msg_tf, 2),
+                                 algorithmic_gbs=round(msg_gbs, 1),
+                                 flops_per_launch=msg_flops, bytes_per_launch=msg_bytes)
+    kern['segment_reduce'].update(algorithmic_gbs=round(agg_gbs, 1), bytes_per_launch=agg_bytes,
+                                  hbm_frac=round(agg_gbs / HBM_PEAK_GBS, 4))
+    kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2))
+    frac_mfma = msg_tf / MFMA_PEAK_TFLOPS[args.dtype]
+    frac_hbm = msg_gbs / HBM_PEAK_GBS
+    if frac_mfma >= frac_hbm:
+        roof = {'kernel': 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)',
+                'bound': 'mfma', 'achieved': round(msg_tf, 2),
+                'peak': MFMA_PEAK_TFLOPS[args.dtype], 'unit': 'TFLOP/s',
+                'frac': round(frac_mfma, 4), 'traffic': None}
+    else:
+        roof = {'kernel': 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)',
+                'bound': 'hbm', 'achieved': round(msg_gbs, 1), 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': None}
+    line = {
+        'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
+        'data': 'synthetic RadarScenes-shaped frames (SURVEY.md §8(d), seeded), random-init '
+                'weights of the yml architecture',
+        'config': {'workload': f'BASELINE config 2: {args.frames} frames x {args.nodes} nodes per '
+                               f'GPU, k={args.k}, L={args.layers}; step = kNN/ball graph build + '
+                               'node/edge features + encoders + message passing + 4 heads',
+                   'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes, 'k': args.k,
+                   'layers': args.layers, 'edges_per_gpu': E,
+                   'parallelism': f'frame-parallel x{world} (no collective in the step)'},
+        'forward_only_frames_per_s': round(frames_total / fwd_elapsed, 2),
+        'roofline': roof,
+        'kernels': kern,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(args, cfg)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,123 @@
+"""ctypes binding of libradargnn.so -- the C ABI declared in include/radar_gnn.h.
+
+The library is built in-tree (``build.py``) and loaded from
+``graph_neural_network_for_radar_perception_amd/lib/libradargnn.so``.  There is
+no fallback: if the library is missing or fails to load, every entry point
+raises ``NativeLibraryError``.
+
+Calls take ``torch.Tensor`` arguments only for convenience at this layer; they
+are reduced to raw device pointers (``data_ptr()``) and sizes before crossing
+the boundary, and every call is enqueued on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import Optional
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, 'lib', 'libradargnn.so')
+HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
+
+RG_F32, RG_BF16 = 0, 1
+ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
+GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2
+REDUCE = {'add': 0, 'sum': 0, 'mean': 1, 'max': 2}
+IN_DENSE, IN_CONCAT2, IN_GATHER3, IN_PAIRADD = 0, 1, 2, 3
+MAX_LAYERS = 8
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class rg_layer(ctypes.Structure):
+    _fields_ = [('w_packed', ctypes.c_void_p), ('norm_mu', ctypes.c_void_p),
+                ('norm_std', ctypes.c_void_p), ('in_dim', ctypes.c_int),
+                ('out_dim', ctypes.c_int), ('act', ctypes.c_int), ('pad_', ctypes.c_int)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_S = ctypes.c_size_t
+_D = ctypes.c_double
+_F = ctypes.c_float
+
+_SIGNATURES = {
+    'rg_last_error': (ctypes.c_char_p, []),
+    'rg_version': (_I, []),
+    'rg_build_graph_workspace_size': (_S, [_I, _I, _I, _I, _I]),
+    'rg_build_graph': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
+    'rg_node_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _P, _P]),
+    'rg_edge_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
+    'rg_link_pairs_workspace_size': (_S, [_I]),
+    'rg_link_pairs': (_I, [_P, _P, _I, _P, _P, _P, _L, _P, _P, _S, _P]),
+    'rg_pairs_from_edge_index_workspace_size': (_S, [_L]),
+    'rg_pairs_from_edge_index': (_I, [_P, _L, _P, _P, _P, _P, _S, _P]),
+    'rg_csr_rows': (_I, [_P, _I, _P, _P]),
+    'rg_csr_by_dst_workspace_size': (_S, [_I, _L]),
+    'rg_csr_by_dst': (_I, [_P, _L, _I, _P, _P, _P, _P, _S, _P]),
+    'rg_dense_adjacency': (_I, [_P, _P, _P, _P, _I, _P, _P, _P]),
+    'rg_i32_to_i64': (_I, [_P, _L, _P, _P]),
+    'rg_gather_rows_f32': (_I, [_P, _P, _L, _I, _P, _P]),
+    'rg_packed_linear_bytes': (_S, [_I, _I, _I]),
+    'rg_pack_linear': (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    'rg_mlp_chain': (_I, [_I, ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,
+                          _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
+    'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+}
+
+_lib = None
+_load_error: Optional[str] = None
+
+
+def header_functions() -> list:
+    """Names of every function declared in include/radar_gnn.h."""
+    with open(HEADER) as fh:
+        text = fh.read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(rg_[a-z0-9_]+)\s*\(', text)))
+
+
+def lib():
+    """The loaded library; raises NativeLibraryError when it is absent."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise NativeLibraryError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f'{LIB_PATH} not built: run `python -m '
+                       'graph_neural_network_for_radar_perception_amd.build` (hipcc, gfx950)')
+        raise NativeLibraryError(_load_error)
+    try:
+        handle = ctypes.CDLL(LIB_PATH)
+    except OSError as exc:  # pragma: no cover - environment dependent
+        _load_error = f'cannot load {LIB_PATH}: {exc}'
+        raise NativeLibraryError(_load_error) from exc
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().rg_last_error().decode(errors='replace')
+        raise RuntimeError(f'{what} failed (code {rc}): {msg}')
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> Optional[int]:
+    """Raw device pointer of a tensor (None stays None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()

@@ -1,0 +1,68 @@
+"""Build libradargnn.so (the HIP library behind the C ABI in include/radar_gnn.h).
+
+Compiles every ``csrc/*.hip`` for gfx950 only with ``hipcc`` and links one
+shared library in-tree at ``graph_neural_network_for_radar_perception_amd/lib/``
+(so it travels with the repository snapshot to the GPU box).  Objects are
+rebuilt only when a source or header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, 'csrc')
+LIBDIR = os.path.join(PKG, 'lib')
+OBJDIR = os.path.join(PKG, 'lib', 'obj')
+LIB = os.path.join(LIBDIR, 'libradargnn.so')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-Wall',
+         '-Wno-unused-function', '-Wno-unused-variable', '-I', os.path.join(REPO, 'include')]
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, '*.h')) + [os.path.join(REPO, 'include', 'radar_gnn.h')]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src, extra):
+    obj = os.path.join(OBJDIR, os.path.basename(src) + '.o')
+    if _stale(obj, [src] + _headers()):
+        cmd = [HIPCC] + FLAGS + extra + ['-c', src, '-o', obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed for {src}:\n{r.stdout}\n{r.stderr}')
+        if r.stderr.strip():
+            sys.stderr.write(r.stderr)
+    return obj
+
+
+def build_library(verbose: bool = False, extra_flags=None) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    extra = list(extra_flags or [])
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, extra), srcs))
+    if _stale(LIB, objs):
+        cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
+    if verbose:
+        print('built', LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    build_library(verbose=True)

@@ -1,0 +1,403 @@
+// Node / edge input features, link pairs, destination-major CSR, tensorization helpers.
+//
+//   rg_node_features  <- compute_node_features   graph_features.py:117-144 (+ normalize_time :47-55)
+//   rg_edge_features  <- compute_edge_features   graph_features.py:147-164
+//   rg_link_pairs     <- edge_formation triu/nonzero gnn_blocks.py:295-296
+//   rg_csr_by_dst     <- PyG's gather/scatter indexing of edge_index[1] (gnn_blocks.py:106)
+//   rg_dense_adjacency<- the dense adj_matrix / distance_mat of graph_features.py:80-84
+#include "rg_common.h"
+#include "scan.h"
+
+namespace rg {
+
+// ------------------------------------------------------------------ node features
+// One block per frame: frame min/max timestamp, then every node of the frame.
+// Arithmetic follows numpy-2 promotion of the reference expressions:
+//   t_norm     = float64(t - tmin) / float64(tmax - tmin)      (int64 / int64 -> f64)
+//   degree/10  = float64(deg) / 10
+//   r          = sqrtf(px*px + py*py)                           (float32)
+//   range_conf = (float64(r) - max_range) / (min_range - max_range)   (np.float64 scalars)
+//   th         = |atan2(py, px)| rounded to float32
+//   azi_conf   = (th - f32(max_az)) / f32(min_az - max_az)     (python-float scalars: weak -> f32)
+__global__ __launch_bounds__(256) void node_features_kernel(
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vr,
+    const float* __restrict__ rcs, const int64_t* __restrict__ ts, const int* __restrict__ deg,
+    const int* __restrict__ frame_ptr, double min_r, double max_r, float az_den, float max_az,
+    float* __restrict__ out) {
+  const int f = blockIdx.x;
+  const int b = frame_ptr[f], e = frame_ptr[f + 1];
+  __shared__ long long smin[256], smax[256];
+  long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000ULL;
+  for (int i = b + threadIdx.x; i < e; i += 256) {
+    long long t = ts[i];
+    mn = t < mn ? t : mn;
+    mx = t > mx ? t : mx;
+  }
+  smin[threadIdx.x] = mn;
+  smax[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = max(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  const long long tmin = smin[0], tmax = smax[0];
+  const double span = (double)(tmax - tmin);
+  for (int i = b + threadIdx.x; i < e; i += 256) {
+    const double tn = tmax == tmin ? (double)(ts[i] - tmin) : (double)(ts[i] - tmin) / span;
+    const double dg = (double)deg[i] / 10.0;
+    const float x = px[i], y = py[i];
+    const float r = __fsqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
+    const double rc = ((double)r - max_r) / (min_r - max_r);
+    const float th = fabsf((float)atan2((double)y, (double)x));
+    const float az = __fdiv_rn(__fsub_rn(th, max_az), az_den);
+    float* o = out + (size_t)i * 6;
+    o[0] = vr[i];
+    o[1] = rcs[i];
+    o[2] = (float)tn;
+    o[3] = (float)dg;
+    o[4] = (float)rc;
+    o[5] = az;
+  }
+}
+
+// ------------------------------------------------------------------ edge features
+// One thread per edge (src -> dst).  graph_features.py:153-161 in float32
+// (dx/10, dl = sqrt(dx^2+dy^2)/10, ...) and dt = float64(t_s - t_d) * 1e-6,
+// all cast to float32 as the tensorization does (datagen_gnn.py:121).
+__global__ __launch_bounds__(256) void edge_features_kernel(
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vx,
+    const float* __restrict__ vy, const int64_t* __restrict__ ts, const int* __restrict__ src,
+    const int* __restrict__ dst, const int* __restrict__ n_edges_dev, long n_edges,
+    float* __restrict__ out) {
+  const long E = n_edges_dev ? (long)*n_edges_dev : n_edges;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < E && p < n_edges; p += stride) {
+    const int s = src[p];
+    const int d = dst[p];
+    const float dx = __fdiv_rn(__fsub_rn(px[s], px[d]), 10.f);
+    const float dy = __fdiv_rn(__fsub_rn(py[s], py[d]), 10.f);
+    const float dl = __fdiv_rn(__fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))), 10.f);
+    const float dvx = __fsub_rn(vx[s], vx[d]);
+    const float dvy = __fsub_rn(vy[s], vy[d]);
+    const float dv = __fsqrt_rn(__fadd_rn(__fmul_rn(dvx, dvx), __fmul_rn(dvy, dvy)));
+    const float dt = (float)((double)(ts[s] - ts[d]) * 1e-6);
+    float* o = out + (size_t)p * 7;
+    o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;
+  }
+}
+
+// ------------------------------------------------------------------ link pairs
+__global__ void pairs_count(const int* __restrict__ row_ptr, const int* __restrict__ col,
+                            int n_nodes, int* __restrict__ cnt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  int lo = row_ptr[i], hi = row_ptr[i + 1];  // first position with col > i
+  const int end = hi;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (col[mid] <= i) lo = mid + 1; else hi = mid;
+  }
+  cnt[i] = end - lo;
+}
+
+__global__ __launch_bounds__(256) void pairs_emit(const int* __restrict__ row_ptr,
+                                                  const int* __restrict__ col, int n_nodes,
+                                                  const int* __restrict__ pair_ptr,
+                                                  int* __restrict__ ps, int* __restrict__ pd,
+                                                  long cap) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n_nodes; row += nw) {
+    const int e = row_ptr[row + 1];
+    const int q0 = pair_ptr[row], q1 = pair_ptr[row + 1];
+    if ((long)q1 > cap) continue;
+    const int n = q1 - q0;
+    const int start = e - n;  // cols > row are the row's suffix
+    for (int t = lane; t < n; t += 64) {
+      ps[q0 + t] = row;
+      pd[q0 + t] = col[start + t];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ CSR by destination
+__global__ void dst_count(const int64_t* __restrict__ ei, long E, int n_nodes,
+                          int* __restrict__ cnt, int* __restrict__ bad) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= E) return;
+  const int64_t s = ei[p], d = ei[E + p];
+  if (s < 0 || s >= n_nodes || d < 0 || d >= n_nodes) {
+    atomicOr(bad, 1);
+    return;
+  }
+  atomicAdd(cnt + d, 1);
+}
+
+__global__ void dst_fill(const int64_t* __restrict__ ei, long E, int n_nodes,
+                         const int* __restrict__ dst_ptr, int* __restrict__ cursor,
+                         int* __restrict__ perm) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= E) return;
+  const int64_t s = ei[p], d = ei[E + p];
+  if (s < 0 || s >= n_nodes || d < 0 || d >= n_nodes) return;
+  const int slot = atomicAdd(cursor + d, 1);
+  perm[dst_ptr[d] + slot] = (int)p;
+}
+
+// order each destination segment by (src, reference position): insertion sort,
+// segments are short (node degree)
+__global__ void dst_sort(const int64_t* __restrict__ ei, int n_nodes, const int* __restrict__ dst_ptr,
+                         int* __restrict__ perm, int* __restrict__ src_sorted) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_nodes) return;
+  const int b = dst_ptr[d], e = dst_ptr[d + 1];
+  for (int i = b + 1; i < e; ++i) {
+    const int v = perm[i];
+    const int64_t kv = ei[v];
+    int j = i - 1;
+    while (j >= b) {
+      const int u = perm[j];
+      const int64_t ku = ei[u];
+      if (ku < kv || (ku == kv && u < v)) break;
+      perm[j + 1] = u;
+      --j;
+    }
+    perm[j + 1] = v;
+  }
+  for (int i = b; i < e; ++i) src_sorted[i] = (int)ei[perm[i]];
+}
+
+// ------------------------------------------------------------------ dense views
+__global__ void dense_adj_kernel(const float* __restrict__ px, const float* __restrict__ py,
+                                 const int* __restrict__ row_ptr, const int* __restrict__ col,
+                                 int n, uint8_t* __restrict__ adj, float* __restrict__ dist) {
+  const int i = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  if (dist) {
+    float dx = __fsub_rn(px[i], px[j]), dy = __fsub_rn(py[i], py[j]);
+    dist[(size_t)i * n + j] = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+  }
+  if (adj) adj[(size_t)i * n + j] = 0;
+}
+
+__global__ void dense_adj_set(const int* __restrict__ row_ptr, const int* __restrict__ col, int n,
+                              uint8_t* __restrict__ adj) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int p = row_ptr[i]; p < row_ptr[i + 1]; ++p) adj[(size_t)i * n + col[p]] = 1;
+}
+
+// CSR row id of every position (edge_index[0] of the np.where order, or the
+// destination of each destination-major edge)
+__global__ __launch_bounds__(256) void csr_rows_kernel(const int* __restrict__ row_ptr, int n_rows,
+                                                       int* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n_rows; row += nw) {
+    const int b = row_ptr[row], e = row_ptr[row + 1];
+    for (int p = b + lane; p < e; p += 64) out[p] = row;
+  }
+}
+
+// link pairs of an arbitrary edge_index: positions p with ei[0][p] < ei[1][p], in order
+__global__ void pair_flags(const int64_t* __restrict__ ei, long E, int* __restrict__ flag) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < E) flag[p] = ei[p] < ei[E + p] ? 1 : 0;
+}
+__global__ void pair_scatter(const int64_t* __restrict__ ei, long E, const int* __restrict__ pos,
+                             int* __restrict__ ps, int* __restrict__ pd) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= E) return;
+  const int64_t s = ei[p], d = ei[E + p];
+  if (s < d) {
+    ps[pos[p]] = (int)s;
+    pd[pos[p]] = (int)d;
+  }
+}
+
+__global__ void i32_to_i64_kernel(const int* __restrict__ in, long n, int64_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+
+__global__ void gather_rows_kernel(const float* __restrict__ in, const int* __restrict__ idx,
+                                   long rows, int w, float* __restrict__ out) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * w) return;
+  const long r = t / w;
+  const int c = (int)(t % w);
+  out[t] = in[(size_t)idx[r] * w + c];
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+extern "C" int rg_node_features(const float* px, const float* py, const float* vr,
+                                const float* rcs, const int64_t* timestamp, const int* ball_degree,
+                                const int* frame_ptr, int n_nodes, int n_frames, double min_range,
+                                double max_range, double min_azimuth, double max_azimuth,
+                                float* out, void* stream) {
+  RG_REQUIRE(n_frames >= 1 && n_nodes >= 0, RG_ERR_ARG, "rg_node_features: bad sizes");
+  if (n_nodes == 0) return RG_OK;
+  node_features_kernel<<<n_frames, 256, 0, (hipStream_t)stream>>>(
+      px, py, vr, rcs, timestamp, ball_degree, frame_ptr, min_range, max_range,
+      (float)(min_azimuth - max_azimuth), (float)max_azimuth, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_edge_features(const float* px, const float* py, const float* vx, const float* vy,
+                                const int64_t* timestamp, const int* src, const int* dst,
+                                const int* n_edges_dev, long n_edges, float* out, void* stream) {
+  if (n_edges <= 0) return RG_OK;
+  long blocks = (n_edges + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  edge_features_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(px, py, vx, vy, timestamp, src, dst,
+                                                                n_edges_dev, n_edges, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_link_pairs_workspace_size(int n_nodes) {
+  return align256((size_t)n_nodes * sizeof(int)) + align256(scan_workspace_bytes(n_nodes));
+}
+
+extern "C" int rg_link_pairs(const int* row_ptr, const int* col, int n_nodes, int* pair_ptr,
+                             int* pair_src, int* pair_dst, long pair_capacity, int* n_pairs,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(workspace_bytes >= rg_link_pairs_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_link_pairs: workspace too small");
+  if (n_nodes == 0) {
+    RG_CHECK_HIP(hipMemsetAsync(pair_ptr, 0, sizeof(int), st));
+    RG_CHECK_HIP(hipMemsetAsync(n_pairs, 0, sizeof(int), st));
+    return RG_OK;
+  }
+  int* cnt = (int*)workspace;
+  void* sws = (char*)workspace + align256((size_t)n_nodes * sizeof(int));
+  pairs_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(row_ptr, col, n_nodes, cnt);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(cnt, n_nodes, pair_ptr, n_pairs, sws, st);
+  if (rc) return rc;
+  int blocks = ceil_div(n_nodes, 4);
+  if (blocks > 8192) blocks = 8192;
+  pairs_emit<<<blocks, 256, 0, st>>>(row_ptr, col, n_nodes, pair_ptr, pair_src, pair_dst,
+                                     pair_capacity);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_csr_by_dst_workspace_size(int n_nodes, long n_edges) {
+  (void)n_edges;
+  return 2 * align256((size_t)n_nodes * sizeof(int)) + align256(sizeof(int) * 64) +
+         align256(scan_workspace_bytes(n_nodes));
+}
+
+extern "C" int rg_csr_by_dst(const int64_t* edge_index, long n_edges, int n_nodes, int* dst_ptr,
+                             int* perm, int* src_sorted, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(workspace_bytes >= rg_csr_by_dst_workspace_size(n_nodes, n_edges), RG_ERR_ARG,
+             "rg_csr_by_dst: workspace too small");
+  char* w = (char*)workspace;
+  int* cnt = (int*)w;
+  w += align256((size_t)n_nodes * sizeof(int));
+  int* cursor = (int*)w;
+  w += align256((size_t)n_nodes * sizeof(int));
+  int* bad = (int*)w;
+  w += align256(sizeof(int) * 64);
+  void* sws = w;
+  RG_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)n_nodes * sizeof(int), st));
+  RG_CHECK_HIP(hipMemsetAsync(cursor, 0, (size_t)n_nodes * sizeof(int), st));
+  RG_CHECK_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+  if (n_edges > 0) {
+    dst_count<<<ceil_div(n_edges, 256), 256, 0, st>>>(edge_index, n_edges, n_nodes, cnt, bad);
+    RG_LAUNCH_CHECK();
+  }
+  int rc = exclusive_scan(cnt, n_nodes, dst_ptr, nullptr, sws, st);
+  if (rc) return rc;
+  if (n_edges > 0) {
+    dst_fill<<<ceil_div(n_edges, 256), 256, 0, st>>>(edge_index, n_edges, n_nodes, dst_ptr, cursor,
+                                                     perm);
+    RG_LAUNCH_CHECK();
+    dst_sort<<<ceil_div(n_nodes, 256), 256, 0, st>>>(edge_index, n_nodes, dst_ptr, perm,
+                                                     src_sorted);
+    RG_LAUNCH_CHECK();
+  }
+  return RG_OK;
+}
+
+extern "C" int rg_dense_adjacency(const float* px, const float* py, const int* row_ptr,
+                                  const int* col, int n_nodes, uint8_t* adj, float* dist,
+                                  void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n_nodes == 0) return RG_OK;
+  dim3 grid(ceil_div(n_nodes, 256), n_nodes);
+  dense_adj_kernel<<<grid, 256, 0, st>>>(px, py, row_ptr, col, n_nodes, adj, dist);
+  RG_LAUNCH_CHECK();
+  if (adj) {
+    dense_adj_set<<<ceil_div(n_nodes, 256), 256, 0, st>>>(row_ptr, col, n_nodes, adj);
+    RG_LAUNCH_CHECK();
+  }
+  return RG_OK;
+}
+
+extern "C" int rg_i32_to_i64(const int* in, long n, int64_t* out, void* stream) {
+  if (n <= 0) return RG_OK;
+  i32_to_i64_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(in, n, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_gather_rows_f32(const float* in, const int* idx, long rows, int w, float* out,
+                                  void* stream) {
+  if (rows <= 0 || w <= 0) return RG_OK;
+  gather_rows_kernel<<<ceil_div(rows * w, 256), 256, 0, (hipStream_t)stream>>>(in, idx, rows, w,
+                                                                                out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream) {
+  if (n_rows <= 0) return RG_OK;
+  int blocks = ceil_div(n_rows, 4);
+  if (blocks > 8192) blocks = 8192;
+  csr_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(row_ptr, n_rows, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_pairs_from_edge_index_workspace_size(long n_edges) {
+  return 2 * align256((size_t)(n_edges + 1) * sizeof(int)) + align256(scan_workspace_bytes(n_edges));
+}
+
+extern "C" int rg_pairs_from_edge_index(const int64_t* edge_index, long n_edges, int* pair_src,
+                                        int* pair_dst, int* n_pairs, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(workspace_bytes >= rg_pairs_from_edge_index_workspace_size(n_edges), RG_ERR_ARG,
+             "rg_pairs_from_edge_index: workspace too small");
+  if (n_edges <= 0) {
+    RG_CHECK_HIP(hipMemsetAsync(n_pairs, 0, sizeof(int), st));
+    return RG_OK;
+  }
+  char* w = (char*)workspace;
+  int* flag = (int*)w;
+  w += align256((size_t)(n_edges + 1) * sizeof(int));
+  int* pos = (int*)w;
+  w += align256((size_t)(n_edges + 1) * sizeof(int));
+  pair_flags<<<ceil_div(n_edges, 256), 256, 0, st>>>(edge_index, n_edges, flag);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(flag, n_edges, pos, n_pairs, w, st);
+  if (rc) return rc;
+  pair_scatter<<<ceil_div(n_edges, 256), 256, 0, st>>>(edge_index, n_edges, pos, pair_src, pair_dst);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

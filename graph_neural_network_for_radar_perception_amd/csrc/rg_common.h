@@ -1,0 +1,80 @@
+// Shared helpers for the radar-GNN HIP library (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/radar_gnn.h"
+
+namespace rg {
+
+// ---------------------------------------------------------------------------
+// error reporting: every C-ABI entry point returns 0 or a nonzero code and
+// leaves a message retrievable with rg_last_error().
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define RG_CHECK_HIP(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      ::rg::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,                \
+                      hipGetErrorString(_e));                                     \
+      return RG_ERR_HIP;                                                          \
+    }                                                                             \
+  } while (0)
+
+#define RG_REQUIRE(cond, code, ...)                                               \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      ::rg::set_error(__VA_ARGS__);                                               \
+      return (code);                                                              \
+    }                                                                             \
+  } while (0)
+
+#define RG_LAUNCH_CHECK()                                                         \
+  do {                                                                            \
+    hipError_t _e = hipGetLastError();                                            \
+    if (_e != hipSuccess) {                                                       \
+      ::rg::set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__,            \
+                      hipGetErrorString(_e));                                     \
+      return RG_ERR_HIP;                                                          \
+    }                                                                             \
+  } while (0)
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// bf16 <-> f32 (round to nearest even; NaN stays NaN via the hardware cvt)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+// MFMA operand / accumulator vector types
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// activation codes (Activation, common.py:256-267)
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2, ACT_SWISH = 3 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_LEAKY) return v > 0.f ? v : v * 0.01f;   // constants.py:10
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_SWISH) return v / (1.f + __expf(-v));
+  return v;
+}
+
+}  // namespace rg

@@ -1,0 +1,545 @@
+"""Native executor: packs the model's parameters for the HIP kernels and runs
+the batched radar-GNN forward on one device.
+
+Layering (all compute is in libradargnn.so; this module only sequences calls,
+owns buffers and converts between the reference's tensor layouts and the
+library's):
+
+  ChainPlan       one fused rg_mlp_chain launch (<= 8 ffn_blocks) with its packed
+                  weights; repacked automatically when a parameter changes
+  ModelPlans      every chain of one Model_Inference (encoders, per-layer message /
+                  update / residual chains, head chains) for one dtype
+  DeviceGraph     destination-major CSR + link pairs of a batch of frames
+  forward_batched the L-layer message passing and the four heads over a DeviceGraph
+                  (Model_Inference.forward, gnn_detector.py:141-201, for many frames
+                  at once: frames are a disjoint union, and every operator of the
+                  shipped config is per row or per destination, so batching is exact)
+
+Data layout in HBM (per batch): node rows [N][C] and edge rows [E][C] row-major in
+the compute dtype, edges in destination-major order (segment of destination i =
+sources ascending == the reference's scatter_add_ order for target i), logits in
+float32.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _native as nat
+from .common import Activation, channel_normalization, ffn_block
+
+DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16)}
+
+
+def _dt_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return nat.RG_F32
+    if t.dtype == torch.bfloat16:
+        return nat.RG_BF16
+    raise TypeError(f'unsupported tensor dtype {t.dtype}')
+
+
+def _require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise RuntimeError(f'{what}: the radar-GNN hot path runs only on a HIP device '
+                           f'(got a {t.device} tensor); move the model and inputs to cuda')
+
+
+# --------------------------------------------------------------------------- chains
+@dataclass
+class LayerSpec:
+    weight: torch.Tensor
+    bias: Optional[torch.Tensor]
+    mu: Optional[torch.Tensor]
+    std: Optional[torch.Tensor]
+    act: str
+
+    @property
+    def in_dim(self):
+        return self.weight.shape[1]
+
+    @property
+    def out_dim(self):
+        return self.weight.shape[0]
+
+
+def _norm_params(norm):
+    if norm is None:
+        return None, None
+    if not isinstance(norm, channel_normalization):
+        raise NotImplementedError(
+            f'{type(norm).__name__}: only channel_normalization (the shipped config, '
+            'configuration_radarscenes_gnn.yml:51) is fused in the HIP chain kernels; '
+            'layer/group normalisation need frame-wide statistics')
+    return norm.mu, norm.std
+
+
+def specs_from_modules(mods) -> List[LayerSpec]:
+    """ffn_block -> (Linear, norm, act); bare nn.Linear -> linear only;
+    residual_connection Sequential(Linear, norm) -> linear + norm, no activation."""
+    out = []
+    for m in mods:
+        if isinstance(m, ffn_block):
+            lin = m.block[0]
+            norm = m.block[1] if len(m.block) == 3 else None
+            act = m.block[-1].kind
+        elif isinstance(m, nn.Linear):
+            lin, norm, act = m, None, 'none'
+        elif isinstance(m, nn.Sequential) and isinstance(m[0], nn.Linear):
+            lin, norm, act = m[0], (m[1] if len(m) > 1 else None), 'none'
+        else:
+            raise TypeError(f'cannot lower {type(m).__name__} to a chain layer')
+        mu, sd = _norm_params(norm)
+        out.append(LayerSpec(lin.weight, lin.bias, mu, sd, act))
+    return out
+
+
+class ChainPlan:
+    """Packed weights + launch descriptors of one or more rg_mlp_chain calls."""
+
+    def __init__(self, specs: List[LayerSpec], dtype: str, device):
+        if not specs:
+            raise ValueError('empty chain')
+        self.specs = specs
+        self.dtype = dtype
+        self.dt, self.tdtype = DTYPES[dtype]
+        self.device = torch.device(device)
+        self.in_dim = specs[0].in_dim
+        self.out_dim = specs[-1].out_dim
+        self._pack()
+
+    def _signature(self):
+        sig = []
+        for s in self.specs:
+            for t in (s.weight, s.bias, s.mu, s.std):
+                if t is not None:
+                    sig.append((t.data_ptr(), t._version))
+        return tuple(sig)
+
+    def _pack(self):
+        lib = nat.lib()
+        for s in self.specs:
+            for t in (s.weight, s.bias, s.mu, s.std):
+                if t is not None:
+                    _require_device(t, 'model parameter')
+        sizes = [lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, self.dt) for s in self.specs]
+        offs, tot = [], 0
+        for sz in sizes:
+            offs.append(tot)
+            tot += (sz + 255) // 256 * 256
+        self.buf = torch.empty(tot, dtype=torch.uint8, device=self.device)
+        st = nat.stream_ptr(self.device)
+        base = self.buf.data_ptr()
+        for s, off in zip(self.specs, offs):
+            w = s.weight.detach().to(torch.float32).contiguous()
+            b = None if s.bias is None else s.bias.detach().to(torch.float32).contiguous()
+            nat.check(lib.rg_pack_linear(w.data_ptr(), nat.ptr(b), s.in_dim, s.out_dim, self.dt,
+                                         base + off, st), 'rg_pack_linear')
+        # groups of <= MAX_LAYERS layers (a longer chain runs as several launches)
+        self.groups = []
+        for g0 in range(0, len(self.specs), nat.MAX_LAYERS):
+            grp = list(range(g0, min(g0 + nat.MAX_LAYERS, len(self.specs))))
+            arr = (nat.rg_layer * len(grp))()
+            for i, li in enumerate(grp):
+                s = self.specs[li]
+                arr[i].w_packed = base + offs[li]
+                arr[i].norm_mu = nat.ptr(s.mu.detach()) if s.mu is not None else None
+                arr[i].norm_std = nat.ptr(s.std.detach()) if s.std is not None else None
+                arr[i].in_dim = s.in_dim
+                arr[i].out_dim = s.out_dim
+                arr[i].act = nat.ACT[s.act]
+            self.groups.append((arr, len(grp), self.specs[grp[-1]].out_dim))
+        self.sig = self._signature()
+
+    def refresh(self):
+        if self._signature() != self.sig:
+            self._pack()
+
+    def __call__(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
+                 mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
+                 idx0=None, idx1=None, residual=None, rows_dev=None):
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        cur_in, cur_w, cur_mode = in0, w0, mode
+        for gi, (arr, n, gout) in enumerate(self.groups):
+            last = gi == len(self.groups) - 1
+            dst = out if last else torch.empty((out.shape[0], gout), dtype=self.tdtype,
+                                               device=self.device)
+            res = residual if last else None
+            i1 = in1 if gi == 0 else None
+            i2 = in2 if gi == 0 else None
+            rc = lib.rg_mlp_chain(
+                self.dt, arr, n, int(rows), nat.ptr(rows_dev), cur_mode, _dt_code(cur_in),
+                cur_in.data_ptr(), cur_in.stride(0), cur_w,
+                nat.ptr(i1), i1.stride(0) if i1 is not None else 0, w1 if gi == 0 else 0,
+                nat.ptr(i2), i2.stride(0) if i2 is not None else 0, w2 if gi == 0 else 0,
+                nat.ptr(idx0 if gi == 0 else None), nat.ptr(idx1 if gi == 0 else None),
+                nat.ptr(res), res.stride(0) if res is not None else 0,
+                _dt_code(res) if res is not None else 0,
+                dst.data_ptr(), dst.stride(0), _dt_code(dst), st)
+            nat.check(rc, 'rg_mlp_chain')
+            cur_in, cur_w, cur_mode = dst, gout, nat.IN_DENSE
+        return out
+
+
+def segment_reduce(src: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int, op: str,
+                   out: torch.Tensor, idx: Optional[torch.Tensor] = None):
+    """CSR segmented sum / mean / max (rg_segment_reduce)."""
+    lib = nat.lib()
+    C = src.shape[1]
+    nat.check(lib.rg_segment_reduce(src.data_ptr(), _dt_code(src), src.stride(0),
+                                    seg_ptr.data_ptr(), nat.ptr(idx), int(n_seg), C,
+                                    nat.REDUCE[op], out.data_ptr(), _dt_code(out), out.stride(0),
+                                    nat.stream_ptr(src.device)), 'rg_segment_reduce')
+    return out
+
+
+# --------------------------------------------------------------------------- graphs
+class DeviceGraph:
+    """Destination-major CSR of a (batched) graph plus its link pairs.
+
+    seg_ptr  int32[N+1]  segment of destination i (PyG target = edge_index[1])
+    dst      int32[E]    destination of each dst-major edge (x_i rows)
+    src      int32[E]    source of each dst-major edge (x_j rows), ascending per segment
+    perm     int32[E]    dst-major position -> reference edge position (or None when
+                         the dst-major order IS the CSR order of a symmetric graph)
+    pair_src/pair_dst int32[U_cap], n_pairs int32[1]: link pairs (i < j) in reference order
+    """
+
+    def __init__(self, n_nodes, n_edges_cap, seg_ptr, dst, src, perm, pair_src, pair_dst,
+                 n_pairs_dev, n_edges_dev=None, n_edges=None, n_pairs=None):
+        self.n_nodes = n_nodes
+        self.n_edges_cap = n_edges_cap
+        self.seg_ptr, self.dst, self.src, self.perm = seg_ptr, dst, src, perm
+        self.pair_src, self.pair_dst, self.n_pairs_dev = pair_src, pair_dst, n_pairs_dev
+        self.n_edges_dev = n_edges_dev
+        self.n_edges = n_edges
+        self.n_pairs = n_pairs
+
+    @staticmethod
+    def from_edge_index(edge_index: torch.Tensor, n_nodes: int, count_pairs: bool = True):
+        """Reference-order edge_index (int64 [2, E]) -> destination-major CSR."""
+        _require_device(edge_index, 'edge_index')
+        lib = nat.lib()
+        dev = edge_index.device
+        ei = edge_index.to(torch.int64).contiguous()
+        E = ei.shape[1]
+        st = nat.stream_ptr(dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        seg_ptr = torch.empty(n_nodes + 1, **i32)
+        perm = torch.empty(max(E, 1), **i32)
+        src = torch.empty(max(E, 1), **i32)
+        ws = torch.empty(lib.rg_csr_by_dst_workspace_size(n_nodes, E), dtype=torch.uint8, device=dev)
+        nat.check(lib.rg_csr_by_dst(ei.data_ptr(), E, n_nodes, seg_ptr.data_ptr(), perm.data_ptr(),
+                                    src.data_ptr(), ws.data_ptr(), ws.numel(), st), 'rg_csr_by_dst')
+        dst = torch.empty(max(E, 1), **i32)
+        nat.check(lib.rg_csr_rows(seg_ptr.data_ptr(), n_nodes, dst.data_ptr(), st), 'rg_csr_rows')
+        ps = torch.empty(max(E, 1), **i32)
+        pd = torch.empty(max(E, 1), **i32)
+        npairs = torch.zeros(1, **i32)
+        ws2 = torch.empty(lib.rg_pairs_from_edge_index_workspace_size(E), dtype=torch.uint8,
+                          device=dev)
+        nat.check(lib.rg_pairs_from_edge_index(ei.data_ptr(), E, ps.data_ptr(), pd.data_ptr(),
+                                               npairs.data_ptr(), ws2.data_ptr(), ws2.numel(), st),
+                  'rg_pairs_from_edge_index')
+        U = int(npairs.item()) if count_pairs else None
+        return DeviceGraph(n_nodes, E, seg_ptr, dst, src, perm, ps, pd, npairs, None, E, U)
+
+
+def build_graph(px, py, frame_ptr: torch.Tensor, frame_sizes: List[int], k: int, eps2: float,
+                mode: int = nat.GRAPH_KNN, edge_capacity: Optional[int] = None,
+                ws_cache: Optional[dict] = None):
+    """Batched kNN / radius graph build (rg_build_graph) -> (row_ptr, col, ball_degree,
+    n_edges_dev, capacity).  For kNN the capacity bound 2*N*min(k, N_f-1) is exact-safe,
+    so no host synchronisation is needed."""
+    lib = nat.lib()
+    dev = px.device
+    n = int(px.shape[0])
+    nf = len(frame_sizes)
+    maxn = max(frame_sizes) if frame_sizes else 0
+    if edge_capacity is None:
+        if mode == nat.GRAPH_KNN:
+            edge_capacity = sum(2 * s * min(k, max(s - 1, 0)) for s in frame_sizes)
+        else:
+            edge_capacity = max(64, sum(s * 48 for s in frame_sizes))
+    edge_capacity = max(int(edge_capacity), 1)
+    i32 = dict(dtype=torch.int32, device=dev)
+    wsz = lib.rg_build_graph_workspace_size(n, nf, maxn, k, mode)
+    key = ('graph_ws', wsz)
+    ws = ws_cache.get(key) if ws_cache is not None else None
+    if ws is None:
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        if ws_cache is not None:
+            ws_cache[key] = ws
+    row_ptr = torch.empty(n + 1, **i32)
+    col = torch.empty(edge_capacity, **i32)
+    deg = torch.empty(max(n, 1), **i32)
+    ne = torch.zeros(1, **i32)
+    nat.check(lib.rg_build_graph(px.data_ptr(), py.data_ptr(), frame_ptr.data_ptr(), n, nf, maxn,
+                                 int(k), float(eps2), mode, row_ptr.data_ptr(), col.data_ptr(),
+                                 edge_capacity, deg.data_ptr(), ne.data_ptr(), ws.data_ptr(),
+                                 ws.numel(), nat.stream_ptr(dev)), 'rg_build_graph')
+    return row_ptr, col, deg, ne, edge_capacity
+
+
+def graph_from_csr(row_ptr, col, n_nodes, n_edges_dev, edge_capacity, ws_cache=None):
+    """Symmetric CSR (our builder) -> DeviceGraph: destination-major segments are the
+    CSR rows themselves (segment i lists the sources of target i ascending)."""
+    lib = nat.lib()
+    dev = row_ptr.device
+    st = nat.stream_ptr(dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    dst = torch.empty(edge_capacity, **i32)
+    nat.check(lib.rg_csr_rows(row_ptr.data_ptr(), n_nodes, dst.data_ptr(), st), 'rg_csr_rows')
+    ucap = max(edge_capacity // 2 + 1, 1)
+    ps = torch.empty(ucap, **i32)
+    pd = torch.empty(ucap, **i32)
+    pptr = torch.empty(n_nodes + 1, **i32)
+    npairs = torch.zeros(1, **i32)
+    ws = torch.empty(lib.rg_link_pairs_workspace_size(n_nodes), dtype=torch.uint8, device=dev)
+    nat.check(lib.rg_link_pairs(row_ptr.data_ptr(), col.data_ptr(), n_nodes, pptr.data_ptr(),
+                                ps.data_ptr(), pd.data_ptr(), ucap, npairs.data_ptr(),
+                                ws.data_ptr(), ws.numel(), st), 'rg_link_pairs')
+    return DeviceGraph(n_nodes, edge_capacity, row_ptr, dst, col, None, ps, pd, npairs,
+                       n_edges_dev=n_edges_dev)
+
+
+def node_features(frame_arrays: dict, ball_degree, frame_ptr, n_frames, cfg) -> torch.Tensor:
+    lib = nat.lib()
+    px = frame_arrays['meas_px']
+    n = px.shape[0]
+    out = torch.empty((n, 6), dtype=torch.float32, device=px.device)
+    nat.check(lib.rg_node_features(
+        px.data_ptr(), frame_arrays['meas_py'].data_ptr(), frame_arrays['meas_vr'].data_ptr(),
+        frame_arrays['meas_rcs'].data_ptr(), frame_arrays['meas_timestamp'].data_ptr(),
+        ball_degree.data_ptr(), frame_ptr.data_ptr(), n, n_frames, float(cfg.grid_min_r),
+        float(cfg.grid_max_r), float(cfg.grid_min_th), float(cfg.grid_max_th), out.data_ptr(),
+        nat.stream_ptr(px.device)), 'rg_node_features')
+    return out
+
+
+def edge_features(frame_arrays: dict, src, dst, n_edges_dev, n_edges: int) -> torch.Tensor:
+    """compute_edge_features for edges src[p] -> dst[p] (rg_edge_features)."""
+    lib = nat.lib()
+    px = frame_arrays['meas_px']
+    out = torch.empty((max(n_edges, 1), 7), dtype=torch.float32, device=px.device)
+    nat.check(lib.rg_edge_features(
+        px.data_ptr(), frame_arrays['meas_py'].data_ptr(), frame_arrays['meas_vx'].data_ptr(),
+        frame_arrays['meas_vy'].data_ptr(), frame_arrays['meas_timestamp'].data_ptr(),
+        src.data_ptr(), dst.data_ptr(), nat.ptr(n_edges_dev), n_edges, out.data_ptr(),
+        nat.stream_ptr(px.device)), 'rg_edge_features')
+    return out
+
+
+# --------------------------------------------------------------------------- model plans
+class ConvPlan:
+    def __init__(self, blk, dtype, device):
+        self.aggr = blk.aggr
+        if self.aggr not in ('add', 'sum', 'mean', 'max'):
+            raise NotImplementedError(f'aggregation {self.aggr!r}')
+        self.msg = ChainPlan(specs_from_modules(list(blk.msg)), dtype, device)
+        self.upd = ChainPlan(specs_from_modules(list(blk.upd)), dtype, device)
+        self.res = (ChainPlan(specs_from_modules([blk.residual_connection]), dtype, device)
+                    if blk.residual_connection is not None else None)
+        self.c_in = self.msg.in_dim  # 2*C + Ce
+        self.c_msg = self.msg.out_dim
+        self.c_out = self.upd.out_dim
+
+    def chains(self):
+        return [c for c in (self.msg, self.upd, self.res) if c is not None]
+
+
+class ModelPlans:
+    """All chains of a Model_Inference for one compute dtype."""
+
+    def __init__(self, pred, dtype: str, device):
+        self.dtype = dtype
+        self.dt, self.tdtype = DTYPES[dtype]
+        mk = lambda mods: ChainPlan(specs_from_modules(mods), dtype, device)  # noqa: E731
+        self.node_enc = mk(list(pred.encode_node_feat.encoder))
+        self.edge_enc = mk(list(pred.encode_edge_feat.encoder))
+        self.convs = [ConvPlan(b, dtype, device) for b in pred.pass_messages.conv_blk]
+        pn, po, pl, pc = pred.predict_node, pred.predict_offset, pred.predict_link, pred.predict_class
+        self.node_head = mk(list(pn.stem) + [pn.pred_cls.head[0], pn.pred_cls.head[1]])
+        self.offset_head = mk(list(po.stem) + [po.pred_offsets.head[0], po.pred_offsets.head[1]])
+        self.link_node = mk(list(pl.compute_edge.stem)) if len(pl.compute_edge.stem) else None
+        self.link_pair = mk(list(pl.stem) + [pl.pred_cls.head[0], pl.pred_cls.head[1]])
+        self.cls_stem = mk(list(pc.stem)) if len(pc.stem) else None
+        self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
+
+    def chains(self):
+        out = [self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
+               self.cls_head]
+        out += [c for c in (self.link_node, self.cls_stem) if c is not None]
+        for cv in self.convs:
+            out += cv.chains()
+        return out
+
+    def refresh(self):
+        for c in self.chains():
+            c.refresh()
+
+
+@dataclass
+class ForwardOutputs:
+    node_cls: torch.Tensor
+    node_reg: torch.Tensor
+    link_cls: torch.Tensor
+    obj_cls: torch.Tensor
+    x: torch.Tensor
+
+
+def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst: torch.Tensor,
+                    g: DeviceGraph, cluster_ptr: torch.Tensor, cluster_idx: torch.Tensor,
+                    n_clusters: int, n_pairs_cap: Optional[int] = None,
+                    buffers: Optional[dict] = None, events: Optional[list] = None) -> ForwardOutputs:
+    """Model_Inference.forward (gnn_detector.py:141-201, cluster branch) over a batch.
+
+    node_feats      float32 [N, 6]
+    edge_feats_dst  float32 [E_cap, 7] in destination-major order
+    cluster_ptr/idx int32 CSR of the object-head clusters (global node ids)
+    """
+    dev = node_feats.device
+    T = plans.tdtype
+    N = g.n_nodes
+
+    def mark(name):
+        # HIP events on the launch stream around one kernel (bench roofline timing)
+        if events is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        events.append((name, ev))
+        return ev
+
+    Ecap = g.n_edges_cap
+    ne_dev = g.n_edges_dev
+    buf = buffers if buffers is not None else {}
+
+    def alloc(name, shape, dtype):
+        t = buf.get(name)
+        if t is None or t.shape != torch.Size(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            buf[name] = t
+        return t
+
+    x = alloc('x0', (N, plans.node_enc.out_dim), T)
+    plans.node_enc(N, x, node_feats, node_feats.shape[1])
+    e = alloc('e', (Ecap, plans.edge_enc.out_dim), T)
+    mark('edge_encoder:start')
+    plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev)
+    mark('edge_encoder:end')
+    for li, cv in enumerate(plans.convs):
+        C = x.shape[1]
+        msg = alloc('msg', (Ecap, cv.c_msg), T)
+        mark('message_chain:start')
+        cv.msg(Ecap, msg, x, C, mode=nat.IN_GATHER3, in2=e, w2=e.shape[1], idx0=g.dst,
+               idx1=g.src, rows_dev=ne_dev)
+        mark('message_chain:end')
+        agg = alloc('agg', (N, cv.c_msg), T)
+        mark('segment_reduce:start')
+        segment_reduce(msg, g.seg_ptr, N, cv.aggr, agg)
+        mark('segment_reduce:end')
+        if cv.res is not None:
+            ident = alloc(f'id{li % 2}', (N, cv.c_out), T)
+            cv.res(N, ident, x, C)
+        else:
+            ident = x
+        xn = alloc(f'x{(li + 1) % 2}' if li + 1 < len(plans.convs) else 'xL', (N, cv.c_out), T)
+        if xn.data_ptr() == x.data_ptr():
+            xn = alloc('xalt', (N, cv.c_out), T)
+        cv.upd(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg, w1=cv.c_msg, residual=ident)
+        x = xn
+    C = x.shape[1]
+    f32 = torch.float32
+    node_cls = torch.empty((N, plans.node_head.out_dim), dtype=f32, device=dev)
+    plans.node_head(N, node_cls, x, C)
+    node_reg = torch.empty((N, plans.offset_head.out_dim), dtype=f32, device=dev)
+    plans.offset_head(N, node_reg, x, C)
+    if plans.link_node is not None:
+        s = alloc('link_s', (N, plans.link_node.out_dim), T)
+        plans.link_node(N, s, x, C)
+    else:
+        s = x
+    ucap = n_pairs_cap if n_pairs_cap is not None else (g.n_pairs if g.n_pairs is not None
+                                                        else g.pair_src.shape[0])
+    link = torch.empty((ucap, plans.link_pair.out_dim), dtype=f32, device=dev)
+    plans.link_pair(ucap, link, s, s.shape[1], mode=nat.IN_PAIRADD, idx0=g.pair_src,
+                    idx1=g.pair_dst, rows_dev=g.n_pairs_dev)
+    if plans.cls_stem is not None:
+        h = alloc('cls_h', (N, plans.cls_stem.out_dim), T)
+        plans.cls_stem(N, h, x, C)
+    else:
+        h = x
+    pooled = alloc('pooled', (n_clusters, h.shape[1]), T)
+    segment_reduce(h, cluster_ptr, n_clusters, 'max', pooled, idx=cluster_idx)
+    obj = torch.empty((n_clusters, plans.cls_head.out_dim), dtype=f32, device=dev)
+    plans.cls_head(n_clusters, obj, pooled, pooled.shape[1])
+    return ForwardOutputs(node_cls, node_reg, link, obj, x)
+
+
+# --------------------------------------------------------------------------- block-level
+_block_cache: dict = {}
+
+
+def _plan_for(mods, dtype='fp32', device=None) -> ChainPlan:
+    key = (tuple(id(m) for m in mods), dtype)
+    p = _block_cache.get(key)
+    if p is None:
+        p = ChainPlan(specs_from_modules(mods), dtype, device)
+        _block_cache[key] = p
+    else:
+        p.refresh()
+    return p
+
+
+def run_blocks(mods, x: torch.Tensor, dtype: str = 'fp32') -> torch.Tensor:
+    """Run a list of ffn_block / Linear modules as one fused chain on x [rows, C]."""
+    _require_device(x, 'input')
+    plan = _plan_for(mods, dtype, x.device)
+    xin = x.contiguous()
+    if xin.dtype not in (torch.float32, torch.bfloat16):
+        xin = xin.float()
+    out = torch.empty((xin.shape[0], plan.out_dim), dtype=torch.float32, device=x.device)
+    plan(xin.shape[0], out, xin, xin.shape[1])
+    return out
+
+
+def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):
+    """residual_graph_conv_block.forward (gnn_blocks.py:96-110) on one graph."""
+    _require_device(node_features, 'node_features')
+    dev = node_features.device
+    cp = _block_cache.get((id(blk), dtype))
+    if cp is None:
+        cp = ConvPlan(blk, dtype, dev)
+        _block_cache[(id(blk), dtype)] = cp
+    else:
+        for c in cp.chains():
+            c.refresh()
+    N = node_features.shape[0]
+    g = DeviceGraph.from_edge_index(edge_index, N, count_pairs=False)
+    E = g.n_edges
+    x = node_features.float().contiguous()
+    ef = edge_features.float().contiguous()
+    e = torch.empty((max(E, 1), ef.shape[1]), dtype=torch.float32, device=dev)
+    lib = nat.lib()
+    if E > 0:
+        nat.check(lib.rg_gather_rows_f32(ef.data_ptr(), g.perm.data_ptr(), E, ef.shape[1],
+                                         e.data_ptr(), nat.stream_ptr(dev)), 'rg_gather_rows_f32')
+    msg = torch.empty((max(E, 1), cp.c_msg), dtype=torch.float32, device=dev)
+    cp.msg(E, msg, x, x.shape[1], mode=nat.IN_GATHER3, in2=e, w2=e.shape[1], idx0=g.dst,
+           idx1=g.src)
+    agg = torch.empty((N, cp.c_msg), dtype=torch.float32, device=dev)
+    segment_reduce(msg, g.seg_ptr, N, cp.aggr, agg)
+    if cp.res is not None:
+        ident = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
+        cp.res(N, ident, x, x.shape[1])
+    else:
+        ident = x
+    out = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
+    cp.upd(N, out, x, x.shape[1], mode=nat.IN_CONCAT2, in1=agg, w1=cp.c_msg, residual=ident)
+    return out

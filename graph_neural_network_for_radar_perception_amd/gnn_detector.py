@@ -1,0 +1,241 @@
+"""Drop-in ``Model_Inference`` / ``Model_Training`` (modules/neural_net/gnn/gnn_detector.py).
+
+Same constructor signatures, same ``forward`` signatures and return tuples, same
+``state_dict`` keys as the reference, so ``set_param_for_inference_gnn.py:21-36``
+(``Model_Training(cfg, device)`` + ``load_state_dict(torch.load(...))`` +
+``.pred.eval()``) works unchanged.  The forward runs on the HIP library:
+the frames handed to one call are batched into one disjoint-union graph and
+processed by ``engine.forward_batched`` (one launch per chain, not per frame).
+
+Compute dtype: ``model.compute_dtype`` = 'fp32' (default; matches the reference
+CPU path within 1e-4) or 'bf16' (BASELINE config 2; bf16 operands, fp32
+accumulation and normalisation statistics).
+"""
+from __future__ import annotations
+
+from collections import namedtuple
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import engine
+from .gnn_blocks import (graph_convolution, graph_feature_encoding, link_predictions,
+                         node_offset_predictions, node_segmentation, object_classification)
+
+det_named_tuple = namedtuple('det_named_tuple', ['node_class_logits', 'node_reg_deltas',
+                                                 'edge_class_logits', 'obj_class_logits'])
+
+
+@torch.no_grad()
+def compute_accuracy(predicted_class, gt_class):
+    """gnn_detector.py:24-29."""
+    _, cls_idx = torch.max(predicted_class, dim=-1)
+    return (cls_idx == gt_class).sum() / gt_class.shape[0]
+
+
+def _batch_frames(node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
+                  edge_index: List[torch.Tensor], cluster_node_idx: List[List[torch.Tensor]]):
+    """Disjoint union of per-frame tensors (the reference loops frame by frame,
+    gnn_detector.py:443-452; every operator is per row / per destination, so
+    the union gives identical per-frame results)."""
+    dev = node_features[0].device
+    sizes = [int(t.shape[0]) for t in node_features]
+    bases = [0]
+    for s in sizes:
+        bases.append(bases[-1] + s)
+    nf = torch.cat([t.to(torch.float32) for t in node_features], 0).contiguous()
+    ef = torch.cat([t.to(torch.float32) for t in edge_features], 0).contiguous()
+    ei = torch.cat([e.to(torch.int64) + b for e, b in zip(edge_index, bases[:-1])], 1).contiguous()
+    lens, idx = [], []
+    for cl, b in zip(cluster_node_idx, bases[:-1]):
+        for c in cl:
+            lens.append(int(c.numel()))
+            idx.append(c.to(torch.int64).reshape(-1) + b)
+    cptr = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+    cidx = (torch.cat(idx).to(torch.int32) if idx else torch.zeros(1, dtype=torch.int32, device=dev))
+    return nf, ef, ei, cptr, cidx.contiguous(), len(lens), sizes
+
+
+class Model_Inference(nn.Module):
+    """gnn_detector.py:31-201."""
+
+    def __init__(self, net_config, extract_proposals=False, eps=1.4,
+                 compute_adj_mat_from_links=False):
+        super().__init__()
+        self.extract_proposals = extract_proposals
+        self.reg_mu = net_config.reg_mu
+        self.reg_sigma = net_config.reg_sigma
+        c = net_config
+        self.encode_node_feat = graph_feature_encoding(
+            c.input_node_feat_dim, c.node_feat_enc_stem_channels, c.activation, c.norm_layer,
+            c.num_groups)
+        self.encode_edge_feat = graph_feature_encoding(
+            c.input_edge_feat_dim, c.edge_feat_enc_stem_channels, c.activation, c.norm_layer,
+            c.num_groups)
+        self.pass_messages = graph_convolution(
+            c.node_feat_enc_stem_channels[-1], c.edge_feat_enc_stem_channels[-1],
+            c.graph_convolution_stem_channels, c.msg_mlp_hidden_dim, c.activation,
+            c.aggregation, c.norm_layer, c.num_groups)
+        cl = c.graph_convolution_stem_channels[-1]
+        self.predict_node = node_segmentation(cl, c.node_pred_stem_channels, c.num_classes,
+                                              c.activation, c.norm_layer, c.num_groups)
+        self.predict_offset = node_offset_predictions(cl, c.node_pred_stem_channels,
+                                                      c.reg_offset_dim, c.activation,
+                                                      c.norm_layer, c.num_groups)
+        self.predict_link = link_predictions(cl, c.num_blocks_to_compute_edge,
+                                             c.link_pred_stem_channels, c.num_edge_classes,
+                                             c.activation, c.norm_layer, c.num_groups)
+        self.predict_class = object_classification(cl, c.node_pred_stem_channels, c.num_classes,
+                                                   c.activation, c.norm_layer, c.num_groups)
+        self.compute_dtype = 'fp32'
+        self._plans: Dict[str, engine.ModelPlans] = {}
+        if extract_proposals:
+            self.set_param_for_proposal_extraction(eps, compute_adj_mat_from_links)
+
+    @staticmethod
+    def freeze_weights(nn_module):
+        for p in nn_module.parameters():
+            p.requires_grad = False
+        return nn_module
+
+    def freeze_layers_except_object_class_predictor(self):
+        for name in ('encode_node_feat', 'encode_edge_feat', 'pass_messages', 'predict_node',
+                     'predict_offset', 'predict_link'):
+            setattr(self, name, self.freeze_weights(getattr(self, name)))
+
+    def set_param_for_proposal_extraction(self, eps, compute_adj_mat_from_links):
+        self.compute_adj_mat_from_links = compute_adj_mat_from_links
+        self.extract_proposals = True
+        self.clustering_eps = eps
+
+    def plans(self, dtype: Optional[str] = None) -> engine.ModelPlans:
+        dtype = dtype or self.compute_dtype
+        p = self._plans.get(dtype)
+        dev = next(self.parameters()).device
+        if p is None:
+            p = engine.ModelPlans(self, dtype, dev)
+            self._plans[dtype] = p
+        else:
+            p.refresh()
+        return p
+
+    def forward_frames(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
+                       edge_index: List[torch.Tensor], cluster_node_idx: List[List[torch.Tensor]]):
+        """Batched forward over several frames; returns per-batch concatenated
+        (node_cls, node_reg, link_cls, obj_cls) exactly as Model_Training.forward
+        concatenates the per-frame outputs (gnn_detector.py:454-457)."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                'backward through the HIP forward is not implemented yet (training path is '
+                'the next milestone); run inference under torch.no_grad() or model.eval() with '
+                'requires_grad_(False)')
+        engine._require_device(node_features[0], 'node_features')
+        nf, ef, ei, cptr, cidx, ncl, sizes = _batch_frames(node_features, edge_features,
+                                                           edge_index, cluster_node_idx)
+        N = nf.shape[0]
+        g = engine.DeviceGraph.from_edge_index(ei, N)
+        E = g.n_edges
+        e_dst = torch.empty((max(E, 1), ef.shape[1]), dtype=torch.float32, device=nf.device)
+        if E > 0:
+            from . import _native as nat
+            nat.check(nat.lib().rg_gather_rows_f32(ef.data_ptr(), g.perm.data_ptr(), E,
+                                                   ef.shape[1], e_dst.data_ptr(),
+                                                   nat.stream_ptr(nf.device)),
+                      'rg_gather_rows_f32')
+        out = engine.forward_batched(self.plans(), nf, e_dst, g, cptr, cidx, ncl,
+                                     n_pairs_cap=g.n_pairs)
+        return out.node_cls, out.node_reg, out.link_cls[:g.n_pairs], out.obj_cls
+
+    def forward(self, node_features: torch.Tensor, edge_features: torch.Tensor,
+                edge_index: torch.Tensor, adj_matrix: torch.Tensor,
+                cluster_node_idx: Optional[List[torch.Tensor]] = None,
+                other_features: Optional[torch.Tensor] = None,
+                augmented_features: Optional[torch.Tensor] = None):
+        """gnn_detector.py:141-201.  Link pairs are taken from edge_index (the
+        entries with src < dst, in edge order), which equals nonzero(triu(adj, 1))
+        because edge_index = np.where(adj) (graph_features.py:79); adj_matrix itself
+        is not read (no N x N transfer)."""
+        if cluster_node_idx is None:
+            if not getattr(self, 'extract_proposals', False):
+                # reference: self.compute_adj_mat_from_links is never set -> AttributeError
+                raise AttributeError("'Model_Inference' object has no attribute "
+                                     "'compute_adj_mat_from_links'")
+            raise NotImplementedError('proposal branch (offsets -> Simple_DBSCAN -> clusters, '
+                                      'gnn_detector.py:164-187) is not built yet')
+        node_cls, node_reg, link_cls, obj_cls = self.forward_frames(
+            [node_features], [edge_features], [edge_index], [cluster_node_idx])
+        if self.extract_proposals:
+            # reference returns cluster_members_list, which is unbound on this branch
+            raise UnboundLocalError("local variable 'cluster_members_list' referenced before "
+                                    "assignment")
+        return node_cls, node_reg, link_cls, obj_cls
+
+
+class Model_Training(nn.Module):
+    """gnn_detector.py:419-478 (``pred`` = Model_Inference; frames of the batch
+    run as ONE batched forward instead of a Python loop)."""
+
+    def __init__(self, net_config, device):
+        super().__init__()
+        self.pred = Model_Inference(net_config)
+        self.device = device
+        self.offset_mu = net_config.offset_mu
+        self.offset_sigma = net_config.offset_sigma
+        self.net_config = net_config
+        self.class_weights = torch.tensor(net_config.class_weights_dyn, dtype=torch.float32)
+
+    def predict(self, node_features, edge_features, edge_index, cluster_node_idx):
+        return det_named_tuple(*self.pred.forward_frames(node_features, edge_features, edge_index,
+                                                         cluster_node_idx))
+
+    def forward(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
+                edge_index: List[torch.Tensor], adj_matrix: List[torch.Tensor],
+                labels: Dict[str, List[torch.Tensor]]):
+        pred = self.predict(node_features, edge_features, edge_index, labels['cluster_node_idx'])
+        gt = det_named_tuple(
+            torch.cat(labels['node_class'], 0),
+            _normalize_offsets(torch.cat(labels['node_offsets'], 0).clone(), self.offset_mu,
+                               self.offset_sigma),
+            torch.cat(labels['edge_class'], 0),
+            torch.cat(labels['cluster_labels'], 0))
+        loss = _loss_graph(self.net_config, self.class_weights.to(pred.node_class_logits.device),
+                           pred, gt)
+        acc = {'segment_accuracy': compute_accuracy(pred.node_class_logits, gt.node_class_logits),
+               'edge_accuracy': compute_accuracy(pred.edge_class_logits, gt.edge_class_logits),
+               'object_accuracy': compute_accuracy(pred.obj_class_logits, gt.obj_class_logits)}
+        return loss, acc
+
+
+def _normalize_offsets(off, mu, sigma):
+    """compute_offsets.py:6-11."""
+    off[..., 0] = (off[..., 0] - mu[0]) / sigma[0]
+    off[..., 1] = (off[..., 1] - mu[1]) / sigma[1]
+    return off
+
+
+def _loss_graph(cfg, class_weights, pred, gt):
+    """Loss_Graph.forward (loss.py:37-76) evaluated on the HIP forward's outputs
+    (validation-time loss; the training backward is the next milestone)."""
+    n_cls, n_edge = cfg.num_classes, cfg.num_edge_classes
+    node_t = F.one_hot(gt.node_class_logits, n_cls).to(torch.float32)
+    edge_t = F.one_hot(gt.edge_class_logits, n_edge).to(torch.float32)
+    obj_t = F.one_hot(gt.obj_class_logits, n_cls).to(torch.float32)
+    x = pred.edge_class_logits
+    p = torch.sigmoid(x)
+    ce = F.binary_cross_entropy_with_logits(x, edge_t, reduction='none')
+    p_t = p * edge_t + (1 - p) * (1 - edge_t)
+    focal = (0.25 * edge_t + 0.75 * (1 - edge_t)) * ce * (1 - p_t) ** 2.0
+    edge_l = focal.sum(-1)
+    edge_l = edge_l.sum() / edge_l.shape[0]
+    node_l = F.cross_entropy(pred.node_class_logits, node_t, class_weights, reduction='none')
+    node_l = node_l.sum() / node_l.shape[0]
+    reg_l = 0.5 * F.mse_loss(pred.node_reg_deltas, gt.node_reg_deltas, reduction='none').sum(-1)
+    reg_l = reg_l.sum() / reg_l.shape[0]
+    obj_l = F.cross_entropy(pred.obj_class_logits, obj_t, reduction='none')
+    obj_l = obj_l.sum() / obj_l.shape[0]
+    return {'loss_node_cls': node_l * cfg.node_cls_loss_weight,
+            'loss_node_reg': reg_l * cfg.node_reg_loss_weight,
+            'loss_edge_cls': edge_l * cfg.edge_cls_loss_weight,
+            'loss_obj_cls': obj_l * cfg.obj_cls_loss_weight}

@@ -1,0 +1,204 @@
+"""Graph build on the GPU with the reference's graph_features API.
+
+Drop-in functions (same names, arguments and result keys as
+``modules/compute_features/graph_features.py``) that run on the HIP library:
+
+  compute_adjacency_information(data_dict, eps, knn)     graph_features.py:58-84
+  compute_adjacency_information_v2(data_dict, eps, knn)  graph_features.py:87-114
+  compute_node_features(data_dict, node_degree, ...)     graph_features.py:117-144
+  compute_edge_features(data_dict, adj_list)             graph_features.py:147-164
+
+They take and return numpy arrays like the reference (one host round trip per
+call; float features come back as float32, the dtype the tensorization
+``datagen_gnn.py:120-124`` converts them to).  The batched device-side entry
+point for many frames is ``FrameBatch`` + ``build_graph_batch`` below, which
+keeps everything in HBM and never materialises an N x N matrix.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from . import engine
+
+_FIELDS_F32 = ('meas_px', 'meas_py', 'meas_vx', 'meas_vy', 'meas_vr', 'meas_rcs')
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError('graph_features: the HIP graph builder needs a GPU (no CPU fallback)')
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def _upload(frame: dict, dev, keys=None):
+    out = {}
+    for k in keys or (_FIELDS_F32 + ('meas_timestamp',)):
+        if k not in frame:
+            continue
+        a = np.asarray(frame[k])
+        a = a.astype(np.int64) if k == 'meas_timestamp' else a.astype(np.float32)
+        out[k] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return out
+
+
+def _adjacency(data_dict, eps, knn, mode):
+    dev = _device()
+    d = _upload(data_dict, dev, ('meas_px', 'meas_py'))
+    n = int(d['meas_px'].shape[0])
+    fp = torch.tensor([0, n], dtype=torch.int32, device=dev)
+    row_ptr, col, deg, ne, cap = engine.build_graph(d['meas_px'], d['meas_py'], fp, [n], knn,
+                                                    eps, mode)
+    E = int(ne.item())
+    if E > cap:  # radius graphs: capacity is a guess; rebuild at the exact size
+        row_ptr, col, deg, ne, cap = engine.build_graph(d['meas_px'], d['meas_py'], fp, [n], knn,
+                                                        eps, mode, edge_capacity=E)
+    rows = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+    lib = nat.lib()
+    st = nat.stream_ptr(dev)
+    nat.check(lib.rg_csr_rows(row_ptr.data_ptr(), n, rows.data_ptr(), st), 'rg_csr_rows')
+    adj = torch.empty((n, n), dtype=torch.uint8, device=dev)
+    dist = torch.empty((n, n), dtype=torch.float32, device=dev)
+    if n > 0:
+        nat.check(lib.rg_dense_adjacency(d['meas_px'].data_ptr(), d['meas_py'].data_ptr(),
+                                         row_ptr.data_ptr(), col.data_ptr(), n, adj.data_ptr(),
+                                         dist.data_ptr(), st), 'rg_dense_adjacency')
+    adj_list = torch.stack((rows[:E], col[:E]), 0).to(torch.int64)
+    return {'adj_matrix': adj.bool().cpu().numpy(),
+            'distance_mat': dist.cpu().numpy(),
+            'adj_list': adj_list.cpu().numpy(),
+            'degree': deg[:n].to(torch.int64).cpu().numpy()}
+
+
+def compute_adjacency_information(data_dict: dict, eps: float, knn: int) -> dict:
+    """graph_features.py:58-84 on the GPU (kNN adjacency; ties -> lower index)."""
+    return _adjacency(data_dict, eps, knn, nat.GRAPH_KNN)
+
+
+def compute_adjacency_information_v2(data_dict: dict, eps: float, knn: int) -> dict:
+    """graph_features.py:87-114 on the GPU (kNN union ball-query adjacency)."""
+    return _adjacency(data_dict, eps, knn, nat.GRAPH_KNN_RADIUS)
+
+
+def compute_radius_graph(data_dict: dict, eps: float) -> dict:
+    """np.where(compute_ball_query(D, eps)) -- the pure radius graph of BASELINE config 5."""
+    return _adjacency(data_dict, eps, 0, nat.GRAPH_RADIUS)
+
+
+def compute_node_features(data_dict, node_degree, include_region_confidence=False,
+                          min_range=None, max_range=None, min_azimuth=None, max_azimuth=None):
+    """graph_features.py:117-144 on the GPU (float32 result)."""
+    dev = _device()
+    d = _upload(data_dict, dev)
+    n = int(d['meas_px'].shape[0])
+    deg = torch.from_numpy(np.asarray(node_degree).astype(np.int32)).to(dev)
+    fp = torch.tensor([0, n], dtype=torch.int32, device=dev)
+
+    class _C:  # range / azimuth limits as the kernel takes them
+        grid_min_r = 0.0 if min_range is None else float(min_range)
+        grid_max_r = 1.0 if max_range is None else float(max_range)
+        grid_min_th = 0.0 if min_azimuth is None else float(min_azimuth)
+        grid_max_th = 1.0 if max_azimuth is None else float(max_azimuth)
+
+    out = engine.node_features(d, deg, fp, 1, _C)
+    out = out if include_region_confidence else out[:, :4]
+    return out.cpu().numpy()
+
+
+def compute_edge_features(data_dict, adj_list):
+    """graph_features.py:147-164 on the GPU (float32 result, edge order of adj_list)."""
+    dev = _device()
+    d = _upload(data_dict, dev)
+    al = torch.from_numpy(np.asarray(adj_list).astype(np.int32)).to(dev)
+    E = int(al.shape[1])
+    src = al[0].contiguous()
+    dst = al[1].contiguous()
+    out = engine.edge_features(d, src, dst, None, E)
+    return out[:E].cpu().numpy()
+
+
+# --------------------------------------------------------------------------- batched device API
+@dataclass
+class FrameBatch:
+    """A batch of radar frames resident in HBM (disjoint union, frame_ptr offsets)."""
+    arrays: dict                  # meas_* -> device tensors [N]
+    frame_ptr: torch.Tensor       # int32 [B+1] on device
+    frame_sizes: List[int]        # host copy of the frame sizes
+    cluster_ptr: torch.Tensor     # int32 [Ncl+1] object-head clusters (global node ids)
+    cluster_idx: torch.Tensor     # int32 [sum |c|]
+    n_clusters: int
+
+    @property
+    def n_nodes(self) -> int:
+        return int(sum(self.frame_sizes))
+
+    @property
+    def n_frames(self) -> int:
+        return len(self.frame_sizes)
+
+    @staticmethod
+    def from_frames(frames: List[dict], clusters: Optional[List[List[np.ndarray]]] = None,
+                    device=None) -> 'FrameBatch':
+        dev = torch.device(device) if device is not None else _device()
+        sizes = [int(np.asarray(f['meas_px']).shape[0]) for f in frames]
+        cat = {}
+        for k in _FIELDS_F32 + ('meas_timestamp',):
+            dt = np.int64 if k == 'meas_timestamp' else np.float32
+            cat[k] = torch.from_numpy(np.concatenate([np.asarray(f[k]).astype(dt) for f in frames])
+                                      ).to(dev)
+        base = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        fp = torch.from_numpy(base.astype(np.int32)).to(dev)
+        lens, idx = [], []
+        if clusters is not None:
+            for b, cl in zip(base[:-1], clusters):
+                for c in cl:
+                    lens.append(len(c))
+                    idx.append(np.asarray(c, dtype=np.int64) + b)
+        cptr = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)).to(dev)
+        cidx = torch.from_numpy((np.concatenate(idx) if idx else np.zeros(1)).astype(np.int32)).to(dev)
+        return FrameBatch(cat, fp, sizes, cptr, cidx, len(lens))
+
+
+@dataclass
+class GraphBatch:
+    row_ptr: torch.Tensor        # int32 [N+1] CSR of the symmetric adjacency
+    col: torch.Tensor            # int32 [cap]
+    ball_degree: torch.Tensor    # int32 [N]
+    n_edges_dev: torch.Tensor    # int32 [1]
+    capacity: int
+    graph: engine.DeviceGraph    # destination-major view + link pairs
+    node_features: torch.Tensor  # float32 [N, 6]
+    edge_features: torch.Tensor  # float32 [cap, 7], destination-major order
+
+    def edge_index(self) -> torch.Tensor:
+        """int64 [2, E] in the reference's np.where order (host sync for E)."""
+        E = int(self.n_edges_dev.item())
+        return torch.stack((self.graph.dst[:E], self.col[:E]), 0).to(torch.int64)
+
+
+def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Optional[float] = None,
+                      mode: int = nat.GRAPH_KNN, ws_cache: Optional[dict] = None) -> GraphBatch:
+    """datagen_gnn.py:104-124 for a whole batch, on the device and without host syncs:
+    adjacency (rg_build_graph), node features, destination-major edge features,
+    link pairs."""
+    k = cfg.k_number_nearest_points if k is None else k
+    eps2 = cfg.ball_query_eps_square if eps2 is None else eps2
+    row_ptr, col, deg, ne, cap = engine.build_graph(batch.arrays['meas_px'],
+                                                    batch.arrays['meas_py'], batch.frame_ptr,
+                                                    batch.frame_sizes, k, eps2, mode,
+                                                    ws_cache=ws_cache)
+    if mode != nat.GRAPH_KNN:
+        # radius graphs have no a-priori edge bound: check (one host sync) and rebuild
+        E = int(ne.item())
+        if E > cap:
+            row_ptr, col, deg, ne, cap = engine.build_graph(
+                batch.arrays['meas_px'], batch.arrays['meas_py'], batch.frame_ptr,
+                batch.frame_sizes, k, eps2, mode, edge_capacity=E, ws_cache=ws_cache)
+    g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
+    nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)
+    # destination-major edge (src = g.src[p] -> dst = g.dst[p])
+    ef = engine.edge_features(batch.arrays, g.src, g.dst, ne, cap)
+    return GraphBatch(row_ptr, col, deg, ne, cap, g, nf, ef)

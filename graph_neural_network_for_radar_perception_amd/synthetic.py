@@ -1,0 +1,94 @@
+"""Seeded synthetic RadarScenes-shaped frames.
+
+The real RadarScenes ``.h5`` data is absent from the reference
+(``dataset/RadarScenesData/.MISSING_LARGE_BLOBS``), so every test and benchmark
+runs on frames drawn here.  A frame is the dict the reference graph builder
+consumes after its grid crop and dynamic filter
+(``modules/data_generator/datagen_gnn.py:97-102``):
+
+    meas_px, meas_py, meas_vx, meas_vy, meas_vr, meas_rcs : float32[N]
+    meas_timestamp                                        : int64[N]  (µs)
+
+plus generator-side ground truth used by the training path
+(``cluster_id`` int64[N], cluster centres) and the object-head cluster lists.
+
+Layout (frame f uses ``np.random.default_rng(seed0 + f)``, seed0 = 1234 =
+``configuration_radarscenes_gnn.yml:2``):
+  * 70 % of points in Gaussian clusters, sigma = 1 m, mean 12 points per
+    cluster, centres uniform in [2, 98] x [-48, 48];
+  * 30 % uniform clutter in [0, 100) x [-50, 50);
+  * everything clipped into the grid ``configuration_radarscenes_gnn.yml:34-38``;
+  * vx, vy, vr ~ N(0, 5) m/s, rcs ~ N(0, 10) dBsm;
+  * timestamps = 1e12 + sorted uniform ints in [0, 155000) (10 scans).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED0 = 1234
+GRID_MIN_X, GRID_MAX_X = 0.0, 100.0
+GRID_MIN_Y, GRID_MAX_Y = -50.0, 50.0
+
+
+def make_frame(num_nodes: int, seed: int = SEED0, lattice: bool = False) -> dict:
+    """One synthetic frame with ``num_nodes`` measurements.
+
+    ``lattice=True`` places the points on an integer lattice (maximal distance
+    ties) -- used to document the reference's implementation-defined kNN tie
+    order (SURVEY.md §7 "Bit-exact edge_index").
+    """
+    rng = np.random.default_rng(seed)
+    n = int(num_nodes)
+    if lattice:
+        side = int(np.ceil(np.sqrt(n)))
+        ii = np.arange(n)
+        px = (ii % side).astype(np.float32) + 10.0
+        py = (ii // side).astype(np.float32) - 10.0
+        cluster_id = np.arange(n, dtype=np.int64) // 5
+    else:
+        n_clu = int(round(0.7 * n))
+        n_bg = n - n_clu
+        n_clusters = max(1, int(round(n_clu / 12.0)))
+        centres = np.stack([rng.uniform(2.0, 98.0, n_clusters),
+                            rng.uniform(-48.0, 48.0, n_clusters)], axis=-1)
+        cid = rng.integers(0, n_clusters, n_clu)
+        pts_c = centres[cid] + rng.normal(0.0, 1.0, (n_clu, 2))
+        pts_b = np.stack([rng.uniform(GRID_MIN_X, GRID_MAX_X, n_bg),
+                          rng.uniform(GRID_MIN_Y, GRID_MAX_Y, n_bg)], axis=-1)
+        pts = np.concatenate([pts_c, pts_b], axis=0)
+        cluster_id = np.concatenate([cid, n_clusters + np.arange(n_bg)]).astype(np.int64)
+        # shuffle so that node order carries no spatial structure
+        perm = rng.permutation(n)
+        pts = pts[perm]
+        cluster_id = cluster_id[perm]
+        hi_x = np.nextafter(np.float32(GRID_MAX_X), np.float32(0.0))
+        hi_y = np.nextafter(np.float32(GRID_MAX_Y), np.float32(0.0))
+        px = np.clip(pts[:, 0], GRID_MIN_X, hi_x).astype(np.float32)
+        py = np.clip(pts[:, 1], GRID_MIN_Y, hi_y).astype(np.float32)
+    vx = rng.normal(0.0, 5.0, n).astype(np.float32)
+    vy = rng.normal(0.0, 5.0, n).astype(np.float32)
+    vr = rng.normal(0.0, 5.0, n).astype(np.float32)
+    rcs = rng.normal(0.0, 10.0, n).astype(np.float32)
+    ts = (np.int64(10**12) + np.sort(rng.integers(0, 155000, n))).astype(np.int64)
+    return {
+        'meas_px': px, 'meas_py': py, 'meas_vx': vx, 'meas_vy': vy,
+        'meas_vr': vr, 'meas_rcs': rcs, 'meas_timestamp': ts,
+        'cluster_id': cluster_id,
+    }
+
+
+def make_batch(num_frames: int, num_nodes: int, seed0: int = SEED0) -> list:
+    """``num_frames`` frames, frame f seeded with ``seed0 + f`` (§8(d))."""
+    return [make_frame(num_nodes, seed0 + f) for f in range(num_frames)]
+
+
+def cluster_lists(num_nodes: int, group: int = 5) -> list:
+    """Object-head cluster lists: consecutive groups of ``group`` nodes (§8(d))."""
+    return [np.arange(s, min(s + group, num_nodes), dtype=np.int64)
+            for s in range(0, num_nodes, group)]
+
+
+def other_features(frame: dict) -> np.ndarray:
+    """(px, py, vx, vy) per node, ``datagen_gnn.py:110-111``."""
+    return np.stack((frame['meas_px'], frame['meas_py'],
+                     frame['meas_vx'], frame['meas_vy']), axis=-1).astype(np.float32)

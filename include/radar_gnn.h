@@ -1,0 +1,210 @@
+/*
+ * radar_gnn.h -- C ABI of the MI355X-native radar GNN hot path (libradargnn.so).
+ *
+ * The library replaces the implicit numpy / ATen / PyG kernels of the
+ * reference's per-frame path (UditBhaskar19/GRAPH_NEURAL_NETWORK_FOR_RADAR_PERCEPTION v2):
+ *   graph build      modules/compute_features/graph_features.py:11-164
+ *   model forward    modules/neural_net/gnn/gnn_detector.py:141-201,
+ *                    modules/neural_net/gnn/gnn_blocks.py:19-389,
+ *                    modules/neural_net/common.py:185-267
+ * Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *  - every pointer is a DEVICE pointer unless its name ends in _host;
+ *  - buffers are owned by the caller (the library allocates nothing that
+ *    outlives a call; scratch comes from a caller workspace sized by the
+ *    matching *_workspace_size function);
+ *  - work is enqueued asynchronously on `stream` (a hipStream_t); no entry point
+ *    synchronises the host, so a caller may capture them in a hipGraph;
+ *  - a batch of radar frames is a disjoint union: nodes of frame f are the rows
+ *    [frame_ptr[f], frame_ptr[f+1]) of every node array (frame_ptr: int32[B+1]);
+ *  - the adjacency is CSR (row_ptr int32[N+1], col int32[E]) with rows and
+ *    columns ascending: position p of row i is edge_index[:, p] = (i, col[p]) of
+ *    the reference's np.where order (graph_features.py:79);
+ *  - return value 0 = success; otherwise an RG_ERR_* code and rg_last_error()
+ *    describes it (the Python layer raises RuntimeError with that text).
+ */
+#ifndef RADAR_GNN_H
+#define RADAR_GNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RG_OK 0
+#define RG_ERR_ARG 1
+#define RG_ERR_HIP 2
+#define RG_ERR_UNSUPPORTED 3
+
+/* element types */
+#define RG_F32 0
+#define RG_BF16 1
+
+/* activations (modules/neural_net/common.py:256-267) */
+#define RG_ACT_NONE 0
+#define RG_ACT_RELU 1
+#define RG_ACT_LEAKY 2
+#define RG_ACT_SWISH 3
+
+/* graph modes */
+#define RG_GRAPH_KNN 0        /* compute_adjacency_information     graph_features.py:58-84  */
+#define RG_GRAPH_RADIUS 1     /* np.where(compute_ball_query(D,eps)) graph_features.py:11-22 */
+#define RG_GRAPH_KNN_RADIUS 2 /* compute_adjacency_information_v2  graph_features.py:87-114 */
+
+/* segment reductions (PyG aggr, gnn_blocks.py:57; cluster max gnn_blocks.py:384-387) */
+#define RG_REDUCE_SUM 0
+#define RG_REDUCE_MEAN 1
+#define RG_REDUCE_MAX 2
+
+/* chain input prologues */
+#define RG_IN_DENSE 0   /* row r <- in0[r]                                           */
+#define RG_IN_CONCAT2 1 /* row r <- cat(in0[r], in1[r])          gnn_blocks.py:108   */
+#define RG_IN_GATHER3 2 /* row r <- cat(in0[idx0[r]], in0[idx1[r]], in2[r])
+                           = cat(x_i, x_j, e) of MessagePassing.message, gnn_blocks.py:113 */
+#define RG_IN_PAIRADD 3 /* row r <- in0[idx0[r]] + in0[idx1[r]]  gnn_blocks.py:297   */
+
+const char* rg_last_error(void);
+int rg_version(void);
+
+/* ---------------------------------------------------------------- graph build */
+
+/* Bytes of scratch rg_build_graph needs. */
+size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int max_frame_nodes, int k,
+                                     int mode);
+
+/* Batched compute_adjacency_information (graph_features.py:58-84):
+ *   D[i,j] = dx*dx + dy*dy in float32 without FMA (graph_features.py:69-76);
+ *   ball_degree[i] = #{j != i : D[i,j] <= eps2}          (:11-22, :78);
+ *   kNN: the k+1 smallest (D, j) pairs of each row (all j if k >= N_f),
+ *        ties -> lower j (a stable argsort; the reference's default argsort is
+ *        unstable, so at exact ties it is implementation-defined) (:25-44);
+ *   adjacency = knn | knn^T minus the diagonal (mode KNN), the ball query
+ *   (mode RADIUS) or their union (mode KNN_RADIUS);
+ *   row_ptr/col = np.where(adjacency) as CSR (:79), global node ids.
+ * px, py:        float32[n_nodes]
+ * frame_ptr:     int32[n_frames+1] (device)
+ * col:           int32[col_capacity]; rg_build_graph fails with RG_ERR_ARG
+ *                through *n_edges_out > col_capacity (checked on device: the
+ *                overflowing rows are not written and n_edges_out reports the need)
+ * n_edges_out:   int32[1] device scalar = E
+ */
+int rg_build_graph(const float* px, const float* py, const int* frame_ptr, int n_nodes,
+                   int n_frames, int max_frame_nodes, int k, float eps2, int mode,
+                   int* row_ptr, int* col, long col_capacity, int* ball_degree,
+                   int* n_edges_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* compute_node_features(include_region_confidence=True) (graph_features.py:117-144),
+ * cast to float32 as datagen_gnn.py:122 does.  out: float32[n_nodes][6] =
+ * (vr, rcs, t_norm, degree/10, range_conf, azimuth_conf). */
+int rg_node_features(const float* px, const float* py, const float* vr, const float* rcs,
+                     const int64_t* timestamp, const int* ball_degree, const int* frame_ptr,
+                     int n_nodes, int n_frames, double min_range, double max_range,
+                     double min_azimuth, double max_azimuth, float* out, void* stream);
+
+/* compute_edge_features (graph_features.py:147-164) -> float32[E][7]
+ * (dx, dy, dl, dvx, dvy, dv, dt) of every edge src[p] -> dst[p].  With
+ * (src, dst) = (edge_index[0], edge_index[1]) this is the reference layout; the
+ * message passing passes its destination-major (source, destination) arrays.
+ * n_edges_dev (optional device int32) overrides n_edges (then the capacity). */
+int rg_edge_features(const float* px, const float* py, const float* vx, const float* vy,
+                     const int64_t* timestamp, const int* src, const int* dst,
+                     const int* n_edges_dev, long n_edges, float* out, void* stream);
+
+/* Undirected link pairs of edge_formation (gnn_blocks.py:295-296):
+ * nonzero(triu(adj,1)) row-major == CSR positions with col > row.
+ * pair_ptr int32[n_nodes+1]; pair_src/pair_dst int32[capacity]; n_pairs int32[1]. */
+size_t rg_link_pairs_workspace_size(int n_nodes);
+int rg_link_pairs(const int* row_ptr, const int* col, int n_nodes, int* pair_ptr, int* pair_src,
+                  int* pair_dst, long pair_capacity, int* n_pairs, void* workspace,
+                  size_t workspace_bytes, void* stream);
+
+/* Link pairs of an arbitrary edge_index (int64[2][E], reference order): the
+ * positions with edge_index[0] < edge_index[1], in edge order; equals
+ * nonzero(triu(adj,1)) when edge_index = np.where(adj) (graph_features.py:79). */
+size_t rg_pairs_from_edge_index_workspace_size(long n_edges);
+int rg_pairs_from_edge_index(const int64_t* edge_index, long n_edges, int* pair_src, int* pair_dst,
+                             int* n_pairs, void* workspace, size_t workspace_bytes, void* stream);
+
+/* out[p] = row of CSR position p (edge_index[0]; destination of a dst-major edge). */
+int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream);
+
+/* Destination-major CSR of an arbitrary edge_index (int64[2][E], reference order):
+ * dst_ptr int32[n_nodes+1]; perm int32[E] (dst-major position -> reference
+ * position), ordered by (dst, src, reference position); src_sorted int32[E]. */
+size_t rg_csr_by_dst_workspace_size(int n_nodes, long n_edges);
+int rg_csr_by_dst(const int64_t* edge_index, long n_edges, int n_nodes, int* dst_ptr, int* perm,
+                  int* src_sorted, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Dense views for the numpy-level drop-in compute_adjacency_information of ONE
+ * frame: adj uint8[N][N] from the CSR and dist float32[N][N] (either may be NULL). */
+int rg_dense_adjacency(const float* px, const float* py, const int* row_ptr, const int* col,
+                       int n_nodes, uint8_t* adj, float* dist, void* stream);
+
+/* out[r] = (int64) in[r] (edge_index boundary: datagen_gnn.py:123 int64) */
+int rg_i32_to_i64(const int* in, long n, int64_t* out, void* stream);
+
+/* out[r][:] = in[idx[r]][:] for float32 rows of width w */
+int rg_gather_rows_f32(const float* in, const int* idx, long rows, int w, float* out,
+                       void* stream);
+
+/* --------------------------------------------------------- dense MLP chains */
+
+/* Bytes of one packed Linear(in_dim -> out_dim) in `dtype`. */
+size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype);
+
+/* Pack a torch nn.Linear (weight float32 [out_dim][in_dim] row-major, bias
+ * float32[out_dim] or NULL; device) into the MFMA fragment order the chain
+ * kernels read, zero padded, followed by the bias padded to a multiple of 16. */
+int rg_pack_linear(const float* weight, const float* bias, int in_dim, int out_dim, int dtype,
+                   void* packed, void* stream);
+
+/* One ffn_block (common.py:185-205): Linear -> [channel_normalization] -> activation. */
+typedef struct rg_layer {
+  const void* w_packed;  /* rg_pack_linear output (weights + bias)             */
+  const float* norm_mu;  /* channel_normalization.mu  (1,) or NULL (no norm)     */
+  const float* norm_std; /* channel_normalization.std (1,)                       */
+  int in_dim;
+  int out_dim;
+  int act; /* RG_ACT_* */
+  int pad_;
+} rg_layer;
+
+#define RG_MAX_LAYERS 8
+
+/* A chain of up to RG_MAX_LAYERS ffn_blocks over `rows` rows (widths <= 256),
+ * fused in one kernel; activations never leave the chip between layers.
+ * Covers graph_feature_encoding (gnn_blocks.py:19-42), the message and update
+ * MLPs of residual_graph_conv_block (:104-113), the stems and
+ * FFN_TaskSpecificHead of every task head (:167-389).
+ *   in_mode  RG_IN_*: how row r's input vector is formed from in0/in1/in2
+ *   in_dtype element type of in0/in1/in2 (RG_F32 or the chain dtype)
+ *   rows_dev optional device int32 row count (overrides `rows` when non-NULL;
+ *            `rows` is then the capacity used for the grid)
+ *   residual optional [rows][out_dim] added after the last layer (:109)
+ *   out      [rows][ld_out] in out_dtype
+ */
+int rg_mlp_chain(int dtype, const rg_layer* layers_host, int n_layers, long rows,
+                 const int* rows_dev, int in_mode, int in_dtype, const void* in0, int ld0,
+                 int w0, const void* in1, int ld1, int w1, const void* in2, int ld2, int w2,
+                 const int* idx0, const int* idx1, const void* residual, int ld_res,
+                 int res_dtype, void* out, int ld_out, int out_dtype, void* stream);
+
+/* ----------------------------------------------------- segment reductions */
+
+/* out[s][c] = reduce_{p in [seg_ptr[s], seg_ptr[s+1])} src[row(p)][c], row(p) =
+ * idx ? idx[p] : p.  Sum in segment order (== the reference CPU scatter_add_ order
+ * for a destination-major CSR), mean = sum / max(count,1), max with empty -> 0
+ * (PyG scatter_reduce include_self=False).  src dtype RG_F32/RG_BF16, out float32
+ * or bf16; C <= 256. */
+int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
+                      const int* idx, int n_seg, int C, int op, void* out, int out_dtype,
+                      int ld_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RADAR_GNN_H */

@@ -1,0 +1,137 @@
+"""ORACLE (test infrastructure only) -- numpy restatement of the reference graph build.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / CPU baseline; the product
+path (the HIP library behind ``graph_neural_network_for_radar_perception_amd``)
+never calls it.
+
+Restates ``modules/compute_features/graph_features.py`` (reference v2) op for op:
+dense N x N float32 distance matrix, full-row argsort, ball query, symmetrised
+kNN adjacency, ``np.where`` edge list, node and edge input features.  It is as
+slow as the reference (O(N^2) memory and time) on purpose: it is the CPU
+baseline ``bench.py`` times.
+
+Pinning: checked bit-for-bit against the fixtures in ``tests/golden/graph_*.npz``,
+which ``tests/golden/make_golden.py`` produced by running the reference's own
+``graph_features.py`` in the build container (tests/test_oracle_golden.py).
+
+One deliberate difference: ``np.argsort(kind='stable')`` instead of the
+reference's default (unstable) kind at ``graph_features.py:34``.  On inputs
+without distance ties at the k-th neighbour the two select identical
+neighbour sets (all golden frames except the lattice); at ties the reference
+is implementation-defined and this oracle -- and the HIP kernel -- use
+"equal distance -> lower column index first".
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_US2SEC = 1e-6  # graph_features.py:7
+
+
+def pairwise_sq_distance(px: np.ndarray, py: np.ndarray) -> np.ndarray:
+    """graph_features.py:69-76: D[i,j] = (p_i-p_j)^T (p_i-p_j) in float32.
+
+    The reference evaluates it as a (N,N,1,2)@(N,N,2,1) matmul; for a 2-vector
+    numpy computes dx*dx + dy*dy (two roundings, no FMA), restated directly."""
+    pxy = np.stack((px, py), axis=-1).astype(np.float32)
+    d = pxy[:, None, :] - pxy[None, :, :]
+    dx = d[..., 0]
+    dy = d[..., 1]
+    return (dx * dx + dy * dy).astype(np.float32)
+
+
+def compute_ball_query(distance_mat: np.ndarray, eps: float) -> np.ndarray:
+    """graph_features.py:11-22: gated = D <= eps, diagonal cleared."""
+    gated = distance_mat <= eps
+    idx = np.arange(gated.shape[0])
+    gated[idx, idx] = False
+    return gated
+
+
+def compute_knn(distance_mat: np.ndarray, knn: int) -> np.ndarray:
+    """graph_features.py:25-44: first k+1 columns of the row argsort (all if
+    k >= N), marked both ways, diagonal cleared.  Stable sort (see module doc)."""
+    n = distance_mat.shape[0]
+    order = np.argsort(distance_mat, axis=-1, kind='stable')
+    kk = n if knn >= n else knn + 1
+    dst = order[:, :kk]
+    src = np.repeat(np.arange(n)[:, None], kk, axis=1)
+    gated = np.zeros((n, n), dtype=np.bool_)
+    gated[src.reshape(-1), dst.reshape(-1)] = True
+    gated[dst.reshape(-1), src.reshape(-1)] = True
+    gated[np.arange(n), np.arange(n)] = False
+    return gated
+
+
+def normalize_time(t: np.ndarray) -> np.ndarray:
+    """graph_features.py:47-55."""
+    tmax = np.max(t)
+    tmin = np.min(t)
+    if tmax == tmin:
+        return t - tmin
+    return (t - tmin) / (tmax - tmin)
+
+
+def compute_adjacency_information(data_dict: dict, eps: float, knn: int) -> dict:
+    """graph_features.py:58-84."""
+    dmat = pairwise_sq_distance(data_dict['meas_px'], data_dict['meas_py'])
+    ball = compute_ball_query(dmat, eps)
+    adj = compute_knn(dmat, knn)
+    degree = np.sum(ball, axis=-1)
+    adj_list = np.stack(np.where(adj), axis=0)
+    return {'adj_matrix': adj, 'distance_mat': dmat, 'adj_list': adj_list, 'degree': degree}
+
+
+def compute_radius_graph(data_dict: dict, eps: float) -> np.ndarray:
+    """Pure radius graph = np.where(compute_ball_query(D, eps)) (BASELINE config 5)."""
+    dmat = pairwise_sq_distance(data_dict['meas_px'], data_dict['meas_py'])
+    return np.stack(np.where(compute_ball_query(dmat, eps)), axis=0)
+
+
+def compute_node_features(data_dict, node_degree, include_region_confidence=False,
+                          min_range=None, max_range=None, min_azimuth=None, max_azimuth=None):
+    """graph_features.py:117-144 (float64 result, as in the reference)."""
+    vr = data_dict['meas_vr']
+    rcs = data_dict['meas_rcs']
+    tn = normalize_time(data_dict['meas_timestamp'])
+    deg = node_degree / 10
+    if include_region_confidence:
+        r = np.sqrt(data_dict['meas_px'] ** 2 + data_dict['meas_py'] ** 2)
+        th = np.abs(np.arctan2(data_dict['meas_py'], data_dict['meas_px']))
+        range_conf = (r - max_range) / (min_range - max_range)
+        azi = (th - max_azimuth) / (min_azimuth - max_azimuth)
+        return np.stack((vr, rcs, tn, deg, range_conf, azi), axis=-1)
+    return np.stack((vr, rcs, tn, deg), axis=-1)
+
+
+def compute_edge_features(data_dict, adj_list):
+    """graph_features.py:147-164 (float64 result; note the double /10 on dl)."""
+    s, d = adj_list[0], adj_list[1]
+    px, py = data_dict['meas_px'], data_dict['meas_py']
+    vx, vy = data_dict['meas_vx'], data_dict['meas_vy']
+    t = data_dict['meas_timestamp']
+    dx = (px[s] - px[d]) / 10
+    dy = (py[s] - py[d]) / 10
+    dl = (np.sqrt(dx ** 2 + dy ** 2)) / 10
+    dvx = vx[s] - vx[d]
+    dvy = vy[s] - vy[d]
+    dvl = np.sqrt(dvx ** 2 + dvy ** 2)
+    dt = (t[s] - t[d]) * _US2SEC
+    return np.stack((dx, dy, dl, dvx, dvy, dvl, dt), axis=-1)
+
+
+def build_frame_graph(frame: dict, eps: float, knn: int, grid_max_r: float,
+                      grid_max_th: float = np.pi * 0.5):
+    """The per-frame sequence of ``datagen_gnn.py:104-124``: adjacency, edge and
+    node features, cast to float32 / int64 as the tensorization does."""
+    adj = compute_adjacency_information(frame, eps, knn)
+    ef = compute_edge_features(frame, adj['adj_list'])
+    nf = compute_node_features(frame, adj['degree'], True, 0, grid_max_r, 0, grid_max_th)
+    return {
+        'edge_index': adj['adj_list'].astype(np.int64),
+        'adj_matrix': adj['adj_matrix'],
+        'degree': adj['degree'],
+        'edge_features': ef.astype(np.float32),
+        'node_features': nf.astype(np.float32),
+    }

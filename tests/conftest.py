@@ -1,0 +1,78 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs a real MI355X (HIP device)')
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
+
+
+def golden_names(prefix):
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, prefix + '*.npz')))
+
+
+# architecture overrides used by tests/golden/make_golden.py for each model fixture
+MODEL_CASES = {
+    'model_trained_N50': dict(),
+    'model_trained_N500': dict(),
+    'model_random_L3_N500_k16': dict(graph_convolution_stem_channels=[64, 64, 64],
+                                     k_number_nearest_points=16),
+    'model_random_L6_N300_k32': dict(graph_convolution_stem_channels=[64] * 6),
+    'model_random_mean_N200': dict(graph_convolution_stem_channels=[64, 64], aggregation='mean'),
+    'model_random_max_N200': dict(graph_convolution_stem_channels=[64, 64], aggregation='max'),
+    'model_random_widths_N120': dict(node_feat_enc_stem_channels=[128, 96],
+                                     edge_feat_enc_stem_channels=[64, 32],
+                                     graph_convolution_stem_channels=[64, 32],
+                                     msg_mlp_hidden_dim=96, link_pred_stem_channels=[32, 32],
+                                     node_pred_stem_channels=[32, 64],
+                                     num_blocks_to_compute_edge=2),
+}
+
+
+def model_cfg(name):
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    return default_config(**MODEL_CASES[name])
+
+
+def model_state_dict(name):
+    """Weights of a model fixture: stored tensors (trained / widths cases) or the
+    seeded reference initialisation reproduced by the mirror module tree."""
+    import torch
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    d = golden(name)
+    if 'w/pred.encode_node_feat.encoder.0.block.0.weight' in d.files:
+        return {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith('w/')}
+    if name.startswith('model_trained'):
+        d0 = golden('model_trained_N50')
+        return {k[2:]: torch.from_numpy(d0[k]) for k in d0.files if k.startswith('w/')}
+    torch.manual_seed(int(d['model_seed']))
+    m = Model_Training(model_cfg(name), 'cpu')
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def cluster_lists(d):
+    import torch
+    ptr, idx = d['cluster_ptr'], d['cluster_idx']
+    return [torch.from_numpy(idx[ptr[i]:ptr[i + 1]].copy()) for i in range(len(ptr) - 1)]
+
+
+@pytest.fixture(scope='session')
+def cuda_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from graph_neural_network_for_radar_perception_amd import _native
+    _native.lib()  # fail loudly if the HIP library is missing on a GPU box
+    return torch.device('cuda', 0)

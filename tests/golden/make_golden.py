@@ -1,0 +1,270 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Runs only in the build container, where /root/reference exists (it never runs on
+the GPU box; nothing in tests/ imports this file).  It imports the reference's
+own modules and records their outputs on seeded synthetic frames:
+
+  * graph build: ``modules/compute_features/graph_features.py`` imports with
+    numpy only -- these fixtures are produced by the unmodified reference code.
+  * model forward: ``modules/neural_net/gnn/gnn_detector.py`` imports two
+    third-party packages that are NOT installed here (no network):
+      - ``torch_geometric`` (>= 2.5.0, README.md:156; no lockfile) for
+        ``MessagePassing`` (call sites gnn_blocks.py:8,57,106,112);
+      - ``torchvision`` for ``ops.sigmoid_focal_loss`` (lossfunc.py:5,55),
+        training-only.
+    For these two, ``_install_third_party_restatements`` registers in-memory
+    modules that restate their PUBLISHED algorithms (PyG 2.5
+    ``MessagePassing.propagate`` with ``flow='source_to_target'``:
+    x_i = x[edge_index[1]], x_j = x[edge_index[0]], aggregate at
+    edge_index[1] with ``scatter_add_`` / mean / ``scatter_reduce_(amax,
+    include_self=False)``; torchvision ``sigmoid_focal_loss``).  Everything
+    else executed is the reference's own code.  Parity for the PyG part is
+    therefore anchored on its published semantics, not on a pinned run of PyG
+    ("parity unpinned" for that part).
+
+Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from graph_neural_network_for_radar_perception_amd import synthetic  # noqa: E402
+
+CKPT = os.path.join(REF, 'model_weights/gnn/1718175257362/graph_based_detector.pt')
+
+
+def _install_third_party_restatements():
+    """In-memory restatement of the two absent third-party APIs (see module doc)."""
+    class MessagePassing(torch.nn.Module):
+        def __init__(self, aggr='add', flow='source_to_target', **kwargs):
+            super().__init__()
+            self.aggr = aggr
+            self.flow = flow
+
+        def propagate(self, edge_index, size=None, **kwargs):
+            x = kwargs['x']
+            i, j = (1, 0) if self.flow == 'source_to_target' else (0, 1)
+            x_i = x.index_select(0, edge_index[i])
+            x_j = x.index_select(0, edge_index[j])
+            msg = self.message(x_i=x_i, x_j=x_j, edge_attr=kwargs.get('edge_attr'))
+            n = x.shape[0]
+            idx = edge_index[i].view(-1, 1).expand_as(msg)
+            if self.aggr in ('add', 'sum'):
+                out = msg.new_zeros((n, msg.shape[1])).scatter_add_(0, idx, msg)
+            elif self.aggr == 'mean':
+                out = msg.new_zeros((n, msg.shape[1])).scatter_add_(0, idx, msg)
+                cnt = msg.new_zeros((n,)).scatter_add_(0, edge_index[i], msg.new_ones((msg.shape[0],)))
+                out = out / cnt.clamp(min=1).view(-1, 1)
+            elif self.aggr == 'max':
+                out = msg.new_zeros((n, msg.shape[1])).scatter_reduce_(
+                    0, idx, msg, reduce='amax', include_self=False)
+            else:
+                raise ValueError(self.aggr)
+            return out
+
+    class GATv2Conv(torch.nn.Module):  # gnn_attention.py:9 -- unused variant
+        def __init__(self, *a, **k):
+            raise NotImplementedError('GATv2Conv is not restated (unused by the reference)')
+
+    def sigmoid_focal_loss(inputs, targets, alpha=0.25, gamma=2.0, reduction='none'):
+        p = torch.sigmoid(inputs)
+        ce = F.binary_cross_entropy_with_logits(inputs, targets, reduction='none')
+        p_t = p * targets + (1 - p) * (1 - targets)
+        loss = ce * ((1 - p_t) ** gamma)
+        if alpha >= 0:
+            loss = (alpha * targets + (1 - alpha) * (1 - targets)) * loss
+        if reduction == 'mean':
+            return loss.mean()
+        if reduction == 'sum':
+            return loss.sum()
+        return loss
+
+    pyg = types.ModuleType('torch_geometric')
+    pyg_nn = types.ModuleType('torch_geometric.nn')
+    pyg_conv = types.ModuleType('torch_geometric.nn.conv')
+    pyg_conv.MessagePassing = MessagePassing
+    pyg_conv.GATv2Conv = GATv2Conv
+    pyg_nn.conv = pyg_conv
+    pyg_nn.GATv2Conv = GATv2Conv
+    pyg.nn = pyg_nn
+    tv = types.ModuleType('torchvision')
+    tv_ops = types.ModuleType('torchvision.ops')
+    tv_ops.sigmoid_focal_loss = sigmoid_focal_loss
+    tv.ops = tv_ops
+    sys.modules.update({'torch_geometric': pyg, 'torch_geometric.nn': pyg_nn,
+                        'torch_geometric.nn.conv': pyg_conv,
+                        'torchvision': tv, 'torchvision.ops': tv_ops})
+
+
+def _ref_graph(frame, eps, knn):
+    from modules.compute_features.graph_features import (
+        compute_adjacency_information, compute_node_features, compute_edge_features)
+    from modules.set_configurations.set_config_gnn import config
+    cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+    adj = compute_adjacency_information(frame, eps, knn)
+    ef = compute_edge_features(frame, adj['adj_list'])
+    nf = compute_node_features(frame, adj['degree'], include_region_confidence=True,
+                               min_range=cfg.grid_min_r, max_range=cfg.grid_max_r,
+                               min_azimuth=cfg.grid_min_th, max_azimuth=cfg.grid_max_th)
+    return adj, nf, ef
+
+
+def _frame_arrays(frame):
+    return {k: frame[k] for k in ('meas_px', 'meas_py', 'meas_vx', 'meas_vy',
+                                  'meas_vr', 'meas_rcs', 'meas_timestamp')}
+
+
+def make_graph_fixtures():
+    cases = [(2, 10, 25.0), (8, 10, 25.0), (11, 10, 25.0), (12, 10, 25.0), (50, 10, 25.0),
+             (500, 16, 25.0), (1000, 32, 25.0), (3000, 10, 25.0), (300, 8, 4.0)]
+    for n, k, eps in cases:
+        seed = synthetic.SEED0 + 7 * n + k
+        fr = synthetic.make_frame(n, seed)
+        adj, nf, ef = _ref_graph(fr, eps, k)
+        out = dict(_frame_arrays(fr))
+        out.update(n=n, k=k, eps=eps, seed=seed,
+                   adj_list=adj['adj_list'].astype(np.int32),
+                   degree=adj['degree'].astype(np.int32),
+                   node_features=nf.astype(np.float32),
+                   node_features_f64=nf,
+                   edge_features=ef.astype(np.float32))
+        np.savez_compressed(os.path.join(HERE, f'graph_N{n}_k{k}.npz'), **out)
+        print('graph', n, k, adj['adj_list'].shape)
+    # tie lattice: distances tie massively; numpy's default argsort is unstable,
+    # so the reference's neighbour choice at ties is implementation-defined.
+    from modules.compute_features.graph_features import compute_adjacency_information, compute_ball_query
+    fr = synthetic.make_frame(400, 99, lattice=True)
+    adj = compute_adjacency_information(fr, 25.0, 10)
+    np.savez_compressed(os.path.join(HERE, 'graph_lattice_N400_k10.npz'),
+                        **_frame_arrays(fr), n=400, k=10, eps=25.0,
+                        adj_list=adj['adj_list'].astype(np.int32),
+                        degree=adj['degree'].astype(np.int32))
+    # pure radius graph (compute_ball_query semantics; BASELINE config 5 shape, small)
+    fr = synthetic.make_frame(2000, 4242)
+    pxy = np.stack((fr['meas_px'], fr['meas_py']), axis=-1)
+    d = np.expand_dims(pxy[:, None, :] - pxy[None, :, :], -1)
+    dist = (d.transpose(0, 1, 3, 2) @ d).squeeze(-1).squeeze(-1)
+    gated = compute_ball_query(dist, 2.5)
+    np.savez_compressed(os.path.join(HERE, 'graph_radius_N2000.npz'),
+                        **_frame_arrays(fr), n=2000, eps=2.5,
+                        adj_list=np.stack(np.where(gated), 0).astype(np.int32))
+    print('lattice/radius done')
+
+
+def _model(cfg, seed=None, ckpt=None):
+    from modules.neural_net.gnn.gnn_detector import Model_Training
+    if seed is not None:
+        torch.manual_seed(seed)
+    m = Model_Training(cfg, 'cpu')
+    if ckpt is not None:
+        sd = torch.load(ckpt, map_location='cpu', weights_only=True)
+        m.load_state_dict(sd)
+    return m.eval()
+
+
+def _forward_case(name, cfg, n, k, seed_frame, model_seed=None, ckpt=None,
+                  save_weights=False, intermediates=False):
+    fr = synthetic.make_frame(n, seed_frame)
+    adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, k)
+    model = _model(cfg, seed=model_seed, ckpt=ckpt)
+    clusters = synthetic.cluster_lists(n)
+    node_t = torch.from_numpy(nf).to(torch.float32)
+    edge_t = torch.from_numpy(ef).to(torch.float32)
+    ei_t = torch.from_numpy(adj['adj_list']).to(torch.int64)
+    adj_t = torch.from_numpy(adj['adj_matrix']).to(torch.bool)
+    cl_t = [torch.from_numpy(c) for c in clusters]
+    inter = {}
+    hooks = []
+    if intermediates:
+        p = model.pred
+        hooks.append(p.encode_node_feat.register_forward_hook(
+            lambda m, i, o: inter.__setitem__('x_enc', o.detach().numpy().copy())))
+        hooks.append(p.encode_edge_feat.register_forward_hook(
+            lambda m, i, o: inter.__setitem__('e_enc', o.detach().numpy().copy())))
+        for li, blk in enumerate(p.pass_messages.conv_blk):
+            hooks.append(blk.register_forward_hook(
+                (lambda li_: lambda m, i, o: inter.__setitem__(f'x_l{li_}', o.detach().numpy().copy()))(li)))
+    with torch.no_grad():
+        outs = model.pred(node_t, edge_t, ei_t, adj_t, cl_t)
+    for h in hooks:
+        h.remove()
+    sd = model.state_dict()
+    fp = {('fp/' + k): np.array([v.double().sum().item(), v.double().abs().sum().item()])
+          for k, v in sd.items()}
+    data = dict(_frame_arrays(fr))
+    data.update(n=n, k=k, eps=float(cfg.ball_query_eps_square), frame_seed=seed_frame,
+                L=len(cfg.graph_convolution_stem_channels), aggregation=cfg.aggregation,
+                model_seed=-1 if model_seed is None else model_seed,
+                node_features=nf.astype(np.float32), edge_features=ef.astype(np.float32),
+                edge_index=adj['adj_list'].astype(np.int32),
+                cluster_ptr=np.cumsum([0] + [len(c) for c in clusters]).astype(np.int64),
+                cluster_idx=np.concatenate(clusters).astype(np.int64),
+                node_cls=outs[0].numpy(), node_reg=outs[1].numpy(),
+                link_cls=outs[2].numpy(), obj_cls=outs[3].numpy(), **fp)
+    for k_, v in inter.items():
+        data['inter/' + k_] = v
+    if save_weights:
+        for k_, v in sd.items():
+            data['w/' + k_] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, name + '.npz'), **data)
+    print('model', name, 'E', adj['adj_list'].shape[1], 'U', outs[2].shape[0])
+
+
+def make_model_fixtures():
+    from modules.set_configurations.set_config_gnn import config
+    ycfg = os.path.join(REF, 'configuration_radarscenes_gnn.yml')
+    # trained checkpoint (metric shape M uses it), yml architecture, k=10
+    cfg = config(ycfg)
+    _forward_case('model_trained_N50', cfg, 50, 10, 5001, ckpt=CKPT,
+                  save_weights=True, intermediates=True)
+    _forward_case('model_trained_N500', cfg, 500, 10, 5002, ckpt=CKPT)
+    # BASELINE config 1: N=500, k=16, L=3, random init torch.manual_seed(1234)
+    cfg = config(ycfg)
+    cfg.graph_convolution_stem_channels = [64, 64, 64]
+    cfg.k_number_nearest_points = 16
+    _forward_case('model_random_L3_N500_k16', cfg, 500, 16, 5003, model_seed=1234)
+    # config 2 per-frame structure (k=32, L=6) at a small N
+    cfg = config(ycfg)
+    cfg.graph_convolution_stem_channels = [64] * 6
+    _forward_case('model_random_L6_N300_k32', cfg, 300, 32, 5004, model_seed=4321)
+    # other PyG aggregations (restated semantics; parity unpinned)
+    for aggr in ('mean', 'max'):
+        cfg = config(ycfg)
+        cfg.graph_convolution_stem_channels = [64, 64]
+        cfg.aggregation = aggr
+        _forward_case(f'model_random_{aggr}_N200', cfg, 200, 10, 5005, model_seed=77,
+                      intermediates=True)
+    # mixed widths: residual_connection path (gnn_blocks.py:84-94) + non-default widths
+    cfg = config(ycfg)
+    cfg.node_feat_enc_stem_channels = [128, 96]
+    cfg.edge_feat_enc_stem_channels = [64, 32]
+    cfg.graph_convolution_stem_channels = [64, 32]
+    cfg.msg_mlp_hidden_dim = 96
+    cfg.link_pred_stem_channels = [32, 32]
+    cfg.node_pred_stem_channels = [32, 64]
+    cfg.num_blocks_to_compute_edge = 2
+    _forward_case('model_random_widths_N120', cfg, 120, 10, 5006, model_seed=99,
+                  save_weights=True, intermediates=True)
+
+
+def main():
+    sys.path.insert(0, REF)
+    _install_third_party_restatements()
+    torch.set_num_threads(8)
+    make_graph_fixtures()
+    make_model_fixtures()
+
+
+if __name__ == '__main__':
+    main()

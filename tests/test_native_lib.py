@@ -1,0 +1,79 @@
+"""The C ABI library builds, loads and exports every function include/radar_gnn.h
+declares; argument validation works without a GPU (no compute calls here)."""
+import ctypes
+
+import pytest
+
+from graph_neural_network_for_radar_perception_amd import _native as nat
+
+
+@pytest.fixture(scope='module')
+def lib():
+    from graph_neural_network_for_radar_perception_amd import build
+    build.build_library()
+    return nat.lib()
+
+
+def test_every_header_function_exported(lib):
+    names = nat.header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in nat._SIGNATURES, f'{n} declared in radar_gnn.h but not bound in _native.py'
+
+
+def test_version(lib):
+    assert lib.rg_version() >= 1
+
+
+def test_packed_sizes(lib):
+    # f32: 16-row M tiles x 16-deep k groups x 64 lanes x float4, + bias padded to 16
+    assert lib.rg_packed_linear_bytes(6, 256, nat.RG_F32) == 16 * 1 * 64 * 16 + 256 * 4
+    # bf16: 16-row M tiles x 32-deep k steps x 64 lanes x 8 bf16, + f32 bias
+    assert lib.rg_packed_linear_bytes(192, 128, nat.RG_BF16) == 8 * 6 * 64 * 16 + 128 * 4
+    assert lib.rg_packed_linear_bytes(64, 7, nat.RG_BF16) == 1 * 2 * 64 * 16 + 16 * 4
+
+
+def test_chain_argument_errors_are_reported(lib):
+    arr = (nat.rg_layer * 1)()
+    rc = lib.rg_mlp_chain(nat.RG_F32, arr, 0, 10, None, 0, 0, None, 0, 0, None, 0, 0, None, 0, 0,
+                          None, None, None, 0, 0, None, 0, 0, None)
+    assert rc == 1
+    assert b'n_layers' in lib.rg_last_error()
+    arr[0].w_packed = 16
+    arr[0].in_dim, arr[0].out_dim = 300, 8
+    rc = lib.rg_mlp_chain(nat.RG_F32, arr, 1, 10, None, 0, 0, 16, 300, 300, None, 0, 0, None, 0, 0,
+                          None, None, None, 0, 0, 16, 8, 0, None)
+    assert rc == 3
+    assert b'outside' in lib.rg_last_error()
+    with pytest.raises(RuntimeError, match='rg_mlp_chain'):
+        nat.check(rc, 'rg_mlp_chain')
+
+
+def test_graph_build_argument_errors(lib):
+    rc = lib.rg_build_graph(None, None, None, 10, 1, 10, 100, 25.0, 0, None, None, 0, None, None,
+                            None, 0, None)
+    assert rc == 3 and b'k=100' in lib.rg_last_error()
+    rc = lib.rg_build_graph(None, None, None, 10, 1, 10, 10, 25.0, 0, None, None, 0, None, None,
+                            None, 0, None)
+    assert rc == 1 and b'workspace' in lib.rg_last_error()
+
+
+def test_segment_reduce_rejects_bad_widths(lib):
+    rc = lib.rg_segment_reduce(None, 0, 6, None, None, 4, 6, 0, None, 0, 6, None)
+    assert rc == 3
+
+
+def test_workspace_queries(lib):
+    assert lib.rg_build_graph_workspace_size(3000, 1, 3000, 10, 0) > 3000 * 94 * 4
+    assert lib.rg_link_pairs_workspace_size(100) > 0
+    assert lib.rg_csr_by_dst_workspace_size(100, 1000) > 0
+    assert lib.rg_pairs_from_edge_index_workspace_size(1000) > 0
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(nat, '_lib', None)
+    monkeypatch.setattr(nat, '_load_error', None)
+    monkeypatch.setattr(nat, 'LIB_PATH', str(tmp_path / 'nope.so'))
+    with pytest.raises(nat.NativeLibraryError):
+        nat.lib()
