@@ -49,10 +49,10 @@ __global__ __launch_bounds__(256) void node_features_kernel(
     const double tn = tmax == tmin ? (double)(ts[i] - tmin) : (double)(ts[i] - tmin) / span;
     const double dg = (double)deg[i] / 10.0;
     const float x = px[i], y = py[i];
-    const float r = __fsqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
+    const float r = sqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
     const double rc = ((double)r - max_r) / (min_r - max_r);
     const float th = fabsf((float)atan2((double)y, (double)x));
-    const float az = __fdiv_rn(__fsub_rn(th, max_az), az_den);
+    const float az = div_rn(__fsub_rn(th, max_az), az_den);
     float* o = out + (size_t)i * 6;
     o[0] = vr[i];
     o[1] = rcs[i];
@@ -77,12 +77,12 @@ __global__ __launch_bounds__(256) void edge_features_kernel(
   for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < E && p < n_edges; p += stride) {
     const int s = src[p];
     const int d = dst[p];
-    const float dx = __fdiv_rn(__fsub_rn(px[s], px[d]), 10.f);
-    const float dy = __fdiv_rn(__fsub_rn(py[s], py[d]), 10.f);
-    const float dl = __fdiv_rn(__fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))), 10.f);
+    const float dx = div_rn(__fsub_rn(px[s], px[d]), 10.f);
+    const float dy = div_rn(__fsub_rn(py[s], py[d]), 10.f);
+    const float dl = div_rn(sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))), 10.f);
     const float dvx = __fsub_rn(vx[s], vx[d]);
     const float dvy = __fsub_rn(vy[s], vy[d]);
-    const float dv = __fsqrt_rn(__fadd_rn(__fmul_rn(dvx, dvx), __fmul_rn(dvy, dvy)));
+    const float dv = sqrt_rn(__fadd_rn(__fmul_rn(dvx, dvx), __fmul_rn(dvy, dvy)));
     const float dt = (float)((double)(ts[s] - ts[d]) * 1e-6);
     float* o = out + (size_t)p * 7;
     o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;

@@ -408,6 +408,10 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 #pragma unroll
         for (int m = 0; m < 16; ++m)
           if (m < mt) st4_slab<T>(row + 16 * m + 4 * g, acc[m]);
+        // zero the next layer's K padding beyond the 16*mt features written above
+        // (bf16 k-steps are 32 deep: an odd tile count leaves 16 stale columns)
+        if (kpad(L.out, Cfg<T>::KPAD) > 16 * mt)
+          st4_slab<T>(row + 16 * mt + 4 * g, (f32x4){0.f, 0.f, 0.f, 0.f});
       } else {
         const long row = r0 + r;
         if (row < rows) store_rows(acc, a, row, mt, L.out, g);

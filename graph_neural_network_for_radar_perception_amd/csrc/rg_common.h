@@ -62,6 +62,14 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// Correctly rounded f32 sqrt / division (numpy semantics).  The hardware f32
+// v_sqrt / v_rcp paths are not correctly rounded; the f64 result rounded once
+// to f32 is (53 >= 2*24 + 2 bits, so the double rounding is exact).
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)__dsqrt_rn((double)x); }
+__device__ __forceinline__ float div_rn(float a, float b) {
+  return (float)__ddiv_rn((double)a, (double)b);
+}
+
 // MFMA operand / accumulator vector types
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

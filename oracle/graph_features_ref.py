@@ -127,7 +127,10 @@ def build_frame_graph(frame: dict, eps: float, knn: int, grid_max_r: float,
     node features, cast to float32 / int64 as the tensorization does."""
     adj = compute_adjacency_information(frame, eps, knn)
     ef = compute_edge_features(frame, adj['adj_list'])
-    nf = compute_node_features(frame, adj['degree'], True, 0, grid_max_r, 0, grid_max_th)
+    # set_config_gnn.py:44 computes grid_max_r with np.sqrt -> np.float64 (a strong
+    # scalar: range_conf is evaluated in float64); grid_max_th = np.pi*0.5 is a python float
+    nf = compute_node_features(frame, adj['degree'], True, 0, np.float64(grid_max_r), 0,
+                               float(grid_max_th))
     return {
         'edge_index': adj['adj_list'].astype(np.int64),
         'adj_matrix': adj['adj_matrix'],

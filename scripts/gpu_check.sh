@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU validation pass used with gpurun: smoke -> gpu tests -> short bench.
+# Stops at the first crash-like exit (fault/abort/timeout); test failures
+# (pytest exit 1) still let the bench run.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
+exit $rc

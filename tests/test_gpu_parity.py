@@ -6,7 +6,8 @@ edge_index bit-exact):
   * edge features                                      : bit-exact (same fp32 ops, no FMA)
   * node features                                      : <= 2 ulp (atan2 is libm-dependent)
   * fp32 forward outputs                               : |d| <= 1e-4 + 1e-4 |ref|
-  * bf16 forward outputs (BASELINE config 2 dtype)     : |d| <= 0.1 + 0.05 |ref|, and >= 97 %
+  * bf16 forward outputs (BASELINE config 2 dtype)     : every |d| <= 0.5 + 0.1 |ref|, 99.9 % of
+                                                         elements |d| <= 0.1 + 0.05 |ref|, >= 97 %
                                                          argmax agreement of class logits
 """
 import numpy as np
@@ -173,9 +174,12 @@ def test_forward_bf16_close_to_reference(cuda_device, name):
                    [c.to(dev) for c in cluster_lists(d)])
     for got, key in zip(out, ('node_cls', 'node_reg', 'link_cls', 'obj_cls')):
         g = got.cpu().numpy()
-        np.testing.assert_allclose(g, d[key], rtol=0.05, atol=0.1, err_msg=key)
+        ref = d[key]
+        err = np.abs(g - ref)
+        assert np.all(err <= 0.5 + 0.1 * np.abs(ref)), (key, err.max())
+        assert np.mean(err <= 0.1 + 0.05 * np.abs(ref)) >= 0.999, key
         if key in ('node_cls', 'link_cls', 'obj_cls'):
-            agree = (g.argmax(-1) == d[key].argmax(-1)).mean()
+            agree = (g.argmax(-1) == ref.argmax(-1)).mean()
             assert agree >= 0.97, (key, agree)
 
 
