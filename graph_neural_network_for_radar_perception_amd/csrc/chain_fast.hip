@@ -1,0 +1,471 @@
+// Register-resident bf16 MLP chains for the shapes of the shipped architecture.
+//
+// Same semantics as rg_mlp_chain (ffn_block chains: Linear -> channel_normalization
+// -> activation, common.py:185-220, gnn_blocks.py:19-389) but every width is a
+// compile-time constant, so the whole chain is unrolled:
+//
+//  * one wave = 32 rows; v_mfma_f32_32x32x16_bf16 computes Y^T = W . X^T, so lane
+//    (r = lane&31, h = lane>>5) holds row r's features {32m + 8(q>>2) + 4h + (q&3)}
+//    in accumulator register q of M-tile m;
+//  * channel_normalization statistics = in-lane sum + ONE xor-32 exchange;
+//  * a layer's accumulators become the next layer's B operand IN REGISTERS
+//    (registers 8s'..8s'+7 of a tile, packed to bf16, are k-step s'; the next
+//    layer's weights are packed with that k permutation, rg_pack_linear format
+//    RG_PACK_FAST_CHAIN), so activations never touch LDS or HBM between layers;
+//  * the first layer's B fragments are loaded straight from HBM/L2 into
+//    registers: dense rows, concatenations (update MLP, gnn_blocks.py:108), the
+//    gathered cat(x_i, x_j, e) of MessagePassing.message (gnn_blocks.py:113) or the
+//    pair sum x_i + x_j of edge_formation (gnn_blocks.py:297);
+//  * every layer's packed weights + bias live in LDS for the whole (persistent)
+//    workgroup: 8 waves, two per SIMD, share them; one 1-KiB ds_read_b128 feeds a
+//    32-cycle MFMA.
+#include "rg_common.h"
+
+namespace rg {
+namespace fast {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+static constexpr int FT = 512;  // 8 waves per workgroup (2 per SIMD)
+static constexpr int FW = FT / 64;
+static constexpr float NORM_EPS = 1e-5f;
+
+struct FLayer {
+  const void* src;  // packed weights (+bias) in global memory
+  const float* mu;
+  const float* sd;
+  int woff;   // byte offset of the layer in the LDS image
+  int bytes;  // packed bytes
+  int out;    // real output width
+  int act;
+};
+
+struct FArgs {
+  FLayer L[RG_MAX_LAYERS];
+  int nl;
+  int total_bytes;
+  long rows;
+  const int* rows_dev;
+  const void* in0;
+  const void* in1;
+  const void* in2;
+  int ld0, ld1, ld2;
+  int in_f32;   // in0 is float32 (DENSE only)
+  int w0real;   // real width of a float32 DENSE input
+  const int* idx0;
+  const int* idx1;
+  const void* res;
+  int ld_res, res_f32;
+  void* out;
+  int ld_out, out_f32, out_real;
+};
+
+__device__ __forceinline__ uint32_t bf2(float a, float b) { return pack_bf16x2(a, b); }
+
+__device__ __forceinline__ bf16x8_t ld_bf8(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *(const u32x4*)p);
+}
+
+__device__ __forceinline__ bf16x8_t zero_bf8() {
+  return __builtin_bit_cast(bf16x8_t, (u32x4){0u, 0u, 0u, 0u});
+}
+
+// x_i + x_j of two bf16x8 rows, added in f32 and rounded once
+__device__ __forceinline__ bf16x8_t add_bf8(bf16x8_t a, bf16x8_t b) {
+  const u32x4 ua = __builtin_bit_cast(u32x4, a), ub = __builtin_bit_cast(u32x4, b);
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a0 = __uint_as_float(ua[i] << 16), a1 = __uint_as_float(ua[i] & 0xffff0000u);
+    const float b0 = __uint_as_float(ub[i] << 16), b1 = __uint_as_float(ub[i] & 0xffff0000u);
+    o[i] = bf2(__fadd_rn(a0, b0), __fadd_rn(a1, b1));
+  }
+  return __builtin_bit_cast(bf16x8_t, o);
+}
+
+// ----------------------------------------------------------------- layer-0 operands
+// k-step s, lane half h: features [16s + 8h, 16s + 8h + 8) of the row's input vector
+template <int MODE, bool IN_F32, int W0, int W1>
+struct Input {
+  static constexpr int K0 = MODE == RG_IN_GATHER3 ? 2 * W0 + W1
+                          : (MODE == RG_IN_CONCAT2 ? W0 + W1 : W0);
+  static constexpr int KS = (K0 + 15) / 16;
+
+  static __device__ __forceinline__ void load(const FArgs& a, long row, bool valid, int h,
+                                              bf16x8_t (&b)[KS]) {
+    if (!valid) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[s] = zero_bf8();
+      return;
+    }
+    if constexpr (MODE == RG_IN_DENSE && IN_F32) {
+      const float* p = (const float*)a.in0 + (size_t)row * a.ld0;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int f = 16 * s + 8 * h + j;
+          v[j] = f < a.w0real ? p[f] : 0.f;
+        }
+        b[s] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0], v[1]), bf2(v[2], v[3]),
+                                                    bf2(v[4], v[5]), bf2(v[6], v[7])});
+      }
+    } else if constexpr (MODE == RG_IN_DENSE) {
+      static_assert(W0 % 16 == 0, "bf16 dense input width must be a multiple of 16");
+      const uint16_t* p = (const uint16_t*)a.in0 + (size_t)row * a.ld0 + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[s] = ld_bf8(p + 16 * s);
+    } else if constexpr (MODE == RG_IN_CONCAT2) {
+      static_assert(W0 % 16 == 0 && W1 % 16 == 0, "concat widths must be multiples of 16");
+      const uint16_t* p0 = (const uint16_t*)a.in0 + (size_t)row * a.ld0 + 8 * h;
+      const uint16_t* p1 = (const uint16_t*)a.in1 + (size_t)row * a.ld1 + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        b[s] = s < W0 / 16 ? ld_bf8(p0 + 16 * s) : ld_bf8(p1 + 16 * (s - W0 / 16));
+    } else if constexpr (MODE == RG_IN_GATHER3) {
+      static_assert(W0 % 16 == 0 && W1 % 16 == 0, "gather widths must be multiples of 16");
+      const int ri = a.idx0[row], rj = a.idx1[row];
+      const uint16_t* pi = (const uint16_t*)a.in0 + (size_t)ri * a.ld0 + 8 * h;
+      const uint16_t* pj = (const uint16_t*)a.in0 + (size_t)rj * a.ld0 + 8 * h;
+      const uint16_t* pe = (const uint16_t*)a.in2 + (size_t)row * a.ld2 + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (s < W0 / 16) b[s] = ld_bf8(pi + 16 * s);
+        else if (s < 2 * W0 / 16) b[s] = ld_bf8(pj + 16 * (s - W0 / 16));
+        else b[s] = ld_bf8(pe + 16 * (s - 2 * W0 / 16));
+      }
+    } else {  // RG_IN_PAIRADD
+      static_assert(W0 % 16 == 0, "pair width must be a multiple of 16");
+      const int ri = a.idx0[row], rj = a.idx1[row];
+      const uint16_t* pi = (const uint16_t*)a.in0 + (size_t)ri * a.ld0 + 8 * h;
+      const uint16_t* pj = (const uint16_t*)a.in0 + (size_t)rj * a.ld0 + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[s] = add_bf8(ld_bf8(pi + 16 * s), ld_bf8(pj + 16 * s));
+    }
+  }
+};
+
+// ----------------------------------------------------------------- one layer
+template <int KS, int MT>
+__device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc)[MT],
+                                           const char* w, int lane) {
+  const int h = lane >> 5;
+  const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = *(const f32x4*)(bias + 32 * m + 8 * g + 4 * h);
+      acc[m][4 * g + 0] = bv.x;
+      acc[m][4 * g + 1] = bv.y;
+      acc[m][4 * g + 2] = bv.z;
+      acc[m][4 * g + 3] = bv.w;
+    }
+  }
+  // software pipeline: the A fragments of k-step s+1 are read from LDS while the
+  // MFMAs of step s issue; a scheduling fence per step keeps the compiler from
+  // hoisting every fragment of the layer (register blow-up)
+  const char* wl = w + lane * 16;
+  bf16x8_t acur[MT], anxt[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS) * 1024));
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + s + 1) * 1024));
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
+    }
+  }
+}
+
+__device__ __forceinline__ int ffeat(int m, int q, int h) {
+  return 32 * m + 8 * (q >> 2) + 4 * h + (q & 3);
+}
+
+template <int MT>
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int h) {
+  const int out = L.out;
+  const bool full = out == 32 * MT;
+  if (L.mu) {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += acc[m][q];
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s / (float)out;
+    float ss = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float d = acc[m][q] - mean;
+        ss += (full || ffeat(m, q, h) < out) ? d * d : 0.f;
+      }
+    ss += __shfl_xor(ss, 32, 64);
+    const float inv = 1.f / (__fsqrt_rn(ss / (float)(out - 1)) + NORM_EPS);
+    const float gs = *L.sd * inv, gb = *L.mu;
+    // y = s * (x - mean) / (std + eps) + m
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
+  }
+  const int act = L.act;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float v = apply_act(acc[m][q], act);
+      if (!full && ffeat(m, q, h) >= out) v = 0.f;
+      acc[m][q] = v;
+    }
+}
+
+template <int MT>
+__device__ __forceinline__ void pack_next(const f32x16 (&acc)[MT], bf16x8_t (&nb)[2 * MT]) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int q = 8 * hf;
+      nb[2 * m + hf] = __builtin_bit_cast(
+          bf16x8_t, (u32x4){bf2(acc[m][q + 0], acc[m][q + 1]), bf2(acc[m][q + 2], acc[m][q + 3]),
+                            bf2(acc[m][q + 4], acc[m][q + 5]), bf2(acc[m][q + 6], acc[m][q + 7])});
+    }
+}
+
+template <int MT>
+__device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& a, long row,
+                                          int h) {
+  const int out = a.out_real;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * m + 8 * g + 4 * h;
+      if (f0 >= out) continue;
+      float v[4] = {acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+      if (f0 + 4 <= out) {
+        if (a.res) {
+          if (a.res_f32) {
+            const f32x4 r = *(const f32x4*)((const float*)a.res + (size_t)row * a.ld_res + f0);
+            v[0] = __fadd_rn(r.x, v[0]); v[1] = __fadd_rn(r.y, v[1]);
+            v[2] = __fadd_rn(r.z, v[2]); v[3] = __fadd_rn(r.w, v[3]);
+          } else {
+            const uint2 r = *(const uint2*)((const uint16_t*)a.res + (size_t)row * a.ld_res + f0);
+            v[0] = __fadd_rn(__uint_as_float(r.x << 16), v[0]);
+            v[1] = __fadd_rn(__uint_as_float(r.x & 0xffff0000u), v[1]);
+            v[2] = __fadd_rn(__uint_as_float(r.y << 16), v[2]);
+            v[3] = __fadd_rn(__uint_as_float(r.y & 0xffff0000u), v[3]);
+          }
+        }
+        if (a.out_f32) {
+          *(f32x4*)((float*)a.out + (size_t)row * a.ld_out + f0) = (f32x4){v[0], v[1], v[2], v[3]};
+        } else {
+          uint2 w;
+          w.x = bf2(v[0], v[1]);
+          w.y = bf2(v[2], v[3]);
+          *(uint2*)((uint16_t*)a.out + (size_t)row * a.ld_out + f0) = w;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int f = f0 + e;
+          if (f < out) {
+            float x = v[e];
+            if (a.res)
+              x = __fadd_rn(a.res_f32 ? ((const float*)a.res)[(size_t)row * a.ld_res + f]
+                                      : bf16_to_f32(((const uint16_t*)a.res)[(size_t)row * a.ld_res + f]),
+                            x);
+            if (a.out_f32) ((float*)a.out)[(size_t)row * a.ld_out + f] = x;
+            else ((uint16_t*)a.out)[(size_t)row * a.ld_out + f] = f32_to_bf16(x);
+          }
+        }
+      }
+    }
+}
+
+template <int LI, int K, int N, int... Rest>
+__device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K + 15) / 16],
+                                          const char* lds, long row, bool valid, int lane) {
+  constexpr int KS = (K + 15) / 16;
+  constexpr int MT = N / 32;
+  static_assert(N % 32 == 0, "padded widths are multiples of 32");
+  f32x16 acc[MT];
+  mfma_layer<KS, MT>(b, acc, lds + a.L[LI].woff, lane);
+  epilogue<MT>(acc, a.L[LI], lane >> 5);
+  if constexpr (sizeof...(Rest) > 0) {
+    bf16x8_t nb[2 * MT];
+    pack_next<MT>(acc, nb);
+    run_chain<LI + 1, N, Rest...>(a, nb, lds, row, valid, lane);
+  } else {
+    if (valid) store_out<MT>(acc, a, row, lane >> 5);
+  }
+}
+
+template <int MODE, bool IN_F32, int W0, int W1, int... Ns>
+__global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  using In = Input<MODE, IN_F32, W0, W1>;
+  // stage all layers' packed weights + biases (static layer indices: no scratch copy)
+#pragma unroll
+  for (int l = 0; l < RG_MAX_LAYERS; ++l) {
+    if (l < a.nl) {
+      const u32x4* src = (const u32x4*)a.L[l].src;
+      u32x4* dst = (u32x4*)(lds + a.L[l].woff);
+      const int n = a.L[l].bytes / 16;
+      for (int i = threadIdx.x; i < n; i += FT) dst[i] = src[i];
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
+  const long ntiles = (rows + 31) / 32;
+  for (long tile = (long)blockIdx.x * FW + wave; tile < ntiles; tile += (long)gridDim.x * FW) {
+    const long row = tile * 32 + (lane & 31);
+    const bool valid = row < rows;
+    bf16x8_t b[In::KS];
+    In::load(a, row, valid, lane >> 5, b);
+    run_chain<0, In::K0, Ns...>(a, b, lds, row, valid, lane);
+  }
+}
+
+template <int MODE, bool IN_F32, int W0, int W1, int... Ns>
+static int launch(const FArgs& a, hipStream_t st) {
+  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, Ns...>;
+  static bool attr = false;
+  if (!attr) {
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    attr = true;
+  }
+  const long tiles = (a.rows + 31) / 32;
+  long blocks = (tiles + FW - 1) / FW;
+  const int per_cu = a.total_bytes <= 76 * 1024 ? 2 : 1;
+  if (blocks > 256L * per_cu) blocks = 256L * per_cu;
+  if (blocks < 1) blocks = 1;
+  kern<<<blocks, FT, a.total_bytes, st>>>(a);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// shape key: mode, f32 input, widths, padded outputs
+struct Key {
+  int mode, in_f32, w0, w1, nl;
+  int n[RG_MAX_LAYERS];
+};
+
+static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
+                  std::initializer_list<int> ns) {
+  if (k.mode != mode || k.in_f32 != in_f32 || k.w0 != w0 || k.w1 != w1 ||
+      k.nl != (int)ns.size())
+    return false;
+  int i = 0;
+  for (int v : ns)
+    if (k.n[i++] != v) return false;
+  return true;
+}
+
+// instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
+static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
+#define RG_FAST(MODE, F32, W0, W1, ...)                                      \
+  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                           \
+    return launch<MODE, F32, W0, W1, __VA_ARGS__>(a, st);
+  // node / edge encoders (graph_feature_encoding, yml:56-57)
+  RG_FAST(RG_IN_DENSE, 1, 6, 0, 256, 128, 64)
+  RG_FAST(RG_IN_DENSE, 1, 7, 0, 256, 128, 128, 64)
+  // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
+  RG_FAST(RG_IN_GATHER3, 0, 64, 64, 128, 64)
+  RG_FAST(RG_IN_CONCAT2, 0, 64, 64, 64)
+  // heads: 3-block stems + FFN_TaskSpecificHead (ffn + Linear -> 7 / 2)
+  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(RG_IN_PAIRADD, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64)
+  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
+  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 32)
+#undef RG_FAST
+  return RG_ERR_UNSUPPORTED;
+}
+
+}  // namespace fast
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::fast;
+
+extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows,
+                                 const int* rows_dev, int in_mode, int in_dtype, const void* in0,
+                                 int ld0, int w0, const void* in1, int ld1, int w1,
+                                 const void* in2, int ld2, int w2, const int* idx0,
+                                 const int* idx1, const void* residual, int ld_res, int res_dtype,
+                                 void* out, int ld_out, int out_dtype, void* stream) {
+  RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_fast: n_layers");
+  Key k;
+  memset(&k, 0, sizeof(k));
+  k.mode = in_mode;
+  k.in_f32 = in_dtype == RG_F32 ? 1 : 0;
+  RG_REQUIRE(in_mode == RG_IN_DENSE || in_dtype == RG_BF16, RG_ERR_UNSUPPORTED,
+             "rg_mlp_chain_fast: gathered / concatenated inputs must be bf16");
+  k.w0 = w0;
+  k.w1 = in_mode == RG_IN_GATHER3 ? w2 : (in_mode == RG_IN_CONCAT2 ? w1 : 0);
+  k.nl = n_layers;
+  FArgs a;
+  memset(&a, 0, sizeof(a));
+  int off = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const rg_layer& s = layers[l];
+    RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_fast: layer %d weights", l);
+    RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
+    k.n[l] = (s.out_dim + 31) / 32 * 32;
+    if (l > 0)
+      RG_REQUIRE(s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG, "rg_mlp_chain_fast: widths");
+    a.L[l].src = s.w_packed;
+    a.L[l].mu = s.norm_mu;
+    a.L[l].sd = s.norm_std;
+    a.L[l].woff = off;
+    a.L[l].bytes = (int)rg_packed_linear_bytes(s.in_dim, s.out_dim,
+                                               l == 0 ? RG_PACK_FAST_IN : RG_PACK_FAST_CHAIN);
+    a.L[l].out = s.out_dim;
+    a.L[l].act = s.act;
+    off += (a.L[l].bytes + 15) & ~15;
+    // chained layers: the previous padded width is the next K (zero columns beyond out)
+    if (l > 0 && layers[l - 1].out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
+  }
+  if (off > 160 * 1024) return RG_ERR_UNSUPPORTED;
+  a.nl = n_layers;
+  a.total_bytes = off;
+  a.rows = rows;
+  a.rows_dev = rows_dev;
+  a.in0 = in0; a.in1 = in1; a.in2 = in2;
+  a.ld0 = ld0; a.ld1 = ld1; a.ld2 = ld2;
+  a.in_f32 = k.in_f32;
+  a.w0real = w0;
+  a.idx0 = idx0; a.idx1 = idx1;
+  a.res = residual; a.ld_res = ld_res; a.res_f32 = res_dtype == RG_F32;
+  a.out = out; a.ld_out = ld_out; a.out_f32 = out_dtype == RG_F32;
+  a.out_real = layers[n_layers - 1].out_dim;
+  // vector paths need 16-B (bf16 x8) aligned rows
+  RG_REQUIRE(in_mode == RG_IN_DENSE && k.in_f32 ? true : (ld0 % 8 == 0 && (!in1 || ld1 % 8 == 0) &&
+                                                         (!in2 || ld2 % 8 == 0)),
+             RG_ERR_UNSUPPORTED, "rg_mlp_chain_fast: row strides must be multiples of 8");
+  RG_REQUIRE(ld_out % 4 == 0 && (!residual || ld_res % 4 == 0), RG_ERR_UNSUPPORTED,
+             "rg_mlp_chain_fast: output strides must be multiples of 4");
+  if (in_mode == RG_IN_DENSE && k.in_f32) {
+    if (w0 > 8) return RG_ERR_UNSUPPORTED;
+    k.w0 = w0;
+  }
+  if (rows <= 0) return RG_OK;
+  return dispatch(k, a, (hipStream_t)stream);
+}

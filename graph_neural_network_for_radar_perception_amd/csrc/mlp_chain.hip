@@ -46,12 +46,15 @@ template <> struct Cfg<uint16_t> {
 __host__ __device__ inline int kpad(int k, int p) { return (k + p - 1) / p * p; }
 
 __host__ __device__ inline size_t frag_bytes(int in_dim, int out_dim, int dtype) {
+  if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN)  // 32x32x16 fragments
+    return (size_t)((out_dim + 31) / 32) * ((in_dim + 15) / 16) * 64 * 8 * sizeof(uint16_t);
   const size_t mt = (size_t)(out_dim + 15) / 16;
   if (dtype == RG_F32) return mt * (kpad(in_dim, 16) / 16) * 64 * 4 * sizeof(float);
   return mt * (kpad(in_dim, 32) / 32) * 64 * 8 * sizeof(uint16_t);
 }
 static size_t packed_bytes(int in_dim, int out_dim, int dtype) {
-  return frag_bytes(in_dim, out_dim, dtype) + (size_t)kpad(out_dim, 16) * sizeof(float);
+  const int bpad = (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) ? 32 : 16;
+  return frag_bytes(in_dim, out_dim, dtype) + (size_t)kpad(out_dim, bpad) * sizeof(float);
 }
 
 struct ChainLayer {
@@ -110,6 +113,27 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
   const int m = (int)(ms / S);
   const int o = 16 * m + (lane & 15);
   const int k = 32 * s + 8 * (lane >> 4) + j;
+  P[t] = (o < out && k < in) ? f32_to_bf16(W[(size_t)o * in + k]) : (uint16_t)0;
+}
+
+// 32x32x16 fragments: [m][s][lane][8] = W[32m + (lane&31)][k(s, lane>>5, j)] with
+// FAST_IN   k = 16s + 8h + j                                  (operand loaded from memory)
+// FAST_CHAIN k = 32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3)    (operand = previous layer's
+//            accumulator registers 8(s&1)..8(s&1)+7 of M-tile s>>1, no lane movement)
+__global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int chain,
+                                 uint16_t* __restrict__ P, long total) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int S = (in + 15) / 16;
+  const int j = (int)(t & 7);
+  const int lane = (int)((t >> 3) & 63);
+  const long ms = t >> 9;
+  const int s = (int)(ms % S);
+  const int m = (int)(ms / S);
+  const int h = lane >> 5;
+  const int o = 32 * m + (lane & 31);
+  const int k = chain ? 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+                      : 16 * s + 8 * h + j;
   P[t] = (o < out && k < in) ? f32_to_bf16(W[(size_t)o * in + k]) : (uint16_t)0;
 }
 
@@ -464,10 +488,14 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
                                                            (uint16_t*)packed, total);
+  } else if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) {
+    long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
+    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(
+        weight, in_dim, out_dim, dtype == RG_PACK_FAST_CHAIN ? 1 : 0, (uint16_t*)packed, total);
   } else {
     RG_REQUIRE(false, RG_ERR_ARG, "rg_pack_linear: bad dtype %d", dtype);
   }
-  const int nb = kpad(out_dim, 16);
+  const int nb = kpad(out_dim, (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) ? 32 : 16);
   pack_bias_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(
       bias, out_dim, nb, (float*)((char*)packed + frag_bytes(in_dim, out_dim, dtype)));
   RG_LAUNCH_CHECK();

@@ -110,6 +110,7 @@ class ChainPlan:
         self.device = torch.device(device)
         self.in_dim = specs[0].in_dim
         self.out_dim = specs[-1].out_dim
+        self.use_fast = True   # try rg_mlp_chain_fast first (bf16 only)
         self._pack()
 
     def _signature(self):
@@ -120,27 +121,27 @@ class ChainPlan:
                     sig.append((t.data_ptr(), t._version))
         return tuple(sig)
 
-    def _pack(self):
+    def _pack_buffer(self, fmt_of_layer):
+        """Pack every layer (format fmt_of_layer(i)) into one device buffer; returns
+        (buffer, ctypes descriptor groups)."""
         lib = nat.lib()
-        for s in self.specs:
-            for t in (s.weight, s.bias, s.mu, s.std):
-                if t is not None:
-                    _require_device(t, 'model parameter')
-        sizes = [lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, self.dt) for s in self.specs]
+        fmts = [fmt_of_layer(i) for i in range(len(self.specs))]
+        sizes = [lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, f)
+                 for s, f in zip(self.specs, fmts)]
         offs, tot = [], 0
         for sz in sizes:
             offs.append(tot)
             tot += (sz + 255) // 256 * 256
-        self.buf = torch.empty(tot, dtype=torch.uint8, device=self.device)
+        buf = torch.empty(tot, dtype=torch.uint8, device=self.device)
         st = nat.stream_ptr(self.device)
-        base = self.buf.data_ptr()
-        for s, off in zip(self.specs, offs):
+        base = buf.data_ptr()
+        for s, off, f in zip(self.specs, offs, fmts):
             w = s.weight.detach().to(torch.float32).contiguous()
             b = None if s.bias is None else s.bias.detach().to(torch.float32).contiguous()
-            nat.check(lib.rg_pack_linear(w.data_ptr(), nat.ptr(b), s.in_dim, s.out_dim, self.dt,
+            nat.check(lib.rg_pack_linear(w.data_ptr(), nat.ptr(b), s.in_dim, s.out_dim, f,
                                          base + off, st), 'rg_pack_linear')
         # groups of <= MAX_LAYERS layers (a longer chain runs as several launches)
-        self.groups = []
+        groups = []
         for g0 in range(0, len(self.specs), nat.MAX_LAYERS):
             grp = list(range(g0, min(g0 + nat.MAX_LAYERS, len(self.specs))))
             arr = (nat.rg_layer * len(grp))()
@@ -152,7 +153,22 @@ class ChainPlan:
                 arr[i].in_dim = s.in_dim
                 arr[i].out_dim = s.out_dim
                 arr[i].act = nat.ACT[s.act]
-            self.groups.append((arr, len(grp), self.specs[grp[-1]].out_dim))
+            groups.append((arr, len(grp), self.specs[grp[-1]].out_dim))
+        return buf, groups
+
+    def _pack(self):
+        for s in self.specs:
+            for t in (s.weight, s.bias, s.mu, s.std):
+                if t is not None:
+                    _require_device(t, 'model parameter')
+        self.buf, self.groups = self._pack_buffer(lambda i: self.dt)
+        # bf16: also the register-resident 32x32x16 formats of rg_mlp_chain_fast
+        self.fast = None
+        if self.dt == nat.RG_BF16 and len(self.specs) <= nat.MAX_LAYERS:
+            self.fast_buf, fg = self._pack_buffer(
+                lambda i: nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN)
+            self.fast = fg[0][0]
+        self.fast_ok = {}   # in_mode -> bool (shape has a compiled fast kernel)
         self.sig = self._signature()
 
     def refresh(self):
@@ -164,6 +180,22 @@ class ChainPlan:
                  idx0=None, idx1=None, residual=None, rows_dev=None):
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
+        if self.use_fast and self.fast is not None and self.fast_ok.get(mode, True):
+            rc = lib.rg_mlp_chain_fast(
+                self.fast, len(self.specs), int(rows), nat.ptr(rows_dev), mode, _dt_code(in0),
+                in0.data_ptr(), in0.stride(0), w0,
+                nat.ptr(in1), in1.stride(0) if in1 is not None else 0, w1,
+                nat.ptr(in2), in2.stride(0) if in2 is not None else 0, w2,
+                nat.ptr(idx0), nat.ptr(idx1),
+                nat.ptr(residual), residual.stride(0) if residual is not None else 0,
+                _dt_code(residual) if residual is not None else 0,
+                out.data_ptr(), out.stride(0), _dt_code(out), st)
+            if rc == 0:
+                self.fast_ok[mode] = True
+                return out
+            if rc != nat.RG_ERR_UNSUPPORTED:
+                nat.check(rc, 'rg_mlp_chain_fast')
+            self.fast_ok[mode] = False
         cur_in, cur_w, cur_mode = in0, w0, mode
         for gi, (arr, n, gout) in enumerate(self.groups):
             last = gi == len(self.groups) - 1

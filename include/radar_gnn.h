@@ -42,6 +42,10 @@ extern "C" {
 /* element types */
 #define RG_F32 0
 #define RG_BF16 1
+/* packed-weight formats of rg_pack_linear: RG_F32 / RG_BF16 for rg_mlp_chain, and
+ * the two 32x32x16 bf16 formats of rg_mlp_chain_fast (first layer / chained layers) */
+#define RG_PACK_FAST_IN 2
+#define RG_PACK_FAST_CHAIN 3
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -191,6 +195,17 @@ int rg_mlp_chain(int dtype, const rg_layer* layers_host, int n_layers, long rows
                  int w0, const void* in1, int ld1, int w1, const void* in2, int ld2, int w2,
                  const int* idx0, const int* idx1, const void* residual, int ld_res,
                  int res_dtype, void* out, int ld_out, int out_dtype, void* stream);
+
+/* Register-resident bf16 chain (same semantics as rg_mlp_chain with dtype RG_BF16)
+ * for the widths of the shipped architecture: layer 0 packed as RG_PACK_FAST_IN,
+ * later layers as RG_PACK_FAST_CHAIN.  Returns RG_ERR_UNSUPPORTED (and launches
+ * nothing) when the shape has no compiled instantiation; the caller then uses
+ * rg_mlp_chain. */
+int rg_mlp_chain_fast(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
+                      int in_mode, int in_dtype, const void* in0, int ld0, int w0,
+                      const void* in1, int ld1, int w1, const void* in2, int ld2, int w2,
+                      const int* idx0, const int* idx1, const void* residual, int ld_res,
+                      int res_dtype, void* out, int ld_out, int out_dtype, void* stream);
 
 /* ----------------------------------------------------- segment reductions */
 

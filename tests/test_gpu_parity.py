@@ -387,3 +387,77 @@ def test_large_batch_graph_properties(cuda_device):
         np.testing.assert_array_equal(np.stack((rows[m], col[m])) - 3000 * f, want['adj_list'])
         np.testing.assert_array_equal(gb.ball_degree[3000 * f:3000 * (f + 1)].cpu().numpy(),
                                       want['degree'])
+
+
+def test_fast_chains_match_generic_and_fp32(cuda_device):
+    """rg_mlp_chain_fast (register-resident, 32x32x16 MFMA) is used for every chain of
+    the yml architecture in bf16 and agrees with the generic bf16 kernel and with a
+    torch fp32 evaluation of the same weights."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    from graph_neural_network_for_radar_perception_amd import engine
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    dev = cuda_device
+    torch.manual_seed(5)
+    cfg = default_config()
+    m = Model_Training(cfg, dev).to(dev).eval().requires_grad_(False)
+    plans = m.pred.plans('bf16')
+    g = torch.Generator(device='cpu').manual_seed(0)
+    R = 2000
+
+    def rnd(*shape, dtype=torch.bfloat16):
+        return (torch.randn(*shape, generator=g) * 2).to(dtype).to(dev)
+
+    def torch_chain(plan, x):
+        h = x.float()
+        for s in plan.specs:
+            h = torch.nn.functional.linear(h, s.weight.float(), s.bias.float())
+            if s.mu is not None:
+                h = (h - h.mean(1, keepdim=True)) / (h.std(1, keepdim=True) + 1e-5) * s.std + s.mu
+            if s.act == 'leakyrelu':
+                h = torch.nn.functional.leaky_relu(h, 0.01)
+        return h
+
+    idx0 = torch.randint(0, R, (R,), generator=g).to(torch.int32).to(dev)
+    idx1 = torch.randint(0, R, (R,), generator=g).to(torch.int32).to(dev)
+    x64 = rnd(R, 64)
+    cases = [
+        (plans.node_enc, dict(in0=rnd(R, 6, dtype=torch.float32), w0=6),
+         lambda: rnd(R, 6, dtype=torch.float32)),
+        (plans.edge_enc, dict(in0=rnd(R, 7, dtype=torch.float32), w0=7), None),
+        (plans.convs[0].msg, dict(in0=x64, w0=64, mode=nat.IN_GATHER3, in2=rnd(R, 64), w2=64,
+                                  idx0=idx0, idx1=idx1), None),
+        (plans.convs[0].upd, dict(in0=x64, w0=64, mode=nat.IN_CONCAT2, in1=rnd(R, 64), w1=64,
+                                  residual=x64), None),
+        (plans.node_head, dict(in0=x64, w0=64), None),
+        (plans.offset_head, dict(in0=x64, w0=64), None),
+        (plans.link_pair, dict(in0=x64, w0=64, mode=nat.IN_PAIRADD, idx0=idx0, idx1=idx1), None),
+        (plans.cls_stem, dict(in0=x64, w0=64), None),
+        (plans.cls_head, dict(in0=x64, w0=64), None),
+    ]
+    for plan, kw, _ in cases:
+        outs = []
+        for use_fast in (True, False):
+            plan.use_fast = use_fast
+            plan.fast_ok = {}
+            out = torch.empty(R, plan.out_dim, device=dev)
+            plan(R, out, **kw)
+            outs.append(out)
+            if use_fast:
+                assert plan.fast_ok.get(kw.get('mode', nat.IN_DENSE)), 'fast kernel not used'
+        plan.use_fast = True
+        mode = kw.get('mode', nat.IN_DENSE)
+        if mode == nat.IN_GATHER3:
+            xin = torch.cat([kw['in0'][idx0.long()], kw['in0'][idx1.long()], kw['in2']], 1)
+        elif mode == nat.IN_CONCAT2:
+            xin = torch.cat([kw['in0'], kw['in1']], 1)
+        elif mode == nat.IN_PAIRADD:
+            xin = kw['in0'][idx0.long()].float() + kw['in0'][idx1.long()].float()
+        else:
+            xin = kw['in0']
+        ref = torch_chain(plan, xin)
+        if kw.get('residual') is not None:
+            ref = ref + kw['residual'].float()
+        torch.testing.assert_close(outs[0], outs[1], rtol=0.05, atol=0.05)
+        err = (outs[0] - ref).abs()
+        assert float((err <= 0.05 + 0.05 * ref.abs()).float().mean()) >= 0.995
