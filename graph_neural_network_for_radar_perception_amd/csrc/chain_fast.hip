@@ -59,6 +59,7 @@ struct FArgs {
   int ld_res, res_f32;
   void* out;
   int ld_out, out_f32, out_real;
+  int out_vec;  // row stride allows 4-wide vector stores
 };
 
 __device__ __forceinline__ uint32_t bf2(float a, float b) { return pack_bf16x2(a, b); }
@@ -257,7 +258,7 @@ __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& 
       const int f0 = 32 * m + 8 * g + 4 * h;
       if (f0 >= out) continue;
       float v[4] = {acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
-      if (f0 + 4 <= out) {
+      if (f0 + 4 <= out && a.out_vec) {
         if (a.res) {
           if (a.res_f32) {
             const f32x4 r = *(const f32x4*)((const float*)a.res + (size_t)row * a.ld_res + f0);
@@ -460,8 +461,7 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
   RG_REQUIRE(in_mode == RG_IN_DENSE && k.in_f32 ? true : (ld0 % 8 == 0 && (!in1 || ld1 % 8 == 0) &&
                                                          (!in2 || ld2 % 8 == 0)),
              RG_ERR_UNSUPPORTED, "rg_mlp_chain_fast: row strides must be multiples of 8");
-  RG_REQUIRE(ld_out % 4 == 0 && (!residual || ld_res % 4 == 0), RG_ERR_UNSUPPORTED,
-             "rg_mlp_chain_fast: output strides must be multiples of 4");
+  a.out_vec = (ld_out % 4 == 0) && (!residual || ld_res % 4 == 0);
   if (in_mode == RG_IN_DENSE && k.in_f32) {
     if (w0 > 8) return RG_ERR_UNSUPPORTED;
     k.w0 = w0;

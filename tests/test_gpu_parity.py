@@ -4,7 +4,9 @@ Tolerances (north_star: fp32 outputs within 1e-4 of the reference CPU path,
 edge_index bit-exact):
   * edge_index, ball degree, CSR, link pairs          : bit-exact
   * edge features                                      : bit-exact (same fp32 ops, no FMA)
-  * node features                                      : <= 2 ulp (atan2 is libm-dependent)
+  * node features                                      : bit-exact except azimuth_conf, which
+                                                         depends on numpy's float32 arctan2
+                                                         (SIMD/libm-specific): <= 4e-7 abs
   * fp32 forward outputs                               : |d| <= 1e-4 + 1e-4 |ref|
   * bf16 forward outputs (BASELINE config 2 dtype)     : every |d| <= 0.5 + 0.1 |ref|, 99.9 % of
                                                          elements |d| <= 0.1 + 0.05 |ref|, >= 97 %
@@ -26,6 +28,18 @@ GRID_MAX_R = float(np.sqrt(np.float64(100 ** 2 + 50 ** 2)))
 
 def _frame(d):
     return {k: d[k] for k in FRAME_KEYS}
+
+
+def _node_features_close(got, want):
+    """Columns 0-4 (vr, rcs, t_norm, degree/10, range_conf) bit-exact.  Column 5
+    (azimuth_conf) goes through numpy's float32 arctan2, which is libm/SIMD
+    dependent (SVML on AVX-512 hosts: up to 3 ulp off the correctly rounded value
+    the kernel produces), so it is checked to 4 ulp of the angle: 4e-7 absolute."""
+    got = np.asarray(got, np.float32)
+    want = np.asarray(want, np.float32)
+    np.testing.assert_array_equal(got[:, :5], want[:, :5])
+    np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=4e-7)
+    return True
 
 
 def _ulp_close(a, b, ulps=2):
@@ -53,7 +67,7 @@ def test_graph_build_bit_exact(cuda_device, name):
     ef = gf.compute_edge_features(fr, adj['adj_list'])
     np.testing.assert_array_equal(ef, d['edge_features'])
     nf = gf.compute_node_features(fr, adj['degree'], True, 0, GRID_MAX_R, 0, np.pi * 0.5)
-    assert _ulp_close(nf, d['node_features']), np.abs(nf - d['node_features']).max()
+    assert _node_features_close(nf, d['node_features'])
 
 
 def test_radius_graph_bit_exact(cuda_device):
@@ -124,7 +138,7 @@ def test_batched_graph_build_equals_per_frame(cuda_device):
         want = gref.build_frame_graph(fr, 25.0, 10, GRID_MAX_R)
         m = (ei[0] >= base) & (ei[0] < base + s)
         np.testing.assert_array_equal(ei[:, m] - base, want['edge_index'])
-        assert _ulp_close(nf[base:base + s], want['node_features'])
+        assert _node_features_close(nf[base:base + s], want['node_features'])
         # destination-major edge features: position p of row i = edge (col -> i)
         E = want['edge_index'].shape[1]
         ef = gb.edge_features[E0:E0 + E].cpu().numpy()
