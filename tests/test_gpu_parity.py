@@ -37,7 +37,8 @@ def _node_features_close(got, want):
     the kernel produces), so it is checked to 4 ulp of the angle: 4e-7 absolute."""
     got = np.asarray(got, np.float32)
     want = np.asarray(want, np.float32)
-    np.testing.assert_array_equal(got[:, :5], want[:, :5])
+    bad = np.argwhere(got[:, :5] != want[:, :5])
+    assert len(bad) == 0, [(int(i), int(c), float(got[i, c]), float(want[i, c])) for i, c in bad[:5]]
     np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=4e-7)
     return True
 
