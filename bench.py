@@ -197,34 +197,45 @@ def main():
     for name, ms in durs.items():
         kern[name] = {'avg_ms': round(float(np.mean(ms)), 4), 'launches_per_step':
                       len(ms) // args.steps}
-    # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
-    msg_ms = float(np.mean(durs['message_chain']))
-    msg_flops = 65536.0 * E                              # 2*(192*128+128*64) per edge
-    msg_bytes = E * (3 * C * s + C * s + 8)              # x_i, x_j, e read; msg write; 2 int32 idx
-    msg_tf = msg_flops / (msg_ms * 1e-3) / 1e12
-    msg_gbs = msg_bytes / (msg_ms * 1e-3) / 1e9
-    agg_ms = float(np.mean(durs['segment_reduce']))
-    agg_bytes = E * C * s + N * C * s + (N + 1) * 4     # SURVEY §8(d) B_agg
-    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
+    if 'conv_fused' in durs:
+        # fused conv layer: gather x_i, x_j, e -> msg MLP -> MFMA segment sum -> update MLP
+        ms = float(np.mean(durs['conv_fused']))
+        flops = 65536.0 * E + 16384.0 * N                   # per layer
+        nbytes = E * (C * s + 8) + N * (2 * C * s + 4)     # e rows + (src,dst) once; x in/out once
+        tf = flops / (ms * 1e-3) / 1e12
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        kern['conv_fused'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
+                                  flops_per_launch=flops, bytes_per_launch=nbytes)
+        kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
+    else:
+        # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
+        ms = float(np.mean(durs['message_chain']))
+        flops = 65536.0 * E                              # 2*(192*128+128*64) per edge
+        nbytes = E * (3 * C * s + C * s + 8)             # x_i, x_j, e read; msg write; 2 int32 idx
+        tf = flops / (ms * 1e-3) / 1e12
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        kern['message_chain'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
+                                     flops_per_launch=flops, bytes_per_launch=nbytes)
+        kname = 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)'
+        agg_ms = float(np.mean(durs['segment_reduce']))
+        agg_bytes = E * C * s + N * C * s + (N + 1) * 4     # SURVEY §8(d) B_agg
+        agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+        kern['segment_reduce'].update(algorithmic_gbs=round(agg_gbs, 1), bytes_per_launch=agg_bytes,
+                                      hbm_frac=round(agg_gbs / HBM_PEAK_GBS, 4))
     enc_ms = float(np.mean(durs['edge_encoder']))
     enc_flops = 118272.0 * E
-    kern['message_chain'].update(algorithmic_tflops=round(msg_tf, 2),
-                                 algorithmic_gbs=round(msg_gbs, 1),
-                                 flops_per_launch=msg_flops, bytes_per_launch=msg_bytes)
-    kern['segment_reduce'].update(algorithmic_gbs=round(agg_gbs, 1), bytes_per_launch=agg_bytes,
-                                  hbm_frac=round(agg_gbs / HBM_PEAK_GBS, 4))
     kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2))
-    frac_mfma = msg_tf / MFMA_PEAK_TFLOPS[args.dtype]
-    frac_hbm = msg_gbs / HBM_PEAK_GBS
+    frac_mfma = tf / peak_tf
+    frac_hbm = gbs / HBM_PEAK_GBS
     if frac_mfma >= frac_hbm:
-        roof = {'kernel': 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)',
-                'bound': 'mfma', 'achieved': round(msg_tf, 2),
-                'peak': MFMA_PEAK_TFLOPS[args.dtype], 'unit': 'TFLOP/s',
-                'frac': round(frac_mfma, 4), 'traffic': None}
+        roof = {'kernel': kname, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak_tf,
+                'unit': 'TFLOP/s', 'frac': round(frac_mfma, 4), 'traffic': None,
+                'hbm_frac': round(frac_hbm, 4)}
     else:
-        roof = {'kernel': 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)',
-                'bound': 'hbm', 'achieved': round(msg_gbs, 1), 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': None}
+        roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': None,
+                'mfma_frac': round(frac_mfma, 4)}
     line = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),

@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(PKG, 'lib', 'libradargnn.so')
 HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 
 RG_F32, RG_BF16 = 0, 1
-RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN = 2, 3
+RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD = 2, 3, 4
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
 GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2
@@ -70,6 +70,9 @@ _SIGNATURES = {
                           _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
     'rg_mlp_chain_fast': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,
                                _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
+    'rg_conv_layer_workspace_size': (_S, []),
+    'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,
+                                 _P, _I, _P, _P, _P, _I, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
 }
 

@@ -1,0 +1,359 @@
+// Fused residual_graph_conv_block (gnn_blocks.py:96-113) for the shipped widths
+// (C = 64 node / edge channels, msg MLP 192 -> 128 -> 64, update 128 -> 64, aggr add
+// or mean), bf16 operands, f32 accumulation.  One launch per layer replaces
+// message chain + scatter-aggregate + update chain; messages and aggregates never
+// touch HBM.
+//
+// Work unit = a block of 16 destination nodes and all their incoming edges (the
+// destination-major CSR makes them one contiguous edge range).  A wave
+//   1. streams the block's edges in tiles of 32: loads cat(x[dst], x[src], e) of
+//      each edge straight into MFMA B fragments, runs the message MLP
+//      (32x32x16 MFMAs, channel_normalization + LeakyReLU in-lane, layer chained
+//      in registers) -> message tile M [64 features x 32 edges], lane = edge;
+//   2. transposes M through a wave-private LDS tile and accumulates
+//      Agg[64 x 16 nodes] += M . S with S the one-hot (edge -> destination slot)
+//      matrix: the segmented scatter-add as 4 MFMAs per tile, summed in edge order
+//      with f32 accumulation (sources ascending within a destination = the
+//      reference scatter_add_ order; bf16-rounded messages as in the unfused path);
+//   3. after the block's last tile: Agg (lane = node) is already the B operand of
+//      the update MLP (k-steps 4..7); x[node] provides k-steps 0..3; update +
+//      norm + act + residual, store x_new[node].
+// Workgroups (8 waves, 2 per SIMD) are persistent and pull node blocks from an
+// atomic counter; all weights (81 KiB packed bf16 + biases) sit in LDS.
+#include "rg_common.h"
+
+namespace rg {
+namespace conv {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+static constexpr int CT = 512;
+static constexpr int CW = CT / 64;
+static constexpr int NB = 16;        // destination nodes per work block
+static constexpr int C = 64;         // node / edge / message / output channels
+static constexpr int HID = 128;      // msg_mlp_hidden_dim
+static constexpr int TSTRIDE = 40;   // bf16 per row of the transpose tile (80 B: conflict-free b128)
+static constexpr float NORM_EPS = 1e-5f;
+
+struct CLayer {
+  int woff, bytes, out, act;
+  const float* mu;
+  const float* sd;
+  const void* src;
+};
+
+struct CArgs {
+  CLayer L[3];  // msg0 (192->128), msg1 (128->64), upd (128->64)
+  int total_bytes;
+  int aggr_mean;
+  int n_nodes;
+  int n_blocks;
+  const uint16_t* x;
+  const uint16_t* e;
+  const int* seg_ptr;
+  const int* src;
+  const int* dst;
+  uint16_t* x_out;
+  int* counter;
+  int ldx, lde, ldo;
+};
+
+__device__ __forceinline__ uint32_t bf2(float a, float b) { return pack_bf16x2(a, b); }
+__device__ __forceinline__ bf16x8_t ld_bf8(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *(const u32x4*)p);
+}
+__device__ __forceinline__ bf16x8_t zero_bf8() {
+  return __builtin_bit_cast(bf16x8_t, (u32x4){0u, 0u, 0u, 0u});
+}
+
+template <int KS, int MT>
+__device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc)[MT],
+                                           const char* w, int lane) {
+  const int h = lane >> 5;
+  const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = *(const f32x4*)(bias + 32 * m + 8 * g + 4 * h);
+      acc[m][4 * g + 0] = bv.x;
+      acc[m][4 * g + 1] = bv.y;
+      acc[m][4 * g + 2] = bv.z;
+      acc[m][4 * g + 3] = bv.w;
+    }
+  const char* wl = w + lane * 16;
+  bf16x8_t acur[MT], anxt[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS) * 1024));
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + s + 1) * 1024));
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
+    }
+  }
+}
+
+// channel_normalization (common.py:208-220) + activation on full-width rows
+template <int MT>
+__device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
+  constexpr int OUT = 32 * MT;
+  if (L.mu) {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += acc[m][q];
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.f / OUT);
+    float ss = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float d = acc[m][q] - mean;
+        ss += d * d;
+      }
+    ss += __shfl_xor(ss, 32, 64);
+    const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (OUT - 1))) + NORM_EPS);
+    const float gs = *L.sd * inv, gb = *L.mu;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
+  }
+  const int act = L.act;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[m][q] = apply_act(acc[m][q], act);
+}
+
+template <int MT>
+__device__ __forceinline__ void pack_acc(const f32x16 (&acc)[MT], bf16x8_t* nb) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int q = 8 * hf;
+      nb[2 * m + hf] = __builtin_bit_cast(
+          bf16x8_t, (u32x4){bf2(acc[m][q + 0], acc[m][q + 1]), bf2(acc[m][q + 2], acc[m][q + 3]),
+                            bf2(acc[m][q + 4], acc[m][q + 5]), bf2(acc[m][q + 6], acc[m][q + 7])});
+    }
+}
+
+__global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  // stage weights (static indices)
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const u32x4* src = (const u32x4*)a.L[l].src;
+    u32x4* dstp = (u32x4*)(lds + a.L[l].woff);
+    const int n = a.L[l].bytes / 16;
+    for (int i = threadIdx.x; i < n; i += CT) dstp[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  // wave-private transpose tile [64 features][32 edges] (+pad) and slot array
+  uint16_t* tile = (uint16_t*)(lds + a.total_bytes + wave * (C * TSTRIDE * 2 + 128));
+  int* slots = (int*)((char*)tile + C * TSTRIDE * 2);
+  const char* w0 = lds + a.L[0].woff;
+  const char* w1 = lds + a.L[1].woff;
+  const char* w2 = lds + a.L[2].woff;
+
+  for (;;) {
+    int blk = 0;
+    if (lane == 0) blk = atomicAdd(a.counter, 1);
+    blk = __shfl(blk, 0, 64);
+    if (blk >= a.n_blocks) break;
+    const int n0 = blk * NB;
+    const int n1 = min(n0 + NB, a.n_nodes);
+    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+    f32x16 agg[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+      const int p = t0 + r;
+      const bool valid = p < e1;
+      // ---- message MLP on cat(x_i, x_j, e) (gnn_blocks.py:112-113)
+      bf16x8_t b[12];
+      int slot = NB;  // invalid edges map to no slot
+      if (valid) {
+        const int di = a.dst[p], sj = a.src[p];
+        slot = di - n0;
+        const uint16_t* pi = a.x + (size_t)di * a.ldx + 8 * h;
+        const uint16_t* pj = a.x + (size_t)sj * a.ldx + 8 * h;
+        const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          b[s] = ld_bf8(pi + 16 * s);
+          b[4 + s] = ld_bf8(pj + 16 * s);
+          b[8 + s] = ld_bf8(pe + 16 * s);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 12; ++s) b[s] = zero_bf8();
+      }
+      f32x16 acc1[4];
+      mfma_layer<12, 4>(b, acc1, w0, lane);
+      norm_act<4>(acc1, a.L[0]);
+      bf16x8_t b2[8];
+      pack_acc<4>(acc1, b2);
+      f32x16 acc2[2];
+      mfma_layer<8, 2>(b2, acc2, w1, lane);
+      norm_act<2>(acc2, a.L[1]);
+      // ---- transpose M (lane = edge) into tile[feature][edge]; invalid edges -> 0
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int f = 32 * m + 8 * (q >> 2) + 4 * h + (q & 3);
+          tile[f * TSTRIDE + r] = valid ? f32_to_bf16(acc2[m][q]) : (uint16_t)0;
+        }
+      if (h == 0) slots[r] = slot;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        // B = S (k = edge 16s + 8h + j, col = slot r): one-hot bf16
+        const int4 sa = *(const int4*)(slots + 16 * s + 8 * h);
+        const int4 sb = *(const int4*)(slots + 16 * s + 8 * h + 4);
+        const uint32_t one = 0x3f80u;
+        u32x4 sv;
+        sv[0] = (sa.x == r ? one : 0u) | ((sa.y == r ? one : 0u) << 16);
+        sv[1] = (sa.z == r ? one : 0u) | ((sa.w == r ? one : 0u) << 16);
+        sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
+        sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
+        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          // A = M[feature 32m + r][edges 16s + 8h .. +8]
+          const bf16x8_t mf = ld_bf8(tile + (32 * m + r) * TSTRIDE + 16 * s + 8 * h);
+          agg[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(mf, sf, agg[m], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
+    const int node = n0 + r;
+    const bool nvalid = node < n1;
+    if (a.aggr_mean) {
+      // PyG mean: sum / max(count, 1)
+      const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
+      const float cnt = (float)(deg > 0 ? deg : 1);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) agg[m][q] = div_rn(agg[m][q], cnt);
+    }
+    bf16x8_t bu[8];
+    const uint16_t* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bu[s] = nvalid ? ld_bf8(px + 16 * s) : zero_bf8();
+    pack_acc<2>(agg, bu + 4);
+    f32x16 accu[2];
+    mfma_layer<8, 2>(bu, accu, w2, lane);
+    norm_act<2>(accu, a.L[2]);
+    if (nvalid) {
+      uint16_t* po = a.x_out + (size_t)node * a.ldo;
+      const uint16_t* pr = a.x + (size_t)node * a.ldx;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int f0 = 32 * m + 8 * g + 4 * h;
+          const uint2 rv = *(const uint2*)(pr + f0);
+          const float v0 = __fadd_rn(__uint_as_float(rv.x << 16), accu[m][4 * g + 0]);
+          const float v1 = __fadd_rn(__uint_as_float(rv.x & 0xffff0000u), accu[m][4 * g + 1]);
+          const float v2 = __fadd_rn(__uint_as_float(rv.y << 16), accu[m][4 * g + 2]);
+          const float v3 = __fadd_rn(__uint_as_float(rv.y & 0xffff0000u), accu[m][4 * g + 3]);
+          uint2 o;
+          o.x = bf2(v0, v1);
+          o.y = bf2(v2, v3);
+          *(uint2*)(po + f0) = o;
+        }
+    }
+  }
+}
+
+}  // namespace conv
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::conv;
+
+extern "C" size_t rg_conv_layer_workspace_size(void) { return 256; }
+
+extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
+                                   const void* x, int ldx, const void* e, int lde,
+                                   const int* seg_ptr, const int* src, const int* dst,
+                                   int n_nodes, void* x_out, int ld_out, void* workspace,
+                                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const rg_layer& m0 = msg_layers[0];
+  const rg_layer& m1 = msg_layers[1];
+  const rg_layer& u = *upd_layer;
+  if (!(m0.in_dim == 3 * C && m0.out_dim == HID && m1.in_dim == HID && m1.out_dim == C &&
+        u.in_dim == 2 * C && u.out_dim == C))
+    return RG_ERR_UNSUPPORTED;
+  if (aggr != RG_REDUCE_SUM && aggr != RG_REDUCE_MEAN) return RG_ERR_UNSUPPORTED;
+  if (!m0.norm_mu || !m1.norm_mu || !u.norm_mu) return RG_ERR_UNSUPPORTED;  // norm assumed
+  RG_REQUIRE(ldx % 8 == 0 && lde % 8 == 0 && ld_out % 8 == 0, RG_ERR_UNSUPPORTED,
+             "rg_conv_layer_fused: strides must be multiples of 8");
+  RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_fused: x_out must not alias x");
+  CArgs a;
+  memset(&a, 0, sizeof(a));
+  const rg_layer* ls[3] = {&m0, &m1, &u};
+  const int fmts[3] = {RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD};
+  int off = 0;
+  for (int l = 0; l < 3; ++l) {
+    a.L[l].src = ls[l]->w_packed;
+    a.L[l].mu = ls[l]->norm_mu;
+    a.L[l].sd = ls[l]->norm_std;
+    a.L[l].woff = off;
+    a.L[l].bytes = (int)rg_packed_linear_bytes(ls[l]->in_dim, ls[l]->out_dim, fmts[l]);
+    a.L[l].out = ls[l]->out_dim;
+    a.L[l].act = ls[l]->act;
+    off += (a.L[l].bytes + 15) & ~15;
+  }
+  a.total_bytes = off;
+  a.aggr_mean = aggr == RG_REDUCE_MEAN;
+  a.n_nodes = n_nodes;
+  a.n_blocks = (n_nodes + NB - 1) / NB;
+  a.x = (const uint16_t*)x;
+  a.e = (const uint16_t*)e;
+  a.seg_ptr = seg_ptr;
+  a.src = src;
+  a.dst = dst;
+  a.x_out = (uint16_t*)x_out;
+  a.counter = (int*)workspace;
+  a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
+  if (n_nodes <= 0) return RG_OK;
+  const size_t lds = (size_t)off + (size_t)CW * (C * TSTRIDE * 2 + 128);
+  RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
+  static bool attr = false;
+  if (!attr) {
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)fused_conv_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  RG_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(int), st));
+  int blocks = 256;
+  if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
+  fused_conv_kernel<<<blocks, CT, lds, st>>>(a);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

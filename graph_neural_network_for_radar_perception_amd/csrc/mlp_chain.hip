@@ -46,14 +46,15 @@ template <> struct Cfg<uint16_t> {
 __host__ __device__ inline int kpad(int k, int p) { return (k + p - 1) / p * p; }
 
 __host__ __device__ inline size_t frag_bytes(int in_dim, int out_dim, int dtype) {
-  if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN)  // 32x32x16 fragments
+  if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD)
     return (size_t)((out_dim + 31) / 32) * ((in_dim + 15) / 16) * 64 * 8 * sizeof(uint16_t);
   const size_t mt = (size_t)(out_dim + 15) / 16;
   if (dtype == RG_F32) return mt * (kpad(in_dim, 16) / 16) * 64 * 4 * sizeof(float);
   return mt * (kpad(in_dim, 32) / 32) * 64 * 8 * sizeof(uint16_t);
 }
 static size_t packed_bytes(int in_dim, int out_dim, int dtype) {
-  const int bpad = (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) ? 32 : 16;
+  const int bpad =
+      (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD) ? 32 : 16;
   return frag_bytes(in_dim, out_dim, dtype) + (size_t)kpad(out_dim, bpad) * sizeof(float);
 }
 
@@ -120,7 +121,9 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
 // FAST_IN   k = 16s + 8h + j                                  (operand loaded from memory)
 // FAST_CHAIN k = 32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3)    (operand = previous layer's
 //            accumulator registers 8(s&1)..8(s&1)+7 of M-tile s>>1, no lane movement)
-__global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int chain,
+// FAST_UPD  k-steps s < in/32 as FAST_IN (x[node] from memory), the rest as FAST_CHAIN
+//           offset by in/2 (aggregate from accumulators): the fused conv layer's update
+__global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int mem_steps,
                                  uint16_t* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
@@ -132,8 +135,10 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
   const int m = (int)(ms / S);
   const int h = lane >> 5;
   const int o = 32 * m + (lane & 31);
-  const int k = chain ? 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
-                      : 16 * s + 8 * h + j;
+  const int sc = s - mem_steps;
+  const int k = s < mem_steps
+                    ? 16 * s + 8 * h + j
+                    : 16 * mem_steps + 32 * (sc >> 1) + 16 * (sc & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
   P[t] = (o < out && k < in) ? f32_to_bf16(W[(size_t)o * in + k]) : (uint16_t)0;
 }
 
@@ -488,14 +493,18 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
                                                            (uint16_t*)packed, total);
-  } else if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) {
+  } else if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
-    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(
-        weight, in_dim, out_dim, dtype == RG_PACK_FAST_CHAIN ? 1 : 0, (uint16_t*)packed, total);
+    const int ks = (in_dim + 15) / 16;
+    RG_REQUIRE(dtype != RG_PACK_FAST_UPD || in_dim % 64 == 0, RG_ERR_ARG,
+               "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
+    const int mem_steps = dtype == RG_PACK_FAST_IN ? ks : (dtype == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
+    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
+                                                           (uint16_t*)packed, total);
   } else {
     RG_REQUIRE(false, RG_ERR_ARG, "rg_pack_linear: bad dtype %d", dtype);
   }
-  const int nb = kpad(out_dim, (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN) ? 32 : 16);
+  const int nb = kpad(out_dim, (dtype >= RG_PACK_FAST_IN) ? 32 : 16);
   pack_bias_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(
       bias, out_dim, nb, (float*)((char*)packed + frag_bytes(in_dim, out_dim, dtype)));
   RG_LAUNCH_CHECK();

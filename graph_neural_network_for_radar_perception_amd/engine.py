@@ -98,6 +98,37 @@ def specs_from_modules(mods) -> List[LayerSpec]:
     return out
 
 
+def pack_specs(specs: List[LayerSpec], fmts: List[int], device):
+    """Pack layers (format fmts[i]) into one device buffer; returns (buffer, offsets)."""
+    lib = nat.lib()
+    sizes = [lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, f) for s, f in zip(specs, fmts)]
+    offs, tot = [], 0
+    for sz in sizes:
+        offs.append(tot)
+        tot += (sz + 255) // 256 * 256
+    buf = torch.empty(tot, dtype=torch.uint8, device=device)
+    st = nat.stream_ptr(device)
+    base = buf.data_ptr()
+    for s, off, f in zip(specs, offs, fmts):
+        w = s.weight.detach().to(torch.float32).contiguous()
+        b = None if s.bias is None else s.bias.detach().to(torch.float32).contiguous()
+        nat.check(lib.rg_pack_linear(w.data_ptr(), nat.ptr(b), s.in_dim, s.out_dim, f,
+                                     base + off, st), 'rg_pack_linear')
+    return buf, offs
+
+
+def layer_array(specs: List[LayerSpec], base: int, offs: List[int]):
+    arr = (nat.rg_layer * len(specs))()
+    for i, s in enumerate(specs):
+        arr[i].w_packed = base + offs[i]
+        arr[i].norm_mu = nat.ptr(s.mu.detach()) if s.mu is not None else None
+        arr[i].norm_std = nat.ptr(s.std.detach()) if s.std is not None else None
+        arr[i].in_dim = s.in_dim
+        arr[i].out_dim = s.out_dim
+        arr[i].act = nat.ACT[s.act]
+    return arr
+
+
 class ChainPlan:
     """Packed weights + launch descriptors of one or more rg_mlp_chain calls."""
 
@@ -123,36 +154,13 @@ class ChainPlan:
 
     def _pack_buffer(self, fmt_of_layer):
         """Pack every layer (format fmt_of_layer(i)) into one device buffer; returns
-        (buffer, ctypes descriptor groups)."""
-        lib = nat.lib()
+        (buffer, descriptor groups of <= MAX_LAYERS layers)."""
         fmts = [fmt_of_layer(i) for i in range(len(self.specs))]
-        sizes = [lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, f)
-                 for s, f in zip(self.specs, fmts)]
-        offs, tot = [], 0
-        for sz in sizes:
-            offs.append(tot)
-            tot += (sz + 255) // 256 * 256
-        buf = torch.empty(tot, dtype=torch.uint8, device=self.device)
-        st = nat.stream_ptr(self.device)
-        base = buf.data_ptr()
-        for s, off, f in zip(self.specs, offs, fmts):
-            w = s.weight.detach().to(torch.float32).contiguous()
-            b = None if s.bias is None else s.bias.detach().to(torch.float32).contiguous()
-            nat.check(lib.rg_pack_linear(w.data_ptr(), nat.ptr(b), s.in_dim, s.out_dim, f,
-                                         base + off, st), 'rg_pack_linear')
-        # groups of <= MAX_LAYERS layers (a longer chain runs as several launches)
+        buf, offs = pack_specs(self.specs, fmts, self.device)
         groups = []
         for g0 in range(0, len(self.specs), nat.MAX_LAYERS):
             grp = list(range(g0, min(g0 + nat.MAX_LAYERS, len(self.specs))))
-            arr = (nat.rg_layer * len(grp))()
-            for i, li in enumerate(grp):
-                s = self.specs[li]
-                arr[i].w_packed = base + offs[li]
-                arr[i].norm_mu = nat.ptr(s.mu.detach()) if s.mu is not None else None
-                arr[i].norm_std = nat.ptr(s.std.detach()) if s.std is not None else None
-                arr[i].in_dim = s.in_dim
-                arr[i].out_dim = s.out_dim
-                arr[i].act = nat.ACT[s.act]
+            arr = layer_array([self.specs[i] for i in grp], buf.data_ptr(), [offs[i] for i in grp])
             groups.append((arr, len(grp), self.specs[grp[-1]].out_dim))
         return buf, groups
 
@@ -373,6 +381,8 @@ class ConvPlan:
         self.aggr = blk.aggr
         if self.aggr not in ('add', 'sum', 'mean', 'max'):
             raise NotImplementedError(f'aggregation {self.aggr!r}')
+        self.device = torch.device(device)
+        self.dtype = dtype
         self.msg = ChainPlan(specs_from_modules(list(blk.msg)), dtype, device)
         self.upd = ChainPlan(specs_from_modules(list(blk.upd)), dtype, device)
         self.res = (ChainPlan(specs_from_modules([blk.residual_connection]), dtype, device)
@@ -380,9 +390,60 @@ class ConvPlan:
         self.c_in = self.msg.in_dim  # 2*C + Ce
         self.c_msg = self.msg.out_dim
         self.c_out = self.upd.out_dim
+        self.fused_ok = None
+        self.use_fused = True   # bf16: one rg_conv_layer_fused launch per layer
+        self._pack_fused()
+
+    def _pack_fused(self):
+        """bf16: the fused layer kernel (rg_conv_layer_fused) when the shapes fit."""
+        self.fused = None
+        if self.dtype != 'bf16' or self.res is not None or self.aggr == 'max':
+            return
+        specs = self.msg.specs + self.upd.specs
+        if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
+            return
+        fmts = [nat.RG_PACK_FAST_IN, nat.RG_PACK_FAST_CHAIN, nat.RG_PACK_FAST_UPD]
+        try:
+            self.fused_buf, offs = pack_specs(specs, fmts, self.device)
+        except RuntimeError:
+            return
+        base = self.fused_buf.data_ptr()
+        self.fused_msg = layer_array(specs[:2], base, offs[:2])
+        self.fused_upd = layer_array(specs[2:], base, offs[2:])
+        self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_workspace_size(), dtype=torch.uint8,
+                                    device=self.device)
+        self.fused = True
+        self.fused_sig = self._sig()
+
+    def _sig(self):
+        return tuple(c._signature() for c in self.chains())
 
     def chains(self):
         return [c for c in (self.msg, self.upd, self.res) if c is not None]
+
+    def refresh(self):
+        for c in self.chains():
+            c.refresh()
+        if self.fused and self._sig() != self.fused_sig:
+            self._pack_fused()
+
+    def run_fused(self, x, e, g, x_out) -> bool:
+        """One launch for the whole layer; False when the fused kernel does not
+        cover this shape (the caller runs the unfused chain + reduce path)."""
+        if not self.use_fused or not self.fused or self.fused_ok is False:
+            return False
+        lib = nat.lib()
+        rc = lib.rg_conv_layer_fused(self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr],
+                                     x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
+                                     g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
+                                     g.n_nodes, x_out.data_ptr(), x_out.stride(0),
+                                     self.fused_ws.data_ptr(), nat.stream_ptr(x.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            self.fused_ok = False
+            return False
+        nat.check(rc, 'rg_conv_layer_fused')
+        self.fused_ok = True
+        return True
 
 
 class ModelPlans:
@@ -412,8 +473,12 @@ class ModelPlans:
         return out
 
     def refresh(self):
-        for c in self.chains():
-            c.refresh()
+        for c in (self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
+                  self.cls_head, self.link_node, self.cls_stem):
+            if c is not None:
+                c.refresh()
+        for cv in self.convs:
+            cv.refresh()
 
 
 @dataclass
@@ -467,6 +532,16 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
     mark('edge_encoder:end')
     for li, cv in enumerate(plans.convs):
         C = x.shape[1]
+        xn = alloc(f'x{(li + 1) % 2}' if li + 1 < len(plans.convs) else 'xL', (N, cv.c_out), T)
+        if xn.data_ptr() == x.data_ptr():
+            xn = alloc('xalt', (N, cv.c_out), T)
+        mark('conv_fused:start')
+        fused = cv.run_fused(x, e, g, xn)
+        if fused:
+            mark('conv_fused:end')
+            x = xn
+            continue
+        events and events.pop()
         msg = alloc('msg', (Ecap, cv.c_msg), T)
         mark('message_chain:start')
         cv.msg(Ecap, msg, x, C, mode=nat.IN_GATHER3, in2=e, w2=e.shape[1], idx0=g.dst,
@@ -481,9 +556,6 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             cv.res(N, ident, x, C)
         else:
             ident = x
-        xn = alloc(f'x{(li + 1) % 2}' if li + 1 < len(plans.convs) else 'xL', (N, cv.c_out), T)
-        if xn.data_ptr() == x.data_ptr():
-            xn = alloc('xalt', (N, cv.c_out), T)
         cv.upd(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg, w1=cv.c_msg, residual=ident)
         x = xn
     C = x.shape[1]

@@ -46,6 +46,7 @@ extern "C" {
  * the two 32x32x16 bf16 formats of rg_mlp_chain_fast (first layer / chained layers) */
 #define RG_PACK_FAST_IN 2
 #define RG_PACK_FAST_CHAIN 3
+#define RG_PACK_FAST_UPD 4 /* update layer of rg_conv_layer_fused: cat(x, aggregate) */
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -206,6 +207,21 @@ int rg_mlp_chain_fast(const rg_layer* layers_host, int n_layers, long rows, cons
                       const void* in1, int ld1, int w1, const void* in2, int ld2, int w2,
                       const int* idx0, const int* idx1, const void* residual, int ld_res,
                       int res_dtype, void* out, int ld_out, int out_dtype, void* stream);
+
+/* One fused residual_graph_conv_block (gnn_blocks.py:96-113) for the shipped
+ * widths (node / edge channels 64, msg MLP 192->128->64, update 128->64, all with
+ * channel_normalization), bf16 operands, aggregation add or mean:
+ *   x_out[i] = x[i] + upd(cat(x[i], AGG_{p in seg i} msg(cat(x[i], x[src[p]], e[p]))))
+ * seg_ptr / src / dst: destination-major CSR (dst[p] = segment of p); e rows in
+ * the same order.  msg_layers[0] packed RG_PACK_FAST_IN, msg_layers[1]
+ * RG_PACK_FAST_CHAIN, upd_layer RG_PACK_FAST_UPD.  Returns RG_ERR_UNSUPPORTED for
+ * other shapes / aggregations (use rg_mlp_chain + rg_segment_reduce).
+ * workspace: rg_conv_layer_workspace_size() bytes (work counter, reset per call). */
+size_t rg_conv_layer_workspace_size(void);
+int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
+                        const void* x, int ldx, const void* e, int lde, const int* seg_ptr,
+                        const int* src, const int* dst, int n_nodes, void* x_out, int ld_out,
+                        void* workspace, void* stream);
 
 /* ----------------------------------------------------- segment reductions */
 

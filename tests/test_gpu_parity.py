@@ -476,3 +476,53 @@ def test_fast_chains_match_generic_and_fp32(cuda_device):
         torch.testing.assert_close(outs[0], outs[1], rtol=0.05, atol=0.05)
         err = (outs[0] - ref).abs()
         assert float((err <= 0.05 + 0.05 * ref.abs()).float().mean()) >= 0.995
+
+
+@pytest.mark.parametrize('aggr', ['add', 'mean'])
+def test_fused_conv_layer_matches_unfused(cuda_device, aggr):
+    """rg_conv_layer_fused (message MLP + MFMA segment sum + update in one launch)
+    against the unfused bf16 path (chain + rg_segment_reduce + chain) and the fp32
+    oracle of residual_graph_conv_block on a batched kNN graph."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from graph_neural_network_for_radar_perception_amd import graph_features as gf
+    dev = cuda_device
+    cfg = default_config(graph_convolution_stem_channels=[64], aggregation=aggr,
+                         k_number_nearest_points=32)
+    torch.manual_seed(11)
+    m = Model_Training(cfg, dev).to(dev).eval().requires_grad_(False)
+    plans = m.pred.plans('bf16')
+    cv = plans.convs[0]
+    assert cv.fused
+    frames = [synthetic.make_frame(n, 70 + i) for i, n in enumerate([700, 33, 1500])]
+    batch = gf.FrameBatch.from_frames(frames, device=dev)
+    gb = gf.build_graph_batch(batch, cfg)
+    g = gb.graph
+    N = batch.n_nodes
+    E = int(gb.n_edges_dev.item())
+    gen = torch.Generator(device='cpu').manual_seed(1)
+    x = (torch.randn(N, 64, generator=gen) * 1.5).bfloat16().to(dev)
+    e = (torch.randn(gb.capacity, 64, generator=gen) * 1.5).bfloat16().to(dev)
+    out_f = torch.empty(N, 64, dtype=torch.bfloat16, device=dev)
+    assert cv.run_fused(x, e, g, out_f)
+    # unfused bf16 path
+    msg = torch.empty(gb.capacity, 64, dtype=torch.bfloat16, device=dev)
+    cv.msg(gb.capacity, msg, x, 64, mode=2, in2=e, w2=64, idx0=g.dst, idx1=g.src,
+           rows_dev=gb.n_edges_dev)
+    agg = torch.empty(N, 64, dtype=torch.bfloat16, device=dev)
+    from graph_neural_network_for_radar_perception_amd import engine
+    engine.segment_reduce(msg, g.seg_ptr, N, aggr, agg)
+    out_u = torch.empty(N, 64, dtype=torch.bfloat16, device=dev)
+    cv.upd(N, out_u, x, 64, mode=1, in1=agg, w1=64, residual=x)
+    # fp32 oracle of the block on the same (bf16-valued) inputs
+    sd = {k: v.float().cpu() for k, v in m.state_dict().items()}
+    ei = torch.stack((g.src[:E], g.dst[:E])).long().cpu()
+    with torch.no_grad():
+        ctx = gnn_forward_ref._Ctx(sd, cfg)
+        ref = gnn_forward_ref.conv_block(ctx, 'pass_messages.conv_blk.0', x.float().cpu(),
+                                         e[:E].float().cpu(), ei)
+    of, ou = out_f.float().cpu(), out_u.float().cpu()
+    torch.testing.assert_close(of, ou, rtol=0.03, atol=0.06)
+    err = (of - ref).abs()
+    assert float((err <= 0.05 + 0.03 * ref.abs()).float().mean()) >= 0.995, float(err.max())
