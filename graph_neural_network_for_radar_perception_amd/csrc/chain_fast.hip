@@ -223,15 +223,16 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
   }
-  const int act = L.act;
+  act_dispatch(L.act, [&](auto A) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      float v = apply_act(acc[m][q], act);
-      if (!full && ffeat(m, q, h) >= out) v = 0.f;
-      acc[m][q] = v;
-    }
+      for (int q = 0; q < 16; ++q) {
+        float v = act_t<decltype(A)::value>(acc[m][q]);
+        if (!full && ffeat(m, q, h) >= out) v = 0.f;
+        acc[m][q] = v;
+      }
+  });
 }
 
 template <int MT>

@@ -83,24 +83,14 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
       acc[m][4 * g + 3] = bv.w;
     }
   const char* wl = w + lane * 16;
-  bf16x8_t acur[MT], anxt[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS) * 1024));
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    if (s + 1 < KS) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + s + 1) * 1024));
+    for (int m = 0; m < MT; ++m) {
+      const bf16x8_t av = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + s) * 1024));
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b[s], acc[m], 0, 0, 0);
     }
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < KS) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
-    }
+    if (s & 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -132,11 +122,12 @@ __device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
   }
-  const int act = L.act;
+  act_dispatch(L.act, [&](auto A) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[m][q] = apply_act(acc[m][q], act);
+      for (int q = 0; q < 16; ++q) acc[m][q] = act_t<decltype(A)::value>(acc[m][q]);
+  });
 }
 
 template <int MT>
@@ -183,27 +174,52 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
-    for (int t0 = e0; t0 < e1; t0 += 32) {
+    // software pipeline over the block's edge tiles: while tile t computes, the
+    // gathered rows of tile t+1 (x[dst], x[src], e) and the indices of tile t+2 are
+    // in flight, so neither the dependent index load nor the row gathers stall
+    bf16x8_t bn[12];
+    int slot_n = NB;
+    int di_n = 0, sj_n = 0;  // indices of the next tile to gather
+    auto load_idx = [&](int t0) {
       const int p = t0 + r;
-      const bool valid = p < e1;
-      // ---- message MLP on cat(x_i, x_j, e) (gnn_blocks.py:112-113)
-      bf16x8_t b[12];
-      int slot = NB;  // invalid edges map to no slot
-      if (valid) {
-        const int di = a.dst[p], sj = a.src[p];
-        slot = di - n0;
-        const uint16_t* pi = a.x + (size_t)di * a.ldx + 8 * h;
-        const uint16_t* pj = a.x + (size_t)sj * a.ldx + 8 * h;
+      if (p < e1) {
+        di_n = a.dst[p];
+        sj_n = a.src[p];
+      }
+    };
+    auto load_rows = [&](int t0) {
+      const int p = t0 + r;
+      slot_n = NB;
+      if (p < e1) {
+        slot_n = di_n - n0;
+        const uint16_t* pi = a.x + (size_t)di_n * a.ldx + 8 * h;
+        const uint16_t* pj = a.x + (size_t)sj_n * a.ldx + 8 * h;
         const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          b[s] = ld_bf8(pi + 16 * s);
-          b[4 + s] = ld_bf8(pj + 16 * s);
-          b[8 + s] = ld_bf8(pe + 16 * s);
+          bn[s] = ld_bf8(pi + 16 * s);
+          bn[4 + s] = ld_bf8(pj + 16 * s);
+          bn[8 + s] = ld_bf8(pe + 16 * s);
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < 12; ++s) b[s] = zero_bf8();
+        for (int s = 0; s < 12; ++s) bn[s] = zero_bf8();
+      }
+    };
+    if (e0 < e1) {
+      load_idx(e0);
+      load_rows(e0);
+      if (e0 + 32 < e1) load_idx(e0 + 32);
+    }
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+      const bool valid = t0 + r < e1;
+      bf16x8_t b[12];
+#pragma unroll
+      for (int s = 0; s < 12; ++s) b[s] = bn[s];
+      const int slot = slot_n;
+      if (t0 + 32 < e1) {
+        load_rows(t0 + 32);
+        if (t0 + 64 < e1) load_idx(t0 + 64);
       }
       f32x16 acc1[4];
       mfma_layer<12, 4>(b, acc1, w0, lane);

@@ -344,12 +344,14 @@ __device__ __forceinline__ void epilogue(f32x4 (&acc)[16], const ChainLayer& L, 
         for (int e = 0; e < 4; ++e)
           acc[m][e] = __fadd_rn(__fmul_rn(gs, __fmul_rn(acc[m][e] - mean, inv)), gb);
   }
+  act_dispatch(L.act, [&](auto A) {
 #pragma unroll
-  for (int m = 0; m < 16; ++m)
-    if (m < mt)
+    for (int m = 0; m < 16; ++m)
+      if (m < mt)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc[m][e] = (16 * m + 4 * g + e) < out ? apply_act(acc[m][e], L.act) : 0.f;
+        for (int e = 0; e < 4; ++e)
+          acc[m][e] = (16 * m + 4 * g + e) < out ? act_t<decltype(A)::value>(acc[m][e]) : 0.f;
+  });
 }
 
 // final layer -> HBM (optional residual add, gnn_blocks.py:109)

@@ -6,6 +6,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../include/radar_gnn.h"
 
 namespace rg {
@@ -81,8 +83,26 @@ enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2, ACT_SWISH = 3 };
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == ACT_LEAKY) return v > 0.f ? v : v * 0.01f;   // constants.py:10
   if (act == ACT_RELU) return v > 0.f ? v : 0.f;
-  if (act == ACT_SWISH) return v / (1.f + __expf(-v));
+  if (act == ACT_SWISH) return v / (1.f + expf(-v));
   return v;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float v) {
+  if constexpr (ACT == ACT_LEAKY) return v > 0.f ? v : v * 0.01f;
+  else if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  else if constexpr (ACT == ACT_SWISH) return v / (1.f + expf(-v));
+  else return v;
+}
+
+// activation over a whole register array with ONE wave-uniform branch (a
+// per-element switch inside unrolled loops explodes into thousands of blocks)
+template <typename F>
+__device__ __forceinline__ void act_dispatch(int act, F&& f) {
+  if (act == ACT_LEAKY) f(std::integral_constant<int, ACT_LEAKY>{});
+  else if (act == ACT_RELU) f(std::integral_constant<int, ACT_RELU>{});
+  else if (act == ACT_SWISH) f(std::integral_constant<int, ACT_SWISH>{});
+  else f(std::integral_constant<int, ACT_NONE>{});
 }
 
 }  // namespace rg
