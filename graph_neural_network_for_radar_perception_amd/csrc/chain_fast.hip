@@ -216,12 +216,12 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int
       }
     ss += __shfl_xor(ss, 32, 64);
     const float inv = 1.f / (__fsqrt_rn(ss / (float)(out - 1)) + NORM_EPS);
-    const float gs = *L.sd * inv, gb = *L.mu;
-    // y = s * (x - mean) / (std + eps) + m
+    // y = s * (x - mean) / (std + eps) + m as one fma: x*gs + (m - mean*gs)
+    const float gs = *L.sd * inv, gb = fmaf(-mean, gs, *L.mu);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
+      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], gs, gb);
   }
   act_dispatch(L.act, [&](auto A) {
 #pragma unroll

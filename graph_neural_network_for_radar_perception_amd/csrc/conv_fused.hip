@@ -10,7 +10,8 @@
 //      each edge straight into MFMA B fragments, runs the message MLP
 //      (32x32x16 MFMAs, channel_normalization + LeakyReLU in-lane, layer chained
 //      in registers) -> message tile M [64 features x 32 edges], lane = edge;
-//   2. transposes M through a wave-private LDS tile and accumulates
+//   2. transposes M through a wave-private LDS tile (8-B row stores, hardware
+//      transposed reads ds_read_b64_tr_b16) and accumulates
 //      Agg[64 x 16 nodes] += M . S with S the one-hot (edge -> destination slot)
 //      matrix: the segmented scatter-add as 4 MFMAs per tile, summed in edge order
 //      with f32 accumulation (sources ascending within a destination = the
@@ -33,7 +34,8 @@ static constexpr int CW = CT / 64;
 static constexpr int NB = 16;        // destination nodes per work block
 static constexpr int C = 64;         // node / edge / message / output channels
 static constexpr int HID = 128;      // msg_mlp_hidden_dim
-static constexpr int TSTRIDE = 40;   // bf16 per row of the transpose tile (80 B: conflict-free b128)
+static constexpr int TSTRIDE = 96;   // bf16 per row of the message tile [edge][feature]
+                                     // (192 B: the 4 rows of a transposed read hit disjoint banks)
 static constexpr float NORM_EPS = 1e-5f;
 
 struct CLayer {
@@ -116,11 +118,12 @@ __device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
       }
     ss += __shfl_xor(ss, 32, 64);
     const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (OUT - 1))) + NORM_EPS);
-    const float gs = *L.sd * inv, gb = *L.mu;
+    // s*(x-mean)/(std+eps) + m as ONE fma per element: x*gs + (m - mean*gs)
+    const float gs = *L.sd * inv, gb = fmaf(-mean, gs, *L.mu);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q] - mean, gs, gb);
+      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], gs, gb);
   }
   act_dispatch(L.act, [&](auto A) {
 #pragma unroll
@@ -157,8 +160,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   // wave-private transpose tile [64 features][32 edges] (+pad) and slot array
-  uint16_t* tile = (uint16_t*)(lds + a.total_bytes + wave * (C * TSTRIDE * 2 + 128));
-  int* slots = (int*)((char*)tile + C * TSTRIDE * 2);
+  uint16_t* tile = (uint16_t*)(lds + a.total_bytes + wave * (32 * TSTRIDE * 2 + 128));
+  int* slots = (int*)((char*)tile + 32 * TSTRIDE * 2);
   const char* w0 = lds + a.L[0].woff;
   const char* w1 = lds + a.L[1].woff;
   const char* w2 = lds + a.L[2].woff;
@@ -229,18 +232,25 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       f32x16 acc2[2];
       mfma_layer<8, 2>(b2, acc2, w1, lane);
       norm_act<2>(acc2, a.L[1]);
-      // ---- transpose M (lane = edge) into tile[feature][edge]; invalid edges -> 0
+      // ---- message tile M -> LDS as rows [edge][feature] (8-B stores of 4 features);
+      //      invalid edges -> 0
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int f = 32 * m + 8 * (q >> 2) + 4 * h + (q & 3);
-          tile[f * TSTRIDE + r] = valid ? f32_to_bf16(acc2[m][q]) : (uint16_t)0;
+        for (int g = 0; g < 4; ++g) {
+          uint2 w;
+          w.x = valid ? bf2(acc2[m][4 * g + 0], acc2[m][4 * g + 1]) : 0u;
+          w.y = valid ? bf2(acc2[m][4 * g + 2], acc2[m][4 * g + 3]) : 0u;
+          *(uint2*)(tile + r * TSTRIDE + 32 * m + 8 * g + 4 * h) = w;
         }
       if (h == 0) slots[r] = slot;
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
+      // A = M (features x edges) via ds_read_b64_tr_b16: lane 4q+p of each 16-lane
+      // group G addresses row (edge) row0+q, columns col0+4p..+3; lane i of the group
+      // receives column (feature) col0+i of the 4 rows.
+      const int G = (lane >> 4) & 3, q4 = (lane & 15) >> 2, p4 = lane & 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // B = S (k = edge 16s + 8h + j, col = slot r): one-hot bf16
@@ -253,10 +263,19 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
         sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
         sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
         const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
+        const int row0 = 16 * s + 8 * (G >> 1);
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
-          // A = M[feature 32m + r][edges 16s + 8h .. +8]
-          const bf16x8_t mf = ld_bf8(tile + (32 * m + r) * TSTRIDE + 16 * s + 8 * h);
+          const int col0 = 32 * m + 16 * (G & 1);
+          typedef short v4s __attribute__((ext_vector_type(4)));
+          typedef __attribute__((address_space(3))) v4s lds_v4s;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s*)(tile + (row0 + q4) * TSTRIDE + col0 + 4 * p4));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s*)(tile + (row0 + 4 + q4) * TSTRIDE + col0 + 4 * p4));
+          const bf16x8_t mf = __builtin_bit_cast(
+              bf16x8_t, (short __attribute__((ext_vector_type(8)))){lo[0], lo[1], lo[2], lo[3],
+                                                                  hi[0], hi[1], hi[2], hi[3]});
           agg[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(mf, sf, agg[m], 0, 0, 0);
         }
       }
@@ -358,7 +377,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   a.counter = (int*)workspace;
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
   if (n_nodes <= 0) return RG_OK;
-  const size_t lds = (size_t)off + (size_t)CW * (C * TSTRIDE * 2 + 128);
+  const size_t lds = (size_t)off + (size_t)CW * (32 * TSTRIDE * 2 + 128);
   RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
   static bool attr = false;
   if (!attr) {

@@ -14,6 +14,9 @@
 #include "rg_common.h"
 #include "scan.h"
 
+// exact numpy distances: no FMA contraction anywhere in this file
+#pragma clang fp contract(off)
+
 #include <stdarg.h>
 
 namespace rg {

@@ -8,6 +8,10 @@
 #include "rg_common.h"
 #include "scan.h"
 
+// numpy semantics: every f32/f64 operation rounds on its own -- never contract
+// a*b+c into an FMA in this file (hipcc's default is -ffp-contract=fast)
+#pragma clang fp contract(off)
+
 namespace rg {
 
 // ------------------------------------------------------------------ node features
@@ -46,11 +50,11 @@ __global__ __launch_bounds__(256) void node_features_kernel(
   const long long tmin = smin[0], tmax = smax[0];
   const double span = (double)(tmax - tmin);
   for (int i = b + threadIdx.x; i < e; i += 256) {
-    const double tn = tmax == tmin ? (double)(ts[i] - tmin) : __ddiv_rn((double)(ts[i] - tmin), span);
-    const double dg = __ddiv_rn((double)deg[i], 10.0);
+    const double tn = tmax == tmin ? (double)(ts[i] - tmin) : (double)(ts[i] - tmin) / span;
+    const double dg = (double)deg[i] / 10.0;
     const float x = px[i], y = py[i];
     const float r = sqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
-    const double rc = __ddiv_rn(__dsub_rn((double)r, max_r), __dsub_rn(min_r, max_r));
+    const double rc = ((double)r - max_r) / (min_r - max_r);
     const float th = fabsf((float)atan2((double)y, (double)x));
     const float az = div_rn(__fsub_rn(th, max_az), az_den);
     float* o = out + (size_t)i * 6;

@@ -54,23 +54,22 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);
 }
+// round-to-nearest-even through the hardware converter (v_cvt_pk_bf16_f32 on
+// gfx950; NaN stays NaN)
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  const bf16x2_hw v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // Correctly rounded f32 sqrt / division (numpy semantics).  The hardware f32
 // v_sqrt / v_rcp paths are not correctly rounded; the f64 result rounded once
 // to f32 is (53 >= 2*24 + 2 bits, so the double rounding is exact).
-__device__ __forceinline__ float sqrt_rn(float x) { return (float)__dsqrt_rn((double)x); }
-__device__ __forceinline__ float div_rn(float a, float b) {
-  return (float)__ddiv_rn((double)a, (double)b);
-}
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
+__device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 
 // MFMA operand / accumulator vector types
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -89,7 +88,8 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 
 template <int ACT>
 __device__ __forceinline__ float act_t(float v) {
-  if constexpr (ACT == ACT_LEAKY) return v > 0.f ? v : v * 0.01f;
+  // leaky: max(v, 0.01 v) == (v > 0 ? v : 0.01 v) for every finite v (slope < 1)
+  if constexpr (ACT == ACT_LEAKY) return fmaxf(v, v * 0.01f);
   else if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
   else if constexpr (ACT == ACT_SWISH) return v / (1.f + expf(-v));
   else return v;
