@@ -111,6 +111,25 @@ def event_durations(events):
     return out
 
 
+def pmc_traffic(args, kernel_substr):
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC table
+    (profiles/rNN_pmc_traffic.json, written by scripts/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command), or None when
+    no table was collected for this workload."""
+    import glob
+    want = {'frames': args.frames, 'nodes': args.nodes, 'k': args.k, 'layers': args.layers,
+            'dtype': args.dtype}
+    for path in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')),
+                       reverse=True):
+        doc = json.load(open(path))
+        if doc.get('workload') != want:
+            continue
+        for name, rec in doc['kernels'].items():
+            if kernel_substr in name:
+                return float(rec['traffic_bytes']), os.path.relpath(path, REPO)
+    return None, None
+
+
 def cpu_baseline(args, cfg):
     """The oracle (numpy dense graph build + op-for-op torch fp32 forward, i.e. the
     reference's own CPU algorithm) on a bounded sample of the same workload."""
@@ -208,6 +227,7 @@ def main():
         kern['conv_fused'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
                                   flops_per_launch=flops, bytes_per_launch=nbytes)
         kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
+        traffic, tsrc = pmc_traffic(args, 'fused_conv_kernel')
     else:
         # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
         ms = float(np.mean(durs['message_chain']))
@@ -218,6 +238,7 @@ def main():
         kern['message_chain'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
                                      flops_per_launch=flops, bytes_per_launch=nbytes)
         kname = 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)'
+        traffic, tsrc = None, None
         agg_ms = float(np.mean(durs['segment_reduce']))
         agg_bytes = E * C * s + N * C * s + (N + 1) * 4     # SURVEY §8(d) B_agg
         agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
@@ -230,12 +251,15 @@ def main():
     frac_hbm = gbs / HBM_PEAK_GBS
     if frac_mfma >= frac_hbm:
         roof = {'kernel': kname, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak_tf,
-                'unit': 'TFLOP/s', 'frac': round(frac_mfma, 4), 'traffic': None,
+                'unit': 'TFLOP/s', 'frac': round(frac_mfma, 4), 'traffic': traffic,
                 'hbm_frac': round(frac_hbm, 4)}
     else:
         roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': None,
+                'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': traffic,
                 'mfma_frac': round(frac_mfma, 4)}
+    if traffic is not None:
+        roof.update(traffic_unit='bytes/launch', traffic_source=tsrc,
+                    algorithmic_bytes=nbytes, traffic_over_algorithmic=round(traffic / nbytes, 3))
     line = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),

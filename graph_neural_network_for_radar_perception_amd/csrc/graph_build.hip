@@ -36,9 +36,9 @@ static constexpr int KNN_CHUNK = 2048;  // points per LDS stage (16 KiB)
 // fp32 squared distance exactly as numpy evaluates graph_features.py:72-73:
 // two products and one sum, each rounded, no fused multiply-add.
 __device__ __forceinline__ float sqdist(float xi, float yi, float xj, float yj) {
-  float dx = __fsub_rn(xi, xj);
-  float dy = __fsub_rn(yi, yj);
-  return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+  float dx = (xi - xj);
+  float dy = (yi - yj);
+  return ((dx * dx) + (dy * dy));
 }
 
 // K = list length kept per row (>= k+1).  Ties: a later (larger) j never

@@ -53,10 +53,10 @@ __global__ __launch_bounds__(256) void node_features_kernel(
     const double tn = tmax == tmin ? (double)(ts[i] - tmin) : (double)(ts[i] - tmin) / span;
     const double dg = (double)deg[i] / 10.0;
     const float x = px[i], y = py[i];
-    const float r = sqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)));
+    const float r = sqrt_rn(((x * x) + (y * y)));
     const double rc = ((double)r - max_r) / (min_r - max_r);
     const float th = fabsf((float)atan2((double)y, (double)x));
-    const float az = div_rn(__fsub_rn(th, max_az), az_den);
+    const float az = div_rn((th - max_az), az_den);
     float* o = out + (size_t)i * 6;
     o[0] = vr[i];
     o[1] = rcs[i];
@@ -81,12 +81,12 @@ __global__ __launch_bounds__(256) void edge_features_kernel(
   for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < E && p < n_edges; p += stride) {
     const int s = src[p];
     const int d = dst[p];
-    const float dx = div_rn(__fsub_rn(px[s], px[d]), 10.f);
-    const float dy = div_rn(__fsub_rn(py[s], py[d]), 10.f);
-    const float dl = div_rn(sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy))), 10.f);
-    const float dvx = __fsub_rn(vx[s], vx[d]);
-    const float dvy = __fsub_rn(vy[s], vy[d]);
-    const float dv = sqrt_rn(__fadd_rn(__fmul_rn(dvx, dvx), __fmul_rn(dvy, dvy)));
+    const float dx = div_rn((px[s] - px[d]), 10.f);
+    const float dy = div_rn((py[s] - py[d]), 10.f);
+    const float dl = div_rn(sqrt_rn(((dx * dx) + (dy * dy))), 10.f);
+    const float dvx = (vx[s] - vx[d]);
+    const float dvy = (vy[s] - vy[d]);
+    const float dv = sqrt_rn(((dvx * dvx) + (dvy * dvy)));
     const float dt = (float)((double)(ts[s] - ts[d]) * 1e-6);
     float* o = out + (size_t)p * 7;
     o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;
@@ -182,8 +182,8 @@ __global__ void dense_adj_kernel(const float* __restrict__ px, const float* __re
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   if (dist) {
-    float dx = __fsub_rn(px[i], px[j]), dy = __fsub_rn(py[i], py[j]);
-    dist[(size_t)i * n + j] = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+    float dx = (px[i] - px[j]), dy = (py[i] - py[j]);
+    dist[(size_t)i * n + j] = ((dx * dx) + (dy * dy));
   }
   if (adj) adj[(size_t)i * n + j] = 0;
 }
