@@ -276,7 +276,7 @@ def main():
         'roofline': roof,
         'kernels': kern,
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args, cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -1,0 +1,79 @@
+"""World-size-2 gloo rehearsal of bench.py's multi-GPU path on the CPU.
+
+bench.py shards FRAMES across ranks (weak scaling): each rank owns
+its own frames, builds and runs them with no data-path collective, and only the timing
+(max over ranks) and the frame count (sum over ranks) are reduced.  These tests run the
+same helpers under two gloo processes and check (1) the shards are disjoint and cover
+the single-process frame set, (2) the reductions are the max / sum, and (3) the per-rank
+graphs (oracle restatement, CPU) concatenate to the single-process result, i.e. the
+sharding needs no exchange step.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, frames, nodes, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import bench
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from oracle import graph_features_ref as gref
+    w, r, _ = bench.setup_dist()
+    assert (w, r) == (world, rank)
+    seeds = bench.rank_frame_seeds(rank, frames, synthetic.SEED0)
+    n_edges = []
+    for s in seeds:
+        fr = synthetic.make_frame(nodes, s)
+        adj = gref.compute_adjacency_information(fr, 25.0, 8)
+        n_edges.append(adj['adj_list'].shape[1])
+    bench.barrier(w)
+    t_max = bench.max_over_ranks(float(rank + 1), w)
+    total = bench.sum_over_ranks(float(len(seeds)), w)
+    np.savez(os.path.join(out_dir, f'rank{rank}.npz'), seeds=np.array(seeds),
+             n_edges=np.array(n_edges), t_max=t_max, total=total)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_frame_sharding_two_ranks_gloo(tmp_path):
+    world, frames, nodes = 2, 3, 120
+    mp.spawn(_worker, args=(world, _free_port(), frames, nodes, str(tmp_path)), nprocs=world,
+             join=True)
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from oracle import graph_features_ref as gref
+    res = [np.load(tmp_path / f'rank{r}.npz') for r in range(world)]
+    seeds = np.concatenate([x['seeds'] for x in res])
+    assert len(set(seeds.tolist())) == world * frames            # disjoint shards
+    for x in res:
+        assert float(x['t_max']) == float(world)                 # max over ranks
+        assert float(x['total']) == float(world * frames)        # whole-job frame count
+    # single process over the union of the shards == concatenation of the ranks' work
+    want = []
+    for s in seeds:
+        adj = gref.compute_adjacency_information(synthetic.make_frame(nodes, int(s)), 25.0, 8)
+        want.append(adj['adj_list'].shape[1])
+    np.testing.assert_array_equal(np.concatenate([x['n_edges'] for x in res]), want)
+
+
+def test_rank_seeds_weak_scaling():
+    import bench
+    a = bench.rank_frame_seeds(0, 64, 7)
+    b = bench.rank_frame_seeds(1, 64, 7)
+    assert len(a) == len(b) == 64 and not set(a) & set(b)
+    assert bench.rank_frame_seeds(0, 64, 7) == a                 # deterministic per rank
