@@ -30,6 +30,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 static constexpr int FT = 512;  // 8 waves per workgroup (2 per SIMD)
 static constexpr int FW = FT / 64;
 static constexpr float NORM_EPS = 1e-5f;
+static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layers 0+1
 
 struct FLayer {
   const void* src;  // packed weights (+bias) in global memory
@@ -190,14 +191,46 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
   }
 }
 
-__device__ __forceinline__ int ffeat(int m, int q, int h) {
-  return 32 * m + 8 * (q >> 2) + 4 * h + (q & 3);
+// packed bytes of a fast-format Linear(K -> N): MT x KS fragments of 1 KiB + the
+// bias padded to N (rg_packed_linear_bytes, mlp_chain.hip); layer images are
+// 16-B aligned and back to back, so every LDS offset is a compile-time constant
+__host__ __device__ constexpr int fast_bytes(int K, int N) {
+  return (N / 32) * ((K + 15) / 16) * 1024 + N * 4;
+}
+template <int K, int... Ns> struct Offsets;
+template <int K> struct Offsets<K> {
+  static constexpr int get(int) { return 0; }
+};
+template <int K, int N, int... Rest> struct Offsets<K, N, Rest...> {
+  static constexpr int get(int l) {
+    return l == 0 ? 0 : ((fast_bytes(K, N) + 15) & ~15) + Offsets<N, Rest...>::get(l - 1);
+  }
+};
+
+// activation of a register array: ACT >= 0 is the chain's hidden activation fixed at
+// compile time (a layer whose act differs is the identity, checked on the host);
+// ACT < 0 dispatches once per layer at run time
+template <int ACT, int MT>
+__device__ __forceinline__ void activate(f32x16 (&acc)[MT], int act) {
+  auto loop = [&](auto A) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = act_t<decltype(A)::value>(acc[m][q]);
+  };
+  if constexpr (ACT >= 0) {
+    if (act == ACT) loop(std::integral_constant<int, ACT>{});
+  } else {
+    act_dispatch(act, loop);
+  }
 }
 
-template <int MT>
-__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int h) {
-  const int out = L.out;
-  const bool full = out == 32 * MT;
+// Padded output features (beyond L.out) need no masking: their weight rows and bias are
+// packed as zeros, so they are exactly 0 before normalisation (normalised layers are
+// never padded, checked on the host) and act(0) = 0; only the LAST layer may be padded
+// and store_out never writes those columns.
+template <int ACT, int MT>
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L) {
   if (L.mu) {
     float s = 0.f;
 #pragma unroll
@@ -205,17 +238,17 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int
 #pragma unroll
       for (int q = 0; q < 16; ++q) s += acc[m][q];
     s += __shfl_xor(s, 32, 64);
-    const float mean = s / (float)out;
+    const float mean = s / (float)(32 * MT);
     float ss = 0.f;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float d = acc[m][q] - mean;
-        ss += (full || ffeat(m, q, h) < out) ? d * d : 0.f;
+        ss += d * d;
       }
     ss += __shfl_xor(ss, 32, 64);
-    const float inv = 1.f / (__fsqrt_rn(ss / (float)(out - 1)) + NORM_EPS);
+    const float inv = 1.f / (__fsqrt_rn(ss / (float)(32 * MT - 1)) + NORM_EPS);
     // y = s * (x - mean) / (std + eps) + m as one fma: x*gs + (m - mean*gs)
     const float gs = *L.sd * inv, gb = fmaf(-mean, gs, *L.mu);
 #pragma unroll
@@ -223,16 +256,7 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, int
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], gs, gb);
   }
-  act_dispatch(L.act, [&](auto A) {
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        float v = act_t<decltype(A)::value>(acc[m][q]);
-        if (!full && ffeat(m, q, h) >= out) v = 0.f;
-        acc[m][q] = v;
-      }
-  });
+  activate<ACT, MT>(acc, L.act);
 }
 
 template <int MT>
@@ -299,28 +323,104 @@ __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& 
     }
 }
 
-template <int LI, int K, int N, int... Rest>
+template <int ACT, int OFF, int LI, int K, int N, int... Rest>
 __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K + 15) / 16],
                                           const char* lds, long row, bool valid, int lane) {
   constexpr int KS = (K + 15) / 16;
   constexpr int MT = N / 32;
   static_assert(N % 32 == 0, "padded widths are multiples of 32");
   f32x16 acc[MT];
-  mfma_layer<KS, MT>(b, acc, lds + a.L[LI].woff, lane);
-  epilogue<MT>(acc, a.L[LI], lane >> 5);
+  mfma_layer<KS, MT>(b, acc, lds + OFF, lane);
+  epilogue<ACT, MT>(acc, a.L[LI]);
   if constexpr (sizeof...(Rest) > 0) {
     bf16x8_t nb[2 * MT];
     pack_next<MT>(acc, nb);
-    run_chain<LI + 1, N, Rest...>(a, nb, lds, row, valid, lane);
+    run_chain<ACT, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, row,
+                                                                             valid, lane);
   } else {
     if (valid) store_out<MT>(acc, a, row, lane >> 5);
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int... Ns>
+// Layers 0 and 1 fused tile by tile, for a first layer WITHOUT normalisation (the
+// encoders' first ffn_block, gnn_blocks.py:31): each 32-wide output tile of layer 0 is
+// activated, packed to bf16 and consumed at once as layer 1's k-steps 2m0, 2m0+1, so
+// layer 0's N0-wide activation never exists in full (the 7 -> 256 edge encoder would
+// otherwise hold 128 accumulators + 64 packed registers and spill).
+template <int ACT, int K0, int N0, int N1, int... Rest>
+__device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[(K0 + 15) / 16],
+                                            const char* lds, long row, bool valid, int lane) {
+  constexpr int KS0 = (K0 + 15) / 16, MT0 = N0 / 32, KS1 = N0 / 16, MT1 = N1 / 32;
+  constexpr int OFF1 = (fast_bytes(K0, N0) + 15) & ~15;
+  constexpr int OFF2 = OFF1 + ((fast_bytes(N0, N1) + 15) & ~15);
+  static_assert(N0 % 32 == 0 && N1 % 32 == 0, "padded widths are multiples of 32");
+  const int h = lane >> 5;
+  const char* w0 = lds + lane * 16;
+  const char* w1 = lds + OFF1 + lane * 16;
+  const float* bias0 = (const float*)(lds + MT0 * KS0 * 1024);
+  const float* bias1 = (const float*)(lds + OFF1 + MT1 * KS1 * 1024);
+  f32x16 acc[MT1];
+#pragma unroll
+  for (int m = 0; m < MT1; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bv = *(const f32x4*)(bias1 + 32 * m + 8 * g + 4 * h);
+      acc[m][4 * g + 0] = bv.x;
+      acc[m][4 * g + 1] = bv.y;
+      acc[m][4 * g + 2] = bv.z;
+      acc[m][4 * g + 3] = bv.w;
+    }
+  auto body = [&](auto A) {
+#pragma unroll
+    for (int m0 = 0; m0 < MT0; ++m0) {
+      f32x16 t;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bv = *(const f32x4*)(bias0 + 32 * m0 + 8 * g + 4 * h);
+        t[4 * g + 0] = bv.x;
+        t[4 * g + 1] = bv.y;
+        t[4 * g + 2] = bv.z;
+        t[4 * g + 3] = bv.w;
+      }
+#pragma unroll
+      for (int s = 0; s < KS0; ++s)
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            ld_bf8((const uint16_t*)(w0 + (m0 * KS0 + s) * 1024)), b[s], t, 0, 0, 0);
+      bf16x8_t nb[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_t<decltype(A)::value>(t[8 * hf + j]);
+        nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0], v[1]), bf2(v[2], v[3]),
+                                                      bf2(v[4], v[5]), bf2(v[6], v[7])});
+      }
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int m = 0; m < MT1; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              ld_bf8((const uint16_t*)(w1 + (m * KS1 + 2 * m0 + hf) * 1024)), nb[hf], acc[m], 0,
+              0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one layer-0 tile in flight: bounded registers
+    }
+  };
+  if constexpr (ACT >= 0) body(std::integral_constant<int, ACT>{});  // layer 0 act == ACT (host)
+  else act_dispatch(a.L[0].act, body);
+  epilogue<ACT, MT1>(acc, a.L[1]);
+  if constexpr (sizeof...(Rest) > 0) {
+    bf16x8_t nb[2 * MT1];
+    pack_next<MT1>(acc, nb);
+    run_chain<ACT, OFF2, 2, N1, Rest...>(a, nb, lds, row, valid, lane);
+  } else {
+    if (valid) store_out<MT1>(acc, a, row, h);
+  }
+}
+
+template <int MODE, bool IN_F32, int W0, int W1, int ACT, int... Ns>
 __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  using In = Input<MODE, IN_F32, W0, W1>;
+  using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
   // stage all layers' packed weights + biases (static layer indices: no scratch copy)
 #pragma unroll
   for (int l = 0; l < RG_MAX_LAYERS; ++l) {
@@ -340,13 +440,21 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     const bool valid = row < rows;
     bf16x8_t b[In::KS];
     In::load(a, row, valid, lane >> 5, b);
-    run_chain<0, In::K0, Ns...>(a, b, lds, row, valid, lane);
+    if constexpr ((MODE & FUSE01) != 0)  // un-normalised first layer: tile-fused layers 0+1
+      run_chain01<ACT, In::K0, Ns...>(a, b, lds, row, valid, lane);
+    else
+      run_chain<ACT, 0, 0, In::K0, Ns...>(a, b, lds, row, valid, lane);
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int... Ns>
+template <int MODE, bool IN_F32, int W0, int W1, int ACT, int... Ns>
 static int launch(const FArgs& a, hipStream_t st) {
-  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, Ns...>;
+  using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
+  // the host-side LDS image must be the layout the kernel assumes
+  using Off = Offsets<In::K0, Ns...>;
+  for (int l = 0; l < a.nl; ++l)
+    RG_REQUIRE(a.L[l].woff == Off::get(l), RG_ERR_ARG, "rg_mlp_chain_fast: LDS layout of layer %d", l);
+  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, ACT, Ns...>;
   static bool attr = false;
   if (!attr) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -363,9 +471,9 @@ static int launch(const FArgs& a, hipStream_t st) {
   return RG_OK;
 }
 
-// shape key: mode, f32 input, widths, padded outputs
+// shape key: mode, f32 input, widths, hidden activation (-1: any), padded outputs
 struct Key {
-  int mode, in_f32, w0, w1, nl;
+  int mode, in_f32, w0, w1, act, nl;
   int n[RG_MAX_LAYERS];
 };
 
@@ -382,12 +490,13 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
 
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
 static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
-#define RG_FAST(MODE, F32, W0, W1, ...)                                      \
-  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                           \
-    return launch<MODE, F32, W0, W1, __VA_ARGS__>(a, st);
+#define RG_FAST(MODE, F32, W0, W1, ...)                                              \
+  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                   \
+    return k.act == ACT_LEAKY ? launch<MODE, F32, W0, W1, ACT_LEAKY, __VA_ARGS__>(a, st) \
+                              : launch<MODE, F32, W0, W1, -1, __VA_ARGS__>(a, st);
   // node / edge encoders (graph_feature_encoding, yml:56-57)
-  RG_FAST(RG_IN_DENSE, 1, 6, 0, 256, 128, 64)
-  RG_FAST(RG_IN_DENSE, 1, 7, 0, 256, 128, 128, 64)
+  RG_FAST(RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
+  RG_FAST(RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
   RG_FAST(RG_IN_GATHER3, 0, 64, 64, 128, 64)
   RG_FAST(RG_IN_CONCAT2, 0, 64, 64, 64)
@@ -466,7 +575,17 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
   if (in_mode == RG_IN_DENSE && k.in_f32) {
     if (w0 > 8) return RG_ERR_UNSUPPORTED;
     k.w0 = w0;
+    // encoders: the first ffn_block has no normalisation (gnn_blocks.py:31)
+    if (n_layers >= 2 && !layers[0].norm_mu) k.mode |= FUSE01;
   }
+  // compile-time hidden activation: every layer uses the yml activation (LeakyReLU,
+  // configuration_radarscenes_gnn.yml:50) except possibly an identity last layer
+  k.act = ACT_LEAKY;
+  for (int l = 0; l < n_layers; ++l)
+    if (layers[l].act != ACT_LEAKY && !(l == n_layers - 1 && layers[l].act == ACT_NONE)) k.act = -1;
+  // normalised layers must be unpadded (epilogue statistics run over 32*MT features)
+  for (int l = 0; l < n_layers; ++l)
+    if (layers[l].norm_mu && layers[l].out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
   if (rows <= 0) return RG_OK;
   return dispatch(k, a, (hipStream_t)stream);
 }
