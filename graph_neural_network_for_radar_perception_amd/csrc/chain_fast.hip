@@ -207,56 +207,13 @@ template <int K, int N, int... Rest> struct Offsets<K, N, Rest...> {
   }
 };
 
-// activation of a register array: ACT >= 0 is the chain's hidden activation fixed at
-// compile time (a layer whose act differs is the identity, checked on the host);
-// ACT < 0 dispatches once per layer at run time
-template <int ACT, int MT>
-__device__ __forceinline__ void activate(f32x16 (&acc)[MT], int act) {
-  auto loop = [&](auto A) {
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = act_t<decltype(A)::value>(acc[m][q]);
-  };
-  if constexpr (ACT >= 0) {
-    if (act == ACT) loop(std::integral_constant<int, ACT>{});
-  } else {
-    act_dispatch(act, loop);
-  }
-}
-
 // Padded output features (beyond L.out) need no masking: their weight rows and bias are
 // packed as zeros, so they are exactly 0 before normalisation (normalised layers are
 // never padded, checked on the host) and act(0) = 0; only the LAST layer may be padded
 // and store_out never writes those columns.
 template <int ACT, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L) {
-  if (L.mu) {
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) s += acc[m][q];
-    s += __shfl_xor(s, 32, 64);
-    const float mean = s / (float)(32 * MT);
-    float ss = 0.f;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float d = acc[m][q] - mean;
-        ss += d * d;
-      }
-    ss += __shfl_xor(ss, 32, 64);
-    const float inv = 1.f / (__fsqrt_rn(ss / (float)(32 * MT - 1)) + NORM_EPS);
-    // y = s * (x - mean) / (std + eps) + m as one fma: x*gs + (m - mean*gs)
-    const float gs = *L.sd * inv, gb = fmaf(-mean, gs, *L.mu);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], gs, gb);
-  }
-  activate<ACT, MT>(acc, L.act);
+  norm_act_rows<ACT, MT>(acc, L.mu, L.sd, L.act, NORM_EPS);
 }
 
 template <int MT>
@@ -389,11 +346,11 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
       bf16x8_t nb[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        float v[8];
+        f32x2 v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = act_t<decltype(A)::value>(t[8 * hf + j]);
-        nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0], v[1]), bf2(v[2], v[3]),
-                                                      bf2(v[4], v[5]), bf2(v[6], v[7])});
+        for (int j = 0; j < 4; ++j) v[j] = act_pk<decltype(A)::value>(pair(t, 4 * hf + j));
+        nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0].x, v[0].y), bf2(v[1].x, v[1].y),
+                                                      bf2(v[2].x, v[2].y), bf2(v[3].x, v[3].y)});
       }
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)

@@ -96,41 +96,13 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
   }
 }
 
-// channel_normalization (common.py:208-220) + activation on full-width rows
-template <int MT>
+// channel_normalization (common.py:208-220) + activation (rg_common.h norm_act_rows)
+// (every block is normalised, and with ACT >= 0 every block uses ACT: host-checked)
+template <int ACT, int MT>
 __device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
-  constexpr int OUT = 32 * MT;
-  if (L.mu) {
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) s += acc[m][q];
-    s += __shfl_xor(s, 32, 64);
-    const float mean = s * (1.f / OUT);
-    float ss = 0.f;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float d = acc[m][q] - mean;
-        ss += d * d;
-      }
-    ss += __shfl_xor(ss, 32, 64);
-    const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (OUT - 1))) + NORM_EPS);
-    // s*(x-mean)/(std+eps) + m as ONE fma per element: x*gs + (m - mean*gs)
-    const float gs = *L.sd * inv, gb = fmaf(-mean, gs, *L.mu);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], gs, gb);
-  }
-  act_dispatch(L.act, [&](auto A) {
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[m][q] = act_t<decltype(A)::value>(acc[m][q]);
-  });
+  channel_norm_pk<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+  if constexpr (ACT >= 0) act_pk_all<ACT, MT>(acc);
+  else act_dispatch(L.act, [&](auto A) { act_pk_all<decltype(A)::value, MT>(acc); });
 }
 
 template <int MT>
@@ -146,6 +118,7 @@ __device__ __forceinline__ void pack_acc(const f32x16 (&acc)[MT], bf16x8_t* nb) 
     }
 }
 
+template <int ACT>
 __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // stage weights (static indices)
@@ -226,12 +199,12 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       }
       f32x16 acc1[4];
       mfma_layer<12, 4>(b, acc1, w0, lane);
-      norm_act<4>(acc1, a.L[0]);
+      norm_act<ACT, 4>(acc1, a.L[0]);
       bf16x8_t b2[8];
       pack_acc<4>(acc1, b2);
       f32x16 acc2[2];
       mfma_layer<8, 2>(b2, acc2, w1, lane);
-      norm_act<2>(acc2, a.L[1]);
+      norm_act<ACT, 2>(acc2, a.L[1]);
       // ---- message tile M -> LDS as rows [edge][feature] (8-B stores of 4 features);
       //      invalid edges -> 0
 #pragma unroll
@@ -301,7 +274,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     pack_acc<2>(agg, bu + 4);
     f32x16 accu[2];
     mfma_layer<8, 2>(bu, accu, w2, lane);
-    norm_act<2>(accu, a.L[2]);
+    norm_act<ACT, 2>(accu, a.L[2]);
     if (nvalid) {
       uint16_t* po = a.x_out + (size_t)node * a.ldo;
       const uint16_t* pr = a.x + (size_t)node * a.ldx;
@@ -379,16 +352,20 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   if (n_nodes <= 0) return RG_OK;
   const size_t lds = (size_t)off + (size_t)CW * (32 * TSTRIDE * 2 + 128);
   RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
-  static bool attr = false;
-  if (!attr) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)fused_conv_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
+  // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
+  // blocks selects the compile-time variant; anything else dispatches per layer
+  const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY;
+  auto kern = leaky ? fused_conv_kernel<ACT_LEAKY> : fused_conv_kernel<-1>;
+  static bool attr[2] = {false, false};
+  if (!attr[leaky]) {
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    attr[leaky] = true;
   }
   RG_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(int), st));
   int blocks = 256;
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
-  fused_conv_kernel<<<blocks, CT, lds, st>>>(a);
+  kern<<<blocks, CT, lds, st>>>(a);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

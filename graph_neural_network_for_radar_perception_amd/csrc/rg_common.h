@@ -105,4 +105,92 @@ __device__ __forceinline__ void act_dispatch(int act, F&& f) {
   else f(std::integral_constant<int, ACT_NONE>{});
 }
 
+// ---------------------------------------------------------------------------
+// Row epilogue of the register-resident bf16 kernels (chain_fast.hip, conv_fused.hip):
+// a row's MT*32 features live in MT f32x16 MFMA accumulators of one lane pair
+// (lane, lane ^ 32).  channel_normalization (common.py:208-220,
+// y = s (x - mean) / (std_unbiased + eps) + m) and the activation run in packed f32
+// math (v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two features per instruction).
+// ---------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pair(const f32x16& v, int i) { return (f32x2){v[2 * i], v[2 * i + 1]}; }
+__device__ __forceinline__ void set_pair(f32x16& v, int i, f32x2 p) {
+  v[2 * i] = p.x;
+  v[2 * i + 1] = p.y;
+}
+
+template <int ACT>
+__device__ __forceinline__ f32x2 act_pk(f32x2 y) {
+  if constexpr (ACT == ACT_LEAKY) {
+    // max(y, 0.01 y) (constants.py:10): one v_pk_mul_f32 + two v_med3_f32 (med3 with +inf
+    // is the max without the operand canonicalisation fmaxf needs in IEEE mode)
+    const f32x2 z = y * (f32x2){0.01f, 0.01f};
+    return (f32x2){__builtin_amdgcn_fmed3f(y.x, z.x, __builtin_inff()),
+                   __builtin_amdgcn_fmed3f(y.y, z.y, __builtin_inff())};
+  } else {
+    return (f32x2){act_t<ACT>(y.x), act_t<ACT>(y.y)};
+  }
+}
+
+template <int MT>
+__device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, float sd, float eps) {
+  constexpr int N = 32 * MT;
+  f32x2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      s0 += pair(acc[m], i);
+      s1 += pair(acc[m], i + 1);
+    }
+  const f32x2 st = s0 + s1;
+  float s = st.x + st.y;
+  s += __shfl_xor(s, 32, 64);
+  const float mean = s * (1.f / N);  // N is a power of two: exact
+  const f32x2 nm = {-mean, -mean};
+  f32x2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const f32x2 d0 = pair(acc[m], i) + nm, d1 = pair(acc[m], i + 1) + nm;
+      q0 = __builtin_elementwise_fma(d0, d0, q0);
+      q1 = __builtin_elementwise_fma(d1, d1, q1);
+    }
+  const f32x2 qt = q0 + q1;
+  float ss = qt.x + qt.y;
+  ss += __shfl_xor(ss, 32, 64);
+  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  // s*(x-mean)/(std+eps) + m as ONE fma per feature: x*gs + (m - mean*gs)
+  const float gs = sd * inv, gb = fmaf(-mean, gs, mu);
+  const f32x2 gs2 = {gs, gs}, gb2 = {gb, gb};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, __builtin_elementwise_fma(pair(acc[m], i), gs2, gb2));
+}
+
+template <int ACT, int MT>
+__device__ __forceinline__ void act_pk_all(f32x16 (&acc)[MT]) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, act_pk<ACT>(pair(acc[m], i)));
+}
+
+// normalisation (if mu) + activation; ACT >= 0: compile-time activation applied when
+// act == ACT (any other act is the identity, as checked by the launchers); ACT < 0:
+// one run-time dispatch
+template <int ACT, int MT>
+__device__ __forceinline__ void norm_act_rows(f32x16 (&acc)[MT], const float* mu, const float* sd,
+                                              int act, float eps) {
+  if (mu) channel_norm_pk<MT>(acc, *mu, *sd, eps);
+  if constexpr (ACT >= 0) {
+    if (act == ACT) act_pk_all<ACT, MT>(acc);
+  } else {
+    act_dispatch(act, [&](auto A) { act_pk_all<decltype(A)::value, MT>(acc); });
+  }
+}
+
 }  // namespace rg
