@@ -17,7 +17,8 @@ import re
 from typing import Optional
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, 'lib', 'libradargnn.so')
+# RG_LIBRARY overrides the in-tree library (kernel experiments: build.build_variant)
+LIB_PATH = os.environ.get('RG_LIBRARY') or os.path.join(PKG, 'lib', 'libradargnn.so')
 HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 
 RG_F32, RG_BF16 = 0, 1

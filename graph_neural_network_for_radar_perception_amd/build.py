@@ -36,8 +36,8 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, extra):
-    obj = os.path.join(OBJDIR, os.path.basename(src) + '.o')
+def _compile(src, extra, objdir=OBJDIR):
+    obj = os.path.join(objdir, os.path.basename(src) + '.o')
     if _stale(obj, [src] + _headers()):
         cmd = [HIPCC] + FLAGS + extra + ['-c', src, '-o', obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -62,6 +62,27 @@ def build_library(verbose: bool = False, extra_flags=None) -> str:
     if verbose:
         print('built', LIB)
     return LIB
+
+
+def build_variant(name: str, defines, only=None) -> str:
+    """A copy of the library built with extra -D flags (kernel experiments), at
+    lib/variants/libradargnn_<name>.so; load it with RG_LIBRARY=<path>."""
+    vdir = os.path.join(LIBDIR, 'variants', name)
+    os.makedirs(vdir, exist_ok=True)
+    extra = [f'-D{d}' for d in defines]
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    objs = []
+    for s in srcs:
+        if only is None or os.path.basename(s) in only:
+            objs.append(_compile(s, extra, vdir))
+        else:
+            objs.append(_compile(s, []))
+    out = os.path.join(LIBDIR, 'variants', f'libradargnn_{name}.so')
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', out] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
+    return out
 
 
 if __name__ == '__main__':

@@ -23,6 +23,11 @@
 // atomic counter; all weights (81 KiB packed bf16 + biases) sit in LDS.
 #include "rg_common.h"
 
+#ifndef RG_CONV_EXP
+#define RG_CONV_EXP 0  // timing experiments only (wrong results): 1 no row gathers after the
+                       // first tile, 2 no message norm/act, 3 no transpose/aggregation
+#endif
+
 namespace rg {
 namespace conv {
 
@@ -194,17 +199,22 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       for (int s = 0; s < 12; ++s) b[s] = bn[s];
       const int slot = slot_n;
       if (t0 + 32 < e1) {
-        load_rows(t0 + 32);
+        if (RG_CONV_EXP != 1) load_rows(t0 + 32);
         if (t0 + 64 < e1) load_idx(t0 + 64);
       }
       f32x16 acc1[4];
       mfma_layer<12, 4>(b, acc1, w0, lane);
-      norm_act<ACT, 4>(acc1, a.L[0]);
+      if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0]);
       bf16x8_t b2[8];
       pack_acc<4>(acc1, b2);
       f32x16 acc2[2];
       mfma_layer<8, 2>(b2, acc2, w1, lane);
-      norm_act<ACT, 2>(acc2, a.L[1]);
+      if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1]);
+      if (RG_CONV_EXP == 3) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) agg[m] += acc2[m];
+        continue;
+      }
       // ---- message tile M -> LDS as rows [edge][feature] (8-B stores of 4 features);
       //      invalid edges -> 0
 #pragma unroll

@@ -3,9 +3,12 @@
 // Replaces modules/compute_features/graph_features.py:11-164 (reference v2):
 // the dense O(N^2) numpy distance matrix, np.argsort kNN, ball query and
 // np.where edge list become
-//   1. knn_scan   : one thread per node row, frame points streamed through LDS,
+//   0. grid_setup / grid_count / scan / grid_scatter: per frame, points bucketed
+//                   into a uniform grid of ~3-point cells (cell-ordered copy);
+//   1. knn_grid   : one thread per point, Chebyshev ring search over the cells,
 //                   exact fp32 distances (no FMA), top-(k+1) by (distance, index)
-//                   kept sorted in registers, ball-query count, optional radius bits;
+//                   kept sorted in registers, ball-query count, optional radius bits,
+//                   stopping once no unvisited cell can change the result;
 //   2. knn_mark   : kNN pairs set in a per-row bitset both ways (atomicOr);
 //   3. row_count  : one wave per row, popcount of the bitset row;
 //   4. exclusive scan -> CSR row_ptr;
@@ -31,7 +34,6 @@ void set_error(const char* fmt, ...) {
 }
 
 static constexpr int KNN_BLOCK = 256;
-static constexpr int KNN_CHUNK = 2048;  // points per LDS stage (16 KiB)
 
 // fp32 squared distance exactly as numpy evaluates graph_features.py:72-73:
 // two products and one sum, each rounded, no fused multiply-add.
@@ -41,85 +43,27 @@ __device__ __forceinline__ float sqdist(float xi, float yi, float xj, float yj) 
   return ((dx * dx) + (dy * dy));
 }
 
-// K = list length kept per row (>= k+1).  Ties: a later (larger) j never
-// displaces an equal distance, i.e. "equal distance -> lower index first".
-template <int K>
-__global__ __launch_bounds__(KNN_BLOCK) void knn_scan(
-    const float* __restrict__ px, const float* __restrict__ py, const int* __restrict__ frame_ptr,
-    int kk, float eps2, int mode, int* __restrict__ knn_idx, int* __restrict__ knn_cnt,
-    int* __restrict__ ball_deg, uint32_t* __restrict__ bits, int W) {
-  __shared__ float2 pts[KNN_CHUNK];
-  const int f = blockIdx.y;
-  const int base = frame_ptr[f];
-  const int nf = frame_ptr[f + 1] - base;
-  if ((int)(blockIdx.x * KNN_BLOCK) >= nf) return;  // block-uniform exit
-  const int il = blockIdx.x * KNN_BLOCK + threadIdx.x;
-  const bool active = il < nf;
-  const float xi = active ? px[base + il] : 0.f;
-  const float yi = active ? py[base + il] : 0.f;
-  const bool want_knn = mode != RG_GRAPH_RADIUS;
-  const bool want_rad = mode != RG_GRAPH_KNN;
+// ---------------------------------------------------------------------------------
+// Uniform-grid neighbour search.  The reference ranks a row against the WHOLE frame
+// (N x N distance matrix + argsort, graph_features.py:25-44); the result -- the k+1
+// smallest (distance, index) keys, the ball-query count and the radius set -- only
+// depends on points near the row, so each frame's points are bucketed into square
+// cells of side s (~3 points per cell) and a row visits cells in Chebyshev rings
+// r = 0, 1, 2, ... around its own cell.  Every point in a cell beyond ring r is at
+// least (r - 0.01) s away (0.01 covers the f32 rounding of the cell coordinates), so
+// once the current (k+1)-th key and eps2 are below that bound squared (minus a 1e-5
+// relative margin for the f32 distance rounding) no unvisited point can enter the
+// result: the selection equals the full scan's, ties included (keys compare as (d, j)).
+// ---------------------------------------------------------------------------------
+struct FrameGrid {
+  float xmin, ymin, inv_s, s;
+  int gw, gh, cell0, n;
+};
 
-  float bd[K];
-  int bi[K];
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    bd[s] = __int_as_float(0x7f800000);  // +inf
-    bi[s] = -1;
-  }
-  int ball = 0;
-  uint32_t* rowbits = bits + (size_t)(base + il) * W;
-
-  for (int c0 = 0; c0 < nf; c0 += KNN_CHUNK) {
-    const int cn = min(KNN_CHUNK, nf - c0);
-    __syncthreads();
-    for (int t = threadIdx.x; t < cn; t += KNN_BLOCK)
-      pts[t] = make_float2(px[base + c0 + t], py[base + c0 + t]);
-    __syncthreads();
-    if (!active) continue;
-    for (int t0 = 0; t0 < cn; t0 += 32) {
-      uint32_t word = 0;
-      const int tn = min(32, cn - t0);
-      for (int u = 0; u < tn; ++u) {
-        const float2 p = pts[t0 + u];
-        const int j = c0 + t0 + u;
-        const float d = sqdist(xi, yi, p.x, p.y);
-        const bool inball = (d <= eps2) && (j != il);
-        ball += inball ? 1 : 0;
-        word |= (inball ? 1u : 0u) << u;
-        if (want_knn && d < bd[K - 1]) {
-          // sorted insert, stable w.r.t. j (strict compares)
-#pragma unroll
-          for (int s = K - 1; s > 0; --s) {
-            const bool shift = d < bd[s - 1];
-            const bool here = !shift && d < bd[s];
-            bd[s] = shift ? bd[s - 1] : (here ? d : bd[s]);
-            bi[s] = shift ? bi[s - 1] : (here ? j : bi[s]);
-          }
-          if (d < bd[0]) {
-            bd[0] = d;
-            bi[0] = j;
-          }
-        }
-      }
-      if (want_rad) rowbits[(c0 + t0) >> 5] = word;
-    }
-  }
-  if (!active) return;
-  ball_deg[base + il] = ball;
-  if (want_knn) {
-    const int cnt = min(kk, nf);
-    knn_cnt[base + il] = cnt;
-    int* out = knn_idx + (size_t)(base + il) * K;
-#pragma unroll
-    for (int s = 0; s < K; ++s)
-      if (s < cnt) out[s] = bi[s];
-  }
-}
-
-// frame base of each global row (needed to translate frame-local <-> global ids)
+// frame id and frame base of every global row (disjoint-union batch)
 __global__ void row_frame_base(const int* __restrict__ frame_ptr, int n_frames,
-                               int* __restrict__ row_base, int n_nodes) {
+                               int* __restrict__ row_base, int* __restrict__ row_frame,
+                               int n_nodes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_nodes) return;
   int lo = 0, hi = n_frames;  // frame_ptr[lo] <= i < frame_ptr[hi]
@@ -128,6 +72,201 @@ __global__ void row_frame_base(const int* __restrict__ frame_ptr, int n_frames,
     if (frame_ptr[mid] <= i) lo = mid; else hi = mid;
   }
   row_base[i] = frame_ptr[lo];
+  row_frame[i] = lo;
+}
+
+// one block per frame: bounding box -> cell size and grid shape (<= cpf cells)
+__global__ __launch_bounds__(256) void grid_setup(const float* __restrict__ px,
+                                                  const float* __restrict__ py,
+                                                  const int* __restrict__ frame_ptr, int cpf,
+                                                  FrameGrid* __restrict__ fg) {
+  __shared__ float r[4][256];
+  const int f = blockIdx.x;
+  const int b = frame_ptr[f], e = frame_ptr[f + 1];
+  float x0 = __int_as_float(0x7f800000), y0 = x0, x1 = -x0, y1 = -x0;
+  for (int i = b + threadIdx.x; i < e; i += 256) {
+    const float x = px[i], y = py[i];
+    x0 = fminf(x0, x); x1 = fmaxf(x1, x);
+    y0 = fminf(y0, y); y1 = fmaxf(y1, y);
+  }
+  r[0][threadIdx.x] = x0; r[1][threadIdx.x] = x1;
+  r[2][threadIdx.x] = y0; r[3][threadIdx.x] = y1;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      const int o = threadIdx.x + st;
+      r[0][threadIdx.x] = fminf(r[0][threadIdx.x], r[0][o]);
+      r[1][threadIdx.x] = fmaxf(r[1][threadIdx.x], r[1][o]);
+      r[2][threadIdx.x] = fminf(r[2][threadIdx.x], r[2][o]);
+      r[3][threadIdx.x] = fmaxf(r[3][threadIdx.x], r[3][o]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const int n = e - b;
+  FrameGrid g;
+  g.cell0 = f * cpf;
+  g.n = n;
+  g.xmin = n > 0 ? r[0][0] : 0.f;
+  g.ymin = n > 0 ? r[2][0] : 0.f;
+  const float w = n > 0 ? r[1][0] - r[0][0] : 0.f;
+  const float h = n > 0 ? r[3][0] - r[2][0] : 0.f;
+  const float ext = fmaxf(w, h);
+  int gw = 1, gh = 1;
+  float s = 1.f;
+  if (ext > 0.f && ext < 1.0e30f && n > 3) {  // finite extent: ~3 points per cell
+    const int target = min(max(n / 3, 1), cpf);
+    const float wm = fmaxf(w, ext * 1e-3f), hm = fmaxf(h, ext * 1e-3f);
+    s = sqrtf(wm * hm / (float)target);
+    for (;;) {
+      gw = (int)(w / s) + 1;
+      gh = (int)(h / s) + 1;
+      if ((long)gw * gh <= cpf) break;
+      s *= 1.25f;
+    }
+  }
+  g.s = s;
+  g.inv_s = 1.f / s;
+  g.gw = gw;
+  g.gh = gh;
+  fg[f] = g;
+}
+
+__device__ __forceinline__ int cell_coord(float v, float v0, float inv_s, int gdim) {
+  const int c = (int)((v - v0) * inv_s);
+  return c < 0 ? 0 : (c >= gdim ? gdim - 1 : c);
+}
+
+__global__ void grid_count(const float* __restrict__ px, const float* __restrict__ py,
+                           const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+                           int n_nodes, int* __restrict__ cell_of, int* __restrict__ cell_cnt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  const FrameGrid g = fg[row_frame[i]];
+  const int cx = cell_coord(px[i], g.xmin, g.inv_s, g.gw);
+  const int cy = cell_coord(py[i], g.ymin, g.inv_s, g.gh);
+  const int c = g.cell0 + cy * g.gw + cx;
+  cell_of[i] = c;
+  atomicAdd(cell_cnt + c, 1);
+}
+
+// points regrouped by cell: {x, y, frame-local index, cell}.  The order inside a cell
+// depends on atomic arrival and does not matter: every consumer compares full keys.
+__global__ void grid_scatter(const float* __restrict__ px, const float* __restrict__ py,
+                             const int* __restrict__ row_base, const int* __restrict__ cell_of,
+                             int n_nodes, int* __restrict__ cursor, float4* __restrict__ pts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  const int c = cell_of[i];
+  const int pos = atomicAdd(cursor + c, 1);
+  pts[pos] = make_float4(px[i], py[i], __int_as_float(i - row_base[i]), __int_as_float(c));
+}
+
+__device__ __forceinline__ bool key_less(float d, int j, float bd, int bj) {
+  return d < bd || (d == bd && j < bj);
+}
+
+// One thread per point in cell order (a wave = spatially adjacent rows, so the cells it
+// visits are shared through L1).  K = list length kept per row (>= kk = k + 1).
+template <int K>
+__global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, int kk, float eps2, int mode,
+    int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
+    uint32_t* __restrict__ bits, int W) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_nodes) return;
+  const int f = row_frame[t];  // the cell-ordered points of frame f fill its row range
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const float xi = me.x, yi = me.y;
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
+  const bool want_knn = mode != RG_GRAPH_RADIUS;
+  const bool want_rad = mode != RG_GRAPH_KNN;
+  uint32_t* rowbits = bits + (size_t)(base + il) * W;
+
+  float bd[K];
+  int bi[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    bd[q] = __int_as_float(0x7f800000);  // +inf
+    bi[q] = 0x7fffffff;
+  }
+  int ball = 0;
+  const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
+  bool knn_done = !want_knn, ball_done = false;
+  for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
+    // cells at Chebyshev distance exactly r: rows cy-r and cy+r in full, then the
+    // columns cx-r and cx+r strictly between them
+    for (int side = 0; side < 4; ++side) {
+      int ya, yb, xa, xb;
+      if (side < 2) {
+        const int yy = side == 0 ? cy - r : cy + r;
+        if (yy < 0 || yy >= g.gh || (side == 1 && r == 0)) continue;
+        ya = yb = yy;
+        xa = max(cx - r, 0);
+        xb = min(cx + r, g.gw - 1);
+      } else {
+        if (r == 0) continue;
+        const int xx = side == 2 ? cx - r : cx + r;
+        if (xx < 0 || xx >= g.gw) continue;
+        xa = xb = xx;
+        ya = max(cy - r + 1, 0);
+        yb = min(cy + r - 1, g.gh - 1);
+      }
+      for (int yy = ya; yy <= yb; ++yy) {
+        // cells xa..xb of one grid row are contiguous in the cell order
+        const int c = g.cell0 + yy * g.gw;
+        const int p0 = cell_start[c + xa], p1 = cell_start[c + xb + 1];
+        for (int p = p0; p < p1; ++p) {
+          const float4 q = pts[p];
+          const int j = __float_as_int(q.z);
+          const float d = sqdist(xi, yi, q.x, q.y);
+          const bool inball = (d <= eps2) && (j != il);
+          ball += inball ? 1 : 0;
+          if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
+          if (want_knn && key_less(d, j, bd[K - 1], bi[K - 1])) {
+            // sorted insert by (d, j): branch-free pass from the tail
+#pragma unroll
+            for (int s2 = K - 1; s2 > 0; --s2) {
+              const bool shift = key_less(d, j, bd[s2 - 1], bi[s2 - 1]);
+              const bool here = !shift && key_less(d, j, bd[s2], bi[s2]);
+              bd[s2] = shift ? bd[s2 - 1] : (here ? d : bd[s2]);
+              bi[s2] = shift ? bi[s2 - 1] : (here ? j : bi[s2]);
+            }
+            if (key_less(d, j, bd[0], bi[0])) {
+              bd[0] = d;
+              bi[0] = j;
+            }
+          }
+        }
+      }
+    }
+    // every point beyond ring r is at least (r - 0.01) s away
+    const float lb = fmaxf((float)r - 0.01f, 0.f) * g.s;
+    const float bound = lb * lb * (1.f - 1e-5f);
+    if (eps2 < bound) ball_done = true;
+    if (!knn_done) {
+      float dk = bd[0];  // the kk-th key so far (+inf while fewer are held)
+#pragma unroll
+      for (int q = 1; q < K; ++q) dk = q == kk - 1 ? bd[q] : dk;
+      if (dk < bound) knn_done = true;
+    }
+  }
+  const int row = base + il;
+  ball_deg[row] = ball;
+  if (want_knn) {
+    const int cnt = min(kk, g.n);
+    knn_cnt[row] = cnt;
+    int* out = knn_idx + (size_t)row * K;
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (q < cnt) out[q] = bi[q];
+  }
 }
 
 // set bits (i, j) and (j, i) for every kNN pair with j != i (graph_features.py:38-43)
@@ -219,16 +358,30 @@ struct GraphWs {
   int* knn_idx;
   int* knn_cnt;
   int* row_base;
+  int* row_frame;
   int* cnt;
+  FrameGrid* fg;
+  int* cell_cnt;
+  int* cell_start;
+  int* cursor;
+  int* cell_of;
+  float4* pts;
   void* scan_ws;
+  int cpf;
+  long n_cells;
 };
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
 
-static size_t graph_ws_layout(int n_nodes, int max_frame_nodes, int k, int mode, GraphWs* ws,
-                              char* base) {
+// grid cells per frame: room for ~3 points per cell at the largest frame
+static int cells_per_frame(int max_frame_nodes) { return max(16, max_frame_nodes / 2); }
+
+static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, int k, int mode,
+                              GraphWs* ws, char* base) {
   const int W = (max_frame_nodes + 31) / 32;
   const int K = mode == RG_GRAPH_RADIUS ? 1 : knn_list_len(k + 1);
+  const int cpf = cells_per_frame(max_frame_nodes);
+  const long n_cells = (long)n_frames * cpf;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* p = base ? base + off : nullptr;
@@ -239,31 +392,46 @@ static size_t graph_ws_layout(int n_nodes, int max_frame_nodes, int k, int mode,
   char* p_idx = take((size_t)n_nodes * (K > 0 ? K : 1) * sizeof(int));
   char* p_cnt = take((size_t)n_nodes * sizeof(int));
   char* p_rb = take((size_t)n_nodes * sizeof(int));
+  char* p_rf = take((size_t)n_nodes * sizeof(int));
   char* p_c2 = take((size_t)n_nodes * sizeof(int));
-  char* p_sc = take(scan_workspace_bytes(n_nodes));
+  char* p_fg = take((size_t)n_frames * sizeof(FrameGrid));
+  char* p_cc = take((size_t)n_cells * sizeof(int));
+  char* p_cs = take((size_t)(n_cells + 1) * sizeof(int));
+  char* p_cu = take((size_t)n_cells * sizeof(int));
+  char* p_co = take((size_t)n_nodes * sizeof(int));
+  char* p_pt = take((size_t)n_nodes * sizeof(float4));
+  char* p_sc = take(scan_workspace_bytes(max((long)n_nodes, n_cells)));
   if (ws) {
     ws->bits = (uint32_t*)p_bits;
     ws->knn_idx = (int*)p_idx;
     ws->knn_cnt = (int*)p_cnt;
     ws->row_base = (int*)p_rb;
+    ws->row_frame = (int*)p_rf;
     ws->cnt = (int*)p_c2;
+    ws->fg = (FrameGrid*)p_fg;
+    ws->cell_cnt = (int*)p_cc;
+    ws->cell_start = (int*)p_cs;
+    ws->cursor = (int*)p_cu;
+    ws->cell_of = (int*)p_co;
+    ws->pts = (float4*)p_pt;
     ws->scan_ws = p_sc;
+    ws->cpf = cpf;
+    ws->n_cells = n_cells;
   }
   return off;
 }
 
 extern "C" size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int max_frame_nodes,
                                                 int k, int mode) {
-  (void)n_frames;
-  return graph_ws_layout(n_nodes, max_frame_nodes, k, mode, nullptr, nullptr);
+  return graph_ws_layout(n_nodes, n_frames, max_frame_nodes, k, mode, nullptr, nullptr);
 }
 
 template <int K>
-static void launch_knn(dim3 grid, hipStream_t st, const float* px, const float* py,
-                       const int* frame_ptr, int kk, float eps2, int mode, GraphWs& ws,
-                       int* ball_degree, int W) {
-  knn_scan<K><<<grid, KNN_BLOCK, 0, st>>>(px, py, frame_ptr, kk, eps2, mode, ws.knn_idx,
-                                          ws.knn_cnt, ball_degree, ws.bits, W);
+static void launch_knn(hipStream_t st, const int* frame_ptr, int n_nodes, int kk, float eps2,
+                       int mode, GraphWs& ws, int* ball_degree, int W) {
+  knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
+      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, eps2, mode, ws.knn_idx,
+      ws.knn_cnt, ball_degree, ws.bits, W);
 }
 
 extern "C" int rg_build_graph(const float* px, const float* py, const int* frame_ptr, int n_nodes,
@@ -280,7 +448,8 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   const int K = mode == RG_GRAPH_RADIUS ? 1 : knn_list_len(kk);
   RG_REQUIRE(K > 0, RG_ERR_UNSUPPORTED, "rg_build_graph: k=%d > 63 unsupported", k);
   GraphWs ws;
-  size_t need = graph_ws_layout(n_nodes, max_frame_nodes, k, mode, &ws, (char*)workspace);
+  size_t need = graph_ws_layout(n_nodes, n_frames, max_frame_nodes, k, mode, &ws,
+                                (char*)workspace);
   RG_REQUIRE(workspace_bytes >= need, RG_ERR_ARG,
              "rg_build_graph: workspace %zu < required %zu", workspace_bytes, need);
   if (n_nodes == 0) {
@@ -291,21 +460,35 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   const int W = (max_frame_nodes + 31) / 32;
   RG_CHECK_HIP(hipMemsetAsync(ws.bits, 0, (size_t)n_nodes * W * sizeof(uint32_t), st));
   row_frame_base<<<ceil_div(n_nodes, 256), 256, 0, st>>>(frame_ptr, n_frames, ws.row_base,
-                                                         n_nodes);
-  dim3 grid(ceil_div(max_frame_nodes, KNN_BLOCK), n_frames);
+                                                         ws.row_frame, n_nodes);
+  // bucket every frame's points into its grid (cell order = frame order, so the scan of
+  // all cells gives absolute positions inside each frame's row range)
+  grid_setup<<<n_frames, 256, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
+  RG_CHECK_HIP(hipMemsetAsync(ws.cell_cnt, 0, (size_t)ws.n_cells * sizeof(int), st));
+  grid_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_frame, ws.fg, n_nodes,
+                                                     ws.cell_of, ws.cell_cnt);
+  RG_LAUNCH_CHECK();
+  int rc0 = exclusive_scan(ws.cell_cnt, ws.n_cells, ws.cell_start, ws.cell_start + ws.n_cells,
+                           ws.scan_ws, st);
+  if (rc0) return rc0;
+  RG_CHECK_HIP(hipMemcpyAsync(ws.cursor, ws.cell_start, (size_t)ws.n_cells * sizeof(int),
+                              hipMemcpyDeviceToDevice, st));
+  grid_scatter<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.cell_of, n_nodes,
+                                                       ws.cursor, ws.pts);
+  RG_LAUNCH_CHECK();
   switch (K) {
-    case 1: launch_knn<1>(grid, st, px, py, frame_ptr, 1, eps2, mode, ws, ball_degree, W); break;
-    case 2: launch_knn<2>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 4: launch_knn<4>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 8: launch_knn<8>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 11: launch_knn<11>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 16: launch_knn<16>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 17: launch_knn<17>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 24: launch_knn<24>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 32: launch_knn<32>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 33: launch_knn<33>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 48: launch_knn<48>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
-    case 64: launch_knn<64>(grid, st, px, py, frame_ptr, kk, eps2, mode, ws, ball_degree, W); break;
+    case 1: launch_knn<1>(st, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
+    case 2: launch_knn<2>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 4: launch_knn<4>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 8: launch_knn<8>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 11: launch_knn<11>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 16: launch_knn<16>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 17: launch_knn<17>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 24: launch_knn<24>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 32: launch_knn<32>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 33: launch_knn<33>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 48: launch_knn<48>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 64: launch_knn<64>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
     default: RG_REQUIRE(false, RG_ERR_UNSUPPORTED, "knn list %d", K);
   }
   RG_LAUNCH_CHECK();

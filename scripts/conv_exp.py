@@ -1,0 +1,37 @@
+"""Build the fused-conv timing experiments (RG_CONV_EXP variants) and, with --run, time
+each with bench.py (RG_LIBRARY=<variant>).  Results are wrong by construction; only
+kernels.conv_fused.avg_ms is read."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+EXPS = {'base': 0, 'nogather': 1, 'nonorm': 2, 'noagg': 3}
+
+
+def main():
+    from graph_neural_network_for_radar_perception_amd import build
+    if '--run' not in sys.argv:
+        for name, v in EXPS.items():
+            print(build.build_variant(f'conv_{name}', [f'RG_CONV_EXP={v}'], only=['conv_fused.hip']))
+        return
+    for name in EXPS:
+        lib = os.path.join(REPO, 'graph_neural_network_for_radar_perception_amd', 'lib', 'variants',
+                           f'libradargnn_conv_{name}.so')
+        env = dict(os.environ, RG_LIBRARY=lib)
+        r = subprocess.run([sys.executable, 'bench.py', '--steps', '5', '--warmup', '1',
+                            '--no-cpu-baseline'], cwd=REPO, env=env, capture_output=True,
+                           text=True, timeout=600)
+        line = [x for x in r.stdout.splitlines() if x.startswith('{')]
+        if r.returncode != 0 or not line:
+            print(name, 'FAILED', r.returncode, r.stderr[-2000:])
+            sys.exit(1)
+        d = json.loads(line[-1])
+        print(f"{name:10s} conv_fused {d['kernels']['conv_fused']['avg_ms']:.4f} ms  "
+              f"step {d['ms_per_step']:.3f} ms", flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,16 @@
+#!/bin/bash
+# SQ counters (issue / stall breakdown) of the bench kernels, two passes.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out/sq
+export TMPDIR=/tmp
+rocprofv3 -L > gpurun_out/sq/counters.txt 2>&1 || true
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS"
+P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES"
+i=0
+for P in "$P1" "$P2"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d gpurun_out/sq -o p$i \
+    -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/sq/bench_p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"; tail -2 gpurun_out/sq/bench_p$i.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -121,6 +121,50 @@ def test_duplicate_points(cuda_device):
     np.testing.assert_array_equal(got['degree'], want['degree'])
 
 
+def _layout(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    fr = synthetic.make_frame(n, seed)
+    if kind == 'blobs':      # dense clusters in an empty field (cell occupancy far from uniform)
+        c = rng.uniform([0, -50], [100, 50], size=(5, 2))
+        pts = c[rng.integers(0, 5, n)] + rng.normal(0, 0.3, size=(n, 2))
+    elif kind == 'same':     # every point identical: all distances tie at 0
+        pts = np.tile([[12.5, -3.25]], (n, 1))
+    elif kind == 'line':     # zero-height bounding box
+        pts = np.stack([rng.uniform(0, 100, n), np.full(n, 7.0)], 1)
+    elif kind == 'outlier':  # one far point stretches the grid
+        pts = rng.uniform([0, -5], [10, 5], size=(n, 2))
+        pts[n // 2] = [9000.0, -7000.0]
+    elif kind == 'lattice':  # integer lattice: exact distance ties everywhere
+        side = int(np.ceil(np.sqrt(n)))
+        g = np.stack(np.meshgrid(np.arange(side), np.arange(side)), -1).reshape(-1, 2)[:n]
+        pts = g.astype(np.float64) * 0.5
+    elif kind == 'offset':   # large coordinates, small spread (f32 cell rounding)
+        pts = np.array([1.0e4, -2.0e4]) + rng.uniform(0, 3, size=(n, 2))
+    else:
+        raise ValueError(kind)
+    fr['meas_px'] = pts[:, 0].astype(np.float32)
+    fr['meas_py'] = pts[:, 1].astype(np.float32)
+    return fr
+
+
+@pytest.mark.parametrize('kind', ['blobs', 'same', 'line', 'outlier', 'lattice', 'offset'])
+@pytest.mark.parametrize('k', [10, 32])
+def test_knn_adversarial_layouts(cuda_device, kind, k):
+    """Grid ring search == dense argsort oracle on layouts that stress the cell grid
+    (kNN set, ties by lower index, ball-query degree, knn | radius union)."""
+    from graph_neural_network_for_radar_perception_amd import graph_features as gf
+    fr = _layout(kind, 700, 4242 + k)
+    got = gf.compute_adjacency_information(fr, 25.0, k)
+    want = gref.compute_adjacency_information(fr, 25.0, k)
+    np.testing.assert_array_equal(got['adj_list'], want['adj_list'])
+    np.testing.assert_array_equal(got['degree'], want['degree'])
+    got2 = gf.compute_adjacency_information_v2(fr, 4.0, k)
+    dm = gref.pairwise_sq_distance(fr['meas_px'], fr['meas_py'])
+    want2 = np.stack(np.where(gref.compute_ball_query(dm, 4.0) | gref.compute_knn(dm, k)), 0)
+    np.testing.assert_array_equal(got2['adj_list'], want2)
+
+
 def test_batched_graph_build_equals_per_frame(cuda_device):
     """Disjoint-union batch (frames of different sizes) == frame-by-frame oracle."""
     from graph_neural_network_for_radar_perception_amd import graph_features as gf
