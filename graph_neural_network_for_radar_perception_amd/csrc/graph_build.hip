@@ -5,10 +5,12 @@
 // np.where edge list become
 //   0. grid_setup / grid_count / scan / grid_scatter: per frame, points bucketed
 //                   into a uniform grid of ~3-point cells (cell-ordered copy);
-//   1. knn_grid   : one thread per point, Chebyshev ring search over the cells,
-//                   exact fp32 distances (no FMA), top-(k+1) by (distance, index)
-//                   kept sorted in registers, ball-query count, optional radius bits,
-//                   stopping once no unvisited cell can change the result;
+//   1. knn_select : one thread per point, Chebyshev ring search over the cells,
+//                   exact fp32 distances (no FMA), counting selection of the top-(k+1)
+//                   (distance, index) keys through a per-row LDS histogram, ball-query
+//                   count, optional radius bits, stopping once no unvisited cell can
+//                   change the result (knn_grid: exact sorted-insert variant for rows
+//                   with massive distance ties);
 //   2. knn_mark   : kNN pairs set in a per-row bitset both ways (atomicOr);
 //   3. row_count  : one wave per row, popcount of the bitset row;
 //   4. exclusive scan -> CSR row_ptr;
@@ -166,17 +168,64 @@ __device__ __forceinline__ bool key_less(float d, int j, float bd, int bj) {
   return d < bd || (d == bd && j < bj);
 }
 
-// One thread per point in cell order (a wave = spatially adjacent rows, so the cells it
-// visits are shared through L1).  K = list length kept per row (>= kk = k + 1).
+// Visit the points of the cells at Chebyshev distance exactly r from (cx, cy): grid
+// rows cy-r and cy+r in full, then columns cx-r and cx+r strictly between them.
+template <typename F>
+__device__ __forceinline__ void for_ring(const FrameGrid& g, const int* __restrict__ cell_start,
+                                         const float4* __restrict__ pts, int cx, int cy, int r,
+                                         F&& body) {
+  for (int side = 0; side < 4; ++side) {
+    int ya, yb, xa, xb;
+    if (side < 2) {
+      const int yy = side == 0 ? cy - r : cy + r;
+      if (yy < 0 || yy >= g.gh || (side == 1 && r == 0)) continue;
+      ya = yb = yy;
+      xa = max(cx - r, 0);
+      xb = min(cx + r, g.gw - 1);
+    } else {
+      if (r == 0) continue;
+      const int xx = side == 2 ? cx - r : cx + r;
+      if (xx < 0 || xx >= g.gw) continue;
+      xa = xb = xx;
+      ya = max(cy - r + 1, 0);
+      yb = min(cy + r - 1, g.gh - 1);
+    }
+    for (int yy = ya; yy <= yb; ++yy) {
+      // cells xa..xb of one grid row are contiguous in the cell order
+      const int c = g.cell0 + yy * g.gw;
+      const int p0 = cell_start[c + xa], p1 = cell_start[c + xb + 1];
+      // four candidate loads in flight per lane before any is consumed
+      for (int p = p0; p < p1; p += 4) {
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = pts[min(p + u, p1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (p + u < p1) body(q[u]);
+      }
+    }
+  }
+}
+
+// lower bound (squared, f32-safe) on the distance of every point beyond ring r
+__device__ __forceinline__ float ring_bound(const FrameGrid& g, int r) {
+  const float lb = fmaxf((float)r - 0.01f, 0.f) * g.s;
+  return lb * lb * (1.f - 1e-5f);
+}
+
+// Exact sorted-insert search: one thread per point in cell order (a wave = spatially
+// adjacent rows, so the cells it visits are shared through L1), K = list length kept
+// per row (>= kk = k + 1).  Used for the rows knn_select flags (massive exact ties).
 template <int K>
 __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
     const float4* __restrict__ pts, const int* __restrict__ cell_start,
     const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
     const int* __restrict__ frame_ptr, int n_nodes, int kk, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
-    uint32_t* __restrict__ bits, int W) {
+    uint32_t* __restrict__ bits, int W, const int* __restrict__ only) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_nodes) return;
+  if (only && !only[t]) return;  // fallback pass: just the rows knn_select flagged
   const int f = row_frame[t];  // the cell-ordered points of frame f fill its row range
   const FrameGrid g = fg[f];
   const int base = frame_ptr[f];
@@ -200,55 +249,28 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
   const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
   bool knn_done = !want_knn, ball_done = false;
   for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
-    // cells at Chebyshev distance exactly r: rows cy-r and cy+r in full, then the
-    // columns cx-r and cx+r strictly between them
-    for (int side = 0; side < 4; ++side) {
-      int ya, yb, xa, xb;
-      if (side < 2) {
-        const int yy = side == 0 ? cy - r : cy + r;
-        if (yy < 0 || yy >= g.gh || (side == 1 && r == 0)) continue;
-        ya = yb = yy;
-        xa = max(cx - r, 0);
-        xb = min(cx + r, g.gw - 1);
-      } else {
-        if (r == 0) continue;
-        const int xx = side == 2 ? cx - r : cx + r;
-        if (xx < 0 || xx >= g.gw) continue;
-        xa = xb = xx;
-        ya = max(cy - r + 1, 0);
-        yb = min(cy + r - 1, g.gh - 1);
-      }
-      for (int yy = ya; yy <= yb; ++yy) {
-        // cells xa..xb of one grid row are contiguous in the cell order
-        const int c = g.cell0 + yy * g.gw;
-        const int p0 = cell_start[c + xa], p1 = cell_start[c + xb + 1];
-        for (int p = p0; p < p1; ++p) {
-          const float4 q = pts[p];
-          const int j = __float_as_int(q.z);
-          const float d = sqdist(xi, yi, q.x, q.y);
-          const bool inball = (d <= eps2) && (j != il);
-          ball += inball ? 1 : 0;
-          if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
-          if (want_knn && key_less(d, j, bd[K - 1], bi[K - 1])) {
-            // sorted insert by (d, j): branch-free pass from the tail
+    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+      const int j = __float_as_int(q.z);
+      const float d = sqdist(xi, yi, q.x, q.y);
+      const bool inball = (d <= eps2) && (j != il);
+      ball += inball ? 1 : 0;
+      if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
+      if (want_knn && key_less(d, j, bd[K - 1], bi[K - 1])) {
+        // sorted insert by (d, j): branch-free pass from the tail
 #pragma unroll
-            for (int s2 = K - 1; s2 > 0; --s2) {
-              const bool shift = key_less(d, j, bd[s2 - 1], bi[s2 - 1]);
-              const bool here = !shift && key_less(d, j, bd[s2], bi[s2]);
-              bd[s2] = shift ? bd[s2 - 1] : (here ? d : bd[s2]);
-              bi[s2] = shift ? bi[s2 - 1] : (here ? j : bi[s2]);
-            }
-            if (key_less(d, j, bd[0], bi[0])) {
-              bd[0] = d;
-              bi[0] = j;
-            }
-          }
+        for (int s2 = K - 1; s2 > 0; --s2) {
+          const bool shift = key_less(d, j, bd[s2 - 1], bi[s2 - 1]);
+          const bool here = !shift && key_less(d, j, bd[s2], bi[s2]);
+          bd[s2] = shift ? bd[s2 - 1] : (here ? d : bd[s2]);
+          bi[s2] = shift ? bi[s2 - 1] : (here ? j : bi[s2]);
+        }
+        if (key_less(d, j, bd[0], bi[0])) {
+          bd[0] = d;
+          bi[0] = j;
         }
       }
-    }
-    // every point beyond ring r is at least (r - 0.01) s away
-    const float lb = fmaxf((float)r - 0.01f, 0.f) * g.s;
-    const float bound = lb * lb * (1.f - 1e-5f);
+    });
+    const float bound = ring_bound(g, r);
     if (eps2 < bound) ball_done = true;
     if (!knn_done) {
       float dk = bd[0];  // the kk-th key so far (+inf while fewer are held)
@@ -267,6 +289,144 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
     for (int q = 0; q < K; ++q)
       if (q < cnt) out[q] = bi[q];
   }
+}
+
+static constexpr int HB = 64;     // distance histogram bins per row (4 per octave of d)
+static constexpr int HSHIFT = 21; // d's bits >> 21 = exponent + 2 mantissa bits
+static constexpr int BBUF = 32;   // boundary-bin candidates a row may buffer
+
+// Counting selection of the k+1 nearest (distance, index) keys -- the same set the
+// sorted-insert search (knn_grid) and the reference's argsort pick:
+//   pass 1: rings are visited until the (k+1)-th key is provably inside; each candidate
+//           only bumps a per-row LDS histogram of its squared distance (bins are the
+//           exponent + 2 mantissa bits of d, monotone in d), so the bin b* holding the
+//           (k+1)-th key and the count below it follow from a prefix over 64 counters;
+//   pass 2: the same rings again: keys in bins < b* are selected outright, keys in b*
+//           go to a per-row LDS buffer from which the missing few are picked exactly.
+// Per candidate that is ~10 instructions instead of a k-long register insert, which
+// under SIMT divergence ran for almost every candidate of the wave.  A row whose
+// boundary bin holds more than BBUF keys (massive exact ties: duplicates, lattices)
+// is flagged and redone by knn_grid.  Ball-query degree and radius bits are produced
+// here for every row.
+__global__ __launch_bounds__(KNN_BLOCK) void knn_select(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, int kk, int K, float eps2, int mode,
+    int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
+    uint32_t* __restrict__ bits, int W, int* __restrict__ redo) {
+  __shared__ uint32_t lds[KNN_BLOCK / 64][HB * 64];  // per wave: [bin][lane]
+  const int lane = threadIdx.x & 63;
+  uint32_t* H = lds[threadIdx.x >> 6] + lane;  // this row's column (stride 64 words)
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_nodes) return;  // no block barriers below: rows own disjoint LDS columns
+  const int f = row_frame[t];  // the cell-ordered points of frame f fill its row range
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const float xi = me.x, yi = me.y;
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
+  const bool want_knn = mode != RG_GRAPH_RADIUS;
+  const bool want_rad = mode != RG_GRAPH_KNN;
+  const int row = base + il;
+  uint32_t* rowbits = bits + (size_t)row * W;
+  // bins: d's exponent + 2 mantissa bits, 16 octaves centred on the cell area s^2
+  const int bin0 = (int)(__float_as_uint(g.s * g.s) >> HSHIFT) - HB / 2;
+  auto bin_of = [&](float d) {
+    const int b = (int)(__float_as_uint(d) >> HSHIFT) - bin0;
+    return b < 0 ? 0 : (b >= HB ? HB - 1 : b);
+  };
+  if (want_knn) {
+#pragma unroll
+    for (int b = 0; b < HB; ++b) H[b * 64] = 0u;
+  }
+  const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
+  int ball = 0, total = 0, r_knn = rmax;
+  bool knn_done = !want_knn, ball_done = false;
+  for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
+    const bool count_knn = !knn_done;
+    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+      const int j = __float_as_int(q.z);
+      const float d = sqdist(xi, yi, q.x, q.y);
+      if (!ball_done) {
+        const bool inball = (d <= eps2) && (j != il);
+        ball += inball ? 1 : 0;
+        if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
+      }
+      if (count_knn) {
+        atomicAdd(H + bin_of(d) * 64, 1u);  // ds_add_u32: the row owns the column
+        ++total;
+      }
+    });
+    const float bound = ring_bound(g, r);
+    if (eps2 < bound) ball_done = true;
+    if (count_knn && total >= kk) {
+      // upper edge of the bin holding the kk-th key bounds the kk-th distance
+      int cum = 0, bs = HB - 1;
+      for (int b = 0; b < HB; ++b) {
+        cum += (int)H[b * 64];
+        if (cum >= kk) { bs = b; break; }
+      }
+      const int ub_bits = bin0 + bs + 1;
+      const float ub = bs == HB - 1 ? __int_as_float(0x7f800000)
+                                    : (ub_bits <= 0 ? 0.f : __uint_as_float((uint32_t)ub_bits << HSHIFT));
+      if (ub <= bound) {
+        knn_done = true;
+        r_knn = r;
+      }
+    }
+  }
+  ball_deg[row] = ball;
+  if (!want_knn) return;
+  // ---- selection: bins below b* entirely, the rest of the kk from bin b* exactly
+  int bs = HB, below = total, in_bs = 0;  // total <= kk: every visited key is selected
+  if (total > kk) {
+    int cum = 0;
+    for (int b = 0; b < HB; ++b) {
+      const int c = (int)H[b * 64];
+      if (cum + c >= kk) { bs = b; below = cum; in_bs = c; break; }
+      cum += c;
+    }
+  }
+  const int cnt = min(kk, total);
+  const int need = cnt - below;
+  if (in_bs > BBUF) {  // massive ties in the boundary bin: exact insert path
+    redo[t] = 1;
+    return;
+  }
+  float* Bd = (float*)H;            // buffer reuses the histogram column:
+  uint32_t* Bj = H + BBUF * 64;     // entries [e][lane], e < BBUF
+  int* out = knn_idx + (size_t)row * K;
+  int n_out = 0, nb = 0;
+  for (int r = 0; r <= r_knn; ++r) {
+    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+      const int j = __float_as_int(q.z);
+      const float d = sqdist(xi, yi, q.x, q.y);
+      const int b = bin_of(d);
+      if (b < bs) {
+        out[n_out++] = j;
+      } else if (b == bs) {
+        Bd[nb * 64] = d;
+        Bj[nb * 64] = (uint32_t)j;
+        ++nb;
+      }
+    });
+  }
+  for (int q = 0; q < need; ++q) {  // need smallest (d, j) of the boundary bin
+    int best = 0;
+    float bd = Bd[0];
+    int bj = (int)Bj[0];
+    for (int e = 1; e < nb; ++e) {
+      const float d = Bd[e * 64];
+      const int j = (int)Bj[e * 64];
+      if (key_less(d, j, bd, bj)) { bd = d; bj = j; best = e; }
+    }
+    out[n_out++] = bj;
+    Bd[best * 64] = __int_as_float(0x7f800000);
+    Bj[best * 64] = 0x7fffffffu;
+  }
+  knn_cnt[row] = cnt;
 }
 
 // set bits (i, j) and (j, i) for every kNN pair with j != i (graph_features.py:38-43)
@@ -366,6 +526,7 @@ struct GraphWs {
   int* cursor;
   int* cell_of;
   float4* pts;
+  int* redo;
   void* scan_ws;
   int cpf;
   long n_cells;
@@ -400,6 +561,7 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
   char* p_cu = take((size_t)n_cells * sizeof(int));
   char* p_co = take((size_t)n_nodes * sizeof(int));
   char* p_pt = take((size_t)n_nodes * sizeof(float4));
+  char* p_rd = take((size_t)n_nodes * sizeof(int));
   char* p_sc = take(scan_workspace_bytes(max((long)n_nodes, n_cells)));
   if (ws) {
     ws->bits = (uint32_t*)p_bits;
@@ -414,6 +576,7 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
     ws->cursor = (int*)p_cu;
     ws->cell_of = (int*)p_co;
     ws->pts = (float4*)p_pt;
+    ws->redo = (int*)p_rd;
     ws->scan_ws = p_sc;
     ws->cpf = cpf;
     ws->n_cells = n_cells;
@@ -426,12 +589,18 @@ extern "C" size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int m
   return graph_ws_layout(n_nodes, n_frames, max_frame_nodes, k, mode, nullptr, nullptr);
 }
 
+// counting selection for every row, then the exact sorted-insert search for the rows
+// it flagged (their outputs are rewritten identically)
 template <int K>
 static void launch_knn(hipStream_t st, const int* frame_ptr, int n_nodes, int kk, float eps2,
                        int mode, GraphWs& ws, int* ball_degree, int W) {
+  knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
+      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, K, eps2, mode,
+      ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo);
+  if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
       ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, eps2, mode, ws.knn_idx,
-      ws.knn_cnt, ball_degree, ws.bits, W);
+      ws.knn_cnt, ball_degree, ws.bits, W, ws.redo);
 }
 
 extern "C" int rg_build_graph(const float* px, const float* py, const int* frame_ptr, int n_nodes,
@@ -476,6 +645,7 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   grid_scatter<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.cell_of, n_nodes,
                                                        ws.cursor, ws.pts);
   RG_LAUNCH_CHECK();
+  RG_CHECK_HIP(hipMemsetAsync(ws.redo, 0, (size_t)n_nodes * sizeof(int), st));
   switch (K) {
     case 1: launch_knn<1>(st, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
     case 2: launch_knn<2>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
