@@ -27,8 +27,10 @@ namespace fast {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-static constexpr int FT = 512;  // 8 waves per workgroup (2 per SIMD)
-static constexpr int FW = FT / 64;
+// Workgroup size is per shape: 512 threads (2 waves per SIMD) for register-heavy
+// chains, 768 / 1024 (3 / 4 per SIMD) where the chain fits 170 / 128 VGPRs -- one
+// workgroup per CU shares one LDS copy of the weights, so more waves per workgroup is
+// the only way to more latency hiding.
 static constexpr float NORM_EPS = 1e-5f;
 static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layers 0+1
 
@@ -374,8 +376,9 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int ACT, int... Ns>
+template <int MODE, bool IN_F32, int W0, int W1, int ACT, int FT, int... Ns>
 __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
+  constexpr int FW = FT / 64;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
   // stage all layers' packed weights + biases (static layer indices: no scratch copy)
@@ -404,14 +407,15 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int ACT, int... Ns>
+template <int MODE, bool IN_F32, int W0, int W1, int ACT, int FT, int... Ns>
 static int launch(const FArgs& a, hipStream_t st) {
+  constexpr int FW = FT / 64;
   using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
   // the host-side LDS image must be the layout the kernel assumes
   using Off = Offsets<In::K0, Ns...>;
   for (int l = 0; l < a.nl; ++l)
     RG_REQUIRE(a.L[l].woff == Off::get(l), RG_ERR_ARG, "rg_mlp_chain_fast: LDS layout of layer %d", l);
-  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, ACT, Ns...>;
+  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, ACT, FT, Ns...>;
   static bool attr = false;
   if (!attr) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -420,7 +424,7 @@ static int launch(const FArgs& a, hipStream_t st) {
   }
   const long tiles = (a.rows + 31) / 32;
   long blocks = (tiles + FW - 1) / FW;
-  const int per_cu = a.total_bytes <= 76 * 1024 ? 2 : 1;
+  const int per_cu = (FT == 512 && a.total_bytes <= 76 * 1024) ? 2 : 1;
   if (blocks > 256L * per_cu) blocks = 256L * per_cu;
   if (blocks < 1) blocks = 1;
   kern<<<blocks, FT, a.total_bytes, st>>>(a);
@@ -447,22 +451,22 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
 
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
 static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
-#define RG_FAST(MODE, F32, W0, W1, ...)                                              \
-  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                   \
-    return k.act == ACT_LEAKY ? launch<MODE, F32, W0, W1, ACT_LEAKY, __VA_ARGS__>(a, st) \
-                              : launch<MODE, F32, W0, W1, -1, __VA_ARGS__>(a, st);
+#define RG_FAST(FT, MODE, F32, W0, W1, ...)                                               \
+  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                        \
+    return k.act == ACT_LEAKY ? launch<MODE, F32, W0, W1, ACT_LEAKY, FT, __VA_ARGS__>(a, st) \
+                              : launch<MODE, F32, W0, W1, -1, FT, __VA_ARGS__>(a, st);
   // node / edge encoders (graph_feature_encoding, yml:56-57)
-  RG_FAST(RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
-  RG_FAST(RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
+  RG_FAST(768, RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
+  RG_FAST(768, RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
-  RG_FAST(RG_IN_GATHER3, 0, 64, 64, 128, 64)
-  RG_FAST(RG_IN_CONCAT2, 0, 64, 64, 64)
+  RG_FAST(512, RG_IN_GATHER3, 0, 64, 64, 128, 64)
+  RG_FAST(1024, RG_IN_CONCAT2, 0, 64, 64, 64)
   // heads: 3-block stems + FFN_TaskSpecificHead (ffn + Linear -> 7 / 2)
-  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 64, 64, 64, 32)
-  RG_FAST(RG_IN_PAIRADD, 0, 64, 0, 64, 64, 64, 64, 32)
-  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64)
-  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
-  RG_FAST(RG_IN_DENSE, 0, 64, 0, 64, 32)
+  RG_FAST(1024, RG_IN_DENSE, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(1024, RG_IN_PAIRADD, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(768, RG_IN_DENSE, 0, 64, 0, 64)
+  RG_FAST(768, RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
+  RG_FAST(1024, RG_IN_DENSE, 0, 64, 0, 64, 32)
 #undef RG_FAST
   return RG_ERR_UNSUPPORTED;
 }

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
       const float d = sqdist(xi, yi, q.x, q.y);
       const bool inball = (d <= eps2) && (j != il);
       ball += inball ? 1 : 0;
-      if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
+      if (want_rad && inball) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
       if (want_knn && key_less(d, j, bd[K - 1], bi[K - 1])) {
         // sorted insert by (d, j): branch-free pass from the tail
 #pragma unroll
@@ -287,13 +287,16 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
     int* out = knn_idx + (size_t)row * K;
 #pragma unroll
     for (int q = 0; q < K; ++q)
-      if (q < cnt) out[q] = bi[q];
+      if (q < cnt) {
+        out[q] = bi[q];
+        if (bi[q] != il) atomicOr(rowbits + (bi[q] >> 5), 1u << (bi[q] & 31));
+      }
   }
 }
 
 static constexpr int HB = 64;     // distance histogram bins per row (4 per octave of d)
 static constexpr int HSHIFT = 21; // d's bits >> 21 = exponent + 2 mantissa bits
-static constexpr int BBUF = 32;   // boundary-bin candidates a row may buffer
+static constexpr int BBUF = 64;   // boundary-bin candidates a row may buffer (indices)
 
 // Counting selection of the k+1 nearest (distance, index) keys -- the same set the
 // sorted-insert search (knn_grid) and the reference's argsort pick:
@@ -302,7 +305,8 @@ static constexpr int BBUF = 32;   // boundary-bin candidates a row may buffer
 //           exponent + 2 mantissa bits of d, monotone in d), so the bin b* holding the
 //           (k+1)-th key and the count below it follow from a prefix over 64 counters;
 //   pass 2: the same rings again: keys in bins < b* are selected outright, keys in b*
-//           go to a per-row LDS buffer from which the missing few are picked exactly.
+//           go to a per-row LDS buffer (indices) from which the missing few are picked
+//           exactly, ordered by (d, j) with d recomputed bit-identically.
 // Per candidate that is ~10 instructions instead of a k-long register insert, which
 // under SIMT divergence ran for almost every candidate of the wave.  A row whose
 // boundary bin holds more than BBUF keys (massive exact ties: duplicates, lattices)
@@ -311,7 +315,8 @@ static constexpr int BBUF = 32;   // boundary-bin candidates a row may buffer
 __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     const float4* __restrict__ pts, const int* __restrict__ cell_start,
     const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
-    const int* __restrict__ frame_ptr, int n_nodes, int kk, int K, float eps2, int mode,
+    const int* __restrict__ frame_ptr, const float* __restrict__ px,
+    const float* __restrict__ py, int n_nodes, int kk, int K, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
     uint32_t* __restrict__ bits, int W, int* __restrict__ redo) {
   __shared__ uint32_t lds[KNN_BLOCK / 64][HB * 64];  // per wave: [bin][lane]
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
       if (!ball_done) {
         const bool inball = (d <= eps2) && (j != il);
         ball += inball ? 1 : 0;
-        if (want_rad && inball) rowbits[j >> 5] |= 1u << (j & 31);
+        if (want_rad && inball) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
       }
       if (count_knn) {
         atomicAdd(H + bin_of(d) * 64, 1u);  // ds_add_u32: the row owns the column
@@ -395,8 +400,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     redo[t] = 1;
     return;
   }
-  float* Bd = (float*)H;            // buffer reuses the histogram column:
-  uint32_t* Bj = H + BBUF * 64;     // entries [e][lane], e < BBUF
+  uint32_t* Bj = H;  // boundary-bin indices reuse the histogram column: [e][lane], e < BBUF
   int* out = knn_idx + (size_t)row * K;
   int n_out = 0, nb = 0;
   for (int r = 0; r <= r_knn; ++r) {
@@ -406,33 +410,41 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
       const int b = bin_of(d);
       if (b < bs) {
         out[n_out++] = j;
+        if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));  // fire-and-forget
       } else if (b == bs) {
-        Bd[nb * 64] = d;
         Bj[nb * 64] = (uint32_t)j;
         ++nb;
       }
     });
   }
-  for (int q = 0; q < need; ++q) {  // need smallest (d, j) of the boundary bin
-    int best = 0;
-    float bd = Bd[0];
-    int bj = (int)Bj[0];
-    for (int e = 1; e < nb; ++e) {
-      const float d = Bd[e * 64];
+  // the need smallest (d, j) of the boundary bin (d recomputed bit-identically)
+  const float* fx = px + base;
+  const float* fy = py + base;
+  int last_j = -1;
+  float last_d = -1.f;
+  for (int q = 0; q < need; ++q) {
+    float bd = __int_as_float(0x7f800000);
+    int bj = 0x7fffffff;
+    for (int e = 0; e < nb; ++e) {
       const int j = (int)Bj[e * 64];
-      if (key_less(d, j, bd, bj)) { bd = d; bj = j; best = e; }
+      const float d = sqdist(xi, yi, fx[j], fy[j]);
+      // next key strictly after the previous pick
+      if (key_less(last_d, last_j, d, j) && key_less(d, j, bd, bj)) { bd = d; bj = j; }
     }
     out[n_out++] = bj;
-    Bd[best * 64] = __int_as_float(0x7f800000);
-    Bj[best * 64] = 0x7fffffffu;
+    if (bj != il) atomicOr(rowbits + (bj >> 5), 1u << (bj & 31));
+    last_d = bd;
+    last_j = bj;
   }
   knn_cnt[row] = cnt;
 }
 
-// set bits (i, j) and (j, i) for every kNN pair with j != i (graph_features.py:38-43)
+// the transposed half of knn | knn^T (graph_features.py:38-43): bit (j, i) for every
+// kNN pair (i, j); bit (i, j) was set by the row's own search.  Mutual neighbours are
+// common, so the word is read first and only a missing bit costs an atomic.
 __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict__ knn_idx,
-                          const int* __restrict__ knn_cnt, int K, int n_nodes,
-                          uint32_t* __restrict__ bits, int W) {
+                         const int* __restrict__ knn_cnt, int K, int n_nodes,
+                         uint32_t* __restrict__ bits, int W) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int i = (int)(t / K);
   const int s = (int)(t % K);
@@ -442,8 +454,9 @@ __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict
   const int il = i - b;
   const int jl = knn_idx[(size_t)i * K + s];
   if (jl == il || jl < 0) return;
-  atomicOr(bits + (size_t)i * W + (jl >> 5), 1u << (jl & 31));
-  atomicOr(bits + (size_t)(b + jl) * W + (il >> 5), 1u << (il & 31));
+  uint32_t* w = bits + (size_t)(b + jl) * W + (il >> 5);
+  const uint32_t m = 1u << (il & 31);
+  if (!(*w & m)) atomicOr(w, m);  // bits are only ever set: a set bit read is final
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -592,10 +605,11 @@ extern "C" size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int m
 // counting selection for every row, then the exact sorted-insert search for the rows
 // it flagged (their outputs are rewritten identically)
 template <int K>
-static void launch_knn(hipStream_t st, const int* frame_ptr, int n_nodes, int kk, float eps2,
-                       int mode, GraphWs& ws, int* ball_degree, int W) {
+static void launch_knn(hipStream_t st, const float* px, const float* py, const int* frame_ptr,
+                       int n_nodes, int kk, float eps2, int mode, GraphWs& ws, int* ball_degree,
+                       int W) {
   knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
-      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, K, eps2, mode,
+      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, px, py, n_nodes, kk, K, eps2, mode,
       ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo);
   if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
@@ -647,18 +661,18 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   RG_LAUNCH_CHECK();
   RG_CHECK_HIP(hipMemsetAsync(ws.redo, 0, (size_t)n_nodes * sizeof(int), st));
   switch (K) {
-    case 1: launch_knn<1>(st, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
-    case 2: launch_knn<2>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 4: launch_knn<4>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 8: launch_knn<8>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 11: launch_knn<11>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 16: launch_knn<16>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 17: launch_knn<17>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 24: launch_knn<24>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 32: launch_knn<32>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 33: launch_knn<33>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 48: launch_knn<48>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 64: launch_knn<64>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 1: launch_knn<1>(st, px, py, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
+    case 2: launch_knn<2>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 4: launch_knn<4>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 8: launch_knn<8>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 11: launch_knn<11>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 16: launch_knn<16>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 17: launch_knn<17>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 24: launch_knn<24>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 32: launch_knn<32>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 33: launch_knn<33>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 48: launch_knn<48>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 64: launch_knn<64>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
     default: RG_REQUIRE(false, RG_ERR_UNSUPPORTED, "knn list %d", K);
   }
   RG_LAUNCH_CHECK();
