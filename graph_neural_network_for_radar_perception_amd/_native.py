@@ -23,6 +23,8 @@ HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 
 RG_F32, RG_BF16 = 0, 1
 RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD = 2, 3, 4
+RG_PACK_CENTERED = 0x100
+RG_LAYER_CENTERED = 1
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
 GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2
@@ -38,7 +40,7 @@ class NativeLibraryError(RuntimeError):
 class rg_layer(ctypes.Structure):
     _fields_ = [('w_packed', ctypes.c_void_p), ('norm_mu', ctypes.c_void_p),
                 ('norm_std', ctypes.c_void_p), ('in_dim', ctypes.c_int),
-                ('out_dim', ctypes.c_int), ('act', ctypes.c_int), ('pad_', ctypes.c_int)]
+                ('out_dim', ctypes.c_int), ('act', ctypes.c_int), ('flags', ctypes.c_int)]
 
 
 _P = ctypes.c_void_p

@@ -42,6 +42,7 @@ struct FLayer {
   int bytes;  // packed bytes
   int out;    // real output width
   int act;
+  int centered;  // RG_LAYER_CENTERED
 };
 
 struct FArgs {
@@ -159,14 +160,7 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
   const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 bv = *(const f32x4*)(bias + 32 * m + 8 * g + 4 * h);
-      acc[m][4 * g + 0] = bv.x;
-      acc[m][4 * g + 1] = bv.y;
-      acc[m][4 * g + 2] = bv.z;
-      acc[m][4 * g + 3] = bv.w;
-    }
+    acc[m] = ld_bias_frag(bias, m, h);  // accumulator-order bias: 4 x ds_read_b128
   }
   // software pipeline: the A fragments of k-step s+1 are read from LDS while the
   // MFMAs of step s issue; a scheduling fence per step keeps the compiler from
@@ -213,9 +207,23 @@ template <int K, int N, int... Rest> struct Offsets<K, N, Rest...> {
 // packed as zeros, so they are exactly 0 before normalisation (normalised layers are
 // never padded, checked on the host) and act(0) = 0; only the LAST layer may be padded
 // and store_out never writes those columns.
-template <int ACT, int MT>
+//
+// SPEC >= 0 fixes the chain's epilogues at compile time: bits 0-7 the hidden activation,
+// bit 8 + l = layer l is normalised (and packed RG_PACK_CENTERED), bit 16 + l = layer l
+// applies the activation (else identity) -- checked against the layer descriptors on
+// the host.  SPEC < 0: the descriptors decide at run time.
+constexpr int spec(int act, int norm_mask, int act_mask) {
+  return act | (norm_mask << 8) | (act_mask << 16);
+}
+template <int SPEC, int LI, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L) {
-  norm_act_rows<ACT, MT>(acc, L.mu, L.sd, L.act, NORM_EPS);
+  if constexpr (SPEC >= 0) {
+    if constexpr (((SPEC >> (8 + LI)) & 1) != 0)  // normalised => centred (host-checked)
+      channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+    if constexpr (((SPEC >> (16 + LI)) & 1) != 0) act_pk_all<(SPEC & 0xff), MT>(acc);
+  } else {
+    norm_act_rows<-1, MT>(acc, L.mu, L.sd, L.act, NORM_EPS, L.centered != 0);
+  }
 }
 
 template <int MT>
@@ -282,7 +290,7 @@ __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& 
     }
 }
 
-template <int ACT, int OFF, int LI, int K, int N, int... Rest>
+template <int SPEC, int OFF, int LI, int K, int N, int... Rest>
 __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K + 15) / 16],
                                           const char* lds, long row, bool valid, int lane) {
   constexpr int KS = (K + 15) / 16;
@@ -290,11 +298,11 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
   static_assert(N % 32 == 0, "padded widths are multiples of 32");
   f32x16 acc[MT];
   mfma_layer<KS, MT>(b, acc, lds + OFF, lane);
-  epilogue<ACT, MT>(acc, a.L[LI]);
+  epilogue<SPEC, LI, MT>(acc, a.L[LI]);
   if constexpr (sizeof...(Rest) > 0) {
     bf16x8_t nb[2 * MT];
     pack_next<MT>(acc, nb);
-    run_chain<ACT, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, row,
+    run_chain<SPEC, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, row,
                                                                              valid, lane);
   } else {
     if (valid) store_out<MT>(acc, a, row, lane >> 5);
@@ -306,7 +314,7 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
 // activated, packed to bf16 and consumed at once as layer 1's k-steps 2m0, 2m0+1, so
 // layer 0's N0-wide activation never exists in full (the 7 -> 256 edge encoder would
 // otherwise hold 128 accumulators + 64 packed registers and spill).
-template <int ACT, int K0, int N0, int N1, int... Rest>
+template <int SPEC, int K0, int N0, int N1, int... Rest>
 __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[(K0 + 15) / 16],
                                             const char* lds, long row, bool valid, int lane) {
   constexpr int KS0 = (K0 + 15) / 16, MT0 = N0 / 32, KS1 = N0 / 16, MT1 = N1 / 32;
@@ -321,26 +329,12 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
   f32x16 acc[MT1];
 #pragma unroll
   for (int m = 0; m < MT1; ++m)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 bv = *(const f32x4*)(bias1 + 32 * m + 8 * g + 4 * h);
-      acc[m][4 * g + 0] = bv.x;
-      acc[m][4 * g + 1] = bv.y;
-      acc[m][4 * g + 2] = bv.z;
-      acc[m][4 * g + 3] = bv.w;
-    }
+    acc[m] = ld_bias_frag(bias1, m, h);  // accumulator-order bias: 4 x ds_read_b128
   auto body = [&](auto A) {
 #pragma unroll
     for (int m0 = 0; m0 < MT0; ++m0) {
       f32x16 t;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 bv = *(const f32x4*)(bias0 + 32 * m0 + 8 * g + 4 * h);
-        t[4 * g + 0] = bv.x;
-        t[4 * g + 1] = bv.y;
-        t[4 * g + 2] = bv.z;
-        t[4 * g + 3] = bv.w;
-      }
+      t = ld_bias_frag(bias0, m0, h);  // accumulator-order bias: 4 x ds_read_b128
 #pragma unroll
       for (int s = 0; s < KS0; ++s)
         t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -364,19 +358,23 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
       __builtin_amdgcn_sched_barrier(0);  // one layer-0 tile in flight: bounded registers
     }
   };
-  if constexpr (ACT >= 0) body(std::integral_constant<int, ACT>{});  // layer 0 act == ACT (host)
-  else act_dispatch(a.L[0].act, body);
-  epilogue<ACT, MT1>(acc, a.L[1]);
+  if constexpr (SPEC >= 0) {
+    if constexpr (((SPEC >> 16) & 1) != 0) body(std::integral_constant<int, (SPEC & 0xff)>{});
+    else body(std::integral_constant<int, ACT_NONE>{});
+  } else {
+    act_dispatch(a.L[0].act, body);
+  }
+  epilogue<SPEC, 1, MT1>(acc, a.L[1]);
   if constexpr (sizeof...(Rest) > 0) {
     bf16x8_t nb[2 * MT1];
     pack_next<MT1>(acc, nb);
-    run_chain<ACT, OFF2, 2, N1, Rest...>(a, nb, lds, row, valid, lane);
+    run_chain<SPEC, OFF2, 2, N1, Rest...>(a, nb, lds, row, valid, lane);
   } else {
     if (valid) store_out<MT1>(acc, a, row, h);
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int ACT, int FT, int... Ns>
+template <int MODE, bool IN_F32, int W0, int W1, int SPEC, int FT, int... Ns>
 __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   constexpr int FW = FT / 64;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -401,13 +399,13 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     bf16x8_t b[In::KS];
     In::load(a, row, valid, lane >> 5, b);
     if constexpr ((MODE & FUSE01) != 0)  // un-normalised first layer: tile-fused layers 0+1
-      run_chain01<ACT, In::K0, Ns...>(a, b, lds, row, valid, lane);
+      run_chain01<SPEC, In::K0, Ns...>(a, b, lds, row, valid, lane);
     else
-      run_chain<ACT, 0, 0, In::K0, Ns...>(a, b, lds, row, valid, lane);
+      run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, row, valid, lane);
   }
 }
 
-template <int MODE, bool IN_F32, int W0, int W1, int ACT, int FT, int... Ns>
+template <int MODE, bool IN_F32, int W0, int W1, int SPEC, int FT, int... Ns>
 static int launch(const FArgs& a, hipStream_t st) {
   constexpr int FW = FT / 64;
   using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
@@ -415,7 +413,7 @@ static int launch(const FArgs& a, hipStream_t st) {
   using Off = Offsets<In::K0, Ns...>;
   for (int l = 0; l < a.nl; ++l)
     RG_REQUIRE(a.L[l].woff == Off::get(l), RG_ERR_ARG, "rg_mlp_chain_fast: LDS layout of layer %d", l);
-  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, ACT, FT, Ns...>;
+  auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, SPEC, FT, Ns...>;
   static bool attr = false;
   if (!attr) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -432,9 +430,9 @@ static int launch(const FArgs& a, hipStream_t st) {
   return RG_OK;
 }
 
-// shape key: mode, f32 input, widths, hidden activation (-1: any), padded outputs
+// shape key: mode, f32 input, widths, epilogue spec (-1: run-time), padded outputs
 struct Key {
-  int mode, in_f32, w0, w1, act, nl;
+  int mode, in_f32, w0, w1, spec, nl;
   int n[RG_MAX_LAYERS];
 };
 
@@ -451,22 +449,24 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
 
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
 static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
-#define RG_FAST(FT, MODE, F32, W0, W1, ...)                                               \
+#define RG_FAST(FT, SP, MODE, F32, W0, W1, ...)                                           \
   if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                        \
-    return k.act == ACT_LEAKY ? launch<MODE, F32, W0, W1, ACT_LEAKY, FT, __VA_ARGS__>(a, st) \
-                              : launch<MODE, F32, W0, W1, -1, FT, __VA_ARGS__>(a, st);
-  // node / edge encoders (graph_feature_encoding, yml:56-57)
-  RG_FAST(768, RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
-  RG_FAST(768, RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
+    return k.spec == (SP) ? launch<MODE, F32, W0, W1, (SP), FT, __VA_ARGS__>(a, st)       \
+                          : launch<MODE, F32, W0, W1, -1, FT, __VA_ARGS__>(a, st);
+  constexpr int L = ACT_LEAKY;
+  // node / edge encoders (graph_feature_encoding, gnn_blocks.py:19-42: block 0 is not
+  // normalised)
+  RG_FAST(768, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
+  RG_FAST(768, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
-  RG_FAST(512, RG_IN_GATHER3, 0, 64, 64, 128, 64)
-  RG_FAST(1024, RG_IN_CONCAT2, 0, 64, 64, 64)
-  // heads: 3-block stems + FFN_TaskSpecificHead (ffn + Linear -> 7 / 2)
-  RG_FAST(1024, RG_IN_DENSE, 0, 64, 0, 64, 64, 64, 64, 32)
-  RG_FAST(1024, RG_IN_PAIRADD, 0, 64, 0, 64, 64, 64, 64, 32)
-  RG_FAST(768, RG_IN_DENSE, 0, 64, 0, 64)
-  RG_FAST(768, RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
-  RG_FAST(1024, RG_IN_DENSE, 0, 64, 0, 64, 32)
+  RG_FAST(512, spec(L, 0b11, 0b11), RG_IN_GATHER3, 0, 64, 64, 128, 64)
+  RG_FAST(1024, spec(L, 0b1, 0b1), RG_IN_CONCAT2, 0, 64, 64, 64)
+  // heads: 3-block stems + FFN_TaskSpecificHead (ffn + bare Linear -> 7 / 2)
+  RG_FAST(1024, spec(L, 0b1111, 0b1111), RG_IN_DENSE, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(1024, spec(L, 0b1111, 0b1111), RG_IN_PAIRADD, 0, 64, 0, 64, 64, 64, 64, 32)
+  RG_FAST(768, spec(L, 0b1, 0b1), RG_IN_DENSE, 0, 64, 0, 64)
+  RG_FAST(768, spec(L, 0b111, 0b111), RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
+  RG_FAST(1024, spec(L, 0b01, 0b01), RG_IN_DENSE, 0, 64, 0, 64, 32)
 #undef RG_FAST
   return RG_ERR_UNSUPPORTED;
 }
@@ -511,6 +511,7 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
                                                l == 0 ? RG_PACK_FAST_IN : RG_PACK_FAST_CHAIN);
     a.L[l].out = s.out_dim;
     a.L[l].act = s.act;
+    a.L[l].centered = (s.flags & RG_LAYER_CENTERED) ? 1 : 0;
     off += (a.L[l].bytes + 15) & ~15;
     // chained layers: the previous padded width is the next K (zero columns beyond out)
     if (l > 0 && layers[l - 1].out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
@@ -539,11 +540,19 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
     // encoders: the first ffn_block has no normalisation (gnn_blocks.py:31)
     if (n_layers >= 2 && !layers[0].norm_mu) k.mode |= FUSE01;
   }
-  // compile-time hidden activation: every layer uses the yml activation (LeakyReLU,
-  // configuration_radarscenes_gnn.yml:50) except possibly an identity last layer
-  k.act = ACT_LEAKY;
-  for (int l = 0; l < n_layers; ++l)
-    if (layers[l].act != ACT_LEAKY && !(l == n_layers - 1 && layers[l].act == ACT_NONE)) k.act = -1;
+  // compile-time epilogues: the yml activation (LeakyReLU,
+  // configuration_radarscenes_gnn.yml:50) or identity per layer, norm per layer
+  {
+    int nm = 0, am = 0;
+    bool ok = true;
+    for (int l = 0; l < n_layers; ++l) {
+      if (layers[l].norm_mu) nm |= 1 << l;
+      if (layers[l].norm_mu && !(layers[l].flags & RG_LAYER_CENTERED)) ok = false;
+      if (layers[l].act == ACT_LEAKY) am |= 1 << l;
+      else if (layers[l].act != ACT_NONE) ok = false;
+    }
+    k.spec = ok ? spec(ACT_LEAKY, nm, am) : -1;
+  }
   // normalised layers must be unpadded (epilogue statistics run over 32*MT features)
   for (int l = 0; l < n_layers; ++l)
     if (layers[l].norm_mu && layers[l].out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;

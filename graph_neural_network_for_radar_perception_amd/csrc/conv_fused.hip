@@ -44,7 +44,7 @@ static constexpr int TSTRIDE = 96;   // bf16 per row of the message tile [edge][
 static constexpr float NORM_EPS = 1e-5f;
 
 struct CLayer {
-  int woff, bytes, out, act;
+  int woff, bytes, out, act, centered;
   const float* mu;
   const float* sd;
   const void* src;
@@ -81,14 +81,7 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
   const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
 #pragma unroll
   for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 bv = *(const f32x4*)(bias + 32 * m + 8 * g + 4 * h);
-      acc[m][4 * g + 0] = bv.x;
-      acc[m][4 * g + 1] = bv.y;
-      acc[m][4 * g + 2] = bv.z;
-      acc[m][4 * g + 3] = bv.w;
-    }
+    acc[m] = ld_bias_frag(bias, m, h);  // accumulator-order bias: 4 x ds_read_b128
   const char* wl = w + lane * 16;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -102,10 +95,13 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
 }
 
 // channel_normalization (common.py:208-220) + activation (rg_common.h norm_act_rows)
-// (every block is normalised, and with ACT >= 0 every block uses ACT: host-checked)
+// (every block is normalised; with ACT >= 0 every block uses ACT and was packed
+// RG_PACK_CENTERED: host-checked)
 template <int ACT, int MT>
 __device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
-  channel_norm_pk<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+  if constexpr (ACT >= 0) channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+  else if (L.centered) channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+  else channel_norm_pk<MT>(acc, *L.mu, *L.sd, NORM_EPS);
   if constexpr (ACT >= 0) act_pk_all<ACT, MT>(acc);
   else act_dispatch(L.act, [&](auto A) { act_pk_all<decltype(A)::value, MT>(acc); });
 }
@@ -345,6 +341,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
     a.L[l].bytes = (int)rg_packed_linear_bytes(ls[l]->in_dim, ls[l]->out_dim, fmts[l]);
     a.L[l].out = ls[l]->out_dim;
     a.L[l].act = ls[l]->act;
+    a.L[l].centered = (ls[l]->flags & RG_LAYER_CENTERED) ? 1 : 0;
     off += (a.L[l].bytes + 15) & ~15;
   }
   a.total_bytes = off;
@@ -364,7 +361,8 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
   // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
   // blocks selects the compile-time variant; anything else dispatches per layer
-  const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY;
+  const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY &&
+                     (m0.flags & m1.flags & u.flags & RG_LAYER_CENTERED);
   auto kern = leaky ? fused_conv_kernel<ACT_LEAKY> : fused_conv_kernel<-1>;
   static bool attr[2] = {false, false};
   if (!attr[leaky]) {

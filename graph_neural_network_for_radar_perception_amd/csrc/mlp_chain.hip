@@ -124,7 +124,7 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
 // FAST_UPD  k-steps s < in/32 as FAST_IN (x[node] from memory), the rest as FAST_CHAIN
 //           offset by in/2 (aggregate from accumulators): the fused conv layer's update
 __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int mem_steps,
-                                 uint16_t* __restrict__ P, long total) {
+                                 int center, uint16_t* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S = (in + 15) / 16;
@@ -139,12 +139,39 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
   const int k = s < mem_steps
                     ? 16 * s + 8 * h + j
                     : 16 * mem_steps + 32 * (sc >> 1) + 16 * (sc & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
-  P[t] = (o < out && k < in) ? f32_to_bf16(W[(size_t)o * in + k]) : (uint16_t)0;
+  float v = 0.f;
+  if (o < out && k < in) {
+    v = W[(size_t)o * in + k];
+    if (center) {  // RG_PACK_CENTERED: subtract the mean over the outputs of column k
+      float cs = 0.f;
+      for (int oo = 0; oo < out; ++oo) cs += W[(size_t)oo * in + k];
+      v -= cs / (float)out;
+    }
+  }
+  P[t] = f32_to_bf16(v);
 }
 
 __global__ void pack_bias_kernel(const float* __restrict__ b, int out, int n, float* __restrict__ P) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n) P[t] = (b && t < out) ? b[t] : 0.f;
+}
+
+// fast formats: the bias in 32x32 accumulator order, [m][h][16] with entry
+// 4g + j = bias[32m + 8g + 4h + j], so lane half h of M-tile m initialises its 16
+// accumulators with four contiguous 16-B LDS reads (no register moves)
+__global__ void pack_bias_frag_kernel(const float* __restrict__ b, int out, int n, int center,
+                                      float* __restrict__ P) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int m = t >> 5, h = (t >> 4) & 1, g = (t >> 2) & 3, j = t & 3;
+  const int f = 32 * m + 8 * g + 4 * h + j;
+  float v = (b && f < out) ? b[f] : 0.f;
+  if (center && b && f < out) {
+    float cs = 0.f;
+    for (int o = 0; o < out; ++o) cs += b[o];
+    v -= cs / (float)out;
+  }
+  P[t] = v;
 }
 
 // ------------------------------------------------------------------ element access
@@ -479,7 +506,7 @@ static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
 using namespace rg;
 
 extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
-  return packed_bytes(in_dim, out_dim, dtype);
+  return packed_bytes(in_dim, out_dim, dtype & ~RG_PACK_CENTERED);
 }
 
 extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim, int out_dim,
@@ -487,6 +514,10 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   RG_REQUIRE(in_dim > 0 && out_dim > 0 && in_dim <= MAXW && out_dim <= MAXW, RG_ERR_UNSUPPORTED,
              "rg_pack_linear: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
   hipStream_t st = (hipStream_t)stream;
+  const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
+  dtype &= ~RG_PACK_CENTERED;
+  RG_REQUIRE(!center || dtype >= RG_PACK_FAST_IN, RG_ERR_ARG,
+             "rg_pack_linear: RG_PACK_CENTERED applies to the RG_PACK_FAST_* formats");
   if (dtype == RG_F32) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
     pack_f32_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, (float*)packed,
@@ -502,13 +533,16 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
     const int mem_steps = dtype == RG_PACK_FAST_IN ? ks : (dtype == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
     pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
-                                                           (uint16_t*)packed, total);
+                                                           center, (uint16_t*)packed, total);
   } else {
     RG_REQUIRE(false, RG_ERR_ARG, "rg_pack_linear: bad dtype %d", dtype);
   }
   const int nb = kpad(out_dim, (dtype >= RG_PACK_FAST_IN) ? 32 : 16);
-  pack_bias_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(
-      bias, out_dim, nb, (float*)((char*)packed + frag_bytes(in_dim, out_dim, dtype)));
+  float* pb = (float*)((char*)packed + frag_bytes(in_dim, out_dim, dtype));
+  if (dtype >= RG_PACK_FAST_IN)
+    pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, center, pb);
+  else
+    pack_bias_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, pb);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -114,6 +114,14 @@ __device__ __forceinline__ void act_dispatch(int act, F&& f) {
 // ---------------------------------------------------------------------------
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// the 16 bias values of M-tile m, lane half h, from a fast-format bias stored in
+// accumulator order (rg_pack_linear, pack_bias_frag_kernel): four 16-B reads
+__device__ __forceinline__ f32x16 ld_bias_frag(const float* bias, int m, int h) {
+  const f32x4* p = (const f32x4*)(bias + (2 * m + h) * 16);
+  const f32x4 a = p[0], b = p[1], c = p[2], d = p[3];
+  return (f32x16){a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+}
+
 __device__ __forceinline__ f32x2 pair(const f32x16& v, int i) { return (f32x2){v[2 * i], v[2 * i + 1]}; }
 __device__ __forceinline__ void set_pair(f32x16& v, int i, f32x2 p) {
   v[2 * i] = p.x;
@@ -123,11 +131,13 @@ __device__ __forceinline__ void set_pair(f32x16& v, int i, f32x2 p) {
 template <int ACT>
 __device__ __forceinline__ f32x2 act_pk(f32x2 y) {
   if constexpr (ACT == ACT_LEAKY) {
-    // max(y, 0.01 y) (constants.py:10): one v_pk_mul_f32 + two v_med3_f32 (med3 with +inf
-    // is the max without the operand canonicalisation fmaxf needs in IEEE mode)
+    // max(y, 0.01 y) (constants.py:10): one v_pk_mul_f32 + two v_max_f32
     const f32x2 z = y * (f32x2){0.01f, 0.01f};
-    return (f32x2){__builtin_amdgcn_fmed3f(y.x, z.x, __builtin_inff()),
-                   __builtin_amdgcn_fmed3f(y.y, z.y, __builtin_inff())};
+    float a, b;  // plain v_max_f32: no operand canonicalisation (the compiler would add a
+                 // v_max x, x per MFMA-produced operand in IEEE mode)
+    asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(y.x), "v"(z.x));
+    asm("v_max_f32 %0, %1, %2" : "=v"(b) : "v"(y.y), "v"(z.y));
+    return (f32x2){a, b};
   } else {
     return (f32x2){act_t<ACT>(y.x), act_t<ACT>(y.y)};
   }
@@ -171,6 +181,34 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
     for (int i = 0; i < 8; ++i) set_pair(acc[m], i, __builtin_elementwise_fma(pair(acc[m], i), gs2, gb2));
 }
 
+// channel_normalization of a CENTRED layer (weights packed with RG_PACK_CENTERED): the
+// pre-activations already have zero mean over the features, so only the sum of squares
+// is needed (one v_pk_fma_f32 per two features) -- the mean pass disappears.
+template <int MT>
+__device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], float mu, float sd,
+                                                         float eps) {
+  constexpr int N = 32 * MT;
+  f32x2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const f32x2 d0 = pair(acc[m], i), d1 = pair(acc[m], i + 1);
+      q0 = __builtin_elementwise_fma(d0, d0, q0);
+      q1 = __builtin_elementwise_fma(d1, d1, q1);
+    }
+  const f32x2 qt = q0 + q1;
+  float ss = qt.x + qt.y;
+  ss += __shfl_xor(ss, 32, 64);
+  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  const float gs = sd * inv;
+  const f32x2 gs2 = {gs, gs}, mu2 = {mu, mu};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, __builtin_elementwise_fma(pair(acc[m], i), gs2, mu2));
+}
+
 template <int ACT, int MT>
 __device__ __forceinline__ void act_pk_all(f32x16 (&acc)[MT]) {
 #pragma unroll
@@ -184,8 +222,11 @@ __device__ __forceinline__ void act_pk_all(f32x16 (&acc)[MT]) {
 // one run-time dispatch
 template <int ACT, int MT>
 __device__ __forceinline__ void norm_act_rows(f32x16 (&acc)[MT], const float* mu, const float* sd,
-                                              int act, float eps) {
-  if (mu) channel_norm_pk<MT>(acc, *mu, *sd, eps);
+                                              int act, float eps, bool centered) {
+  if (mu) {
+    if (centered) channel_norm_pk_centered<MT>(acc, *mu, *sd, eps);
+    else channel_norm_pk<MT>(acc, *mu, *sd, eps);
+  }
   if constexpr (ACT >= 0) {
     if (act == ACT) act_pk_all<ACT, MT>(acc);
   } else {

@@ -117,9 +117,17 @@ def pack_specs(specs: List[LayerSpec], fmts: List[int], device):
     return buf, offs
 
 
-def layer_array(specs: List[LayerSpec], base: int, offs: List[int]):
+def centered_fmt(spec: LayerSpec, fmt: int) -> int:
+    """Fast formats of a normalised layer are packed zero-mean over the outputs
+    (RG_PACK_CENTERED): the kernels' channel_normalization then skips its mean pass."""
+    return fmt | nat.RG_PACK_CENTERED if spec.mu is not None else fmt
+
+
+def layer_array(specs: List[LayerSpec], base: int, offs: List[int], fmts=None):
     arr = (nat.rg_layer * len(specs))()
     for i, s in enumerate(specs):
+        arr[i].flags = (nat.RG_LAYER_CENTERED
+                        if fmts is not None and fmts[i] & nat.RG_PACK_CENTERED else 0)
         arr[i].w_packed = base + offs[i]
         arr[i].norm_mu = nat.ptr(s.mu.detach()) if s.mu is not None else None
         arr[i].norm_std = nat.ptr(s.std.detach()) if s.std is not None else None
@@ -160,7 +168,8 @@ class ChainPlan:
         groups = []
         for g0 in range(0, len(self.specs), nat.MAX_LAYERS):
             grp = list(range(g0, min(g0 + nat.MAX_LAYERS, len(self.specs))))
-            arr = layer_array([self.specs[i] for i in grp], buf.data_ptr(), [offs[i] for i in grp])
+            arr = layer_array([self.specs[i] for i in grp], buf.data_ptr(), [offs[i] for i in grp],
+                              [fmts[i] for i in grp])
             groups.append((arr, len(grp), self.specs[grp[-1]].out_dim))
         return buf, groups
 
@@ -173,8 +182,8 @@ class ChainPlan:
         # bf16: also the register-resident 32x32x16 formats of rg_mlp_chain_fast
         self.fast = None
         if self.dt == nat.RG_BF16 and len(self.specs) <= nat.MAX_LAYERS:
-            self.fast_buf, fg = self._pack_buffer(
-                lambda i: nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN)
+            self.fast_buf, fg = self._pack_buffer(lambda i: centered_fmt(
+                self.specs[i], nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN))
             self.fast = fg[0][0]
         self.fast_ok = {}   # in_mode -> bool (shape has a compiled fast kernel)
         self.sig = self._signature()
@@ -402,14 +411,15 @@ class ConvPlan:
         specs = self.msg.specs + self.upd.specs
         if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
             return
-        fmts = [nat.RG_PACK_FAST_IN, nat.RG_PACK_FAST_CHAIN, nat.RG_PACK_FAST_UPD]
+        fmts = [centered_fmt(sp, f) for sp, f in
+                zip(specs, [nat.RG_PACK_FAST_IN, nat.RG_PACK_FAST_CHAIN, nat.RG_PACK_FAST_UPD])]
         try:
             self.fused_buf, offs = pack_specs(specs, fmts, self.device)
         except RuntimeError:
             return
         base = self.fused_buf.data_ptr()
-        self.fused_msg = layer_array(specs[:2], base, offs[:2])
-        self.fused_upd = layer_array(specs[2:], base, offs[2:])
+        self.fused_msg = layer_array(specs[:2], base, offs[:2], fmts[:2])
+        self.fused_upd = layer_array(specs[2:], base, offs[2:], fmts[2:])
         self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_workspace_size(), dtype=torch.uint8,
                                     device=self.device)
         self.fused = True

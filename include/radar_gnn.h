@@ -47,6 +47,11 @@ extern "C" {
 #define RG_PACK_FAST_IN 2
 #define RG_PACK_FAST_CHAIN 3
 #define RG_PACK_FAST_UPD 4 /* update layer of rg_conv_layer_fused: cat(x, aggregate) */
+/* OR-ed into a RG_PACK_FAST_* format for a layer followed by channel_normalization:
+ * the rows of W and b are shifted to zero mean over the outputs (W - 1 mean_o(W),
+ * b - mean(b)).  The normalisation then sees (x - mean) directly -- it is invariant
+ * to that shift -- and skips its mean pass.  Mark such layers RG_LAYER_CENTERED. */
+#define RG_PACK_CENTERED 0x100
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -173,9 +178,11 @@ typedef struct rg_layer {
   const float* norm_std; /* channel_normalization.std (1,)                       */
   int in_dim;
   int out_dim;
-  int act; /* RG_ACT_* */
-  int pad_;
+  int act;   /* RG_ACT_* */
+  int flags; /* RG_LAYER_* */
 } rg_layer;
+
+#define RG_LAYER_CENTERED 1 /* w_packed was packed with RG_PACK_CENTERED */
 
 #define RG_MAX_LAYERS 8
 
