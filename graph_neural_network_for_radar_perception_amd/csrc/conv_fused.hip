@@ -4,15 +4,18 @@
 // message chain + scatter-aggregate + update chain; messages and aggregates never
 // touch HBM.
 //
-// Work unit = a block of 16 destination nodes and all their incoming edges (the
+// Work unit = a block of 8 destination nodes and all their incoming edges (the
 // destination-major CSR makes them one contiguous edge range).  A wave
-//   1. streams the block's edges in tiles of 32: loads cat(x[dst], x[src], e) of
-//      each edge straight into MFMA B fragments, runs the message MLP
-//      (32x32x16 MFMAs, channel_normalization + LeakyReLU in-lane, layer chained
-//      in registers) -> message tile M [64 features x 32 edges], lane = edge;
-//   2. transposes M through a wave-private LDS tile (8-B row stores, hardware
-//      transposed reads ds_read_b64_tr_b16) and accumulates
-//      Agg[64 x 16 nodes] += M . S with S the one-hot (edge -> destination slot)
+//   0. computes P[node] = W1[:, :C] x[node] + b1 for the block's nodes (the x_i = x[dst]
+//      third of the first message layer is shared by all edges into a node) into LDS;
+//   1. streams the block's edges in tiles of 32: accumulators start from P[dst], the
+//      x[src] and e rows go straight into MFMA B fragments for the remaining 2/3 of
+//      the first layer, then the rest of the message MLP (32x32x16 MFMAs,
+//      channel_normalization + LeakyReLU in-lane, layers chained in registers)
+//      -> message tile M [64 features x 32 edges], lane = edge;
+//   2. transposes M through a wave-private, XOR-swizzled LDS tile (8-B row stores,
+//      hardware transposed reads ds_read_b64_tr_b16, both bank-conflict free) and
+//      accumulates Agg[64 x 8 nodes] += M . S with S the one-hot (edge -> destination slot)
 //      matrix: the segmented scatter-add as 4 MFMAs per tile, summed in edge order
 //      with f32 accumulation (sources ascending within a destination = the
 //      reference scatter_add_ order; bf16-rounded messages as in the unfused path);
@@ -36,11 +39,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 static constexpr int CT = 512;
 static constexpr int CW = CT / 64;
-static constexpr int NB = 16;        // destination nodes per work block
+static constexpr int NB = 8;         // destination nodes per work block
 static constexpr int C = 64;         // node / edge / message / output channels
 static constexpr int HID = 128;      // msg_mlp_hidden_dim
-static constexpr int TSTRIDE = 96;   // bf16 per row of the message tile [edge][feature]
-                                     // (192 B: the 4 rows of a transposed read hit disjoint banks)
+// wave-private LDS: P (NB x HID f32), message tile (32 x C bf16), slots (32 int)
+static constexpr int WAVE_LDS = NB * HID * 4 + 32 * C * 2 + 128;
 static constexpr float NORM_EPS = 1e-5f;
 
 struct CLayer {
@@ -74,27 +77,24 @@ __device__ __forceinline__ bf16x8_t zero_bf8() {
   return __builtin_bit_cast(bf16x8_t, (u32x4){0u, 0u, 0u, 0u});
 }
 
-template <int KS, int MT>
-__device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc)[MT],
-                                           const char* w, int lane) {
-  const int h = lane >> 5;
-  const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-    acc[m] = ld_bias_frag(bias, m, h);  // accumulator-order bias: 4 x ds_read_b128
+// k-steps [S0, S0 + KS) of a packed 32x32x16 layer with KT k-steps in total
+// (fragment (m, s) at byte (m * KT + s) * 1024); acc holds the initial values
+template <int KS, int MT, int KT, int S0>
+__device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
+                                           int lane) {
   const char* wl = w + lane * 16;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const bf16x8_t av = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + s) * 1024));
+      const bf16x8_t av = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s) * 1024));
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b[s], acc[m], 0, 0, 0);
     }
     if (s & 1) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// channel_normalization (common.py:208-220) + activation (rg_common.h norm_act_rows)
+// channel_normalization (common.py:208-220) + activation (rg_common.h)
 // (every block is normalised; with ACT >= 0 every block uses ACT and was packed
 // RG_PACK_CENTERED: host-checked)
 template <int ACT, int MT>
@@ -119,6 +119,14 @@ __device__ __forceinline__ void pack_acc(const f32x16 (&acc)[MT], bf16x8_t* nb) 
     }
 }
 
+// XOR swizzle of the 4-feature granules of message-tile row `row` (64 bf16 = 128 B per
+// row).  Row stores (ds_write_b64, lane = row) and transposed reads (ds_read_b64_tr_b16,
+// 4 rows x 8 granules per half-wave) are both bank-conflict free: granule g of row r
+// lives at g ^ swz(r), swz a bijection on 0..15 whose bit 3 differs for rows r, r + 2.
+__device__ __forceinline__ int swz(int row) {
+  return (row & 7) | ((((row >> 1) ^ (row >> 3)) & 1) << 3);
+}
+
 template <int ACT>
 __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -133,12 +141,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  // wave-private transpose tile [64 features][32 edges] (+pad) and slot array
-  uint16_t* tile = (uint16_t*)(lds + a.total_bytes + wave * (32 * TSTRIDE * 2 + 128));
-  int* slots = (int*)((char*)tile + 32 * TSTRIDE * 2);
+  // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
+  char* wbase = lds + a.total_bytes + wave * WAVE_LDS;
+  float* P = (float*)wbase;
+  uint16_t* tile = (uint16_t*)(wbase + NB * HID * 4);
+  int* slots = (int*)((char*)tile + 32 * C * 2);
   const char* w0 = lds + a.L[0].woff;
   const char* w1 = lds + a.L[1].woff;
   const char* w2 = lds + a.L[2].woff;
+  const float* bias0 = (const float*)(w0 + 4 * 12 * 1024);
+  const float* bias1 = (const float*)(w1 + 2 * 8 * 1024);
+  const float* bias2 = (const float*)(w2 + 2 * 8 * 1024);
 
   for (;;) {
     int blk = 0;
@@ -148,86 +161,95 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     const int n0 = blk * NB;
     const int n1 = min(n0 + NB, a.n_nodes);
     const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+
+    // ---- P[node] = W1[:, x_i part] x[node] + b1 for the block's nodes: the x_i = x[dst]
+    //      third of the message MLP's first layer is the same for every edge into a node,
+    //      so it is computed once per node here instead of once per edge
+    {
+      const int node = min(n0 + r, n1 - 1);
+      const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
+      bf16x8_t bx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
+      f32x16 accp[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
+      mfma_steps<4, 4, 12, 0>(bx, accp, w0, lane);
+      if (r < NB) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          f32x4* pw = (f32x4*)(P + r * HID + (2 * m + h) * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pw[q] = (f32x4){accp[m][4 * q], accp[m][4 * q + 1], accp[m][4 * q + 2], accp[m][4 * q + 3]};
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the whole wave
+      __builtin_amdgcn_wave_barrier();
+    }
+
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
-    // software pipeline over the block's edge tiles: while tile t computes, the
-    // gathered rows of tile t+1 (x[dst], x[src], e) and the indices of tile t+2 are
-    // in flight, so neither the dependent index load nor the row gathers stall
-    bf16x8_t bn[12];
-    int slot_n = NB;
-    int di_n = 0, sj_n = 0;  // indices of the next tile to gather
+
+    // ---- edge tiles, software pipelined: while tile t computes, the rows of tile t+1
+    //      (x[src], e) and the indices of tile t+2 are in flight.  Lanes past the end
+    //      of the block's edges load the last edge (finite data) and aggregate into the
+    //      unused slot 31.
+    int di_n = 0, sj_n = 0;
     auto load_idx = [&](int t0) {
-      const int p = t0 + r;
-      if (p < e1) {
-        di_n = a.dst[p];
-        sj_n = a.src[p];
+      const int p = min(t0 + r, e1 - 1);
+      di_n = a.dst[p];
+      sj_n = a.src[p];
+    };
+    auto load_rows = [&](int t0, bf16x8_t (&bb)[8], int& slot) {
+      const int p = min(t0 + r, e1 - 1);
+      slot = di_n - n0;
+      const uint16_t* pj = a.x + (size_t)sj_n * a.ldx + 8 * h;
+      const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bb[s] = ld_bf8(pj + 16 * s);
+        bb[4 + s] = ld_bf8(pe + 16 * s);
       }
     };
-    auto load_rows = [&](int t0) {
-      const int p = t0 + r;
-      slot_n = NB;
-      if (p < e1) {
-        slot_n = di_n - n0;
-        const uint16_t* pi = a.x + (size_t)di_n * a.ldx + 8 * h;
-        const uint16_t* pj = a.x + (size_t)sj_n * a.ldx + 8 * h;
-        const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          bn[s] = ld_bf8(pi + 16 * s);
-          bn[4 + s] = ld_bf8(pj + 16 * s);
-          bn[8 + s] = ld_bf8(pe + 16 * s);
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < 12; ++s) bn[s] = zero_bf8();
-      }
-    };
-    if (e0 < e1) {
-      load_idx(e0);
-      load_rows(e0);
-      if (e0 + 32 < e1) load_idx(e0 + 32);
-    }
-    for (int t0 = e0; t0 < e1; t0 += 32) {
+    auto compute = [&](const bf16x8_t (&b)[8], int slot, int t0) {
       const bool valid = t0 + r < e1;
-      bf16x8_t b[12];
-#pragma unroll
-      for (int s = 0; s < 12; ++s) b[s] = bn[s];
-      const int slot = slot_n;
-      if (t0 + 32 < e1) {
-        if (RG_CONV_EXP != 1) load_rows(t0 + 32);
-        if (t0 + 64 < e1) load_idx(t0 + 64);
-      }
       f32x16 acc1[4];
-      mfma_layer<12, 4>(b, acc1, w0, lane);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc1[m] = ld_bias_frag(P + slot * HID, m, h);
+      mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
       if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0]);
       bf16x8_t b2[8];
       pack_acc<4>(acc1, b2);
       f32x16 acc2[2];
-      mfma_layer<8, 2>(b2, acc2, w1, lane);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias1, m, h);
+      mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
       if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1]);
       if (RG_CONV_EXP == 3) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) agg[m] += acc2[m];
-        continue;
+        return;
       }
-      // ---- message tile M -> LDS as rows [edge][feature] (8-B stores of 4 features);
-      //      invalid edges -> 0
+      // ---- message tile M -> LDS rows [edge][feature] (8-B stores of 4 features)
+      const int sr = swz(r);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          uint2 w;
-          w.x = valid ? bf2(acc2[m][4 * g + 0], acc2[m][4 * g + 1]) : 0u;
-          w.y = valid ? bf2(acc2[m][4 * g + 2], acc2[m][4 * g + 3]) : 0u;
-          *(uint2*)(tile + r * TSTRIDE + 32 * m + 8 * g + 4 * h) = w;
+          uint2 wv;
+          wv.x = bf2(acc2[m][4 * g + 0], acc2[m][4 * g + 1]);
+          wv.y = bf2(acc2[m][4 * g + 2], acc2[m][4 * g + 3]);
+          const int gr = (8 * m + 2 * g + h) ^ sr;
+          *(uint2*)(tile + r * C + 4 * gr) = wv;
         }
-      if (h == 0) slots[r] = slot;
+      if (h == 0) slots[r] = valid ? slot : 31;
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
       // A = M (features x edges) via ds_read_b64_tr_b16: lane 4q+p of each 16-lane
-      // group G addresses row (edge) row0+q, columns col0+4p..+3; lane i of the group
+      // group G addresses row (edge) row0+q, granule col0/4+p; lane i of the group
       // receives column (feature) col0+i of the 4 rows.
       const int G = (lane >> 4) & 3, q4 = (lane & 15) >> 2, p4 = lane & 3;
 #pragma unroll
@@ -242,16 +264,16 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
         sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
         sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
         const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
-        const int row0 = 16 * s + 8 * (G >> 1);
+        const int row_lo = 16 * s + 8 * (G >> 1) + q4, row_hi = row_lo + 4;
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
-          const int col0 = 32 * m + 16 * (G & 1);
+          const int gcol = 8 * m + 4 * (G & 1) + p4;
           typedef short v4s __attribute__((ext_vector_type(4)));
           typedef __attribute__((address_space(3))) v4s lds_v4s;
           const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4s*)(tile + (row0 + q4) * TSTRIDE + col0 + 4 * p4));
+              (lds_v4s*)(tile + row_lo * C + 4 * (gcol ^ swz(row_lo))));
           const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4s*)(tile + (row0 + 4 + q4) * TSTRIDE + col0 + 4 * p4));
+              (lds_v4s*)(tile + row_hi * C + 4 * (gcol ^ swz(row_hi))));
           const bf16x8_t mf = __builtin_bit_cast(
               bf16x8_t, (short __attribute__((ext_vector_type(8)))){lo[0], lo[1], lo[2], lo[3],
                                                                   hi[0], hi[1], hi[2], hi[3]});
@@ -260,10 +282,36 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
+    };
+
+    if (e0 < e1) {
+      bf16x8_t bA[8], bB[8];
+      int slotA = 0, slotB = 0;
+      load_idx(e0);
+      load_rows(e0, bA, slotA);
+      if (e0 + 32 < e1) load_idx(e0 + 32);
+      for (int t0 = e0;;) {
+        if (t0 + 32 < e1) {
+          if (RG_CONV_EXP != 1) load_rows(t0 + 32, bB, slotB);
+          else slotB = slotA;
+          if (t0 + 64 < e1) load_idx(t0 + 64);
+        }
+        compute(bA, slotA, t0);
+        t0 += 32;
+        if (t0 >= e1) break;
+        if (t0 + 32 < e1) {
+          if (RG_CONV_EXP != 1) load_rows(t0 + 32, bA, slotA);
+          else slotA = slotB;
+          if (t0 + 64 < e1) load_idx(t0 + 64);
+        }
+        compute(RG_CONV_EXP != 1 ? bB : bA, slotB, t0);
+        t0 += 32;
+        if (t0 >= e1) break;
+      }
     }
     // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
     const int node = n0 + r;
-    const bool nvalid = node < n1;
+    const bool nvalid = r < NB && node < n1;
     if (a.aggr_mean) {
       // PyG mean: sum / max(count, 1)
       const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
@@ -276,10 +324,12 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     bf16x8_t bu[8];
     const uint16_t* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 8 * h;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) bu[s] = nvalid ? ld_bf8(px + 16 * s) : zero_bf8();
+    for (int s = 0; s < 4; ++s) bu[s] = ld_bf8(px + 16 * s);
     pack_acc<2>(agg, bu + 4);
     f32x16 accu[2];
-    mfma_layer<8, 2>(bu, accu, w2, lane);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(bias2, m, h);
+    mfma_steps<8, 2, 8, 0>(bu, accu, w2, lane);
     norm_act<ACT, 2>(accu, a.L[2]);
     if (nvalid) {
       uint16_t* po = a.x_out + (size_t)node * a.ldo;
@@ -357,7 +407,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   a.counter = (int*)workspace;
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
   if (n_nodes <= 0) return RG_OK;
-  const size_t lds = (size_t)off + (size_t)CW * (32 * TSTRIDE * 2 + 128);
+  const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
   RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
   // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
   // blocks selects the compile-time variant; anything else dispatches per layer
