@@ -215,14 +215,16 @@ template <int K, int N, int... Rest> struct Offsets<K, N, Rest...> {
 constexpr int spec(int act, int norm_mask, int act_mask) {
   return act | (norm_mask << 8) | (act_mask << 16);
 }
+// nrm: the layers' channel_normalization (mu, sd) staged in LDS at kernel start
 template <int SPEC, int LI, int MT>
-__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L) {
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, const float* nrm) {
   if constexpr (SPEC >= 0) {
     if constexpr (((SPEC >> (8 + LI)) & 1) != 0)  // normalised => centred (host-checked)
-      channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+      channel_norm_pk_centered<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1], NORM_EPS);
     if constexpr (((SPEC >> (16 + LI)) & 1) != 0) act_pk_all<(SPEC & 0xff), MT>(acc);
   } else {
-    norm_act_rows<-1, MT>(acc, L.mu, L.sd, L.act, NORM_EPS, L.centered != 0);
+    norm_act_rows<-1, MT>(acc, L.mu != nullptr, nrm[2 * LI], nrm[2 * LI + 1], L.act, NORM_EPS,
+                          L.centered != 0);
   }
 }
 
@@ -292,18 +294,19 @@ __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& 
 
 template <int SPEC, int OFF, int LI, int K, int N, int... Rest>
 __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K + 15) / 16],
-                                          const char* lds, long row, bool valid, int lane) {
+                                          const char* lds, const float* nrm, long row, bool valid,
+                                          int lane) {
   constexpr int KS = (K + 15) / 16;
   constexpr int MT = N / 32;
   static_assert(N % 32 == 0, "padded widths are multiples of 32");
   f32x16 acc[MT];
   mfma_layer<KS, MT>(b, acc, lds + OFF, lane);
-  epilogue<SPEC, LI, MT>(acc, a.L[LI]);
+  epilogue<SPEC, LI, MT>(acc, a.L[LI], nrm);
   if constexpr (sizeof...(Rest) > 0) {
     bf16x8_t nb[2 * MT];
     pack_next<MT>(acc, nb);
-    run_chain<SPEC, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, row,
-                                                                             valid, lane);
+    run_chain<SPEC, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, nrm,
+                                                                             row, valid, lane);
   } else {
     if (valid) store_out<MT>(acc, a, row, lane >> 5);
   }
@@ -316,7 +319,8 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
 // otherwise hold 128 accumulators + 64 packed registers and spill).
 template <int SPEC, int K0, int N0, int N1, int... Rest>
 __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[(K0 + 15) / 16],
-                                            const char* lds, long row, bool valid, int lane) {
+                                            const char* lds, const float* nrm, long row,
+                                            bool valid, int lane) {
   constexpr int KS0 = (K0 + 15) / 16, MT0 = N0 / 32, KS1 = N0 / 16, MT1 = N1 / 32;
   constexpr int OFF1 = (fast_bytes(K0, N0) + 15) & ~15;
   constexpr int OFF2 = OFF1 + ((fast_bytes(N0, N1) + 15) & ~15);
@@ -364,11 +368,11 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
   } else {
     act_dispatch(a.L[0].act, body);
   }
-  epilogue<SPEC, 1, MT1>(acc, a.L[1]);
+  epilogue<SPEC, 1, MT1>(acc, a.L[1], nrm);
   if constexpr (sizeof...(Rest) > 0) {
     bf16x8_t nb[2 * MT1];
     pack_next<MT1>(acc, nb);
-    run_chain<SPEC, OFF2, 2, N1, Rest...>(a, nb, lds, row, valid, lane);
+    run_chain<SPEC, OFF2, 2, N1, Rest...>(a, nb, lds, nrm, row, valid, lane);
   } else {
     if (valid) store_out<MT1>(acc, a, row, h);
   }
@@ -378,7 +382,16 @@ template <int MODE, bool IN_F32, int W0, int W1, int SPEC, int FT, int... Ns>
 __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   constexpr int FW = FT / 64;
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[2 * RG_MAX_LAYERS];
   using In = Input<MODE & ~FUSE01, IN_F32, W0, W1>;
+  if (threadIdx.x == 0) {  // static layer indices: a dynamic a.L[i] would copy a to scratch
+#pragma unroll
+    for (int l = 0; l < RG_MAX_LAYERS; ++l) {
+      const bool n = l < a.nl && a.L[l].mu;
+      nrm[2 * l] = n ? *a.L[l].mu : 0.f;
+      nrm[2 * l + 1] = n ? *a.L[l].sd : 0.f;
+    }
+  }
   // stage all layers' packed weights + biases (static layer indices: no scratch copy)
 #pragma unroll
   for (int l = 0; l < RG_MAX_LAYERS; ++l) {
@@ -399,9 +412,9 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     bf16x8_t b[In::KS];
     In::load(a, row, valid, lane >> 5, b);
     if constexpr ((MODE & FUSE01) != 0)  // un-normalised first layer: tile-fused layers 0+1
-      run_chain01<SPEC, In::K0, Ns...>(a, b, lds, row, valid, lane);
+      run_chain01<SPEC, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
     else
-      run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, row, valid, lane);
+      run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
   }
 }
 
@@ -417,7 +430,7 @@ static int launch(const FArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024));
+                                     DYN_LDS_MAX));
     attr = true;
   }
   const long tiles = (a.rows + 31) / 32;
@@ -452,7 +465,7 @@ static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
 #define RG_FAST(FT, SP, MODE, F32, W0, W1, ...)                                           \
   if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                        \
     return k.spec == (SP) ? launch<MODE, F32, W0, W1, (SP), FT, __VA_ARGS__>(a, st)       \
-                          : launch<MODE, F32, W0, W1, -1, FT, __VA_ARGS__>(a, st);
+                          : launch<MODE, F32, W0, W1, -1, 512, __VA_ARGS__>(a, st);
   constexpr int L = ACT_LEAKY;
   // node / edge encoders (graph_feature_encoding, gnn_blocks.py:19-42: block 0 is not
   // normalised)
@@ -516,7 +529,7 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
     // chained layers: the previous padded width is the next K (zero columns beyond out)
     if (l > 0 && layers[l - 1].out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
   }
-  if (off > 160 * 1024) return RG_ERR_UNSUPPORTED;
+  if (off > DYN_LDS_MAX) return RG_ERR_UNSUPPORTED;
   a.nl = n_layers;
   a.total_bytes = off;
   a.rows = rows;

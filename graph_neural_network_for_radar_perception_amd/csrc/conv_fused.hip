@@ -97,11 +97,12 @@ __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT],
 // channel_normalization (common.py:208-220) + activation (rg_common.h)
 // (every block is normalised; with ACT >= 0 every block uses ACT and was packed
 // RG_PACK_CENTERED: host-checked)
+// (mu, sd = the layer's channel_normalization scalars, staged in LDS once per kernel)
 template <int ACT, int MT>
-__device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L) {
-  if constexpr (ACT >= 0) channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
-  else if (L.centered) channel_norm_pk_centered<MT>(acc, *L.mu, *L.sd, NORM_EPS);
-  else channel_norm_pk<MT>(acc, *L.mu, *L.sd, NORM_EPS);
+__device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L, float mu, float sd) {
+  if constexpr (ACT >= 0) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
+  else if (L.centered) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
+  else channel_norm_pk<MT>(acc, mu, sd, NORM_EPS);
   if constexpr (ACT >= 0) act_pk_all<ACT, MT>(acc);
   else act_dispatch(L.act, [&](auto A) { act_pk_all<decltype(A)::value, MT>(acc); });
 }
@@ -130,6 +131,14 @@ __device__ __forceinline__ int swz(int row) {
 template <int ACT>
 __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[6];  // (mu, sd) of the three channel_normalizations
+  if (threadIdx.x == 0) {  // static layer indices: a dynamic a.L[i] would copy a to scratch
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      nrm[2 * l] = *a.L[l].mu;
+      nrm[2 * l + 1] = *a.L[l].sd;
+    }
+  }
   // stage weights (static indices)
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
@@ -193,19 +202,19 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
 
     // ---- edge tiles, software pipelined: while tile t computes, the rows of tile t+1
-    //      (x[src], e) and the indices of tile t+2 are in flight.  Lanes past the end
-    //      of the block's edges load the last edge (finite data) and aggregate into the
-    //      unused slot 31.
-    int di_n = 0, sj_n = 0;
+    //      (x[src], e) and the indices of tile t+2 are in flight.  The loop is unrolled
+    //      by two with separate A / B registers for rows AND indices, so no loaded value
+    //      is ever copied (a copy would wait for the load and serialise the pipeline).
+    //      Lanes past the end of the block's edges load the last edge (finite data) and
+    //      aggregate into the unused slot 31.
+    struct Idx { int di, sj; };
     auto load_idx = [&](int t0) {
       const int p = min(t0 + r, e1 - 1);
-      di_n = a.dst[p];
-      sj_n = a.src[p];
+      return Idx{a.dst[p], a.src[p]};
     };
-    auto load_rows = [&](int t0, bf16x8_t (&bb)[8], int& slot) {
+    auto load_rows = [&](int t0, const Idx& ix, bf16x8_t (&bb)[8]) {
       const int p = min(t0 + r, e1 - 1);
-      slot = di_n - n0;
-      const uint16_t* pj = a.x + (size_t)sj_n * a.ldx + 8 * h;
+      const uint16_t* pj = a.x + (size_t)ix.sj * a.ldx + 8 * h;
       const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -219,14 +228,14 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc1[m] = ld_bias_frag(P + slot * HID, m, h);
       mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
-      if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0]);
+      if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
       bf16x8_t b2[8];
       pack_acc<4>(acc1, b2);
       f32x16 acc2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias1, m, h);
       mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
-      if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1]);
+      if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1], nrm[2], nrm[3]);
       if (RG_CONV_EXP == 3) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) agg[m] += acc2[m];
@@ -286,23 +295,22 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 
     if (e0 < e1) {
       bf16x8_t bA[8], bB[8];
-      int slotA = 0, slotB = 0;
-      load_idx(e0);
-      load_rows(e0, bA, slotA);
-      if (e0 + 32 < e1) load_idx(e0 + 32);
+      Idx iA = load_idx(e0);
+      load_rows(e0, iA, bA);
+      Idx iB = load_idx(e0 + 32);  // clamped: harmless when the block has one tile
       for (int t0 = e0;;) {
+        const int slotA = iA.di - n0;
         if (t0 + 32 < e1) {
-          if (RG_CONV_EXP != 1) load_rows(t0 + 32, bB, slotB);
-          else slotB = slotA;
-          if (t0 + 64 < e1) load_idx(t0 + 64);
+          if (RG_CONV_EXP != 1) load_rows(t0 + 32, iB, bB);
+          if (t0 + 64 < e1) iA = load_idx(t0 + 64);
         }
         compute(bA, slotA, t0);
         t0 += 32;
         if (t0 >= e1) break;
+        const int slotB = iB.di - n0;
         if (t0 + 32 < e1) {
-          if (RG_CONV_EXP != 1) load_rows(t0 + 32, bA, slotA);
-          else slotA = slotB;
-          if (t0 + 64 < e1) load_idx(t0 + 64);
+          if (RG_CONV_EXP != 1) load_rows(t0 + 32, iA, bA);
+          if (t0 + 64 < e1) iB = load_idx(t0 + 64);
         }
         compute(RG_CONV_EXP != 1 ? bB : bA, slotB, t0);
         t0 += 32;
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(bias2, m, h);
     mfma_steps<8, 2, 8, 0>(bu, accu, w2, lane);
-    norm_act<ACT, 2>(accu, a.L[2]);
+    norm_act<ACT, 2>(accu, a.L[2], nrm[4], nrm[5]);
     if (nvalid) {
       uint16_t* po = a.x_out + (size_t)node * a.ldo;
       const uint16_t* pr = a.x + (size_t)node * a.ldx;
@@ -408,7 +416,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
   if (n_nodes <= 0) return RG_OK;
   const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
-  RG_REQUIRE(lds <= 160 * 1024, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
+  RG_REQUIRE(lds <= DYN_LDS_MAX, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
   // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
   // blocks selects the compile-time variant; anything else dispatches per layer
   const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY &&
@@ -417,7 +425,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   static bool attr[2] = {false, false};
   if (!attr[leaky]) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024));
+                                     DYN_LDS_MAX));
     attr[leaky] = true;
   }
   RG_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(int), st));

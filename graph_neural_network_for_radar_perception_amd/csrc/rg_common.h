@@ -71,6 +71,10 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 __device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
 __device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 
+// dynamic LDS a kernel may request: 160 KiB per CU minus room for the few static
+// __shared__ scalars the fused kernels keep (norm parameters)
+static constexpr int DYN_LDS_MAX = 160 * 1024 - 1024;
+
 // MFMA operand / accumulator vector types
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -217,15 +221,17 @@ __device__ __forceinline__ void act_pk_all(f32x16 (&acc)[MT]) {
     for (int i = 0; i < 8; ++i) set_pair(acc[m], i, act_pk<ACT>(pair(acc[m], i)));
 }
 
-// normalisation (if mu) + activation; ACT >= 0: compile-time activation applied when
+// normalisation (if has_norm; mu / sd are the channel_normalization scalars, read once
+// per kernel -- a per-tile load of them would be a vector-memory load whose wait also
+// drains every prefetch in flight) + activation; ACT >= 0: compile-time activation applied when
 // act == ACT (any other act is the identity, as checked by the launchers); ACT < 0:
 // one run-time dispatch
 template <int ACT, int MT>
-__device__ __forceinline__ void norm_act_rows(f32x16 (&acc)[MT], const float* mu, const float* sd,
+__device__ __forceinline__ void norm_act_rows(f32x16 (&acc)[MT], bool has_norm, float mu, float sd,
                                               int act, float eps, bool centered) {
-  if (mu) {
-    if (centered) channel_norm_pk_centered<MT>(acc, *mu, *sd, eps);
-    else channel_norm_pk<MT>(acc, *mu, *sd, eps);
+  if (has_norm) {
+    if (centered) channel_norm_pk_centered<MT>(acc, mu, sd, eps);
+    else channel_norm_pk<MT>(acc, mu, sd, eps);
   }
   if constexpr (ACT >= 0) {
     if (act == ACT) act_pk_all<ACT, MT>(acc);
