@@ -78,19 +78,32 @@ __device__ __forceinline__ bf16x8_t zero_bf8() {
 }
 
 // k-steps [S0, S0 + KS) of a packed 32x32x16 layer with KT k-steps in total
-// (fragment (m, s) at byte (m * KT + s) * 1024); acc holds the initial values
+// (fragment (m, s) at byte (m * KT + s) * 1024); acc holds the initial values.
+// Software pipelined: the A fragments of step s+1 are read from LDS while the MFMAs of
+// step s issue, so an MFMA never waits for the LDS read that feeds it; one scheduling
+// fence per step keeps the compiler from hoisting the whole layer's fragments.
 template <int KS, int MT, int KT, int S0>
 __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
                                            int lane) {
   const char* wl = w + lane * 16;
+  bf16x8_t acur[MT], anxt[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0) * 1024));
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const bf16x8_t av = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s) * 1024));
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, b[s], acc[m], 0, 0, 0);
+      for (int m = 0; m < MT; ++m)
+        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s + 1) * 1024));
     }
-    if (s & 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
+    }
   }
 }
 
@@ -162,41 +175,22 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   const float* bias1 = (const float*)(w1 + 2 * 8 * 1024);
   const float* bias2 = (const float*)(w2 + 2 * 8 * 1024);
 
-  for (;;) {
-    int blk = 0;
-    if (lane == 0) blk = atomicAdd(a.counter, 1);
-    blk = __shfl(blk, 0, 64);
-    if (blk >= a.n_blocks) break;
+  // block ids come from an atomic counter (dynamic balance); the NEXT block's id and
+  // edge range are fetched at the start of the current block, so a block starts with
+  // two dependent global round trips (indices -> rows) instead of four
+  int blk = 0;
+  if (lane == 0) blk = atomicAdd(a.counter, 1);
+  blk = __shfl(blk, 0, 64);
+  int e0 = 0, e1 = 0;
+  if (blk < a.n_blocks) {
+    e0 = a.seg_ptr[blk * NB];
+    e1 = a.seg_ptr[min(blk * NB + NB, a.n_nodes)];
+  }
+  while (blk < a.n_blocks) {
     const int n0 = blk * NB;
     const int n1 = min(n0 + NB, a.n_nodes);
-    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
-
-    // ---- P[node] = W1[:, x_i part] x[node] + b1 for the block's nodes: the x_i = x[dst]
-    //      third of the message MLP's first layer is the same for every edge into a node,
-    //      so it is computed once per node here instead of once per edge
-    {
-      const int node = min(n0 + r, n1 - 1);
-      const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
-      bf16x8_t bx[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
-      f32x16 accp[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
-      mfma_steps<4, 4, 12, 0>(bx, accp, w0, lane);
-      if (r < NB) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          f32x4* pw = (f32x4*)(P + r * HID + (2 * m + h) * 16);
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            pw[q] = (f32x4){accp[m][4 * q], accp[m][4 * q + 1], accp[m][4 * q + 2], accp[m][4 * q + 3]};
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the whole wave
-      __builtin_amdgcn_wave_barrier();
-    }
-
+    int nxt_raw = 0;
+    if (lane == 0) nxt_raw = atomicAdd(a.counter, 1);
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
@@ -293,11 +287,48 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       __builtin_amdgcn_wave_barrier();
     };
 
+    bf16x8_t bA[8], bB[8];
+    Idx iA{0, 0}, iB{0, 0};
     if (e0 < e1) {
-      bf16x8_t bA[8], bB[8];
-      Idx iA = load_idx(e0);
-      load_rows(e0, iA, bA);
-      Idx iB = load_idx(e0 + 32);  // clamped: harmless when the block has one tile
+      iA = load_idx(e0);
+      iB = load_idx(e0 + 32);  // clamped: harmless when the block has one tile
+    }
+    // ---- P[node] = W1[:, x_i part] x[node] + b1 for the block's nodes: the x_i = x[dst]
+    //      third of the message MLP's first layer is the same for every edge into a node,
+    //      so it is computed once per node here instead of once per edge
+    {
+      const int node = min(n0 + r, n1 - 1);
+      const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
+      bf16x8_t bx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
+      f32x16 accp[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
+      // tile 0's rows go out while P is computed (their indices were issued above)
+      if (e0 < e1) load_rows(e0, iA, bA);
+      mfma_steps<4, 4, 12, 0>(bx, accp, w0, lane);
+      if (r < NB) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          f32x4* pw = (f32x4*)(P + r * HID + (2 * m + h) * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pw[q] = (f32x4){accp[m][4 * q], accp[m][4 * q + 1], accp[m][4 * q + 2], accp[m][4 * q + 3]};
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the whole wave
+      __builtin_amdgcn_wave_barrier();
+    }
+
+    const int nxt = __shfl(nxt_raw, 0, 64);
+    int ne0 = 0, ne1 = 0;
+    if (nxt < a.n_blocks) {
+      ne0 = a.seg_ptr[nxt * NB];
+      ne1 = a.seg_ptr[min(nxt * NB + NB, a.n_nodes)];
+    }
+
+    if (e0 < e1) {
       for (int t0 = e0;;) {
         const int slotA = iA.di - n0;
         if (t0 + 32 < e1) {
@@ -358,6 +389,9 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
           *(uint2*)(po + f0) = o;
         }
     }
+    blk = nxt;
+    e0 = ne0;
+    e1 = ne1;
   }
 }
 

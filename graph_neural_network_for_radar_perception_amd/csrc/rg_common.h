@@ -118,6 +118,14 @@ __device__ __forceinline__ void act_dispatch(int act, F&& f) {
 // ---------------------------------------------------------------------------
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// x[lane] + x[lane ^ 32] with v_permlane32_swap (a VALU lane exchange on gfx950; the
+// generic __shfl_xor goes through ds_bpermute and an LDS round trip on the critical path)
+__device__ __forceinline__ float add_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // the 16 bias values of M-tile m, lane half h, from a fast-format bias stored in
 // accumulator order (rg_pack_linear, pack_bias_frag_kernel): four 16-B reads
 __device__ __forceinline__ f32x16 ld_bias_frag(const float* bias, int m, int h) {
@@ -160,7 +168,7 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
     }
   const f32x2 st = s0 + s1;
   float s = st.x + st.y;
-  s += __shfl_xor(s, 32, 64);
+  s = add_xor32(s);
   const float mean = s * (1.f / N);  // N is a power of two: exact
   const f32x2 nm = {-mean, -mean};
   f32x2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
@@ -174,7 +182,7 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
     }
   const f32x2 qt = q0 + q1;
   float ss = qt.x + qt.y;
-  ss += __shfl_xor(ss, 32, 64);
+  ss = add_xor32(ss);
   const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
   // s*(x-mean)/(std+eps) + m as ONE fma per feature: x*gs + (m - mean*gs)
   const float gs = sd * inv, gb = fmaf(-mean, gs, mu);
@@ -203,7 +211,7 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
     }
   const f32x2 qt = q0 + q1;
   float ss = qt.x + qt.y;
-  ss += __shfl_xor(ss, 32, 64);
+  ss = add_xor32(ss);
   const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
   const float gs = sd * inv;
   const f32x2 gs2 = {gs, gs}, mu2 = {mu, mu};
