@@ -47,7 +47,7 @@ def parse():
     p.add_argument('--k', type=int, default=32)
     p.add_argument('--layers', type=int, default=6)
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    p.add_argument('--cpu-frames', type=int, default=2, help='CPU baseline sample (frames)')
+    p.add_argument('--cpu-frames', type=int, default=5, help='CPU baseline sample (timed frames)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
     return p.parse_args()
@@ -130,38 +130,66 @@ def pmc_traffic(args, kernel_substr):
     return None, None
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def cpu_baseline(args, cfg):
     """The oracle (numpy dense graph build + op-for-op torch fp32 forward, i.e. the
-    reference's own CPU algorithm) on a bounded sample of the same workload."""
+    reference's own CPU algorithm) on a bounded sample of the same workload
+    (2 warm-up frames, median of the timed frames, graph build and
+    forward reported separately, plus a 1-thread forward on one frame)."""
     from oracle import gnn_forward_ref, graph_features_ref as gref
     threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    model = None
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
     torch.manual_seed(1234)
     model = Model_Training(cfg, 'cpu')
     sd = {k: v.detach() for k, v in model.state_dict().items()}
+    warm = 2
     frames = [synthetic.make_frame(args.nodes, args.seed + 10**6 + i)
-              for i in range(args.cpu_frames + 1)]
-    times = []
+              for i in range(args.cpu_frames + warm)]
     gmax = float(np.sqrt(np.float64(cfg.max_x ** 2 + cfg.max_y ** 2)))
-    for i, fr in enumerate(frames):
+
+    def one(fr):
         t0 = time.perf_counter()
         g = gref.build_frame_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points, gmax)
+        t1 = time.perf_counter()
         cl = [torch.from_numpy(c) for c in synthetic.cluster_lists(args.nodes)]
         with torch.no_grad():
             gnn_forward_ref.forward(sd, cfg, torch.from_numpy(g['node_features']),
                                     torch.from_numpy(g['edge_features']),
                                     torch.from_numpy(g['edge_index']),
                                     torch.from_numpy(g['adj_matrix']), cl)
-        if i > 0:  # first frame = warm-up
-            times.append(time.perf_counter() - t0)
-    sec = float(np.median(times))
-    return {'value': round(1.0 / sec, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{len(times)} frame(s) of {args.nodes} nodes, k={args.k}, L={args.layers} '
-                      f'after 1 warm-up frame: oracle graph build (dense numpy, '
+        return t1 - t0, time.perf_counter() - t1
+
+    torch.set_num_threads(threads)
+    tb, tf = [], []
+    for i, fr in enumerate(frames):
+        b_, f_ = one(fr)
+        if i >= warm:
+            tb.append(b_)
+            tf.append(f_)
+    build_ms = float(np.median(tb)) * 1e3
+    fwd_ms = float(np.median(tf)) * 1e3
+    total_ms = float(np.median(np.array(tb) + np.array(tf))) * 1e3
+    torch.set_num_threads(1)
+    _, f1 = one(frames[0])
+    torch.set_num_threads(threads)
+    return {'value': round(1e3 / total_ms, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'graph_build_ms': round(build_ms, 1), 'forward_ms': round(fwd_ms, 1),
+            'forward_only_frames_per_s': round(1e3 / fwd_ms, 4),
+            'forward_1thread_ms': round(f1 * 1e3, 1), 'cpu_model': _cpu_model(),
+            'sample': f'{len(tb)} frame(s) of {args.nodes} nodes, k={args.k}, L={args.layers} '
+                      f'after {warm} warm-up frames: oracle graph build (dense numpy, '
                       f'graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
-                      f'{sec * 1e3:.0f} ms/frame, torch threads={threads}'}
+                      f'{total_ms:.0f} ms/frame at torch threads={threads}; the forward also '
+                      f'timed on 1 thread (1 frame)'}
 
 
 def main():
