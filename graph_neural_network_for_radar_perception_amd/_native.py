@@ -62,6 +62,12 @@ _SIGNATURES = {
     'rg_pairs_from_edge_index_workspace_size': (_S, [_L]),
     'rg_pairs_from_edge_index': (_I, [_P, _L, _P, _P, _P, _P, _S, _P]),
     'rg_csr_rows': (_I, [_P, _I, _P, _P]),
+    'rg_proposal_centres': (_I, [_P, _I, _P, _I, _I, _F, _F, _F, _F, _P, _P, _P]),
+    'rg_cluster_radius_workspace_size': (_S, [_I, _I, _I]),
+    'rg_cluster_radius': (_I, [_P, _P, _P, _I, _I, _I, _F, _P, _P, _S, _P]),
+    'rg_cluster_pairs': (_I, [_P, _P, _P, _P, _P, _L, _P, _I, _F, _I, _P, _P]),
+    'rg_cluster_lists_workspace_size': (_S, [_I]),
+    'rg_cluster_lists': (_I, [_P, _I, _P, _P, _P, _P, _P, _S, _P]),
     'rg_csr_by_dst_workspace_size': (_S, [_I, _L]),
     'rg_csr_by_dst': (_I, [_P, _L, _I, _P, _P, _P, _P, _S, _P]),
     'rg_dense_adjacency': (_I, [_P, _P, _P, _P, _I, _P, _P, _P]),

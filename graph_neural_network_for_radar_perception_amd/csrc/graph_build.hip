@@ -512,6 +512,88 @@ __global__ __launch_bounds__(256) void row_emit(const int* __restrict__ row_base
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Connected components for the proposal branch (Simple_DBSCAN, clustering.py:43-93:
+// breadth-first components of the eps-graph on predicted centres, numbered by each
+// component's lowest node index).  Lock-free union-find: a union hooks the LARGER root
+// under the smaller one with atomicCAS, so a root only ever gains a smaller parent and
+// every component's final root is its minimum node index -- the label is independent
+// of thread timing.  parent[x] <= x holds throughout, so finds always terminate.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ int cc_find(volatile int* parent, int x) {
+  for (;;) {
+    const int p = parent[x];
+    if (p == x) return x;
+    const int gp = parent[p];
+    if (gp == p) return p;
+    parent[x] = gp;  // path halving: stores an ancestor, a benign race
+    x = gp;
+  }
+}
+
+__device__ __forceinline__ void cc_union(int* parent, int a, int b) {
+  int ra = cc_find(parent, a), rb = cc_find(parent, b);
+  while (ra != rb) {
+    if (ra > rb) { const int t = ra; ra = rb; rb = t; }
+    const int old = atomicCAS(parent + rb, rb, ra);
+    if (old == rb) return;
+    rb = cc_find(parent, old);
+    ra = cc_find(parent, ra);
+  }
+}
+
+__global__ void cc_init(int* __restrict__ parent, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) parent[i] = i;
+}
+
+// eps-graph edges (squared distance <= eps2, clustering.py:26-39) found by the same
+// ring search as the ball query, one thread per point in cell order
+__global__ __launch_bounds__(KNN_BLOCK) void cc_radius_hook(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, float eps2, int* parent) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_nodes) return;
+  const int f = row_frame[t];
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
+  const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
+  for (int r = 0; r <= rmax; ++r) {
+    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+      const int j = __float_as_int(q.z);
+      if (j > il && sqdist(me.x, me.y, q.x, q.y) <= eps2) cc_union(parent, base + il, base + j);
+    });
+    if (eps2 < ring_bound(g, r)) break;
+  }
+}
+
+// predicted links (argmax of the 2-class logits == 1, gnn_detector.py:158-159) among the
+// link pairs, dropped when sqrt(dx^2 + dy^2) >= eps (clustering.py:8-23)
+__global__ void cc_pairs_hook(const float* __restrict__ px, const float* __restrict__ py,
+                              const int* __restrict__ pair_src, const int* __restrict__ pair_dst,
+                              const int* __restrict__ n_pairs_dev, long n_pairs,
+                              const float* __restrict__ logits, int ld, float eps, int* parent) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long np_ = n_pairs_dev ? min((long)*n_pairs_dev, n_pairs) : n_pairs;
+  if (p >= np_) return;
+  if (!(logits[p * ld + 1] > logits[p * ld + 0])) return;
+  const int a = pair_src[p], b = pair_dst[p];
+  const float dx = px[a] - px[b], dy = py[a] - py[b];
+  const float dist = sqrt_rn((dx * dx) + (dy * dy));
+  if (dist >= eps) return;
+  cc_union(parent, a, b);
+}
+
+__global__ void cc_compress(int* parent, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) parent[i] = cc_find(parent, i);
+}
+
 }  // namespace rg
 
 using namespace rg;
@@ -689,6 +771,112 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   if (rc) return rc;
   row_emit<<<ceil_div(n_nodes, 4), 256, 0, st>>>(ws.row_base, ws.bits, W, n_nodes, row_ptr, col,
                                                  col_capacity);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------------- proposal clustering
+struct GridWs {
+  int* row_base;
+  int* row_frame;
+  FrameGrid* fg;
+  int* cell_cnt;
+  int* cell_start;
+  int* cursor;
+  int* cell_of;
+  float4* pts;
+  void* scan_ws;
+  int cpf;
+  long n_cells;
+};
+
+static size_t grid_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, GridWs* ws,
+                             char* base) {
+  const int cpf = cells_per_frame(max_frame_nodes);
+  const long n_cells = (long)n_frames * cpf;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += align_up(bytes);
+    return p;
+  };
+  char* p_rb = take((size_t)n_nodes * sizeof(int));
+  char* p_rf = take((size_t)n_nodes * sizeof(int));
+  char* p_fg = take((size_t)n_frames * sizeof(FrameGrid));
+  char* p_cc = take((size_t)n_cells * sizeof(int));
+  char* p_cs = take((size_t)(n_cells + 1) * sizeof(int));
+  char* p_cu = take((size_t)n_cells * sizeof(int));
+  char* p_co = take((size_t)n_nodes * sizeof(int));
+  char* p_pt = take((size_t)n_nodes * sizeof(float4));
+  char* p_sc = take(scan_workspace_bytes(max((long)n_nodes, n_cells)));
+  if (ws) {
+    ws->row_base = (int*)p_rb;
+    ws->row_frame = (int*)p_rf;
+    ws->fg = (FrameGrid*)p_fg;
+    ws->cell_cnt = (int*)p_cc;
+    ws->cell_start = (int*)p_cs;
+    ws->cursor = (int*)p_cu;
+    ws->cell_of = (int*)p_co;
+    ws->pts = (float4*)p_pt;
+    ws->scan_ws = p_sc;
+    ws->cpf = cpf;
+    ws->n_cells = n_cells;
+  }
+  return off;
+}
+
+extern "C" size_t rg_cluster_radius_workspace_size(int n_nodes, int n_frames, int max_frame_nodes) {
+  return grid_ws_layout(n_nodes, n_frames, max_frame_nodes, nullptr, nullptr);
+}
+
+extern "C" int rg_cluster_radius(const float* px, const float* py, const int* frame_ptr,
+                                 int n_nodes, int n_frames, int max_frame_nodes, float eps2,
+                                 int* labels, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(n_nodes >= 0 && n_frames >= 1 && max_frame_nodes >= 0, RG_ERR_ARG,
+             "rg_cluster_radius: bad sizes");
+  if (n_nodes == 0) return RG_OK;
+  GridWs ws;
+  const size_t need = grid_ws_layout(n_nodes, n_frames, max_frame_nodes, &ws, (char*)workspace);
+  RG_REQUIRE(workspace_bytes >= need, RG_ERR_ARG, "rg_cluster_radius: workspace %zu < %zu",
+             workspace_bytes, need);
+  row_frame_base<<<ceil_div(n_nodes, 256), 256, 0, st>>>(frame_ptr, n_frames, ws.row_base,
+                                                         ws.row_frame, n_nodes);
+  grid_setup<<<n_frames, 256, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
+  RG_CHECK_HIP(hipMemsetAsync(ws.cell_cnt, 0, (size_t)ws.n_cells * sizeof(int), st));
+  grid_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_frame, ws.fg, n_nodes,
+                                                     ws.cell_of, ws.cell_cnt);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(ws.cell_cnt, ws.n_cells, ws.cell_start, ws.cell_start + ws.n_cells,
+                          ws.scan_ws, st);
+  if (rc) return rc;
+  RG_CHECK_HIP(hipMemcpyAsync(ws.cursor, ws.cell_start, (size_t)ws.n_cells * sizeof(int),
+                              hipMemcpyDeviceToDevice, st));
+  grid_scatter<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.cell_of, n_nodes,
+                                                       ws.cursor, ws.pts);
+  cc_init<<<ceil_div(n_nodes, 256), 256, 0, st>>>(labels, n_nodes);
+  cc_radius_hook<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
+      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, eps2, labels);
+  cc_compress<<<ceil_div(n_nodes, 256), 256, 0, st>>>(labels, n_nodes);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_cluster_pairs(const float* px, const float* py, const int* pair_src,
+                                const int* pair_dst, const int* n_pairs_dev, long n_pairs,
+                                const float* link_logits, int ld_logits, float eps, int n_nodes,
+                                int* labels, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(n_nodes >= 0 && n_pairs >= 0 && ld_logits >= 2, RG_ERR_ARG,
+             "rg_cluster_pairs: bad sizes");
+  if (n_nodes == 0) return RG_OK;
+  cc_init<<<ceil_div(n_nodes, 256), 256, 0, st>>>(labels, n_nodes);
+  if (n_pairs > 0)
+    cc_pairs_hook<<<ceil_div(n_pairs, 256), 256, 0, st>>>(px, py, pair_src, pair_dst, n_pairs_dev,
+                                                          n_pairs, link_logits, ld_logits, eps,
+                                                          labels);
+  cc_compress<<<ceil_div(n_nodes, 256), 256, 0, st>>>(labels, n_nodes);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

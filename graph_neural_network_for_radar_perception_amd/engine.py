@@ -498,17 +498,22 @@ class ForwardOutputs:
     link_cls: torch.Tensor
     obj_cls: torch.Tensor
     x: torch.Tensor
+    cluster_ptr: Optional[torch.Tensor] = None   # proposal branch: the clusters used
+    cluster_idx: Optional[torch.Tensor] = None
 
 
 def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst: torch.Tensor,
                     g: DeviceGraph, cluster_ptr: torch.Tensor, cluster_idx: torch.Tensor,
                     n_clusters: int, n_pairs_cap: Optional[int] = None,
-                    buffers: Optional[dict] = None, events: Optional[list] = None) -> ForwardOutputs:
-    """Model_Inference.forward (gnn_detector.py:141-201, cluster branch) over a batch.
+                    buffers: Optional[dict] = None, events: Optional[list] = None,
+                    clusters_fn=None) -> ForwardOutputs:
+    """Model_Inference.forward (gnn_detector.py:141-201) over a batch.
 
     node_feats      float32 [N, 6]
     edge_feats_dst  float32 [E_cap, 7] in destination-major order
-    cluster_ptr/idx int32 CSR of the object-head clusters (global node ids)
+    cluster_ptr/idx int32 CSR of the object-head clusters (global node ids); None with
+                    clusters_fn(node_reg, link_cls) -> (ptr, idx, n) for the proposal
+                    branch (clusters from the predicted offsets / links)
     """
     dev = node_feats.device
     T = plans.tdtype
@@ -589,11 +594,13 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
         plans.cls_stem(N, h, x, C)
     else:
         h = x
+    if cluster_ptr is None:
+        cluster_ptr, cluster_idx, n_clusters = clusters_fn(node_reg, link)
     pooled = alloc('pooled', (n_clusters, h.shape[1]), T)
     segment_reduce(h, cluster_ptr, n_clusters, 'max', pooled, idx=cluster_idx)
     obj = torch.empty((n_clusters, plans.cls_head.out_dim), dtype=f32, device=dev)
     plans.cls_head(n_clusters, obj, pooled, pooled.shape[1])
-    return ForwardOutputs(node_cls, node_reg, link, obj, x)
+    return ForwardOutputs(node_cls, node_reg, link, obj, x, cluster_ptr, cluster_idx)
 
 
 # --------------------------------------------------------------------------- block-level
@@ -657,3 +664,68 @@ def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):
     out = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
     cp.upd(N, out, x, x.shape[1], mode=nat.IN_CONCAT2, in1=agg, w1=cp.c_msg, residual=ident)
     return out
+
+
+# --------------------------------------------------------------------------- proposals
+def propose_clusters(node_reg: torch.Tensor, other_xy: torch.Tensor, frame_ptr: torch.Tensor,
+                     frame_sizes: List[int], mu, sigma, eps: float, from_links: bool = False,
+                     g: Optional['DeviceGraph'] = None, link_cls: Optional[torch.Tensor] = None,
+                     ws_cache: Optional[dict] = None):
+    """The proposal branch of Model_Inference.forward (gnn_detector.py:164-184) for a
+    batch of frames: centres = other_xy + unnormalised offsets, Simple_DBSCAN
+    (clustering.py:43-93) as connected components on the GPU (eps-graph on the centres,
+    or the predicted links when ``from_links``), cluster lists in the reference's order.
+    Returns (cluster_ptr int32 [Ncl+1], cluster_idx int32 [N], n_clusters) -- the one
+    host synchronisation is reading n_clusters (the reference syncs here too)."""
+    lib = nat.lib()
+    dev = node_reg.device
+    N = int(node_reg.shape[0])
+    st = nat.stream_ptr(dev)
+    cache = ws_cache if ws_cache is not None else {}
+    i32 = dict(dtype=torch.int32, device=dev)
+    cx = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
+    cy = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
+    reg = node_reg.contiguous()
+    xy = other_xy.to(torch.float32)
+    if xy.stride(1) != 1:
+        xy = xy.contiguous()
+    nat.check(lib.rg_proposal_centres(reg.data_ptr(), reg.stride(0), xy.data_ptr(), xy.stride(0),
+                                      N, float(mu[0]), float(mu[1]), float(sigma[0]),
+                                      float(sigma[1]), cx.data_ptr(), cy.data_ptr(), st),
+              'rg_proposal_centres')
+    labels = torch.empty(max(N, 1), **i32)
+    if from_links:
+        if g is None or link_cls is None:
+            raise ValueError('from_links needs the batch graph and the link logits')
+        nat.check(lib.rg_cluster_pairs(cx.data_ptr(), cy.data_ptr(), g.pair_src.data_ptr(),
+                                       g.pair_dst.data_ptr(), nat.ptr(g.n_pairs_dev),
+                                       int(link_cls.shape[0]), link_cls.data_ptr(),
+                                       link_cls.stride(0), float(eps), N, labels.data_ptr(), st),
+                  'rg_cluster_pairs')
+    else:
+        nf = len(frame_sizes)
+        maxn = max(frame_sizes) if frame_sizes else 0
+        wsz = lib.rg_cluster_radius_workspace_size(N, nf, maxn)
+        ws = _workspace(cache, 'cluster_ws', wsz, dev)
+        nat.check(lib.rg_cluster_radius(cx.data_ptr(), cy.data_ptr(), frame_ptr.data_ptr(), N, nf,
+                                        maxn, float(eps), labels.data_ptr(), ws.data_ptr(), wsz,
+                                        st), 'rg_cluster_radius')
+    cluster_of = torch.empty(max(N, 1), **i32)
+    cptr = torch.empty(N + 1, **i32)
+    cidx = torch.empty(max(N, 1), **i32)
+    ncl_dev = torch.zeros(1, **i32)
+    lsz = lib.rg_cluster_lists_workspace_size(N)
+    lws = _workspace(cache, 'cluster_list_ws', lsz, dev)
+    nat.check(lib.rg_cluster_lists(labels.data_ptr(), N, cluster_of.data_ptr(), cptr.data_ptr(),
+                                   cidx.data_ptr(), ncl_dev.data_ptr(), lws.data_ptr(), lsz, st),
+              'rg_cluster_lists')
+    ncl = int(ncl_dev.item())
+    return cptr[:ncl + 1], cidx[:N], ncl
+
+
+def _workspace(cache: dict, name: str, nbytes: int, dev) -> torch.Tensor:
+    t = cache.get(name)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        cache[name] = t
+    return t

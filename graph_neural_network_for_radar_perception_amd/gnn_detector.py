@@ -16,6 +16,7 @@ from __future__ import annotations
 from collections import namedtuple
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -106,8 +107,11 @@ class Model_Inference(nn.Module):
             setattr(self, name, self.freeze_weights(getattr(self, name)))
 
     def set_param_for_proposal_extraction(self, eps, compute_adj_mat_from_links):
+        """gnn_detector.py:135-139 (Simple_DBSCAN(eps, compute_adj_mat_from_links) runs on the
+        GPU: engine.propose_clusters)."""
         self.compute_adj_mat_from_links = compute_adj_mat_from_links
         self.extract_proposals = True
+        self.meas_noise_cov = np.array([[0.5, 0.0], [0.0, 0.5]], dtype=np.float32)
         self.clustering_eps = eps
 
     def plans(self, dtype: Optional[str] = None) -> engine.ModelPlans:
@@ -122,16 +126,24 @@ class Model_Inference(nn.Module):
         return p
 
     def forward_frames(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
-                       edge_index: List[torch.Tensor], cluster_node_idx: List[List[torch.Tensor]]):
+                       edge_index: List[torch.Tensor],
+                       cluster_node_idx: Optional[List[List[torch.Tensor]]],
+                       other_features: Optional[List[torch.Tensor]] = None):
         """Batched forward over several frames; returns per-batch concatenated
         (node_cls, node_reg, link_cls, obj_cls) exactly as Model_Training.forward
-        concatenates the per-frame outputs (gnn_detector.py:454-457)."""
+        concatenates the per-frame outputs (gnn_detector.py:454-457).  With
+        ``cluster_node_idx=None`` the object head runs on the proposal clusters
+        (gnn_detector.py:164-187; needs ``other_features`` and extract_proposals) and a
+        fifth value, the per-frame cluster member lists, is returned."""
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             raise NotImplementedError(
                 'backward through the HIP forward is not implemented yet (training path is '
                 'the next milestone); run inference under torch.no_grad() or model.eval() with '
                 'requires_grad_(False)')
         engine._require_device(node_features[0], 'node_features')
+        proposals = cluster_node_idx is None
+        if proposals:
+            cluster_node_idx = [[] for _ in node_features]
         nf, ef, ei, cptr, cidx, ncl, sizes = _batch_frames(node_features, edge_features,
                                                            edge_index, cluster_node_idx)
         N = nf.shape[0]
@@ -144,9 +156,44 @@ class Model_Inference(nn.Module):
                                                    ef.shape[1], e_dst.data_ptr(),
                                                    nat.stream_ptr(nf.device)),
                       'rg_gather_rows_f32')
+        clusters_fn = None
+        if proposals:
+            other_xy = torch.cat([o[:, :2].to(torch.float32) for o in other_features], 0)
+            fptr = torch.tensor([0] + sizes, dtype=torch.int64).cumsum(0).to(torch.int32)
+            fptr = fptr.to(nf.device)
+
+            def clusters_fn(node_reg, link_cls):
+                return engine.propose_clusters(
+                    node_reg, other_xy, fptr, sizes, self.reg_mu, self.reg_sigma,
+                    self.clustering_eps, from_links=self.compute_adj_mat_from_links, g=g,
+                    link_cls=link_cls[:g.n_pairs])
+            cptr, cidx, ncl = None, None, 0
         out = engine.forward_batched(self.plans(), nf, e_dst, g, cptr, cidx, ncl,
-                                     n_pairs_cap=g.n_pairs)
-        return out.node_cls, out.node_reg, out.link_cls[:g.n_pairs], out.obj_cls
+                                     n_pairs_cap=g.n_pairs, clusters_fn=clusters_fn)
+        res = (out.node_cls, out.node_reg, out.link_cls[:g.n_pairs], out.obj_cls)
+        if not proposals:
+            return res
+        # per-frame member lists with frame-local indices, int64 (gnn_detector.py:180-184):
+        # one device op for the local indices, one host copy for the split points, then
+        # views (no launch per cluster)
+        ptr = out.cluster_ptr.cpu().tolist()
+        idx = out.cluster_idx.to(torch.int64)
+        bases = [0]
+        for sz in sizes:
+            bases.append(bases[-1] + sz)
+        node_base = torch.repeat_interleave(
+            torch.tensor(bases[:-1], dtype=torch.int64, device=idx.device),
+            torch.tensor(sizes, dtype=torch.int64, device=idx.device))
+        local = idx - node_base[idx]
+        first = idx[torch.tensor(ptr[:-1], dtype=torch.int64, device=idx.device)].cpu().tolist() \
+            if len(ptr) > 1 else []
+        lists = [[] for _ in sizes]
+        f = 0
+        for c in range(len(ptr) - 1):
+            while first[c] >= bases[f + 1]:
+                f += 1
+            lists[f].append(local[ptr[c]:ptr[c + 1]])
+        return res + (lists,)
 
     def forward(self, node_features: torch.Tensor, edge_features: torch.Tensor,
                 edge_index: torch.Tensor, adj_matrix: torch.Tensor,
@@ -162,8 +209,12 @@ class Model_Inference(nn.Module):
                 # reference: self.compute_adj_mat_from_links is never set -> AttributeError
                 raise AttributeError("'Model_Inference' object has no attribute "
                                      "'compute_adj_mat_from_links'")
-            raise NotImplementedError('proposal branch (offsets -> Simple_DBSCAN -> clusters, '
-                                      'gnn_detector.py:164-187) is not built yet')
+            if other_features is None:
+                # reference: other_features[:, :2] on None
+                raise TypeError("'NoneType' object is not subscriptable")
+            node_cls, node_reg, link_cls, obj_cls, lists = self.forward_frames(
+                [node_features], [edge_features], [edge_index], None, [other_features])
+            return node_cls, node_reg, link_cls, obj_cls, lists[0]
         node_cls, node_reg, link_cls, obj_cls = self.forward_frames(
             [node_features], [edge_features], [edge_index], [cluster_node_idx])
         if self.extract_proposals:

@@ -241,6 +241,43 @@ int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg
                       const int* idx, int n_seg, int C, int op, void* out, int out_dtype,
                       int ld_out, void* stream);
 
+
+/* ------------------------------------------------------------ proposal branch */
+
+/* Predicted cluster centres (gnn_detector.py:164-167): unnormalize_gt_offsets
+ * (compute_offsets.py:13-17, offset * sigma + mu) added to other_features[:, :2];
+ * float32, no FMA.  offsets: f32 [N][ld_off] (node_offsets_predictions), xy: f32
+ * [N][ld_xy]; cx, cy: f32 [N]. */
+int rg_proposal_centres(const float* offsets, int ld_off, const float* xy, int ld_xy, int n_nodes,
+                        float mu_x, float mu_y, float sigma_x, float sigma_y, float* cx,
+                        float* cy, void* stream);
+
+/* Connected components of the eps-graph on the centres, per frame
+ * (Simple_DBSCAN with compute_adjacency_mat_from_predicted_offsets, clustering.py:26-93:
+ * an edge where the SQUARED distance <= eps2).  labels: int32 [N], label = the
+ * component's lowest global node index. */
+size_t rg_cluster_radius_workspace_size(int n_nodes, int n_frames, int max_frame_nodes);
+int rg_cluster_radius(const float* px, const float* py, const int* frame_ptr, int n_nodes,
+                      int n_frames, int max_frame_nodes, float eps2, int* labels,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* Connected components over predicted links (compute_adjacency_mat_from_predicted_edges,
+ * clustering.py:8-23): pair p = (pair_src[p], pair_dst[p]) is an edge when
+ * link_logits[p][1] > link_logits[p][0] (the argmax of gnn_detector.py:158-159) and
+ * sqrt(dx^2 + dy^2) < eps on the centres.  labels as rg_cluster_radius. */
+int rg_cluster_pairs(const float* px, const float* py, const int* pair_src, const int* pair_dst,
+                     const int* n_pairs_dev, long n_pairs, const float* link_logits,
+                     int ld_logits, float eps, int n_nodes, int* labels, void* stream);
+
+/* Cluster ids in the reference's order (ascending lowest node index; frames are
+ * concatenated, each numbered from its own first cluster) and the member lists,
+ * ascending (gnn_detector.py:180-184): cluster_of int32 [N], cluster_ptr int32 [N+1]
+ * (entries past *n_clusters repeat N), cluster_idx int32 [N], *n_clusters device int. */
+size_t rg_cluster_lists_workspace_size(int n_nodes);
+int rg_cluster_lists(const int* labels, int n_nodes, int* cluster_of, int* cluster_ptr,
+                     int* cluster_idx, int* n_clusters, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

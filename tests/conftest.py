@@ -27,6 +27,7 @@ def golden_names(prefix):
 MODEL_CASES = {
     'model_trained_N50': dict(),
     'model_trained_N500': dict(),
+    'proposals_model_trained_N300': dict(),
     'model_random_L3_N500_k16': dict(graph_convolution_stem_channels=[64, 64, 64],
                                      k_number_nearest_points=16),
     'model_random_L6_N300_k32': dict(graph_convolution_stem_channels=[64] * 6),

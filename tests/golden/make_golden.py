@@ -258,12 +258,73 @@ def make_model_fixtures():
                   save_weights=True, intermediates=True)
 
 
+def make_proposal_fixtures():
+    """Simple_DBSCAN (clustering.py:43-93) on predicted centres, both adjacency modes,
+    and the full proposal branch of Model_Inference (gnn_detector.py:164-195)."""
+    from modules.inference.clustering import Simple_DBSCAN
+    from modules.compute_groundtruth.compute_offsets import unnormalize_gt_offsets
+    from modules.compute_features.graph_features import compute_adjacency_information
+    from modules.set_configurations.set_config_gnn import config
+    cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+    mu, sigma, eps = cfg.reg_mu, cfg.reg_sigma, float(cfg.clustering_eps)
+    for n, seed in ((400, 6001), (1500, 6002)):
+        fr = synthetic.make_frame(n, seed)
+        rng = np.random.default_rng(seed)
+        offsets = rng.normal(0.0, 0.15, (n, 2)).astype(np.float32)
+        other_xy = np.stack([fr['meas_px'], fr['meas_py']], -1).astype(np.float32)
+        deltas = unnormalize_gt_offsets(torch.from_numpy(offsets).clone(), mu, sigma)
+        centres = (torch.from_numpy(other_xy) + deltas).numpy()
+        db = Simple_DBSCAN(eps)
+        db.cluster_nodes(centres)
+        ids_off = db.meas_to_cluster_id.astype(np.int64)
+        adj = compute_adjacency_information(fr, 25.0, 10)
+        r, c = np.nonzero(np.triu(adj['adj_matrix'], k=1))
+        pred_edges = (rng.random(r.shape[0]) < 0.6).astype(np.int64)
+        db2 = Simple_DBSCAN(eps, compute_adj_mat_from_links=True)
+        db2.cluster_nodes(centres, pred_edges.copy(), adj['adj_matrix'])
+        ids_links = db2.meas_to_cluster_id.astype(np.int64)
+        np.savez_compressed(os.path.join(HERE, f'proposals_dbscan_N{n}.npz'),
+                            other_xy=other_xy, offsets=offsets, mu=np.array(mu, np.float64),
+                            sigma=np.array(sigma, np.float64), eps=eps, centres=centres,
+                            ids_offsets=ids_off, ids_links=ids_links, pred_edges=pred_edges,
+                            adj_list=adj['adj_list'].astype(np.int32))
+        print('proposals', n, 'clusters', ids_off.max() + 1, ids_links.max() + 1)
+    # full branch with the trained checkpoint
+    n, k = 300, 10
+    fr = synthetic.make_frame(n, 5007)
+    adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, k)
+    model = _model(cfg, ckpt=CKPT)
+    other = np.stack([fr['meas_px'], fr['meas_py'], fr['meas_vx'], fr['meas_vy']], -1).astype(np.float32)
+    data = dict(_frame_arrays(fr))
+    data.update(n=n, k=k, eps_graph=float(cfg.ball_query_eps_square), eps=eps,
+                node_features=nf.astype(np.float32), edge_features=ef.astype(np.float32),
+                edge_index=adj['adj_list'].astype(np.int32), other_features=other)
+    for tag, links in (('off', False), ('links', True)):
+        model.pred.set_param_for_proposal_extraction(eps, links)
+        with torch.no_grad():
+            outs = model.pred(torch.from_numpy(nf).float(), torch.from_numpy(ef).float(),
+                              torch.from_numpy(adj['adj_list']).long(),
+                              torch.from_numpy(adj['adj_matrix']), None,
+                              other_features=torch.from_numpy(other))
+        cl = outs[4]
+        data.update({f'{tag}/node_cls': outs[0].numpy(), f'{tag}/node_reg': outs[1].numpy(),
+                     f'{tag}/link_cls': outs[2].numpy(), f'{tag}/obj_cls': outs[3].numpy(),
+                     f'{tag}/cluster_ptr': np.cumsum([0] + [len(c) for c in cl]).astype(np.int64),
+                     f'{tag}/cluster_idx': np.concatenate([c.numpy() for c in cl]).astype(np.int64)})
+        print('model proposals', tag, 'clusters', len(cl))
+    for k_, v in model.state_dict().items():
+        data['w/' + k_] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, 'proposals_model_trained_N300.npz'), **data)
+
+
 def main():
     sys.path.insert(0, REF)
     _install_third_party_restatements()
     torch.set_num_threads(8)
-    make_graph_fixtures()
-    make_model_fixtures()
+    if '--proposals-only' not in sys.argv:
+        make_graph_fixtures()
+        make_model_fixtures()
+    make_proposal_fixtures()
 
 
 if __name__ == '__main__':

@@ -570,3 +570,100 @@ def test_fused_conv_layer_matches_unfused(cuda_device, aggr):
     torch.testing.assert_close(of, ou, rtol=0.03, atol=0.06)
     err = (of - ref).abs()
     assert float((err <= 0.05 + 0.03 * ref.abs()).float().mean()) >= 0.995, float(err.max())
+
+
+# ------------------------------------------------------------------------ proposal branch
+def _lists_from_ids(ids):
+    ids = np.asarray(ids)
+    return [np.nonzero(ids == i)[0] for i in range(int(ids.max()) + 1)]
+
+
+def _assert_same_lists(got_ptr, got_idx, want_lists, base=0):
+    got_ptr = np.asarray(got_ptr)
+    got_idx = np.asarray(got_idx)
+    assert len(got_ptr) - 1 == len(want_lists), (len(got_ptr) - 1, len(want_lists))
+    for i, w in enumerate(want_lists):
+        np.testing.assert_array_equal(got_idx[got_ptr[i]:got_ptr[i + 1]] - base, w)
+
+
+@pytest.mark.parametrize('name', golden_names('proposals_dbscan'))
+def test_proposal_clusters_match_reference_dbscan(cuda_device, name):
+    """rg_proposal_centres + rg_cluster_radius / rg_cluster_pairs + rg_cluster_lists ==
+    the reference's Simple_DBSCAN (clustering.py:43-93), both adjacency modes, and the
+    centres bit-exact (compute_offsets.py:13-17)."""
+    from graph_neural_network_for_radar_perception_amd import engine
+    import graph_neural_network_for_radar_perception_amd._native as nat
+    d = golden(name)
+    n = d['centres'].shape[0]
+    dev = cuda_device
+    off = torch.from_numpy(d['offsets']).to(dev)
+    xy = torch.from_numpy(d['other_xy']).to(dev)
+    cx = torch.empty(n, device=dev)
+    cy = torch.empty(n, device=dev)
+    nat.check(nat.lib().rg_proposal_centres(off.data_ptr(), 2, xy.data_ptr(), 2, n,
+                                            float(d['mu'][0]), float(d['mu'][1]),
+                                            float(d['sigma'][0]), float(d['sigma'][1]),
+                                            cx.data_ptr(), cy.data_ptr(), 0), 'centres')
+    np.testing.assert_array_equal(torch.stack([cx, cy], 1).cpu().numpy(), d['centres'])
+    fptr = torch.tensor([0, n], dtype=torch.int32, device=dev)
+    ptr, idx, ncl = engine.propose_clusters(off, xy, fptr, [n], d['mu'], d['sigma'],
+                                            float(d['eps']))
+    _assert_same_lists(ptr.cpu(), idx.cpu(), _lists_from_ids(d['ids_offsets']))
+    # predicted-link mode: logits whose argmax is the fixture's pred_edges
+    ei = torch.from_numpy(d['adj_list'].astype(np.int64)).to(dev)
+    g = engine.DeviceGraph.from_edge_index(ei, n)
+    pe = torch.from_numpy(d['pred_edges']).to(dev).float()
+    logits = torch.stack([1.0 - pe, pe], 1).contiguous()
+    assert logits.shape[0] == g.n_pairs
+    ptr, idx, ncl = engine.propose_clusters(off, xy, fptr, [n], d['mu'], d['sigma'],
+                                            float(d['eps']), from_links=True, g=g,
+                                            link_cls=logits)
+    _assert_same_lists(ptr.cpu(), idx.cpu(), _lists_from_ids(d['ids_links']))
+
+
+def test_proposal_clusters_batched_frames(cuda_device):
+    """Several frames in one call: per-frame components, frames concatenated in order."""
+    from graph_neural_network_for_radar_perception_amd import engine
+    ds = [golden(nm) for nm in golden_names('proposals_dbscan')]
+    dev = cuda_device
+    off = torch.from_numpy(np.concatenate([d['offsets'] for d in ds])).to(dev)
+    xy = torch.from_numpy(np.concatenate([d['other_xy'] for d in ds])).to(dev)
+    sizes = [d['offsets'].shape[0] for d in ds]
+    fptr = torch.tensor(np.cumsum([0] + sizes), dtype=torch.int32, device=dev)
+    ptr, idx, ncl = engine.propose_clusters(off, xy, fptr, sizes, ds[0]['mu'], ds[0]['sigma'],
+                                            float(ds[0]['eps']))
+    want, base = [], 0
+    for d, s in zip(ds, sizes):
+        want += [w + base for w in _lists_from_ids(d['ids_offsets'])]
+        base += s
+    _assert_same_lists(ptr.cpu(), idx.cpu(), want)
+
+
+@pytest.mark.parametrize('tag', ['off', 'links'])
+def test_model_inference_proposals_match_reference(cuda_device, tag):
+    """Model_Inference(extract_proposals=True).forward without cluster_node_idx
+    (gnn_detector.py:164-195) against the reference run: the clusters (exact, unless a
+    centre pair sits within 1e-4 of the eps threshold) and all five outputs."""
+    from oracle import proposals_ref as pref
+    d = golden('proposals_model_trained_N300')
+    m, _ = _model('proposals_model_trained_N300', cuda_device)
+    m.set_param_for_proposal_extraction(float(d['eps']), tag == 'links')
+    dev = cuda_device
+    args = (torch.from_numpy(d['node_features']).to(dev), torch.from_numpy(d['edge_features']).to(dev),
+            torch.from_numpy(d['edge_index'].astype(np.int64)).to(dev), None)
+    with torch.no_grad():
+        out = m(*args, None, other_features=torch.from_numpy(d['other_features']).to(dev))
+    assert len(out) == 5
+    for got, key in zip(out[:3], ('node_cls', 'node_reg', 'link_cls')):
+        np.testing.assert_allclose(got.cpu().numpy(), d[f'{tag}/{key}'], rtol=1e-4, atol=1e-4)
+    ptr, idx = d[f'{tag}/cluster_ptr'], d[f'{tag}/cluster_idx']
+    want = [idx[ptr[i]:ptr[i + 1]] for i in range(len(ptr) - 1)]
+    centres = pref.cluster_centres(d['other_features'][:, :2], d[f'{tag}/node_reg'], [0, 0], [8, 4])
+    dd = ((centres[:, None, :] - centres[None]) ** 2).sum(-1)
+    near = np.abs(dd - float(d['eps'])) < 1e-4
+    if not near.any():
+        got = [c.cpu().numpy() for c in out[4]]
+        assert len(got) == len(want)
+        for gw, ww in zip(got, want):
+            np.testing.assert_array_equal(gw, ww)
+        np.testing.assert_allclose(out[3].cpu().numpy(), d[f'{tag}/obj_cls'], rtol=1e-4, atol=1e-4)

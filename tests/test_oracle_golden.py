@@ -95,3 +95,63 @@ def test_pairs_from_edge_index_equal_triu():
     si, di = gnn_forward_ref.link_pairs_from_adj(adj)
     m = ei[0] < ei[1]
     assert torch.equal(si, ei[0][m]) and torch.equal(di, ei[1][m])
+
+
+# ------------------------------------------------------------------ proposal branch
+@pytest.mark.parametrize('name', golden_names('proposals_dbscan'))
+def test_proposal_oracle_matches_reference_dbscan(name):
+    """oracle/proposals_ref.py == the reference's Simple_DBSCAN (clustering.py:43-93) on
+    the same predicted centres, both adjacency modes."""
+    from oracle import proposals_ref as pref
+    d = golden(name)
+    centres = pref.cluster_centres(d['other_xy'], d['offsets'], d['mu'], d['sigma'])
+    np.testing.assert_array_equal(centres, d['centres'])
+    eps = float(d['eps'])
+    ids = pref.connected_components(pref.adjacency_from_offsets(centres, eps))
+    np.testing.assert_array_equal(ids, d['ids_offsets'])
+    n = centres.shape[0]
+    adj = np.zeros((n, n), dtype=np.bool_)
+    adj[d['adj_list'][0], d['adj_list'][1]] = True
+    ids2 = pref.connected_components(pref.adjacency_from_links(adj, centres, d['pred_edges'], eps))
+    np.testing.assert_array_equal(ids2, d['ids_links'])
+
+
+def _proposal_clusters(node_reg, other_xy, mu, sigma, eps, links, adj, link_cls):
+    from oracle import proposals_ref as pref
+    centres = pref.cluster_centres(other_xy, node_reg, mu, sigma)
+    if links:
+        pred = (link_cls[:, 1] > link_cls[:, 0]).astype(np.int64)
+        a = pref.adjacency_from_links(adj, centres, pred, eps)
+    else:
+        a = pref.adjacency_from_offsets(centres, eps)
+    return pref.cluster_lists(pref.connected_components(a)), centres
+
+
+@pytest.mark.parametrize('tag', ['off', 'links'])
+def test_proposal_branch_oracle_matches_reference(tag):
+    """Model_Inference(extract_proposals=True) (gnn_detector.py:164-195) restated by the
+    oracle: same cluster lists and object logits as the reference run."""
+    d = golden('proposals_model_trained_N300')
+    cfg = model_cfg('proposals_model_trained_N300')
+    sd = model_state_dict('proposals_model_trained_N300')
+    ei = torch.from_numpy(d['edge_index'].astype(np.int64))
+    n = int(d['n'])
+    adj = torch.zeros((n, n), dtype=torch.bool)
+    adj[ei[0], ei[1]] = True
+    with torch.no_grad():
+        out = gnn_forward_ref.forward(sd, cfg, torch.from_numpy(d['node_features']),
+                                      torch.from_numpy(d['edge_features']), ei, adj,
+                                      [torch.zeros(1, dtype=torch.int64)])
+    np.testing.assert_allclose(out[1].numpy(), d[f'{tag}/node_reg'], rtol=1e-5, atol=1e-5)
+    cl, _ = _proposal_clusters(d[f'{tag}/node_reg'], d['other_features'][:, :2], cfg.reg_mu,
+                               cfg.reg_sigma, float(d['eps']), tag == 'links', adj.numpy(),
+                               d[f'{tag}/link_cls'])
+    ptr, idx = d[f'{tag}/cluster_ptr'], d[f'{tag}/cluster_idx']
+    assert len(cl) == len(ptr) - 1
+    for i, c in enumerate(cl):
+        np.testing.assert_array_equal(c, idx[ptr[i]:ptr[i + 1]])
+    with torch.no_grad():
+        out2 = gnn_forward_ref.forward(sd, cfg, torch.from_numpy(d['node_features']),
+                                       torch.from_numpy(d['edge_features']), ei, adj,
+                                       [torch.from_numpy(c) for c in cl])
+    np.testing.assert_allclose(out2[3].numpy(), d[f'{tag}/obj_cls'], rtol=1e-5, atol=1e-5)
