@@ -34,6 +34,19 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 static constexpr float NORM_EPS = 1e-5f;
 static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layers 0+1
 
+#ifndef RG_CHAIN_EXP
+#define RG_CHAIN_EXP 0  // timing experiments only (wrong results): 1 no epilogue VALU,
+                        // 2 no MFMA (accumulators keep the bias)
+#endif
+// MFMA wrapper for the timing experiments
+__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  if constexpr (RG_CHAIN_EXP == 2) {
+    return c;
+  } else {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+}
+
 struct FLayer {
   const void* src;  // packed weights (+bias) in global memory
   const float* mu;
@@ -178,7 +191,7 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
+      acc[m] = mfma32(acur[m], b[s], acc[m]);
     __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < KS) {
 #pragma unroll
@@ -218,6 +231,7 @@ constexpr int spec(int act, int norm_mask, int act_mask) {
 // nrm: the layers' channel_normalization (mu, sd) staged in LDS at kernel start
 template <int SPEC, int LI, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, const float* nrm) {
+  if constexpr (RG_CHAIN_EXP == 1) return;
   if constexpr (SPEC >= 0) {
     if constexpr (((SPEC >> (8 + LI)) & 1) != 0)  // normalised => centred (host-checked)
       channel_norm_pk_centered<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1], NORM_EPS);
@@ -334,32 +348,61 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
 #pragma unroll
   for (int m = 0; m < MT1; ++m)
     acc[m] = ld_bias_frag(bias1, m, h);  // accumulator-order bias: 4 x ds_read_b128
+  // skewed by one layer-0 tile: the layer-0 MFMA + activation of tile m0+1 are
+  // independent of the 2*MT1 layer-1 MFMAs of tile m0, so the scheduler can issue that
+  // VALU work while the matrix pipe runs (MFMA / VALU co-execution inside one wave)
+  auto l0_tile = [&](auto A, int m0, bf16x8_t (&nb)[2]) {
+    f32x16 t = ld_bias_frag(bias0, m0, h);  // accumulator-order bias: 4 x ds_read_b128
+#pragma unroll
+    for (int s = 0; s < KS0; ++s)
+      t = mfma32(ld_bf8((const uint16_t*)(w0 + (m0 * KS0 + s) * 1024)), b[s], t);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x2 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = act_pk<decltype(A)::value>(pair(t, 4 * hf + j));
+      nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0].x, v[0].y), bf2(v[1].x, v[1].y),
+                                                    bf2(v[2].x, v[2].y), bf2(v[3].x, v[3].y)});
+    }
+  };
+  // layer-1 A fragments of layer-0 tile m0: 2*MT1 contiguous fragments, read one tile
+  // ahead (double-buffered) so no MFMA waits on its LDS read
+  auto l1_frags = [&](int m0, bf16x8_t (&f)[2 * MT1]) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int m = 0; m < MT1; ++m)
+        f[hf * MT1 + m] = ld_bf8((const uint16_t*)(w1 + (m * KS1 + 2 * m0 + hf) * 1024));
+  };
   auto body = [&](auto A) {
+    bf16x8_t ncur[2], nnxt[2];
+    bf16x8_t fcur[2 * MT1], fnxt[2 * MT1];
+    l1_frags(0, fcur);
+    l0_tile(A, 0, ncur);
 #pragma unroll
     for (int m0 = 0; m0 < MT0; ++m0) {
-      f32x16 t;
-      t = ld_bias_frag(bias0, m0, h);  // accumulator-order bias: 4 x ds_read_b128
-#pragma unroll
-      for (int s = 0; s < KS0; ++s)
-        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            ld_bf8((const uint16_t*)(w0 + (m0 * KS0 + s) * 1024)), b[s], t, 0, 0, 0);
-      bf16x8_t nb[2];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        f32x2 v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_pk<decltype(A)::value>(pair(t, 4 * hf + j));
-        nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0].x, v[0].y), bf2(v[1].x, v[1].y),
-                                                      bf2(v[2].x, v[2].y), bf2(v[3].x, v[3].y)});
+      if (m0 + 1 < MT0) {
+        l1_frags(m0 + 1, fnxt);
+        l0_tile(A, m0 + 1, nnxt);
       }
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int m = 0; m < MT1; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              ld_bf8((const uint16_t*)(w1 + (m * KS1 + 2 * m0 + hf) * 1024)), nb[hf], acc[m], 0,
-              0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // one layer-0 tile in flight: bounded registers
+          acc[m] = mfma32(fcur[hf * MT1 + m], ncur[hf], acc[m]);
+      // interleave: the next tile's activation VALU between this tile's layer-1 MFMAs
+#pragma unroll
+      for (int i = 0; i < 2 * MT1; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // 4 VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);  // two layer-0 tiles in flight: bounded registers
+      if (m0 + 1 < MT0) {
+        ncur[0] = nnxt[0];
+        ncur[1] = nnxt[1];
+#pragma unroll
+        for (int i = 0; i < 2 * MT1; ++i) fcur[i] = fnxt[i];
+      }
     }
   };
   if constexpr (SPEC >= 0) {
@@ -469,8 +512,8 @@ static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
   constexpr int L = ACT_LEAKY;
   // node / edge encoders (graph_feature_encoding, gnn_blocks.py:19-42: block 0 is not
   // normalised)
-  RG_FAST(768, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
-  RG_FAST(768, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
+  RG_FAST(512, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
+  RG_FAST(512, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
   RG_FAST(512, spec(L, 0b11, 0b11), RG_IN_GATHER3, 0, 64, 64, 128, 64)
   RG_FAST(1024, spec(L, 0b1, 0b1), RG_IN_CONCAT2, 0, 64, 64, 64)

@@ -37,7 +37,10 @@ namespace conv {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-static constexpr int CT = 512;
+#ifndef RG_CONV_CT
+#define RG_CONV_CT 512  // threads per workgroup (8 waves, 2 per SIMD)
+#endif
+static constexpr int CT = RG_CONV_CT;
 static constexpr int CW = CT / 64;
 static constexpr int NB = 8;         // destination nodes per work block
 static constexpr int C = 64;         // node / edge / message / output channels
@@ -163,6 +166,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
+#ifdef RG_CONV_PRIO
+  // static priority for the second-dispatched half of the waves (MI355X_MICROARCH.md,
+  // "two waves per SIMD", item 4)
+  if (wave >= CW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
   char* wbase = lds + a.total_bytes + wave * WAVE_LDS;
   float* P = (float*)wbase;

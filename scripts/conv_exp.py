@@ -8,14 +8,18 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-EXPS = {'base': 0, 'nogather': 1, 'nonorm': 2, 'noagg': 3}
+EXPS_ALL = {'base': ['RG_CONV_EXP=0'], 'nogather': ['RG_CONV_EXP=1'], 'nonorm': ['RG_CONV_EXP=2'],
+        'noagg': ['RG_CONV_EXP=3'], 'ct256': ['RG_CONV_CT=256'], 'prio': ['RG_CONV_PRIO=1'],
+        'chain_noepi': ['RG_CHAIN_EXP=1'], 'chain_nomfma': ['RG_CHAIN_EXP=2']}
+EXPS = {k: v for k, v in EXPS_ALL.items()
+        if len(sys.argv) < 3 or k in sys.argv[2].split(',') or k == 'base'}
 
 
 def main():
     from graph_neural_network_for_radar_perception_amd import build
     if '--run' not in sys.argv:
         for name, v in EXPS.items():
-            print(build.build_variant(f'conv_{name}', [f'RG_CONV_EXP={v}'], only=['conv_fused.hip']))
+            print(build.build_variant(f'conv_{name}', v, only=['conv_fused.hip', 'chain_fast.hip']))
         return
     for name in EXPS:
         lib = os.path.join(REPO, 'graph_neural_network_for_radar_perception_amd', 'lib', 'variants',
@@ -29,7 +33,8 @@ def main():
             print(name, 'FAILED', r.returncode, r.stderr[-2000:])
             sys.exit(1)
         d = json.loads(line[-1])
-        print(f"{name:10s} conv_fused {d['kernels']['conv_fused']['avg_ms']:.4f} ms  "
+        print(f"{name:12s} conv_fused {d['kernels']['conv_fused']['avg_ms']:.4f} ms  "
+              f"edge_encoder {d['kernels']['edge_encoder']['avg_ms']:.4f} ms  "
               f"step {d['ms_per_step']:.3f} ms", flush=True)
 
 
