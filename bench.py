@@ -12,6 +12,10 @@ Multi-GPU (torchrun, one process per GPU): every rank owns its own 64 frames
 (frame-parallel, weak scaling, no collective in the timed region; barrier +
 max-over-ranks timing only).
 
+``--config c5``: BASELINE config 5 (dense-scene stress): one frame of 20,000 nodes per GPU,
+pure radius graph (compute_ball_query semantics, eps^2 = 2.5 -> E ~ 400k), L = 7; the
+half-precision type is bf16 (the MFMA path has no separate fp16 build).
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -37,20 +41,36 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}   # dense MFMA peaks (same doc)
 
 
+# workloads; k is unused by the pure radius graph
+PRESETS = {
+    'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
+               cpu_warm=2),
+    'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
+               cpu_warm=1),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--frames', type=int, default=64, help='frames per GPU')
-    p.add_argument('--nodes', type=int, default=3000)
-    p.add_argument('--k', type=int, default=32)
-    p.add_argument('--layers', type=int, default=6)
+    p.add_argument('--config', default='c2', choices=sorted(PRESETS),
+                   help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress')
+    p.add_argument('--frames', type=int, default=None, help='frames per GPU')
+    p.add_argument('--nodes', type=int, default=None)
+    p.add_argument('--k', type=int, default=None)
+    p.add_argument('--layers', type=int, default=None)
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    p.add_argument('--cpu-frames', type=int, default=5, help='CPU baseline sample (timed frames)')
+    p.add_argument('--cpu-frames', type=int, default=None,
+                   help='CPU baseline sample (timed frames)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
-    return p.parse_args()
+    a = p.parse_args()
+    for key, v in PRESETS[a.config].items():
+        if getattr(a, key, None) is None:
+            setattr(a, key, v)
+    return a
 
 
 def setup_dist():
@@ -119,6 +139,8 @@ def pmc_traffic(args, kernel_substr):
     import glob
     want = {'frames': args.frames, 'nodes': args.nodes, 'k': args.k, 'layers': args.layers,
             'dtype': args.dtype}
+    if args.graph != 'knn':
+        want.update(graph=args.graph, eps2=args.eps2)
     for path in sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')),
                        reverse=True):
         doc = json.load(open(path))
@@ -128,6 +150,12 @@ def pmc_traffic(args, kernel_substr):
             if kernel_substr in name:
                 return float(rec['traffic_bytes']), os.path.relpath(path, REPO)
     return None, None
+
+
+def graph_desc(args) -> str:
+    if args.graph == 'radius':
+        return f'radius graph eps^2={args.eps2}'
+    return f'k={args.k}'
 
 
 def _cpu_model() -> str:
@@ -151,20 +179,25 @@ def cpu_baseline(args, cfg):
     torch.manual_seed(1234)
     model = Model_Training(cfg, 'cpu')
     sd = {k: v.detach() for k, v in model.state_dict().items()}
-    warm = 2
+    warm = args.cpu_warm
     frames = [synthetic.make_frame(args.nodes, args.seed + 10**6 + i)
               for i in range(args.cpu_frames + warm)]
     gmax = float(np.sqrt(np.float64(cfg.max_x ** 2 + cfg.max_y ** 2)))
 
     def one(fr):
         t0 = time.perf_counter()
-        g = gref.build_frame_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points, gmax)
+        if args.graph == 'radius':
+            g = gref.build_frame_graph_radius(fr, args.eps2, gmax)
+        else:
+            g = gref.build_frame_graph(fr, cfg.ball_query_eps_square,
+                                       cfg.k_number_nearest_points, gmax)
         t1 = time.perf_counter()
         cl = [torch.from_numpy(c) for c in synthetic.cluster_lists(args.nodes)]
         with torch.no_grad():
             gnn_forward_ref.forward(sd, cfg, torch.from_numpy(g['node_features']),
                                     torch.from_numpy(g['edge_features']),
                                     torch.from_numpy(g['edge_index']),
+                                    None if g['adj_matrix'] is None else
                                     torch.from_numpy(g['adj_matrix']), cl)
         return t1 - t0, time.perf_counter() - t1
 
@@ -178,18 +211,21 @@ def cpu_baseline(args, cfg):
     build_ms = float(np.median(tb)) * 1e3
     fwd_ms = float(np.median(tf)) * 1e3
     total_ms = float(np.median(np.array(tb) + np.array(tf))) * 1e3
-    torch.set_num_threads(1)
-    _, f1 = one(frames[0])
-    torch.set_num_threads(threads)
+    f1 = None
+    if args.config == 'c2':  # (a 1-thread pass over a 20k-node frame would take minutes)
+        torch.set_num_threads(1)
+        _, f1 = one(frames[0])
+        torch.set_num_threads(threads)
     return {'value': round(1e3 / total_ms, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
             'graph_build_ms': round(build_ms, 1), 'forward_ms': round(fwd_ms, 1),
             'forward_only_frames_per_s': round(1e3 / fwd_ms, 4),
-            'forward_1thread_ms': round(f1 * 1e3, 1), 'cpu_model': _cpu_model(),
-            'sample': f'{len(tb)} frame(s) of {args.nodes} nodes, k={args.k}, L={args.layers} '
-                      f'after {warm} warm-up frames: oracle graph build (dense numpy, '
-                      f'graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
-                      f'{total_ms:.0f} ms/frame at torch threads={threads}; the forward also '
-                      f'timed on 1 thread (1 frame)'}
+            'forward_1thread_ms': None if f1 is None else round(f1 * 1e3, 1),
+            'cpu_model': _cpu_model(),
+            'sample': f'{len(tb)} frame(s) of {args.nodes} nodes, {graph_desc(args)}, '
+                      f'L={args.layers} after {warm} warm-up frame(s): oracle graph build (dense '
+                      f'numpy, graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
+                      f'{total_ms:.0f} ms/frame at torch threads={threads}'
+                      + ('; the forward also timed on 1 thread (1 frame)' if f1 else '')}
 
 
 def main():
@@ -203,12 +239,14 @@ def main():
 
     cfg = default_config(graph_convolution_stem_channels=[64] * args.layers,
                          k_number_nearest_points=args.k)
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    mode = nat.GRAPH_RADIUS if args.graph == 'radius' else nat.GRAPH_KNN
     model = make_model(cfg, dev)
     seeds = rank_frame_seeds(rank, args.frames, args.seed)
     frames = [synthetic.make_frame(args.nodes, s) for s in seeds]
     clusters = [synthetic.cluster_lists(args.nodes) for _ in seeds]
     batch = FrameBatch.from_frames(frames, clusters, device=dev)
-    pipe = RadarGNNPipeline(model, cfg, args.dtype)
+    pipe = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -294,11 +332,13 @@ def main():
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
         'data': 'synthetic RadarScenes-shaped frames (SURVEY.md §8(d), seeded), random-init '
                 'weights of the yml architecture',
-        'config': {'workload': f'BASELINE config 2: {args.frames} frames x {args.nodes} nodes per '
-                               f'GPU, k={args.k}, L={args.layers}; step = kNN/ball graph build + '
-                               'node/edge features + encoders + message passing + 4 heads',
-                   'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes, 'k': args.k,
-                   'layers': args.layers, 'edges_per_gpu': E,
+        'config': {'workload': f'BASELINE config {args.config[1:]}: {args.frames} frame(s) x '
+                               f'{args.nodes} nodes per GPU, {graph_desc(args)}, L={args.layers}; '
+                               'step = graph build + node/edge features + encoders + message '
+                               'passing + 4 heads',
+                   'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes,
+                   'graph': args.graph, 'k': args.k if args.graph == 'knn' else None,
+                   'eps2': args.eps2, 'layers': args.layers, 'edges_per_gpu': E,
                    'parallelism': f'frame-parallel x{world} (no collective in the step)'},
         'forward_only_frames_per_s': round(frames_total / fwd_elapsed, 2),
         'roofline': roof,

@@ -36,12 +36,15 @@ static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layer
 
 #ifndef RG_CHAIN_EXP
 #define RG_CHAIN_EXP 0  // timing experiments only (wrong results): 1 no epilogue VALU,
-                        // 2 no MFMA (accumulators keep the bias)
+                        // 2 no MFMA (accumulators keep the bias),
+                        // 3 MFMAs without their A-fragment LDS reads
 #endif
 // MFMA wrapper for the timing experiments
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
   if constexpr (RG_CHAIN_EXP == 2) {
     return c;
+  } else if constexpr (RG_CHAIN_EXP == 3) {  // no A-fragment LDS reads (A := B)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, b, c, 0, 0, 0);
   } else {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }

@@ -135,6 +135,29 @@ __device__ __forceinline__ f32x16 ld_bias_frag(const float* bias, int m, int h) 
 }
 
 __device__ __forceinline__ f32x2 pair(const f32x16& v, int i) { return (f32x2){v[2 * i], v[2 * i + 1]}; }
+
+// two-feature math: v_pk_*_f32 by default; RG_NO_PK (timing experiments) keeps it scalar
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) {
+#ifdef RG_NO_PK
+  return (f32x2){fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)};
+#else
+  return __builtin_elementwise_fma(a, b, c);
+#endif
+}
+__device__ __forceinline__ f32x2 mul2(f32x2 a, f32x2 b) {
+#ifdef RG_NO_PK
+  return (f32x2){a.x * b.x, a.y * b.y};
+#else
+  return a * b;
+#endif
+}
+__device__ __forceinline__ f32x2 add2(f32x2 a, f32x2 b) {
+#ifdef RG_NO_PK
+  return (f32x2){a.x + b.x, a.y + b.y};
+#else
+  return a + b;
+#endif
+}
 __device__ __forceinline__ void set_pair(f32x16& v, int i, f32x2 p) {
   v[2 * i] = p.x;
   v[2 * i + 1] = p.y;
@@ -144,7 +167,7 @@ template <int ACT>
 __device__ __forceinline__ f32x2 act_pk(f32x2 y) {
   if constexpr (ACT == ACT_LEAKY) {
     // max(y, 0.01 y) (constants.py:10): one v_pk_mul_f32 + two v_max_f32
-    const f32x2 z = y * (f32x2){0.01f, 0.01f};
+    const f32x2 z = mul2(y, (f32x2){0.01f, 0.01f});
     float a, b;  // plain v_max_f32: no operand canonicalisation (the compiler would add a
                  // v_max x, x per MFMA-produced operand in IEEE mode)
     asm("v_max_f32 %0, %1, %2" : "=v"(a) : "v"(y.x), "v"(z.x));
@@ -163,10 +186,10 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
-      s0 += pair(acc[m], i);
-      s1 += pair(acc[m], i + 1);
+      s0 = add2(s0, pair(acc[m], i));
+      s1 = add2(s1, pair(acc[m], i + 1));
     }
-  const f32x2 st = s0 + s1;
+  const f32x2 st = add2(s0, s1);
   float s = st.x + st.y;
   s = add_xor32(s);
   const float mean = s * (1.f / N);  // N is a power of two: exact
@@ -176,11 +199,11 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
-      const f32x2 d0 = pair(acc[m], i) + nm, d1 = pair(acc[m], i + 1) + nm;
-      q0 = __builtin_elementwise_fma(d0, d0, q0);
-      q1 = __builtin_elementwise_fma(d1, d1, q1);
+      const f32x2 d0 = add2(pair(acc[m], i), nm), d1 = add2(pair(acc[m], i + 1), nm);
+      q0 = fma2(d0, d0, q0);
+      q1 = fma2(d1, d1, q1);
     }
-  const f32x2 qt = q0 + q1;
+  const f32x2 qt = add2(q0, q1);
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
   const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
@@ -190,7 +213,7 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, __builtin_elementwise_fma(pair(acc[m], i), gs2, gb2));
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, fma2(pair(acc[m], i), gs2, gb2));
 }
 
 // channel_normalization of a CENTRED layer (weights packed with RG_PACK_CENTERED): the
@@ -206,10 +229,10 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
       const f32x2 d0 = pair(acc[m], i), d1 = pair(acc[m], i + 1);
-      q0 = __builtin_elementwise_fma(d0, d0, q0);
-      q1 = __builtin_elementwise_fma(d1, d1, q1);
+      q0 = fma2(d0, d0, q0);
+      q1 = fma2(d1, d1, q1);
     }
-  const f32x2 qt = q0 + q1;
+  const f32x2 qt = add2(q0, q1);
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
   const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
@@ -218,7 +241,7 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, __builtin_elementwise_fma(pair(acc[m], i), gs2, mu2));
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, fma2(pair(acc[m], i), gs2, mu2));
 }
 
 template <int ACT, int MT>

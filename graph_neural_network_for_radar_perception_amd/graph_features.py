@@ -186,17 +186,22 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
     link pairs."""
     k = cfg.k_number_nearest_points if k is None else k
     eps2 = cfg.ball_query_eps_square if eps2 is None else eps2
+    # radius graphs have no a-priori edge bound: the capacity that sufficed last time
+    # (kept in ws_cache) is tried first, then checked (one host sync) and rebuilt if short
+    cap_key = ('radius_cap', mode, float(eps2))
+    cap0 = ws_cache.get(cap_key) if (ws_cache is not None and mode != nat.GRAPH_KNN) else None
     row_ptr, col, deg, ne, cap = engine.build_graph(batch.arrays['meas_px'],
                                                     batch.arrays['meas_py'], batch.frame_ptr,
                                                     batch.frame_sizes, k, eps2, mode,
-                                                    ws_cache=ws_cache)
+                                                    edge_capacity=cap0, ws_cache=ws_cache)
     if mode != nat.GRAPH_KNN:
-        # radius graphs have no a-priori edge bound: check (one host sync) and rebuild
         E = int(ne.item())
         if E > cap:
             row_ptr, col, deg, ne, cap = engine.build_graph(
                 batch.arrays['meas_px'], batch.arrays['meas_py'], batch.frame_ptr,
                 batch.frame_sizes, k, eps2, mode, edge_capacity=E, ws_cache=ws_cache)
+        if ws_cache is not None:
+            ws_cache[cap_key] = cap
     g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
     nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)
     # destination-major edge (src = g.src[p] -> dst = g.dst[p])

@@ -19,17 +19,24 @@ from .graph_features import FrameBatch, GraphBatch, build_graph_batch
 
 
 class RadarGNNPipeline:
-    def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN):
+    def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
+                 eps2: Optional[float] = None):
+        """mode: nat.GRAPH_KNN (datagen_gnn.py:104-106, the default), nat.GRAPH_RADIUS (a pure
+        ball-query graph, BASELINE config 5) or nat.GRAPH_KNN_RADIUS
+        (compute_adjacency_information_v2); eps2: squared radius (default
+        cfg.ball_query_eps_square)."""
         self.model = model
         self.cfg = cfg
         self.dtype = dtype
         self.mode = mode
+        self.eps2 = eps2
         self.plans = model.plans(dtype)
         self.ws_cache: dict = {}
         self.buffers: dict = {}
 
     def build(self, batch: FrameBatch) -> GraphBatch:
-        return build_graph_batch(batch, self.cfg, mode=self.mode, ws_cache=self.ws_cache)
+        return build_graph_batch(batch, self.cfg, eps2=self.eps2, mode=self.mode,
+                                 ws_cache=self.ws_cache)
 
     def forward(self, batch: FrameBatch, gb: GraphBatch, events=None) -> engine.ForwardOutputs:
         return engine.forward_batched(self.plans, gb.node_features, gb.edge_features, gb.graph,

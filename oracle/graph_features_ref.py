@@ -89,6 +89,40 @@ def compute_radius_graph(data_dict: dict, eps: float) -> np.ndarray:
     return np.stack(np.where(compute_ball_query(dmat, eps)), axis=0)
 
 
+def compute_radius_graph_rows(px: np.ndarray, py: np.ndarray, eps: float,
+                              chunk: int = 2048) -> np.ndarray:
+    """compute_radius_graph evaluated block-row by block-row (same f32 arithmetic, same
+    row-major order) so that N = 20,000 (BASELINE config 5) fits in memory."""
+    px = np.asarray(px, np.float32)
+    py = np.asarray(py, np.float32)
+    n = px.shape[0]
+    rows, cols = [], []
+    for r0 in range(0, n, chunk):
+        r1 = min(n, r0 + chunk)
+        dx = px[r0:r1, None] - px[None, :]
+        dy = py[r0:r1, None] - py[None, :]
+        g = (dx * dx + dy * dy).astype(np.float32) <= eps
+        g[np.arange(r1 - r0), np.arange(r0, r1)] = False
+        r, c = np.where(g)
+        rows.append(r + r0)
+        cols.append(c)
+    return np.stack((np.concatenate(rows), np.concatenate(cols)), 0).astype(np.int64)
+
+
+def build_frame_graph_radius(frame: dict, eps: float, grid_max_r: float,
+                             grid_max_th: float = np.pi * 0.5):
+    """build_frame_graph with the pure radius graph of BASELINE config 5: edge_index =
+    np.where(compute_ball_query(D, eps)), degree = the ball-query count (= row length),
+    features as datagen_gnn.py:112-123.  No dense matrices (adj_matrix is None)."""
+    ei = compute_radius_graph_rows(frame['meas_px'], frame['meas_py'], eps)
+    deg = np.bincount(ei[0], minlength=frame['meas_px'].shape[0]).astype(np.int64)
+    ef = compute_edge_features(frame, ei)
+    nf = compute_node_features(frame, deg, True, 0, np.float64(grid_max_r), 0,
+                               float(grid_max_th))
+    return {'edge_index': ei, 'adj_matrix': None, 'degree': deg,
+            'edge_features': ef.astype(np.float32), 'node_features': nf.astype(np.float32)}
+
+
 def compute_node_features(data_dict, node_degree, include_region_confidence=False,
                           min_range=None, max_range=None, min_azimuth=None, max_azimuth=None):
     """graph_features.py:117-144 (float64 result, as in the reference)."""
