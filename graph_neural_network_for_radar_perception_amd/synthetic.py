@@ -92,3 +92,45 @@ def other_features(frame: dict) -> np.ndarray:
     """(px, py, vx, vy) per node, ``datagen_gnn.py:110-111``."""
     return np.stack((frame['meas_px'], frame['meas_py'],
                      frame['meas_vx'], frame['meas_vy']), axis=-1).astype(np.float32)
+
+
+def make_labels(frame: dict, edge_index: np.ndarray, num_classes: int = 7, seed: int = SEED0):
+    """Synthetic training labels of one frame in the reference's label layout
+    (``datagen_gnn.py:126-139``), from the generator's cluster ids:
+
+      node_class       int64 [N]   class of the node's cluster; clutter (single-point
+                                   clusters) gets the last class ('FALSE')
+      node_offsets     f32 [N, 2]  cluster centre - point (raw metres; the model
+                                   normalises them, compute_offsets.py:6-11)
+      edge_class       int64 [U]   link pairs (i < j, row-major = nonzero(triu(adj, 1)),
+                                   compute_edge_labels.py:7-20): 1 if both ends are in
+                                   the same real cluster
+      cluster_node_idx list of int64 member lists of the real clusters (ascending,
+                                   clusters ordered by their lowest member)
+      cluster_labels   int64 [Ncl] class of each listed cluster
+    """
+    rng = np.random.default_rng(seed)
+    cid = np.asarray(frame['cluster_id'], np.int64)
+    n = cid.shape[0]
+    px = frame['meas_px'].astype(np.float64)
+    py = frame['meas_py'].astype(np.float64)
+    ids, inv, counts = np.unique(cid, return_inverse=True, return_counts=True)
+    real = counts[inv] > 1
+    cls_of = rng.integers(0, num_classes - 1, ids.shape[0])
+    node_class = np.where(real, cls_of[inv], num_classes - 1).astype(np.int64)
+    cx = np.bincount(inv, px) / counts
+    cy = np.bincount(inv, py) / counts
+    node_offsets = np.stack((cx[inv] - px, cy[inv] - py), -1).astype(np.float32)
+    ei = np.asarray(edge_index)
+    m = ei[0] < ei[1]
+    s, d = ei[0][m], ei[1][m]
+    edge_class = ((cid[s] == cid[d]) & real[s]).astype(np.int64)
+    firsts = {}
+    for i in range(n):
+        if real[i]:
+            firsts.setdefault(int(inv[i]), []).append(i)
+    groups = sorted(firsts.values(), key=lambda g: g[0])
+    cluster_node_idx = [np.asarray(g, np.int64) for g in groups]
+    cluster_labels = np.asarray([cls_of[inv[g[0]]] for g in groups], np.int64)
+    return {'node_class': node_class, 'node_offsets': node_offsets, 'edge_class': edge_class,
+            'cluster_node_idx': cluster_node_idx, 'cluster_labels': cluster_labels}

@@ -317,14 +317,85 @@ def make_proposal_fixtures():
     np.savez_compressed(os.path.join(HERE, 'proposals_model_trained_N300.npz'), **data)
 
 
+def make_training_fixtures():
+    """Model_Training.forward + Loss_Graph (loss.py:37-76) + backward + two
+    torch.optim.SGD steps (set_param_for_training_gnn.py:44-46: momentum 0.9, lr and
+    weight decay from the yml) on a 2-frame batch with synthetic labels
+    (synthetic.make_labels) -- the reference's own training step (training.py:66-85)."""
+    from modules.set_configurations.set_config_gnn import config
+    from modules.neural_net.gnn.gnn_detector import Model_Training
+    cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+    sizes, seeds = (160, 100), (7001, 7002)
+    frames, graphs, labels = [], [], []
+    for n, sd_ in zip(sizes, seeds):
+        fr = synthetic.make_frame(n, sd_)
+        adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points)
+        frames.append(fr)
+        graphs.append((adj, nf, ef))
+        labels.append(synthetic.make_labels(fr, adj['adj_list'], cfg.num_classes, sd_))
+    torch.manual_seed(2024)
+    model = Model_Training(cfg, 'cpu')
+    init = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = torch.optim.SGD(params, momentum=0.9, lr=cfg.learning_rate, weight_decay=cfg.weight_decay)
+    lab = {'node_class': [torch.from_numpy(l['node_class']) for l in labels],
+           'node_offsets': [torch.from_numpy(l['node_offsets']) for l in labels],
+           'edge_class': [torch.from_numpy(l['edge_class']) for l in labels],
+           'cluster_node_idx': [[torch.from_numpy(c) for c in l['cluster_node_idx']] for l in labels],
+           'cluster_labels': [torch.from_numpy(l['cluster_labels']) for l in labels]}
+    args = dict(node_features=[torch.from_numpy(g[1]).float() for g in graphs],
+                edge_features=[torch.from_numpy(g[2]).float() for g in graphs],
+                edge_index=[torch.from_numpy(g[0]['adj_list']).long() for g in graphs],
+                adj_matrix=[torch.from_numpy(g[0]['adj_matrix']) for g in graphs])
+    data = {}
+    model.train()
+    for step in (1, 2):
+        loss, acc = model(labels=lab, **args)
+        total = loss['loss_node_cls'] + loss['loss_node_reg'] + loss['loss_edge_cls'] + loss['loss_obj_cls']
+        total.backward()
+        for k_, v in loss.items():
+            data[f's{step}/{k_}'] = np.float64(v.item())
+        for k_, v in acc.items():
+            data[f's{step}/{k_}'] = np.float64(float(v))
+        if step == 1:
+            for name, p in model.named_parameters():
+                data['g1/' + name] = p.grad.detach().numpy().copy()
+        opt.step()
+        opt.zero_grad()
+    for k_, v in model.state_dict().items():
+        data['w2/' + k_] = v.numpy()
+    for k_, v in init.items():
+        data['w/' + k_] = v
+    for f, (fr, g, l) in enumerate(zip(frames, graphs, labels)):
+        for k_, v in _frame_arrays(fr).items():
+            data[f'f{f}/{k_}'] = v
+        data[f'f{f}/node_features'] = g[1].astype(np.float32)
+        data[f'f{f}/edge_features'] = g[2].astype(np.float32)
+        data[f'f{f}/edge_index'] = g[0]['adj_list'].astype(np.int32)
+        data[f'f{f}/node_class'] = l['node_class']
+        data[f'f{f}/node_offsets'] = l['node_offsets']
+        data[f'f{f}/edge_class'] = l['edge_class']
+        data[f'f{f}/cluster_ptr'] = np.cumsum([0] + [len(c) for c in l['cluster_node_idx']]).astype(np.int64)
+        data[f'f{f}/cluster_idx'] = np.concatenate(l['cluster_node_idx']).astype(np.int64)
+        data[f'f{f}/cluster_labels'] = l['cluster_labels']
+    data.update(n_frames=len(sizes), lr=cfg.learning_rate, weight_decay=cfg.weight_decay,
+                momentum=0.9)
+    np.savez_compressed(os.path.join(HERE, 'train_yml_2frames.npz'), **data)
+    print('training', {k: v for k, v in data.items() if k.startswith('s')})
+
+
 def main():
     sys.path.insert(0, REF)
     _install_third_party_restatements()
     torch.set_num_threads(8)
+    if '--training-only' in sys.argv:
+        make_training_fixtures()
+        return
     if '--proposals-only' not in sys.argv:
         make_graph_fixtures()
         make_model_fixtures()
     make_proposal_fixtures()
+    make_training_fixtures()
 
 
 if __name__ == '__main__':
