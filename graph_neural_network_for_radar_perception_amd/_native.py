@@ -24,6 +24,7 @@ HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 RG_F32, RG_BF16 = 0, 1
 RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD = 2, 3, 4
 RG_PACK_CENTERED = 0x100
+RG_PACK_TRANSPOSE = 0x200
 RG_LAYER_CENTERED = 1
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
@@ -40,7 +41,22 @@ class NativeLibraryError(RuntimeError):
 class rg_layer(ctypes.Structure):
     _fields_ = [('w_packed', ctypes.c_void_p), ('norm_mu', ctypes.c_void_p),
                 ('norm_std', ctypes.c_void_p), ('in_dim', ctypes.c_int),
-                ('out_dim', ctypes.c_int), ('act', ctypes.c_int), ('flags', ctypes.c_int)]
+                ('out_dim', ctypes.c_int), ('act', ctypes.c_int), ('flags', ctypes.c_int),
+                ('save_pre', ctypes.c_void_p), ('save_out', ctypes.c_void_p)]
+
+
+class rg_loss_args(ctypes.Structure):
+    _fields_ = [('node_cls', ctypes.c_void_p), ('node_reg', ctypes.c_void_p),
+                ('link', ctypes.c_void_p), ('obj', ctypes.c_void_p),
+                ('node_class', ctypes.c_void_p), ('node_offsets', ctypes.c_void_p),
+                ('edge_class', ctypes.c_void_p), ('obj_class', ctypes.c_void_p),
+                ('class_w', ctypes.c_void_p),
+                ('n_nodes', ctypes.c_long), ('n_pairs', ctypes.c_long),
+                ('n_clusters', ctypes.c_long), ('n_classes', ctypes.c_int),
+                ('mu_x', ctypes.c_float), ('mu_y', ctypes.c_float),
+                ('sigma_x', ctypes.c_float), ('sigma_y', ctypes.c_float),
+                ('w_node_cls', ctypes.c_float), ('w_node_reg', ctypes.c_float),
+                ('w_edge_cls', ctypes.c_float), ('w_obj_cls', ctypes.c_float)]
 
 
 _P = ctypes.c_void_p
@@ -83,6 +99,20 @@ _SIGNATURES = {
     'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,
                                  _P, _I, _P, _P, _P, _I, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+    # training (train.hip)
+    'rg_ffn_backward_workspace_size': (_S, []),
+    'rg_ffn_backward': (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
+    'rg_linear_grad_workspace_size': (_S, [_L, _I, _I]),
+    'rg_linear_grad': (_I, [_P, _I, _L, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P,
+                            _P, _P, _P, _S, _P]),
+    'rg_incidence_workspace_size': (_S, [_I, _L]),
+    'rg_incidence': (_I, [_P, _P, _L, _I, _P, _P, _P, _S, _P]),
+    'rg_gather_segment_sum': (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P, _I, _I, _P]),
+    'rg_segment_max_backward': (_I, [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
+    'rg_loss_workspace_size': (_S, [_L, _L, _L]),
+    'rg_loss_graph': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _S, _P]),
+    'rg_loss_graph_backward': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _P, _P, _P]),
+    'rg_sgd_step': (_I, [_P, _P, _P, _L, _F, _F, _F, _I, _P]),
 }
 
 _lib = None

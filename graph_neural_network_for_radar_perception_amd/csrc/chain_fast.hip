@@ -558,6 +558,7 @@ extern "C" int rg_mlp_chain_fast(const rg_layer* layers, int n_layers, long rows
   for (int l = 0; l < n_layers; ++l) {
     const rg_layer& s = layers[l];
     RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_fast: layer %d weights", l);
+    if (s.save_pre || s.save_out) return RG_ERR_UNSUPPORTED;  // tapes: the f32 generic chain
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
     k.n[l] = (s.out_dim + 31) / 32 * 32;
     if (l > 0)

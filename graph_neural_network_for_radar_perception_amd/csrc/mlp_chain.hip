@@ -62,6 +62,8 @@ struct ChainLayer {
   const void* w;  // packed fragments, followed by the f32 bias padded to 16*mt
   const float* mu;
   const float* sd;
+  float* save_pre;  // training tape (f32 chains): z = x W^T + b, [rows][out]
+  float* save_out;  // and the activation output, [rows][out]
   int in, out, act, woff;  // woff: byte offset of this layer in the LDS weight image
 };
 
@@ -87,8 +89,8 @@ struct ChainArgs {
 // ------------------------------------------------------------------ packing
 // f32 : [m][s4][lane][4] = W[16m + (lane&15)][16*s4 + 4*(lane>>4) + t]
 // bf16: [m][s ][lane][8] = W[16m + (lane&15)][32*s  + 8*(lane>>4) + j]
-__global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, float* __restrict__ P,
-                                long total) {
+__global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, int transpose,
+                                float* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S4 = kpad(in, 16) / 16;
@@ -99,7 +101,8 @@ __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, fl
   const int m = (int)(ms / S4);
   const int o = 16 * m + (lane & 15);
   const int k = 16 * s4 + 4 * (lane >> 4) + e;
-  P[t] = (o < out && k < in) ? W[(size_t)o * in + k] : 0.f;
+  // transpose: W holds the [in][out] matrix whose transpose is the layer
+  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k]) : 0.f;
 }
 
 __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
@@ -416,6 +419,25 @@ __device__ __forceinline__ void store_rows(const f32x4 (&acc)[16], const ChainAr
   }
 }
 
+// training tape: row `row`'s features 16m + 4g + e (< out) -> dst[row][out]
+__device__ __forceinline__ void save_rows(const f32x4 (&acc)[16], float* dst, long row, int mt,
+                                          int out, int g) {
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    if (m < mt) {
+      const int f0 = 16 * m + 4 * g;
+      float* p = dst + (size_t)row * out + f0;
+      if ((out & 3) == 0 && f0 < out) {
+        *(f32x4*)p = acc[m];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (f0 + e < out) p[e] = acc[m][e];
+      }
+    }
+  }
+}
+
 template <typename T, bool WLDS>
 __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -460,7 +482,9 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       for (int m = 0; m < 16; ++m)
         if (m < mt) acc[m] = *(const f32x4*)(bias + 16 * m + 4 * g);
       Mfma<T>::run(acc, slab, P, mt, L.in, lane);
+      if (L.save_pre && r0 + r < rows) save_rows(acc, L.save_pre, r0 + r, mt, L.out, g);
       epilogue(acc, L, mt, g);
+      if (L.save_out && r0 + r < rows) save_rows(acc, L.save_out, r0 + r, mt, L.out, g);
       if (l + 1 < a.nl) {
         T* row = slab + r * Cfg<T>::STRIDE;
 #pragma unroll
@@ -506,7 +530,7 @@ static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
 using namespace rg;
 
 extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
-  return packed_bytes(in_dim, out_dim, dtype & ~RG_PACK_CENTERED);
+  return packed_bytes(in_dim, out_dim, dtype & ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE));
 }
 
 extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim, int out_dim,
@@ -515,13 +539,16 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
              "rg_pack_linear: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
   hipStream_t st = (hipStream_t)stream;
   const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
-  dtype &= ~RG_PACK_CENTERED;
+  const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;
+  dtype &= ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE);
+  RG_REQUIRE(!transpose || dtype == RG_F32, RG_ERR_ARG,
+             "rg_pack_linear: RG_PACK_TRANSPOSE applies to RG_F32");
   RG_REQUIRE(!center || dtype >= RG_PACK_FAST_IN, RG_ERR_ARG,
              "rg_pack_linear: RG_PACK_CENTERED applies to the RG_PACK_FAST_* formats");
   if (dtype == RG_F32) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
-    pack_f32_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, (float*)packed,
-                                                          total);
+    pack_f32_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
+                                                          (float*)packed, total);
   } else if (dtype == RG_BF16) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
@@ -581,7 +608,11 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
                "rg_mlp_chain: layer %d in_dim %d does not match its input", l, s.in_dim);
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG,
                "rg_mlp_chain: layer %d norm needs mu, std and out_dim >= 2", l);
+    RG_REQUIRE((!s.save_pre && !s.save_out) || dtype == RG_F32, RG_ERR_ARG,
+               "rg_mlp_chain: training tapes (save_pre / save_out) need dtype RG_F32");
     a.L[l].w = s.w_packed;
+    a.L[l].save_pre = s.save_pre;
+    a.L[l].save_out = s.save_out;
     a.L[l].mu = s.norm_mu;
     a.L[l].sd = s.norm_std;
     a.L[l].in = s.in_dim;

@@ -1,0 +1,708 @@
+// Training backward of the radar-GNN hot path, float32 (the reference trains in f32):
+// Model_Training.forward + Loss_Graph + loss.backward() + torch.optim.SGD
+// (gnn_detector.py:428-478, loss.py:37-76, lossfunc.py:20-55, training.py:66-85,
+// set_param_for_training_gnn.py:44-46).
+//
+//   rg_ffn_backward         channel_normalization + activation backward, row per wave,
+//                           statistics recomputed from the saved pre-norm rows
+//   rg_linear_grad          dW += dZ^T X, db += sum dZ with X formed on the fly from the
+//                           chain input modes (gathered / concatenated / pair-added rows):
+//                           v_mfma_f32_16x16x4_f32 over 64-row LDS tiles, fixed row
+//                           chunks, chunk partials reduced in a fixed order
+//   rg_incidence            node -> items lists (transpose of an index_select)
+//   rg_gather_segment_sum   per-node ordered sums of gradient rows
+//   rg_segment_max_backward per-cluster channel max backward (first maximum)
+//   rg_loss_graph(+_backward) the four losses, accuracies and logit gradients
+//   rg_sgd_step             the SGD update on flat arrays
+// The data GEMM of the backward (dX = dZ W) is rg_mlp_chain on W packed transposed
+// (RG_PACK_TRANSPOSE).  Every reduction runs in a fixed order (no float atomics except
+// rg_segment_max_backward, where clusters may share a node), so a step is
+// bit-reproducible.
+#include "rg_common.h"
+#include "scan.h"
+
+namespace rg {
+namespace train {
+
+static constexpr int PARTS = 512;          // fixed grid of the partial-sum kernels
+static constexpr float NORM_EPS = 1e-5f;   // constants.py:9
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// d act(y) / d y as torch's backward kernels: leaky_relu (self > 0 ? 1 : slope),
+// relu (result > 0), silu (s (1 + y (1 - s)))
+__device__ __forceinline__ float act_grad(float y, int act) {
+  if (act == ACT_LEAKY) return y > 0.f ? 1.f : 0.01f;
+  if (act == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == ACT_SWISH) {
+    const float s = 1.f / (1.f + expf(-y));
+    return s * (1.f + y * (1.f - s));
+  }
+  return 1.f;
+}
+
+// ------------------------------------------------------------------ ffn backward
+// One wave per row, feature f = lane + 64 j.  Forward (common.py:215-220, as the
+// chain kernel evaluates it): mean = sum z / C, d = z - mean, std = sqrt(sum d^2 / (C-1)),
+// r = 1 / (std + eps), n = d r, y = s n + m, a = act(y).  Backward:
+//   gy = da act'(y);  ds += sum gy n;  dm += sum gy;  gn = s gy;
+//   gd = r gn - r^2 (sum gn d) d / ((C-1) std);  dz = gd - mean(gd).
+__global__ __launch_bounds__(256) void ffn_backward_kernel(
+    const float* __restrict__ z, int ldz, const float* __restrict__ da, int ldda, long rows,
+    int C, int has_norm, const float* __restrict__ mu, const float* __restrict__ sd, int act,
+    float* __restrict__ dz, int lddz, float* __restrict__ part) {
+  __shared__ float red[4][2];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float s = has_norm ? *sd : 1.f;
+  const float m = has_norm ? *mu : 0.f;
+  float acc_s = 0.f, acc_m = 0.f;  // lane-0 running sums, rows in fixed order
+  for (long row = (long)blockIdx.x * 4 + wave; row < rows; row += (long)gridDim.x * 4) {
+    float zv[4], gv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = lane + 64 * j;
+      zv[j] = f < C ? z[(size_t)row * ldz + f] : 0.f;
+      gv[j] = f < C ? da[(size_t)row * ldda + f] : 0.f;
+    }
+    if (has_norm) {
+      const float mean = wave_sum(zv[0] + zv[1] + zv[2] + zv[3]) / (float)C;
+      float d[4], ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d[j] = (lane + 64 * j) < C ? zv[j] - mean : 0.f;
+        ss += d[j] * d[j];
+      }
+      ss = wave_sum(ss);
+      const float stdv = __fsqrt_rn(ss / (float)(C - 1));
+      const float r = 1.f / (stdv + NORM_EPS);
+      float gn[4], ps = 0.f, pm = 0.f, A = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float n = d[j] * r;
+        const float y = __fadd_rn(__fmul_rn(s, n), m);
+        const float gy = (lane + 64 * j) < C ? gv[j] * act_grad(y, act) : 0.f;
+        ps += gy * n;
+        pm += gy;
+        gn[j] = s * gy;
+        A += gn[j] * d[j];
+      }
+      ps = wave_sum(ps);
+      pm = wave_sum(pm);
+      A = wave_sum(A);
+      acc_s += ps;
+      acc_m += pm;
+      const float coef = stdv > 0.f ? r * r * A / ((float)(C - 1) * stdv) : 0.f;
+      float gd[4], sg = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gd[j] = (lane + 64 * j) < C ? r * gn[j] - coef * d[j] : 0.f;
+        sg += gd[j];
+      }
+      const float mg = wave_sum(sg) / (float)C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = lane + 64 * j;
+        if (f < C) dz[(size_t)row * lddz + f] = gd[j] - mg;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = lane + 64 * j;
+        if (f < C) dz[(size_t)row * lddz + f] = gv[j] * act_grad(zv[j], act);
+      }
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = acc_s;
+    red[wave][1] = acc_m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    part[2 * blockIdx.x + 1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+  }
+}
+
+// sum of PARTS (s, m) partials in a fixed order, added to the parameter gradients
+__global__ __launch_bounds__(256) void ffn_param_reduce(const float* __restrict__ part,
+                                                        float* __restrict__ d_mu,
+                                                        float* __restrict__ d_sd) {
+  __shared__ float red[4][2];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  float s = 0.f, m = 0.f;
+  for (int i = t; i < PARTS; i += 256) {
+    s += part[2 * i];
+    m += part[2 * i + 1];
+  }
+  s = wave_sum(s);
+  m = wave_sum(m);
+  if (lane == 0) {
+    red[wave][0] = s;
+    red[wave][1] = m;
+  }
+  __syncthreads();
+  if (t == 0) {
+    *d_sd += (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    *d_mu += (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+  }
+}
+
+// ------------------------------------------------------------------ linear weight grad
+struct GradIn {
+  int mode, in_dim;
+  const float* in0;
+  const float* in1;
+  const float* in2;
+  int ld0, ld1, ld2, w0, w1, w2;
+  const int* idx0;
+  const int* idx1;
+};
+
+// element f of row `row` of the layer input; f == in_dim is the bias column (1)
+__device__ __forceinline__ float x_elem(const GradIn& a, long row, int f) {
+  if (f >= a.in_dim) return f == a.in_dim ? 1.f : 0.f;
+  switch (a.mode) {
+    case RG_IN_DENSE:
+      return a.in0[(size_t)row * a.ld0 + f];
+    case RG_IN_CONCAT2:
+      return f < a.w0 ? a.in0[(size_t)row * a.ld0 + f] : a.in1[(size_t)row * a.ld1 + (f - a.w0)];
+    case RG_IN_GATHER3:
+      if (f < a.w0) return a.in0[(size_t)a.idx0[row] * a.ld0 + f];
+      if (f < 2 * a.w0) return a.in0[(size_t)a.idx1[row] * a.ld0 + (f - a.w0)];
+      return a.in2[(size_t)row * a.ld2 + (f - 2 * a.w0)];
+    default:  // RG_IN_PAIRADD
+      return __fadd_rn(a.in0[(size_t)a.idx0[row] * a.ld0 + f], a.in0[(size_t)a.idx1[row] * a.ld0 + f]);
+  }
+}
+
+static constexpr int GT = 64;       // output tile (out x in) and row block
+static constexpr int GS = 80;       // LDS row stride (floats): 4 consecutive rows hit
+                                    // disjoint bank quarters
+struct GradGeom {
+  int ot, it, nchunk;
+  long rpc;  // rows per chunk (multiple of GT)
+};
+static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
+  GradGeom g;
+  g.ot = (out_dim + GT - 1) / GT;
+  g.it = (in_dim + 1 + GT - 1) / GT;
+  const long blocks = (rows + GT - 1) / GT;
+  long want = 2048 / (g.ot * g.it);
+  if (want < 1) want = 1;
+  if (want > blocks) want = blocks;
+  if (want < 1) want = 1;
+  g.rpc = ((blocks + want - 1) / want) * GT;
+  g.nchunk = (int)((rows + g.rpc - 1) / g.rpc);
+  if (g.nchunk < 1) g.nchunk = 1;
+  return g;
+}
+
+__global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restrict__ dz, int lddz,
+                                                          long rows, int out_dim, GradIn in,
+                                                          long rpc, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* sZ = sm;                 // [GT][GS]  dz rows x out-tile
+  float* sX = sm + GT * GS;       // [GT][GS]  x rows x in-tile
+  float* sR = sm + 2 * GT * GS;   // [4][GT][GT] per-wave results
+  const int chunk = blockIdx.x, ot = blockIdx.y, it = blockIdx.z;
+  const int o0 = ot * GT, i0 = it * GT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r_begin = (long)chunk * rpc;
+  const long r_end = min(rows, r_begin + rpc);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (long rb = r_begin; rb < r_end; rb += GT) {
+    for (int t = threadIdx.x; t < GT * GT; t += 256) {
+      const int rr = t / GT, c = t % GT;
+      const long row = rb + rr;
+      const bool ok = row < r_end;
+      sZ[rr * GS + c] = (ok && o0 + c < out_dim) ? dz[(size_t)row * lddz + o0 + c] : 0.f;
+      sX[rr * GS + c] = ok ? x_elem(in, row, i0 + c) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = 16 * wave + 4 * ks + (lane >> 4);
+      float av[4], bv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) av[m] = sZ[kr * GS + 16 * m + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bv[n] = sX[kr * GS + 16 * n + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // lane holds D[o = 16m + 4(lane>>4) + e][i = 16n + (lane&15)]
+  float* R = sR + wave * GT * GT;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        R[(16 * m + 4 * (lane >> 4) + e) * GT + 16 * n + (lane & 15)] = acc[m][n][e];
+  __syncthreads();
+  float* P = part + ((size_t)(chunk * gridDim.y + ot) * gridDim.z + it) * GT * GT;
+  for (int t = threadIdx.x; t < GT * GT; t += 256)
+    P[t] = (sR[t] + sR[GT * GT + t]) + (sR[2 * GT * GT + t] + sR[3 * GT * GT + t]);
+}
+
+__global__ void linear_grad_reduce(const float* __restrict__ part, int nchunk, int ot_n, int it_n,
+                                   int out_dim, int in_dim, float* __restrict__ dW,
+                                   float* __restrict__ db) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)out_dim * (in_dim + 1);
+  if (t >= total) return;
+  const int o = (int)(t / (in_dim + 1)), i = (int)(t % (in_dim + 1));
+  const int ot = o / GT, it = i / GT;
+  const int oo = o % GT, ii = i % GT;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c)
+    s += part[((size_t)(c * ot_n + ot) * it_n + it) * GT * GT + oo * GT + ii];
+  if (i < in_dim) dW[(size_t)o * in_dim + i] += s;
+  else if (db) db[o] += s;
+}
+
+// ------------------------------------------------------------------ incidence lists
+__global__ void inc_count(const int* __restrict__ a, const int* __restrict__ b, long n,
+                          int* __restrict__ cnt) {
+  const long u = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n) return;
+  atomicAdd(cnt + a[u], 1);
+  if (b) atomicAdd(cnt + b[u], 1);
+}
+__global__ void inc_fill(const int* __restrict__ a, const int* __restrict__ b, long n,
+                         int* __restrict__ cursor, int* __restrict__ list) {
+  const long u = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n) return;
+  list[atomicAdd(cursor + a[u], 1)] = (int)u;
+  if (b) list[atomicAdd(cursor + b[u], 1)] = (int)u;
+}
+// each list ascending (fill order is arbitrary); lists are short (node degrees)
+__global__ void inc_sort(const int* __restrict__ ptr, int n_nodes, int* __restrict__ list) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n_nodes) return;
+  const int b = ptr[v], e = ptr[v + 1];
+  for (int i = b + 1; i < e; ++i) {
+    const int key = list[i];
+    int j = i - 1;
+    while (j >= b && list[j] > key) {
+      list[j + 1] = list[j];
+      --j;
+    }
+    list[j + 1] = key;
+  }
+}
+
+// ------------------------------------------------------------------ gather-segment sum
+__global__ __launch_bounds__(256) void gather_segsum_kernel(
+    const float* __restrict__ src, int ld_src, int col0, int width, const int* __restrict__ ptr,
+    const int* __restrict__ list, const float* __restrict__ scale, int n_nodes,
+    float* __restrict__ out, int ld_out, int accumulate) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int v = blockIdx.x * 4 + wave; v < n_nodes; v += gridDim.x * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int b = ptr[v], e = ptr[v + 1];
+    for (int k = b; k < e; ++k) {
+      const int row = list ? list[k] : k;
+      const float sc = scale ? scale[row] : 1.f;
+      const float* p = src + (size_t)row * ld_src + col0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = lane + 64 * j;
+        if (f < width) acc[j] += scale ? p[f] * sc : p[f];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = lane + 64 * j;
+      if (f < width) {
+        float* o = out + (size_t)v * ld_out + f;
+        *o = accumulate ? *o + acc[j] : acc[j];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ segment max backward
+__global__ void segmax_backward_kernel(const float* __restrict__ h, int ld_h, int C,
+                                       const int* __restrict__ cptr, const int* __restrict__ cidx,
+                                       int n_clusters, const float* __restrict__ dp, int ld_p,
+                                       float* __restrict__ dh, int ld_dh) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)n_clusters * C) return;
+  const int c = (int)(t / C), f = (int)(t % C);
+  const int b = cptr[c], e = cptr[c + 1];
+  if (b >= e) return;
+  int best = cidx[b];
+  float bv = h[(size_t)best * ld_h + f];
+  for (int k = b + 1; k < e; ++k) {
+    const int n = cidx[k];
+    const float v = h[(size_t)n * ld_h + f];
+    if (v > bv || (v != v && bv == bv)) {  // NaN propagates as the maximum (torch.max)
+      bv = v;
+      best = n;
+    }
+  }
+  atomicAdd(dh + (size_t)best * ld_dh + f, dp[(size_t)c * ld_p + f]);
+}
+
+// ------------------------------------------------------------------ losses
+// log-sum-exp and argmax (first maximum) of a logit row
+__device__ __forceinline__ void row_stats(const float* x, int nc, float& lse, int& amax) {
+  float mx = x[0];
+  amax = 0;
+  for (int c = 1; c < nc; ++c)
+    if (x[c] > mx) {
+      mx = x[c];
+      amax = c;
+    }
+  float s = 0.f;
+  for (int c = 0; c < nc; ++c) s += expf(x[c] - mx);
+  lse = mx + logf(s);
+}
+
+// sigmoid_focal_loss (torchvision; alpha 0.25, gamma 2) of one logit and its 0/1 target,
+// and its derivative
+__device__ __forceinline__ float focal(float x, float t) {
+  const float p = 1.f / (1.f + expf(-x));
+  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  const float pt = p * t + (1.f - p) * (1.f - t);
+  const float at = 0.25f * t + 0.75f * (1.f - t);
+  return at * ce * (1.f - pt) * (1.f - pt);
+}
+__device__ __forceinline__ float focal_grad(float x, float t) {
+  const float p = 1.f / (1.f + expf(-x));
+  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  const float pt = p * t + (1.f - p) * (1.f - t);
+  const float at = 0.25f * t + 0.75f * (1.f - t);
+  const float q = 1.f - pt;
+  return at * ((p - t) * q * q - 2.f * ce * q * (2.f * t - 1.f) * p * (1.f - p));
+}
+
+__device__ __forceinline__ long term_rows(const rg_loss_args& a, int term) {
+  return term == 0 || term == 1 ? a.n_nodes : (term == 2 ? a.n_pairs : a.n_clusters);
+}
+
+// per (term, block): sum of the row losses (f64) and of the correct argmaxes
+__global__ __launch_bounds__(256) void loss_rows_kernel(rg_loss_args a, double* __restrict__ pl,
+                                                        int* __restrict__ pc) {
+  __shared__ double rl[4];
+  __shared__ int rc[4];
+  const int term = blockIdx.y;
+  const long rows = term_rows(a, term);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double sl = 0.0;
+  int sc = 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < rows; i += (long)gridDim.x * 256) {
+    if (term == 0 || term == 3) {
+      const int nc = a.n_classes;
+      const float* x = term == 0 ? a.node_cls + (size_t)i * nc : a.obj + (size_t)i * nc;
+      const int k = (int)(term == 0 ? a.node_class[i] : a.obj_class[i]);
+      float lse;
+      int am;
+      row_stats(x, nc, lse, am);
+      const float w = term == 0 ? a.class_w[k] : 1.f;
+      sl += (double)(-(w * (x[k] - lse)));
+      sc += am == k;
+    } else if (term == 1) {
+      const float t0 = (a.node_offsets[2 * i] - a.mu_x) / a.sigma_x;
+      const float t1 = (a.node_offsets[2 * i + 1] - a.mu_y) / a.sigma_y;
+      const float d0 = a.node_reg[2 * i] - t0, d1 = a.node_reg[2 * i + 1] - t1;
+      sl += (double)(0.5f * (d0 * d0)) + (double)(0.5f * (d1 * d1));
+    } else {
+      const float* x = a.link + 2 * i;
+      const int k = (int)a.edge_class[i];
+      sl += (double)focal(x[0], k == 0 ? 1.f : 0.f) + (double)focal(x[1], k == 1 ? 1.f : 0.f);
+      sc += (x[1] > x[0] ? 1 : 0) == k;
+    }
+  }
+  sl = wave_sum_d(sl);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o, 64);
+  if (lane == 0) {
+    rl[wave] = sl;
+    rc[wave] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pl[term * PARTS + blockIdx.x] = (rl[0] + rl[1]) + (rl[2] + rl[3]);
+    pc[term * PARTS + blockIdx.x] = rc[0] + rc[1] + rc[2] + rc[3];
+  }
+}
+
+__global__ __launch_bounds__(256) void loss_final_kernel(rg_loss_args a, const double* __restrict__ pl,
+                                                         const int* __restrict__ pc,
+                                                         float* __restrict__ losses,
+                                                         float* __restrict__ acc) {
+  __shared__ double rl[4];
+  __shared__ long long rc[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int term = 0; term < 4; ++term) {
+    double s = 0.0;
+    long long c = 0;
+    for (int i = threadIdx.x; i < PARTS; i += 256) {
+      s += pl[term * PARTS + i];
+      c += pc[term * PARTS + i];
+    }
+    s = wave_sum_d(s);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) {
+      rl[wave] = s;
+      rc[wave] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double tot = (rl[0] + rl[1]) + (rl[2] + rl[3]);
+      const long long cnt = rc[0] + rc[1] + rc[2] + rc[3];
+      const long rows = term_rows(a, term);
+      const float w = term == 0 ? a.w_node_cls : term == 1 ? a.w_node_reg
+                                               : term == 2 ? a.w_edge_cls : a.w_obj_cls;
+      losses[term] = (float)(tot / (double)rows) * w;  // 0 rows: NaN, as torch's 0 / 0
+      const int ai = term == 0 ? 0 : term == 2 ? 1 : term == 3 ? 2 : -1;
+      if (ai >= 0) acc[ai] = (float)((double)cnt / (double)rows);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void loss_backward_kernel(rg_loss_args a, const float* __restrict__ g,
+                                     float* __restrict__ dnc, float* __restrict__ dnr,
+                                     float* __restrict__ dl, float* __restrict__ dob) {
+  const int term = blockIdx.y;
+  const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3];
+  const long rows = term_rows(a, term);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < rows;
+       i += (long)gridDim.x * blockDim.x) {
+    if (term == 0 || term == 3) {
+      const int nc = a.n_classes;
+      const float* x = term == 0 ? a.node_cls + (size_t)i * nc : a.obj + (size_t)i * nc;
+      float* d = term == 0 ? dnc + (size_t)i * nc : dob + (size_t)i * nc;
+      const int k = (int)(term == 0 ? a.node_class[i] : a.obj_class[i]);
+      float lse;
+      int am;
+      row_stats(x, nc, lse, am);
+      const float w = term == 0 ? a.class_w[k] : 1.f;
+      const float sc = term == 0 ? g0 * a.w_node_cls / (float)rows : g3 * a.w_obj_cls / (float)rows;
+      for (int c = 0; c < nc; ++c) d[c] = sc * w * (expf(x[c] - lse) - (c == k ? 1.f : 0.f));
+    } else if (term == 1) {
+      const float t0 = (a.node_offsets[2 * i] - a.mu_x) / a.sigma_x;
+      const float t1 = (a.node_offsets[2 * i + 1] - a.mu_y) / a.sigma_y;
+      const float sc = g1 * a.w_node_reg / (float)rows;
+      dnr[2 * i] = sc * (a.node_reg[2 * i] - t0);
+      dnr[2 * i + 1] = sc * (a.node_reg[2 * i + 1] - t1);
+    } else {
+      const float* x = a.link + 2 * i;
+      const int k = (int)a.edge_class[i];
+      const float sc = g2 * a.w_edge_cls / (float)rows;
+      dl[2 * i] = sc * focal_grad(x[0], k == 0 ? 1.f : 0.f);
+      dl[2 * i + 1] = sc * focal_grad(x[1], k == 1 ? 1.f : 0.f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ SGD
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                           float* __restrict__ buf, long n, float lr, float momentum, float wd,
+                           int first) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float d = fmaf(wd, p[i], g[i]);               // d_p.add(p, alpha=wd)
+  const float b = first ? d : __fadd_rn(__fmul_rn(momentum, buf[i]), d);  // buf.mul_(m).add_(d)
+  buf[i] = b;
+  p[i] = fmaf(-lr, b, p[i]);                          // p.add_(buf, alpha=-lr)
+}
+
+}  // namespace train
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::train;
+
+// ----------------------------------------------------------------------------- C ABI
+extern "C" size_t rg_ffn_backward_workspace_size(void) { return (size_t)PARTS * 2 * sizeof(float); }
+
+extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
+                               int has_norm, const float* mu, const float* std_, int act,
+                               float* dz, int lddz, float* d_mu, float* d_std, void* workspace,
+                               void* stream) {
+  RG_REQUIRE(C >= 1 && C <= 256, RG_ERR_UNSUPPORTED, "rg_ffn_backward: C=%d outside 1..256", C);
+  RG_REQUIRE(!has_norm || (mu && std_ && d_mu && d_std && C >= 2 && workspace), RG_ERR_ARG,
+             "rg_ffn_backward: norm needs mu, std, their gradients, C >= 2 and a workspace");
+  RG_REQUIRE(act >= ACT_NONE && act <= ACT_SWISH, RG_ERR_ARG, "rg_ffn_backward: act %d", act);
+  if (rows <= 0) return RG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  ffn_backward_kernel<<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_, act,
+                                             dz, lddz, part);
+  RG_LAUNCH_CHECK();
+  if (has_norm) {
+    ffn_param_reduce<<<1, 256, 0, st>>>(part, d_mu, d_std);
+    RG_LAUNCH_CHECK();
+  }
+  return RG_OK;
+}
+
+extern "C" size_t rg_linear_grad_workspace_size(long rows, int out_dim, int in_dim) {
+  if (rows <= 0) return 256;
+  const GradGeom g = grad_geom(rows, out_dim, in_dim);
+  return (size_t)g.nchunk * g.ot * g.it * GT * GT * sizeof(float);
+}
+
+extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim,
+                              int in_mode, const float* in0, int ld0, int w0, const float* in1,
+                              int ld1, int w1, const float* in2, int ld2, int w2, const int* idx0,
+                              const int* idx1, float* dW, float* db, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(out_dim >= 1 && in_dim >= 1, RG_ERR_ARG, "rg_linear_grad: dims");
+  RG_REQUIRE(in_mode >= RG_IN_DENSE && in_mode <= RG_IN_PAIRADD, RG_ERR_ARG, "bad in_mode");
+  RG_REQUIRE((in_mode != RG_IN_GATHER3 && in_mode != RG_IN_PAIRADD) || (idx0 && idx1), RG_ERR_ARG,
+             "rg_linear_grad: gather modes need idx0 and idx1");
+  int expect = in_mode == RG_IN_CONCAT2 ? w0 + w1 : in_mode == RG_IN_GATHER3 ? 2 * w0 + w2 : w0;
+  RG_REQUIRE(expect == in_dim, RG_ERR_ARG, "rg_linear_grad: input width %d != in_dim %d", expect,
+             in_dim);
+  if (rows <= 0) return RG_OK;
+  const GradGeom g = grad_geom(rows, out_dim, in_dim);
+  const size_t need = (size_t)g.nchunk * g.ot * g.it * GT * GT * sizeof(float);
+  RG_REQUIRE(workspace_bytes >= need, RG_ERR_ARG, "rg_linear_grad: workspace %zu < %zu",
+             workspace_bytes, need);
+  GradIn in;
+  in.mode = in_mode; in.in_dim = in_dim;
+  in.in0 = in0; in.in1 = in1; in.in2 = in2;
+  in.ld0 = ld0; in.ld1 = ld1; in.ld2 = ld2; in.w0 = w0; in.w1 = w1; in.w2 = w2;
+  in.idx0 = idx0; in.idx1 = idx1;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)(2 * GT * GS + 4 * GT * GT) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)linear_grad_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  linear_grad_kernel<<<dim3(g.nchunk, g.ot, g.it), 256, lds, st>>>(dz, lddz, rows, out_dim, in,
+                                                                   g.rpc, (float*)workspace);
+  RG_LAUNCH_CHECK();
+  const long total = (long)out_dim * (in_dim + 1);
+  linear_grad_reduce<<<ceil_div(total, 256), 256, 0, st>>>((const float*)workspace, g.nchunk, g.ot,
+                                                           g.it, out_dim, in_dim, dW, db);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_incidence_workspace_size(int n_nodes, long n_items) {
+  (void)n_items;
+  return ((size_t)2 * (n_nodes + 1) * sizeof(int) + 255) / 256 * 256 + scan_workspace_bytes(n_nodes);
+}
+
+extern "C" int rg_incidence(const int* a, const int* b, long n_items, int n_nodes, int* ptr,
+                            int* list, void* workspace, size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(n_nodes >= 0 && n_items >= 0 && a, RG_ERR_ARG, "rg_incidence: args");
+  RG_REQUIRE(workspace_bytes >= rg_incidence_workspace_size(n_nodes, n_items), RG_ERR_ARG,
+             "rg_incidence: workspace");
+  hipStream_t st = (hipStream_t)stream;
+  int* cnt = (int*)workspace;
+  int* cursor = cnt + (n_nodes + 1);
+  void* sws = (char*)workspace + ((size_t)2 * (n_nodes + 1) * sizeof(int) + 255) / 256 * 256;
+  if (n_nodes == 0) return RG_OK;
+  RG_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)n_nodes * sizeof(int), st));
+  if (n_items > 0) {
+    inc_count<<<ceil_div(n_items, 256), 256, 0, st>>>(a, b, n_items, cnt);
+    RG_LAUNCH_CHECK();
+  }
+  int rc = exclusive_scan(cnt, n_nodes, ptr, nullptr, sws, st);
+  if (rc) return rc;
+  if (n_items == 0) return RG_OK;
+  RG_CHECK_HIP(hipMemcpyAsync(cursor, ptr, (size_t)n_nodes * sizeof(int), hipMemcpyDeviceToDevice, st));
+  inc_fill<<<ceil_div(n_items, 256), 256, 0, st>>>(a, b, n_items, cursor, list);
+  RG_LAUNCH_CHECK();
+  inc_sort<<<ceil_div(n_nodes, 256), 256, 0, st>>>(ptr, n_nodes, list);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_gather_segment_sum(const float* src, int ld_src, int col0, int width,
+                                     const int* ptr, const int* list, const float* scale,
+                                     int n_nodes, float* out, int ld_out, int accumulate,
+                                     void* stream) {
+  RG_REQUIRE(width >= 1 && width <= 256, RG_ERR_UNSUPPORTED, "rg_gather_segment_sum: width %d",
+             width);
+  if (n_nodes <= 0) return RG_OK;
+  int blocks = ceil_div(n_nodes, 4);
+  if (blocks > 4096) blocks = 4096;
+  gather_segsum_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(
+      src, ld_src, col0, width, ptr, list, scale, n_nodes, out, ld_out, accumulate);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_segment_max_backward(const float* h, int ld_h, int C, const int* cluster_ptr,
+                                       const int* cluster_idx, int n_clusters,
+                                       const float* dpooled, int ld_p, float* dh, int ld_dh,
+                                       void* stream) {
+  if (n_clusters <= 0 || C <= 0) return RG_OK;
+  const long total = (long)n_clusters * C;
+  segmax_backward_kernel<<<ceil_div(total, 256), 256, 0, (hipStream_t)stream>>>(
+      h, ld_h, C, cluster_ptr, cluster_idx, n_clusters, dpooled, ld_p, dh, ld_dh);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_loss_workspace_size(long n_nodes, long n_pairs, long n_clusters) {
+  (void)n_nodes; (void)n_pairs; (void)n_clusters;
+  return (size_t)4 * PARTS * (sizeof(double) + sizeof(int));
+}
+
+extern "C" int rg_loss_graph(const rg_loss_args* args, float* losses, float* acc, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(args && losses && acc, RG_ERR_ARG, "rg_loss_graph: args");
+  RG_REQUIRE(args->n_classes >= 1 && args->n_classes <= 64, RG_ERR_UNSUPPORTED,
+             "rg_loss_graph: n_classes");
+  RG_REQUIRE(workspace_bytes >= rg_loss_workspace_size(0, 0, 0), RG_ERR_ARG,
+             "rg_loss_graph: workspace");
+  hipStream_t st = (hipStream_t)stream;
+  double* pl = (double*)workspace;
+  int* pc = (int*)(pl + 4 * PARTS);
+  loss_rows_kernel<<<dim3(PARTS, 4), 256, 0, st>>>(*args, pl, pc);
+  RG_LAUNCH_CHECK();
+  loss_final_kernel<<<1, 256, 0, st>>>(*args, pl, pc, losses, acc);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_loss_graph_backward(const rg_loss_args* args, const float* g, float* d_node_cls,
+                                      float* d_node_reg, float* d_link, float* d_obj,
+                                      void* stream) {
+  RG_REQUIRE(args && g, RG_ERR_ARG, "rg_loss_graph_backward: args");
+  RG_REQUIRE(args->n_classes >= 1 && args->n_classes <= 64, RG_ERR_UNSUPPORTED,
+             "rg_loss_graph_backward: n_classes");
+  loss_backward_kernel<<<dim3(256, 4), 256, 0, (hipStream_t)stream>>>(
+      *args, g, d_node_cls, d_node_reg, d_link, d_obj);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_sgd_step(float* param, const float* grad, float* momentum_buf, long n, float lr,
+                           float momentum, float weight_decay, int first_step, void* stream) {
+  if (n <= 0) return RG_OK;
+  sgd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(param, grad, momentum_buf, n, lr,
+                                                               momentum, weight_decay, first_step);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

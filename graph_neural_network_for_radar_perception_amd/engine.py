@@ -192,6 +192,10 @@ class ChainPlan:
         if self._signature() != self.sig:
             self._pack()
 
+    def invalidate(self):
+        """Parameters were written behind torch's version counters (FusedSGD)."""
+        self.sig = None
+
     def __call__(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
                  mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
                  idx0=None, idx1=None, residual=None, rows_dev=None):
@@ -437,6 +441,11 @@ class ConvPlan:
         if self.fused and self._sig() != self.fused_sig:
             self._pack_fused()
 
+    def invalidate(self):
+        for c in self.chains():
+            c.invalidate()
+        self.fused_sig = None
+
     def run_fused(self, x, e, g, x_out) -> bool:
         """One launch for the whole layer; False when the fused kernel does not
         cover this shape (the caller runs the unfused chain + reduce path)."""
@@ -489,6 +498,14 @@ class ModelPlans:
                 c.refresh()
         for cv in self.convs:
             cv.refresh()
+
+    def invalidate(self):
+        for c in (self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
+                  self.cls_head, self.link_node, self.cls_stem):
+            if c is not None:
+                c.invalidate()
+        for cv in self.convs:
+            cv.invalidate()
 
 
 @dataclass

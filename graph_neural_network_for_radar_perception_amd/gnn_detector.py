@@ -114,6 +114,11 @@ class Model_Inference(nn.Module):
         self.meas_noise_cov = np.array([[0.5, 0.0], [0.0, 0.5]], dtype=np.float32)
         self.clustering_eps = eps
 
+    def invalidate_plans(self):
+        """Re-pack every plan on next use (weights written outside torch, FusedSGD)."""
+        for p in self._plans.values():
+            p.invalidate()
+
     def plans(self, dtype: Optional[str] = None) -> engine.ModelPlans:
         dtype = dtype or self.compute_dtype
         p = self._plans.get(dtype)
@@ -137,9 +142,9 @@ class Model_Inference(nn.Module):
         fifth value, the per-frame cluster member lists, is returned."""
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             raise NotImplementedError(
-                'backward through the HIP forward is not implemented yet (training path is '
-                'the next milestone); run inference under torch.no_grad() or model.eval() with '
-                'requires_grad_(False)')
+                'Model_Inference.forward has no autograd graph: train through '
+                'Model_Training.forward (native forward tape + backward, training.py), or run '
+                'inference under torch.no_grad()')
         engine._require_device(node_features[0], 'node_features')
         proposals = cluster_node_idx is None
         if proposals:
@@ -226,7 +231,14 @@ class Model_Inference(nn.Module):
 
 class Model_Training(nn.Module):
     """gnn_detector.py:419-478 (``pred`` = Model_Inference; frames of the batch
-    run as ONE batched forward instead of a Python loop)."""
+    run as ONE batched graph instead of a Python loop).
+
+    With autograd enabled (training.py:66-85: ``loss, acc = detector(...)``,
+    ``total.backward()``, ``optimizer.step()``) the forward runs the float32 training
+    tape and the returned losses carry a native backward (training._TrainStep): any
+    torch optimizer works, and ``fused_sgd()`` gives the one-launch SGD on flat buffers.
+    Under ``torch.no_grad()`` (validation, training.py:112-118) it is the inference
+    forward plus the native loss kernel."""
 
     def __init__(self, net_config, device):
         super().__init__()
@@ -236,57 +248,99 @@ class Model_Training(nn.Module):
         self.offset_sigma = net_config.offset_sigma
         self.net_config = net_config
         self.class_weights = torch.tensor(net_config.class_weights_dyn, dtype=torch.float32)
+        self._train_engine = None
 
     def predict(self, node_features, edge_features, edge_index, cluster_node_idx):
         return det_named_tuple(*self.pred.forward_frames(node_features, edge_features, edge_index,
                                                          cluster_node_idx))
 
+    def train_engine(self):
+        from .training import TrainEngine
+        dev = next(self.parameters()).device
+        if self._train_engine is None or self._train_engine.device != dev:
+            self._train_engine = TrainEngine(self, dev)
+        return self._train_engine
+
+    def invalidate_plans(self):
+        self.pred.invalidate_plans()
+        if self._train_engine is not None:
+            self._train_engine.invalidate()
+
+    def fused_sgd(self, lr: float, momentum: float = 0.9, weight_decay: float = 0.0):
+        """torch.optim.SGD(params, momentum, lr, weight_decay) (set_param_for_training_gnn.py:46)
+        as training.FusedSGD: one rg_sgd_step launch; step(flat_grad) after backward."""
+        from .training import FusedSGD
+        return FusedSGD([p for p in self.parameters()], lr, momentum, weight_decay,
+                        on_update=self.invalidate_plans)
+
+    def _labels(self, labels, dev):
+        return {'node_class': torch.cat(labels['node_class'], 0).to(dev, torch.int64).contiguous(),
+                'node_offsets': torch.cat(labels['node_offsets'], 0).to(dev, torch.float32).contiguous(),
+                'edge_class': torch.cat(labels['edge_class'], 0).to(dev, torch.int64).contiguous(),
+                'cluster_labels': torch.cat(labels['cluster_labels'], 0).to(dev, torch.int64).contiguous(),
+                'class_weights': self.class_weights.to(dev).contiguous()}
+
     def forward(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
                 edge_index: List[torch.Tensor], adj_matrix: List[torch.Tensor],
                 labels: Dict[str, List[torch.Tensor]]):
-        pred = self.predict(node_features, edge_features, edge_index, labels['cluster_node_idx'])
-        gt = det_named_tuple(
-            torch.cat(labels['node_class'], 0),
-            _normalize_offsets(torch.cat(labels['node_offsets'], 0).clone(), self.offset_mu,
-                               self.offset_sigma),
-            torch.cat(labels['edge_class'], 0),
-            torch.cat(labels['cluster_labels'], 0))
-        loss = _loss_graph(self.net_config, self.class_weights.to(pred.node_class_logits.device),
-                           pred, gt)
-        acc = {'segment_accuracy': compute_accuracy(pred.node_class_logits, gt.node_class_logits),
-               'edge_accuracy': compute_accuracy(pred.edge_class_logits, gt.edge_class_logits),
-               'object_accuracy': compute_accuracy(pred.obj_class_logits, gt.obj_class_logits)}
+        dev = node_features[0].device
+        engine._require_device(node_features[0], 'node_features')
+        lab = self._labels(labels, dev)
+        names = ('loss_node_cls', 'loss_node_reg', 'loss_edge_cls', 'loss_obj_cls')
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from .training import train_step_losses
+            nf, ef, ei, cptr, cidx, ncl, _ = _batch_frames(node_features, edge_features, edge_index,
+                                                           labels['cluster_node_idx'])
+            g = engine.DeviceGraph.from_edge_index(ei, nf.shape[0])
+            e_dst = _edges_dst_major(ef, g)
+            eng = self.train_engine()
+            losses = train_step_losses(eng, (nf, e_dst, g, cptr, cidx, ncl, lab))
+            acc_t = eng.last_acc
+        else:
+            pred = self.predict(node_features, edge_features, edge_index, labels['cluster_node_idx'])
+            losses, acc_t = native_loss_graph(self.net_config, pred, lab)
+        loss = {k: losses[i] for i, k in enumerate(names)}
+        acc = {'segment_accuracy': acc_t[0], 'edge_accuracy': acc_t[1],
+               'object_accuracy': acc_t[2]}
         return loss, acc
 
 
-def _normalize_offsets(off, mu, sigma):
-    """compute_offsets.py:6-11."""
-    off[..., 0] = (off[..., 0] - mu[0]) / sigma[0]
-    off[..., 1] = (off[..., 1] - mu[1]) / sigma[1]
-    return off
+def _edges_dst_major(ef: torch.Tensor, g: engine.DeviceGraph) -> torch.Tensor:
+    from . import _native as nat
+    E = g.n_edges
+    e_dst = torch.empty((max(E, 1), ef.shape[1]), dtype=torch.float32, device=ef.device)
+    if E > 0:
+        nat.check(nat.lib().rg_gather_rows_f32(ef.data_ptr(), g.perm.data_ptr(), E, ef.shape[1],
+                                               e_dst.data_ptr(), nat.stream_ptr(ef.device)),
+                  'rg_gather_rows_f32')
+    return e_dst
 
 
-def _loss_graph(cfg, class_weights, pred, gt):
-    """Loss_Graph.forward (loss.py:37-76) evaluated on the HIP forward's outputs
-    (validation-time loss; the training backward is the next milestone)."""
-    n_cls, n_edge = cfg.num_classes, cfg.num_edge_classes
-    node_t = F.one_hot(gt.node_class_logits, n_cls).to(torch.float32)
-    edge_t = F.one_hot(gt.edge_class_logits, n_edge).to(torch.float32)
-    obj_t = F.one_hot(gt.obj_class_logits, n_cls).to(torch.float32)
-    x = pred.edge_class_logits
-    p = torch.sigmoid(x)
-    ce = F.binary_cross_entropy_with_logits(x, edge_t, reduction='none')
-    p_t = p * edge_t + (1 - p) * (1 - edge_t)
-    focal = (0.25 * edge_t + 0.75 * (1 - edge_t)) * ce * (1 - p_t) ** 2.0
-    edge_l = focal.sum(-1)
-    edge_l = edge_l.sum() / edge_l.shape[0]
-    node_l = F.cross_entropy(pred.node_class_logits, node_t, class_weights, reduction='none')
-    node_l = node_l.sum() / node_l.shape[0]
-    reg_l = 0.5 * F.mse_loss(pred.node_reg_deltas, gt.node_reg_deltas, reduction='none').sum(-1)
-    reg_l = reg_l.sum() / reg_l.shape[0]
-    obj_l = F.cross_entropy(pred.obj_class_logits, obj_t, reduction='none')
-    obj_l = obj_l.sum() / obj_l.shape[0]
-    return {'loss_node_cls': node_l * cfg.node_cls_loss_weight,
-            'loss_node_reg': reg_l * cfg.node_reg_loss_weight,
-            'loss_edge_cls': edge_l * cfg.edge_cls_loss_weight,
-            'loss_obj_cls': obj_l * cfg.obj_cls_loss_weight}
+def native_loss_graph(cfg, pred, lab):
+    """Loss_Graph.forward (loss.py:37-76) + compute_accuracy on the device (rg_loss_graph):
+    returns (losses f32 [4], accuracies f32 [3])."""
+    import ctypes
+    from . import _native as nat
+    lib = nat.lib()
+    outs = [t.to(torch.float32).contiguous() for t in pred]
+    dev = outs[0].device
+    N, U, ncl = outs[0].shape[0], outs[2].shape[0], outs[3].shape[0]
+    a = nat.rg_loss_args()
+    a.node_cls, a.node_reg, a.link, a.obj = (t.data_ptr() for t in outs)
+    a.node_class = lab['node_class'].data_ptr()
+    a.node_offsets = lab['node_offsets'].data_ptr()
+    a.edge_class = lab['edge_class'].data_ptr()
+    a.obj_class = lab['cluster_labels'].data_ptr()
+    a.class_w = lab['class_weights'].data_ptr()
+    a.n_nodes, a.n_pairs, a.n_clusters = N, U, ncl
+    a.n_classes = outs[0].shape[1]
+    a.mu_x, a.mu_y = float(cfg.offset_mu[0]), float(cfg.offset_mu[1])
+    a.sigma_x, a.sigma_y = float(cfg.offset_sigma[0]), float(cfg.offset_sigma[1])
+    a.w_node_cls, a.w_node_reg = float(cfg.node_cls_loss_weight), float(cfg.node_reg_loss_weight)
+    a.w_edge_cls, a.w_obj_cls = float(cfg.edge_cls_loss_weight), float(cfg.obj_cls_loss_weight)
+    losses = torch.empty(4, dtype=torch.float32, device=dev)
+    acc = torch.empty(3, dtype=torch.float32, device=dev)
+    ws = torch.empty(lib.rg_loss_workspace_size(N, U, ncl), dtype=torch.uint8, device=dev)
+    nat.check(lib.rg_loss_graph(ctypes.byref(a), losses.data_ptr(), acc.data_ptr(), ws.data_ptr(),
+                                ws.numel(), nat.stream_ptr(dev)), 'rg_loss_graph')
+    return losses, acc

@@ -1,0 +1,537 @@
+"""Native training step: Model_Training.forward + Loss_Graph + backward (+ SGD).
+
+Reference: ``modules/neural_net/gnn/gnn_detector.py:419-478`` (Model_Training),
+``loss.py:37-76`` (Loss_Graph), ``training.py:66-85`` (loss.backward(); optimizer.step()),
+``set_param_for_training_gnn.py:44-46`` (SGD, momentum 0.9).
+
+Everything runs in float32 (the reference trains in f32) on the HIP library:
+
+  forward   rg_mlp_chain with rg_layer.save_pre / save_out (one launch per chain, the
+            tape = every layer's pre-normalisation and activation rows), rg_segment_reduce
+            (aggregation, cluster max), rg_loss_graph (losses + accuracies)
+  backward  rg_loss_graph_backward (logit gradients), per layer rg_ffn_backward
+            (normalisation + activation), rg_linear_grad (dW, db over the layer's input
+            rows, gathered on the fly), rg_mlp_chain on W packed transposed (dX = dZ W),
+            rg_gather_segment_sum / rg_incidence (the transposes of the gathers:
+            x_i = x[dst] is a segment sum over the destination-major CSR, x_j = x[src]
+            and the link pairs' x[i] + x[j] are sums over incidence lists),
+            rg_segment_max_backward (object head)
+  update    rg_sgd_step on the flat parameter / gradient buffers (FusedSGD)
+
+This module only sequences calls and owns buffers.  The batch of frames is one
+disjoint-union graph, as in the forward (engine.forward_batched): every operator is per
+row or per destination, and the losses are sums over rows divided by the batch's row
+counts (loss.py:59-73 on the concatenated predictions), so batching is exact.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _native as nat
+from . import engine
+from .engine import ChainPlan, specs_from_modules
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f'training path is float32; got {t.dtype}')
+    return t
+
+
+class Workspaces:
+    """Device scratch reused across calls (grown on demand)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs: Dict[str, torch.Tensor] = {}
+
+    def get(self, name: str, nbytes: int) -> torch.Tensor:
+        t = self.bufs.get(name)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+            self.bufs[name] = t
+        return t
+
+
+@dataclass
+class ChainTape:
+    rows: int
+    mode: int
+    in0: torch.Tensor
+    w0: int
+    in1: Optional[torch.Tensor]
+    w1: int
+    in2: Optional[torch.Tensor]
+    w2: int
+    idx0: Optional[torch.Tensor]
+    idx1: Optional[torch.Tensor]
+    z: List[torch.Tensor]
+    a: List[torch.Tensor]
+
+
+class TrainChain:
+    """One sequence of ffn_blocks / Linears (a ChainPlan in fp32) with its tape and
+    backward.  Gradients accumulate into ``grads[param]`` tensors."""
+
+    def __init__(self, mods, device, ws: Workspaces):
+        self.specs = specs_from_modules(mods)
+        if len(self.specs) > nat.MAX_LAYERS:
+            raise NotImplementedError(f'chain of {len(self.specs)} layers > {nat.MAX_LAYERS}')
+        self.plan = ChainPlan(self.specs, 'fp32', device)
+        self.device = torch.device(device)
+        self.ws = ws
+        self._tsig = None
+        self.in_dim = self.plan.in_dim
+        self.out_dim = self.plan.out_dim
+
+    def refresh(self):
+        self.plan.refresh()
+
+    def invalidate(self):
+        self.plan.sig = None
+        self._tsig = None
+
+    def _transposed(self):
+        """W^T of every layer packed as an RG_F32 layer (no bias / norm / activation):
+        the data GEMM of the backward, dX = dZ W, on the chain kernel."""
+        sig = self.plan.sig
+        if self._tsig == sig:
+            return self._tarr
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        fmt = nat.RG_F32 | nat.RG_PACK_TRANSPOSE
+        sizes = [lib.rg_packed_linear_bytes(s.out_dim, s.in_dim, nat.RG_F32) for s in self.specs]
+        offs, tot = [], 0
+        for sz in sizes:
+            offs.append(tot)
+            tot += (sz + 255) // 256 * 256
+        self._tbuf = torch.empty(tot, dtype=torch.uint8, device=self.device)
+        self._tarr = []
+        for s, off in zip(self.specs, offs):
+            w = s.weight.detach()
+            nat.check(lib.rg_pack_linear(w.data_ptr(), None, s.out_dim, s.in_dim, fmt,
+                                         self._tbuf.data_ptr() + off, st), 'rg_pack_linear')
+            arr = (nat.rg_layer * 1)()
+            arr[0].w_packed = self._tbuf.data_ptr() + off
+            arr[0].in_dim = s.out_dim
+            arr[0].out_dim = s.in_dim
+            arr[0].act = nat.ACT['none']
+            self._tarr.append(arr)
+        self._tsig = sig
+        return self._tarr
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
+                mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
+                idx0=None, idx1=None, residual=None) -> ChainTape:
+        self.plan.refresh()
+        lib = nat.lib()
+        dev = self.device
+        arr0, n, _ = self.plan.groups[0]
+        arr = (nat.rg_layer * n)()
+        z, a = [], []
+        for i in range(n):
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(arr0[i]), ctypes.sizeof(nat.rg_layer))
+            zi = torch.empty((max(rows, 1), self.specs[i].out_dim), dtype=torch.float32, device=dev)
+            ai = torch.empty_like(zi)
+            arr[i].save_pre = zi.data_ptr()
+            arr[i].save_out = ai.data_ptr()
+            z.append(zi)
+            a.append(ai)
+        rc = lib.rg_mlp_chain(
+            nat.RG_F32, arr, n, int(rows), None, mode, nat.RG_F32, in0.data_ptr(), in0.stride(0), w0,
+            nat.ptr(in1), in1.stride(0) if in1 is not None else 0, w1,
+            nat.ptr(in2), in2.stride(0) if in2 is not None else 0, w2,
+            nat.ptr(idx0), nat.ptr(idx1),
+            nat.ptr(residual), residual.stride(0) if residual is not None else 0, nat.RG_F32,
+            out.data_ptr(), out.stride(0), nat.RG_F32, nat.stream_ptr(dev))
+        nat.check(rc, 'rg_mlp_chain (training tape)')
+        return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, tape: ChainTape, d_out: torch.Tensor, grads: Dict[int, torch.Tensor],
+                 din: Optional[torch.Tensor] = None, din_accumulate: bool = False):
+        """d_out: f32 [rows][out_dim] gradient of the chain output (overwritten).
+        Parameter gradients accumulate into grads[id(param)]; with ``din`` the gradient of
+        the chain input (dense [rows][in_dim]) is written (or added) there."""
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        rows = tape.rows
+        if rows <= 0:
+            return
+        tarr = self._transposed()
+        dA = d_out
+        for l in range(len(self.specs) - 1, -1, -1):
+            sp = self.specs[l]
+            act = nat.ACT[sp.act]
+            has_norm = sp.mu is not None
+            if has_norm or act != 0:
+                ws = self.ws.get('ffn', lib.rg_ffn_backward_workspace_size())
+                nat.check(lib.rg_ffn_backward(
+                    tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0), rows,
+                    sp.out_dim, int(has_norm), nat.ptr(sp.mu), nat.ptr(sp.std), act, dA.data_ptr(),
+                    dA.stride(0), nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
+                    ws.data_ptr(), st), 'rg_ffn_backward')
+            dZ = dA
+            # dW, db over this layer's input rows
+            if l == 0:
+                m, i0, w0, i1, w1, i2, w2 = (tape.mode, tape.in0, tape.w0, tape.in1, tape.w1,
+                                             tape.in2, tape.w2)
+                x0, x1 = tape.idx0, tape.idx1
+            else:
+                m, i0, w0, i1, w1, i2, w2 = nat.IN_DENSE, tape.a[l - 1], sp.in_dim, None, 0, None, 0
+                x0 = x1 = None
+            wsz = lib.rg_linear_grad_workspace_size(rows, sp.out_dim, sp.in_dim)
+            ws = self.ws.get('lgrad', wsz)
+            nat.check(lib.rg_linear_grad(
+                dZ.data_ptr(), dZ.stride(0), rows, sp.out_dim, sp.in_dim, m, i0.data_ptr(),
+                i0.stride(0), w0, nat.ptr(i1), i1.stride(0) if i1 is not None else 0, w1,
+                nat.ptr(i2), i2.stride(0) if i2 is not None else 0, w2, nat.ptr(x0), nat.ptr(x1),
+                grads[id(sp.weight)].data_ptr(), nat.ptr(grads.get(id(sp.bias))) if sp.bias is not None
+                else None, ws.data_ptr(), ws.numel(), st), 'rg_linear_grad')
+            if l == 0 and din is None:
+                break
+            if l == 0:
+                out, res = din, (din if din_accumulate else None)
+            else:
+                out = torch.empty((rows, sp.in_dim), dtype=torch.float32, device=self.device)
+                res = None
+            nat.check(lib.rg_mlp_chain(
+                nat.RG_F32, tarr[l], 1, rows, None, nat.IN_DENSE, nat.RG_F32, dZ.data_ptr(),
+                dZ.stride(0), sp.out_dim, None, 0, 0, None, 0, 0, None, None,
+                nat.ptr(res), res.stride(0) if res is not None else 0, nat.RG_F32,
+                out.data_ptr(), out.stride(0), nat.RG_F32, st), 'rg_mlp_chain (dX = dZ W)')
+            dA = out
+
+
+class TrainConv:
+    def __init__(self, blk, device, ws):
+        self.aggr = blk.aggr
+        if self.aggr not in ('add', 'sum', 'mean'):
+            raise NotImplementedError(f'training with aggregation {self.aggr!r} (the shipped '
+                                      'configuration uses add, configuration_radarscenes_gnn.yml:55)')
+        self.msg = TrainChain(list(blk.msg), device, ws)
+        self.upd = TrainChain(list(blk.upd), device, ws)
+        self.res = (TrainChain([blk.residual_connection], device, ws)
+                    if blk.residual_connection is not None else None)
+
+    def chains(self):
+        return [c for c in (self.msg, self.upd, self.res) if c is not None]
+
+
+class TrainEngine:
+    """Forward-with-tape and backward of a whole Model_Inference (``pred``)."""
+
+    def __init__(self, model_training, device):
+        self.model = model_training
+        pred = model_training.pred
+        self.device = torch.device(device)
+        self.ws = Workspaces(self.device)
+        mk = lambda mods: TrainChain(mods, self.device, self.ws)  # noqa: E731
+        self.node_enc = mk(list(pred.encode_node_feat.encoder))
+        self.edge_enc = mk(list(pred.encode_edge_feat.encoder))
+        self.convs = [TrainConv(b, self.device, self.ws) for b in pred.pass_messages.conv_blk]
+        pn, po, pl, pc = pred.predict_node, pred.predict_offset, pred.predict_link, pred.predict_class
+        self.node_head = mk(list(pn.stem) + [pn.pred_cls.head[0], pn.pred_cls.head[1]])
+        self.offset_head = mk(list(po.stem) + [po.pred_offsets.head[0], po.pred_offsets.head[1]])
+        self.link_node = mk(list(pl.compute_edge.stem)) if len(pl.compute_edge.stem) else None
+        self.link_pair = mk(list(pl.stem) + [pl.pred_cls.head[0], pl.pred_cls.head[1]])
+        self.cls_stem = mk(list(pc.stem)) if len(pc.stem) else None
+        self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
+        # flat gradient buffer: one view per parameter (one bucket for the DDP all-reduce)
+        self.params = [p for p in model_training.parameters()]
+        n = sum(p.numel() for p in self.params)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.grads: Dict[int, torch.Tensor] = {}
+        o = 0
+        for p in self.params:
+            self.grads[id(p)] = self.flat_grad[o:o + p.numel()].view_as(p)
+            o += p.numel()
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, nf, e_dst, g: engine.DeviceGraph, cptr, cidx, ncl: int, labels: dict):
+        """Model_Training.forward on a batched graph.  labels (device): node_class int64 [N],
+        node_offsets f32 [N,2] (raw), edge_class int64 [U] (pair order), cluster_labels
+        int64 [Ncl].  Returns (losses f32 [4], accuracies f32 [3], tape)."""
+        lib = nat.lib()
+        dev = self.device
+        st = nat.stream_ptr(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        N, E, U = g.n_nodes, g.n_edges, g.n_pairs
+        T = {}
+        x = torch.empty((N, self.node_enc.out_dim), **f32)
+        T['node_enc'] = self.node_enc.forward(N, x, nf, nf.shape[1])
+        e = torch.empty((max(E, 1), self.edge_enc.out_dim), **f32)
+        T['edge_enc'] = self.edge_enc.forward(E, e, e_dst, e_dst.shape[1])
+        xs = [x]
+        T['conv'] = []
+        for cv in self.convs:
+            C = x.shape[1]
+            ct = {}
+            msg = torch.empty((max(E, 1), cv.msg.out_dim), **f32)
+            ct['msg'] = cv.msg.forward(E, msg, x, C, mode=nat.IN_GATHER3, in2=e, w2=e.shape[1],
+                                       idx0=g.dst, idx1=g.src)
+            agg = torch.empty((N, cv.msg.out_dim), **f32)
+            engine.segment_reduce(msg, g.seg_ptr, N, cv.aggr, agg)
+            ct['agg'] = agg
+            if cv.res is not None:
+                ident = torch.empty((N, cv.upd.out_dim), **f32)
+                ct['res'] = cv.res.forward(N, ident, x, C)
+            else:
+                ident = x
+            xn = torch.empty((N, cv.upd.out_dim), **f32)
+            ct['upd'] = cv.upd.forward(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg,
+                                       w1=cv.msg.out_dim, residual=ident)
+            T['conv'].append(ct)
+            x = xn
+            xs.append(x)
+        T['xs'] = xs
+        C = x.shape[1]
+        node_cls = torch.empty((N, self.node_head.out_dim), **f32)
+        T['node_head'] = self.node_head.forward(N, node_cls, x, C)
+        node_reg = torch.empty((N, self.offset_head.out_dim), **f32)
+        T['offset_head'] = self.offset_head.forward(N, node_reg, x, C)
+        if self.link_node is not None:
+            s = torch.empty((N, self.link_node.out_dim), **f32)
+            T['link_node'] = self.link_node.forward(N, s, x, C)
+        else:
+            s = x
+        T['s'] = s
+        link = torch.empty((max(U, 1), self.link_pair.out_dim), **f32)
+        T['link_pair'] = self.link_pair.forward(U, link, s, s.shape[1], mode=nat.IN_PAIRADD,
+                                                idx0=g.pair_src, idx1=g.pair_dst)
+        if self.cls_stem is not None:
+            h = torch.empty((N, self.cls_stem.out_dim), **f32)
+            T['cls_stem'] = self.cls_stem.forward(N, h, x, C)
+        else:
+            h = x
+        T['h'] = h
+        pooled = torch.empty((max(ncl, 1), h.shape[1]), **f32)
+        engine.segment_reduce(h, cptr, ncl, 'max', pooled, idx=cidx)
+        obj = torch.empty((max(ncl, 1), self.cls_head.out_dim), **f32)
+        T['cls_head'] = self.cls_head.forward(ncl, obj, pooled, pooled.shape[1])
+        outs = (node_cls, node_reg, link[:U], obj[:ncl])
+        losses = torch.empty(4, **f32)
+        acc = torch.empty(3, **f32)
+        args = self._loss_args(outs, labels, N, U, ncl)
+        ws = self.ws.get('loss', lib.rg_loss_workspace_size(N, U, ncl))
+        nat.check(lib.rg_loss_graph(ctypes.byref(args), losses.data_ptr(), acc.data_ptr(),
+                                    ws.data_ptr(), ws.numel(), st), 'rg_loss_graph')
+        T.update(g=g, cptr=cptr, cidx=cidx, ncl=ncl, outs=outs, labels=labels, args=args,
+                 N=N, E=E, U=U)
+        return losses, acc, T
+
+    def _loss_args(self, outs, labels, N, U, ncl):
+        cfg = self.model.net_config
+        a = nat.rg_loss_args()
+        a.node_cls, a.node_reg, a.link, a.obj = (t.data_ptr() for t in outs)
+        a.node_class = labels['node_class'].data_ptr()
+        a.node_offsets = labels['node_offsets'].data_ptr()
+        a.edge_class = labels['edge_class'].data_ptr()
+        a.obj_class = labels['cluster_labels'].data_ptr()
+        a.class_w = labels['class_weights'].data_ptr()
+        a.n_nodes, a.n_pairs, a.n_clusters = N, U, ncl
+        a.n_classes = outs[0].shape[1]
+        a.mu_x, a.mu_y = float(cfg.offset_mu[0]), float(cfg.offset_mu[1])
+        a.sigma_x, a.sigma_y = float(cfg.offset_sigma[0]), float(cfg.offset_sigma[1])
+        a.w_node_cls = float(cfg.node_cls_loss_weight)
+        a.w_node_reg = float(cfg.node_reg_loss_weight)
+        a.w_edge_cls = float(cfg.edge_cls_loss_weight)
+        a.w_obj_cls = float(cfg.obj_cls_loss_weight)
+        return a
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, T: dict, g_losses: torch.Tensor, zero_grads: bool = True):
+        """Gradients of sum_i g_losses[i] * losses[i] into self.flat_grad."""
+        lib = nat.lib()
+        dev = self.device
+        st = nat.stream_ptr(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        if zero_grads:
+            self.flat_grad.zero_()
+        G = self.grads
+        g, N, E, U, ncl = T['g'], T['N'], T['E'], T['U'], T['ncl']
+        node_cls, node_reg, link, obj = T['outs']
+        d_nc = torch.empty_like(node_cls)
+        d_nr = torch.empty_like(node_reg)
+        d_l = torch.empty((max(U, 1), link.shape[1]), **f32)
+        d_o = torch.empty((max(ncl, 1), obj.shape[1]), **f32)
+        gl = g_losses.detach().to(torch.float32).contiguous()
+        nat.check(lib.rg_loss_graph_backward(ctypes.byref(T['args']), gl.data_ptr(),
+                                             d_nc.data_ptr(), d_nr.data_ptr(), d_l.data_ptr(),
+                                             d_o.data_ptr(), st), 'rg_loss_graph_backward')
+        x = T['xs'][-1]
+        C = x.shape[1]
+        dx = torch.zeros((N, C), **f32)
+        # heads (gnn_blocks.py:200-389)
+        self.node_head.backward(T['node_head'], d_nc, G, din=dx, din_accumulate=True)
+        self.offset_head.backward(T['offset_head'], d_nr, G, din=dx, din_accumulate=True)
+        s = T['s']
+        d_pairin = torch.empty((max(U, 1), s.shape[1]), **f32)
+        self.link_pair.backward(T['link_pair'], d_l, G, din=d_pairin)
+        ptr, lst = self._incidence('pairs', g.pair_src, g.pair_dst, U, N)
+        if self.link_node is not None:
+            ds = torch.empty((N, s.shape[1]), **f32)
+            self._segsum(d_pairin, 0, s.shape[1], ptr, lst, None, ds, accumulate=False)
+            self.link_node.backward(T['link_node'], ds, G, din=dx, din_accumulate=True)
+        else:
+            self._segsum(d_pairin, 0, s.shape[1], ptr, lst, None, dx, accumulate=True)
+        h = T['h']
+        d_pooled = torch.empty((max(ncl, 1), h.shape[1]), **f32)
+        self.cls_head.backward(T['cls_head'], d_o, G, din=d_pooled)
+        dh = torch.zeros((N, h.shape[1]), **f32) if self.cls_stem is not None else dx
+        nat.check(lib.rg_segment_max_backward(h.data_ptr(), h.stride(0), h.shape[1],
+                                              T['cptr'].data_ptr(), T['cidx'].data_ptr(), ncl,
+                                              d_pooled.data_ptr(), d_pooled.stride(0),
+                                              dh.data_ptr(), dh.stride(0), st),
+                  'rg_segment_max_backward')
+        if self.cls_stem is not None:
+            self.cls_stem.backward(T['cls_stem'], dh, G, din=dx, din_accumulate=True)
+        # message passing, last layer first (gnn_blocks.py:96-113, 150-164)
+        e_enc_out_dim = self.edge_enc.out_dim
+        de = torch.zeros((max(E, 1), e_enc_out_dim), **f32)
+        eptr = self._identity_ptr(E)
+        src_ptr, src_lst = self._incidence('src', g.src, None, E, N)
+        for li in range(len(self.convs) - 1, -1, -1):
+            cv, ct = self.convs[li], T['conv'][li]
+            x_in = T['xs'][li]
+            Cin = x_in.shape[1]
+            Cm = cv.msg.out_dim
+            # x_out = ident + upd(cat(x, agg))
+            d_updin = torch.empty((N, Cin + Cm), **f32)
+            cv.upd.backward(ct['upd'], dx.clone(), G, din=d_updin)   # (d_out is consumed)
+            if cv.res is not None:
+                dx_new = torch.empty((N, Cin), **f32)
+                cv.res.backward(ct['res'], dx, G, din=dx_new)
+            else:
+                dx_new = dx   # identity: d x += d x_out (already in dx)
+            # d x += first half of the update input gradient
+            self._add_cols(d_updin, 0, Cin, dx_new)
+            # d msg[p] = d agg[dst[p]] (mean: / count)
+            d_msg = torch.empty((max(E, 1), Cm), **f32)
+            scale = self._mean_scale(g, N) if cv.aggr == 'mean' else None
+            self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
+            dG = torch.empty((max(E, 1), cv.msg.in_dim), **f32)
+            cv.msg.backward(ct['msg'], d_msg, G, din=dG)
+            # x_i = x[dst]: segment sums over the destination-major CSR
+            self._segsum(dG, 0, Cin, g.seg_ptr, None, None, dx_new, accumulate=True)
+            # x_j = x[src]: sums over each node's outgoing positions
+            self._segsum(dG, Cin, Cin, src_ptr, src_lst, None, dx_new, accumulate=True)
+            # e (the same encoded edges every layer, gnn_blocks.py:159-163)
+            self._segsum(dG, 2 * Cin, e_enc_out_dim, eptr, None, None, de, accumulate=True)
+            dx = dx_new
+        # encoders (gnn_blocks.py:19-42): inputs are data, no input gradient
+        self.edge_enc.backward(T['edge_enc'], de, G)
+        self.node_enc.backward(T['node_enc'], dx, G)
+
+    def chains(self):
+        out = [self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
+               self.cls_head]
+        out += [c for c in (self.link_node, self.cls_stem) if c is not None]
+        for cv in self.convs:
+            out += cv.chains()
+        return out
+
+    def invalidate(self):
+        """Parameters changed behind torch's version counters (FusedSGD): re-pack."""
+        for c in self.chains():
+            c.invalidate()
+
+    # ------------------------------------------------------------------ helpers
+    def _segsum(self, src, col0, width, ptr, lst, scale, out, accumulate):
+        lib = nat.lib()
+        nat.check(lib.rg_gather_segment_sum(src.data_ptr(), src.stride(0), col0, width,
+                                            ptr.data_ptr(), nat.ptr(lst), nat.ptr(scale),
+                                            out.shape[0], out.data_ptr(), out.stride(0),
+                                            int(accumulate), nat.stream_ptr(self.device)),
+                  'rg_gather_segment_sum')
+
+    def _add_cols(self, src, col0, width, out):
+        """out[n][:] += src[n][col0:col0+width] (a one-row segment sum)."""
+        self._segsum(src, col0, width, self._identity_ptr(out.shape[0]), None, None, out, True)
+
+    def _identity_ptr(self, n):
+        key = ('iota', n)
+        t = self.ws.bufs.get(key)
+        if t is None:
+            t = torch.arange(n + 1, dtype=torch.int32, device=self.device)
+            self.ws.bufs[key] = t
+        return t
+
+    def _incidence(self, name, a, b, n_items, n_nodes):
+        lib = nat.lib()
+        ptr = torch.empty(n_nodes + 1, dtype=torch.int32, device=self.device)
+        lst = torch.empty(max(n_items * (2 if b is not None else 1), 1), dtype=torch.int32,
+                          device=self.device)
+        ws = self.ws.get('inc', lib.rg_incidence_workspace_size(n_nodes, n_items))
+        nat.check(lib.rg_incidence(a.data_ptr(), nat.ptr(b), n_items, n_nodes, ptr.data_ptr(),
+                                   lst.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   nat.stream_ptr(self.device)), 'rg_incidence')
+        return ptr, lst
+
+    def _mean_scale(self, g, N):
+        deg = (g.seg_ptr[1:] - g.seg_ptr[:-1]).clamp(min=1).to(torch.float32)
+        return 1.0 / deg
+
+
+class _TrainStep(torch.autograd.Function):
+    """Loss_Graph values as an autograd node over every parameter: loss.backward()
+    (training.py:77) runs TrainEngine.backward and hands torch the flat gradients."""
+
+    @staticmethod
+    def forward(ctx, engine_, batch, *params):
+        losses, acc, tape = engine_.forward(*batch)
+        ctx.engine = engine_
+        ctx.tape = tape
+        engine_.last_acc = acc
+        return losses
+
+    @staticmethod
+    def backward(ctx, g_losses):
+        eng = ctx.engine
+        eng.backward(ctx.tape, g_losses)
+        ctx.tape = None
+        return (None, None) + tuple(eng.grads[id(p)].clone() for p in eng.params)
+
+
+def train_step_losses(engine_: TrainEngine, batch) -> torch.Tensor:
+    """losses f32 [4] (node_cls, node_reg, edge_cls, obj_cls) with autograd attached."""
+    return _TrainStep.apply(engine_, batch, *engine_.params)
+
+
+class FusedSGD:
+    """torch.optim.SGD(params, lr, momentum, weight_decay) (set_param_for_training_gnn.py:46)
+    as one rg_sgd_step launch over a flat copy of the parameters.  The module's
+    parameters become views of the flat buffer, so the model sees every update."""
+
+    def __init__(self, params, lr: float, momentum: float = 0.9, weight_decay: float = 0.0,
+                 on_update=None):
+        self.params = list(params)
+        self.on_update = on_update
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        o = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.flat[o:o + k].copy_(p.reshape(-1))
+                p.data = self.flat[o:o + k].view_as(p)
+                o += k
+        self.buf = torch.zeros_like(self.flat)
+        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
+        self.steps = 0
+
+    def step(self, flat_grad: torch.Tensor):
+        lib = nat.lib()
+        nat.check(lib.rg_sgd_step(self.flat.data_ptr(), flat_grad.data_ptr(), self.buf.data_ptr(),
+                                  self.flat.numel(), float(self.lr), float(self.momentum),
+                                  float(self.weight_decay), int(self.steps == 0),
+                                  nat.stream_ptr(self.flat.device)), 'rg_sgd_step')
+        if self.on_update is not None:   # weights changed outside torch: re-pack the plans
+            self.on_update()
+        self.steps += 1

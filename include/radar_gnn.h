@@ -52,6 +52,9 @@ extern "C" {
  * b - mean(b)).  The normalisation then sees (x - mean) directly -- it is invariant
  * to that shift -- and skips its mean pass.  Mark such layers RG_LAYER_CENTERED. */
 #define RG_PACK_CENTERED 0x100
+/* OR-ed into RG_F32: `weight` holds the TRANSPOSE of the packed layer, i.e. a row-major
+ * [in_dim][out_dim] matrix (the backward data GEMM dX = dZ W packs W^T this way) */
+#define RG_PACK_TRANSPOSE 0x200
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -180,6 +183,11 @@ typedef struct rg_layer {
   int out_dim;
   int act;   /* RG_ACT_* */
   int flags; /* RG_LAYER_* */
+  /* training forward (rg_mlp_chain, RG_F32 only; NULL for inference): the layer's
+   * pre-normalisation output z = x W^T + b and its post-activation output a, both
+   * float32 [rows][out_dim] -- the tape rg_ffn_backward / rg_linear_grad read */
+  float* save_pre;
+  float* save_out;
 } rg_layer;
 
 #define RG_LAYER_CENTERED 1 /* w_packed was packed with RG_PACK_CENTERED */
@@ -277,6 +285,81 @@ size_t rg_cluster_lists_workspace_size(int n_nodes);
 int rg_cluster_lists(const int* labels, int n_nodes, int* cluster_of, int* cluster_ptr,
                      int* cluster_idx, int* n_clusters, void* workspace, size_t workspace_bytes,
                      void* stream);
+
+
+/* ------------------------------------------------------------------ training */
+/* The backward of the hot path (Model_Training + Loss_Graph + loss.backward(),
+ * gnn_detector.py:428-478, loss.py:37-76, training.py:66-85), float32.  Forward
+ * tapes come from rg_mlp_chain with rg_layer.save_pre / save_out set. */
+
+/* Backward of channel_normalization + activation (common.py:208-220, 256-267) for
+ * `rows` rows of width C: from the saved pre-normalisation z and the gradient of the
+ * activation output da, dz (may alias da) and the gradients of the scalar parameters,
+ * ACCUMULATED into *d_mu / *d_std (device; deterministic order).  has_norm = 0: only
+ * the activation.  workspace: rg_ffn_backward_workspace_size() bytes. */
+size_t rg_ffn_backward_workspace_size(void);
+int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
+                    int has_norm, const float* mu, const float* std_, int act, float* dz,
+                    int lddz, float* d_mu, float* d_std, void* workspace, void* stream);
+
+/* Weight / bias gradient of nn.Linear (common.py:195): dW[out][in] += sum_r dz[r]^T x[r],
+ * db[out] += sum_r dz[r] (db may be NULL), x[r] formed from in0/in1/in2 by in_mode as in
+ * rg_mlp_chain (float32 inputs).  Rows are reduced in fixed chunks, the chunk partials
+ * in a fixed order: bit-reproducible.  workspace: rg_linear_grad_workspace_size(). */
+size_t rg_linear_grad_workspace_size(long rows, int out_dim, int in_dim);
+int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim, int in_mode,
+                   const float* in0, int ld0, int w0, const float* in1, int ld1, int w1,
+                   const float* in2, int ld2, int w2, const int* idx0, const int* idx1,
+                   float* dW, float* db, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Incidence lists: for node n, every u < n_items with a[u] == n or b[u] == n (b may be
+ * NULL), ascending: ptr int32 [n_nodes+1], list int32 [n_items * (b ? 2 : 1)].  The
+ * transpose of an index_select (PyG x_j = x[edge_index[0]], the link pairs' x[i] + x[j]),
+ * used to sum its gradient per node in a fixed order. */
+size_t rg_incidence_workspace_size(int n_nodes, long n_items);
+int rg_incidence(const int* a, const int* b, long n_items, int n_nodes, int* ptr, int* list,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* out[n][0:width] (+)= sum_{k in [ptr[n], ptr[n+1])} src[row(k)][col0 : col0 + width],
+ * row(k) = list ? list[k] : k; scale (per row of src, may be NULL) multiplies each term
+ * (PyG mean: 1 / count).  accumulate = 0 overwrites.  float32, width <= 256. */
+int rg_gather_segment_sum(const float* src, int ld_src, int col0, int width, const int* ptr,
+                          const int* list, const float* scale, int n_nodes, float* out,
+                          int ld_out, int accumulate, void* stream);
+
+/* Backward of the per-cluster channel max (object_classification gnn_blocks.py:384-387,
+ * torch.max(dim=0)): dh[argmax_c(f)][f] += dpooled[c][f], argmax = first maximum in
+ * list order.  h float32 [N][ld_h]; cluster lists as rg_segment_reduce's idx CSR. */
+int rg_segment_max_backward(const float* h, int ld_h, int C, const int* cluster_ptr,
+                            const int* cluster_idx, int n_clusters, const float* dpooled,
+                            int ld_p, float* dh, int ld_dh, void* stream);
+
+/* Loss_Graph.forward (loss.py:37-76) + compute_accuracy (gnn_detector.py:24-28).
+ * node_cls f32 [N][nc], node_reg f32 [N][2], link f32 [U][2], obj f32 [Ncl][nc];
+ * labels int64 (node_class [N], edge_class [U], obj_class [Ncl]); node_offsets f32
+ * [N][2] raw (normalised inside: (o - mu) / sigma, compute_offsets.py:6-11);
+ * class_w f32 [nc].  losses f32 [4] = weighted (node_cls, node_reg, edge_cls, obj_cls)
+ * as loss.py:71-75, acc f32 [3] = (segment, edge, object) accuracy (device). */
+typedef struct rg_loss_args {
+  const float* node_cls; const float* node_reg; const float* link; const float* obj;
+  const long long* node_class; const float* node_offsets; const long long* edge_class;
+  const long long* obj_class; const float* class_w;
+  long n_nodes; long n_pairs; long n_clusters; int n_classes;
+  float mu_x, mu_y, sigma_x, sigma_y;
+  float w_node_cls, w_node_reg, w_edge_cls, w_obj_cls;
+} rg_loss_args;
+size_t rg_loss_workspace_size(long n_nodes, long n_pairs, long n_clusters);
+int rg_loss_graph(const rg_loss_args* args, float* losses, float* acc, void* workspace,
+                  size_t workspace_bytes, void* stream);
+/* d(sum_i g[i] * losses[i]) / d(logits) (g: device f32 [4], the upstream gradients of
+ * the four losses): d_node_cls [N][nc], d_node_reg [N][2], d_link [U][2], d_obj [Ncl][nc]. */
+int rg_loss_graph_backward(const rg_loss_args* args, const float* g, float* d_node_cls,
+                           float* d_node_reg, float* d_link, float* d_obj, void* stream);
+
+/* torch.optim.SGD step (dampening 0, no nesterov; set_param_for_training_gnn.py:46) on
+ * flat float32 arrays: d = g + wd p; buf = first ? d : momentum buf + d; p -= lr buf. */
+int rg_sgd_step(float* param, const float* grad, float* momentum_buf, long n, float lr,
+                float momentum, float weight_decay, int first_step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,40 @@
+"""Diagnostic: gradient error of the native training step and of the fp32 oracle, both
+against the oracle evaluated in float64 (the exact-arithmetic stand-in)."""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, '.'); sys.path.insert(0, 'tests')
+from test_gpu_training import _synthetic_batch, LOSS_NAMES
+from oracle import train_ref
+from graph_neural_network_for_radar_perception_amd.config import default_config
+from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+
+dev = torch.device('cuda', 0)
+for L, aggr in [(2, 'mean'), (7, 'add')]:
+    cfg = default_config(graph_convolution_stem_channels=[64] * L, aggregation=aggr)
+    torch.manual_seed(11)
+    m = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev).train()
+    fo, nf, ef, ei, lab = _synthetic_batch([1500, 700, 40], 10, 8100, dev)
+    loss, acc = m(nf, ef, ei, [None] * 3, lab)
+    sum(loss[k] for k in LOSS_NAMES).backward()
+    l32, _, g32 = train_ref.training_grads(sd, cfg, fo)
+    torch.set_default_dtype(torch.float64)
+    sd64 = {k: v.double() for k, v in sd.items()}
+    fo64 = [{k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v)
+             for k, v in f.items()} for f in fo]
+    l64, _, g64 = train_ref.training_grads(sd64, cfg, fo64)
+    torch.set_default_dtype(torch.float32)
+    rows = []
+    for name, p in m.named_parameters():
+        b = g64[name].numpy()
+        s = np.max(np.abs(b)) + 1e-30
+        ours = np.max(np.abs(p.grad.double().cpu().numpy() - b)) / s
+        orc = np.max(np.abs(g32[name].double().numpy() - b)) / s
+        rows.append((ours / max(orc, 1e-12), ours, orc, name))
+    rows.sort(reverse=True)
+    print(L, aggr, 'loss', {k: (float(loss[k].detach()), l64[k]) for k in LOSS_NAMES})
+    for r in rows[:12]:
+        print(f'  ratio {r[0]:8.2f}  ours {r[1]:.2e}  oracle32 {r[2]:.2e}  {r[3]}')
+    print('  max ours', max(r[1] for r in rows), 'max oracle32', max(r[2] for r in rows))
