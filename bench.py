@@ -47,6 +47,9 @@ PRESETS = {
                cpu_warm=2),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
                cpu_warm=1),
+    # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
+    'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
+               cpu_warm=1),
 }
 
 
@@ -56,7 +59,8 @@ def parse():
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--config', default='c2', choices=sorted(PRESETS),
-                   help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress')
+                   help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress; '
+                        'c4: config 4 training step (forward + backward + SGD, DDP)')
     p.add_argument('--frames', type=int, default=None, help='frames per GPU')
     p.add_argument('--nodes', type=int, default=None)
     p.add_argument('--k', type=int, default=None)
@@ -228,11 +232,116 @@ def cpu_baseline(args, cfg):
                       + ('; the forward also timed on 1 thread (1 frame)' if f1 else '')}
 
 
+def batch_labels(frames, gb, cfg, device):
+    """Synthetic labels of a batch on its device-built graph (synthetic.batch_labels)."""
+    rp = gb.row_ptr.cpu().numpy().astype(np.int64)
+    col = gb.col[:int(rp[-1])].cpu().numpy().astype(np.int64)
+    lab, clusters = synthetic.batch_labels(frames, rp, col, cfg.num_classes)
+    lab = {k: torch.from_numpy(v).to(device) for k, v in lab.items()}
+    lab['class_weights'] = torch.tensor(cfg.class_weights_dyn, dtype=torch.float32, device=device)
+    return lab, clusters
+
+
+def cpu_train_baseline(args, cfg):
+    """The oracle's training step (torch fp32 forward + autograd backward of
+    Model_Training + Loss_Graph, i.e. the reference's CPU algorithm) on a bounded sample:
+    args.cpu_frames single-frame steps after args.cpu_warm warm-up frames."""
+    from oracle import graph_features_ref as gref, train_ref
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    sd = {k: v.detach() for k, v in Model_Training(cfg, 'cpu').state_dict().items()}
+    gmax = float(np.sqrt(np.float64(cfg.max_x ** 2 + cfg.max_y ** 2)))
+    times = []
+    for i in range(args.cpu_warm + args.cpu_frames):
+        fr = synthetic.make_frame(args.nodes, args.seed + 10**6 + i)
+        t0 = time.perf_counter()
+        g = gref.build_frame_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points, gmax)
+        lb = synthetic.make_labels(fr, g['edge_index'], cfg.num_classes, i)
+        f = {'node_features': torch.from_numpy(g['node_features']),
+             'edge_features': torch.from_numpy(g['edge_features']),
+             'edge_index': torch.from_numpy(g['edge_index']),
+             'node_class': torch.from_numpy(lb['node_class']),
+             'node_offsets': torch.from_numpy(lb['node_offsets']),
+             'edge_class': torch.from_numpy(lb['edge_class']),
+             'cluster_node_idx': [torch.from_numpy(c) for c in lb['cluster_node_idx']],
+             'cluster_labels': torch.from_numpy(lb['cluster_labels'])}
+        train_ref.training_grads(sd, cfg, [f])
+        if i >= args.cpu_warm:
+            times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    return {'value': round(1e3 / ms, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'step_ms_per_frame': round(ms, 1), 'cpu_model': _cpu_model(),
+            'sample': f'{len(times)} single-frame training step(s) of {args.nodes} nodes, k={args.k}, '
+                      f'L={args.layers} after {args.cpu_warm} warm-up: oracle graph build + '
+                      'labels + torch-fp32 forward + Loss_Graph + autograd backward, '
+                      f'torch threads={threads} (SGD update excluded)'}
+
+
+def train_main(args, world, rank, local):
+    """BASELINE config 4: one data-parallel training iteration per step."""
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from graph_neural_network_for_radar_perception_amd.graph_features import (FrameBatch,
+                                                                                build_graph_batch)
+    from graph_neural_network_for_radar_perception_amd.training import RadarGNNTrainer
+    dev = torch.device('cuda', local)
+    cfg = default_config(graph_convolution_stem_channels=[64] * args.layers,
+                         k_number_nearest_points=args.k)
+    torch.manual_seed(1234)
+    model = Model_Training(cfg, dev).to(dev).train()
+    seeds = rank_frame_seeds(rank, args.frames, args.seed)
+    frames = [synthetic.make_frame(args.nodes, s) for s in seeds]
+    batch0 = FrameBatch.from_frames(frames, device=dev)
+    labels, clusters = batch_labels(frames, build_graph_batch(batch0, cfg), cfg, dev)
+    batch = FrameBatch.from_frames(frames, clusters, device=dev)
+    trainer = RadarGNNTrainer(model, cfg, world)
+    for _ in range(args.warmup):
+        losses, acc, gb = trainer.step(batch, labels)
+    torch.cuda.synchronize()
+    E = int(gb.n_edges_dev.item())
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses, acc, gb = trainer.step(batch, labels)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    frames_total = sum_over_ranks(args.frames * args.steps, world)
+    line = {
+        'metric': 'radar frames/sec training (BASELINE config 4: yml k=10, L=7, batch 8/GPU, '
+                  'SGD momentum 0.9, DDP gradient all-reduce over RCCL)',
+        'value': round(frames_total / elapsed, 2), 'unit': 'frames/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+        'data': 'synthetic RadarScenes-shaped frames + synthetic labels (SURVEY.md §8(d)), '
+                'random-init weights of the yml architecture',
+        'config': {'workload': f'BASELINE config 4: {args.frames} frames x {args.nodes} nodes per '
+                               f'GPU, k={args.k}, L={args.layers}; step = graph build + features + '
+                               'forward tape + Loss_Graph + backward + all-reduce + SGD',
+                   'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes, 'k': args.k,
+                   'layers': args.layers, 'edges_per_gpu': E,
+                   'parallelism': f'data-parallel x{world} (one flat-gradient all-reduce per step)'},
+        'last_losses': [round(float(x), 5) for x in losses.cpu()],
+        'roofline': None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_train_baseline(args, cfg)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist()
     if not torch.cuda.is_available():
         raise SystemExit('bench.py needs a HIP device')
+    if args.config == 'c4':
+        return train_main(args, world, rank, local)
     dev = torch.device('cuda', local)
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
     from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline

@@ -112,7 +112,7 @@ _SIGNATURES = {
     'rg_loss_workspace_size': (_S, [_L, _L, _L]),
     'rg_loss_graph': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _S, _P]),
     'rg_loss_graph_backward': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _P, _P, _P]),
-    'rg_sgd_step': (_I, [_P, _P, _P, _L, _F, _F, _F, _I, _P]),
+    'rg_sgd_step': (_I, [_P, _P, _P, _L, _F, _F, _F, _I, _F, _P]),
 }
 
 _lib = None

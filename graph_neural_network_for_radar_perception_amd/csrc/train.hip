@@ -521,10 +521,10 @@ __global__ void loss_backward_kernel(rg_loss_args a, const float* __restrict__ g
 // ------------------------------------------------------------------ SGD
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                            float* __restrict__ buf, long n, float lr, float momentum, float wd,
-                           int first) {
+                           int first, float gscale) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float d = fmaf(wd, p[i], g[i]);               // d_p.add(p, alpha=wd)
+  const float d = fmaf(wd, p[i], __fmul_rn(g[i], gscale));  // d_p.add(p, alpha=wd)
   const float b = first ? d : __fadd_rn(__fmul_rn(momentum, buf[i]), d);  // buf.mul_(m).add_(d)
   buf[i] = b;
   p[i] = fmaf(-lr, b, p[i]);                          // p.add_(buf, alpha=-lr)
@@ -699,10 +699,11 @@ extern "C" int rg_loss_graph_backward(const rg_loss_args* args, const float* g, 
 }
 
 extern "C" int rg_sgd_step(float* param, const float* grad, float* momentum_buf, long n, float lr,
-                           float momentum, float weight_decay, int first_step, void* stream) {
+                           float momentum, float weight_decay, int first_step, float grad_scale,
+                           void* stream) {
   if (n <= 0) return RG_OK;
-  sgd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(param, grad, momentum_buf, n, lr,
-                                                               momentum, weight_decay, first_step);
+  sgd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(
+      param, grad, momentum_buf, n, lr, momentum, weight_decay, first_step, grad_scale);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -134,3 +134,22 @@ def make_labels(frame: dict, edge_index: np.ndarray, num_classes: int = 7, seed:
     cluster_labels = np.asarray([cls_of[inv[g[0]]] for g in groups], np.int64)
     return {'node_class': node_class, 'node_offsets': node_offsets, 'edge_class': edge_class,
             'cluster_node_idx': cluster_node_idx, 'cluster_labels': cluster_labels}
+
+
+def batch_labels(frames: list, row_ptr: np.ndarray, col: np.ndarray, num_classes: int = 7):
+    """make_labels for every frame of a batch whose disjoint-union CSR (global node ids,
+    rows / columns ascending = np.where order) is row_ptr / col: the labels concatenated
+    (edge_class in link-pair order, frame by frame) and the per-frame cluster lists."""
+    out = {k: [] for k in ('node_class', 'node_offsets', 'edge_class', 'cluster_labels')}
+    clusters = []
+    base = 0
+    for f, fr in enumerate(frames):
+        n = fr['meas_px'].shape[0]
+        r = np.repeat(np.arange(n), np.diff(row_ptr[base:base + n + 1]))
+        c = col[row_ptr[base]:row_ptr[base + n]] - base
+        lb = make_labels(fr, np.stack((r, c)), num_classes, f)
+        for k in out:
+            out[k].append(lb[k])
+        clusters.append(lb['cluster_node_idx'])
+        base += n
+    return {k: np.concatenate(v) for k, v in out.items()}, clusters

@@ -526,12 +526,69 @@ class FusedSGD:
         self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
         self.steps = 0
 
-    def step(self, flat_grad: torch.Tensor):
+    def step(self, flat_grad: torch.Tensor, grad_scale: float = 1.0):
         lib = nat.lib()
         nat.check(lib.rg_sgd_step(self.flat.data_ptr(), flat_grad.data_ptr(), self.buf.data_ptr(),
                                   self.flat.numel(), float(self.lr), float(self.momentum),
                                   float(self.weight_decay), int(self.steps == 0),
-                                  nat.stream_ptr(self.flat.device)), 'rg_sgd_step')
+                                  float(grad_scale), nat.stream_ptr(self.flat.device)),
+                  'rg_sgd_step')
         if self.on_update is not None:   # weights changed outside torch: re-pack the plans
             self.on_update()
         self.steps += 1
+
+
+# ------------------------------------------------------------------ data parallel
+def allreduce_gradients(flat_grad: torch.Tensor, world: int) -> float:
+    """DistributedDataParallel's gradient sync for BASELINE config 4:
+    the whole model's gradient is ONE flat bucket (463,144 f32 = 1.85 MB for the yml
+    model), all-reduced (SUM) over RCCL / xGMI in one call -- a message this small is
+    latency-bound, so bucketing or overlap with the backward gains nothing.  Returns the
+    averaging factor the SGD kernel applies (1 / world)."""
+    if world <= 1:
+        return 1.0
+    import torch.distributed as dist
+    dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
+    return 1.0 / world
+
+
+def broadcast_parameters(flat: torch.Tensor, world: int, src: int = 0):
+    """Every rank starts from rank 0's weights (DDP's construction-time broadcast)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.broadcast(flat, src)
+
+
+class RadarGNNTrainer:
+    """One data-parallel training iteration (training.py:66-85 for one rank's batch):
+    graph build + features (pipeline) -> forward tape + Loss_Graph -> backward ->
+    gradient all-reduce -> fused SGD.  Labels are per batch on the device (node_class,
+    node_offsets, edge_class in link-pair order, cluster_labels)."""
+
+    def __init__(self, model_training, cfg, world: int = 1, lr: Optional[float] = None,
+                 momentum: float = 0.9, weight_decay: Optional[float] = None):
+        self.model = model_training
+        self.cfg = cfg
+        self.world = world
+        lr = cfg.learning_rate if lr is None else lr
+        wd = cfg.weight_decay if weight_decay is None else weight_decay
+        self.opt = model_training.fused_sgd(lr, momentum, wd)
+        broadcast_parameters(self.opt.flat, world)
+        model_training.invalidate_plans()
+        self.engine = model_training.train_engine()
+        self.ones = torch.ones(4, dtype=torch.float32, device=self.engine.device)
+        self.ws_cache: dict = {}
+
+    def step(self, batch, labels: dict, events=None):
+        from .graph_features import build_graph_batch
+        gb = build_graph_batch(batch, self.cfg, ws_cache=self.ws_cache)
+        g = gb.graph
+        g.n_edges = int(gb.n_edges_dev.item())      # host sizes for the backward's launches
+        g.n_pairs = int(g.n_pairs_dev.item())
+        losses, acc, tape = self.engine.forward(gb.node_features, gb.edge_features, g,
+                                                batch.cluster_ptr, batch.cluster_idx,
+                                                batch.n_clusters, labels)
+        self.engine.backward(tape, self.ones)
+        scale = allreduce_gradients(self.engine.flat_grad, self.world)
+        self.opt.step(self.engine.flat_grad, grad_scale=scale)
+        return losses, acc, gb

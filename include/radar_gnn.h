@@ -357,9 +357,12 @@ int rg_loss_graph_backward(const rg_loss_args* args, const float* g, float* d_no
                            float* d_node_reg, float* d_link, float* d_obj, void* stream);
 
 /* torch.optim.SGD step (dampening 0, no nesterov; set_param_for_training_gnn.py:46) on
- * flat float32 arrays: d = g + wd p; buf = first ? d : momentum buf + d; p -= lr buf. */
+ * flat float32 arrays: d = grad_scale g + wd p; buf = first ? d : momentum buf + d;
+ * p -= lr buf.  grad_scale = 1 / world_size averages an all-reduced (summed) gradient
+ * as DistributedDataParallel does; 1 on one GPU (exact). */
 int rg_sgd_step(float* param, const float* grad, float* momentum_buf, long n, float lr,
-                float momentum, float weight_decay, int first_step, void* stream);
+                float momentum, float weight_decay, int first_step, float grad_scale,
+                void* stream);
 
 #ifdef __cplusplus
 }

@@ -77,3 +77,32 @@ def test_rank_seeds_weak_scaling():
     b = bench.rank_frame_seeds(1, 64, 7)
     assert len(a) == len(b) == 64 and not set(a) & set(b)
     assert bench.rank_frame_seeds(0, 64, 7) == a                 # deterministic per rank
+
+
+def _ddp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    dist.init_process_group('gloo')
+    from graph_neural_network_for_radar_perception_amd.training import (allreduce_gradients,
+                                                                          broadcast_parameters)
+    g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    scale = allreduce_gradients(g, world)
+    p = torch.full((4,), float(rank))
+    broadcast_parameters(p, world)
+    np.savez(os.path.join(out_dir, f'ddp{rank}.npz'), g=g.numpy(), scale=scale, p=p.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gradient_allreduce_two_ranks_gloo(tmp_path):
+    """BASELINE config 4's data-parallel sync (training.allreduce_gradients /
+    broadcast_parameters): one flat bucket summed over ranks, averaged by the SGD step's
+    grad_scale = 1/world; every rank starts from rank 0's weights."""
+    world = 2
+    mp.spawn(_ddp_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = np.arange(10, dtype=np.float32) * 3
+    for r in range(world):
+        d = np.load(tmp_path / f'ddp{r}.npz')
+        np.testing.assert_array_equal(d['g'], want)
+        assert float(d['scale']) == 0.5
+        np.testing.assert_array_equal(d['p'], np.zeros(4, np.float32))

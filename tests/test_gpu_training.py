@@ -183,3 +183,53 @@ def test_training_step_is_deterministic(cuda_device):
         flats.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).cpu())
         m.zero_grad(set_to_none=True)
     assert torch.equal(flats[0], flats[1])
+
+
+def test_trainer_step_matches_oracle(cuda_device):
+    """training.RadarGNNTrainer (device graph build + features + tape + backward + fused
+    SGD, as bench.py --config c4 times it) for one iteration == the oracle's gradient and
+    SGD update on the same frames and labels."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from graph_neural_network_for_radar_perception_amd.graph_features import (FrameBatch,
+                                                                                build_graph_batch)
+    from graph_neural_network_for_radar_perception_amd.training import RadarGNNTrainer
+    cfg = default_config(graph_convolution_stem_channels=[64] * 3)
+    torch.manual_seed(21)
+    m = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(cuda_device).train()
+    frames = [synthetic.make_frame(n, 8300 + i) for i, n in enumerate([600, 250])]
+    gb = build_graph_batch(FrameBatch.from_frames(frames, device=cuda_device), cfg)
+    rp = gb.row_ptr.cpu().numpy().astype(np.int64)
+    col = gb.col[:int(rp[-1])].cpu().numpy().astype(np.int64)
+    lab_np, clusters = synthetic.batch_labels(frames, rp, col, cfg.num_classes)
+    lab = {k: torch.from_numpy(v).to(cuda_device) for k, v in lab_np.items()}
+    lab['class_weights'] = torch.tensor(cfg.class_weights_dyn, device=cuda_device)
+    batch = FrameBatch.from_frames(frames, clusters, device=cuda_device)
+    tr = RadarGNNTrainer(m, cfg, world=1)
+    losses, acc, _ = tr.step(batch, lab)
+    # oracle: same frames through the reference graph build, same labels
+    from oracle import graph_features_ref as gref
+    gmax = float(np.sqrt(np.float64(100 ** 2 + 50 ** 2)))
+    fo = []
+    for i, fr in enumerate(frames):
+        g = gref.build_frame_graph(fr, 25.0, 10, gmax)
+        lb = synthetic.make_labels(fr, g['edge_index'], cfg.num_classes, i)
+        fo.append({'node_features': torch.from_numpy(g['node_features']),
+                   'edge_features': torch.from_numpy(g['edge_features']),
+                   'edge_index': torch.from_numpy(g['edge_index']),
+                   'node_class': torch.from_numpy(lb['node_class']),
+                   'node_offsets': torch.from_numpy(lb['node_offsets']),
+                   'edge_class': torch.from_numpy(lb['edge_class']),
+                   'cluster_node_idx': [torch.from_numpy(c) for c in lb['cluster_node_idx']],
+                   'cluster_labels': torch.from_numpy(lb['cluster_labels'])})
+    want_loss, _, g32 = train_ref.training_grads(sd, cfg, fo)
+    for i, k in enumerate(LOSS_NAMES):
+        assert abs(float(losses[i]) - want_loss[k]) <= 1e-5 * max(1.0, abs(want_loss[k])), k
+    params = {k: v.clone() for k, v in sd.items()}
+    train_ref.sgd_step(params, g32, {}, cfg.learning_rate, 0.9, cfg.weight_decay)
+    got = m.state_dict()
+    for k, v in params.items():
+        np.testing.assert_allclose(got[k].cpu().numpy(), v.numpy(), rtol=1e-5, atol=2e-7, err_msg=k)
