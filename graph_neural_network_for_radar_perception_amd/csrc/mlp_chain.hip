@@ -75,6 +75,7 @@ struct ChainArgs {
   int ld0, ld1, ld2;
   int ld_res, res_dtype, ld_out, out_dtype;
   int wbytes;  // total packed bytes (LDS image size when staged)
+  int sstride; // slab row stride (elements): f32 kpad(widest input, 64) + 8, bf16 MAXW + 16
   long rows;
   const int* rows_dev;
   const void* in0;
@@ -281,6 +282,7 @@ __device__ __forceinline__ f32x4 input_chunk(const ChainArgs& a, long row, int f
 // fill the wave slab with the chain input of rows [r0, r0+16), zero padded to K0p
 template <typename T>
 __device__ __forceinline__ void load_input(const ChainArgs& a, T* slab, long r0, long rows, int lane, int K0p) {
+  const int SS = a.sstride;
   const int nch = K0p / 4;
   const int total = TR * nch;
   const bool al0 = (a.ld0 % 4 == 0) && (a.w0 % 4 == 0);
@@ -292,7 +294,7 @@ __device__ __forceinline__ void load_input(const ChainArgs& a, T* slab, long r0,
     const long row = r0 + r;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (row < rows) v = input_chunk(a, row, f, al0, al1, al2);
-    st4_slab<T>(slab + r * Cfg<T>::STRIDE + f, v);
+    st4_slab<T>(slab + r * SS + f, v);
   }
 }
 
@@ -303,9 +305,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <typename T> struct Mfma;
 template <> struct Mfma<float> {
   static __device__ __forceinline__ void run(f32x4 (&acc)[16], const float* slab, const float* P,
-                                             int mt, int K, int lane) {
+                                             int mt, int K, int lane, int SS) {
     const int S4 = kpad(K, 16) / 16;
-    const float* brow = slab + (lane & 15) * Cfg<float>::STRIDE + 4 * (lane >> 4);
+    const float* brow = slab + (lane & 15) * SS + 4 * (lane >> 4);
     for (int s4 = 0; s4 < S4; ++s4) {
       const f32x4 b = *(const f32x4*)(brow + 16 * s4);
 #pragma unroll
@@ -323,9 +325,9 @@ template <> struct Mfma<float> {
 };
 template <> struct Mfma<uint16_t> {
   static __device__ __forceinline__ void run(f32x4 (&acc)[16], const uint16_t* slab,
-                                             const uint16_t* P, int mt, int K, int lane) {
+                                             const uint16_t* P, int mt, int K, int lane, int SS) {
     const int S = kpad(K, 32) / 32;
-    const uint16_t* brow = slab + (lane & 15) * Cfg<uint16_t>::STRIDE + 8 * (lane >> 4);
+    const uint16_t* brow = slab + (lane & 15) * SS + 8 * (lane >> 4);
     for (int s = 0; s < S; ++s) {
       const bf16x8_t b = __builtin_bit_cast(bf16x8_t, *(const u32x4*)(brow + 32 * s));
 #pragma unroll
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, r = lane & 15;
   T* slab = (T*)(wimg + (WLDS ? ((a.wbytes + 15) & ~15) : 0) +
-                 (size_t)wave * TR * Cfg<T>::STRIDE * sizeof(T));
+                 (size_t)wave * TR * a.sstride * sizeof(T));
   __syncthreads();
   if (WLDS) {
     // stage every layer's packed weights (+bias) into LDS once per workgroup
@@ -481,12 +483,12 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (m < mt) acc[m] = *(const f32x4*)(bias + 16 * m + 4 * g);
-      Mfma<T>::run(acc, slab, P, mt, L.in, lane);
+      Mfma<T>::run(acc, slab, P, mt, L.in, lane, a.sstride);
       if (L.save_pre && r0 + r < rows) save_rows(acc, L.save_pre, r0 + r, mt, L.out, g);
       epilogue(acc, L, mt, g);
       if (L.save_out && r0 + r < rows) save_rows(acc, L.save_out, r0 + r, mt, L.out, g);
       if (l + 1 < a.nl) {
-        T* row = slab + r * Cfg<T>::STRIDE;
+        T* row = slab + r * a.sstride;
 #pragma unroll
         for (int m = 0; m < 16; ++m)
           if (m < mt) st4_slab<T>(row + 16 * m + 4 * g, acc[m]);
@@ -506,7 +508,7 @@ template <typename T, bool WLDS>
 static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
   const size_t dbytes = (sizeof(ChainLayer) * RG_MAX_LAYERS + 15) & ~(size_t)15;
   const size_t lds = dbytes + (WLDS ? ((size_t)(a.wbytes + 15) & ~(size_t)15) : 0) +
-                     (size_t)CH_WAVES * TR * Cfg<T>::STRIDE * sizeof(T);
+                     (size_t)CH_WAVES * TR * a.sstride * sizeof(T);
   static bool attr_set = false;
   if (!attr_set) {
     RG_CHECK_HIP(hipFuncSetAttribute((const void*)chain_kernel<T, WLDS>,
@@ -635,10 +637,16 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
   hipStream_t st = (hipStream_t)stream;
   const size_t dbytes = (sizeof(ChainLayer) * RG_MAX_LAYERS + 15) & ~(size_t)15;
   if (dtype == RG_F32) {
-    const size_t slabs = (size_t)CH_WAVES * TR * Cfg<float>::STRIDE * sizeof(float);
+    // f32 slab rows sized to the chain's widest input (kpad 64 + 8 keeps the B reads
+    // conflict-free): single large layers (the training backward's W^T) then fit in LDS
+    int kmax = layers[0].in_dim;
+    for (int l = 0; l + 1 < n_layers; ++l) kmax = layers[l].out_dim > kmax ? layers[l].out_dim : kmax;
+    a.sstride = kpad(kmax, 64) + 8;
+    const size_t slabs = (size_t)CH_WAVES * TR * a.sstride * sizeof(float);
     if (dbytes + woff + slabs <= LDS_LIMIT) return launch_chain<float, true>(a, rows, st);
     return launch_chain<float, false>(a, rows, st);
   }
+  a.sstride = Cfg<uint16_t>::STRIDE;
   const size_t slabs = (size_t)CH_WAVES * TR * Cfg<uint16_t>::STRIDE * sizeof(uint16_t);
   if (dbytes + woff + slabs <= LDS_LIMIT) return launch_chain<uint16_t, true>(a, rows, st);
   return launch_chain<uint16_t, false>(a, rows, st);

@@ -51,84 +51,104 @@ __device__ __forceinline__ float act_grad(float y, int act) {
 }
 
 // ------------------------------------------------------------------ ffn backward
-// One wave per row, feature f = lane + 64 j.  Forward (common.py:215-220, as the
-// chain kernel evaluates it): mean = sum z / C, d = z - mean, std = sqrt(sum d^2 / (C-1)),
+// 16 lanes per row (4 rows per wave), feature f = q + 16 j (q = lane & 15): row sums are
+// 4 xor-shuffles inside the 16-lane group.  Forward (common.py:215-220, as the chain
+// kernel evaluates it): mean = sum z / C, d = z - mean, std = sqrt(sum d^2 / (C-1)),
 // r = 1 / (std + eps), n = d r, y = s n + m, a = act(y).  Backward:
 //   gy = da act'(y);  ds += sum gy n;  dm += sum gy;  gn = s gy;
 //   gd = r gn - r^2 (sum gn d) d / ((C-1) std);  dz = gd - mean(gd).
+__device__ __forceinline__ float group16_sum(float v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+template <int J>  // features per lane = J (C <= 16 J)
 __global__ __launch_bounds__(256) void ffn_backward_kernel(
     const float* __restrict__ z, int ldz, const float* __restrict__ da, int ldda, long rows,
     int C, int has_norm, const float* __restrict__ mu, const float* __restrict__ sd, int act,
     float* __restrict__ dz, int lddz, float* __restrict__ part) {
-  __shared__ float red[4][2];
+  __shared__ float red[16][2];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, q = lane & 15;
   const float s = has_norm ? *sd : 1.f;
   const float m = has_norm ? *mu : 0.f;
-  float acc_s = 0.f, acc_m = 0.f;  // lane-0 running sums, rows in fixed order
-  for (long row = (long)blockIdx.x * 4 + wave; row < rows; row += (long)gridDim.x * 4) {
-    float zv[4], gv[4];
+  float acc_s = 0.f, acc_m = 0.f;  // per 16-lane group, rows in fixed order
+  for (long row = ((long)blockIdx.x * 4 + wave) * 4 + grp; row < rows;
+       row += (long)gridDim.x * 16) {
+    float zv[J], gv[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = lane + 64 * j;
+    for (int j = 0; j < J; ++j) {
+      const int f = q + 16 * j;
       zv[j] = f < C ? z[(size_t)row * ldz + f] : 0.f;
       gv[j] = f < C ? da[(size_t)row * ldda + f] : 0.f;
     }
     if (has_norm) {
-      const float mean = wave_sum(zv[0] + zv[1] + zv[2] + zv[3]) / (float)C;
-      float d[4], ss = 0.f;
+      float t = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        d[j] = (lane + 64 * j) < C ? zv[j] - mean : 0.f;
+      for (int j = 0; j < J; ++j) t += zv[j];
+      const float mean = group16_sum(t) / (float)C;
+      float d[J], ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        d[j] = (q + 16 * j) < C ? zv[j] - mean : 0.f;
         ss += d[j] * d[j];
       }
-      ss = wave_sum(ss);
+      ss = group16_sum(ss);
       const float stdv = __fsqrt_rn(ss / (float)(C - 1));
       const float r = 1.f / (stdv + NORM_EPS);
-      float gn[4], ps = 0.f, pm = 0.f, A = 0.f;
+      float gn[J], ps = 0.f, pm = 0.f, A = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < J; ++j) {
         const float n = d[j] * r;
         const float y = __fadd_rn(__fmul_rn(s, n), m);
-        const float gy = (lane + 64 * j) < C ? gv[j] * act_grad(y, act) : 0.f;
+        const float gy = (q + 16 * j) < C ? gv[j] * act_grad(y, act) : 0.f;
         ps += gy * n;
         pm += gy;
         gn[j] = s * gy;
         A += gn[j] * d[j];
       }
-      ps = wave_sum(ps);
-      pm = wave_sum(pm);
-      A = wave_sum(A);
+      ps = group16_sum(ps);
+      pm = group16_sum(pm);
+      A = group16_sum(A);
       acc_s += ps;
       acc_m += pm;
       const float coef = stdv > 0.f ? r * r * A / ((float)(C - 1) * stdv) : 0.f;
-      float gd[4], sg = 0.f;
+      float gd[J], sg = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        gd[j] = (lane + 64 * j) < C ? r * gn[j] - coef * d[j] : 0.f;
+      for (int j = 0; j < J; ++j) {
+        gd[j] = (q + 16 * j) < C ? r * gn[j] - coef * d[j] : 0.f;
         sg += gd[j];
       }
-      const float mg = wave_sum(sg) / (float)C;
+      const float mg = group16_sum(sg) / (float)C;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = lane + 64 * j;
+      for (int j = 0; j < J; ++j) {
+        const int f = q + 16 * j;
         if (f < C) dz[(size_t)row * lddz + f] = gd[j] - mg;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = lane + 64 * j;
+      for (int j = 0; j < J; ++j) {
+        const int f = q + 16 * j;
         if (f < C) dz[(size_t)row * lddz + f] = gv[j] * act_grad(zv[j], act);
       }
     }
   }
-  if (lane == 0) {
-    red[wave][0] = acc_s;
-    red[wave][1] = acc_m;
+  if (q == 0) {
+    red[wave * 4 + grp][0] = acc_s;
+    red[wave * 4 + grp][1] = acc_m;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
-    part[2 * blockIdx.x + 1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    float ts = 0.f, tm = 0.f;
+    for (int i = 0; i < 16; ++i) {
+      ts += red[i][0];
+      tm += red[i][1];
+    }
+    part[2 * blockIdx.x] = ts;
+    part[2 * blockIdx.x + 1] = tm;
   }
 }
 
@@ -184,99 +204,189 @@ __device__ __forceinline__ float x_elem(const GradIn& a, long row, int f) {
   }
 }
 
-static constexpr int GT = 64;       // output tile (out x in) and row block
-static constexpr int GS = 80;       // LDS row stride (floats): 4 consecutive rows hit
-                                    // disjoint bank quarters
+// 4 consecutive input features [f, f+4) of row `row` (vec: every segment width and row
+// stride is a multiple of 4, so the group never straddles two segments)
+__device__ __forceinline__ f32x4 x_chunk(const GradIn& a, long row, int f, bool vec) {
+  if (vec && f + 4 <= a.in_dim) {
+    switch (a.mode) {
+      case RG_IN_DENSE:
+        return *(const f32x4*)(a.in0 + (size_t)row * a.ld0 + f);
+      case RG_IN_CONCAT2:
+        return f < a.w0 ? *(const f32x4*)(a.in0 + (size_t)row * a.ld0 + f)
+                        : *(const f32x4*)(a.in1 + (size_t)row * a.ld1 + (f - a.w0));
+      case RG_IN_GATHER3:
+        if (f < a.w0) return *(const f32x4*)(a.in0 + (size_t)a.idx0[row] * a.ld0 + f);
+        if (f < 2 * a.w0) return *(const f32x4*)(a.in0 + (size_t)a.idx1[row] * a.ld0 + (f - a.w0));
+        return *(const f32x4*)(a.in2 + (size_t)row * a.ld2 + (f - 2 * a.w0));
+      default: {
+        const f32x4 u = *(const f32x4*)(a.in0 + (size_t)a.idx0[row] * a.ld0 + f);
+        const f32x4 v = *(const f32x4*)(a.in0 + (size_t)a.idx1[row] * a.ld0 + f);
+        return (f32x4){__fadd_rn(u.x, v.x), __fadd_rn(u.y, v.y), __fadd_rn(u.z, v.z),
+                       __fadd_rn(u.w, v.w)};
+      }
+    }
+  }
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = f + e < a.in_dim ? x_elem(a, row, f + e) : 0.f;
+  return v;
+}
+
+// Weight gradient tile: out rows [o0, o0 + 64 OW) x in columns [i0, i0 + 16 NT) over one
+// chunk of rows.  Wave w owns out rows 16 OW w .. +16 OW and every column, so the whole
+// tile stays in registers (OW * NT f32x4 accumulators) and dz / x rows are read once
+// per chunk.  Rows are staged 32 at a time in LDS; one k-step = 4 rows = OW * NT
+// v_mfma_f32_16x16x4_f32 (A = dz^T: lane -> (out 16m + (lane&15), row lane>>4);
+// B = x: lane -> (row lane>>4, in 16n + (lane&15))).  The bias column sum is a VALU
+// side sum of the staged dz rows.
+static constexpr int GR = 32;  // rows per staged block
+__host__ __device__ constexpr int grad_stride(int cols) { return (cols + 63) / 64 * 64 + 16; }
+
+template <int OW, int NT>
+__global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restrict__ dz, int lddz,
+                                                          long rows, int out_dim, GradIn in,
+                                                          long rpc, int vec_x, int vec_z,
+                                                          float* __restrict__ part,
+                                                          float* __restrict__ part_b) {
+  constexpr int OC = 64 * OW, IC = 16 * NT;
+  constexpr int SZ = grad_stride(OC), SX = grad_stride(IC);
+  __shared__ __attribute__((aligned(16))) float sZ[GR * SZ];
+  __shared__ __attribute__((aligned(16))) float sX[GR * SX];
+  const int chunk = blockIdx.x, ot = blockIdx.y, it = blockIdx.z;
+  const int o0 = ot * OC, i0 = it * IC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r_begin = (long)chunk * rpc;
+  const long r_end = min(rows, r_begin + rpc);
+  f32x4 acc[OW][NT];
+#pragma unroll
+  for (int m = 0; m < OW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (long rb = r_begin; rb < r_end; rb += GR) {
+    for (int t = threadIdx.x; t < GR * (OC / 4); t += 256) {
+      const int rr = t / (OC / 4), c = 4 * (t % (OC / 4));
+      const long row = rb + rr;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row < r_end) {
+        const float* pz = dz + (size_t)row * lddz + o0 + c;
+        if (vec_z && o0 + c + 4 <= out_dim) {
+          v = *(const f32x4*)pz;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = o0 + c + e < out_dim ? pz[e] : 0.f;
+        }
+      }
+      *(f32x4*)(sZ + rr * SZ + c) = v;
+    }
+    for (int t = threadIdx.x; t < GR * (IC / 4); t += 256) {
+      const int rr = t / (IC / 4), c = 4 * (t % (IC / 4));
+      const long row = rb + rr;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (row < r_end && i0 + c < in.in_dim) v = x_chunk(in, row, i0 + c, vec_x);
+      *(f32x4*)(sX + rr * SX + c) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < GR / 4; ++ks) {
+      const int kr = 4 * ks + (lane >> 4);
+      float av[OW], bv[NT];
+#pragma unroll
+      for (int m = 0; m < OW; ++m) av[m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bv[n] = sX[kr * SX + 16 * n + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < OW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+    if (it == 0 && threadIdx.x < OC) {
+#pragma unroll 8
+      for (int rr = 0; rr < GR; ++rr) bsum += sZ[rr * SZ + threadIdx.x];
+    }
+    __syncthreads();
+  }
+  // lane holds D[o = 16(OW wave + m) + 4(lane>>4) + e][i = 16n + (lane&15)]
+  float* P = part + ((size_t)(chunk * gridDim.y + ot) * gridDim.z + it) * OC * IC;
+#pragma unroll
+  for (int m = 0; m < OW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        P[(16 * (OW * wave + m) + 4 * (lane >> 4) + e) * IC + 16 * n + (lane & 15)] = acc[m][n][e];
+  if (it == 0 && threadIdx.x < OC) part_b[((size_t)chunk * gridDim.y + ot) * OC + threadIdx.x] = bsum;
+}
+
 struct GradGeom {
-  int ot, it, nchunk;
-  long rpc;  // rows per chunk (multiple of GT)
+  int ow, nt, ot, it, nchunk;
+  long rpc;  // rows per chunk (multiple of GR)
 };
 static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
   GradGeom g;
-  g.ot = (out_dim + GT - 1) / GT;
-  g.it = (in_dim + 1 + GT - 1) / GT;
-  const long blocks = (rows + GT - 1) / GT;
-  long want = 2048 / (g.ot * g.it);
+  g.ow = out_dim > 64 ? 2 : 1;
+  const int nt_need = (in_dim + 15) / 16;
+  g.nt = nt_need <= 1 ? 1 : nt_need <= 4 ? 4 : nt_need <= 8 ? 8 : nt_need <= 12 ? 12 : 16;
+  g.ot = (out_dim + 64 * g.ow - 1) / (64 * g.ow);
+  g.it = (in_dim + 16 * g.nt - 1) / (16 * g.nt);
+  const long blocks = (rows + GR - 1) / GR;
+  long want = 256 / (g.ot * g.it);  // ~one workgroup per CU
   if (want < 1) want = 1;
-  if (want > blocks) want = blocks;
+  if (want > (blocks + 31) / 32) want = (blocks + 31) / 32;  // >= 1024 rows per chunk
   if (want < 1) want = 1;
-  g.rpc = ((blocks + want - 1) / want) * GT;
+  g.rpc = ((blocks + want - 1) / want) * GR;
   g.nchunk = (int)((rows + g.rpc - 1) / g.rpc);
   if (g.nchunk < 1) g.nchunk = 1;
   return g;
 }
-
-__global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restrict__ dz, int lddz,
-                                                          long rows, int out_dim, GradIn in,
-                                                          long rpc, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sZ = sm;                 // [GT][GS]  dz rows x out-tile
-  float* sX = sm + GT * GS;       // [GT][GS]  x rows x in-tile
-  float* sR = sm + 2 * GT * GS;   // [4][GT][GT] per-wave results
-  const int chunk = blockIdx.x, ot = blockIdx.y, it = blockIdx.z;
-  const int o0 = ot * GT, i0 = it * GT;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long r_begin = (long)chunk * rpc;
-  const long r_end = min(rows, r_begin + rpc);
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (long rb = r_begin; rb < r_end; rb += GT) {
-    for (int t = threadIdx.x; t < GT * GT; t += 256) {
-      const int rr = t / GT, c = t % GT;
-      const long row = rb + rr;
-      const bool ok = row < r_end;
-      sZ[rr * GS + c] = (ok && o0 + c < out_dim) ? dz[(size_t)row * lddz + o0 + c] : 0.f;
-      sX[rr * GS + c] = ok ? x_elem(in, row, i0 + c) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int kr = 16 * wave + 4 * ks + (lane >> 4);
-      float av[4], bv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) av[m] = sZ[kr * GS + 16 * m + (lane & 15)];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = sX[kr * GS + 16 * n + (lane & 15)];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // lane holds D[o = 16m + 4(lane>>4) + e][i = 16n + (lane&15)]
-  float* R = sR + wave * GT * GT;
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        R[(16 * m + 4 * (lane >> 4) + e) * GT + 16 * n + (lane & 15)] = acc[m][n][e];
-  __syncthreads();
-  float* P = part + ((size_t)(chunk * gridDim.y + ot) * gridDim.z + it) * GT * GT;
-  for (int t = threadIdx.x; t < GT * GT; t += 256)
-    P[t] = (sR[t] + sR[GT * GT + t]) + (sR[2 * GT * GT + t] + sR[3 * GT * GT + t]);
+static size_t grad_part_floats(const GradGeom& g) {
+  return (size_t)g.nchunk * g.ot * g.it * (64 * g.ow) * (16 * g.nt);
+}
+static size_t grad_ws_bytes(const GradGeom& g) {
+  return (grad_part_floats(g) + (size_t)g.nchunk * g.ot * 64 * g.ow) * sizeof(float);
 }
 
-__global__ void linear_grad_reduce(const float* __restrict__ part, int nchunk, int ot_n, int it_n,
-                                   int out_dim, int in_dim, float* __restrict__ dW,
-                                   float* __restrict__ db) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// dW / db += the chunk partials, summed in chunk order: 64 consecutive (o, i) entries
+// per workgroup, wave w sums chunks w, w + 4, ... and the four wave sums combine in a
+// fixed order
+__global__ __launch_bounds__(256) void linear_grad_reduce(
+    const float* __restrict__ part, const float* __restrict__ part_b, int nchunk, int ot_n,
+    int it_n, int oc, int ic, int out_dim, int in_dim, float* __restrict__ dW,
+    float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long t = (long)blockIdx.x * 64 + lane;
   const long total = (long)out_dim * (in_dim + 1);
-  if (t >= total) return;
-  const int o = (int)(t / (in_dim + 1)), i = (int)(t % (in_dim + 1));
-  const int ot = o / GT, it = i / GT;
-  const int oo = o % GT, ii = i % GT;
   float s = 0.f;
-  for (int c = 0; c < nchunk; ++c)
-    s += part[((size_t)(c * ot_n + ot) * it_n + it) * GT * GT + oo * GT + ii];
-  if (i < in_dim) dW[(size_t)o * in_dim + i] += s;
-  else if (db) db[o] += s;
+  int o = 0, i = 0;
+  if (t < total) {
+    o = (int)(t / (in_dim + 1));
+    i = (int)(t % (in_dim + 1));
+    const int ot = o / oc, oo = o % oc;
+    if (i < in_dim) {
+      const int it = i / ic, ii = i % ic;
+      for (int c = wave; c < nchunk; c += 4)
+        s += part[((size_t)(c * ot_n + ot) * it_n + it) * oc * ic + (size_t)oo * ic + ii];
+    } else {
+      for (int c = wave; c < nchunk; c += 4) s += part_b[((size_t)c * ot_n + ot) * oc + oo];
+    }
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && t < total) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (i < in_dim) dW[(size_t)o * in_dim + i] += v;
+    else if (db) db[o] += v;
+  }
+}
+
+template <int OW, int NT>
+static void launch_grad(const GradGeom& g, const float* dz, int lddz, long rows, int out_dim,
+                        const GradIn& in, int vec_x, int vec_z, float* part, float* part_b,
+                        hipStream_t st) {
+  linear_grad_kernel<OW, NT><<<dim3(g.nchunk, g.ot, g.it), 256, 0, st>>>(
+      dz, lddz, rows, out_dim, in, g.rpc, vec_x, vec_z, part, part_b);
 }
 
 // ------------------------------------------------------------------ incidence lists
@@ -550,8 +660,18 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
   if (rows <= 0) return RG_OK;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)workspace;
-  ffn_backward_kernel<<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_, act,
-                                             dz, lddz, part);
+  if (C <= 16)
+    ffn_backward_kernel<1><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+                                                  act, dz, lddz, part);
+  else if (C <= 64)
+    ffn_backward_kernel<4><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+                                                  act, dz, lddz, part);
+  else if (C <= 128)
+    ffn_backward_kernel<8><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+                                                  act, dz, lddz, part);
+  else
+    ffn_backward_kernel<16><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+                                                   act, dz, lddz, part);
   RG_LAUNCH_CHECK();
   if (has_norm) {
     ffn_param_reduce<<<1, 256, 0, st>>>(part, d_mu, d_std);
@@ -562,8 +682,7 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
 
 extern "C" size_t rg_linear_grad_workspace_size(long rows, int out_dim, int in_dim) {
   if (rows <= 0) return 256;
-  const GradGeom g = grad_geom(rows, out_dim, in_dim);
-  return (size_t)g.nchunk * g.ot * g.it * GT * GT * sizeof(float);
+  return grad_ws_bytes(grad_geom(rows, out_dim, in_dim));
 }
 
 extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim,
@@ -580,7 +699,7 @@ extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim,
              in_dim);
   if (rows <= 0) return RG_OK;
   const GradGeom g = grad_geom(rows, out_dim, in_dim);
-  const size_t need = (size_t)g.nchunk * g.ot * g.it * GT * GT * sizeof(float);
+  const size_t need = grad_ws_bytes(g);
   RG_REQUIRE(workspace_bytes >= need, RG_ERR_ARG, "rg_linear_grad: workspace %zu < %zu",
              workspace_bytes, need);
   GradIn in;
@@ -588,20 +707,25 @@ extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim,
   in.in0 = in0; in.in1 = in1; in.in2 = in2;
   in.ld0 = ld0; in.ld1 = ld1; in.ld2 = ld2; in.w0 = w0; in.w1 = w1; in.w2 = w2;
   in.idx0 = idx0; in.idx1 = idx1;
+  // vector (16-B) staging when no 4-feature group straddles a segment or a row
+  const bool a0 = ld0 % 4 == 0 && w0 % 4 == 0;
+  const bool a1 = in_mode != RG_IN_CONCAT2 || (ld1 % 4 == 0 && w1 % 4 == 0);
+  const bool a2 = in_mode != RG_IN_GATHER3 || (ld2 % 4 == 0 && w2 % 4 == 0);
+  const int vec_x = a0 && a1 && a2 && in_dim % 4 == 0;
+  const int vec_z = lddz % 4 == 0;
   hipStream_t st = (hipStream_t)stream;
-  const size_t lds = (size_t)(2 * GT * GS + 4 * GT * GT) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)linear_grad_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  linear_grad_kernel<<<dim3(g.nchunk, g.ot, g.it), 256, lds, st>>>(dz, lddz, rows, out_dim, in,
-                                                                   g.rpc, (float*)workspace);
+  float* part = (float*)workspace;
+  float* part_b = part + grad_part_floats(g);
+#define RG_GRAD_CASE(OW, NT) \
+  if (g.ow == OW && g.nt == NT) launch_grad<OW, NT>(g, dz, lddz, rows, out_dim, in, vec_x, vec_z, part, part_b, st);
+  RG_GRAD_CASE(1, 1) RG_GRAD_CASE(1, 4) RG_GRAD_CASE(1, 8) RG_GRAD_CASE(1, 12) RG_GRAD_CASE(1, 16)
+  RG_GRAD_CASE(2, 1) RG_GRAD_CASE(2, 4) RG_GRAD_CASE(2, 8) RG_GRAD_CASE(2, 12) RG_GRAD_CASE(2, 16)
+#undef RG_GRAD_CASE
   RG_LAUNCH_CHECK();
   const long total = (long)out_dim * (in_dim + 1);
-  linear_grad_reduce<<<ceil_div(total, 256), 256, 0, st>>>((const float*)workspace, g.nchunk, g.ot,
-                                                           g.it, out_dim, in_dim, dW, db);
+  linear_grad_reduce<<<ceil_div(total, 64), 256, 0, st>>>(part, part_b, g.nchunk, g.ot, g.it,
+                                                           64 * g.ow, 16 * g.nt, out_dim, in_dim,
+                                                           dW, db);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -124,32 +124,59 @@ class TrainChain:
         self._tsig = sig
         return self._tarr
 
+    def _fits_lds(self, layers) -> bool:
+        """Whether rg_mlp_chain stages these f32 layers' weights in LDS (its rule:
+        descriptors + packed weights + 4 slabs of 16 rows x (kpad(widest input, 64) + 8)
+        floats <= 160 KiB - 2 KiB)."""
+        lib = nat.lib()
+        wb = sum(lib.rg_packed_linear_bytes(s.in_dim, s.out_dim, nat.RG_F32) for s in layers)
+        kmax = max([layers[0].in_dim] + [s.out_dim for s in layers[:-1]])
+        slabs = 4 * 16 * ((kmax + 63) // 64 * 64 + 8) * 4
+        return 400 + wb + slabs <= 160 * 1024 - 2048
+
     # ------------------------------------------------------------------ forward
     def forward(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
                 mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
                 idx0=None, idx1=None, residual=None) -> ChainTape:
+        """One launch for the chain when its weights fit in LDS, else one launch per
+        layer (the tape holds every layer's output anyway, so splitting costs one extra
+        read of each intermediate instead of re-reading the weights from L2 per tile)."""
         self.plan.refresh()
         lib = nat.lib()
         dev = self.device
         arr0, n, _ = self.plan.groups[0]
-        arr = (nat.rg_layer * n)()
         z, a = [], []
         for i in range(n):
-            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(arr0[i]), ctypes.sizeof(nat.rg_layer))
             zi = torch.empty((max(rows, 1), self.specs[i].out_dim), dtype=torch.float32, device=dev)
-            ai = torch.empty_like(zi)
-            arr[i].save_pre = zi.data_ptr()
-            arr[i].save_out = ai.data_ptr()
             z.append(zi)
-            a.append(ai)
-        rc = lib.rg_mlp_chain(
-            nat.RG_F32, arr, n, int(rows), None, mode, nat.RG_F32, in0.data_ptr(), in0.stride(0), w0,
-            nat.ptr(in1), in1.stride(0) if in1 is not None else 0, w1,
-            nat.ptr(in2), in2.stride(0) if in2 is not None else 0, w2,
-            nat.ptr(idx0), nat.ptr(idx1),
-            nat.ptr(residual), residual.stride(0) if residual is not None else 0, nat.RG_F32,
-            out.data_ptr(), out.stride(0), nat.RG_F32, nat.stream_ptr(dev))
-        nat.check(rc, 'rg_mlp_chain (training tape)')
+            a.append(torch.empty_like(zi))
+        groups = [list(range(n))] if self._fits_lds(self.specs) else [[i] for i in range(n)]
+        st = nat.stream_ptr(dev)
+        for gi, grp in enumerate(groups):
+            arr = (nat.rg_layer * len(grp))()
+            for j, i in enumerate(grp):
+                ctypes.memmove(ctypes.byref(arr[j]), ctypes.byref(arr0[i]),
+                               ctypes.sizeof(nat.rg_layer))
+                arr[j].save_pre = z[i].data_ptr()
+                arr[j].save_out = a[i].data_ptr()
+            first, last = gi == 0, gi == len(groups) - 1
+            if first:
+                m_, i0, w0_, i1, w1_, i2, w2_, x0, x1 = mode, in0, w0, in1, w1, in2, w2, idx0, idx1
+            else:
+                prev = a[grp[0] - 1]
+                m_, i0, w0_, i1, w1_, i2, w2_, x0, x1 = (nat.IN_DENSE, prev, prev.shape[1], None, 0,
+                                                         None, 0, None, None)
+            dst = out if last else a[grp[-1]]
+            res = residual if last else None
+            rc = lib.rg_mlp_chain(
+                nat.RG_F32, arr, len(grp), int(rows), None, m_, nat.RG_F32, i0.data_ptr(),
+                i0.stride(0), w0_,
+                nat.ptr(i1), i1.stride(0) if i1 is not None else 0, w1_,
+                nat.ptr(i2), i2.stride(0) if i2 is not None else 0, w2_,
+                nat.ptr(x0), nat.ptr(x1),
+                nat.ptr(res), res.stride(0) if res is not None else 0, nat.RG_F32,
+                dst.data_ptr(), dst.stride(0), nat.RG_F32, st)
+            nat.check(rc, 'rg_mlp_chain (training tape)')
         return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a)
 
     # ------------------------------------------------------------------ backward
