@@ -336,21 +336,21 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       ne1 = a.seg_ptr[min(nxt * NB + NB, a.n_nodes)];
     }
 
+    // The next tile's rows and the tile after's indices are loaded UNCONDITIONALLY
+    // (clamped to the block's last edge: past the end every lane reads one row): a load
+    // under a branch leaves the compiler unsure how many loads are in flight at the
+    // join, and it then waits for the freshly issued prefetch before this tile's MFMAs.
     if (e0 < e1) {
       for (int t0 = e0;;) {
         const int slotA = iA.di - n0;
-        if (t0 + 32 < e1) {
-          if (RG_CONV_EXP != 1) load_rows(t0 + 32, iB, bB);
-          if (t0 + 64 < e1) iA = load_idx(t0 + 64);
-        }
+        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iB, bB);
+        iA = load_idx(t0 + 64);
         compute(bA, slotA, t0);
         t0 += 32;
         if (t0 >= e1) break;
         const int slotB = iB.di - n0;
-        if (t0 + 32 < e1) {
-          if (RG_CONV_EXP != 1) load_rows(t0 + 32, iA, bA);
-          if (t0 + 64 < e1) iB = load_idx(t0 + 64);
-        }
+        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iA, bA);
+        iB = load_idx(t0 + 64);
         compute(RG_CONV_EXP != 1 ? bB : bA, slotB, t0);
         t0 += 32;
         if (t0 >= e1) break;
@@ -381,16 +381,23 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     if (nvalid) {
       uint16_t* po = a.x_out + (size_t)node * a.ldo;
       const uint16_t* pr = a.x + (size_t)node * a.ldx;
+      // all residual loads first: interleaved with the stores, each load would wait
+      // for the previous store (possible aliasing) -- eight serial round trips
+      uint2 rv[2][4];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) rv[m][g] = *(const uint2*)(pr + 32 * m + 8 * g + 4 * h);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int f0 = 32 * m + 8 * g + 4 * h;
-          const uint2 rv = *(const uint2*)(pr + f0);
-          const float v0 = __fadd_rn(__uint_as_float(rv.x << 16), accu[m][4 * g + 0]);
-          const float v1 = __fadd_rn(__uint_as_float(rv.x & 0xffff0000u), accu[m][4 * g + 1]);
-          const float v2 = __fadd_rn(__uint_as_float(rv.y << 16), accu[m][4 * g + 2]);
-          const float v3 = __fadd_rn(__uint_as_float(rv.y & 0xffff0000u), accu[m][4 * g + 3]);
+          const uint2 r2 = rv[m][g];
+          const float v0 = __fadd_rn(__uint_as_float(r2.x << 16), accu[m][4 * g + 0]);
+          const float v1 = __fadd_rn(__uint_as_float(r2.x & 0xffff0000u), accu[m][4 * g + 1]);
+          const float v2 = __fadd_rn(__uint_as_float(r2.y << 16), accu[m][4 * g + 2]);
+          const float v3 = __fadd_rn(__uint_as_float(r2.y & 0xffff0000u), accu[m][4 * g + 3]);
           uint2 o;
           o.x = bf2(v0, v1);
           o.y = bf2(v2, v3);

@@ -296,7 +296,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
 
 static constexpr int HB = 64;     // distance histogram bins per row (4 per octave of d)
 static constexpr int HSHIFT = 21; // d's bits >> 21 = exponent + 2 mantissa bits
-static constexpr int BBUF = 64;   // boundary-bin candidates a row may buffer (indices)
+static constexpr int HW = HB / 2; // LDS words per row: two 16-bit bin counters per word
+static constexpr int BBUF = HW;   // boundary-bin candidates a row may buffer (indices)
 
 // Counting selection of the k+1 nearest (distance, index) keys -- the same set the
 // sorted-insert search (knn_grid) and the reference's argsort pick:
@@ -319,7 +320,9 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     const float* __restrict__ py, int n_nodes, int kk, int K, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
     uint32_t* __restrict__ bits, int W, int* __restrict__ redo) {
-  __shared__ uint32_t lds[KNN_BLOCK / 64][HB * 64];  // per wave: [bin][lane]
+  // per wave: [bin pair][lane], 16-bit counters (a row has < 65536 candidates per bin:
+  // frames are far smaller); 8 KiB per wave lets 4-5 blocks share a CU
+  __shared__ uint32_t lds[KNN_BLOCK / 64][HW * 64];
   const int lane = threadIdx.x & 63;
   uint32_t* H = lds[threadIdx.x >> 6] + lane;  // this row's column (stride 64 words)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   };
   if (want_knn) {
 #pragma unroll
-    for (int b = 0; b < HB; ++b) H[b * 64] = 0u;
+    for (int b = 0; b < HW; ++b) H[b * 64] = 0u;
   }
   const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
   int ball = 0, total = 0, r_knn = rmax;
@@ -360,7 +363,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
         if (want_rad && inball) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
       }
       if (count_knn) {
-        atomicAdd(H + bin_of(d) * 64, 1u);  // ds_add_u32: the row owns the column
+        const int bb = bin_of(d);
+        atomicAdd(H + (bb >> 1) * 64, 1u << ((bb & 1) << 4));  // ds_add_u32: the row owns the column
         ++total;
       }
     });
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
       // upper edge of the bin holding the kk-th key bounds the kk-th distance
       int cum = 0, bs = HB - 1;
       for (int b = 0; b < HB; ++b) {
-        cum += (int)H[b * 64];
+        cum += (int)((H[(b >> 1) * 64] >> ((b & 1) << 4)) & 0xffffu);
         if (cum >= kk) { bs = b; break; }
       }
       const int ub_bits = bin0 + bs + 1;
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   if (total > kk) {
     int cum = 0;
     for (int b = 0; b < HB; ++b) {
-      const int c = (int)H[b * 64];
+      const int c = (int)((H[(b >> 1) * 64] >> ((b & 1) << 4)) & 0xffffu);
       if (cum + c >= kk) { bs = b; below = cum; in_bs = c; break; }
       cum += c;
     }
