@@ -8,102 +8,121 @@
 //   object_classification cluster pooling (gnn_blocks.py:384-387):
 //     out[c] = max over member rows of the stem output
 //
-// Layout: 16 lanes per segment, 4 consecutive channels per lane (16-B f32 /
-// 8-B bf16 loads), 4 segments per wave.  Rows of a segment are read in segment
-// order and summed sequentially, so for a destination-major CSR whose sources
-// ascend the f32 sum is bit-identical to the reference scatter_add_ order.
-// Reads are unrolled 4 deep to keep several row loads in flight per lane.
+// Layout: one segment per group of 64/VEC lanes, VEC consecutive channels per lane
+// (one 16-B load per row and lane: 8 bf16 or 4 f32 channels; 8-B bf16 loads only when
+// C or the row stride is not a multiple of 8), so a 64-channel row is one fully used
+// 128-B (bf16) / 256-B (f32) line per lane group.  Rows of a segment are read in
+// segment order and summed sequentially, so for a destination-major CSR whose sources
+// ascend the f32 sum is bit-identical to the reference scatter_add_ order.  Each lane
+// keeps U = 8 row loads in flight: the loop issues 8 loads (indices clamped to the
+// segment's last row) before the first add, and a row past the end is masked out of
+// the sum -- the tail never falls back to one dependent load at a time.
 #include "rg_common.h"
 
 namespace rg {
 
-template <typename TS, typename TO, int OP>
+// a lane's VEC channels of one row as loaded (16 B, or 8 B for the bf16 VEC=4 fallback);
+// rows in flight stay in this raw form (4 VGPRs per bf16 row instead of 8 unpacked
+// floats: 8 waves per SIMD instead of 5) and are unpacked only when summed
+template <typename TS, int VEC>
+using raw_t = std::conditional_t<sizeof(TS) == 4 || VEC == 8, uint4, uint2>;
+
+template <typename TS, int VEC>
+__device__ __forceinline__ raw_t<TS, VEC> load_raw(const TS* __restrict__ p) {
+  static_assert(sizeof(TS) == 2 || VEC == 4, "f32 rows: 4 channels per lane");
+  return *(const raw_t<TS, VEC>*)p;
+}
+
+template <typename TS, int VEC>
+__device__ __forceinline__ float chan(const raw_t<TS, VEC>& x, int i) {
+  if constexpr (sizeof(TS) == 4) {
+    return __uint_as_float(((const uint32_t*)&x)[i]);
+  } else {
+    const uint32_t w = ((const uint32_t*)&x)[i >> 1];
+    return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+  }
+}
+
+template <typename TO, int VEC>
+__device__ __forceinline__ void store_vec(TO* __restrict__ o, const float (&a)[VEC]) {
+  if constexpr (sizeof(TO) == 4) {
+#pragma unroll
+    for (int i = 0; i < VEC; i += 4) *(f32x4*)(o + i) = (f32x4){a[i], a[i + 1], a[i + 2], a[i + 3]};
+  } else if constexpr (VEC == 8) {
+    *(uint4*)o = (uint4){pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]),
+                         pack_bf16x2(a[6], a[7])};
+  } else {
+    *(uint2*)o = (uint2){pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3])};
+  }
+}
+
+template <typename TS, typename TO, int OP, int VEC>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
                                                              const int* __restrict__ idx,
                                                              int n_seg, int C,
                                                              TO* __restrict__ out, int ld_out) {
-  const int g = threadIdx.x & 15;
-  const int seg_in_block = threadIdx.x >> 4;
-  const int stride = gridDim.x * 16;
-  for (int s = blockIdx.x * 16 + seg_in_block; s < n_seg; s += stride) {
+  constexpr int LPS = 64 / VEC;          // lanes per segment: 64 channels per pass
+  constexpr int SPB = 256 / LPS;         // segments per workgroup
+  constexpr int U = 8;                   // row loads in flight per lane
+  const int g = threadIdx.x % LPS;
+  const int seg_in_block = threadIdx.x / LPS;
+  const int stride = gridDim.x * SPB;
+  for (int s = blockIdx.x * SPB + seg_in_block; s < n_seg; s += stride) {
     const int b = seg_ptr[s], e = seg_ptr[s + 1];
     for (int c0 = 0; c0 < C; c0 += 64) {
-      const int c = c0 + 4 * g;
+      const int c = c0 + VEC * g;
       if (c >= C) continue;
-      float a0, a1, a2, a3;
-      if (OP == RG_REDUCE_MAX) {
-        a0 = a1 = a2 = a3 = -__int_as_float(0x7f800000);
-      } else {
-        a0 = a1 = a2 = a3 = 0.f;
-      }
-      auto load4 = [&](int p, float& v0, float& v1, float& v2, float& v3) {
-        const size_t row = idx ? (size_t)idx[p] : (size_t)p;
-        if constexpr (sizeof(TS) == 4) {
-          const f32x4 v = *(const f32x4*)((const float*)src + row * ld_src + c);
-          v0 = v.x; v1 = v.y; v2 = v.z; v3 = v.w;
-        } else {
-          const uint2 v = *(const uint2*)((const uint16_t*)src + row * ld_src + c);
-          v0 = __uint_as_float(v.x << 16);
-          v1 = __uint_as_float(v.x & 0xffff0000u);
-          v2 = __uint_as_float(v.y << 16);
-          v3 = __uint_as_float(v.y & 0xffff0000u);
-        }
-      };
-      auto acc = [&](float v0, float v1, float v2, float v3) {
-        if (OP == RG_REDUCE_MAX) {
-          a0 = fmaxf(a0, v0); a1 = fmaxf(a1, v1); a2 = fmaxf(a2, v2); a3 = fmaxf(a3, v3);
-        } else {
-          a0 = __fadd_rn(a0, v0); a1 = __fadd_rn(a1, v1);
-          a2 = __fadd_rn(a2, v2); a3 = __fadd_rn(a3, v3);
-        }
-      };
-      int p = b;
-      for (; p + 4 <= e; p += 4) {
-        float x[4][4];
-        load4(p, x[0][0], x[0][1], x[0][2], x[0][3]);
-        load4(p + 1, x[1][0], x[1][1], x[1][2], x[1][3]);
-        load4(p + 2, x[2][0], x[2][1], x[2][2], x[2][3]);
-        load4(p + 3, x[3][0], x[3][1], x[3][2], x[3][3]);
+      float a[VEC];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc(x[u][0], x[u][1], x[u][2], x[u][3]);
-      }
-      for (; p < e; ++p) {
-        float v0, v1, v2, v3;
-        load4(p, v0, v1, v2, v3);
-        acc(v0, v1, v2, v3);
+      for (int i = 0; i < VEC; ++i) a[i] = OP == RG_REDUCE_MAX ? -__int_as_float(0x7f800000) : 0.f;
+      for (int p = b; p < e; p += U) {
+        raw_t<TS, VEC> x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int q = p + u < e ? p + u : e - 1;
+          const size_t row = idx ? (size_t)idx[q] : (size_t)q;
+          x[u] = load_raw<TS, VEC>(src + row * ld_src + c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (p + u < e) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+              const float v = chan<TS, VEC>(x[u], i);
+              a[i] = OP == RG_REDUCE_MAX ? fmaxf(a[i], v) : __fadd_rn(a[i], v);
+            }
+          }
+        }
       }
       if (OP == RG_REDUCE_MAX) {
-        if (e == b) a0 = a1 = a2 = a3 = 0.f;
+        if (e == b)
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) a[i] = 0.f;
       } else if (OP == RG_REDUCE_MEAN) {
         const float n = (float)(e - b > 0 ? e - b : 1);
-        a0 = __fdiv_rn(a0, n); a1 = __fdiv_rn(a1, n); a2 = __fdiv_rn(a2, n); a3 = __fdiv_rn(a3, n);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) a[i] = __fdiv_rn(a[i], n);
       }
-      TO* o = out + (size_t)s * ld_out + c;
-      if constexpr (sizeof(TO) == 4) {
-        *(f32x4*)o = (f32x4){a0, a1, a2, a3};
-      } else {
-        uint2 w;
-        w.x = pack_bf16x2(a0, a1);
-        w.y = pack_bf16x2(a2, a3);
-        *(uint2*)o = w;
-      }
+      store_vec<TO, VEC>(out + (size_t)s * ld_out + c, a);
     }
   }
 }
 
-template <typename TS, typename TO>
-static void launch_seg(int op, int grid, hipStream_t st, const void* src, int ld_src,
-                       const int* seg_ptr, const int* idx, int n_seg, int C, void* out,
-                       int ld_out) {
+template <typename TS, typename TO, int VEC>
+static void launch_seg(int op, hipStream_t st, const void* src, int ld_src, const int* seg_ptr,
+                       const int* idx, int n_seg, int C, void* out, int ld_out) {
+  constexpr int SPB = 256 / (64 / VEC);
+  int grid = ceil_div(n_seg, SPB);
+  if (grid > 16384) grid = 16384;
   if (op == RG_REDUCE_SUM)
-    segment_reduce_kernel<TS, TO, RG_REDUCE_SUM><<<grid, 256, 0, st>>>(
+    segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(
         (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
   else if (op == RG_REDUCE_MEAN)
-    segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN><<<grid, 256, 0, st>>>(
+    segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN, VEC><<<grid, 256, 0, st>>>(
         (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
   else
-    segment_reduce_kernel<TS, TO, RG_REDUCE_MAX><<<grid, 256, 0, st>>>(
+    segment_reduce_kernel<TS, TO, RG_REDUCE_MAX, VEC><<<grid, 256, 0, st>>>(
         (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
 }
 
@@ -119,17 +138,22 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
              RG_ERR_UNSUPPORTED, "rg_segment_reduce: C=%d ld_src=%d ld_out=%d must be multiples of 4",
              C, ld_src, ld_out);
   if (n_seg <= 0) return RG_OK;
-  int grid = ceil_div(n_seg, 16);
-  if (grid > 16384) grid = 16384;
   hipStream_t st = (hipStream_t)stream;
+  // bf16 rows: 16-B loads (8 channels per lane) when C and the row stride allow
+  const bool v8 = C % 8 == 0 && ld_src % 8 == 0 && (out_dtype == RG_F32 || ld_out % 8 == 0) &&
+                  (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
   if (src_dtype == RG_F32 && out_dtype == RG_F32)
-    launch_seg<float, float>(op, grid, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<float, float, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+  else if (src_dtype == RG_BF16 && out_dtype == RG_F32 && v8)
+    launch_seg<uint16_t, float, 8>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32)
-    launch_seg<uint16_t, float>(op, grid, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, float, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+  else if (src_dtype == RG_BF16 && out_dtype == RG_BF16 && v8)
+    launch_seg<uint16_t, uint16_t, 8>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16)
-    launch_seg<uint16_t, uint16_t>(op, grid, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, uint16_t, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_F32 && out_dtype == RG_BF16)
-    launch_seg<float, uint16_t>(op, grid, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<float, uint16_t, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
   else
     RG_REQUIRE(false, RG_ERR_ARG, "rg_segment_reduce: bad dtypes");
   RG_LAUNCH_CHECK();
