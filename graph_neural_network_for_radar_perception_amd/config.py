@@ -143,3 +143,66 @@ def default_config(**overrides) -> config:
     """The yml configuration, with optional attribute overrides
     (e.g. ``graph_convolution_stem_channels=[64]*3`` for BASELINE config 1)."""
     return config(None, overrides)
+
+
+# values of configuration_radarscenes_classifier.yml (line numbers cited per key)
+_CLASSIFIER_DEFAULTS = {
+    'CLUSTERING': {'clustering_eps': 1.4, 'valid_cluster_num_meas_thr': 2,   # yml:5-8
+                   'meas_noise_var': 1},
+    'GNN_ARCHITECTURE': {                                                    # yml:10-18
+        'node_features': ['px', 'py', 'r', 'th', 'rcs'],
+        'activation': 'leakyrelu',
+        'aggregation': 'sum',
+        'node_feat_enc_stem_channels': [256, 128, 128],
+        'graph_convolution_stem_channels': [128, 128, 128, 128, 128],
+        'msg_mlp_hidden_dim': 128,
+        'node_pred_stem_channels': [128, 128, 128],
+    },
+    'OPTIMIZATION': {'optim': 'sgd', 'max_training_iterations': 100000,      # yml:20-24
+                     'learning_rate': 0.001, 'weight_decay': 0.0001},
+}
+
+
+class classifier_config(config):
+    """``set_config_classifier.config`` (set_config_classifier.py:9-52): the detector
+    attributes plus the ``classifier_*`` ones read by classifier/classifier.py:11-20.
+    Note the reference's own quirk kept as written: the classifier's OPTIMIZATION values
+    overwrite the detector's ``optim`` / ``learning_rate`` / ``weight_decay``."""
+
+    def __init__(self, config_gnn_filepath: Optional[str] = None,
+                 config_classifier_filepath: Optional[str] = None,
+                 overrides: Optional[dict] = None):
+        super().__init__(config_gnn_filepath)
+        if config_classifier_filepath is not None:
+            import yaml
+            with open(config_classifier_filepath, 'r') as fh:
+                c = yaml.safe_load(fh)
+        else:
+            import copy
+            c = copy.deepcopy(_CLASSIFIER_DEFAULTS)
+        cl = c['CLUSTERING']
+        self.clustering_eps = cl['clustering_eps']
+        self.valid_cluster_num_meas_thr = cl['valid_cluster_num_meas_thr']
+        import numpy as np
+        self.meas_noise_cov = cl['meas_noise_var'] * np.eye(2, dtype=np.float32)
+        a = c['GNN_ARCHITECTURE']
+        self.classifier_node_features = list(a['node_features'])
+        self.classifier_input_node_feat_dim = len(a['node_features'])
+        self.classifier_activation = a['activation']
+        self.classifier_aggregation = a['aggregation']
+        self.classifier_node_feat_enc_stem_channels = list(a['node_feat_enc_stem_channels'])
+        self.classifier_graph_convolution_stem_channels = list(a['graph_convolution_stem_channels'])
+        self.classifier_msg_mlp_hidden_dim = a['msg_mlp_hidden_dim']
+        self.classifier_node_pred_stem_channels = list(a['node_pred_stem_channels'])
+        o = c['OPTIMIZATION']
+        self.optim = o['optim']
+        self.max_train_iter = o['max_training_iterations']
+        self.learning_rate = o['learning_rate']
+        self.weight_decay = o['weight_decay']
+        for k, v in (overrides or {}).items():
+            setattr(self, k, v)
+
+
+def default_classifier_config(**overrides) -> classifier_config:
+    """The classifier yml configuration (on top of the detector yml), with overrides."""
+    return classifier_config(None, None, overrides)

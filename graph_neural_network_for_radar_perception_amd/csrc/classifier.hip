@@ -1,0 +1,183 @@
+// Graph build of the cluster-level classifier GNN.
+//
+//   compute_edge_index (datagen_classifier.py:124-133): the block-diagonal union of
+//     complete graphs, one per object (cluster of n measurements), self loops
+//     removed, edge_index = np.nonzero(adj) -- row-major: source ascending, then
+//     destination ascending.  Node i of object c (rows [off_c, off_c + n_c)) has the
+//     n_c - 1 neighbours off_c .. off_c + n_c - 1 except itself, so the CSR is closed
+//     form: row_ptr[i] = Epref_c + (i - off_c) (n_c - 1), Epref = prefix sum of
+//     n (n - 1).  The graph is symmetric, so this CSR is also the destination-major
+//     view the aggregation reads (segment i = sources of target i, ascending).
+//
+//   object row ranges of classifier Model_Inference.forward (classifier.py:60-68):
+//     startidx[0] = 0, startidx[i] = object_size[i-1], endidx = cumsum(object_size);
+//     object i pools rows [startidx[i], endidx[i]).  (startidx is NOT a cumulative
+//     offset in the reference -- for i >= 2 the pooled range starts at the previous
+//     object's SIZE -- and the drop-in reproduces exactly that.)
+#include "rg_common.h"
+#include "scan.h"
+
+namespace rg {
+
+static size_t align256_c(size_t v) { return (v + 255) & ~(size_t)255; }
+
+__global__ void object_sizes_kernel(const int64_t* __restrict__ object_size, int n_obj,
+                                    int* __restrict__ sz, int* __restrict__ pairs) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_obj) return;
+  const int n = (int)object_size[c];
+  sz[c] = n;
+  if (pairs) pairs[c] = n * (n - 1);
+}
+
+// one thread per node: its object by binary search over the node offsets, then its
+// n_c - 1 neighbours in ascending order
+__global__ void complete_rows_kernel(const int* __restrict__ node_off, const int* __restrict__ edge_off,
+                                     int n_obj, int n_nodes, int* __restrict__ row_ptr,
+                                     int* __restrict__ col, int64_t* __restrict__ edge_index,
+                                     long n_edges) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) row_ptr[n_nodes] = edge_off[n_obj];
+  if (i >= n_nodes) return;
+  if (i >= node_off[n_obj]) {  // past the last object: no edges
+    row_ptr[i] = edge_off[n_obj];
+    return;
+  }
+  int lo = 0, hi = n_obj - 1;   // last c with node_off[c] <= i (empty objects skipped)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (node_off[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  const int c = lo, off = node_off[c], n = node_off[c + 1] - off;
+  int p = edge_off[c] + (i - off) * (n - 1);
+  row_ptr[i] = p;
+  for (int j = off; j < off + n; ++j) {
+    if (j == i) continue;
+    if (col) col[p] = j;
+    if (edge_index) {
+      edge_index[p] = i;
+      edge_index[n_edges + p] = j;
+    }
+    ++p;
+  }
+}
+
+__global__ void object_ranges_kernel(const int64_t* __restrict__ object_size,
+                                     const int* __restrict__ node_off, int n_obj, int node_base,
+                                     int* __restrict__ begin, int* __restrict__ end) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_obj) return;
+  begin[c] = node_base + (c == 0 ? 0 : (int)object_size[c - 1]);
+  end[c] = node_base + node_off[c + 1];
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+extern "C" size_t rg_object_graph_workspace_size(int n_obj) {
+  return 4 * align256_c(((size_t)n_obj + 1) * sizeof(int)) + align256_c(scan_workspace_bytes(n_obj));
+}
+
+extern "C" int rg_object_complete_graph(const int64_t* object_size, int n_obj, int n_nodes,
+                                        long n_edges, int* row_ptr, int* col, int64_t* edge_index,
+                                        void* workspace, size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(n_obj >= 0 && n_nodes >= 0 && n_edges >= 0 && row_ptr, RG_ERR_ARG,
+             "rg_object_complete_graph: bad arguments");
+  RG_REQUIRE(workspace_bytes >= rg_object_graph_workspace_size(n_obj), RG_ERR_ARG,
+             "rg_object_complete_graph: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (n_obj == 0) {
+    RG_CHECK_HIP(hipMemsetAsync(row_ptr, 0, ((size_t)n_nodes + 1) * sizeof(int), st));
+    return RG_OK;
+  }
+  char* w = (char*)workspace;
+  const size_t a = align256_c(((size_t)n_obj + 1) * sizeof(int));
+  int* sz = (int*)w;
+  int* pairs = (int*)(w + a);
+  int* node_off = (int*)(w + 2 * a);
+  int* edge_off = (int*)(w + 3 * a);
+  void* sws = w + 4 * a;
+  object_sizes_kernel<<<ceil_div(n_obj, 256), 256, 0, st>>>(object_size, n_obj, sz, pairs);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(sz, n_obj, node_off, nullptr, sws, st);
+  if (rc) return rc;
+  rc = exclusive_scan(pairs, n_obj, edge_off, nullptr, sws, st);
+  if (rc) return rc;
+  complete_rows_kernel<<<ceil_div((long)n_nodes + 1, 256), 256, 0, st>>>(
+      node_off, edge_off, n_obj, n_nodes, row_ptr, col, edge_index, n_edges);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_object_row_ranges(const int64_t* object_size, int n_obj, int node_base,
+                                    int* begin, int* end, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
+  RG_REQUIRE(workspace_bytes >= rg_object_graph_workspace_size(n_obj), RG_ERR_ARG,
+             "rg_object_row_ranges: workspace too small");
+  if (n_obj <= 0) return RG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  char* w = (char*)workspace;
+  const size_t a = align256_c(((size_t)n_obj + 1) * sizeof(int));
+  int* sz = (int*)w;
+  int* node_off = (int*)(w + 2 * a);
+  void* sws = w + 4 * a;
+  object_sizes_kernel<<<ceil_div(n_obj, 256), 256, 0, st>>>(object_size, n_obj, sz, nullptr);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(sz, n_obj, node_off, nullptr, sws, st);
+  if (rc) return rc;
+  object_ranges_kernel<<<ceil_div(n_obj, 256), 256, 0, st>>>(object_size, node_off, n_obj,
+                                                             node_base, begin, end);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// classifier Loss (classifier/loss.py:5-14, lossfunc.py:52-60): torchvision
+// sigmoid_focal_loss(x, t, alpha=-1 (no alpha weighting), gamma=2) with one-hot t,
+//   ce = max(x, 0) - x t + log1p(exp(-|x|)),  p = sigmoid(x),
+//   p_t = p t + (1 - p)(1 - t),  loss = ce (1 - p_t)^2,
+// summed over the classes, then sum / n.
+// ---------------------------------------------------------------------------
+namespace rg {
+
+__global__ __launch_bounds__(256) void object_focal_loss_kernel(const float* __restrict__ logits,
+                                                                int ld,
+                                                                const int64_t* __restrict__ labels,
+                                                                int n, int nc, float* __restrict__ out) {
+  __shared__ double part[256];
+  double acc = 0.0;
+  for (int r = threadIdx.x; r < n; r += 256) {
+    const int64_t lab = labels[r];
+    float row = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float x = logits[(size_t)r * ld + c];
+      const float t = c == lab ? 1.f : 0.f;
+      const float p = 1.f / (1.f + expf(-x));
+      const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+      const float pt = p * t + (1.f - p) * (1.f - t);
+      const float m = 1.f - pt;
+      row += ce * (m * m);
+    }
+    acc += (double)row;
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(part[0] / (double)n);
+}
+
+}  // namespace rg
+
+extern "C" int rg_object_focal_loss(const float* logits, int ld, const int64_t* labels, int n,
+                                    int nc, float* out, void* stream) {
+  RG_REQUIRE(n > 0 && nc > 0 && ld >= nc, RG_ERR_ARG, "rg_object_focal_loss: n=%d nc=%d ld=%d",
+             n, nc, ld);
+  object_focal_loss_kernel<<<1, 256, 0, (hipStream_t)stream>>>(logits, ld, labels, n, nc, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -59,6 +59,7 @@ __device__ __forceinline__ void store_vec(TO* __restrict__ o, const float (&a)[V
 template <typename TS, typename TO, int OP, int VEC>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
+                                                             const int* __restrict__ seg_end,
                                                              const int* __restrict__ idx,
                                                              int n_seg, int C,
                                                              TO* __restrict__ out, int ld_out) {
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
   const int seg_in_block = threadIdx.x / LPS;
   const int stride = gridDim.x * SPB;
   for (int s = blockIdx.x * SPB + seg_in_block; s < n_seg; s += stride) {
-    const int b = seg_ptr[s], e = seg_ptr[s + 1];
+    const int b = seg_ptr[s], e = seg_end ? seg_end[s] : seg_ptr[s + 1];
     for (int c0 = 0; c0 < C; c0 += 64) {
       const int c = c0 + VEC * g;
       if (c >= C) continue;
@@ -111,28 +112,29 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
 
 template <typename TS, typename TO, int VEC>
 static void launch_seg(int op, hipStream_t st, const void* src, int ld_src, const int* seg_ptr,
-                       const int* idx, int n_seg, int C, void* out, int ld_out) {
+                       const int* seg_end, const int* idx, int n_seg, int C, void* out,
+                       int ld_out) {
   constexpr int SPB = 256 / (64 / VEC);
   int grid = ceil_div(n_seg, SPB);
   if (grid > 16384) grid = 16384;
   if (op == RG_REDUCE_SUM)
     segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
+        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
   else if (op == RG_REDUCE_MEAN)
     segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
+        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
   else
     segment_reduce_kernel<TS, TO, RG_REDUCE_MAX, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, idx, n_seg, C, (TO*)out, ld_out);
+        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
 }
 
 }  // namespace rg
 
 using namespace rg;
 
-extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
-                                 const int* idx, int n_seg, int C, int op, void* out,
-                                 int out_dtype, int ld_out, void* stream) {
+static int segment_reduce_impl(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
+                               const int* seg_end, const int* idx, int n_seg, int C, int op,
+                               void* out, int out_dtype, int ld_out, void* stream) {
   RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
   RG_REQUIRE(C > 0 && C <= 256 && C % 4 == 0 && ld_src % 4 == 0 && ld_out % 4 == 0,
              RG_ERR_UNSUPPORTED, "rg_segment_reduce: C=%d ld_src=%d ld_out=%d must be multiples of 4",
@@ -143,19 +145,35 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
   const bool v8 = C % 8 == 0 && ld_src % 8 == 0 && (out_dtype == RG_F32 || ld_out % 8 == 0) &&
                   (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
   if (src_dtype == RG_F32 && out_dtype == RG_F32)
-    launch_seg<float, float, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<float, float, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32 && v8)
-    launch_seg<uint16_t, float, 8>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, float, 8>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32)
-    launch_seg<uint16_t, float, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, float, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16 && v8)
-    launch_seg<uint16_t, uint16_t, 8>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, uint16_t, 8>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16)
-    launch_seg<uint16_t, uint16_t, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, uint16_t, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else if (src_dtype == RG_F32 && out_dtype == RG_BF16)
-    launch_seg<float, uint16_t, 4>(op, st, src, ld_src, seg_ptr, idx, n_seg, C, out, ld_out);
+    launch_seg<float, uint16_t, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
   else
     RG_REQUIRE(false, RG_ERR_ARG, "rg_segment_reduce: bad dtypes");
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
+                                 const int* idx, int n_seg, int C, int op, void* out,
+                                 int out_dtype, int ld_out, void* stream) {
+  return segment_reduce_impl(src, src_dtype, ld_src, seg_ptr, nullptr, idx, n_seg, C, op, out,
+                             out_dtype, ld_out, stream);
+}
+
+extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src,
+                                        const int* seg_begin, const int* seg_end, int n_seg, int C,
+                                        int op, void* out, int out_dtype, int ld_out,
+                                        void* stream) {
+  RG_REQUIRE(seg_begin && seg_end, RG_ERR_ARG, "rg_segment_reduce_ranges: begin / end missing");
+  return segment_reduce_impl(src, src_dtype, ld_src, seg_begin, seg_end, nullptr, n_seg, C, op,
+                             out, out_dtype, ld_out, stream);
 }

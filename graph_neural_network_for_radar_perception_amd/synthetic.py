@@ -153,3 +153,28 @@ def batch_labels(frames: list, row_ptr: np.ndarray, col: np.ndarray, num_classes
         clusters.append(lb['cluster_node_idx'])
         base += n
     return {k: np.concatenate(v) for k, v in out.items()}, clusters
+
+
+def make_objects(num_objects: int, seed: int = SEED0, min_size: int = 2, max_size: int = 24,
+                 num_classes: int = 7) -> dict:
+    """A synthetic classifier sample (the per-object features of
+    datagen_classifier.extract_and_compute_features_and_labels, datagen_classifier.py:62-100):
+    for each object, measurements centred on their mean and expressed in the covariance's
+    eigenbasis, as (x, y, r = |xy|, th = atan2(y, x), rcs); object sizes >=
+    valid_cluster_num_meas_thr (2, configuration_radarscenes_classifier.yml:7); labels
+    uniform over the classes.  Returns float32 node_features [N, 5], int64 object_size
+    [n_obj], int64 object_class [n_obj]."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(min_size, max_size + 1, num_objects).astype(np.int64)
+    feats = []
+    for n in sizes:
+        ext = rng.uniform(0.3, 2.5, 2)
+        xy = rng.normal(0.0, 1.0, (int(n), 2)) * ext
+        xy -= xy.mean(0)
+        r = np.sqrt(xy[:, 0] ** 2 + xy[:, 1] ** 2)
+        th = np.arctan2(xy[:, 1], xy[:, 0])
+        rcs = rng.normal(0.0, 10.0, int(n))
+        feats.append(np.stack((xy[:, 0], xy[:, 1], r, th, rcs), -1))
+    return {'node_features': np.concatenate(feats, 0).astype(np.float32),
+            'object_size': sizes,
+            'object_class': rng.integers(0, num_classes, num_objects).astype(np.int64)}

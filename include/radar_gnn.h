@@ -249,6 +249,40 @@ int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg
                       const int* idx, int n_seg, int C, int op, void* out, int out_dtype,
                       int ld_out, void* stream);
 
+/* The same reductions over explicit row ranges [seg_begin[s], seg_end[s]) (ranges may
+ * overlap): the per-object max-pool of the classifier GNN, whose reference ranges are
+ * not a CSR (classifier/classifier.py:60-68, see rg_object_row_ranges). */
+int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src, const int* seg_begin,
+                             const int* seg_end, int n_seg, int C, int op, void* out,
+                             int out_dtype, int ld_out, void* stream);
+
+/* ------------------------------------------- cluster-level classifier GNN */
+
+/* compute_edge_index (data_generator/datagen_classifier.py:124-133): block-diagonal
+ * union of complete graphs, one per object of object_size[c] (int64) measurements,
+ * no self loops, np.nonzero order.  n_nodes = sum(object_size), n_edges =
+ * sum(n (n - 1)).  row_ptr int32[n_nodes+1], col int32[n_edges] (nullable),
+ * edge_index int64[2][n_edges] (nullable).  The graph is symmetric: the CSR is also
+ * the destination-major view rg_segment_reduce reads. */
+size_t rg_object_graph_workspace_size(int n_obj);
+int rg_object_complete_graph(const int64_t* object_size, int n_obj, int n_nodes, long n_edges,
+                             int* row_ptr, int* col, int64_t* edge_index, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/* Pooling ranges of the classifier's Model_Inference.forward (classifier.py:60-68) for
+ * one sample whose rows start at node_base: begin[0] = 0, begin[c] = object_size[c-1],
+ * end = cumsum(object_size), each + node_base -- the reference's startidx, reproduced
+ * as written.  int32 [n_obj] each; workspace rg_object_graph_workspace_size(n_obj). */
+int rg_object_row_ranges(const int64_t* object_size, int n_obj, int node_base, int* begin,
+                         int* end, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Classifier Loss (classifier/loss.py:5-14): torchvision sigmoid_focal_loss with
+ * alpha = -1, gamma = 2 on one-hot targets, summed over classes, averaged over the
+ * n objects.  logits f32 [n][ld], labels int64 [n]; out f32 [1].  One workgroup,
+ * fixed-order f64 reduction (deterministic). */
+int rg_object_focal_loss(const float* logits, int ld, const int64_t* labels, int n, int nc,
+                         float* out, void* stream);
+
 
 /* ------------------------------------------------------------ proposal branch */
 

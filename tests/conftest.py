@@ -77,3 +77,32 @@ def cuda_device():
     from graph_neural_network_for_radar_perception_amd import _native
     _native.lib()  # fail loudly if the HIP library is missing on a GPU box
     return torch.device('cuda', 0)
+
+
+# classifier architecture overrides used by make_golden.make_classifier_fixtures
+CLASSIFIER_CASES = {
+    'classifier_yml': dict(),
+    'classifier_mean': dict(classifier_aggregation='mean',
+                            classifier_graph_convolution_stem_channels=[128, 128]),
+    'classifier_max': dict(classifier_aggregation='max',
+                           classifier_graph_convolution_stem_channels=[128, 128]),
+    'classifier_widths': dict(classifier_node_feat_enc_stem_channels=[96, 64],
+                              classifier_graph_convolution_stem_channels=[128, 64],
+                              classifier_msg_mlp_hidden_dim=96,
+                              classifier_node_pred_stem_channels=[64, 32]),
+}
+
+
+def classifier_cfg(name):
+    from graph_neural_network_for_radar_perception_amd.config import default_classifier_config
+    return default_classifier_config(**CLASSIFIER_CASES[name])
+
+
+def classifier_samples(d):
+    import torch
+    n = int(d['n_samples'])
+    return [dict(nf=torch.from_numpy(d[f's{i}/node_features']),
+                 ei=torch.from_numpy(d[f's{i}/edge_index'].astype(np.int64)),
+                 osz=torch.from_numpy(d[f's{i}/object_size']),
+                 gt=torch.from_numpy(d[f's{i}/object_class']),
+                 logits=d[f's{i}/logits']) for i in range(n)]

@@ -57,7 +57,11 @@ def _install_third_party_restatements():
             i, j = (1, 0) if self.flow == 'source_to_target' else (0, 1)
             x_i = x.index_select(0, edge_index[i])
             x_j = x.index_select(0, edge_index[j])
-            msg = self.message(x_i=x_i, x_j=x_j, edge_attr=kwargs.get('edge_attr'))
+            # PyG passes message() only the arguments its signature names
+            import inspect
+            names = inspect.signature(self.message).parameters
+            args = {'x_i': x_i, 'x_j': x_j, 'edge_attr': kwargs.get('edge_attr')}
+            msg = self.message(**{k: v for k, v in args.items() if k in names})
             n = x.shape[0]
             idx = edge_index[i].view(-1, 1).expand_as(msg)
             if self.aggr in ('add', 'sum'):
@@ -384,10 +388,72 @@ def make_training_fixtures():
     print('training', {k: v for k, v in data.items() if k.startswith('s')})
 
 
+def make_classifier_fixtures():
+    """Cluster-level classifier GNN (modules/neural_net/classifier):
+    the reference's own Model_Training(cfg) -- pred forward per sample and the loss over
+    a batch of samples -- on synthetic object samples (synthetic.make_objects).  The
+    edges come from the oracle's restatement of compute_edge_index: the reference's
+    datagen_classifier imports h5py (absent) through read_data."""
+    sys.path.insert(0, REPO)
+    from oracle.classifier_ref import compute_edge_index
+    from modules.set_configurations.set_config_classifier import config
+    from modules.neural_net.classifier.classifier import Model_Training
+    ycfg = os.path.join(REF, 'configuration_radarscenes_gnn.yml')
+    ccfg = os.path.join(REF, 'configuration_radarscenes_classifier.yml')
+
+    def case(name, cfg, n_objs, seed0, model_seed, save_weights=True):
+        torch.manual_seed(model_seed)
+        m = Model_Training(cfg).eval()
+        # the N(0, 0.01) head init makes every logit ~ the -ln 99 bias; scale the last
+        # Linear so that the logits depend visibly on the pooled features
+        with torch.no_grad():
+            m.pred.predict_node.pred_cls.head[1].weight.mul_(100.0)
+        samples = [synthetic.make_objects(n, seed0 + i) for i, n in enumerate(n_objs)]
+        nf = [torch.from_numpy(s['node_features']) for s in samples]
+        ei = [torch.from_numpy(compute_edge_index(s['object_size'].tolist())) for s in samples]
+        osz = [torch.from_numpy(s['object_size']) for s in samples]
+        gt = [torch.from_numpy(s['object_class']) for s in samples]
+        data = {}
+        with torch.no_grad():
+            for i in range(len(samples)):
+                data[f's{i}/logits'] = m.pred(nf[i], ei[i], osz[i]).numpy()
+                data[f's{i}/node_features'] = samples[i]['node_features']
+                data[f's{i}/object_size'] = samples[i]['object_size']
+                data[f's{i}/object_class'] = samples[i]['object_class']
+                data[f's{i}/edge_index'] = ei[i].numpy().astype(np.int32)
+            data['loss'] = np.float64(m(nf, ei, osz, gt).item())
+        sd = m.state_dict()
+        for k_, v in sd.items():
+            data['fp/' + k_] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+            if save_weights:
+                data['w/' + k_] = v.numpy()
+        data.update(n_samples=len(samples), model_seed=model_seed,
+                    aggregation=cfg.classifier_aggregation)
+        np.savez_compressed(os.path.join(HERE, name + '.npz'), **data)
+        print('classifier', name, 'loss', data['loss'],
+              'nodes', [int(s['object_size'].sum()) for s in samples])
+
+    case('classifier_yml', config(ycfg, ccfg), (40, 25, 9), 8001, 1234)
+    for aggr in ('mean', 'max'):
+        cfg = config(ycfg, ccfg)
+        cfg.classifier_aggregation = aggr
+        cfg.classifier_graph_convolution_stem_channels = [128, 128]
+        case(f'classifier_{aggr}', cfg, (30,), 8100, 77, save_weights=True)
+    cfg = config(ycfg, ccfg)
+    cfg.classifier_node_feat_enc_stem_channels = [96, 64]
+    cfg.classifier_graph_convolution_stem_channels = [128, 64]
+    cfg.classifier_msg_mlp_hidden_dim = 96
+    cfg.classifier_node_pred_stem_channels = [64, 32]
+    case('classifier_widths', cfg, (20, 7), 8200, 99)
+
+
 def main():
     sys.path.insert(0, REF)
     _install_third_party_restatements()
     torch.set_num_threads(8)
+    if '--classifier-only' in sys.argv:
+        make_classifier_fixtures()
+        return
     if '--training-only' in sys.argv:
         make_training_fixtures()
         return
@@ -396,6 +462,7 @@ def main():
         make_model_fixtures()
     make_proposal_fixtures()
     make_training_fixtures()
+    make_classifier_fixtures()
 
 
 if __name__ == '__main__':
