@@ -50,6 +50,11 @@ PRESETS = {
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
     'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
                cpu_warm=1),
+    # cluster-level classifier GNN (configuration_radarscenes_classifier.yml):
+    # 'frames' = samples per GPU, 'nodes' = objects per sample (2..24 measurements each),
+    # L = 5 layers of C = 128, complete graph per object
+    'cls': dict(frames=64, nodes=200, k=0, layers=5, graph='objects', eps2=0.0, cpu_frames=4,
+                cpu_warm=1),
 }
 
 
@@ -60,12 +65,15 @@ def parse():
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--config', default='c2', choices=sorted(PRESETS),
                    help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress; '
-                        'c4: config 4 training step (forward + backward + SGD, DDP)')
+                        'c4: config 4 training step (forward + backward + SGD, DDP); '
+                        'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4)')
     p.add_argument('--frames', type=int, default=None, help='frames per GPU')
     p.add_argument('--nodes', type=int, default=None)
     p.add_argument('--k', type=int, default=None)
     p.add_argument('--layers', type=int, default=None)
-    p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    p.add_argument('--dtype', default=None, choices=['bf16', 'fp32'],
+                   help='compute dtype (default bf16; fp32 for --config cls, the reference '
+                        'precision of the classifier)')
     p.add_argument('--cpu-frames', type=int, default=None,
                    help='CPU baseline sample (timed frames)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -74,6 +82,8 @@ def parse():
     for key, v in PRESETS[a.config].items():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
+    if a.dtype is None:
+        a.dtype = 'fp32' if a.config == 'cls' else 'bf16'
     return a
 
 
@@ -367,6 +377,116 @@ def train_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def cpu_classifier_baseline(args, cfg, sd):
+    """The oracle (numpy compute_edge_index + op-for-op torch fp32 classifier forward, the
+    reference's CPU algorithm) on a bounded sample: args.cpu_frames samples after
+    args.cpu_warm warm-up samples, median per sample."""
+    from oracle import classifier_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    times = []
+    for i in range(args.cpu_warm + args.cpu_frames):
+        smp = synthetic.make_objects(args.nodes, args.seed + 10**6 + i)
+        t0 = time.perf_counter()
+        ei = classifier_ref.compute_edge_index(smp['object_size'].tolist())
+        with torch.no_grad():
+            classifier_ref.forward(sd, cfg, torch.from_numpy(smp['node_features']),
+                                   torch.from_numpy(ei), torch.from_numpy(smp['object_size']))
+        if i >= args.cpu_warm:
+            times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    return {'value': round(args.nodes * 1e3 / ms, 2), 'unit': 'objects/s', 'cores': threads,
+            'kind': 'port', 'ms_per_sample': round(ms, 1), 'cpu_model': _cpu_model(),
+            'sample': f'{len(times)} sample(s) of {args.nodes} objects after {args.cpu_warm} '
+                      'warm-up: oracle compute_edge_index (numpy block_diag + nonzero) + '
+                      f'torch-fp32 classifier forward, median, torch threads={threads}'}
+
+
+def cls_main(args, world, rank, local):
+    """Cluster-level classifier GNN: one step = the batch's graph
+    (complete graph per object, from the object sizes) + pooling ranges + encoder + L
+    conv blocks + max-pool + stem/head, over `frames` samples of `nodes` objects."""
+    from graph_neural_network_for_radar_perception_amd.classifier import Model_Training
+    from graph_neural_network_for_radar_perception_amd.classifier import engine as ce
+    from graph_neural_network_for_radar_perception_amd.config import default_classifier_config
+    dev = torch.device('cuda', local)
+    cfg = default_classifier_config(classifier_graph_convolution_stem_channels=[128] * args.layers)
+    torch.manual_seed(1234)
+    model = Model_Training(cfg)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).eval().requires_grad_(False)
+    seeds = rank_frame_seeds(rank, args.frames, args.seed)
+    smps = [synthetic.make_objects(args.nodes, s) for s in seeds]
+    nf = torch.from_numpy(np.concatenate([s['node_features'] for s in smps])).to(dev)
+    sizes = np.concatenate([s['object_size'] for s in smps])
+    osz = torch.from_numpy(sizes).to(dev)
+    nodes = [int(s['object_size'].sum()) for s in smps]
+    sobj = torch.tensor(np.arange(0, args.frames + 1) * args.nodes, dtype=torch.int32).to(dev)
+    nbase = torch.tensor(np.cumsum([0] + nodes[:-1]), dtype=torch.int32).to(dev)
+    N = int(sum(nodes))
+    E = int((sizes * (sizes - 1)).sum())
+
+    def step(events=None):
+        g = ce.object_graph(osz, N, E)
+        b, e = ce.object_row_ranges(osz, sobj, nbase, args.frames)
+        return ce.forward_graph(model.pred, nf, g, b, e, args.dtype, events)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        events = []
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(events)
+        torch.cuda.synchronize()
+        barrier(world)
+        elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    durs = event_durations(events)
+    objs_total = sum_over_ranks(args.frames * args.nodes * args.steps, world)
+    s = 2 if args.dtype == 'bf16' else 4
+    C = 128
+    kern = {k: {'avg_ms': round(float(np.mean(v)), 4), 'launches_per_step': len(v) // args.steps}
+            for k, v in durs.items()}
+    ms = float(np.mean(durs['message_chain']))
+    flops = 2.0 * (2 * C * C + C * C) * E        # msg MLP 256 -> 128 -> 128 per edge
+    tf = flops / (ms * 1e-3) / 1e12
+    peak = MFMA_PEAK_TFLOPS[args.dtype]
+    kern['message_chain'].update(flops_per_launch=flops, algorithmic_tflops=round(tf, 2))
+    agg_ms = float(np.mean(durs['segment_reduce']))
+    agg_bytes = E * C * s + N * C * s + (N + 1) * 4
+    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    kern['segment_reduce'].update(bytes_per_launch=agg_bytes, algorithmic_gbs=round(agg_gbs, 1),
+                                  hbm_frac=round(agg_gbs / HBM_PEAK_GBS, 4))
+    line = {
+        'metric': 'classifier objects/sec (cluster-level classifier GNN, SURVEY §8(f) rank 4)',
+        'value': round(objs_total / elapsed, 1), 'unit': 'objects/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
+        'data': 'synthetic object samples (synthetic.make_objects: 2..24 measurements per '
+                'object), random-init weights of the classifier yml architecture',
+        'config': {'workload': f'classifier: {args.frames} samples x {args.nodes} objects per GPU, '
+                               f'L={args.layers} (C=128); step = complete-graph build + pooling '
+                               'ranges + encoder + message passing + max-pool + head',
+                   'samples_per_gpu': args.frames, 'objects_per_sample': args.nodes,
+                   'nodes_per_gpu': N, 'edges_per_gpu': E, 'layers': args.layers,
+                   'parallelism': f'sample-parallel x{world} (no collective in the step)'},
+        'roofline': {'kernel': 'message_chain (rg_mlp_chain GATHER3, classifier/blocks.py:84-85)',
+                     'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
+                     'frac': round(tf / peak, 4), 'traffic': None},
+        'kernels': kern,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_classifier_baseline(args, cfg, sd_cpu)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist()
@@ -374,6 +494,8 @@ def main():
         raise SystemExit('bench.py needs a HIP device')
     if args.config == 'c4':
         return train_main(args, world, rank, local)
+    if args.config == 'cls':
+        return cls_main(args, world, rank, local)
     dev = torch.device('cuda', local)
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
     from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline

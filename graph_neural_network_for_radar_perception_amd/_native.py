@@ -99,11 +99,13 @@ _SIGNATURES = {
     'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,
                                  _P, _I, _P, _P, _P, _I, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
-    'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+    'rg_segment_reduce_ranges_workspace_size': (_S, [_L, _I, _I]),
+    'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P, _S,
+                                      _P]),
     # classifier GNN graph build (classifier.hip)
     'rg_object_graph_workspace_size': (_S, [_I]),
     'rg_object_complete_graph': (_I, [_P, _I, _I, _L, _P, _P, _P, _P, _S, _P]),
-    'rg_object_row_ranges': (_I, [_P, _I, _I, _P, _P, _P, _S, _P]),
+    'rg_object_row_ranges': (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _S, _P]),
     'rg_object_focal_loss': (_I, [_P, _I, _P, _I, _I, _P, _P]),
     # training (train.hip)
     'rg_ffn_backward_workspace_size': (_S, []),

@@ -16,42 +16,20 @@ import numpy as np
 import torch
 
 from .. import _native as nat
-from ..engine import (ChainPlan, ConvPlan, DeviceGraph, _require_device, segment_reduce,
-                      specs_from_modules)
-
-_cache: dict = {}
-
+from ..engine import (ChainPlan, ConvPlan, DeviceGraph, _require_device, cached_plan,
+                      segment_reduce, specs_from_modules)
 
 def _dt(dtype: str):
     return torch.bfloat16 if dtype == 'bf16' else torch.float32
 
 
 def _conv_plan(blk, dtype, dev) -> ConvPlan:
-    key = (id(blk), dtype)
-    cp = _cache.get(key)
-    if cp is None:
-        cp = ConvPlan(blk, dtype, dev)
-        _cache[key] = cp
-    else:
-        cp.refresh()
-    return cp
+    return cached_plan(blk, ('conv', dtype), lambda: ConvPlan(blk, dtype, dev))
 
 
 def _chain_plan(mods, dtype, dev) -> ChainPlan:
-    key = (tuple(id(m) for m in mods), dtype)
-    p = _cache.get(key)
-    if p is None:
-        p = ChainPlan(specs_from_modules(mods), dtype, dev)
-        _cache[key] = p
-    else:
-        p.refresh()
-    return p
-
-
-def invalidate(model):
-    """Parameters changed behind torch's version counters."""
-    for k in list(_cache):
-        del _cache[k]
+    return cached_plan(mods[0], (tuple(id(m) for m in mods), dtype),
+                       lambda: ChainPlan(specs_from_modules(mods), dtype, dev))
 
 
 # --------------------------------------------------------------------------- graph build
@@ -86,23 +64,48 @@ def compute_edge_index(object_num_meas_list: Sequence[int], device='cuda') -> np
     return ei.cpu().numpy()
 
 
-def object_row_ranges(object_size: torch.Tensor, node_base: int, begin: torch.Tensor,
-                      end: torch.Tensor):
-    """The reference's pooling ranges (startidx / endidx, classifier.py:60-62) of one
-    sample, shifted by node_base, written into begin / end (int32)."""
+def object_graph(object_size: torch.Tensor, n_nodes: int, n_edges: int) -> DeviceGraph:
+    """The batch's classifier graph straight from the object sizes (no edge list):
+    the complete-graph CSR is symmetric, so it is its own destination-major view."""
+    lib = nat.lib()
+    dev = object_size.device
+    row_ptr, col, _ = object_complete_graph(object_size, n_nodes, n_edges, want_edge_index=False)
+    dst = torch.empty(max(n_edges, 1), dtype=torch.int32, device=dev)
+    nat.check(lib.rg_csr_rows(row_ptr.data_ptr(), n_nodes, dst.data_ptr(), nat.stream_ptr(dev)),
+              'rg_csr_rows')
+    return DeviceGraph(n_nodes, n_edges, row_ptr, dst, col, None, None, None, None,
+                       n_edges=n_edges)
+
+
+def object_row_ranges(object_size: torch.Tensor, sample_obj_ptr=None, sample_node_base=None,
+                      n_samples: int = 1):
+    """The reference's pooling ranges (startidx / endidx, classifier.py:60-62) of every
+    object of a batch of samples: int32 (begin, end) [n_obj]."""
     lib = nat.lib()
     dev = object_size.device
     osz = object_size.to(torch.int64).contiguous()
     n_obj = int(osz.numel())
+    begin = torch.empty(max(n_obj, 1), dtype=torch.int32, device=dev)
+    end = torch.empty(max(n_obj, 1), dtype=torch.int32, device=dev)
     ws = torch.empty(lib.rg_object_graph_workspace_size(n_obj), dtype=torch.uint8, device=dev)
-    nat.check(lib.rg_object_row_ranges(osz.data_ptr(), n_obj, int(node_base), begin.data_ptr(),
-                                       end.data_ptr(), ws.data_ptr(), ws.numel(),
+    nat.check(lib.rg_object_row_ranges(osz.data_ptr(), n_obj, nat.ptr(sample_obj_ptr),
+                                       nat.ptr(sample_node_base), int(n_samples),
+                                       begin.data_ptr(), end.data_ptr(), ws.data_ptr(), ws.numel(),
                                        nat.stream_ptr(dev)), 'rg_object_row_ranges')
+    return begin[:n_obj], end[:n_obj]
 
 
 # --------------------------------------------------------------------------- forward
+def _mark(events, name, dev):
+    """HIP event on the launch stream (bench.py per-kernel timing)."""
+    if events is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        events.append((name, ev))
+
+
 def run_conv_block_nodes(blk, x: torch.Tensor, edge_index: torch.Tensor, dtype: str = 'fp32',
-                         g: DeviceGraph = None) -> torch.Tensor:
+                         g: DeviceGraph = None, events=None) -> torch.Tensor:
     """classifier residual_graph_conv_block.forward (classifier/blocks.py:70-85):
     msg = MLP(cat(x[ei[1]], x[ei[0]])), agg = aggregate at ei[1], x' = identity +
     upd(cat(x, agg)).  Chain kernel in GATHER3 mode with no edge part (w2 = 0)."""
@@ -117,10 +120,14 @@ def run_conv_block_nodes(blk, x: torch.Tensor, edge_index: torch.Tensor, dtype: 
     x = x.to(tdt).contiguous()
     msg = torch.empty((max(E, 1), cp.c_msg), dtype=tdt, device=dev)
     if E > 0:
+        _mark(events, 'message_chain:start', dev)
         cp.msg(E, msg, x, x.shape[1], mode=nat.IN_GATHER3, idx0=g.dst, idx1=g.src)
+        _mark(events, 'message_chain:end', dev)
     agg = torch.empty((N, cp.c_msg), dtype=tdt, device=dev)
     if E > 0:
+        _mark(events, 'segment_reduce:start', dev)
         segment_reduce(msg, g.seg_ptr, N, cp.aggr, agg)
+        _mark(events, 'segment_reduce:end', dev)
     else:
         agg.zero_()
     if cp.res is not None:
@@ -129,7 +136,9 @@ def run_conv_block_nodes(blk, x: torch.Tensor, edge_index: torch.Tensor, dtype: 
     else:
         ident = x
     out = torch.empty((N, cp.c_out), dtype=tdt, device=dev)
+    _mark(events, 'update_chain:start', dev)
     cp.upd(N, out, x, x.shape[1], mode=nat.IN_CONCAT2, in1=agg, w1=cp.c_msg, residual=ident)
+    _mark(events, 'update_chain:end', dev)
     return out
 
 
@@ -145,15 +154,39 @@ def pool_and_classify(pred, x: torch.Tensor, begin: torch.Tensor, end: torch.Ten
     tdt = _dt(dtype)
     pooled = torch.empty((max(n_obj, 1), C), dtype=tdt, device=dev)
     if n_obj > 0:
+        sdt = nat.RG_BF16 if x.dtype == torch.bfloat16 else nat.RG_F32
+        N = x.shape[0]
+        ws = torch.empty(lib.rg_segment_reduce_ranges_workspace_size(N, C, sdt),
+                         dtype=torch.uint8, device=dev)
         nat.check(lib.rg_segment_reduce_ranges(
-            x.data_ptr(), nat.RG_BF16 if x.dtype == torch.bfloat16 else nat.RG_F32, x.stride(0),
-            begin.data_ptr(), end.data_ptr(), n_obj, C, nat.REDUCE['max'], pooled.data_ptr(),
+            x.data_ptr(), sdt, x.stride(0), N, begin.data_ptr(), end.data_ptr(), n_obj, C,
+            nat.REDUCE['max'], pooled.data_ptr(),
             nat.RG_BF16 if tdt == torch.bfloat16 else nat.RG_F32, pooled.stride(0),
-            nat.stream_ptr(dev)), 'rg_segment_reduce_ranges')
+            ws.data_ptr(), ws.numel(), nat.stream_ptr(dev)), 'rg_segment_reduce_ranges')
     head = _chain_plan(pred.chain(), dtype, dev)
     out = torch.empty((n_obj, head.out_dim), dtype=torch.float32, device=dev)
     if n_obj > 0:
         head(n_obj, out, pooled, C)
+    return out
+
+
+def forward_graph(model, node_features: torch.Tensor, g: DeviceGraph, begin: torch.Tensor,
+                  end: torch.Tensor, dtype: str = 'fp32', events=None) -> torch.Tensor:
+    """Encoder -> L conv blocks over g -> per-object max-pool over [begin, end) ->
+    stem + head: logits float32 [n_obj, num_classes] (classifier.py:50-72)."""
+    dev = node_features.device
+    N = g.n_nodes
+    enc = _chain_plan(list(model.encode_node_feat.encoder), dtype, dev)
+    x = torch.empty((N, enc.out_dim), dtype=_dt(dtype), device=dev)
+    xin = node_features.to(torch.float32).contiguous()
+    _mark(events, 'node_encoder:start', dev)
+    enc(N, x, xin, xin.shape[1])
+    _mark(events, 'node_encoder:end', dev)
+    for blk in model.pass_messages.conv_blk:
+        x = run_conv_block_nodes(blk, x, None, dtype, g, events)
+    _mark(events, 'pool_head:start', dev)
+    out = pool_and_classify(model.predict_node, x, begin, end, dtype)
+    _mark(events, 'pool_head:end', dev)
     return out
 
 
@@ -168,28 +201,19 @@ def forward_samples(model, node_features: List[torch.Tensor], edge_index: List[t
     bases = np.cumsum([0] + sizes)
     if len(node_features) == 1:
         nf, ei = node_features[0], edge_index[0].to(torch.int64)
+        osz = object_size[0].to(dev)
+        sobj = nbase = None
     else:
         nf = torch.cat(node_features, 0)
         ei = torch.cat([e.to(torch.int64) + int(b) for e, b in zip(edge_index, bases[:-1])], 1)
+        osz = torch.cat([o.to(dev).to(torch.int64) for o in object_size], 0)
+        nobj = np.cumsum([0] + [int(o.numel()) for o in object_size])
+        sobj = torch.tensor(nobj, dtype=torch.int32).to(dev)
+        nbase = torch.tensor(bases[:-1], dtype=torch.int32).to(dev)
     N = int(bases[-1])
     g = DeviceGraph.from_edge_index(ei.contiguous(), N, count_pairs=False)
-    enc = _chain_plan(list(model.encode_node_feat.encoder), dtype, dev)
-    tdt = _dt(dtype)
-    x = torch.empty((N, enc.out_dim), dtype=tdt, device=dev)
-    xin = nf.to(torch.float32).contiguous()
-    enc(N, x, xin, xin.shape[1])
-    for blk in model.pass_messages.conv_blk:
-        x = run_conv_block_nodes(blk, x, ei, dtype, g)
-    n_objs = [int(o.numel()) for o in object_size]
-    tot = sum(n_objs)
-    begin = torch.empty(max(tot, 1), dtype=torch.int32, device=dev)
-    end = torch.empty(max(tot, 1), dtype=torch.int32, device=dev)
-    o0 = 0
-    for osz, n, b in zip(object_size, n_objs, bases[:-1]):
-        if n:
-            object_row_ranges(osz, int(b), begin[o0:o0 + n], end[o0:o0 + n])
-        o0 += n
-    return pool_and_classify(model.predict_node, x, begin[:tot], end[:tot], dtype)
+    begin, end = object_row_ranges(osz, sobj, nbase, len(node_features))
+    return forward_graph(model, nf, g, begin, end, dtype)
 
 
 def focal_loss(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

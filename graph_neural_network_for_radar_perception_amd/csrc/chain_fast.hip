@@ -526,6 +526,13 @@ static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
   RG_FAST(768, spec(L, 0b1, 0b1), RG_IN_DENSE, 0, 64, 0, 64)
   RG_FAST(768, spec(L, 0b111, 0b111), RG_IN_DENSE, 0, 64, 0, 64, 64, 64)
   RG_FAST(1024, spec(L, 0b01, 0b01), RG_IN_DENSE, 0, 64, 0, 64, 32)
+  // cluster-level classifier GNN (classifier/blocks.py, classifier yml: C = 128, no
+  // normalisation): encoder 5 -> 256 -> 128 -> 128, message MLP on cat(x_i, x_j),
+  // update on cat(x, agg), pooled stem 3 x 128 + head (ffn 128 + Linear -> 7)
+  RG_FAST(512, spec(L, 0b000, 0b111), RG_IN_DENSE | FUSE01, 1, 5, 0, 256, 128, 128)
+  RG_FAST(512, spec(L, 0b00, 0b11), RG_IN_GATHER3, 0, 128, 0, 128, 128)
+  RG_FAST(512, spec(L, 0b0, 0b1), RG_IN_CONCAT2, 0, 128, 128, 128)
+  RG_FAST(512, spec(L, 0b00000, 0b01111), RG_IN_DENSE, 0, 128, 0, 128, 128, 128, 128, 32)
 #undef RG_FAST
   return RG_ERR_UNSUPPORTED;
 }

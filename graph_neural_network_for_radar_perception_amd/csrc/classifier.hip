@@ -63,13 +63,29 @@ __global__ void complete_rows_kernel(const int* __restrict__ node_off, const int
   }
 }
 
+// object c of sample s (objects [sobj[s], sobj[s+1]), rows from nbase[s]):
+//   begin = nbase[s] + (c == first ? 0 : object_size[c-1]),
+//   end   = nbase[s] + (node_off[c+1] - node_off[first])   (cumsum within the sample)
 __global__ void object_ranges_kernel(const int64_t* __restrict__ object_size,
-                                     const int* __restrict__ node_off, int n_obj, int node_base,
-                                     int* __restrict__ begin, int* __restrict__ end) {
+                                     const int* __restrict__ node_off, int n_obj,
+                                     const int* __restrict__ sobj, const int* __restrict__ nbase,
+                                     int n_samples, int* __restrict__ begin,
+                                     int* __restrict__ end) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n_obj) return;
-  begin[c] = node_base + (c == 0 ? 0 : (int)object_size[c - 1]);
-  end[c] = node_base + node_off[c + 1];
+  int first = 0, base = 0;
+  if (sobj) {
+    int lo = 0, hi = n_samples - 1;   // last s with sobj[s] <= c
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sobj[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    first = sobj[lo];
+    base = nbase[lo];
+  }
+  begin[c] = base + (c == first ? 0 : (int)object_size[c - 1]);
+  end[c] = base + (node_off[c + 1] - node_off[first]);
 }
 
 }  // namespace rg
@@ -111,9 +127,12 @@ extern "C" int rg_object_complete_graph(const int64_t* object_size, int n_obj, i
   return RG_OK;
 }
 
-extern "C" int rg_object_row_ranges(const int64_t* object_size, int n_obj, int node_base,
-                                    int* begin, int* end, void* workspace, size_t workspace_bytes,
-                                    void* stream) {
+extern "C" int rg_object_row_ranges(const int64_t* object_size, int n_obj,
+                                    const int* sample_obj_ptr, const int* sample_node_base,
+                                    int n_samples, int* begin, int* end, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(!sample_obj_ptr || (sample_node_base && n_samples >= 1), RG_ERR_ARG,
+             "rg_object_row_ranges: sample_obj_ptr needs sample_node_base and n_samples >= 1");
   RG_REQUIRE(workspace_bytes >= rg_object_graph_workspace_size(n_obj), RG_ERR_ARG,
              "rg_object_row_ranges: workspace too small");
   if (n_obj <= 0) return RG_OK;
@@ -127,8 +146,8 @@ extern "C" int rg_object_row_ranges(const int64_t* object_size, int n_obj, int n
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(sz, n_obj, node_off, nullptr, sws, st);
   if (rc) return rc;
-  object_ranges_kernel<<<ceil_div(n_obj, 256), 256, 0, st>>>(object_size, node_off, n_obj,
-                                                             node_base, begin, end);
+  object_ranges_kernel<<<ceil_div(n_obj, 256), 256, 0, st>>>(
+      object_size, node_off, n_obj, sample_obj_ptr, sample_node_base, n_samples, begin, end);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -21,6 +21,8 @@
 
 namespace rg {
 
+static constexpr int RANGE_BLOCK = 32;   // rows per block maximum (range max-pool)
+
 // a lane's VEC channels of one row as loaded (16 B, or 8 B for the bf16 VEC=4 fallback);
 // rows in flight stay in this raw form (4 VGPRs per bf16 row instead of 8 unpacked
 // floats: 8 waves per SIMD instead of 5) and are unpacked only when summed
@@ -56,45 +58,74 @@ __device__ __forceinline__ void store_vec(TO* __restrict__ o, const float (&a)[V
   }
 }
 
+// rows [b, e) of src (row(p) = idx ? idx[p] : p) folded into a[]: U = 8 row loads in
+// flight, indices past e clamped to e - 1 (cache hits) and masked out of the fold
+template <typename TS, int VEC, int OP>
+__device__ __forceinline__ void fold_rows(const TS* __restrict__ src, int ld, const int* __restrict__ idx,
+                                          int c, int b, int e, float (&a)[VEC]) {
+  constexpr int U = 8;
+  for (int p = b; p < e; p += U) {
+    raw_t<TS, VEC> x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = p + u < e ? p + u : e - 1;
+      const size_t row = idx ? (size_t)idx[q] : (size_t)q;
+      x[u] = load_raw<TS, VEC>(src + row * ld + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p + u < e) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float v = chan<TS, VEC>(x[u], i);
+          a[i] = OP == RG_REDUCE_MAX ? fmaxf(a[i], v) : __fadd_rn(a[i], v);
+        }
+      }
+    }
+  }
+}
+
+// Segment s covers rows [b, e): b = seg_ptr[s], e = seg_end ? seg_end[s] : seg_ptr[s+1];
+// uniform mode (uni > 0): b = s * uni, e = min(b + uni, n_uni) -- the 32-row block maxima
+// of the range max-pool.  bm (max only): 32-row block maxima of src; a long range then
+// reads its head rows, its whole blocks from bm and its tail rows (exact: max is
+// order-free).
 template <typename TS, typename TO, int OP, int VEC>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
                                                              const int* __restrict__ seg_end,
                                                              const int* __restrict__ idx,
+                                                             int uni, int n_uni,
+                                                             const TS* __restrict__ bm, int ld_bm,
                                                              int n_seg, int C,
                                                              TO* __restrict__ out, int ld_out) {
   constexpr int LPS = 64 / VEC;          // lanes per segment: 64 channels per pass
   constexpr int SPB = 256 / LPS;         // segments per workgroup
-  constexpr int U = 8;                   // row loads in flight per lane
   const int g = threadIdx.x % LPS;
   const int seg_in_block = threadIdx.x / LPS;
   const int stride = gridDim.x * SPB;
   for (int s = blockIdx.x * SPB + seg_in_block; s < n_seg; s += stride) {
-    const int b = seg_ptr[s], e = seg_end ? seg_end[s] : seg_ptr[s + 1];
+    int b, e;
+    if (uni > 0) {
+      b = s * uni;
+      e = min(b + uni, n_uni);
+    } else {
+      b = seg_ptr[s];
+      e = seg_end ? seg_end[s] : seg_ptr[s + 1];
+    }
     for (int c0 = 0; c0 < C; c0 += 64) {
       const int c = c0 + VEC * g;
       if (c >= C) continue;
       float a[VEC];
 #pragma unroll
       for (int i = 0; i < VEC; ++i) a[i] = OP == RG_REDUCE_MAX ? -__int_as_float(0x7f800000) : 0.f;
-      for (int p = b; p < e; p += U) {
-        raw_t<TS, VEC> x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int q = p + u < e ? p + u : e - 1;
-          const size_t row = idx ? (size_t)idx[q] : (size_t)q;
-          x[u] = load_raw<TS, VEC>(src + row * ld_src + c);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (p + u < e) {
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) {
-              const float v = chan<TS, VEC>(x[u], i);
-              a[i] = OP == RG_REDUCE_MAX ? fmaxf(a[i], v) : __fadd_rn(a[i], v);
-            }
-          }
-        }
+      if (OP == RG_REDUCE_MAX && bm && e - b >= 2 * RANGE_BLOCK) {
+        const int hb = (b + RANGE_BLOCK - 1) / RANGE_BLOCK, te = e / RANGE_BLOCK;
+        fold_rows<TS, VEC, OP>(src, ld_src, nullptr, c, b, hb * RANGE_BLOCK, a);
+        fold_rows<TS, VEC, OP>(bm, ld_bm, nullptr, c, hb, te, a);
+        fold_rows<TS, VEC, OP>(src, ld_src, nullptr, c, te * RANGE_BLOCK, e, a);
+      } else {
+        fold_rows<TS, VEC, OP>(src, ld_src, idx, c, b, e, a);
       }
       if (OP == RG_REDUCE_MAX) {
         if (e == b)
@@ -110,70 +141,120 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
   }
 }
 
+struct SegArgs {
+  const void* src;
+  int ld_src;
+  const int* seg_ptr;
+  const int* seg_end;
+  const int* idx;
+  int uni, n_uni;
+  const void* bm;
+  int ld_bm;
+  int n_seg, C;
+  void* out;
+  int ld_out;
+};
+
 template <typename TS, typename TO, int VEC>
-static void launch_seg(int op, hipStream_t st, const void* src, int ld_src, const int* seg_ptr,
-                       const int* seg_end, const int* idx, int n_seg, int C, void* out,
-                       int ld_out) {
+static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
   constexpr int SPB = 256 / (64 / VEC);
-  int grid = ceil_div(n_seg, SPB);
+  int grid = ceil_div(g.n_seg, SPB);
   if (grid > 16384) grid = 16384;
+#define RG_SEG_ARGS                                                                         \
+  (const TS*)g.src, g.ld_src, g.seg_ptr, g.seg_end, g.idx, g.uni, g.n_uni, (const TS*)g.bm,   \
+      g.ld_bm, g.n_seg, g.C, (TO*)g.out, g.ld_out
   if (op == RG_REDUCE_SUM)
-    segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
+    segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
   else if (op == RG_REDUCE_MEAN)
-    segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
+    segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
   else
-    segment_reduce_kernel<TS, TO, RG_REDUCE_MAX, VEC><<<grid, 256, 0, st>>>(
-        (const TS*)src, ld_src, seg_ptr, seg_end, idx, n_seg, C, (TO*)out, ld_out);
+    segment_reduce_kernel<TS, TO, RG_REDUCE_MAX, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
+#undef RG_SEG_ARGS
 }
 
-}  // namespace rg
-
-using namespace rg;
-
-static int segment_reduce_impl(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
-                               const int* seg_end, const int* idx, int n_seg, int C, int op,
-                               void* out, int out_dtype, int ld_out, void* stream) {
-  RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
-  RG_REQUIRE(C > 0 && C <= 256 && C % 4 == 0 && ld_src % 4 == 0 && ld_out % 4 == 0,
-             RG_ERR_UNSUPPORTED, "rg_segment_reduce: C=%d ld_src=%d ld_out=%d must be multiples of 4",
-             C, ld_src, ld_out);
-  if (n_seg <= 0) return RG_OK;
-  hipStream_t st = (hipStream_t)stream;
-  // bf16 rows: 16-B loads (8 channels per lane) when C and the row stride allow
-  const bool v8 = C % 8 == 0 && ld_src % 8 == 0 && (out_dtype == RG_F32 || ld_out % 8 == 0) &&
-                  (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
+// dispatch on (src dtype, out dtype, 16-B / 8-B lanes)
+static int launch_any(int op, int src_dtype, int out_dtype, bool v8, hipStream_t st,
+                      const SegArgs& g) {
   if (src_dtype == RG_F32 && out_dtype == RG_F32)
-    launch_seg<float, float, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<float, float, 4>(op, st, g);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32 && v8)
-    launch_seg<uint16_t, float, 8>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, float, 8>(op, st, g);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32)
-    launch_seg<uint16_t, float, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, float, 4>(op, st, g);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16 && v8)
-    launch_seg<uint16_t, uint16_t, 8>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, uint16_t, 8>(op, st, g);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16)
-    launch_seg<uint16_t, uint16_t, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<uint16_t, uint16_t, 4>(op, st, g);
   else if (src_dtype == RG_F32 && out_dtype == RG_BF16)
-    launch_seg<float, uint16_t, 4>(op, st, src, ld_src, seg_ptr, seg_end, idx, n_seg, C, out, ld_out);
+    launch_seg<float, uint16_t, 4>(op, st, g);
   else
     RG_REQUIRE(false, RG_ERR_ARG, "rg_segment_reduce: bad dtypes");
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
+}  // namespace rg
+
+using namespace rg;
+
+static bool check_shape(int C, int ld_src, int ld_out) {
+  return C > 0 && C <= 256 && C % 4 == 0 && ld_src % 4 == 0 && ld_out % 4 == 0;
+}
+
+// bf16 rows: 16-B loads (8 channels per lane) when C, the strides and the pointers allow
+static bool vec8(int C, int ld_src, int out_dtype, int ld_out, const void* src, const void* out) {
+  return C % 8 == 0 && ld_src % 8 == 0 && (out_dtype == RG_F32 || ld_out % 8 == 0) &&
+         (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
+}
+
 extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
                                  const int* idx, int n_seg, int C, int op, void* out,
                                  int out_dtype, int ld_out, void* stream) {
-  return segment_reduce_impl(src, src_dtype, ld_src, seg_ptr, nullptr, idx, n_seg, C, op, out,
-                             out_dtype, ld_out, stream);
+  RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
+  RG_REQUIRE(check_shape(C, ld_src, ld_out), RG_ERR_UNSUPPORTED,
+             "rg_segment_reduce: C=%d ld_src=%d ld_out=%d must be multiples of 4", C, ld_src,
+             ld_out);
+  if (n_seg <= 0) return RG_OK;
+  const SegArgs g = {src, ld_src, seg_ptr, nullptr, idx, 0, 0, nullptr, 0, n_seg, C, out, ld_out};
+  return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out),
+                    (hipStream_t)stream, g);
 }
 
-extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src,
+static int bm_ld(int C) { return (C + 7) / 8 * 8; }
+
+extern "C" size_t rg_segment_reduce_ranges_workspace_size(long n_rows, int C, int src_dtype) {
+  const size_t es = src_dtype == RG_BF16 ? 2 : 4;
+  return ((size_t)(n_rows + RANGE_BLOCK - 1) / RANGE_BLOCK) * bm_ld(C) * es + 256;
+}
+
+extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src, long n_rows,
                                         const int* seg_begin, const int* seg_end, int n_seg, int C,
                                         int op, void* out, int out_dtype, int ld_out,
-                                        void* stream) {
+                                        void* workspace, size_t workspace_bytes, void* stream) {
   RG_REQUIRE(seg_begin && seg_end, RG_ERR_ARG, "rg_segment_reduce_ranges: begin / end missing");
-  return segment_reduce_impl(src, src_dtype, ld_src, seg_begin, seg_end, nullptr, n_seg, C, op,
-                             out, out_dtype, ld_out, stream);
+  RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
+  RG_REQUIRE(check_shape(C, ld_src, ld_out), RG_ERR_UNSUPPORTED,
+             "rg_segment_reduce_ranges: C=%d ld_src=%d ld_out=%d must be multiples of 4", C,
+             ld_src, ld_out);
+  if (n_seg <= 0) return RG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const void* bm = nullptr;
+  const int ldb = bm_ld(C);
+  if (op == RG_REDUCE_MAX && workspace && n_rows >= 2 * RANGE_BLOCK &&
+      workspace_bytes >= rg_segment_reduce_ranges_workspace_size(n_rows, C, src_dtype)) {
+    // pass 1: 32-row block maxima of src, in src's dtype (exact)
+    void* w = (void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    const int nb = (int)((n_rows + RANGE_BLOCK - 1) / RANGE_BLOCK);
+    const SegArgs g1 = {src, ld_src, nullptr, nullptr, nullptr, RANGE_BLOCK, (int)n_rows,
+                        nullptr, 0, nb, C, w, ldb};
+    const int rc = launch_any(op, src_dtype, src_dtype,
+                              vec8(C, ld_src, src_dtype, ldb, src, w), st, g1);
+    if (rc) return rc;
+    bm = w;
+  }
+  const SegArgs g = {src, ld_src, seg_begin, seg_end, nullptr, 0, 0, bm, ldb, n_seg, C, out,
+                     ld_out};
+  return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out) &&
+                                                  (!bm || ldb % 8 == 0),
+                    st, g);
 }

@@ -23,6 +23,7 @@ float32.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -621,18 +622,30 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
 
 
 # --------------------------------------------------------------------------- block-level
-_block_cache: dict = {}
+# Plans of block-level calls, held weakly by the module that owns them (the first module
+# of a chain): a plan dies with its module, so a later module that happens to reuse a
+# freed module's id() never picks up a stale plan.
+_block_cache: 'weakref.WeakKeyDictionary[nn.Module, dict]' = weakref.WeakKeyDictionary()
 
 
-def _plan_for(mods, dtype='fp32', device=None) -> ChainPlan:
-    key = (tuple(id(m) for m in mods), dtype)
-    p = _block_cache.get(key)
+def cached_plan(owner: nn.Module, key, factory):
+    """The plan stored under `key` on `owner` (built by factory() on first use)."""
+    d = _block_cache.get(owner)
+    if d is None:
+        d = {}
+        _block_cache[owner] = d
+    p = d.get(key)
     if p is None:
-        p = ChainPlan(specs_from_modules(mods), dtype, device)
-        _block_cache[key] = p
+        p = factory()
+        d[key] = p
     else:
         p.refresh()
     return p
+
+
+def _plan_for(mods, dtype='fp32', device=None) -> ChainPlan:
+    return cached_plan(mods[0], (tuple(id(m) for m in mods), dtype),
+                       lambda: ChainPlan(specs_from_modules(mods), dtype, device))
 
 
 def run_blocks(mods, x: torch.Tensor, dtype: str = 'fp32') -> torch.Tensor:
@@ -651,13 +664,7 @@ def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):
     """residual_graph_conv_block.forward (gnn_blocks.py:96-110) on one graph."""
     _require_device(node_features, 'node_features')
     dev = node_features.device
-    cp = _block_cache.get((id(blk), dtype))
-    if cp is None:
-        cp = ConvPlan(blk, dtype, dev)
-        _block_cache[(id(blk), dtype)] = cp
-    else:
-        for c in cp.chains():
-            c.refresh()
+    cp = cached_plan(blk, ('conv', dtype), lambda: ConvPlan(blk, dtype, dev))
     N = node_features.shape[0]
     g = DeviceGraph.from_edge_index(edge_index, N, count_pairs=False)
     E = g.n_edges

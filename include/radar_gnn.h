@@ -249,12 +249,18 @@ int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg
                       const int* idx, int n_seg, int C, int op, void* out, int out_dtype,
                       int ld_out, void* stream);
 
-/* The same reductions over explicit row ranges [seg_begin[s], seg_end[s]) (ranges may
- * overlap): the per-object max-pool of the classifier GNN, whose reference ranges are
- * not a CSR (classifier/classifier.py:60-68, see rg_object_row_ranges). */
-int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src, const int* seg_begin,
-                             const int* seg_end, int n_seg, int C, int op, void* out,
-                             int out_dtype, int ld_out, void* stream);
+/* The same reductions over explicit row ranges [seg_begin[s], seg_end[s]) of src
+ * [n_rows] (ranges may overlap): the per-object max-pool of the classifier GNN, whose
+ * reference ranges are not a CSR (classifier/classifier.py:60-68, see
+ * rg_object_row_ranges) and overlap heavily.  For op = max with a workspace of
+ * rg_segment_reduce_ranges_workspace_size() bytes, a first pass writes 32-row block
+ * maxima and a long range reads its head rows, its whole blocks and its tail rows
+ * (exact); without one every row of every range is read. */
+size_t rg_segment_reduce_ranges_workspace_size(long n_rows, int C, int src_dtype);
+int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_src, long n_rows,
+                             const int* seg_begin, const int* seg_end, int n_seg, int C, int op,
+                             void* out, int out_dtype, int ld_out, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------- cluster-level classifier GNN */
 
@@ -269,12 +275,15 @@ int rg_object_complete_graph(const int64_t* object_size, int n_obj, int n_nodes,
                              int* row_ptr, int* col, int64_t* edge_index, void* workspace,
                              size_t workspace_bytes, void* stream);
 
-/* Pooling ranges of the classifier's Model_Inference.forward (classifier.py:60-68) for
- * one sample whose rows start at node_base: begin[0] = 0, begin[c] = object_size[c-1],
- * end = cumsum(object_size), each + node_base -- the reference's startidx, reproduced
- * as written.  int32 [n_obj] each; workspace rg_object_graph_workspace_size(n_obj). */
-int rg_object_row_ranges(const int64_t* object_size, int n_obj, int node_base, int* begin,
-                         int* end, void* workspace, size_t workspace_bytes, void* stream);
+/* Pooling ranges of the classifier's Model_Inference.forward (classifier.py:60-68),
+ * for a batch of samples: sample s owns objects [sample_obj_ptr[s], sample_obj_ptr[s+1])
+ * and its rows start at sample_node_base[s] (both int32; NULL = one sample at row 0).
+ * Per sample: begin[0] = 0, begin[c] = object_size[c-1], end = cumsum(object_size),
+ * each + the sample's row base -- the reference's startidx, reproduced as written.
+ * int32 [n_obj] each; workspace rg_object_graph_workspace_size(n_obj). */
+int rg_object_row_ranges(const int64_t* object_size, int n_obj, const int* sample_obj_ptr,
+                         const int* sample_node_base, int n_samples, int* begin, int* end,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* Classifier Loss (classifier/loss.py:5-14): torchvision sigmoid_focal_loss with
  * alpha = -1, gamma = 2 on one-hot targets, summed over classes, averaged over the

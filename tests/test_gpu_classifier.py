@@ -71,15 +71,41 @@ def test_compute_edge_index_bit_exact(cuda_device, sizes):
     np.testing.assert_array_equal(got, classifier_ref.compute_edge_index(sizes))
 
 
-def test_object_ranges_and_range_max(cuda_device):
+def test_object_ranges_batched(cuda_device):
+    """The reference's per-sample startidx / endidx (classifier.py:60-62), for a batch of
+    samples whose rows start at given bases (bit-exact)."""
     from graph_neural_network_for_radar_perception_amd.classifier import engine as ce
-    osz = torch.tensor([3, 5, 2, 4, 1], dtype=torch.int64)
-    n = len(osz)
-    b = torch.empty(n, dtype=torch.int32, device=cuda_device)
-    e = torch.empty(n, dtype=torch.int32, device=cuda_device)
-    ce.object_row_ranges(osz.to(cuda_device), 7, b, e)
-    sb, se = classifier_ref.object_ranges(osz)
-    assert b.cpu().tolist() == (sb + 7).tolist() and e.cpu().tolist() == (se + 7).tolist()
+    samples = [torch.tensor([3, 5, 2, 4, 1]), torch.tensor([2]), torch.tensor([7, 3, 9])]
+    bases = [0, 15, 17]
+    osz = torch.cat(samples).to(cuda_device)
+    sobj = torch.tensor([0, 5, 6, 9], dtype=torch.int32, device=cuda_device)
+    nbase = torch.tensor(bases, dtype=torch.int32, device=cuda_device)
+    b, e = ce.object_row_ranges(osz, sobj, nbase, 3)
+    want_b, want_e = [], []
+    for o, base in zip(samples, bases):
+        sb, se = classifier_ref.object_ranges(o)
+        want_b += (sb + base).tolist()
+        want_e += (se + base).tolist()
+    assert b.cpu().tolist() == want_b and e.cpu().tolist() == want_e
+    b1, e1 = ce.object_row_ranges(samples[0].to(cuda_device))
+    sb, se = classifier_ref.object_ranges(samples[0])
+    assert b1.cpu().tolist() == sb.tolist() and e1.cpu().tolist() == se.tolist()
+
+
+def test_object_graph_from_sizes_equals_edge_index_path(cuda_device):
+    """The bench's graph build (CSR straight from the object sizes) gives the same
+    logits as the drop-in path that takes the reference edge_index."""
+    from graph_neural_network_for_radar_perception_amd.classifier import engine as ce
+    m, d = _model('classifier_yml', cuda_device)
+    s = classifier_samples(d)[0]
+    osz = s['osz'].to(cuda_device)
+    N = int(s['osz'].sum())
+    E = int((s['osz'] * (s['osz'] - 1)).sum())
+    g = ce.object_graph(osz, N, E)
+    b, e = ce.object_row_ranges(osz)
+    with torch.no_grad():
+        out = ce.forward_graph(m.pred, s['nf'].to(cuda_device), g, b, e)
+    np.testing.assert_allclose(out.cpu().numpy(), s['logits'], **FP32_TOL)
 
 
 def test_classifier_singleton_objects(cuda_device):
@@ -96,3 +122,33 @@ def test_classifier_singleton_objects(cuda_device):
         ref = classifier_ref.forward(sd, cfg, nf, ei, osz)
         out = m.pred(nf.to(cuda_device), ei.to(cuda_device), osz.to(cuda_device))
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), **FP32_TOL)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('C', [128, 36])
+def test_range_max_block_path_exact(cuda_device, dtype, C):
+    """rg_segment_reduce_ranges max: the 32-row block-maximum path (long overlapping
+    ranges, unaligned heads / tails, empty and short ranges) is bit-identical to a
+    row-by-row max, with and without the workspace."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    lib = nat.lib()
+    g = torch.Generator().manual_seed(5)
+    N = 1000
+    x = torch.randn(N, C, generator=g).to(dtype).to(cuda_device)
+    ranges = [(0, 0), (3, 9), (0, 1000), (31, 33), (5, 700), (64, 128), (63, 129), (999, 1000),
+              (17, 600), (200, 263)]
+    b = torch.tensor([r[0] for r in ranges], dtype=torch.int32, device=cuda_device)
+    e = torch.tensor([r[1] for r in ranges], dtype=torch.int32, device=cuda_device)
+    want = torch.stack([x[s:t].float().amax(0) if t > s else torch.zeros(C, device=cuda_device)
+                        for s, t in ranges])
+    sdt = nat.RG_BF16 if dtype == torch.bfloat16 else nat.RG_F32
+    for use_ws in (True, False):
+        out = torch.empty(len(ranges), C, dtype=torch.float32, device=cuda_device)
+        ws = torch.empty(lib.rg_segment_reduce_ranges_workspace_size(N, C, sdt), dtype=torch.uint8,
+                         device=cuda_device)
+        nat.check(lib.rg_segment_reduce_ranges(
+            x.data_ptr(), sdt, x.stride(0), N, b.data_ptr(), e.data_ptr(), len(ranges), C,
+            nat.REDUCE['max'], out.data_ptr(), nat.RG_F32, out.stride(0),
+            ws.data_ptr() if use_ws else None, ws.numel() if use_ws else 0,
+            nat.stream_ptr(cuda_device)), 'rg_segment_reduce_ranges')
+        torch.testing.assert_close(out, want, rtol=0, atol=0)
