@@ -452,15 +452,44 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
   const long ntiles = (rows + 31) / 32;
-  for (long tile = (long)blockIdx.x * FW + wave; tile < ntiles; tile += (long)gridDim.x * FW) {
-    const long row = tile * 32 + (lane & 31);
-    const bool valid = row < rows;
-    bf16x8_t b[In::KS];
-    In::load(a, row, valid, lane >> 5, b);
+  const long tstride = (long)gridDim.x * FW;
+  auto run = [&](const bf16x8_t (&b)[In::KS], long row, bool valid) {
     if constexpr ((MODE & FUSE01) != 0)  // un-normalised first layer: tile-fused layers 0+1
       run_chain01<SPEC, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
     else
       run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
+  };
+  if constexpr ((MODE & ~FUSE01) == RG_IN_DENSE && IN_F32 && In::KS == 1) {
+    // float32 encoder inputs (<= 8 features per row): the next tile's row is loaded
+    // while this tile runs its chain, so no tile waits for an HBM round trip; lanes of
+    // the upper half (features 8..15) only supply zeros
+    const int h = lane >> 5;
+    float nx[8];
+    auto fetch = [&](long t, float (&v)[8]) {
+      const long r = t * 32 + (lane & 31);
+      const float* p = (const float*)a.in0 + (size_t)r * a.ld0;
+      const bool ok = h == 0 && t < ntiles && r < rows;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ok && j < a.w0real ? p[j] : 0.f;
+    };
+    long tile = (long)blockIdx.x * FW + wave;
+    fetch(tile, nx);
+    for (; tile < ntiles; tile += tstride) {
+      bf16x8_t b[1];
+      b[0] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(nx[0], nx[1]), bf2(nx[2], nx[3]),
+                                                  bf2(nx[4], nx[5]), bf2(nx[6], nx[7])});
+      fetch(tile + tstride, nx);
+      const long row = tile * 32 + (lane & 31);
+      run(b, row, row < rows);
+    }
+  } else {
+    for (long tile = (long)blockIdx.x * FW + wave; tile < ntiles; tile += tstride) {
+      const long row = tile * 32 + (lane & 31);
+      const bool valid = row < rows;
+      bf16x8_t b[In::KS];
+      In::load(a, row, valid, lane >> 5, b);
+      run(b, row, valid);
+    }
   }
 }
 

@@ -85,28 +85,33 @@ __device__ __forceinline__ bf16x8_t zero_bf8() {
 // Software pipelined: the A fragments of step s+1 are read from LDS while the MFMAs of
 // step s issue, so an MFMA never waits for the LDS read that feeds it; one scheduling
 // fence per step keeps the compiler from hoisting the whole layer's fragments.
+#ifndef RG_CONV_PFD
+#define RG_CONV_PFD 1  // A-fragment prefetch distance (k-steps) for layers with MT <= 2
+#endif
+
 template <int KS, int MT, int KT, int S0>
 __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
                                            int lane) {
   const char* wl = w + lane * 16;
-  bf16x8_t acur[MT], anxt[MT];
+  // narrow layers (MT <= 2) issue only MT MFMAs per k-step, less than an LDS round trip:
+  // their fragments are read PD steps ahead (registers: (PD + 1) * MT fragments)
+  constexpr int PD = MT <= 2 ? RG_CONV_PFD : 1;
+  bf16x8_t f[KS][MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0) * 1024));
+  for (int s = 0; s < PD && s < KS; ++s)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) f[s][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s) * 1024));
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    if (s + 1 < KS) {
+    if (s + PD < KS) {
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s + 1) * 1024));
+        f[s + PD][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s + PD) * 1024));
     }
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], b[s], acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s][m], b[s], acc[m], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < KS) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
-    }
   }
 }
 

@@ -399,11 +399,56 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     }
   }
   const int cnt = min(kk, total);
+  // A boundary bin with more than BBUF keys is refined in place: the same rings again,
+  // histogramming the next 6 bits of d's pattern among the keys of the boundary prefix
+  // (d >= 0, so its bit pattern is monotone), until the boundary prefix holds <= BBUF
+  // keys.  Only exact ties beyond BBUF (every bit equal: duplicates, lattices) or a
+  // boundary in a clamped edge bin still go to the sorted-insert pass (knn_grid), which
+  // runs one thread per row and would otherwise cost a whole wave per flagged row.
+  int sh = -1;         // refined: the boundary keys are those with (bits >> sh) == pref
+  uint32_t pref = 0;
+  if (in_bs > BBUF && bs > 0 && bs < HB - 1) {
+    sh = HSHIFT;
+    pref = (uint32_t)(bin0 + bs);
+    while (in_bs > BBUF && sh > 0) {
+      const int nsh = sh > 6 ? sh - 6 : 0;
+      const uint32_t msk = (1u << (sh - nsh)) - 1u;
+#pragma unroll
+      for (int b = 0; b < HW; ++b) H[b * 64] = 0u;
+      for (int r = 0; r <= r_knn; ++r) {
+        for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+          const uint32_t bits = __float_as_uint(sqdist(xi, yi, q.x, q.y));
+          if ((bits >> sh) == pref) {
+            const uint32_t sub = (bits >> nsh) & msk;
+            atomicAdd(H + (sub >> 1) * 64, 1u << ((sub & 1) << 4));
+          }
+        });
+      }
+      int cum = 0, sb = (int)msk;
+      for (int b = 0; b <= (int)msk; ++b) {
+        const int c = (int)((H[(b >> 1) * 64] >> ((b & 1) << 4)) & 0xffffu);
+        if (below + cum + c >= kk) { sb = b; in_bs = c; break; }
+        cum += c;
+      }
+      below += cum;
+      pref = (pref << (sh - nsh)) | (uint32_t)sb;
+      sh = nsh;
+    }
+  }
   const int need = cnt - below;
-  if (in_bs > BBUF) {  // massive ties in the boundary bin: exact insert path
+  if (in_bs > BBUF) {  // exact ties beyond the buffer: exact insert path
     redo[t] = 1;
     return;
   }
+  // key class: 0 selected outright, 1 boundary (buffered), 2 beyond
+  auto key_class = [&](float d) {
+    if (sh < 0) {
+      const int b = bin_of(d);
+      return b < bs ? 0 : (b == bs ? 1 : 2);
+    }
+    const uint32_t p = __float_as_uint(d) >> sh;
+    return p < pref ? 0 : (p == pref ? 1 : 2);
+  };
   uint32_t* Bj = H;  // boundary-bin indices reuse the histogram column: [e][lane], e < BBUF
   int* out = knn_idx + (size_t)row * K;
   int n_out = 0, nb = 0;
@@ -411,11 +456,11 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
-      const int b = bin_of(d);
-      if (b < bs) {
+      const int kc = key_class(d);
+      if (kc == 0) {
         out[n_out++] = j;
         if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));  // fire-and-forget
-      } else if (b == bs) {
+      } else if (kc == 1) {
         Bj[nb * 64] = (uint32_t)j;
         ++nb;
       }

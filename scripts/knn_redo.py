@@ -1,0 +1,43 @@
+"""Debug: how many rows does knn_select hand to the knn_grid fallback on the C2 batch?
+Reads the redo flags straight out of rg_build_graph's workspace (layout of
+graph_ws_layout in csrc/graph_build.hip).  GPU box: python scripts/knn_redo.py"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from graph_neural_network_for_radar_perception_amd import engine, synthetic  # noqa: E402
+
+
+def align(v):
+    return (v + 255) & ~255
+
+
+def main(frames=64, nodes=3000, k=32):
+    dev = torch.device('cuda', 0)
+    frs = [synthetic.make_frame(nodes, 1234 + i) for i in range(frames)]
+    px = torch.from_numpy(np.concatenate([f['meas_px'] for f in frs])).to(dev)
+    py = torch.from_numpy(np.concatenate([f['meas_py'] for f in frs])).to(dev)
+    fptr = torch.tensor(np.arange(frames + 1) * nodes, dtype=torch.int32).to(dev)
+    cache = {}
+    engine.build_graph(px, py, fptr, [nodes] * frames, k, 25.0, ws_cache=cache)
+    torch.cuda.synchronize()
+    ws = next(iter(cache.values()))
+    n = frames * nodes
+    W = (nodes + 31) // 32
+    K = next(x for x in (2, 4, 8, 11, 16, 17, 24, 32, 33, 48, 64) if x >= k + 1)
+    cpf = max(16, nodes // 2)
+    ncell = frames * cpf
+    sizes = [n * W * 4, n * K * 4, n * 4, n * 4, n * 4, n * 4, frames * 32, ncell * 4,
+             (ncell + 1) * 4, ncell * 4, n * 4, n * 16]
+    off = sum(align(s) for s in sizes)
+    redo = ws[off:off + 4 * n].view(torch.int32).cpu().numpy()
+    print('rows flagged for knn_grid:', int((redo != 0).sum()), 'of', n, flush=True)
+    wave_hit = (redo.reshape(-1, 64) != 0).any(1).sum()
+    print('waves with a flagged row:', int(wave_hit), 'of', n // 64)
+
+
+if __name__ == '__main__':
+    main()
