@@ -236,9 +236,16 @@ template <int SPEC, int LI, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, const float* nrm) {
   if constexpr (RG_CHAIN_EXP == 1) return;
   if constexpr (SPEC >= 0) {
-    if constexpr (((SPEC >> (8 + LI)) & 1) != 0)  // normalised => centred (host-checked)
+    constexpr bool NORM = ((SPEC >> (8 + LI)) & 1) != 0, ACTV = ((SPEC >> (16 + LI)) & 1) != 0;
+#ifndef RG_NO_FUSED_LEAKY
+    if constexpr (NORM && ACTV && (SPEC & 0xff) == ACT_LEAKY) {  // centred: two fmas
+      channel_norm_leaky_centered<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1], NORM_EPS);
+      return;
+    }
+#endif
+    if constexpr (NORM)  // normalised => centred (host-checked)
       channel_norm_pk_centered<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1], NORM_EPS);
-    if constexpr (((SPEC >> (16 + LI)) & 1) != 0) act_pk_all<(SPEC & 0xff), MT>(acc);
+    if constexpr (ACTV) act_pk_all<(SPEC & 0xff), MT>(acc);
   } else {
     norm_act_rows<-1, MT>(acc, L.mu != nullptr, nrm[2 * LI], nrm[2 * LI + 1], L.act, NORM_EPS,
                           L.centered != 0);

@@ -121,6 +121,12 @@ __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT],
 // (mu, sd = the layer's channel_normalization scalars, staged in LDS once per kernel)
 template <int ACT, int MT>
 __device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L, float mu, float sd) {
+#ifndef RG_NO_FUSED_LEAKY
+  if constexpr (ACT == ACT_LEAKY) {  // centred (host-checked): norm + leaky in two fmas
+    channel_norm_leaky_centered<MT>(acc, mu, sd, NORM_EPS);
+    return;
+  }
+#endif
   if constexpr (ACT >= 0) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
   else if (L.centered) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
   else channel_norm_pk<MT>(acc, mu, sd, NORM_EPS);

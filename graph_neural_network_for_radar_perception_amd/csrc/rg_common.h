@@ -244,6 +244,44 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
     for (int i = 0; i < 8; ++i) set_pair(acc[m], i, fma2(pair(acc[m], i), gs2, mu2));
 }
 
+// channel_normalization of a CENTRED layer fused with LeakyReLU(0.01) (constants.py:10):
+// leaky(y) = 0.505 y + 0.495 |y|, and |.| is a free source modifier of v_fma_f32, so with
+// y' = 0.505 y = x (0.505 gs) + 0.505 mu (one fma, the 0.505 folded into the row scale)
+// the activation is ONE fma per feature, out = |y'| C + y', C = 0.495 / 0.505 -- instead
+// of a multiply and a max.  Exact up to f32 rounding: y > 0 gives y' (1 + C) = y (1 +-
+// a few ulp), y < 0 gives 0.01 y to ~3e-6 relative (the cancellation in 1 - C), far
+// below the bf16 rounding the result goes through next.
+static constexpr float LEAKY_PRE = 0.505f;
+static constexpr float LEAKY_C = 0.495f / 0.505f;
+
+template <int MT>
+__device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], float mu, float sd,
+                                                            float eps) {
+  constexpr int N = 32 * MT;
+  f32x2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const f32x2 d0 = pair(acc[m], i), d1 = pair(acc[m], i + 1);
+      q0 = fma2(d0, d0, q0);
+      q1 = fma2(d1, d1, q1);
+    }
+  const f32x2 qt = add2(q0, q1);
+  float ss = qt.x + qt.y;
+  ss = add_xor32(ss);
+  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  const float gs = LEAKY_PRE * (sd * inv);
+  const f32x2 gs2 = {gs, gs}, mu2 = {LEAKY_PRE * mu, LEAKY_PRE * mu};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x2 y = fma2(pair(acc[m], i), gs2, mu2);
+      set_pair(acc[m], i, (f32x2){fmaf(fabsf(y.x), LEAKY_C, y.x), fmaf(fabsf(y.y), LEAKY_C, y.y)});
+    }
+}
+
 template <int ACT, int MT>
 __device__ __forceinline__ void act_pk_all(f32x16 (&acc)[MT]) {
 #pragma unroll
