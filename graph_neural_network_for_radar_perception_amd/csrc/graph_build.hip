@@ -222,7 +222,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
     const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
     const int* __restrict__ frame_ptr, int n_nodes, int kk, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
-    uint32_t* __restrict__ bits, int W, const int* __restrict__ only) {
+    uint32_t* __restrict__ bits, int W, const int* __restrict__ only, int2* __restrict__ kth) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_nodes) return;
   if (only && !only[t]) return;  // fallback pass: just the rows knn_select flagged
@@ -284,6 +284,12 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_grid(
   if (want_knn) {
     const int cnt = min(kk, g.n);
     knn_cnt[row] = cnt;
+    float kd = bd[0];
+    int kj = bi[0];
+#pragma unroll
+    for (int q = 1; q < K; ++q)
+      if (q == cnt - 1) { kd = bd[q]; kj = bi[q]; }
+    kth[row] = cnt < kk ? make_int2(0x7f800000, 0x7fffffff) : make_int2(__float_as_int(kd), kj);
     int* out = knn_idx + (size_t)row * K;
 #pragma unroll
     for (int q = 0; q < K; ++q)
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     const int* __restrict__ frame_ptr, const float* __restrict__ px,
     const float* __restrict__ py, int n_nodes, int kk, int K, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
-    uint32_t* __restrict__ bits, int W, int* __restrict__ redo) {
+    uint32_t* __restrict__ bits, int W, int* __restrict__ redo, int2* __restrict__ kth) {
   // per wave: [bin pair][lane], 16-bit counters (a row has < 65536 candidates per bin:
   // frames are far smaller); 8 KiB per wave lets 4-5 blocks share a CU
   __shared__ uint32_t lds[KNN_BLOCK / 64][HW * 64];
@@ -452,12 +458,15 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   uint32_t* Bj = H;  // boundary-bin indices reuse the histogram column: [e][lane], e < BBUF
   int* out = knn_idx + (size_t)row * K;
   int n_out = 0, nb = 0;
+  float md = -1.f;  // largest key selected outright (the kk-th key when need == 0)
+  int mj = -1;
   for (int r = 0; r <= r_knn; ++r) {
     for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
       const int kc = key_class(d);
       if (kc == 0) {
+        if (key_less(md, mj, d, j)) { md = d; mj = j; }
         out[n_out++] = j;
         if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));  // fire-and-forget
       } else if (kc == 1) {
@@ -486,14 +495,23 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     last_j = bj;
   }
   knn_cnt[row] = cnt;
+  // the kk-th key (+inf when the frame has fewer than kk points: every point is in)
+  if (cnt < kk) kth[row] = make_int2(0x7f800000, 0x7fffffff);
+  else kth[row] = need > 0 ? make_int2(__float_as_int(last_d), last_j)
+                           : make_int2(__float_as_int(md), mj);
 }
 
 // the transposed half of knn | knn^T (graph_features.py:38-43): bit (j, i) for every
 // kNN pair (i, j); bit (i, j) was set by the row's own search.  Mutual neighbours are
-// common, so the word is read first and only a missing bit costs an atomic.
+// common and need no write: i is in row j's own kNN set iff key (d_ij, i) <= row j's
+// kk-th key (the same (distance, index) order the selection used; d_ij recomputed
+// bit-identically from the coordinates), so the test reads two small L2-resident
+// arrays instead of a cache line of the bitset per pair, and only a missing bit costs
+// an atomic.
 __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict__ knn_idx,
-                         const int* __restrict__ knn_cnt, int K, int n_nodes,
-                         uint32_t* __restrict__ bits, int W) {
+                         const int* __restrict__ knn_cnt, const float* __restrict__ px,
+                         const float* __restrict__ py, const int2* __restrict__ kth, int K,
+                         int n_nodes, uint32_t* __restrict__ bits, int W) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int i = (int)(t / K);
   const int s = (int)(t % K);
@@ -503,9 +521,11 @@ __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict
   const int il = i - b;
   const int jl = knn_idx[(size_t)i * K + s];
   if (jl == il || jl < 0) return;
-  uint32_t* w = bits + (size_t)(b + jl) * W + (il >> 5);
-  const uint32_t m = 1u << (il & 31);
-  if (!(*w & m)) atomicOr(w, m);  // bits are only ever set: a set bit read is final
+  const int j = b + jl;
+  const float d = sqdist(px[j], py[j], px[i], py[i]);
+  const int2 kj = kth[j];
+  if (!key_less(__int_as_float(kj.x), kj.y, d, il)) return;  // (d, il) <= row j's kk-th key
+  atomicOr(bits + (size_t)j * W + (il >> 5), 1u << (il & 31));
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -672,6 +692,7 @@ struct GraphWs {
   float4* pts;
   int* redo;
   void* scan_ws;
+  int2* kth;   // per row: the kk-th (distance bits, frame-local index) key of its kNN set
   int cpf;
   long n_cells;
 };
@@ -707,7 +728,9 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
   char* p_pt = take((size_t)n_nodes * sizeof(float4));
   char* p_rd = take((size_t)n_nodes * sizeof(int));
   char* p_sc = take(scan_workspace_bytes(max((long)n_nodes, n_cells)));
+  char* p_kt = take((size_t)n_nodes * sizeof(int2));
   if (ws) {
+    ws->kth = (int2*)p_kt;
     ws->bits = (uint32_t*)p_bits;
     ws->knn_idx = (int*)p_idx;
     ws->knn_cnt = (int*)p_cnt;
@@ -741,11 +764,11 @@ static void launch_knn(hipStream_t st, const float* px, const float* py, const i
                        int W) {
   knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
       ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, px, py, n_nodes, kk, K, eps2, mode,
-      ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo);
+      ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo, ws.kth);
   if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
       ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, eps2, mode, ws.knn_idx,
-      ws.knn_cnt, ball_degree, ws.bits, W, ws.redo);
+      ws.knn_cnt, ball_degree, ws.bits, W, ws.redo, ws.kth);
 }
 
 extern "C" int rg_build_graph(const float* px, const float* py, const int* frame_ptr, int n_nodes,
@@ -809,8 +832,8 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   RG_LAUNCH_CHECK();
   if (mode != RG_GRAPH_RADIUS) {
     long tot = (long)n_nodes * K;
-    knn_mark<<<ceil_div(tot, 256), 256, 0, st>>>(ws.row_base, ws.knn_idx, ws.knn_cnt, K, n_nodes,
-                                                  ws.bits, W);
+    knn_mark<<<ceil_div(tot, 256), 256, 0, st>>>(ws.row_base, ws.knn_idx, ws.knn_cnt, px, py,
+                                                  ws.kth, K, n_nodes, ws.bits, W);
     RG_LAUNCH_CHECK();
   }
   row_count<<<ceil_div(n_nodes, 4), 256, 0, st>>>(ws.row_base, frame_ptr, ws.bits, W, n_nodes,

@@ -31,7 +31,7 @@ def main(frames=64, nodes=3000, k=32):
     cpf = max(16, nodes // 2)
     ncell = frames * cpf
     sizes = [n * W * 4, n * K * 4, n * 4, n * 4, n * 4, n * 4, frames * 32, ncell * 4,
-             (ncell + 1) * 4, ncell * 4, n * 4, n * 16]
+             (ncell + 1) * 4, ncell * 4, n * 4, n * 16]  # ... redo follows; kth after the scan ws
     off = sum(align(s) for s in sizes)
     redo = ws[off:off + 4 * n].view(torch.int32).cpu().numpy()
     print('rows flagged for knn_grid:', int((redo != 0).sum()), 'of', n, flush=True)
