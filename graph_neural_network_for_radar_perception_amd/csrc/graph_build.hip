@@ -319,32 +319,54 @@ static constexpr int BBUF = HW;   // boundary-bin candidates a row may buffer (i
 // boundary bin holds more than BBUF keys (massive exact ties: duplicates, lattices)
 // is flagged and redone by knn_grid.  Ball-query degree and radius bits are produced
 // here for every row.
-__global__ __launch_bounds__(KNN_BLOCK) void knn_select(
-    const float4* __restrict__ pts, const int* __restrict__ cell_start,
-    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
-    const int* __restrict__ frame_ptr, const float* __restrict__ px,
-    const float* __restrict__ py, int n_nodes, int kk, int K, float eps2, int mode,
-    int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
-    uint32_t* __restrict__ bits, int W, int* __restrict__ redo, int2* __restrict__ kth) {
-  // per wave: [bin pair][lane], 16-bit counters (a row has < 65536 candidates per bin:
-  // frames are far smaller); 8 KiB per wave lets 4-5 blocks share a CU
-  __shared__ uint32_t lds[KNN_BLOCK / 64][HW * 64];
-  const int lane = threadIdx.x & 63;
-  uint32_t* H = lds[threadIdx.x >> 6] + lane;  // this row's column (stride 64 words)
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_nodes) return;  // no block barriers below: rows own disjoint LDS columns
-  const int f = row_frame[t];  // the cell-ordered points of frame f fill its row range
-  const FrameGrid g = fg[f];
-  const int base = frame_ptr[f];
-  const float4 me = pts[t];
-  const float xi = me.x, yi = me.y;
-  const int il = __float_as_int(me.z);
-  const int cme = __float_as_int(me.w) - g.cell0;
-  const int cx = cme % g.gw, cy = cme / g.gw;
+// Ring visit over a point source (the global cell-ordered copy; an LDS-staged frame was
+// measured slower: 653 vs 587 us per C2 build, the LDS footprint halves occupancy):
+// cs(c) = first position of frame-relative cell c (cs(c + 1) its end),
+// pt(p) = the point at position p as {x, y, frame-local index}; body(q, p).
+template <typename CS, typename PT, typename F>
+__device__ __forceinline__ void for_ring_src(const FrameGrid& g, CS&& cs, PT&& pt, int cx, int cy,
+                                             int r, F&& body) {
+  for (int side = 0; side < 4; ++side) {
+    int ya, yb, xa, xb;
+    if (side < 2) {
+      const int yy = side == 0 ? cy - r : cy + r;
+      if (yy < 0 || yy >= g.gh || (side == 1 && r == 0)) continue;
+      ya = yb = yy;
+      xa = max(cx - r, 0);
+      xb = min(cx + r, g.gw - 1);
+    } else {
+      if (r == 0) continue;
+      const int xx = side == 2 ? cx - r : cx + r;
+      if (xx < 0 || xx >= g.gw) continue;
+      xa = xb = xx;
+      ya = max(cy - r + 1, 0);
+      yb = min(cy + r - 1, g.gh - 1);
+    }
+    for (int yy = ya; yy <= yb; ++yy) {
+      const int c = yy * g.gw;
+      const int p0 = cs(c + xa), p1 = cs(c + xb + 1);
+      for (int p = p0; p < p1; p += 4) {
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = pt(min(p + u, p1 - 1));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (p + u < p1) body(q[u], p + u);
+      }
+    }
+  }
+}
+
+// One row of the counting selection (see below); H = the row's LDS histogram column
+// (stride 64 words), redo_flag = where to flag the row for knn_grid.
+template <typename CS, typename PT>
+__device__ __forceinline__ void knn_select_row(
+    uint32_t* H, const FrameGrid& g, CS&& cs, PT&& pt, float xi, float yi, int il, int cx,
+    int cy, int row, int kk, int K, float eps2, int mode, int* __restrict__ knn_idx,
+    int* __restrict__ knn_cnt, int* __restrict__ ball_deg, uint32_t* __restrict__ rowbits,
+    int* redo_flag, int2* __restrict__ kth) {
   const bool want_knn = mode != RG_GRAPH_RADIUS;
   const bool want_rad = mode != RG_GRAPH_KNN;
-  const int row = base + il;
-  uint32_t* rowbits = bits + (size_t)row * W;
   // bins: d's exponent + 2 mantissa bits, 16 octaves centred on the cell area s^2
   const int bin0 = (int)(__float_as_uint(g.s * g.s) >> HSHIFT) - HB / 2;
   auto bin_of = [&](float d) {
@@ -360,7 +382,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   bool knn_done = !want_knn, ball_done = false;
   for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
     const bool count_knn = !knn_done;
-    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+    for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
       if (!ball_done) {
@@ -422,7 +444,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
 #pragma unroll
       for (int b = 0; b < HW; ++b) H[b * 64] = 0u;
       for (int r = 0; r <= r_knn; ++r) {
-        for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+        for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int) {
           const uint32_t bits = __float_as_uint(sqdist(xi, yi, q.x, q.y));
           if ((bits >> sh) == pref) {
             const uint32_t sub = (bits >> nsh) & msk;
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   }
   const int need = cnt - below;
   if (in_bs > BBUF) {  // exact ties beyond the buffer: exact insert path
-    redo[t] = 1;
+    *redo_flag = 1;
     return;
   }
   // key class: 0 selected outright, 1 boundary (buffered), 2 beyond
@@ -455,13 +477,13 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     const uint32_t p = __float_as_uint(d) >> sh;
     return p < pref ? 0 : (p == pref ? 1 : 2);
   };
-  uint32_t* Bj = H;  // boundary-bin indices reuse the histogram column: [e][lane], e < BBUF
+  uint32_t* Bp = H;  // boundary-key positions reuse the histogram column: [e][lane], e < BBUF
   int* out = knn_idx + (size_t)row * K;
   int n_out = 0, nb = 0;
   float md = -1.f;  // largest key selected outright (the kk-th key when need == 0)
   int mj = -1;
   for (int r = 0; r <= r_knn; ++r) {
-    for_ring(g, cell_start, pts, cx, cy, r, [&](const float4& q) {
+    for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int p) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
       const int kc = key_class(d);
@@ -470,22 +492,21 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
         out[n_out++] = j;
         if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));  // fire-and-forget
       } else if (kc == 1) {
-        Bj[nb * 64] = (uint32_t)j;
+        Bp[nb * 64] = (uint32_t)p;
         ++nb;
       }
     });
   }
-  // the need smallest (d, j) of the boundary bin (d recomputed bit-identically)
-  const float* fx = px + base;
-  const float* fy = py + base;
+  // the need smallest (d, j) of the boundary keys (d recomputed bit-identically)
   int last_j = -1;
   float last_d = -1.f;
   for (int q = 0; q < need; ++q) {
     float bd = __int_as_float(0x7f800000);
     int bj = 0x7fffffff;
     for (int e = 0; e < nb; ++e) {
-      const int j = (int)Bj[e * 64];
-      const float d = sqdist(xi, yi, fx[j], fy[j]);
+      const float4 c = pt((int)Bp[e * 64]);
+      const int j = __float_as_int(c.z);
+      const float d = sqdist(xi, yi, c.x, c.y);
       // next key strictly after the previous pick
       if (key_less(last_d, last_j, d, j) && key_less(d, j, bd, bj)) { bd = d; bj = j; }
     }
@@ -499,6 +520,34 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   if (cnt < kk) kth[row] = make_int2(0x7f800000, 0x7fffffff);
   else kth[row] = need > 0 ? make_int2(__float_as_int(last_d), last_j)
                            : make_int2(__float_as_int(md), mj);
+}
+
+// one thread per cell-ordered point, points and cell starts read from global memory
+// (frames too large to stage in LDS)
+__global__ __launch_bounds__(KNN_BLOCK) void knn_select(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, int kk, int K, float eps2, int mode,
+    int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
+    uint32_t* __restrict__ bits, int W, int* __restrict__ redo, int2* __restrict__ kth) {
+  // per wave: [bin pair][lane], 16-bit counters (a row has < 65536 candidates per bin:
+  // frames are far smaller); 8 KiB per wave lets 4-5 blocks share a CU
+  __shared__ uint32_t lds[KNN_BLOCK / 64][HW * 64];
+  const int lane = threadIdx.x & 63;
+  uint32_t* H = lds[threadIdx.x >> 6] + lane;  // this row's column (stride 64 words)
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_nodes) return;  // no block barriers below: rows own disjoint LDS columns
+  const int f = row_frame[t];  // the cell-ordered points of frame f fill its row range
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int row = base + il;
+  knn_select_row(H, g, [&](int c) { return cell_start[g.cell0 + c]; },
+                 [&](int p) { return pts[p]; }, me.x, me.y, il, cme % g.gw, cme / g.gw, row, kk,
+                 K, eps2, mode, knn_idx, knn_cnt, ball_deg, bits + (size_t)row * W, redo + t,
+                 kth);
 }
 
 // the transposed half of knn | knn^T (graph_features.py:38-43): bit (j, i) for every
@@ -759,11 +808,10 @@ extern "C" size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int m
 // counting selection for every row, then the exact sorted-insert search for the rows
 // it flagged (their outputs are rewritten identically)
 template <int K>
-static void launch_knn(hipStream_t st, const float* px, const float* py, const int* frame_ptr,
-                       int n_nodes, int kk, float eps2, int mode, GraphWs& ws, int* ball_degree,
-                       int W) {
+static void launch_knn(hipStream_t st, const int* frame_ptr, int n_nodes, int kk, float eps2,
+                       int mode, GraphWs& ws, int* ball_degree, int W) {
   knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
-      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, px, py, n_nodes, kk, K, eps2, mode,
+      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, K, eps2, mode,
       ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo, ws.kth);
   if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
@@ -815,18 +863,18 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   RG_LAUNCH_CHECK();
   RG_CHECK_HIP(hipMemsetAsync(ws.redo, 0, (size_t)n_nodes * sizeof(int), st));
   switch (K) {
-    case 1: launch_knn<1>(st, px, py, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
-    case 2: launch_knn<2>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 4: launch_knn<4>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 8: launch_knn<8>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 11: launch_knn<11>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 16: launch_knn<16>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 17: launch_knn<17>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 24: launch_knn<24>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 32: launch_knn<32>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 33: launch_knn<33>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 48: launch_knn<48>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 64: launch_knn<64>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 1: launch_knn<1>(st, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
+    case 2: launch_knn<2>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 4: launch_knn<4>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 8: launch_knn<8>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 11: launch_knn<11>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 16: launch_knn<16>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 17: launch_knn<17>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 24: launch_knn<24>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 32: launch_knn<32>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 33: launch_knn<33>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 48: launch_knn<48>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 64: launch_knn<64>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
     default: RG_REQUIRE(false, RG_ERR_UNSUPPORTED, "knn list %d", K);
   }
   RG_LAUNCH_CHECK();
