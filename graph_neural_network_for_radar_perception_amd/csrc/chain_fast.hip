@@ -466,7 +466,11 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     else
       run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
   };
+#ifdef RG_ENC_NOPF
+  if constexpr (false) {
+#else
   if constexpr ((MODE & ~FUSE01) == RG_IN_DENSE && IN_F32 && In::KS == 1) {
+#endif
     // float32 encoder inputs (<= 8 features per row): the next tile's row is loaded
     // while this tile runs its chain, so no tile waits for an HBM round trip; lanes of
     // the upper half (features 8..15) only supply zeros
@@ -542,6 +546,9 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
   return true;
 }
 
+#ifndef RG_ENC_FT
+#define RG_ENC_FT 768  // edge-encoder workgroup: 3 waves/SIMD (167 VGPRs, 13 dwords spilled) beat 2 (179) by 4 %
+#endif
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
 static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
 #define RG_FAST(FT, SP, MODE, F32, W0, W1, ...)                                           \
@@ -552,7 +559,7 @@ static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
   // node / edge encoders (graph_feature_encoding, gnn_blocks.py:19-42: block 0 is not
   // normalised)
   RG_FAST(512, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
-  RG_FAST(512, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
+  RG_FAST(RG_ENC_FT, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
   RG_FAST(512, spec(L, 0b11, 0b11), RG_IN_GATHER3, 0, 64, 64, 128, 64)
   RG_FAST(1024, spec(L, 0b1, 0b1), RG_IN_CONCAT2, 0, 64, 64, 64)
