@@ -319,52 +319,55 @@ static constexpr int BBUF = HW;   // boundary-bin candidates a row may buffer (i
 // boundary bin holds more than BBUF keys (massive exact ties: duplicates, lattices)
 // is flagged and redone by knn_grid.  Ball-query degree and radius bits are produced
 // here for every row.
-// Ring visit over a point source (the global cell-ordered copy; an LDS-staged frame was
-// measured slower: 653 vs 587 us per C2 build, the LDS footprint halves occupancy):
-// cs(c) = first position of frame-relative cell c (cs(c + 1) its end),
-// pt(p) = the point at position p as {x, y, frame-local index}; body(q, p).
-template <typename CS, typename PT, typename F>
-__device__ __forceinline__ void for_ring_src(const FrameGrid& g, CS&& cs, PT&& pt, int cx, int cy,
-                                             int r, F&& body) {
+// Ring visit for the selection, over TWO cell-ordered copies of the frame: the grid
+// rows cy - r and cy + r are contiguous position ranges of the row-major copy, the
+// columns cx - r and cx + r (strictly between them) contiguous ranges of the
+// column-major copy, so ring r is at most four ranges whose eight bounds are loaded
+// together -- one dependent round trip per ring instead of one per cell of the two
+// columns (a ring-r column side is 2r - 1 cells of ~3 points each).
+template <typename F>
+__device__ __forceinline__ void for_ring_rc(const FrameGrid& g, const int* __restrict__ cs_r,
+                                            const float4* __restrict__ pts_r,
+                                            const int* __restrict__ cs_c,
+                                            const float4* __restrict__ pts_c, int cx, int cy,
+                                            int r, F&& body) {
+  const int xa = max(cx - r, 0), xb = min(cx + r, g.gw - 1);
+  const int ya = max(cy - r + 1, 0), yb = min(cy + r - 1, g.gh - 1);
+  const bool s0 = cy - r >= 0;
+  const bool s1 = r > 0 && cy + r < g.gh;
+  const bool s2 = r > 0 && cx - r >= 0 && ya <= yb;
+  const bool s3 = r > 0 && cx + r < g.gw && ya <= yb;
+  const int c0 = g.cell0 + (cy - r) * g.gw, c1 = g.cell0 + (cy + r) * g.gw;
+  const int c2 = g.cell0 + (cx - r) * g.gh, c3 = g.cell0 + (cx + r) * g.gh;
+  int b[4], e[4];
+  b[0] = s0 ? cs_r[c0 + xa] : 0; e[0] = s0 ? cs_r[c0 + xb + 1] : 0;
+  b[1] = s1 ? cs_r[c1 + xa] : 0; e[1] = s1 ? cs_r[c1 + xb + 1] : 0;
+  b[2] = s2 ? cs_c[c2 + ya] : 0; e[2] = s2 ? cs_c[c2 + yb + 1] : 0;
+  b[3] = s3 ? cs_c[c3 + ya] : 0; e[3] = s3 ? cs_c[c3 + yb + 1] : 0;
+#pragma unroll
   for (int side = 0; side < 4; ++side) {
-    int ya, yb, xa, xb;
-    if (side < 2) {
-      const int yy = side == 0 ? cy - r : cy + r;
-      if (yy < 0 || yy >= g.gh || (side == 1 && r == 0)) continue;
-      ya = yb = yy;
-      xa = max(cx - r, 0);
-      xb = min(cx + r, g.gw - 1);
-    } else {
-      if (r == 0) continue;
-      const int xx = side == 2 ? cx - r : cx + r;
-      if (xx < 0 || xx >= g.gw) continue;
-      xa = xb = xx;
-      ya = max(cy - r + 1, 0);
-      yb = min(cy + r - 1, g.gh - 1);
-    }
-    for (int yy = ya; yy <= yb; ++yy) {
-      const int c = yy * g.gw;
-      const int p0 = cs(c + xa), p1 = cs(c + xb + 1);
-      for (int p = p0; p < p1; p += 4) {
-        float4 q[4];
+    const float4* __restrict__ pts = side < 2 ? pts_r : pts_c;
+    const int p0 = b[side], p1 = e[side];
+    for (int p = p0; p < p1; p += 4) {
+      float4 q[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] = pt(min(p + u, p1 - 1));
+      for (int u = 0; u < 4; ++u) q[u] = pts[min(p + u, p1 - 1)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (p + u < p1) body(q[u], p + u);
-      }
+      for (int u = 0; u < 4; ++u)
+        if (p + u < p1) body(q[u]);
     }
   }
 }
 
 // One row of the counting selection (see below); H = the row's LDS histogram column
 // (stride 64 words), redo_flag = where to flag the row for knn_grid.
-template <typename CS, typename PT>
+template <typename RING>
 __device__ __forceinline__ void knn_select_row(
-    uint32_t* H, const FrameGrid& g, CS&& cs, PT&& pt, float xi, float yi, int il, int cx,
-    int cy, int row, int kk, int K, float eps2, int mode, int* __restrict__ knn_idx,
-    int* __restrict__ knn_cnt, int* __restrict__ ball_deg, uint32_t* __restrict__ rowbits,
-    int* redo_flag, int2* __restrict__ kth) {
+    uint32_t* H, const FrameGrid& g, RING&& ring, const float* __restrict__ fx,
+    const float* __restrict__ fy, float xi, float yi, int il, int cx, int cy, int row, int kk,
+    int K, float eps2, int mode, int* __restrict__ knn_idx, int* __restrict__ knn_cnt,
+    int* __restrict__ ball_deg, uint32_t* __restrict__ rowbits, int* redo_flag,
+    int2* __restrict__ kth) {
   const bool want_knn = mode != RG_GRAPH_RADIUS;
   const bool want_rad = mode != RG_GRAPH_KNN;
   // bins: d's exponent + 2 mantissa bits, 16 octaves centred on the cell area s^2
@@ -382,7 +385,7 @@ __device__ __forceinline__ void knn_select_row(
   bool knn_done = !want_knn, ball_done = false;
   for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
     const bool count_knn = !knn_done;
-    for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int) {
+    ring(r, [&](const float4& q) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
       if (!ball_done) {
@@ -444,7 +447,7 @@ __device__ __forceinline__ void knn_select_row(
 #pragma unroll
       for (int b = 0; b < HW; ++b) H[b * 64] = 0u;
       for (int r = 0; r <= r_knn; ++r) {
-        for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int) {
+        ring(r, [&](const float4& q) {
           const uint32_t bits = __float_as_uint(sqdist(xi, yi, q.x, q.y));
           if ((bits >> sh) == pref) {
             const uint32_t sub = (bits >> nsh) & msk;
@@ -477,13 +480,13 @@ __device__ __forceinline__ void knn_select_row(
     const uint32_t p = __float_as_uint(d) >> sh;
     return p < pref ? 0 : (p == pref ? 1 : 2);
   };
-  uint32_t* Bp = H;  // boundary-key positions reuse the histogram column: [e][lane], e < BBUF
+  uint32_t* Bj = H;  // boundary-key indices reuse the histogram column: [e][lane], e < BBUF
   int* out = knn_idx + (size_t)row * K;
   int n_out = 0, nb = 0;
   float md = -1.f;  // largest key selected outright (the kk-th key when need == 0)
   int mj = -1;
   for (int r = 0; r <= r_knn; ++r) {
-    for_ring_src(g, cs, pt, cx, cy, r, [&](const float4& q, int p) {
+    ring(r, [&](const float4& q) {
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
       const int kc = key_class(d);
@@ -492,7 +495,7 @@ __device__ __forceinline__ void knn_select_row(
         out[n_out++] = j;
         if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));  // fire-and-forget
       } else if (kc == 1) {
-        Bp[nb * 64] = (uint32_t)p;
+        Bj[nb * 64] = (uint32_t)j;
         ++nb;
       }
     });
@@ -504,9 +507,8 @@ __device__ __forceinline__ void knn_select_row(
     float bd = __int_as_float(0x7f800000);
     int bj = 0x7fffffff;
     for (int e = 0; e < nb; ++e) {
-      const float4 c = pt((int)Bp[e * 64]);
-      const int j = __float_as_int(c.z);
-      const float d = sqdist(xi, yi, c.x, c.y);
+      const int j = (int)Bj[e * 64];
+      const float d = sqdist(xi, yi, fx[j], fy[j]);
       // next key strictly after the previous pick
       if (key_less(last_d, last_j, d, j) && key_less(d, j, bd, bj)) { bd = d; bj = j; }
     }
@@ -522,12 +524,13 @@ __device__ __forceinline__ void knn_select_row(
                            : make_int2(__float_as_int(md), mj);
 }
 
-// one thread per cell-ordered point, points and cell starts read from global memory
-// (frames too large to stage in LDS)
+// one thread per cell-ordered point (row-major copy: a wave is a patch of neighbours)
 __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
     const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const float4* __restrict__ pts_t, const int* __restrict__ cell_start_t,
     const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
-    const int* __restrict__ frame_ptr, int n_nodes, int kk, int K, float eps2, int mode,
+    const int* __restrict__ frame_ptr, const float* __restrict__ px,
+    const float* __restrict__ py, int n_nodes, int kk, int K, float eps2, int mode,
     int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
     uint32_t* __restrict__ bits, int W, int* __restrict__ redo, int2* __restrict__ kth) {
   // per wave: [bin pair][lane], 16-bit counters (a row has < 65536 candidates per bin:
@@ -543,11 +546,46 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
   const float4 me = pts[t];
   const int il = __float_as_int(me.z);
   const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
   const int row = base + il;
-  knn_select_row(H, g, [&](int c) { return cell_start[g.cell0 + c]; },
-                 [&](int p) { return pts[p]; }, me.x, me.y, il, cme % g.gw, cme / g.gw, row, kk,
-                 K, eps2, mode, knn_idx, knn_cnt, ball_deg, bits + (size_t)row * W, redo + t,
-                 kth);
+  knn_select_row(H, g,
+                 [&](int r, auto&& body) {
+                   for_ring_rc(g, cell_start, pts, cell_start_t, pts_t, cx, cy, r, body);
+                 },
+                 px + base, py + base, me.x, me.y, il, cx, cy, row, kk, K, eps2, mode, knn_idx,
+                 knn_cnt, ball_deg, bits + (size_t)row * W, redo + t, kth);
+}
+
+// column-major copy of the grid (for_ring_rc): transposed cell counts, then points
+// scattered by transposed cell (cell index cell0 + cx * gh + cy)
+__global__ void grid_transpose_counts(const FrameGrid* __restrict__ fg, int cpf, long n_cells,
+                                      const int* __restrict__ cell_cnt,
+                                      int* __restrict__ cell_cnt_t) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cells) return;
+  const int f = (int)(c / cpf);
+  const int cr = (int)(c - (long)f * cpf);
+  const FrameGrid g = fg[f];
+  if (cr < g.gw * g.gh) {
+    const int cx = cr % g.gw, cy = cr / g.gw;
+    cell_cnt_t[g.cell0 + cx * g.gh + cy] = cell_cnt[c];
+  } else {
+    cell_cnt_t[c] = 0;
+  }
+}
+
+__global__ void grid_scatter_t(const float* __restrict__ px, const float* __restrict__ py,
+                               const int* __restrict__ row_base, const int* __restrict__ row_frame,
+                               const FrameGrid* __restrict__ fg, const int* __restrict__ cell_of,
+                               int n_nodes, int* __restrict__ cursor,
+                               float4* __restrict__ pts_t) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  const FrameGrid g = fg[row_frame[i]];
+  const int cr = cell_of[i] - g.cell0;
+  const int ct = g.cell0 + (cr % g.gw) * g.gh + cr / g.gw;
+  const int pos = atomicAdd(cursor + ct, 1);
+  pts_t[pos] = make_float4(px[i], py[i], __int_as_float(i - row_base[i]), __int_as_float(ct));
 }
 
 // the transposed half of knn | knn^T (graph_features.py:38-43): bit (j, i) for every
@@ -742,6 +780,9 @@ struct GraphWs {
   int* redo;
   void* scan_ws;
   int2* kth;   // per row: the kk-th (distance bits, frame-local index) key of its kNN set
+  int* cell_cnt_t;     // column-major copy of the grid (for_ring_rc)
+  int* cell_start_t;
+  float4* pts_t;
   int cpf;
   long n_cells;
 };
@@ -778,8 +819,14 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
   char* p_rd = take((size_t)n_nodes * sizeof(int));
   char* p_sc = take(scan_workspace_bytes(max((long)n_nodes, n_cells)));
   char* p_kt = take((size_t)n_nodes * sizeof(int2));
+  char* p_ct = take((size_t)n_cells * sizeof(int));
+  char* p_st = take((size_t)(n_cells + 1) * sizeof(int));
+  char* p_pq = take((size_t)n_nodes * sizeof(float4));
   if (ws) {
     ws->kth = (int2*)p_kt;
+    ws->cell_cnt_t = (int*)p_ct;
+    ws->cell_start_t = (int*)p_st;
+    ws->pts_t = (float4*)p_pq;
     ws->bits = (uint32_t*)p_bits;
     ws->knn_idx = (int*)p_idx;
     ws->knn_cnt = (int*)p_cnt;
@@ -808,11 +855,13 @@ extern "C" size_t rg_build_graph_workspace_size(int n_nodes, int n_frames, int m
 // counting selection for every row, then the exact sorted-insert search for the rows
 // it flagged (their outputs are rewritten identically)
 template <int K>
-static void launch_knn(hipStream_t st, const int* frame_ptr, int n_nodes, int kk, float eps2,
-                       int mode, GraphWs& ws, int* ball_degree, int W) {
+static void launch_knn(hipStream_t st, const float* px, const float* py, const int* frame_ptr,
+                       int n_nodes, int kk, float eps2, int mode, GraphWs& ws, int* ball_degree,
+                       int W) {
   knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
-      ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, K, eps2, mode,
-      ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo, ws.kth);
+      ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr, px, py,
+      n_nodes, kk, K, eps2, mode, ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo,
+      ws.kth);
   if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
       ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, eps2, mode, ws.knn_idx,
@@ -861,20 +910,32 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   grid_scatter<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.cell_of, n_nodes,
                                                        ws.cursor, ws.pts);
   RG_LAUNCH_CHECK();
+  // the column-major copy of the same grid
+  grid_transpose_counts<<<ceil_div(ws.n_cells, 256), 256, 0, st>>>(ws.fg, ws.cpf, ws.n_cells,
+                                                                    ws.cell_cnt, ws.cell_cnt_t);
+  RG_LAUNCH_CHECK();
+  rc0 = exclusive_scan(ws.cell_cnt_t, ws.n_cells, ws.cell_start_t, ws.cell_start_t + ws.n_cells,
+                       ws.scan_ws, st);
+  if (rc0) return rc0;
+  RG_CHECK_HIP(hipMemcpyAsync(ws.cursor, ws.cell_start_t, (size_t)ws.n_cells * sizeof(int),
+                              hipMemcpyDeviceToDevice, st));
+  grid_scatter_t<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.row_frame, ws.fg,
+                                                         ws.cell_of, n_nodes, ws.cursor, ws.pts_t);
+  RG_LAUNCH_CHECK();
   RG_CHECK_HIP(hipMemsetAsync(ws.redo, 0, (size_t)n_nodes * sizeof(int), st));
   switch (K) {
-    case 1: launch_knn<1>(st, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
-    case 2: launch_knn<2>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 4: launch_knn<4>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 8: launch_knn<8>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 11: launch_knn<11>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 16: launch_knn<16>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 17: launch_knn<17>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 24: launch_knn<24>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 32: launch_knn<32>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 33: launch_knn<33>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 48: launch_knn<48>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
-    case 64: launch_knn<64>(st, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 1: launch_knn<1>(st, px, py, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
+    case 2: launch_knn<2>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 4: launch_knn<4>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 8: launch_knn<8>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 11: launch_knn<11>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 16: launch_knn<16>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 17: launch_knn<17>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 24: launch_knn<24>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 32: launch_knn<32>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 33: launch_knn<33>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 48: launch_knn<48>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
+    case 64: launch_knn<64>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
     default: RG_REQUIRE(false, RG_ERR_UNSUPPORTED, "knn list %d", K);
   }
   RG_LAUNCH_CHECK();
