@@ -178,6 +178,19 @@ __device__ __forceinline__ f32x2 act_pk(f32x2 y) {
   }
 }
 
+// 1 / (sqrt(ss / (N - 1)) + eps) of the bf16 kernels' channel_normalization: the raw
+// v_sqrt_f32 and v_rcp_f32 (~1 ulp each) instead of the correctly rounded sequences
+// (~20 dependent instructions on the critical path of every epilogue).  The scale they
+// feed multiplies values rounded to bf16 right after (2^-9 relative), so the <= 3-ulp
+// (2e-7) difference is invisible; the f32 parity path (mlp_chain.hip) stays exact.
+__device__ __forceinline__ float inv_std_bf16(float ss, int n, float eps) {
+#ifdef RG_EXACT_NORM
+  return 1.f / (__fsqrt_rn(ss * (1.f / (float)(n - 1))) + eps);
+#else
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(n - 1))) + eps);
+#endif
+}
+
 template <int MT>
 __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, float sd, float eps) {
   constexpr int N = 32 * MT;
@@ -206,7 +219,7 @@ __device__ __forceinline__ void channel_norm_pk(f32x16 (&acc)[MT], float mu, flo
   const f32x2 qt = add2(q0, q1);
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
-  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  const float inv = inv_std_bf16(ss, N, eps);
   // s*(x-mean)/(std+eps) + m as ONE fma per feature: x*gs + (m - mean*gs)
   const float gs = sd * inv, gb = fmaf(-mean, gs, mu);
   const f32x2 gs2 = {gs, gs}, gb2 = {gb, gb};
@@ -235,7 +248,7 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
   const f32x2 qt = add2(q0, q1);
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
-  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  const float inv = inv_std_bf16(ss, N, eps);
   const float gs = sd * inv;
   const f32x2 gs2 = {gs, gs}, mu2 = {mu, mu};
 #pragma unroll
@@ -270,7 +283,7 @@ __device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], f
   const f32x2 qt = add2(q0, q1);
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
-  const float inv = 1.f / (__fsqrt_rn(ss * (1.f / (N - 1))) + eps);
+  const float inv = inv_std_bf16(ss, N, eps);
   const float gs = LEAKY_PRE * (sd * inv);
   const f32x2 gs2 = {gs, gs}, mu2 = {LEAKY_PRE * mu, LEAKY_PRE * mu};
 #pragma unroll
