@@ -37,6 +37,10 @@ namespace conv {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef RG_CONV_PFX
+#define RG_CONV_PFX 0  // 1: the next block's x rows for P are loaded one block ahead
+#endif
+
 #ifndef RG_CONV_CT
 #define RG_CONV_CT 512  // threads per workgroup (8 waves, 2 per SIMD)
 #endif
@@ -205,6 +209,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     e0 = a.seg_ptr[blk * NB];
     e1 = a.seg_ptr[min(blk * NB + NB, a.n_nodes)];
   }
+#if RG_CONV_PFX
+  // x rows of the block's nodes for P, loaded one block ahead (the block start otherwise
+  // waits a full global round trip before its first MFMA)
+  bf16x8_t bxn[4];
+  {
+    const int nb0 = min(blk, a.n_blocks - 1) * NB;
+    const uint16_t* px = a.x + (size_t)min(nb0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
+  }
+#endif
   while (blk < a.n_blocks) {
     const int n0 = blk * NB;
     const int n1 = min(n0 + NB, a.n_nodes);
@@ -316,11 +331,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     //      third of the message MLP's first layer is the same for every edge into a node,
     //      so it is computed once per node here instead of once per edge
     {
+#if RG_CONV_PFX
+      bf16x8_t bx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bx[s] = bxn[s];
+#else
       const int node = min(n0 + r, n1 - 1);
       const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
       bf16x8_t bx[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
+#endif
       f32x16 accp[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
@@ -346,6 +367,14 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       ne0 = a.seg_ptr[nxt * NB];
       ne1 = a.seg_ptr[min(nxt * NB + NB, a.n_nodes)];
     }
+#if RG_CONV_PFX
+    {
+      const int nb0 = min(nxt, a.n_blocks - 1) * NB;  // clamped: always a valid row
+      const uint16_t* px = a.x + (size_t)min(nb0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
+    }
+#endif
 
     // The next tile's rows and the tile after's indices are loaded UNCONDITIONALLY
     // (clamped to the block's last edge: past the end every lane reads one row): a load

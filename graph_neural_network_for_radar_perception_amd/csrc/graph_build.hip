@@ -37,6 +37,11 @@ void set_error(const char* fmt, ...) {
 
 static constexpr int KNN_BLOCK = 256;
 
+#ifndef RG_KNN_EXP
+#define RG_KNN_EXP 0  // timing experiments only (wrong results): 1 no boundary pick,
+                      // 2 no selection pass (histogram pass only)
+#endif
+
 // fp32 squared distance exactly as numpy evaluates graph_features.py:72-73:
 // two products and one sum, each rounded, no fused multiply-add.
 __device__ __forceinline__ float sqdist(float xi, float yi, float xj, float yj) {
@@ -466,7 +471,12 @@ __device__ __forceinline__ void knn_select_row(
       sh = nsh;
     }
   }
-  const int need = cnt - below;
+  const int need = RG_KNN_EXP == 1 ? 0 : cnt - below;
+  if (RG_KNN_EXP == 2) {
+    knn_cnt[row] = 0;
+    kth[row] = make_int2(0, 0);
+    return;
+  }
   if (in_bs > BBUF) {  // exact ties beyond the buffer: exact insert path
     *redo_flag = 1;
     return;
@@ -554,6 +564,294 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
                  },
                  px + base, py + base, me.x, me.y, il, cx, cy, row, kk, K, eps2, mode, knn_idx,
                  knn_cnt, ball_deg, bits + (size_t)row * W, redo + t, kth);
+}
+
+// ---------------------------------------------------------------------------------
+// Cooperative counting selection (pure kNN mode): a group of CL lanes per row instead
+// of one thread per row.  The ring ranges of for_ring_rc are flattened into one index
+// space and the group's lanes load CL consecutive candidates at a time (four loads in
+// flight per lane), so a ring costs ceil(T / 4CL) dependent round trips instead of
+// ~T/4 per thread, and a wave's lanes no longer idle on the longest row's ring walk.
+// Same two passes and the same keys as knn_select_row: pass 1 histograms the candidate
+// distances in the row's LDS counters (shared by the group, ds_add), pass 2 selects the
+// keys below the boundary bin (ballot-compacted) and buffers the boundary keys
+// (distance bits + index) in LDS, from which the missing `need` are taken by rank.
+// The selected SET, the kk-th key, the ball count and the redo flag equal knn_select's;
+// only the order inside a row's knn_idx list differs (no consumer depends on it).
+// ---------------------------------------------------------------------------------
+#ifndef RG_KNN_COOP
+#define RG_KNN_COOP 1  // pure kNN mode: the cooperative selection (0: one thread per row)
+#endif
+#ifndef RG_KNN_CL
+#define RG_KNN_CL 16
+#endif
+static constexpr int CL = RG_KNN_CL;             // lanes per row
+static constexpr int CO_ROWS = KNN_BLOCK / CL;   // rows per workgroup
+static constexpr int CO_BUF = 32;                // boundary keys a row may buffer
+
+__device__ __forceinline__ void grp_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS traffic landed
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ int grp_sum(int v) {
+#pragma unroll
+  for (int d = 1; d < CL; d <<= 1) v += __shfl_xor(v, d, CL);
+  return v;
+}
+__device__ __forceinline__ int grp_incl_scan(int v, int sl) {
+#pragma unroll
+  for (int d = 1; d < CL; d <<= 1) {
+    const int t = __shfl_up(v, d, CL);
+    if (sl >= d) v += t;
+  }
+  return v;
+}
+
+// first bin b (of 64 16-bit counters in 32 words H[0..31]) with cum(0..b) >= target;
+// returns b (63 if never reached), the count below it and its own count
+struct BinPick { int bs, below, in_bs; };
+__device__ __forceinline__ BinPick grp_find_bin(const uint32_t* H, int sl, int target) {
+  constexpr int WPL = HW / CL;  // words (two 16-bit bins each) per lane
+  int c[2 * WPL];
+  int cl = 0;
+#pragma unroll
+  for (int w = 0; w < WPL; ++w) {
+    const uint32_t v = H[WPL * sl + w];
+    c[2 * w] = (int)(v & 0xffffu);
+    c[2 * w + 1] = (int)(v >> 16);
+    cl += c[2 * w] + c[2 * w + 1];
+  }
+  const int excl = grp_incl_scan(cl, sl) - cl;
+  const bool mine = excl < target && target <= excl + cl;
+  int bl = 0, cb = 0, own = 0, pre = excl;
+  bool found = false;
+#pragma unroll
+  for (int q = 0; q < 2 * WPL; ++q) {
+    if (!found && pre + c[q] >= target) { found = true; bl = q; cb = pre; own = c[q]; }
+    pre += c[q];
+  }
+  const uint64_t gm = ((1ull << CL) - 1ull) << (__lane_id() & ~(CL - 1));
+  const uint64_t m = __ballot(mine) & gm;
+  BinPick p{HB - 1, 0, 0};  // not reached (cannot happen for target <= the counted keys)
+  if (m == 0ull) return p;
+  const int src = (__ffsll((unsigned long long)m) - 1) & (CL - 1);
+  p.bs = __shfl(2 * WPL * sl + bl, src, CL);
+  p.below = __shfl(cb, src, CL);
+  p.in_bs = __shfl(own, src, CL);
+  return p;
+}
+
+// ring r of for_ring_rc, flattened: the group's lanes take candidates sl, sl + CL, ...
+// body(q, ok) runs on every lane of the group (ok = the lane holds a real candidate),
+// so ballots inside it see the whole group; returns the ring's candidate count
+template <typename F>
+__device__ __forceinline__ int ring_coop(const FrameGrid& g, const int* __restrict__ cs_r,
+                                         const float4* __restrict__ pts_r,
+                                         const int* __restrict__ cs_c,
+                                         const float4* __restrict__ pts_c, int cx, int cy, int r,
+                                         int sl, F&& body) {
+  const int xa = max(cx - r, 0), xb = min(cx + r, g.gw - 1);
+  const int ya = max(cy - r + 1, 0), yb = min(cy + r - 1, g.gh - 1);
+  const bool s0 = cy - r >= 0;
+  const bool s1 = r > 0 && cy + r < g.gh;
+  const bool s2 = r > 0 && cx - r >= 0 && ya <= yb;
+  const bool s3 = r > 0 && cx + r < g.gw && ya <= yb;
+  const int c0 = g.cell0 + (cy - r) * g.gw, c1 = g.cell0 + (cy + r) * g.gw;
+  const int c2 = g.cell0 + (cx - r) * g.gh, c3 = g.cell0 + (cx + r) * g.gh;
+  const int b0 = s0 ? cs_r[c0 + xa] : 0, e0 = s0 ? cs_r[c0 + xb + 1] : 0;
+  const int b1 = s1 ? cs_r[c1 + xa] : 0, e1 = s1 ? cs_r[c1 + xb + 1] : 0;
+  const int b2 = s2 ? cs_c[c2 + ya] : 0, e2 = s2 ? cs_c[c2 + yb + 1] : 0;
+  const int b3 = s3 ? cs_c[c3 + ya] : 0, e3 = s3 ? cs_c[c3 + yb + 1] : 0;
+  const int n0 = e0 - b0, n01 = n0 + (e1 - b1), n012 = n01 + (e2 - b2), T = n012 + (e3 - b3);
+  for (int o0 = 0; o0 < T; o0 += 4 * CL) {
+    float4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = min(o0 + sl + CL * u, T - 1);
+      const bool rm = o < n01;  // row-major copy (sides 0, 1) or column-major (2, 3)
+      const int p = o < n0 ? b0 + o : (o < n01 ? b1 + (o - n0) : (o < n012 ? b2 + (o - n01) : b3 + (o - n012)));
+      q[u] = rm ? pts_r[p] : pts_c[p];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(q[u], o0 + sl + CL * u < T);
+  }
+  return T;
+}
+
+__global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const float4* __restrict__ pts_t, const int* __restrict__ cell_start_t,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, int kk, int K, float eps2,
+    int* __restrict__ knn_idx, int* __restrict__ knn_cnt, int* __restrict__ ball_deg,
+    uint32_t* __restrict__ bits, int W, int* __restrict__ redo, int2* __restrict__ kth) {
+  __shared__ uint32_t hist_s[CO_ROWS][HW];
+  __shared__ uint32_t bufd_s[CO_ROWS][CO_BUF];
+  __shared__ int bufj_s[CO_ROWS][CO_BUF];
+  const int sl = threadIdx.x & (CL - 1), grp = threadIdx.x / CL;
+  const int lane = __lane_id();
+  const uint64_t gm = ((1ull << CL) - 1ull) << (lane & ~(CL - 1));
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int t = blockIdx.x * CO_ROWS + grp;  // cell-ordered point (neighbouring rows share a wave)
+  if (t >= n_nodes) return;                  // group-uniform; no block barriers below
+  uint32_t* H = hist_s[grp];
+  uint32_t* Bd = bufd_s[grp];
+  int* Bj = bufj_s[grp];
+  const int f = row_frame[t];
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const float xi = me.x, yi = me.y;
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
+  const int row = base + il;
+  uint32_t* rowbits = bits + (size_t)row * W;
+  auto ring = [&](int r, auto&& body) {
+    return ring_coop(g, cell_start, pts, cell_start_t, pts_t, cx, cy, r, sl, body);
+  };
+  const int bin0 = (int)(__float_as_uint(g.s * g.s) >> HSHIFT) - HB / 2;
+  auto bin_of = [&](float d) {
+    const int b = (int)(__float_as_uint(d) >> HSHIFT) - bin0;
+    return b < 0 ? 0 : (b >= HB ? HB - 1 : b);
+  };
+  for (int w = sl; w < HW; w += CL) H[w] = 0u;
+  grp_sync();
+  // ---- pass 1: histogram until the kk-th key is provably inside; ball count
+  const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
+  int ball = 0, total = 0, r_knn = rmax;
+  bool knn_done = false, ball_done = false;
+  for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
+    const bool count_knn = !knn_done, count_ball = !ball_done;
+    const int T = ring(r, [&](const float4& q, bool ok) {
+      if (!ok) return;
+      const int j = __float_as_int(q.z);
+      const float d = sqdist(xi, yi, q.x, q.y);
+      if (count_ball) ball += ((d <= eps2) && (j != il)) ? 1 : 0;
+      if (count_knn) {
+        const int bb = bin_of(d);
+        atomicAdd(H + (bb >> 1), 1u << ((bb & 1) << 4));
+      }
+    });
+    const float bound = ring_bound(g, r);
+    if (eps2 < bound) ball_done = true;
+    if (count_knn) {
+      total += T;
+      if (total >= kk) {
+        grp_sync();
+        const BinPick bp = grp_find_bin(H, sl, kk);
+        const int ub_bits = bin0 + bp.bs + 1;
+        const float ub = bp.bs == HB - 1 ? __int_as_float(0x7f800000)
+                                         : (ub_bits <= 0 ? 0.f : __uint_as_float((uint32_t)ub_bits << HSHIFT));
+        if (ub <= bound) {
+          knn_done = true;
+          r_knn = r;
+        }
+      }
+    }
+  }
+  ball = grp_sum(ball);
+  if (sl == 0) ball_deg[row] = ball;
+  grp_sync();
+  // ---- boundary bin (and in-place refinement of an over-full one, as knn_select_row)
+  int bs = HB, below = total, in_bs = 0;
+  if (total > kk) {
+    const BinPick bp = grp_find_bin(H, sl, kk);
+    bs = bp.bs; below = bp.below; in_bs = bp.in_bs;
+  }
+  const int cnt = min(kk, total);
+  int sh = -1;
+  uint32_t pref = 0;
+  if (in_bs > CO_BUF && bs > 0 && bs < HB - 1) {
+    sh = HSHIFT;
+    pref = (uint32_t)(bin0 + bs);
+    while (in_bs > CO_BUF && sh > 0) {
+      const int nsh = sh > 6 ? sh - 6 : 0;
+      const uint32_t msk = (1u << (sh - nsh)) - 1u;
+      grp_sync();
+      for (int w = sl; w < HW; w += CL) H[w] = 0u;
+      grp_sync();
+      for (int r = 0; r <= r_knn; ++r) {
+        ring(r, [&](const float4& q, bool ok) {
+          if (!ok) return;
+          const uint32_t bits = __float_as_uint(sqdist(xi, yi, q.x, q.y));
+          if ((bits >> sh) == pref) {
+            const uint32_t sub = (bits >> nsh) & msk;
+            atomicAdd(H + (sub >> 1), 1u << ((sub & 1) << 4));
+          }
+        });
+      }
+      grp_sync();
+      const BinPick bp = grp_find_bin(H, sl, kk - below);
+      below += bp.below;
+      in_bs = bp.in_bs;
+      pref = (pref << (sh - nsh)) | (uint32_t)bp.bs;
+      sh = nsh;
+    }
+  }
+  const int need = cnt - below;
+  if (in_bs > CO_BUF) {  // exact ties beyond the buffer: the sorted-insert pass redoes the row
+    if (sl == 0) redo[t] = 1;
+    return;
+  }
+  auto key_class = [&](float d) {
+    if (sh < 0) {
+      const int b = bin_of(d);
+      return b < bs ? 0 : (b == bs ? 1 : 2);
+    }
+    const uint32_t p = __float_as_uint(d) >> sh;
+    return p < pref ? 0 : (p == pref ? 1 : 2);
+  };
+  // ---- pass 2: keys below the boundary selected outright, boundary keys buffered
+  int* out = knn_idx + (size_t)row * K;
+  int n_out = 0, nb = 0;
+  float md = -1.f;  // largest key selected outright (this lane's share)
+  int mj = -1;
+  for (int r = 0; r <= r_knn; ++r) {
+    ring(r, [&](const float4& q, bool ok) {
+      const int j = __float_as_int(q.z);
+      const float d = sqdist(xi, yi, q.x, q.y);
+      const int kc = ok ? key_class(d) : 2;
+      const uint64_t ms = __ballot(kc == 0) & gm;
+      const uint64_t mb = __ballot(kc == 1) & gm;
+      if (kc == 0) {
+        if (key_less(md, mj, d, j)) { md = d; mj = j; }
+        out[n_out + __popcll(ms & lt)] = j;
+        if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
+      } else if (kc == 1) {
+        const int e = nb + __popcll(mb & lt);
+        if (e < CO_BUF) { Bd[e] = __float_as_uint(d); Bj[e] = j; }
+      }
+      n_out += __popcll(ms);
+      nb += __popcll(mb);
+    });
+  }
+  grp_sync();
+  // ---- the need smallest (d, j) boundary keys, by rank (keys are distinct: j is)
+  nb = min(nb, CO_BUF);
+  for (int e = sl; e < nb; e += CL) {
+    const float de = __uint_as_float(Bd[e]);
+    const int je = Bj[e];
+    int rank = 0;
+    for (int e2 = 0; e2 < nb; ++e2) rank += key_less(__uint_as_float(Bd[e2]), Bj[e2], de, je) ? 1 : 0;
+    if (rank < need) {
+      out[n_out + rank] = je;
+      if (je != il) atomicOr(rowbits + (je >> 5), 1u << (je & 31));
+      if (rank == need - 1 && cnt >= kk) kth[row] = make_int2(__float_as_int(de), je);
+    }
+  }
+  // the kk-th key when nothing came from the boundary: the largest key selected outright
+#pragma unroll
+  for (int dd = 1; dd < CL; dd <<= 1) {
+    const float od = __shfl_xor(md, dd, CL);
+    const int oj = __shfl_xor(mj, dd, CL);
+    if (key_less(md, mj, od, oj)) { md = od; mj = oj; }
+  }
+  if (sl == 0) {
+    knn_cnt[row] = cnt;
+    if (cnt < kk) kth[row] = make_int2(0x7f800000, 0x7fffffff);
+    else if (need <= 0) kth[row] = make_int2(__float_as_int(md), mj);
+  }
 }
 
 // column-major copy of the grid (for_ring_rc): transposed cell counts, then points
@@ -858,10 +1156,16 @@ template <int K>
 static void launch_knn(hipStream_t st, const float* px, const float* py, const int* frame_ptr,
                        int n_nodes, int kk, float eps2, int mode, GraphWs& ws, int* ball_degree,
                        int W) {
-  knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
-      ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr, px, py,
-      n_nodes, kk, K, eps2, mode, ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo,
-      ws.kth);
+  if (RG_KNN_COOP && mode == RG_GRAPH_KNN) {
+    knn_select_coop<<<ceil_div(n_nodes, CO_ROWS), KNN_BLOCK, 0, st>>>(
+        ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr,
+        n_nodes, kk, K, eps2, ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo, ws.kth);
+  } else {
+    knn_select<<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
+        ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr, px, py,
+        n_nodes, kk, K, eps2, mode, ws.knn_idx, ws.knn_cnt, ball_degree, ws.bits, W, ws.redo,
+        ws.kth);
+  }
   if (mode == RG_GRAPH_RADIUS) return;
   knn_grid<K><<<ceil_div(n_nodes, KNN_BLOCK), KNN_BLOCK, 0, st>>>(
       ws.pts, ws.cell_start, ws.row_frame, ws.fg, frame_ptr, n_nodes, kk, eps2, mode, ws.knn_idx,
