@@ -588,6 +588,10 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select(
 static constexpr int CL = RG_KNN_CL;             // lanes per row
 static constexpr int CO_ROWS = KNN_BLOCK / CL;   // rows per workgroup
 static constexpr int CO_BUF = 32;                // boundary keys a row may buffer
+#ifndef RG_KNN_CAP
+#define RG_KNN_CAP 128
+#endif
+static constexpr int CO_CAP = RG_KNN_CAP;        // pass-1 keys cached per row for pass 2
 
 __device__ __forceinline__ void grp_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS traffic landed
@@ -642,8 +646,9 @@ __device__ __forceinline__ BinPick grp_find_bin(const uint32_t* H, int sl, int t
 }
 
 // ring r of for_ring_rc, flattened: the group's lanes take candidates sl, sl + CL, ...
-// body(q, ok) runs on every lane of the group (ok = the lane holds a real candidate),
-// so ballots inside it see the whole group; returns the ring's candidate count
+// body(q, ok, o) runs on every lane of the group (ok = the lane holds a real candidate,
+// o = its index in the ring), so ballots inside it see the whole group; returns the
+// ring's candidate count
 template <typename F>
 __device__ __forceinline__ int ring_coop(const FrameGrid& g, const int* __restrict__ cs_r,
                                          const float4* __restrict__ pts_r,
@@ -673,7 +678,7 @@ __device__ __forceinline__ int ring_coop(const FrameGrid& g, const int* __restri
       q[u] = rm ? pts_r[p] : pts_c[p];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) body(q[u], o0 + sl + CL * u < T);
+    for (int u = 0; u < 4; ++u) body(q[u], o0 + sl + CL * u < T, o0 + sl + CL * u);
   }
   return T;
 }
@@ -688,6 +693,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   __shared__ uint32_t hist_s[CO_ROWS][HW];
   __shared__ uint32_t bufd_s[CO_ROWS][CO_BUF];
   __shared__ int bufj_s[CO_ROWS][CO_BUF];
+  __shared__ uint2 cache_s[CO_ROWS][CO_CAP];  // (distance bits, index) of the counted keys
   const int sl = threadIdx.x & (CL - 1), grp = threadIdx.x / CL;
   const int lane = __lane_id();
   const uint64_t gm = ((1ull << CL) - 1ull) << (lane & ~(CL - 1));
@@ -697,6 +703,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   uint32_t* H = hist_s[grp];
   uint32_t* Bd = bufd_s[grp];
   int* Bj = bufj_s[grp];
+  uint2* Ck = cache_s[grp];
   const int f = row_frame[t];
   const FrameGrid g = fg[f];
   const int base = frame_ptr[f];
@@ -723,7 +730,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   bool knn_done = false, ball_done = false;
   for (int r = 0; r <= rmax && !(knn_done && ball_done); ++r) {
     const bool count_knn = !knn_done, count_ball = !ball_done;
-    const int T = ring(r, [&](const float4& q, bool ok) {
+    const int T = ring(r, [&](const float4& q, bool ok, int o) {
       if (!ok) return;
       const int j = __float_as_int(q.z);
       const float d = sqdist(xi, yi, q.x, q.y);
@@ -731,6 +738,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
       if (count_knn) {
         const int bb = bin_of(d);
         atomicAdd(H + (bb >> 1), 1u << ((bb & 1) << 4));
+        if (total + o < CO_CAP) Ck[total + o] = make_uint2(__float_as_uint(d), (uint32_t)j);
       }
     });
     const float bound = ring_bound(g, r);
@@ -760,6 +768,22 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
     bs = bp.bs; below = bp.below; in_bs = bp.in_bs;
   }
   const int cnt = min(kk, total);
+  // the counted keys again: from the LDS cache when they all fit, else the same rings
+  const bool cached = total <= CO_CAP;
+  auto visit = [&](auto&& body) {
+    if (cached) {
+      for (int e0 = 0; e0 < total; e0 += CL) {
+        const int e = e0 + sl;
+        const uint2 kv = Ck[min(e, total - 1)];
+        body(__uint_as_float(kv.x), (int)kv.y, e < total);
+      }
+    } else {
+      for (int r = 0; r <= r_knn; ++r)
+        ring(r, [&](const float4& q, bool ok, int) {
+          body(sqdist(xi, yi, q.x, q.y), __float_as_int(q.z), ok);
+        });
+    }
+  };
   int sh = -1;
   uint32_t pref = 0;
   if (in_bs > CO_BUF && bs > 0 && bs < HB - 1) {
@@ -771,16 +795,13 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
       grp_sync();
       for (int w = sl; w < HW; w += CL) H[w] = 0u;
       grp_sync();
-      for (int r = 0; r <= r_knn; ++r) {
-        ring(r, [&](const float4& q, bool ok) {
-          if (!ok) return;
-          const uint32_t bits = __float_as_uint(sqdist(xi, yi, q.x, q.y));
-          if ((bits >> sh) == pref) {
-            const uint32_t sub = (bits >> nsh) & msk;
-            atomicAdd(H + (sub >> 1), 1u << ((sub & 1) << 4));
-          }
-        });
-      }
+      visit([&](float d, int, bool ok) {
+        const uint32_t bits = __float_as_uint(d);
+        if (ok && (bits >> sh) == pref) {
+          const uint32_t sub = (bits >> nsh) & msk;
+          atomicAdd(H + (sub >> 1), 1u << ((sub & 1) << 4));
+        }
+      });
       grp_sync();
       const BinPick bp = grp_find_bin(H, sl, kk - below);
       below += bp.below;
@@ -807,25 +828,21 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   int n_out = 0, nb = 0;
   float md = -1.f;  // largest key selected outright (this lane's share)
   int mj = -1;
-  for (int r = 0; r <= r_knn; ++r) {
-    ring(r, [&](const float4& q, bool ok) {
-      const int j = __float_as_int(q.z);
-      const float d = sqdist(xi, yi, q.x, q.y);
-      const int kc = ok ? key_class(d) : 2;
-      const uint64_t ms = __ballot(kc == 0) & gm;
-      const uint64_t mb = __ballot(kc == 1) & gm;
-      if (kc == 0) {
-        if (key_less(md, mj, d, j)) { md = d; mj = j; }
-        out[n_out + __popcll(ms & lt)] = j;
-        if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
-      } else if (kc == 1) {
-        const int e = nb + __popcll(mb & lt);
-        if (e < CO_BUF) { Bd[e] = __float_as_uint(d); Bj[e] = j; }
-      }
-      n_out += __popcll(ms);
-      nb += __popcll(mb);
-    });
-  }
+  visit([&](float d, int j, bool ok) {
+    const int kc = ok ? key_class(d) : 2;
+    const uint64_t ms = __ballot(kc == 0) & gm;
+    const uint64_t mb = __ballot(kc == 1) & gm;
+    if (kc == 0) {
+      if (key_less(md, mj, d, j)) { md = d; mj = j; }
+      out[n_out + __popcll(ms & lt)] = j;
+      if (j != il) atomicOr(rowbits + (j >> 5), 1u << (j & 31));
+    } else if (kc == 1) {
+      const int e = nb + __popcll(mb & lt);
+      if (e < CO_BUF) { Bd[e] = __float_as_uint(d); Bj[e] = j; }
+    }
+    n_out += __popcll(ms);
+    nb += __popcll(mb);
+  });
   grp_sync();
   // ---- the need smallest (d, j) boundary keys, by rank (keys are distinct: j is)
   nb = min(nb, CO_BUF);

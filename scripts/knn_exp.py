@@ -8,10 +8,11 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 EXPS = {'thread': ['RG_KNN_COOP=0'], 'cl16': ['RG_KNN_CL=16'], 'cl8': ['RG_KNN_CL=8'],
-        'cl32': ['RG_KNN_CL=32'], 'histonly': ['RG_KNN_COOP=0', 'RG_KNN_EXP=2']}
+        'cl32': ['RG_KNN_CL=32'], 'cap64': ['RG_KNN_CAP=64'], 'cap128': ['RG_KNN_CAP=128'],
+        'cap192': ['RG_KNN_CAP=192'], 'histonly': ['RG_KNN_COOP=0', 'RG_KNN_EXP=2']}
 
 
-def time_one(frames=64, nodes=3000, k=32):
+def time_one(frames=64, nodes=3000, k=int(os.environ.get('RG_EXP_K', 32))):
     import numpy as np
     import torch
     from graph_neural_network_for_radar_perception_amd import engine, synthetic
@@ -25,7 +26,8 @@ def time_one(frames=64, nodes=3000, k=32):
     for it in range(25):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        engine.build_graph(px, py, fptr, [nodes] * frames, k, 25.0, ws_cache=cache)
+        engine.build_graph(px, py, fptr, [nodes] * frames, k, float(os.environ.get('RG_EXP_EPS2', 25.0)),
+                           ws_cache=cache)
         b.record()
         torch.cuda.synchronize()
         if it >= 5:
