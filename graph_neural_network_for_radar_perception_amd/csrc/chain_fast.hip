@@ -114,7 +114,7 @@ struct Input {
   static constexpr int KS = (K0 + 15) / 16;
 
   static __device__ __forceinline__ void load(const FArgs& a, long row, bool valid, int h,
-                                              bf16x8_t (&b)[KS]) {
+                                              bf16x8_t (&b)[KS], float pre = 1.f) {
     if (!valid) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) b[s] = zero_bf8();
@@ -128,7 +128,7 @@ struct Input {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int f = 16 * s + 8 * h + j;
-          v[j] = f < a.w0real ? p[f] : 0.f;
+          v[j] = f < a.w0real ? p[f] * pre : 0.f;
         }
         b[s] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0], v[1]), bf2(v[2], v[3]),
                                                     bf2(v[4], v[5]), bf2(v[6], v[7])});
@@ -209,6 +209,7 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
 __host__ __device__ constexpr int fast_bytes(int K, int N) {
   return (N / 32) * ((K + 15) / 16) * 1024 + N * 4;
 }
+template <int N, int... Rest> struct FirstOf { static constexpr int value = N; };
 template <int K, int... Ns> struct Offsets;
 template <int K> struct Offsets<K> {
   static constexpr int get(int) { return 0; }
@@ -336,6 +337,15 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
   }
 }
 
+// A tile-fused first layer with a compile-time LeakyReLU runs on PRESCALED operands:
+// the kernel multiplies its float32 inputs and its staged bias by 0.505 (LEAKY_PRE), so
+// the accumulator holds y' = 0.505 y and leaky(y) = 0.505 y + 0.495 |y| = y' + c |y'| is
+// ONE fma with a free |.| source modifier instead of a multiply and a max (the encoders
+// apply it to 256 features per row).
+constexpr bool pre_scaled_l0(int spec_) {
+  return spec_ >= 0 && ((spec_ >> 16) & 1) != 0 && (spec_ & 0xff) == ACT_LEAKY;
+}
+
 // Layers 0 and 1 fused tile by tile, for a first layer WITHOUT normalisation (the
 // encoders' first ffn_block, gnn_blocks.py:31): each 32-wide output tile of layer 0 is
 // activated, packed to bf16 and consumed at once as layer 1's k-steps 2m0, 2m0+1, so
@@ -347,6 +357,7 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
                                             bool valid, int lane) {
   constexpr int KS0 = (K0 + 15) / 16, MT0 = N0 / 32, KS1 = N0 / 16, MT1 = N1 / 32;
   constexpr int OFF1 = (fast_bytes(K0, N0) + 15) & ~15;
+  constexpr bool PRE0 = pre_scaled_l0(SPEC);
   constexpr int OFF2 = OFF1 + ((fast_bytes(N0, N1) + 15) & ~15);
   static_assert(N0 % 32 == 0 && N1 % 32 == 0, "padded widths are multiples of 32");
   const int h = lane >> 5;
@@ -370,7 +381,14 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
     for (int hf = 0; hf < 2; ++hf) {
       f32x2 v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = act_pk<decltype(A)::value>(pair(t, 4 * hf + j));
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (PRE0) {  // prescaled layer 0: leaky(y) = y' + c |y'|, one fma each
+          const f32x2 y = pair(t, 4 * hf + j);
+          v[j] = (f32x2){fmaf(fabsf(y.x), LEAKY_C, y.x), fmaf(fabsf(y.y), LEAKY_C, y.y)};
+        } else {
+          v[j] = act_pk<decltype(A)::value>(pair(t, 4 * hf + j));
+        }
+      }
       nb[hf] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0].x, v[0].y), bf2(v[1].x, v[1].y),
                                                     bf2(v[2].x, v[2].y), bf2(v[3].x, v[3].y)});
     }
@@ -456,6 +474,13 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     }
   }
   __syncthreads();
+  constexpr bool PRE0 = (MODE & FUSE01) != 0 && pre_scaled_l0(SPEC);
+  if constexpr (PRE0) {  // layer 0's bias, scaled like its inputs (run_chain01)
+    constexpr int N0 = FirstOf<Ns...>::value;
+    float* b0 = (float*)(lds + (N0 / 32) * In::KS * 1024);
+    for (int i = threadIdx.x; i < N0; i += FT) b0[i] *= LEAKY_PRE;
+    __syncthreads();
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
   const long ntiles = (rows + 31) / 32;
@@ -487,6 +512,10 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     fetch(tile, nx);
     for (; tile < ntiles; tile += tstride) {
       bf16x8_t b[1];
+      if constexpr (PRE0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nx[j] *= LEAKY_PRE;
+      }
       b[0] = __builtin_bit_cast(bf16x8_t, (u32x4){bf2(nx[0], nx[1]), bf2(nx[2], nx[3]),
                                                   bf2(nx[4], nx[5]), bf2(nx[6], nx[7])});
       fetch(tile + tstride, nx);
@@ -498,7 +527,7 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
       const long row = tile * 32 + (lane & 31);
       const bool valid = row < rows;
       bf16x8_t b[In::KS];
-      In::load(a, row, valid, lane >> 5, b);
+      In::load(a, row, valid, lane >> 5, b, PRE0 ? LEAKY_PRE : 1.f);
       run(b, row, valid);
     }
   }
