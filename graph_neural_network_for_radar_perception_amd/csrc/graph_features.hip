@@ -71,25 +71,46 @@ __global__ __launch_bounds__(256) void node_features_kernel(
 // One thread per edge (src -> dst).  graph_features.py:153-161 in float32
 // (dx/10, dl = sqrt(dx^2+dy^2)/10, ...) and dt = float64(t_s - t_d) * 1e-6,
 // all cast to float32 as the tensorization does (datagen_gnn.py:121).
+// x / 10 correctly rounded to f32 without a division: x = M 2^E (24-bit M), so x / 10
+// is either exactly representable or at least 2^-27 (relative) away from every f32
+// rounding midpoint (the distance is 2^(e-1) |M 2^j - 10 (2k+1)| / 10 with a nonzero
+// integer numerator), while the f64 product x * 0.1 is within 2^-52 of x / 10: rounding
+// it to f32 gives the correctly rounded quotient (numpy's float32 x / 10) for every x.
+__device__ __forceinline__ float div10_rn(float x) { return (float)((double)x * 0.1); }
+
 __global__ __launch_bounds__(256) void edge_features_kernel(
     const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vx,
     const float* __restrict__ vy, const int64_t* __restrict__ ts, const int* __restrict__ src,
     const int* __restrict__ dst, const int* __restrict__ n_edges_dev, long n_edges,
     float* __restrict__ out) {
-  const long E = n_edges_dev ? (long)*n_edges_dev : n_edges;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < E && p < n_edges; p += stride) {
-    const int s = src[p];
-    const int d = dst[p];
-    const float dx = div_rn((px[s] - px[d]), 10.f);
-    const float dy = div_rn((py[s] - py[d]), 10.f);
-    const float dl = div_rn(sqrt_rn(((dx * dx) + (dy * dy))), 10.f);
-    const float dvx = (vx[s] - vx[d]);
-    const float dvy = (vy[s] - vy[d]);
-    const float dv = sqrt_rn(((dvx * dvx) + (dvy * dvy)));
-    const float dt = (float)((double)(ts[s] - ts[d]) * 1e-6);
-    float* o = out + (size_t)p * 7;
-    o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;
+  // rows of 7 floats (28 B) written per lane would touch every cache line of the block's
+  // output seven times with partial writes: the block stages its 256 x 7 values in LDS
+  // (stride 7 words: conflict-free) and writes them back as contiguous 16-B vectors
+  __shared__ float4 stage4[256 * 7 / 4];
+  float* stage = (float*)stage4;
+  const long E = min(n_edges_dev ? (long)*n_edges_dev : n_edges, n_edges);
+  for (long b0 = (long)blockIdx.x * 256; b0 < E; b0 += (long)gridDim.x * 256) {
+    const long p = b0 + threadIdx.x;
+    if (p < E) {
+      const int s = src[p];
+      const int d = dst[p];
+      const float dx = div10_rn((px[s] - px[d]));
+      const float dy = div10_rn((py[s] - py[d]));
+      const float dl = div10_rn(sqrt_rn(((dx * dx) + (dy * dy))));
+      const float dvx = (vx[s] - vx[d]);
+      const float dvy = (vy[s] - vy[d]);
+      const float dv = sqrt_rn(((dvx * dvx) + (dvy * dvy)));
+      const float dt = (float)((double)(ts[s] - ts[d]) * 1e-6);
+      float* o = stage + threadIdx.x * 7;
+      o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;
+    }
+    __syncthreads();
+    const int n = (int)min(256L, E - b0) * 7;  // floats of this block; b0 * 7 * 4 B is 16-B aligned
+    const int n4 = ((uintptr_t)out & 15) == 0 ? n / 4 : 0;  // a caller's unaligned view: dwords
+    float4* o4 = (float4*)(out + (size_t)b0 * 7);
+    for (int i = threadIdx.x; i < n4; i += 256) o4[i] = stage4[i];
+    for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) out[(size_t)b0 * 7 + i] = stage[i];
+    __syncthreads();
   }
 }
 

@@ -65,10 +65,13 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// Correctly rounded f32 sqrt / division (numpy semantics).  The hardware f32
-// v_sqrt / v_rcp paths are not correctly rounded; the f64 result rounded once
-// to f32 is (53 >= 2*24 + 2 bits, so the double rounding is exact).
-__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
+// Correctly rounded f32 sqrt / division (numpy semantics).  The bare v_sqrt_f32 /
+// v_rcp_f32 (and __fsqrt_rn, which is v_sqrt_f32 with denormal scaling) are not
+// correctly rounded.  sqrtf compiles (HIP's default correctly rounded f32 sqrt) to
+// v_sqrt_f32 plus the exact two-neighbour fma residual fix-up, ~14 f32 instructions;
+// the division goes through f64: the f64 quotient rounded once to f32 is exact (53 >=
+// 2*24 + 2 bits, so the double rounding cannot differ).
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrtf(x); }
 __device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 
 // dynamic LDS a kernel may request: 160 KiB per CU minus room for the few static
