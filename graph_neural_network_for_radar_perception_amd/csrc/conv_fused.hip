@@ -448,6 +448,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     e0 = ne0;
     e1 = ne1;
   }
+  // the last workgroup out re-zeroes the block counter for the next launch (no memset
+  // per layer: each cost a ~10 us stream gap).  Every wave's final counter atomic has
+  // returned before its workgroup reaches the barrier, so when `done` reaches the grid
+  // size no workgroup can touch the counter again.
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(a.counter + 1, 1) == (int)gridDim.x - 1) {
+      atomicExch(a.counter, 0);
+      atomicExch(a.counter + 1, 0);
+    }
+  }
 }
 
 }  // namespace conv
@@ -501,7 +512,7 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   a.src = src;
   a.dst = dst;
   a.x_out = (uint16_t*)x_out;
-  a.counter = (int*)workspace;
+  a.counter = (int*)workspace;  // [0] next block, [1] workgroups done: zero between launches
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
   if (n_nodes <= 0) return RG_OK;
   const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
@@ -517,7 +528,6 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
                                      DYN_LDS_MAX));
     attr[leaky] = true;
   }
-  RG_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(int), st));
   int blocks = 256;
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
   kern<<<blocks, CT, lds, st>>>(a);

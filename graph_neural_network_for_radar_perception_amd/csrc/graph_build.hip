@@ -67,6 +67,30 @@ struct FrameGrid {
   int gw, gh, cell0, n;
 };
 
+// the build's first kernel: row frames (row_frame_base's work) and every zero the build
+// needs -- redo flags, cell counts, both scatter cursors -- in one launch instead of a
+// memset / copy each (each cost a ~10 us stream gap)
+__global__ void build_init(const int* __restrict__ frame_ptr, int n_frames,
+                           int* __restrict__ row_base, int* __restrict__ row_frame, int n_nodes,
+                           int* __restrict__ redo, long n_cells, int* __restrict__ cell_cnt,
+                           int* __restrict__ cursor, int* __restrict__ cursor_t) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_cells) {
+    cell_cnt[i] = 0;
+    cursor[i] = 0;
+    cursor_t[i] = 0;
+  }
+  if (i >= n_nodes) return;
+  int lo = 0, hi = n_frames;  // frame_ptr[lo] <= i < frame_ptr[hi]
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (frame_ptr[mid] <= i) lo = mid; else hi = mid;
+  }
+  row_base[i] = frame_ptr[lo];
+  row_frame[i] = lo;
+  redo[i] = 0;
+}
+
 // frame id and frame base of every global row (disjoint-union batch)
 __global__ void row_frame_base(const int* __restrict__ frame_ptr, int n_frames,
                                int* __restrict__ row_base, int* __restrict__ row_frame,
@@ -161,11 +185,13 @@ __global__ void grid_count(const float* __restrict__ px, const float* __restrict
 // depends on atomic arrival and does not matter: every consumer compares full keys.
 __global__ void grid_scatter(const float* __restrict__ px, const float* __restrict__ py,
                              const int* __restrict__ row_base, const int* __restrict__ cell_of,
-                             int n_nodes, int* __restrict__ cursor, float4* __restrict__ pts) {
+                             int n_nodes, int* __restrict__ cursor, float4* __restrict__ pts,
+                             const int* __restrict__ base = nullptr) {
+  // position = base[c] + arrival (cursor zeroed), or cursor pre-set to the cell starts
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_nodes) return;
   const int c = cell_of[i];
-  const int pos = atomicAdd(cursor + c, 1);
+  const int pos = (base ? base[c] : 0) + atomicAdd(cursor + c, 1);
   pts[pos] = make_float4(px[i], py[i], __int_as_float(i - row_base[i]), __int_as_float(c));
 }
 
@@ -714,6 +740,11 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   const int cx = cme % g.gw, cy = cme / g.gw;
   const int row = base + il;
   uint32_t* rowbits = bits + (size_t)row * W;
+  // this row's bitset words are zeroed here (no memset of the whole N x W bitset): only
+  // this row's selection writes the row before knn_mark; the release fence orders the
+  // zeros before every later atomicOr of the group
+  for (int w = sl; w < W; w += CL) rowbits[w] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   auto ring = [&](int r, auto&& body) {
     return ring_coop(g, cell_start, pts, cell_start_t, pts_t, cx, cy, r, sl, body);
   };
@@ -893,13 +924,13 @@ __global__ void grid_scatter_t(const float* __restrict__ px, const float* __rest
                                const int* __restrict__ row_base, const int* __restrict__ row_frame,
                                const FrameGrid* __restrict__ fg, const int* __restrict__ cell_of,
                                int n_nodes, int* __restrict__ cursor,
-                               float4* __restrict__ pts_t) {
+                               float4* __restrict__ pts_t, const int* __restrict__ base) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_nodes) return;
   const FrameGrid g = fg[row_frame[i]];
   const int cr = cell_of[i] - g.cell0;
   const int ct = g.cell0 + (cr % g.gw) * g.gh + cr / g.gw;
-  const int pos = atomicAdd(cursor + ct, 1);
+  const int pos = base[ct] + atomicAdd(cursor + ct, 1);
   pts_t[pos] = make_float4(px[i], py[i], __int_as_float(i - row_base[i]), __int_as_float(ct));
 }
 
@@ -1098,6 +1129,7 @@ struct GraphWs {
   int* cell_cnt_t;     // column-major copy of the grid (for_ring_rc)
   int* cell_start_t;
   float4* pts_t;
+  int* cursor_t;       // arrival counters of the column-major scatter
   int cpf;
   long n_cells;
 };
@@ -1137,7 +1169,9 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
   char* p_ct = take((size_t)n_cells * sizeof(int));
   char* p_st = take((size_t)(n_cells + 1) * sizeof(int));
   char* p_pq = take((size_t)n_nodes * sizeof(float4));
+  char* p_cv = take((size_t)n_cells * sizeof(int));
   if (ws) {
+    ws->cursor_t = (int*)p_cv;
     ws->kth = (int2*)p_kt;
     ws->cell_cnt_t = (int*)p_ct;
     ws->cell_start_t = (int*)p_st;
@@ -1213,23 +1247,23 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
     return RG_OK;
   }
   const int W = (max_frame_nodes + 31) / 32;
-  RG_CHECK_HIP(hipMemsetAsync(ws.bits, 0, (size_t)n_nodes * W * sizeof(uint32_t), st));
-  row_frame_base<<<ceil_div(n_nodes, 256), 256, 0, st>>>(frame_ptr, n_frames, ws.row_base,
-                                                         ws.row_frame, n_nodes);
+  // the cooperative selection zeroes its own bitset rows
+  if (!(RG_KNN_COOP && mode == RG_GRAPH_KNN))
+    RG_CHECK_HIP(hipMemsetAsync(ws.bits, 0, (size_t)n_nodes * W * sizeof(uint32_t), st));
+  build_init<<<ceil_div(max((long)n_nodes, ws.n_cells), 256), 256, 0, st>>>(
+      frame_ptr, n_frames, ws.row_base, ws.row_frame, n_nodes, ws.redo, ws.n_cells, ws.cell_cnt,
+      ws.cursor, ws.cursor_t);
   // bucket every frame's points into its grid (cell order = frame order, so the scan of
   // all cells gives absolute positions inside each frame's row range)
   grid_setup<<<n_frames, 256, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
-  RG_CHECK_HIP(hipMemsetAsync(ws.cell_cnt, 0, (size_t)ws.n_cells * sizeof(int), st));
   grid_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_frame, ws.fg, n_nodes,
                                                      ws.cell_of, ws.cell_cnt);
   RG_LAUNCH_CHECK();
   int rc0 = exclusive_scan(ws.cell_cnt, ws.n_cells, ws.cell_start, ws.cell_start + ws.n_cells,
                            ws.scan_ws, st);
   if (rc0) return rc0;
-  RG_CHECK_HIP(hipMemcpyAsync(ws.cursor, ws.cell_start, (size_t)ws.n_cells * sizeof(int),
-                              hipMemcpyDeviceToDevice, st));
   grid_scatter<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.cell_of, n_nodes,
-                                                       ws.cursor, ws.pts);
+                                                       ws.cursor, ws.pts, ws.cell_start);
   RG_LAUNCH_CHECK();
   // the column-major copy of the same grid
   grid_transpose_counts<<<ceil_div(ws.n_cells, 256), 256, 0, st>>>(ws.fg, ws.cpf, ws.n_cells,
@@ -1238,12 +1272,10 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   rc0 = exclusive_scan(ws.cell_cnt_t, ws.n_cells, ws.cell_start_t, ws.cell_start_t + ws.n_cells,
                        ws.scan_ws, st);
   if (rc0) return rc0;
-  RG_CHECK_HIP(hipMemcpyAsync(ws.cursor, ws.cell_start_t, (size_t)ws.n_cells * sizeof(int),
-                              hipMemcpyDeviceToDevice, st));
   grid_scatter_t<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_base, ws.row_frame, ws.fg,
-                                                         ws.cell_of, n_nodes, ws.cursor, ws.pts_t);
+                                                         ws.cell_of, n_nodes, ws.cursor_t, ws.pts_t,
+                                                         ws.cell_start_t);
   RG_LAUNCH_CHECK();
-  RG_CHECK_HIP(hipMemsetAsync(ws.redo, 0, (size_t)n_nodes * sizeof(int), st));
   switch (K) {
     case 1: launch_knn<1>(st, px, py, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
     case 2: launch_knn<2>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;

@@ -332,7 +332,7 @@ def build_graph(px, py, frame_ptr: torch.Tensor, frame_sizes: List[int], k: int,
     row_ptr = torch.empty(n + 1, **i32)
     col = torch.empty(edge_capacity, **i32)
     deg = torch.empty(max(n, 1), **i32)
-    ne = torch.zeros(1, **i32)
+    ne = torch.empty(1, **i32)  # written by the build's scan (or its n_nodes == 0 path)
     nat.check(lib.rg_build_graph(px.data_ptr(), py.data_ptr(), frame_ptr.data_ptr(), n, nf, maxn,
                                  int(k), float(eps2), mode, row_ptr.data_ptr(), col.data_ptr(),
                                  edge_capacity, deg.data_ptr(), ne.data_ptr(), ws.data_ptr(),
@@ -353,7 +353,7 @@ def graph_from_csr(row_ptr, col, n_nodes, n_edges_dev, edge_capacity, ws_cache=N
     ps = torch.empty(ucap, **i32)
     pd = torch.empty(ucap, **i32)
     pptr = torch.empty(n_nodes + 1, **i32)
-    npairs = torch.zeros(1, **i32)
+    npairs = torch.empty(1, **i32)  # written by rg_link_pairs (scan total / n_nodes == 0)
     ws = torch.empty(lib.rg_link_pairs_workspace_size(n_nodes), dtype=torch.uint8, device=dev)
     nat.check(lib.rg_link_pairs(row_ptr.data_ptr(), col.data_ptr(), n_nodes, pptr.data_ptr(),
                                 ps.data_ptr(), pd.data_ptr(), ucap, npairs.data_ptr(),

@@ -231,7 +231,8 @@ int rg_mlp_chain_fast(const rg_layer* layers_host, int n_layers, long rows, cons
  * the same order.  msg_layers[0] packed RG_PACK_FAST_IN, msg_layers[1]
  * RG_PACK_FAST_CHAIN, upd_layer RG_PACK_FAST_UPD.  Returns RG_ERR_UNSUPPORTED for
  * other shapes / aggregations (use rg_mlp_chain + rg_segment_reduce).
- * workspace: rg_conv_layer_workspace_size() bytes (work counter, reset per call). */
+ * workspace: rg_conv_layer_workspace_size() bytes, ZEROED before the first call (block
+ * counters; every completed launch leaves them zero again, so no per-call memset). */
 size_t rg_conv_layer_workspace_size(void);
 int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
                         const void* x, int ldx, const void* e, int lde, const int* seg_ptr,
