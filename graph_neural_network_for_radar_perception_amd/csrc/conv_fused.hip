@@ -28,7 +28,8 @@
 
 #ifndef RG_CONV_EXP
 #define RG_CONV_EXP 0  // timing experiments only (wrong results): 1 no row gathers after the
-                       // first tile, 2 no message norm/act, 3 no transpose/aggregation
+                       // first tile, 2 no message norm/act, 3 no transpose/aggregation,
+                       // 4 accumulators start from zero instead of P (no LDS reads)
 #endif
 
 namespace rg {
@@ -93,13 +94,17 @@ __device__ __forceinline__ bf16x8_t zero_bf8() {
 #define RG_CONV_PFD 1  // A-fragment prefetch distance (k-steps) for layers with MT <= 2
 #endif
 
+#ifndef RG_CONV_PFD4
+#define RG_CONV_PFD4 1  // the same for the 4-tile first message layer
+#endif
+
 template <int KS, int MT, int KT, int S0>
 __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
                                            int lane) {
   const char* wl = w + lane * 16;
   // narrow layers (MT <= 2) issue only MT MFMAs per k-step, less than an LDS round trip:
   // their fragments are read PD steps ahead (registers: (PD + 1) * MT fragments)
-  constexpr int PD = MT <= 2 ? RG_CONV_PFD : 1;
+  constexpr int PD = MT <= 2 ? RG_CONV_PFD : RG_CONV_PFD4;
   bf16x8_t f[KS][MT];
 #pragma unroll
   for (int s = 0; s < PD && s < KS; ++s)
@@ -254,7 +259,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       const bool valid = t0 + r < e1;
       f32x16 acc1[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) acc1[m] = ld_bias_frag(P + slot * HID, m, h);
+      for (int m = 0; m < 4; ++m)
+        acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * HID, m, h);
       mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
       if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
       bf16x8_t b2[8];
