@@ -98,6 +98,10 @@ _SIGNATURES = {
     'rg_conv_layer_workspace_size': (_S, []),
     'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,
                                  _P, _I, _P, _P, _P, _I, _P, _I, _P, _P]),
+    'rg_conv_layer_fused_blocks': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I,
+                                        _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
+    'rg_conv_blocks_workspace_size': (_S, [_I]),
+    'rg_conv_blocks': (_I, [_P, _I, _P, _P, _P, _S, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
     'rg_segment_reduce_ranges_workspace_size': (_S, [_L, _I, _I]),
     'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P, _S,

@@ -25,6 +25,7 @@
 // Workgroups (8 waves, 2 per SIMD) are persistent and pull node blocks from an
 // atomic counter; all weights (81 KiB packed bf16 + biases) sit in LDS.
 #include "rg_common.h"
+#include "scan.h"
 
 #ifndef RG_CONV_EXP
 #define RG_CONV_EXP 0  // timing experiments only (wrong results): 1 no row gathers after the
@@ -75,6 +76,10 @@ struct CArgs {
   uint16_t* x_out;
   int* counter;
   int ldx, lde, ldo;
+  // optional edge-balanced work blocks (rg_conv_blocks): block b = nodes
+  // [blk_nodes[b], blk_nodes[b + 1]), at most NB, *n_blk_dev blocks; null: b = 8-node run
+  const int* blk_nodes;
+  const int* n_blk_dev;
 };
 
 __device__ __forceinline__ uint32_t bf2(float a, float b) { return pack_bf16x2(a, b); }
@@ -206,28 +211,39 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // block ids come from an atomic counter (dynamic balance); the NEXT block's id and
   // edge range are fetched at the start of the current block, so a block starts with
   // two dependent global round trips (indices -> rows) instead of four
+  const int n_blocks = a.blk_nodes ? *a.n_blk_dev : a.n_blocks;
+  // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
+  auto block_nodes = [&](int b, int& n0, int& n1) {
+    if (a.blk_nodes) {
+      n0 = a.blk_nodes[b];
+      n1 = a.blk_nodes[b + 1];
+    } else {
+      n0 = b * NB;
+      n1 = min(n0 + NB, a.n_nodes);
+    }
+  };
   int blk = 0;
   if (lane == 0) blk = atomicAdd(a.counter, 1);
   blk = __shfl(blk, 0, 64);
-  int e0 = 0, e1 = 0;
-  if (blk < a.n_blocks) {
-    e0 = a.seg_ptr[blk * NB];
-    e1 = a.seg_ptr[min(blk * NB + NB, a.n_nodes)];
+  int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
+  if (blk < n_blocks) {
+    block_nodes(blk, bn0, bn1);
+    e0 = a.seg_ptr[bn0];
+    e1 = a.seg_ptr[bn1];
   }
 #if RG_CONV_PFX
   // x rows of the block's nodes for P, loaded one block ahead (the block start otherwise
   // waits a full global round trip before its first MFMA)
   bf16x8_t bxn[4];
   {
-    const int nb0 = min(blk, a.n_blocks - 1) * NB;
-    const uint16_t* px = a.x + (size_t)min(nb0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+    const uint16_t* px = a.x + (size_t)min(bn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
 #pragma unroll
     for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
   }
 #endif
-  while (blk < a.n_blocks) {
-    const int n0 = blk * NB;
-    const int n1 = min(n0 + NB, a.n_nodes);
+  while (blk < n_blocks) {
+    const int n0 = bn0;
+    const int n1 = bn1;
     int nxt_raw = 0;
     if (lane == 0) nxt_raw = atomicAdd(a.counter, 1);
     f32x16 agg[2];
@@ -368,15 +384,15 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     }
 
     const int nxt = __shfl(nxt_raw, 0, 64);
-    int ne0 = 0, ne1 = 0;
-    if (nxt < a.n_blocks) {
-      ne0 = a.seg_ptr[nxt * NB];
-      ne1 = a.seg_ptr[min(nxt * NB + NB, a.n_nodes)];
+    int ne0 = 0, ne1 = 0, nn0 = 0, nn1 = 0;
+    if (nxt < n_blocks) {
+      block_nodes(nxt, nn0, nn1);
+      ne0 = a.seg_ptr[nn0];
+      ne1 = a.seg_ptr[nn1];
     }
 #if RG_CONV_PFX
     {
-      const int nb0 = min(nxt, a.n_blocks - 1) * NB;  // clamped: always a valid row
-      const uint16_t* px = a.x + (size_t)min(nb0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+      const uint16_t* px = a.x + (size_t)min(nn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
 #pragma unroll
       for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
     }
@@ -453,6 +469,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     blk = nxt;
     e0 = ne0;
     e1 = ne1;
+    bn0 = nn0;
+    bn1 = nn1;
   }
   // the last workgroup out re-zeroes the block counter for the next launch (no memset
   // per layer: each cost a ~10 us stream gap).  Every wave's final counter atomic has
@@ -467,19 +485,82 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   }
 }
 
+// Edge-balanced work blocks: each run of NB nodes is split at node boundaries wherever
+// its running edge count would pass `cap` (a single node is never split), so no work
+// block holds many more edges than the mean share of a wave.  cap = max(CAP_MIN, E / 4096)
+// (4096 = two blocks per wave of the 256 x 8-wave grid): a 20 000-node radius frame
+// (~160 edges per 8 nodes, hubs of ~100) is cut to ~4-tile blocks, while a C2 batch
+// (~300 edges per 8 nodes, cap 1 778) keeps its 8-node runs.
+static constexpr int CAP_MIN = 128;
+
+__device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes) {
+  return max(CAP_MIN, seg_ptr[n_nodes] / 4096);
+}
+
+template <bool EMIT>
+__global__ void conv_blocks_kernel(const int* __restrict__ seg_ptr, int n_nodes,
+                                   int* __restrict__ cnt, const int* __restrict__ off,
+                                   int* __restrict__ blk_nodes) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb8 = (n_nodes + NB - 1) / NB;
+  if (b >= nb8) return;
+  const int cap = block_cap(seg_ptr, n_nodes);
+  const int n0 = b * NB, n1 = min(n0 + NB, n_nodes);
+  int c = 0, acc = 0, o = EMIT ? off[b] : 0;
+  for (int n = n0; n < n1; ++n) {
+    const int d = seg_ptr[n + 1] - seg_ptr[n];
+    if (n == n0 || (acc > 0 && acc + d > cap)) {
+      if (EMIT) blk_nodes[o + c] = n;
+      ++c;
+      acc = 0;
+    }
+    acc += d;
+  }
+  if (!EMIT) cnt[b] = c;
+  if (EMIT && b == nb8 - 1) blk_nodes[o + c] = n_nodes;  // sentinel
+}
+
 }  // namespace conv
 }  // namespace rg
 
 using namespace rg;
 using namespace rg::conv;
 
+extern "C" size_t rg_conv_blocks_workspace_size(int n_nodes) {
+  const long nb8 = ((long)n_nodes + NB - 1) / NB;
+  return 2 * ((size_t)((nb8 + 1) * sizeof(int) + 255) / 256 * 256) + scan_workspace_bytes(nb8);
+}
+
+extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(n_nodes >= 1, RG_ERR_ARG, "rg_conv_blocks: n_nodes must be >= 1");
+  RG_REQUIRE(workspace_bytes >= rg_conv_blocks_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_conv_blocks: workspace too small");
+  const int nb8 = (n_nodes + NB - 1) / NB;
+  const size_t arr = ((size_t)(nb8 + 1) * sizeof(int) + 255) / 256 * 256;
+  int* cnt = (int*)workspace;                 // sub-blocks per 8-node run
+  int* off = (int*)((char*)workspace + arr);  // their exclusive scan
+  void* sws = (char*)workspace + 2 * arr;
+  conv_blocks_kernel<false><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, cnt, nullptr,
+                                                                nullptr);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(cnt, nb8, off, n_blocks, sws, st);
+  if (rc) return rc;
+  conv_blocks_kernel<true><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, nullptr, off,
+                                                               blk_nodes);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" size_t rg_conv_layer_workspace_size(void) { return 256; }
 
-extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
-                                   const void* x, int ldx, const void* e, int lde,
-                                   const int* seg_ptr, const int* src, const int* dst,
-                                   int n_nodes, void* x_out, int ld_out, void* workspace,
-                                   void* stream) {
+extern "C" int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_layer,
+                                          int aggr, const void* x, int ldx, const void* e,
+                                          int lde, const int* seg_ptr, const int* src,
+                                          const int* dst, int n_nodes, void* x_out, int ld_out,
+                                          const int* blk_nodes, const int* n_blocks_dev,
+                                          void* workspace, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const rg_layer& m0 = msg_layers[0];
   const rg_layer& m1 = msg_layers[1];
@@ -520,6 +601,10 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
   a.x_out = (uint16_t*)x_out;
   a.counter = (int*)workspace;  // [0] next block, [1] workgroups done: zero between launches
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
+  RG_REQUIRE((blk_nodes == nullptr) == (n_blocks_dev == nullptr), RG_ERR_ARG,
+             "rg_conv_layer_fused_blocks: block table and count go together");
+  a.blk_nodes = blk_nodes;
+  a.n_blk_dev = n_blocks_dev;
   if (n_nodes <= 0) return RG_OK;
   const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
   RG_REQUIRE(lds <= DYN_LDS_MAX, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
@@ -534,9 +619,19 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
                                      DYN_LDS_MAX));
     attr[leaky] = true;
   }
-  int blocks = 256;
+  int blocks = 256;  // a block table has at least ceil(N / NB) entries
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
   kern<<<blocks, CT, lds, st>>>(a);
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
+                                   const void* x, int ldx, const void* e, int lde,
+                                   const int* seg_ptr, const int* src, const int* dst,
+                                   int n_nodes, void* x_out, int ld_out, void* workspace,
+                                   void* stream) {
+  return rg_conv_layer_fused_blocks(msg_layers, upd_layer, aggr, x, ldx, e, lde, seg_ptr, src,
+                                    dst, n_nodes, x_out, ld_out, nullptr, nullptr, workspace,
+                                    stream);
 }

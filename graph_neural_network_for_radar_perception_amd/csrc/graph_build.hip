@@ -107,15 +107,16 @@ __global__ void row_frame_base(const int* __restrict__ frame_ptr, int n_frames,
 }
 
 // one block per frame: bounding box -> cell size and grid shape (<= cpf cells)
-__global__ __launch_bounds__(256) void grid_setup(const float* __restrict__ px,
-                                                  const float* __restrict__ py,
-                                                  const int* __restrict__ frame_ptr, int cpf,
-                                                  FrameGrid* __restrict__ fg) {
-  __shared__ float r[4][256];
+static constexpr int GS_T = 1024;  // a 20 000-point frame is 20 loads per thread
+__global__ __launch_bounds__(GS_T) void grid_setup(const float* __restrict__ px,
+                                                   const float* __restrict__ py,
+                                                   const int* __restrict__ frame_ptr, int cpf,
+                                                   FrameGrid* __restrict__ fg) {
+  __shared__ float r[4][GS_T];
   const int f = blockIdx.x;
   const int b = frame_ptr[f], e = frame_ptr[f + 1];
   float x0 = __int_as_float(0x7f800000), y0 = x0, x1 = -x0, y1 = -x0;
-  for (int i = b + threadIdx.x; i < e; i += 256) {
+  for (int i = b + threadIdx.x; i < e; i += GS_T) {
     const float x = px[i], y = py[i];
     x0 = fminf(x0, x); x1 = fmaxf(x1, x);
     y0 = fminf(y0, y); y1 = fmaxf(y1, y);
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(256) void grid_setup(const float* __restrict__ px,
   r[0][threadIdx.x] = x0; r[1][threadIdx.x] = x1;
   r[2][threadIdx.x] = y0; r[3][threadIdx.x] = y1;
   __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
+  for (int st = GS_T / 2; st > 0; st >>= 1) {
     if ((int)threadIdx.x < st) {
       const int o = threadIdx.x + st;
       r[0][threadIdx.x] = fminf(r[0][threadIdx.x], r[0][o]);
@@ -1255,7 +1256,7 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
       ws.cursor, ws.cursor_t);
   // bucket every frame's points into its grid (cell order = frame order, so the scan of
   // all cells gives absolute positions inside each frame's row range)
-  grid_setup<<<n_frames, 256, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
+  grid_setup<<<n_frames, GS_T, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
   grid_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_frame, ws.fg, n_nodes,
                                                      ws.cell_of, ws.cell_cnt);
   RG_LAUNCH_CHECK();
@@ -1377,7 +1378,7 @@ extern "C" int rg_cluster_radius(const float* px, const float* py, const int* fr
              workspace_bytes, need);
   row_frame_base<<<ceil_div(n_nodes, 256), 256, 0, st>>>(frame_ptr, n_frames, ws.row_base,
                                                          ws.row_frame, n_nodes);
-  grid_setup<<<n_frames, 256, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
+  grid_setup<<<n_frames, GS_T, 0, st>>>(px, py, frame_ptr, ws.cpf, ws.fg);
   RG_CHECK_HIP(hipMemsetAsync(ws.cell_cnt, 0, (size_t)ws.n_cells * sizeof(int), st));
   grid_count<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.row_frame, ws.fg, n_nodes,
                                                      ws.cell_of, ws.cell_cnt);

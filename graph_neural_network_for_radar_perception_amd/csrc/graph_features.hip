@@ -15,7 +15,10 @@
 namespace rg {
 
 // ------------------------------------------------------------------ node features
-// One block per frame: frame min/max timestamp, then every node of the frame.
+// Blocks (chunk c = blockIdx.x, frame f = blockIdx.y): every block reduces its frame's
+// min/max timestamp (an L2-resident re-read; a frame of one block would serialise a
+// 20 000-node frame's f64 atan2 work on one CU), then computes the nodes of chunks
+// c, c + gridDim.x, ... of the frame.
 // Arithmetic follows numpy-2 promotion of the reference expressions:
 //   t_norm     = float64(t - tmin) / float64(tmax - tmin)      (int64 / int64 -> f64)
 //   degree/10  = float64(deg) / 10
@@ -28,8 +31,9 @@ __global__ __launch_bounds__(256) void node_features_kernel(
     const float* __restrict__ rcs, const int64_t* __restrict__ ts, const int* __restrict__ deg,
     const int* __restrict__ frame_ptr, double min_r, double max_r, float az_den, float max_az,
     float* __restrict__ out) {
-  const int f = blockIdx.x;
+  const int f = blockIdx.y;
   const int b = frame_ptr[f], e = frame_ptr[f + 1];
+  if (b + (int)blockIdx.x * 256 >= e) return;  // block-uniform: no chunk of this frame
   __shared__ long long smin[256], smax[256];
   long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000ULL;
   for (int i = b + threadIdx.x; i < e; i += 256) {
@@ -49,7 +53,7 @@ __global__ __launch_bounds__(256) void node_features_kernel(
   }
   const long long tmin = smin[0], tmax = smax[0];
   const double span = (double)(tmax - tmin);
-  for (int i = b + threadIdx.x; i < e; i += 256) {
+  for (int i = b + (int)blockIdx.x * 256 + threadIdx.x; i < e; i += 256 * gridDim.x) {
     const double tn = tmax == tmin ? (double)(ts[i] - tmin) : (double)(ts[i] - tmin) / span;
     const double dg = (double)deg[i] / 10.0;
     const float x = px[i], y = py[i];
@@ -271,7 +275,9 @@ extern "C" int rg_node_features(const float* px, const float* py, const float* v
                                 float* out, void* stream) {
   RG_REQUIRE(n_frames >= 1 && n_nodes >= 0, RG_ERR_ARG, "rg_node_features: bad sizes");
   if (n_nodes == 0) return RG_OK;
-  node_features_kernel<<<n_frames, 256, 0, (hipStream_t)stream>>>(
+  // chunks of 256 nodes per frame at the mean frame size (larger frames stride)
+  const int chunks = max(1, min(1024, (int)((n_nodes / n_frames + 255) / 256)));
+  node_features_kernel<<<dim3(chunks, n_frames), 256, 0, (hipStream_t)stream>>>(
       px, py, vr, rcs, timestamp, ball_degree, frame_ptr, min_range, max_range,
       (float)(min_azimuth - max_azimuth), (float)max_azimuth, out);
   RG_LAUNCH_CHECK();

@@ -273,6 +273,30 @@ class DeviceGraph:
         self.n_edges_dev = n_edges_dev
         self.n_edges = n_edges
         self.n_pairs = n_pairs
+        self._conv_blocks = None
+
+    # few 8-node runs per wave of the fused conv's 2 048-wave grid: dynamic scheduling of
+    # whole runs leaves a tail of the heaviest runs (dense radius frames, BASELINE config 5)
+    CONV_BLOCK_TABLE_MAX_RUNS = 4 * 2048
+
+    def conv_blocks(self):
+        """(blk_nodes, n_blocks_dev) of rg_conv_blocks -- edge-balanced work blocks for
+        rg_conv_layer_fused_blocks -- or (None, None) when the graph has enough 8-node runs
+        for the plain schedule.  Built once per graph (one count + scan + emit)."""
+        n = self.n_nodes
+        if n == 0 or (n + 7) // 8 >= self.CONV_BLOCK_TABLE_MAX_RUNS:
+            return None, None
+        if self._conv_blocks is None:
+            lib = nat.lib()
+            dev = self.seg_ptr.device
+            tbl = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            nb = torch.empty(1, dtype=torch.int32, device=dev)
+            ws = torch.empty(lib.rg_conv_blocks_workspace_size(n), dtype=torch.uint8, device=dev)
+            nat.check(lib.rg_conv_blocks(self.seg_ptr.data_ptr(), n, tbl.data_ptr(), nb.data_ptr(),
+                                         ws.data_ptr(), ws.numel(), nat.stream_ptr(dev)),
+                      'rg_conv_blocks')
+            self._conv_blocks = (tbl, nb)
+        return self._conv_blocks
 
     @staticmethod
     def from_edge_index(edge_index: torch.Tensor, n_nodes: int, count_pairs: bool = True):
@@ -453,11 +477,12 @@ class ConvPlan:
         if not self.use_fused or not self.fused or self.fused_ok is False:
             return False
         lib = nat.lib()
-        rc = lib.rg_conv_layer_fused(self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr],
-                                     x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
-                                     g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
-                                     g.n_nodes, x_out.data_ptr(), x_out.stride(0),
-                                     self.fused_ws.data_ptr(), nat.stream_ptr(x.device))
+        tbl, nb = g.conv_blocks()
+        rc = lib.rg_conv_layer_fused_blocks(
+            self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),
+            e.data_ptr(), e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
+            g.n_nodes, x_out.data_ptr(), x_out.stride(0), nat.ptr(tbl), nat.ptr(nb),
+            self.fused_ws.data_ptr(), nat.stream_ptr(x.device))
         if rc == nat.RG_ERR_UNSUPPORTED:
             self.fused_ok = False
             return False
