@@ -111,6 +111,9 @@ _SIGNATURES = {
     'rg_object_complete_graph': (_I, [_P, _I, _I, _L, _P, _P, _P, _P, _S, _P]),
     'rg_object_row_ranges': (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _S, _P]),
     'rg_object_focal_loss': (_I, [_P, _I, _P, _I, _I, _P, _P]),
+    'rg_object_focal_loss_backward': (_I, [_P, _I, _P, _I, _I, _P, _P, _I, _P]),
+    'rg_range_max_backward': (_I, [_P, _I, _I, _P, _P, _I, _P, _I, _P, _I, _P]),
+    'rg_segment_amax_backward': (_I, [_P, _I, _I, _P, _I, _P, _I, _P, _I, _P]),
     # training (train.hip)
     'rg_ffn_backward_workspace_size': (_S, []),
     'rg_ffn_backward': (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P]),

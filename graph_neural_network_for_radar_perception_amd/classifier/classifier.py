@@ -50,7 +50,8 @@ class Model_Inference(nn.Module):
 
 
 class Model_Training(nn.Module):
-    """classifier.py:75-100: ``pred`` + ``loss``; forward returns the scalar loss."""
+    """classifier.py:75-100: ``pred`` + ``loss``; forward returns the scalar loss (with a
+    native backward when gradients are enabled, ``classifier/training.py``)."""
 
     def __init__(self, net_config):
         super().__init__()
@@ -66,8 +67,19 @@ class Model_Training(nn.Module):
     def forward(self, node_features: List[torch.Tensor], edge_index: List[torch.Tensor],
                 object_size: List[torch.Tensor], groundtruths: List[torch.Tensor]):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError('the classifier GNN has no native backward; evaluate the '
-                                      'loss under torch.no_grad()')
+            # training (classifier/training.py: loss.backward(); optimizer.step()): the
+            # float32 tape forward, with the native backward attached to the loss
+            from . import training
+            if self.pred.compute_dtype != 'fp32':
+                raise NotImplementedError('classifier training runs in float32 (the '
+                                          'reference precision); set compute_dtype = "fp32"')
+            dev = node_features[0].device
+            eng = getattr(self, '_train_engine', None)
+            if eng is None or eng.device != dev:
+                eng = training.ClassifierTrainEngine(self, dev)
+                object.__setattr__(self, '_train_engine', eng)  # not a submodule
+            batch = training.prepare_batch(node_features, edge_index, object_size, groundtruths)
+            return training.train_step_loss(eng, batch)
         predictions = self.predict(node_features, edge_index, object_size)
         gt = torch.cat([g.to(predictions.device) for g in groundtruths], 0)
         return self.loss(predictions, gt)

@@ -200,3 +200,115 @@ extern "C" int rg_object_focal_loss(const float* logits, int ld, const int64_t* 
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Backward of the classifier loss and of its pooling (Model_Training + loss.backward(),
+// classifier/training.py).
+//
+// d loss / d x for the focal loss above, scaled by g / n (g = upstream gradient of the
+// scalar loss, on the device):
+//   d ce / dx = p - t,  d p_t / dx = (2t - 1) p (1 - p),
+//   d [ce (1 - p_t)^2] / dx = (p - t) m^2 - 2 ce m (2t - 1) p (1 - p),  m = 1 - p_t.
+// ---------------------------------------------------------------------------
+namespace rg {
+
+__global__ __launch_bounds__(256) void object_focal_loss_backward_kernel(
+    const float* __restrict__ logits, int ld, const int64_t* __restrict__ labels, int n, int nc,
+    const float* __restrict__ g_loss, float* __restrict__ d_logits, int ldd) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)n * nc) return;
+  const int r = (int)(i / nc), c = (int)(i % nc);
+  const float x = logits[(size_t)r * ld + c];
+  const float t = c == labels[r] ? 1.f : 0.f;
+  const float p = 1.f / (1.f + expf(-x));
+  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  const float pt = p * t + (1.f - p) * (1.f - t);
+  const float m = 1.f - pt;
+  const float d = (p - t) * (m * m) - 2.f * ce * m * (2.f * t - 1.f) * p * (1.f - p);
+  d_logits[(size_t)r * ldd + c] = d * (g_loss[0] / (float)n);
+}
+
+// torch.max(x[begin:end], dim=0) backward (classifier/blocks.py:171-176): the gradient
+// of object o, channel c goes to the FIRST row of [begin[o], end[o]) holding the maximum
+// (torch's index for ties); ranges overlap (classifier.py:60-62), so rows accumulate
+// with atomics.  One thread per (object, channel), rows scanned in order.
+__global__ __launch_bounds__(256) void range_max_backward_kernel(
+    const float* __restrict__ x, int ldx, int C, const int* __restrict__ begin,
+    const int* __restrict__ end, int n_obj, const float* __restrict__ d_pooled, int ldp,
+    float* __restrict__ dx, int lddx) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)n_obj * C) return;
+  const int o = (int)(i / C), c = (int)(i % C);
+  const int b = begin[o], e = end[o];
+  if (b >= e) return;
+  int arg = b;
+  float best = x[(size_t)b * ldx + c];
+  for (int r = b + 1; r < e; ++r) {
+    const float v = x[(size_t)r * ldx + c];
+    if (v > best || (v != v && best == best)) { best = v; arg = r; }  // NaN wins, as torch.max
+  }
+  atomicAdd(dx + (size_t)arg * lddx + c, d_pooled[(size_t)o * ldp + c]);
+}
+
+}  // namespace rg
+
+extern "C" int rg_object_focal_loss_backward(const float* logits, int ld, const int64_t* labels,
+                                             int n, int nc, const float* g_loss, float* d_logits,
+                                             int ldd, void* stream) {
+  RG_REQUIRE(n > 0 && nc > 0 && ld >= nc && ldd >= nc, RG_ERR_ARG,
+             "rg_object_focal_loss_backward: n=%d nc=%d", n, nc);
+  const long tot = (long)n * nc;
+  object_focal_loss_backward_kernel<<<(tot + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      logits, ld, labels, n, nc, g_loss, d_logits, ldd);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_range_max_backward(const float* x, int ldx, int C, const int* begin,
+                                     const int* end, int n_obj, const float* d_pooled, int ldp,
+                                     float* dx, int lddx, void* stream) {
+  RG_REQUIRE(n_obj >= 0 && C > 0, RG_ERR_ARG, "rg_range_max_backward: n_obj=%d C=%d", n_obj, C);
+  if (n_obj == 0) return RG_OK;
+  const long tot = (long)n_obj * C;
+  range_max_backward_kernel<<<(tot + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      x, ldx, C, begin, end, n_obj, d_pooled, ldp, dx, lddx);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// PyG aggr='max' (scatter_reduce amax, include_self=False, classifier/blocks.py:62-66)
+// backward over a destination-major CSR whose position p IS the message row: torch's
+// amax backward splits the gradient evenly among the messages equal to the maximum.
+// One thread per (segment, channel); empty segments have no messages.
+namespace rg {
+__global__ __launch_bounds__(256) void segment_amax_backward_kernel(
+    const float* __restrict__ msg, int ldm, int C, const int* __restrict__ seg_ptr, int n_seg,
+    const float* __restrict__ d_agg, int ldd, float* __restrict__ d_msg, int ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)n_seg * C) return;
+  const int s = (int)(i / C), c = (int)(i % C);
+  const int b = seg_ptr[s], e = seg_ptr[s + 1];
+  if (b >= e) return;
+  float m = msg[(size_t)b * ldm + c];
+  int cnt = 1;
+  for (int p = b + 1; p < e; ++p) {
+    const float v = msg[(size_t)p * ldm + c];
+    if (v > m) { m = v; cnt = 1; } else if (v == m) { ++cnt; }
+  }
+  const float g = d_agg[(size_t)s * ldd + c] / (float)cnt;
+  for (int p = b; p < e; ++p)
+    d_msg[(size_t)p * ldo + c] = msg[(size_t)p * ldm + c] == m ? g : 0.f;
+}
+}  // namespace rg
+
+extern "C" int rg_segment_amax_backward(const float* msg, int ldm, int C, const int* seg_ptr,
+                                        int n_seg, const float* d_agg, int ldd, float* d_msg,
+                                        int ldo, void* stream) {
+  RG_REQUIRE(n_seg >= 0 && C > 0, RG_ERR_ARG, "rg_segment_amax_backward: n_seg=%d C=%d", n_seg, C);
+  if (n_seg == 0) return RG_OK;
+  const long tot = (long)n_seg * C;
+  segment_amax_backward_kernel<<<(tot + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      msg, ldm, C, seg_ptr, n_seg, d_agg, ldd, d_msg, ldo);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

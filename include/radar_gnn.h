@@ -307,6 +307,23 @@ int rg_object_row_ranges(const int64_t* object_size, int n_obj, const int* sampl
  * fixed-order f64 reduction (deterministic). */
 int rg_object_focal_loss(const float* logits, int ld, const int64_t* labels, int n, int nc,
                          float* out, void* stream);
+/* Its gradient: d_logits[n][ldd] = (g_loss[0] / n) * d(loss_row)/d(logits) (g_loss: f32 [1]
+ * on the device, the upstream gradient of the scalar loss). */
+int rg_object_focal_loss_backward(const float* logits, int ld, const int64_t* labels, int n,
+                                  int nc, const float* g_loss, float* d_logits, int ldd,
+                                  void* stream);
+/* Backward of the classifier's per-object channel max over rows [begin[o], end[o])
+ * (classifier/blocks.py:171-176, torch.max(dim=0)): dx[first argmax row][c] +=
+ * d_pooled[o][c] (atomic: the reference's ranges overlap).  x, dx f32. */
+int rg_range_max_backward(const float* x, int ldx, int C, const int* begin, const int* end,
+                          int n_obj, const float* d_pooled, int ldp, float* dx, int lddx,
+                          void* stream);
+/* Backward of PyG aggr='max' (scatter_reduce amax, include_self=False) over a
+ * destination-major CSR whose position p is message row p: d_msg[p][c] = d_agg[s][c] /
+ * (number of maxima) for the messages equal to the segment maximum, else 0 (torch's
+ * amax backward).  f32. */
+int rg_segment_amax_backward(const float* msg, int ldm, int C, const int* seg_ptr, int n_seg,
+                             const float* d_agg, int ldd, float* d_msg, int ldo, void* stream);
 
 
 /* ------------------------------------------------------------ proposal branch */
