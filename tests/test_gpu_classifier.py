@@ -175,7 +175,7 @@ def test_classifier_training_gradients_match_oracle(cuda_device, name):
              [s['osz'].to(dev) for s in ss], [s['gt'].to(dev) for s in ss])
     assert loss.requires_grad
     loss.backward()
-    assert abs(float(loss) - float(d['loss'])) <= 1e-4 + 1e-4 * abs(float(d['loss']))
+    assert abs(float(loss.detach()) - float(d["loss"])) <= 1e-4 + 1e-4 * abs(float(d["loss"]))
     ref_sd = {k[len('pred.'):]: v.clone().float().requires_grad_(True)
               for k, v in sd.items() if k.startswith('pred.')}
     logits = torch.cat([classifier_ref.forward(ref_sd, cfg, s['nf'], s['ei'], s['osz'])
