@@ -1,0 +1,62 @@
+"""HIP-graph experiment: capture one full pipeline step (graph build + forward) of the
+BASELINE config-2 batch with torch.cuda.CUDAGraph (hipGraph on ROCm) and compare the
+replay time with eager launches.  GPU box: python scripts/graph_exp.py"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from graph_neural_network_for_radar_perception_amd import synthetic  # noqa: E402
+from graph_neural_network_for_radar_perception_amd.config import default_config  # noqa: E402
+from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training  # noqa: E402
+from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch  # noqa: E402
+from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline  # noqa: E402
+
+
+def main(frames=64, nodes=3000, k=32, layers=6, steps=30):
+    dev = torch.device('cuda', 0)
+    cfg = default_config(graph_convolution_stem_channels=[64] * layers, k_number_nearest_points=k)
+    torch.manual_seed(1234)
+    m = Model_Training(cfg, dev).to(dev)
+    model = m.pred.eval().requires_grad_(False)
+    frs = [synthetic.make_frame(nodes, 1234 + i) for i in range(frames)]
+    cls = [synthetic.cluster_lists(nodes) for _ in range(frames)]
+    batch = FrameBatch.from_frames(frs, cls, device=dev)
+    pipe = RadarGNNPipeline(model, cfg, 'bf16')
+    with torch.no_grad():
+        for _ in range(3):
+            gb, out = pipe.step(batch)
+        torch.cuda.synchronize()
+        ref = [t.clone() for t in (out.node_cls, out.node_reg, out.obj_cls)]
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pipe.step(batch)
+        torch.cuda.synchronize()
+        eager = (time.perf_counter() - t0) / steps * 1e3
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            pipe.step(batch)  # warm the side stream's allocations
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            gb2, out2 = pipe.step(batch)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(ref, (out2.node_cls, out2.node_reg, out2.obj_cls)):
+            assert torch.equal(a, b), 'graph replay differs from eager'
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        graph = (time.perf_counter() - t0) / steps * 1e3
+    print(f'eager {eager:.3f} ms/step  graph {graph:.3f} ms/step  '
+          f'({frames / graph * 1e3:.0f} vs {frames / eager * 1e3:.0f} frames/s)', flush=True)
+
+
+if __name__ == '__main__':
+    main()
