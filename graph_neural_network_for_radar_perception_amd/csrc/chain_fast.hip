@@ -32,6 +32,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // workgroup per CU shares one LDS copy of the weights, so more waves per workgroup is
 // the only way to more latency hiding.
 static constexpr float NORM_EPS = 1e-5f;
+#ifndef RG_PAIR_SPLIT
+#define RG_PAIR_SPLIT 1  // PAIRADD chains: the MFMAs add the pair (see Input::PAIR_SPLIT)
+#endif
 static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layers 0+1
 
 #ifndef RG_CHAIN_EXP
@@ -112,12 +115,17 @@ struct Input {
   static constexpr int K0 = MODE == RG_IN_GATHER3 ? 2 * W0 + W1
                           : (MODE == RG_IN_CONCAT2 ? W0 + W1 : W0);
   static constexpr int KS = (K0 + 15) / 16;
+  // B fragments handed to layer 0: PAIRADD keeps x[i] and x[j] apart (KS each) and lets
+  // the MFMAs add them, W (x_i + x_j) = W x_i + W x_j, instead of ~28 VALU per fragment
+  // to unpack, add and repack the pair in bf16 (the chain is VALU-bound)
+  static constexpr bool PAIR_SPLIT = MODE == RG_IN_PAIRADD && RG_PAIR_SPLIT;
+  static constexpr int KSB = PAIR_SPLIT ? 2 * KS : KS;
 
   static __device__ __forceinline__ void load(const FArgs& a, long row, bool valid, int h,
-                                              bf16x8_t (&b)[KS], float pre = 1.f) {
+                                              bf16x8_t (&b)[KSB], float pre = 1.f) {
     if (!valid) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) b[s] = zero_bf8();
+      for (int s = 0; s < KSB; ++s) b[s] = zero_bf8();
       return;
     }
     if constexpr (MODE == RG_IN_DENSE && IN_F32) {
@@ -162,8 +170,16 @@ struct Input {
       const int ri = a.idx0[row], rj = a.idx1[row];
       const uint16_t* pi = (const uint16_t*)a.in0 + (size_t)ri * a.ld0 + 8 * h;
       const uint16_t* pj = (const uint16_t*)a.in0 + (size_t)rj * a.ld0 + 8 * h;
+      if constexpr (PAIR_SPLIT) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) b[s] = add_bf8(ld_bf8(pi + 16 * s), ld_bf8(pj + 16 * s));
+        for (int s = 0; s < KS; ++s) {
+          b[s] = ld_bf8(pi + 16 * s);
+          b[KS + s] = ld_bf8(pj + 16 * s);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) b[s] = add_bf8(ld_bf8(pi + 16 * s), ld_bf8(pj + 16 * s));
+      }
     }
   }
 };
@@ -197,6 +213,36 @@ __device__ __forceinline__ void mfma_layer(const bf16x8_t (&b)[KS], f32x16 (&acc
       acc[m] = mfma32(acur[m], b[s], acc[m]);
     __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
+    }
+  }
+}
+
+// layer 0 of a split pair: REP x KS B fragments against the same KS weight k-steps
+// (acc = bias + W b[0..KS) + W b[KS..2KS)), fragments of step s+1 read during step s
+template <int KS, int MT, int REP>
+__device__ __forceinline__ void mfma_layer_rep(const bf16x8_t (&b)[REP * KS], f32x16 (&acc)[MT],
+                                               const char* w, int lane) {
+  const int h = lane >> 5;
+  const float* bias = (const float*)(w + (size_t)MT * KS * 1024);
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = ld_bias_frag(bias, m, h);
+  const char* wl = w + lane * 16;
+  bf16x8_t acur[MT], anxt[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acur[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS) * 1024));
+#pragma unroll
+  for (int s = 0; s < REP * KS; ++s) {
+    if (s + 1 < REP * KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        anxt[m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KS + (s + 1) % KS) * 1024));
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma32(acur[m], b[s], acc[m]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < REP * KS) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) acur[m] = anxt[m];
     }
@@ -346,6 +392,28 @@ constexpr bool pre_scaled_l0(int spec_) {
   return spec_ >= 0 && ((spec_ >> 16) & 1) != 0 && (spec_ & 0xff) == ACT_LEAKY;
 }
 
+// a chain whose layer 0 takes a split pair (Input::PAIR_SPLIT): layer 0 over 2 KS
+// fragments, then the rest of the chain as usual
+template <int SPEC, int K, int N, int... Rest>
+__device__ __forceinline__ void run_chain_pair(const FArgs& a,
+                                               const bf16x8_t (&b)[2 * ((K + 15) / 16)],
+                                               const char* lds, const float* nrm, long row,
+                                               bool valid, int lane) {
+  constexpr int KS = (K + 15) / 16;
+  constexpr int MT = N / 32;
+  f32x16 acc[MT];
+  mfma_layer_rep<KS, MT, 2>(b, acc, lds, lane);
+  epilogue<SPEC, 0, MT>(acc, a.L[0], nrm);
+  if constexpr (sizeof...(Rest) > 0) {
+    bf16x8_t nb[2 * MT];
+    pack_next<MT>(acc, nb);
+    run_chain<SPEC, ((fast_bytes(K, N) + 15) & ~15), 1, N, Rest...>(a, nb, lds, nrm, row, valid,
+                                                                    lane);
+  } else {
+    if (valid) store_out<MT>(acc, a, row, lane >> 5);
+  }
+}
+
 // Layers 0 and 1 fused tile by tile, for a first layer WITHOUT normalisation (the
 // encoders' first ffn_block, gnn_blocks.py:31): each 32-wide output tile of layer 0 is
 // activated, packed to bf16 and consumed at once as layer 1's k-steps 2m0, 2m0+1, so
@@ -485,9 +553,11 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
   const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
   const long ntiles = (rows + 31) / 32;
   const long tstride = (long)gridDim.x * FW;
-  auto run = [&](const bf16x8_t (&b)[In::KS], long row, bool valid) {
+  auto run = [&](const bf16x8_t (&b)[In::KSB], long row, bool valid) {
     if constexpr ((MODE & FUSE01) != 0)  // un-normalised first layer: tile-fused layers 0+1
       run_chain01<SPEC, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
+    else if constexpr (In::PAIR_SPLIT)
+      run_chain_pair<SPEC, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
     else
       run_chain<SPEC, 0, 0, In::K0, Ns...>(a, b, lds, nrm, row, valid, lane);
   };
@@ -526,7 +596,7 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     for (long tile = (long)blockIdx.x * FW + wave; tile < ntiles; tile += tstride) {
       const long row = tile * 32 + (lane & 31);
       const bool valid = row < rows;
-      bf16x8_t b[In::KS];
+      bf16x8_t b[In::KSB];
       In::load(a, row, valid, lane >> 5, b, PRE0 ? LEAKY_PRE : 1.f);
       run(b, row, valid);
     }

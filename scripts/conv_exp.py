@@ -12,7 +12,7 @@ EXPS_ALL = {'base': ['RG_CONV_EXP=0'], 'nogather': ['RG_CONV_EXP=1'], 'nonorm': 
         'noagg': ['RG_CONV_EXP=3'], 'ct256': ['RG_CONV_CT=256'], 'prio': ['RG_CONV_PRIO=1'],
         'chain_noepi': ['RG_CHAIN_EXP=1'], 'chain_nomfma': ['RG_CHAIN_EXP=2'],
         'chain_nolds': ['RG_CHAIN_EXP=3'],
-        'scalar': ['RG_NO_PK', '-fno-slp-vectorize'], 'pfx': ['RG_CONV_PFX=1'], 'noP': ['RG_CONV_EXP=4'], 'pfd4': ['RG_CONV_PFD4=2'],
+        'scalar': ['RG_NO_PK', '-fno-slp-vectorize'], 'nosplit': ['RG_PAIR_SPLIT=0'], 'pfx': ['RG_CONV_PFX=1'], 'noP': ['RG_CONV_EXP=4'], 'pfd4': ['RG_CONV_PFD4=2'],
         'pfd4b': ['RG_CONV_PFD4=2', 'RG_CONV_PFD=2']}
 EXPS = {k: v for k, v in EXPS_ALL.items()
         if len(sys.argv) < 3 or k in sys.argv[2].split(',') or k == 'base'}
