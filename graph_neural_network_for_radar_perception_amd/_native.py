@@ -78,6 +78,14 @@ _SIGNATURES = {
     'rg_pairs_from_edge_index_workspace_size': (_S, [_L]),
     'rg_pairs_from_edge_index': (_I, [_P, _L, _P, _P, _P, _P, _S, _P]),
     'rg_csr_rows': (_I, [_P, _I, _P, _P]),
+    # real-data front-end (frontend.hip)
+    'rg_frontend_sync': (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P,
+                              _P, _P]),
+    'rg_frontend_labels_workspace_size': (_S, [_I]),
+    'rg_frontend_labels': (_I, [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _S, _P]),
+    'rg_frontend_select_workspace_size': (_S, [_I]),
+    'rg_frontend_select': (_I, [_P, _P, _P, _I, _F, _F, _F, _F, _F, _P, _I, _P, _P, _P, _P, _S,
+                                _P]),
     'rg_proposal_centres': (_I, [_P, _I, _P, _I, _I, _F, _F, _F, _F, _P, _P, _P]),
     'rg_cluster_radius_workspace_size': (_S, [_I, _I, _I]),
     'rg_cluster_radius': (_I, [_P, _P, _P, _I, _I, _I, _F, _P, _P, _S, _P]),

@@ -1,0 +1,241 @@
+// Real-data front-end: the step before the graph build, for a
+// window of radar scans already in HBM (the .h5 reading of read_data.py stays on the
+// host).  Replaces, per window:
+//   read_data.extract_and_sync_radar_data (read_data.py:227-303) and extract_frame
+//   (:442-486): per scan the stationary gate identify_stationary_measurements
+//   (meas_selection.py:22-70,169-200; ransac off, configuration_radarscenes_gnn.yml:11),
+//   vr_cartesian_vf (meas_sync.py:15-20) and ego_compensate_radar_frames_list
+//   (meas_sync.py:23-103) into the last scan's vehicle frame, cast to float32;
+//   compute_ground_truth (compute_node_labels.py:50-105): class labels and per-track
+//   offsets to the track mean;
+//   grid_properties.select_meas_within_the_grid (grid_features.py:162-174) and
+//   select_moving_data (graph_features.py:167-182) as ONE order-preserving compaction.
+// One thread per measurement; the per-scan transforms are recomputed per thread from
+// the scan's float64 pose (a few flops).  Arithmetic follows the reference's numpy
+// promotion (comments at each step); transcendental functions of float32 arrays are
+// evaluated in float32 as numpy does.
+#include "rg_common.h"
+#include "scan.h"
+
+// numpy evaluates every product and sum separately
+#pragma clang fp contract(off)
+
+namespace rg {
+
+struct ScanPose {  // per scan, float64: mount (tx, ty, yaw), odometry (x, y, yaw, vx, yaw_rate)
+  double tx, ty, myaw, ox, oy, oyaw, ovx, oyr;
+};
+
+__device__ __forceinline__ int scan_of(const int* __restrict__ scan_ptr, int n_scans, int i) {
+  int lo = 0, hi = n_scans;  // scan_ptr[lo] <= i < scan_ptr[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (scan_ptr[mid] <= i) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ ScanPose load_pose(const double* __restrict__ mount,
+                                              const double* __restrict__ odo, int s) {
+  ScanPose p;
+  p.tx = mount[3 * s]; p.ty = mount[3 * s + 1]; p.myaw = mount[3 * s + 2];
+  p.ox = odo[5 * s]; p.oy = odo[5 * s + 1]; p.oyaw = odo[5 * s + 2];
+  p.ovx = odo[5 * s + 3]; p.oyr = odo[5 * s + 4];
+  return p;
+}
+
+__global__ __launch_bounds__(256) void frontend_sync_kernel(
+    const float* __restrict__ x_cc, const float* __restrict__ y_cc,
+    const float* __restrict__ azimuth, const float* __restrict__ vr,
+    const float* __restrict__ vr_comp, const int* __restrict__ scan_ptr, int n_scans,
+    const int* __restrict__ scan_ref, const double* __restrict__ mount,
+    const double* __restrict__ odo, float gamma, int n,
+    float* __restrict__ px, float* __restrict__ py, float* __restrict__ vx,
+    float* __restrict__ vy, uint8_t* __restrict__ stationary) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = scan_of(scan_ptr, n_scans, i);
+  const ScanPose p = load_pose(mount, odo, s);
+  const float az = azimuth[i];
+  // ---- stationary gate (meas_selection.py:22-70): the sensor-frame ego velocity is
+  // float64 (odometry scalars are np.float64), cos / sin of the float32 azimuths are
+  // float32, their products with the float64 scalars float64
+  const double vxs0 = p.ovx - p.oyr * p.ty;
+  const double vys0 = 0.0 + p.oyr * p.tx;
+  const double c = cos(-p.myaw), sn = sin(-p.myaw);
+  const double vxs = vxs0 * c - vys0 * sn;
+  const double vys = vxs0 * sn + vys0 * c;
+  const double vr_pred = -((vxs * (double)cosf(az)) + (vys * (double)sinf(az)));
+  const double err = vr_pred - (double)vr[i];
+  stationary[i] = fabs(err) <= (double)gamma ? 1 : 0;
+  // ---- vr_cartesian_vf (meas_sync.py:15-20): float32 array + python-float mount yaw
+  // stays float32 (NEP 50 weak scalar); products float32
+  const float ang = az + (float)p.myaw;
+  const float v = vr_comp[i];
+  vx[i] = v * cosf(ang);
+  vy[i] = v * sinf(ang);
+  // ---- ego compensation (meas_sync.py:52-71): T = T_curr^-1 T_prev in float64,
+  // position R p + t, velocities unchanged; extract_frame casts to float32
+  // the window's current scan (a batch of windows: each scan names its own)
+  const ScanPose q = load_pose(mount, odo, scan_ref ? scan_ref[s] : n_scans - 1);
+  const double cc = cos(q.oyaw), sc = sin(q.oyaw), cp = cos(p.oyaw), sp = sin(p.oyaw);
+  const double r00 = cc * cp + sc * sp, r01 = -(cc * sp) + sc * cp;
+  const double r10 = -(sc * cp) + cc * sp, r11 = sc * sp + cc * cp;
+  const double dx = p.ox - q.ox, dy = p.oy - q.oy;
+  const double t0 = cc * dx + sc * dy, t1 = -(sc * dx) + cc * dy;
+  const double x = (double)x_cc[i], y = (double)y_cc[i];
+  px[i] = (float)((r00 * x + r01 * y) + t0);
+  py[i] = (float)((r10 * x + r11 * y) + t1);
+}
+
+// class labels (compute_node_labels.py:70-86) and per-track float64 sums for the offsets
+__global__ __launch_bounds__(256) void frontend_labels_kernel(
+    const int* __restrict__ track_key, const int64_t* __restrict__ label_id,
+    const uint8_t* __restrict__ stationary, const int* __restrict__ old_to_new, int n_old,
+    const float* __restrict__ px, const float* __restrict__ py, int n,
+    float* __restrict__ cls, double* __restrict__ tsum, int* __restrict__ tcnt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = track_key[i];
+  float c;
+  if (k > 0) {  // valid object: reassigned label id
+    const int64_t o = label_id[i];
+    c = (o >= 0 && o < n_old) ? (float)old_to_new[o] : -1.f;
+    atomicAdd(tsum + 2 * k, (double)px[i]);
+    atomicAdd(tsum + 2 * k + 1, (double)py[i]);
+    atomicAdd(tcnt + k, 1);
+  } else {      // no track: clutter 'FALSE' (6) or static environment 'STATIC' (7)
+    c = stationary[i] ? 7.f : 6.f;
+  }
+  cls[i] = c;
+}
+
+// offsets to the track mean (compute_node_labels.py:50-67): mean in float64 from exact
+// sums, rounded once to float32 (numpy's float32 pairwise mean is within an ulp), minus
+// the float32 position in float32; untracked measurements keep 0
+__global__ __launch_bounds__(256) void frontend_offsets_kernel(
+    const int* __restrict__ track_key, const float* __restrict__ px,
+    const float* __restrict__ py, const double* __restrict__ tsum,
+    const int* __restrict__ tcnt, int n, float* __restrict__ offx, float* __restrict__ offy) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = track_key[i];
+  if (k > 0) {
+    const double m = (double)tcnt[k];
+    offx[i] = (float)(tsum[2 * k] / m) - px[i];
+    offy[i] = (float)(tsum[2 * k + 1] / m) - py[i];
+  } else {
+    offx[i] = 0.f;
+    offy[i] = 0.f;
+  }
+}
+
+// keep = inside [min_x, max_x) x [min_y, max_y) and class != STATIC
+__global__ __launch_bounds__(256) void frontend_keep_kernel(
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ cls,
+    float min_x, float max_x, float min_y, float max_y, float static_id, int n,
+    int* __restrict__ keep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = px[i], y = py[i];
+  keep[i] = (x >= min_x && x < max_x && y >= min_y && y < max_y && cls[i] != static_id) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void frontend_index_kernel(const int* __restrict__ keep,
+                                                             const int* __restrict__ pos, int n,
+                                                             int* __restrict__ index) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (keep[i]) index[pos[i]] = i;
+}
+
+// the dynamic frames of a batch of windows: frame w = selected rows
+// [pos[win_ptr[w]], pos[win_ptr[w + 1]]) (pos[n] = the total)
+__global__ void frontend_frame_ptr_kernel(const int* __restrict__ pos,
+                                          const int* __restrict__ win_ptr, int n_windows,
+                                          int* __restrict__ frame_ptr) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w <= n_windows) frame_ptr[w] = pos[win_ptr[w]];
+}
+
+}  // namespace rg
+
+using namespace rg;
+
+extern "C" int rg_frontend_sync(const float* x_cc, const float* y_cc, const float* azimuth_sc,
+                                const float* vr, const float* vr_compensated,
+                                const int* scan_ptr, int n_scans, const int* scan_ref,
+                                const double* mount, const double* odometry,
+                                float gamma_stationary, int n_meas,
+                                float* px, float* py, float* vx, float* vy,
+                                uint8_t* stationary, void* stream) {
+  RG_REQUIRE(n_scans >= 1 && n_meas >= 0, RG_ERR_ARG, "rg_frontend_sync: n_scans=%d n_meas=%d",
+             n_scans, n_meas);
+  if (n_meas == 0) return RG_OK;
+  frontend_sync_kernel<<<ceil_div(n_meas, 256), 256, 0, (hipStream_t)stream>>>(
+      x_cc, y_cc, azimuth_sc, vr, vr_compensated, scan_ptr, n_scans, scan_ref, mount, odometry,
+      gamma_stationary, n_meas, px, py, vx, vy, stationary);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_frontend_labels_workspace_size(int n_tracks) {
+  return ((size_t)(n_tracks + 1) * 2 * sizeof(double) + 255) / 256 * 256 +
+         ((size_t)(n_tracks + 1) * sizeof(int) + 255) / 256 * 256;
+}
+
+extern "C" int rg_frontend_labels(const int* track_key, int n_tracks, const int64_t* label_id,
+                                  const uint8_t* stationary, const int* old_to_new, int n_old,
+                                  const float* px, const float* py, int n_meas, float* cls,
+                                  float* offset_x, float* offset_y, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(n_tracks >= 0 && n_meas >= 0, RG_ERR_ARG, "rg_frontend_labels: bad sizes");
+  RG_REQUIRE(workspace_bytes >= rg_frontend_labels_workspace_size(n_tracks), RG_ERR_ARG,
+             "rg_frontend_labels: workspace too small");
+  if (n_meas == 0) return RG_OK;
+  double* tsum = (double*)workspace;
+  int* tcnt = (int*)((char*)workspace +
+                     ((size_t)(n_tracks + 1) * 2 * sizeof(double) + 255) / 256 * 256);
+  RG_CHECK_HIP(hipMemsetAsync(workspace, 0, rg_frontend_labels_workspace_size(n_tracks), st));
+  frontend_labels_kernel<<<ceil_div(n_meas, 256), 256, 0, st>>>(
+      track_key, label_id, stationary, old_to_new, n_old, px, py, n_meas, cls, tsum, tcnt);
+  frontend_offsets_kernel<<<ceil_div(n_meas, 256), 256, 0, st>>>(track_key, px, py, tsum, tcnt,
+                                                                   n_meas, offset_x, offset_y);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" size_t rg_frontend_select_workspace_size(int n_meas) {
+  return 2 * (((size_t)(n_meas + 1) * sizeof(int) + 255) / 256 * 256) +
+         scan_workspace_bytes(n_meas);
+}
+
+extern "C" int rg_frontend_select(const float* px, const float* py, const float* cls, int n_meas,
+                                  float min_x, float max_x, float min_y, float max_y,
+                                  float static_id, const int* win_ptr, int n_windows,
+                                  int* frame_ptr, int* index, int* n_selected, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(workspace_bytes >= rg_frontend_select_workspace_size(n_meas), RG_ERR_ARG,
+             "rg_frontend_select: workspace too small");
+  if (n_meas == 0) {
+    RG_CHECK_HIP(hipMemsetAsync(n_selected, 0, sizeof(int), st));
+    return RG_OK;
+  }
+  const size_t arr = ((size_t)(n_meas + 1) * sizeof(int) + 255) / 256 * 256;
+  int* keep = (int*)workspace;
+  int* pos = (int*)((char*)workspace + arr);
+  void* sws = (char*)workspace + 2 * arr;
+  frontend_keep_kernel<<<ceil_div(n_meas, 256), 256, 0, st>>>(px, py, cls, min_x, max_x, min_y,
+                                                                max_y, static_id, n_meas, keep);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(keep, n_meas, pos, n_selected, sws, st);
+  if (rc) return rc;
+  frontend_index_kernel<<<ceil_div(n_meas, 256), 256, 0, st>>>(keep, pos, n_meas, index);
+  if (win_ptr && frame_ptr)
+    frontend_frame_ptr_kernel<<<ceil_div(n_windows + 1, 256), 256, 0, st>>>(pos, win_ptr,
+                                                                             n_windows, frame_ptr);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

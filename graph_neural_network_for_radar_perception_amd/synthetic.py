@@ -178,3 +178,67 @@ def make_objects(num_objects: int, seed: int = SEED0, min_size: int = 2, max_siz
     return {'node_features': np.concatenate(feats, 0).astype(np.float32),
             'object_size': sizes,
             'object_class': rng.integers(0, num_classes, num_objects).astype(np.int64)}
+
+
+def make_scan_window(seed: int, n_scans: int = 10, mean_meas: int = 160) -> dict:
+    """A window of radar scans with RadarScenes field names and dtypes (the inputs of
+    read_data.extract_and_sync_radar_data, read_data.py:227-303): per measurement
+    x_cc, y_cc, azimuth_sc, vr, vr_compensated, rcs (f32), timestamp (int64 us),
+    track_id (bytes, b'' = no track) + its integer key, sensor_id, label_id (old ids
+    0..11, labels.py:44-58); per scan the radar mount (x, y, yaw) and the odometry
+    (x_seq, y_seq, yaw_seq, vx, yaw_rate) as float64.  Static returns carry the range
+    rate the ego motion predicts (plus noise) so the stationary gate sees both classes."""
+    rng = np.random.default_rng(seed)
+    mounts = np.array([[3.66, -0.64, -1.48], [3.86, -0.70, -0.09],
+                       [3.86, 0.74, 0.09], [3.66, 0.68, 1.48]])  # 4 corner radars
+    sizes = rng.integers(mean_meas // 2, mean_meas * 3 // 2, n_scans)
+    ptr = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    N = int(ptr[-1])
+    out = {k: np.zeros(N, np.float32) for k in ('x_cc', 'y_cc', 'azimuth_sc', 'vr',
+                                                'vr_compensated', 'rcs')}
+    out['timestamp'] = np.zeros(N, np.int64)
+    out['sensor_id'] = np.zeros(N, np.int64)
+    out['label_id'] = np.zeros(N, np.int64)
+    out['track_key'] = np.zeros(N, np.int64)
+    tid = np.zeros(N, dtype='S8')
+    mount = np.zeros((n_scans, 3))
+    odo = np.zeros((n_scans, 5))
+    x, y, yaw = rng.uniform(-50, 50), rng.uniform(-50, 50), rng.uniform(-np.pi, np.pi)
+    t0 = 10 ** 12
+    for s in range(n_scans):
+        sid = int(rng.integers(1, 5))
+        tx, ty, myaw = mounts[sid - 1]
+        vx_e, yr = rng.uniform(2, 15), rng.uniform(-0.2, 0.2)
+        mount[s] = (tx, ty, myaw)
+        odo[s] = (x, y, yaw, vx_e, yr)
+        a, b = int(ptr[s]), int(ptr[s + 1])
+        n = b - a
+        az = rng.uniform(-1.3, 1.3, n)
+        r = rng.uniform(1.0, 90.0, n)
+        # sensor-frame ego velocity (meas_selection.py:22-34) and the static range rate
+        vxs, vys = vx_e - yr * ty, 0.0 + yr * tx
+        c, sn = np.cos(-myaw), np.sin(-myaw)
+        vxs, vys = vxs * c - vys * sn, vxs * sn + vys * c
+        vr_static = -(vxs * np.cos(az) + vys * np.sin(az))
+        moving = rng.random(n) < 0.35
+        vr = np.where(moving, vr_static + rng.normal(0, 6, n), vr_static + rng.normal(0, 0.5, n))
+        out['azimuth_sc'][a:b] = az
+        out['vr'][a:b] = vr
+        out['vr_compensated'][a:b] = vr - vr_static
+        out['x_cc'][a:b] = tx + r * np.cos(az + myaw)
+        out['y_cc'][a:b] = ty + r * np.sin(az + myaw)
+        out['rcs'][a:b] = rng.normal(0, 10, n)
+        out['timestamp'][a:b] = t0 + s * 15500 + rng.integers(0, 200)
+        out['sensor_id'][a:b] = sid
+        tracked = moving & (rng.random(n) < 0.8)
+        keys = np.where(tracked, rng.integers(1, 9, n), 0)
+        out['track_key'][a:b] = keys
+        tid[a:b] = [b'' if k == 0 else b'trk%d' % k for k in keys]
+        out['label_id'][a:b] = np.where(tracked, rng.integers(0, 11, n), 11)
+        # ego motion to the next scan (~15.5 ms)
+        dt = 0.0155
+        x += vx_e * dt * np.cos(yaw)
+        y += vx_e * dt * np.sin(yaw)
+        yaw += yr * dt
+    out.update(n_scans=n_scans, scan_ptr=ptr, mount=mount, odometry=odo, track_id_bytes=tid)
+    return out

@@ -326,6 +326,45 @@ int rg_segment_amax_backward(const float* msg, int ldm, int C, const int* seg_pt
                              const float* d_agg, int ldd, float* d_msg, int ldo, void* stream);
 
 
+/* ------------------------------------------------------------ real-data front-end */
+
+/* read_data.extract_and_sync_radar_data + extract_frame (read_data.py:227-303, 442-486)
+ * for a window of n_scans scans already in device memory (measurements of scan s at
+ * [scan_ptr[s], scan_ptr[s+1])): the stationary gate of identify_stationary_measurements
+ * (meas_selection.py:22-70, 169-200, |predicted - measured range rate| <= gamma; ransac
+ * not supported), vr_cartesian_vf (meas_sync.py:15-20) and the ego compensation into the
+ * window's current scan (meas_sync.py:23-103), float32 outputs.  A batch of windows is
+ * one call: scan_ref[s] = the current scan of scan s's window (NULL: one window whose
+ * current scan is the last).  mount: f64 [n_scans][3] (x, y, yaw); odometry: f64
+ * [n_scans][5] (x_seq, y_seq, yaw_seq, vx, yaw_rate).  stationary: u8 [n_meas]. */
+int rg_frontend_sync(const float* x_cc, const float* y_cc, const float* azimuth_sc,
+                     const float* vr, const float* vr_compensated, const int* scan_ptr,
+                     int n_scans, const int* scan_ref, const double* mount,
+                     const double* odometry,
+                     float gamma_stationary, int n_meas, float* px, float* py, float* vx,
+                     float* vy, uint8_t* stationary, void* stream);
+/* compute_ground_truth (compute_node_labels.py:50-105): class labels (tracked: the
+ * old -> new label id map, labels.py:90-100; untracked: FALSE = 6 / STATIC = 7 by the
+ * stationary flag) and offsets to each track's mean position (track_key int32, 0 = no
+ * track, keys <= n_tracks).  f32 outputs. */
+size_t rg_frontend_labels_workspace_size(int n_tracks);
+int rg_frontend_labels(const int* track_key, int n_tracks, const int64_t* label_id,
+                       const uint8_t* stationary, const int* old_to_new, int n_old,
+                       const float* px, const float* py, int n_meas, float* cls,
+                       float* offset_x, float* offset_y, void* workspace,
+                       size_t workspace_bytes, void* stream);
+/* select_meas_within_the_grid (grid_features.py:162-174) + select_moving_data
+ * (graph_features.py:167-182): index[0..*n_selected) = the measurements inside
+ * [min_x, max_x) x [min_y, max_y) whose class is not static_id, in order.  With a batch
+ * of windows (measurements of window w at [win_ptr[w], win_ptr[w+1])), frame_ptr
+ * [n_windows + 1] receives each window's range of selected rows (the graph build's
+ * frame_ptr); both may be NULL. */
+size_t rg_frontend_select_workspace_size(int n_meas);
+int rg_frontend_select(const float* px, const float* py, const float* cls, int n_meas,
+                       float min_x, float max_x, float min_y, float max_y, float static_id,
+                       const int* win_ptr, int n_windows, int* frame_ptr, int* index,
+                       int* n_selected, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------ proposal branch */
 
 /* Predicted cluster centres (gnn_detector.py:164-167): unnormalize_gt_offsets
