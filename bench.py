@@ -55,6 +55,10 @@ PRESETS = {
     # L = 5 layers of C = 128, complete graph per object
     'cls': dict(frames=64, nodes=200, k=0, layers=5, graph='objects', eps2=0.0, cpu_frames=4,
                 cpu_warm=1),
+    # real-data front-end: 'frames' = windows per GPU of 10 scans
+    # (configuration_radarscenes_gnn.yml:12), 'nodes' = mean measurements per scan
+    'frontend': dict(frames=64, nodes=160, k=0, layers=10, graph='scans', eps2=0.0,
+                     cpu_frames=16, cpu_warm=2),
 }
 
 
@@ -66,7 +70,8 @@ def parse():
     p.add_argument('--config', default='c2', choices=sorted(PRESETS),
                    help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress; '
                         'c4: config 4 training step (forward + backward + SGD, DDP); '
-                        'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4)')
+                        'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4); '
+                        'frontend: the real-data front-end (SURVEY 8(f) rank 3)')
     p.add_argument('--frames', type=int, default=None, help='frames per GPU')
     p.add_argument('--nodes', type=int, default=None)
     p.add_argument('--k', type=int, default=None)
@@ -494,6 +499,88 @@ def cls_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def frontend_main(args, world, rank, local):
+    """Real-data front-end: a batch of windows of 10 radar scans in
+    HBM -> stationary gate, ego compensation, ground truth, grid + moving selection ->
+    the dynamic frames (frame_ptr) the graph build takes.  One step = the batch; the
+    step synchronises once (the selected count), as the reference's boolean indexing."""
+    from graph_neural_network_for_radar_perception_amd import frontend
+    dev = torch.device('cuda', torch.cuda.current_device())
+    seeds = rank_frame_seeds(rank, args.frames, args.seed)
+    wins = [synthetic.make_scan_window(s, n_scans=args.layers, mean_meas=args.nodes)
+            for s in seeds]
+    batch = frontend.scan_window_batch(wins, dev)
+    n_meas = batch.n_meas
+
+    def step(events=None):
+        if events is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            events.append(('sync:start', ev))
+        d = frontend.extract_and_sync_radar_data(batch)
+        if events is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            events.append(('sync:end', ev))
+        gt = frontend.compute_ground_truth(d)
+        return frontend.select_dynamic(d, gt)
+
+    for _ in range(args.warmup):
+        dd, _ = step()
+    torch.cuda.synchronize()
+    n_dyn = int(dd['frame_ptr'][-1].item())
+    events = []
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(events)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    durs = event_durations(events)
+    total = sum_over_ranks(args.frames * args.steps, world)
+    ms = float(np.mean(durs['sync']))
+    nbytes = n_meas * (5 * 4 + 4 * 4 + 1)   # 5 f32 fields in, px py vx vy out, flag
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    line = {
+        'metric': 'radar windows/sec through the real-data front-end (SURVEY §8(f) rank 3)',
+        'value': round(total / elapsed, 1), 'unit': 'windows/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32/f64',
+        'data': 'synthetic RadarScenes-shaped scan windows (synthetic.make_scan_window)',
+        'config': {'workload': f'frontend: {args.frames} windows x {args.layers} scans x '
+                               f'~{args.nodes} measurements per GPU; step = sync (gate, ego '
+                               'compensation) + labels + grid/moving selection',
+                   'windows_per_gpu': args.frames, 'measurements_per_gpu': n_meas,
+                   'dynamic_per_gpu': n_dyn,
+                   'parallelism': f'window-parallel x{world} (no collective in the step)'},
+        'roofline': {'kernel': 'frontend_sync_kernel (rg_frontend_sync)', 'bound': 'hbm',
+                     'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'avg_ms': round(ms, 4), 'bytes_per_launch': nbytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import frontend_ref  # the CPU baseline leg only
+        sample = wins[:args.cpu_frames]
+        t = time.perf_counter()
+        for w in sample:
+            w2 = dict(w)
+            w2['track_key'] = frontend._host_track_keys(w)
+            full = frontend_ref.sync_window(w2)
+            frontend_ref.select_dynamic(full, frontend_ref.ground_truth(full, w2['track_key']))
+        dt = time.perf_counter() - t
+        line['cpu_baseline'] = {'value': round(len(sample) / dt, 1), 'unit': 'windows/s',
+                                'cores': 1, 'kind': 'port',
+                                'sample': f'{len(sample)} windows through the numpy oracle '
+                                          '(oracle/frontend_ref.py), one thread'}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist()
@@ -503,6 +590,8 @@ def main():
         return train_main(args, world, rank, local)
     if args.config == 'cls':
         return cls_main(args, world, rank, local)
+    if args.config == 'frontend':
+        return frontend_main(args, world, rank, local)
     dev = torch.device('cuda', torch.cuda.current_device())  # set from LOCAL_RANK in setup_dist
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
     from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
