@@ -312,9 +312,27 @@ __device__ __forceinline__ void pack_next(const f32x16 (&acc)[MT], bf16x8_t (&nb
     }
 }
 
-template <int MT>
+// SPEC bit 30: the launch checked on the host that the output is bf16 with 4-wide
+// vector rows, full width and no residual (the encoders' x and e), so the epilogue is
+// plain packed stores -- no run-time branches or kernel arguments live across the tile
+static constexpr int SPEC_PLAIN_OUT = 1 << 30;
+
+template <int MT, bool PLAIN = false>
 __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& a, long row,
                                           int h) {
+  if constexpr (PLAIN) {
+    uint16_t* o = (uint16_t*)a.out + (size_t)row * a.ld_out;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 w;
+        w.x = bf2(acc[m][4 * g], acc[m][4 * g + 1]);
+        w.y = bf2(acc[m][4 * g + 2], acc[m][4 * g + 3]);
+        *(uint2*)(o + 32 * m + 8 * g + 4 * h) = w;
+      }
+    return;
+  }
   const int out = a.out_real;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -379,7 +397,7 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
     run_chain<SPEC, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, nrm,
                                                                              row, valid, lane);
   } else {
-    if (valid) store_out<MT>(acc, a, row, lane >> 5);
+    if (valid) store_out<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, lane >> 5);
   }
 }
 
@@ -410,7 +428,7 @@ __device__ __forceinline__ void run_chain_pair(const FArgs& a,
     run_chain<SPEC, ((fast_bytes(K, N) + 15) & ~15), 1, N, Rest...>(a, nb, lds, nrm, row, valid,
                                                                     lane);
   } else {
-    if (valid) store_out<MT>(acc, a, row, lane >> 5);
+    if (valid) store_out<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, lane >> 5);
   }
 }
 
@@ -513,7 +531,7 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
     pack_next<MT1>(acc, nb);
     run_chain<SPEC, OFF2, 2, N1, Rest...>(a, nb, lds, nrm, row, valid, lane);
   } else {
-    if (valid) store_out<MT1>(acc, a, row, h);
+    if (valid) store_out<MT1, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, h);
   }
 }
 
@@ -648,15 +666,27 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
 #ifndef RG_ENC_FT
 #define RG_ENC_FT 768  // edge-encoder workgroup: 3 waves/SIMD (167 VGPRs, 13 dwords spilled) beat 2 (179) by 4 %
 #endif
+// output of width nl written as bf16 rows of 4-wide vectors, no residual
+static bool plain_out(const FArgs& a, int nl) {
+  return !a.res && !a.out_f32 && a.out_vec && a.out_real == nl;
+}
+
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
 static int dispatch(const Key& k, const FArgs& a, hipStream_t st) {
 #define RG_FAST(FT, SP, MODE, F32, W0, W1, ...)                                           \
   if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}))                                        \
     return k.spec == (SP) ? launch<MODE, F32, W0, W1, (SP), FT, __VA_ARGS__>(a, st)       \
                           : launch<MODE, F32, W0, W1, -1, 512, __VA_ARGS__>(a, st);
+  // the same with a plain bf16 output epilogue when the call allows it (SPEC_PLAIN_OUT)
+#define RG_FAST_P(FT, SP, MODE, F32, W0, W1, NL, ...)                                      \
+  if (match(k, MODE, F32, W0, W1, {__VA_ARGS__}) && k.spec == (SP) && plain_out(a, NL))  \
+    return launch<MODE, F32, W0, W1, (SP) | SPEC_PLAIN_OUT, FT, __VA_ARGS__>(a, st);
   constexpr int L = ACT_LEAKY;
   // node / edge encoders (graph_feature_encoding, gnn_blocks.py:19-42: block 0 is not
   // normalised)
+  RG_FAST_P(512, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 64, 256, 128, 64)
+  RG_FAST_P(RG_ENC_FT, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 64, 256, 128, 128,
+            64)
   RG_FAST(512, spec(L, 0b110, 0b111), RG_IN_DENSE | FUSE01, 1, 6, 0, 256, 128, 64)
   RG_FAST(RG_ENC_FT, spec(L, 0b1110, 0b1111), RG_IN_DENSE | FUSE01, 1, 7, 0, 256, 128, 128, 64)
   // message MLP on cat(x_i, x_j, e) and update MLP on cat(x, agg) (msg_mlp_hidden_dim 128)
