@@ -73,6 +73,8 @@ _SIGNATURES = {
     'rg_build_graph': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
     'rg_node_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _P, _P]),
     'rg_edge_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
+    'rg_pack_kinematics': (_I, [_P, _P, _P, _P, _I, _P, _P]),
+    'rg_edge_features_packed': (_I, [_P, _P, _P, _P, _P, _L, _P, _P]),
     'rg_link_pairs_workspace_size': (_S, [_I]),
     'rg_link_pairs': (_I, [_P, _P, _I, _P, _P, _P, _L, _P, _P, _S, _P]),
     'rg_pairs_from_edge_index_workspace_size': (_S, [_L]),

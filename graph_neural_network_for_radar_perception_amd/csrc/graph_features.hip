@@ -118,6 +118,50 @@ __global__ __launch_bounds__(256) void edge_features_kernel(
   }
 }
 
+// The same from node kinematics packed as float4 (px, py, vx, vy): two gathers per
+// endpoint (the float4 and the timestamp) instead of five separate arrays (the kernel
+// above is bound by its ten gathered loads per edge).
+__global__ __launch_bounds__(256) void pack_kinematics_kernel(
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vx,
+    const float* __restrict__ vy, int n, float4* __restrict__ kin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) kin[i] = make_float4(px[i], py[i], vx[i], vy[i]);
+}
+
+__global__ __launch_bounds__(256) void edge_features_packed_kernel(
+    const float4* __restrict__ kin, const int64_t* __restrict__ ts, const int* __restrict__ src,
+    const int* __restrict__ dst, const int* __restrict__ n_edges_dev, long n_edges,
+    float* __restrict__ out) {
+  __shared__ float4 stage4[256 * 7 / 4];
+  float* stage = (float*)stage4;
+  const long E = min(n_edges_dev ? (long)*n_edges_dev : n_edges, n_edges);
+  for (long b0 = (long)blockIdx.x * 256; b0 < E; b0 += (long)gridDim.x * 256) {
+    const long p = b0 + threadIdx.x;
+    if (p < E) {
+      const int s = src[p];
+      const int d = dst[p];
+      const float4 ks = kin[s], kd = kin[d];
+      const int64_t tsd = ts[s] - ts[d];
+      const float dx = div10_rn((ks.x - kd.x));
+      const float dy = div10_rn((ks.y - kd.y));
+      const float dl = div10_rn(sqrt_rn(((dx * dx) + (dy * dy))));
+      const float dvx = (ks.z - kd.z);
+      const float dvy = (ks.w - kd.w);
+      const float dv = sqrt_rn(((dvx * dvx) + (dvy * dvy)));
+      const float dt = (float)((double)tsd * 1e-6);
+      float* o = stage + threadIdx.x * 7;
+      o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv; o[6] = dt;
+    }
+    __syncthreads();
+    const int n = (int)min(256L, E - b0) * 7;
+    const int n4 = ((uintptr_t)out & 15) == 0 ? n / 4 : 0;
+    float4* o4 = (float4*)(out + (size_t)b0 * 7);
+    for (int i = threadIdx.x; i < n4; i += 256) o4[i] = stage4[i];
+    for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) out[(size_t)b0 * 7 + i] = stage[i];
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ link pairs
 __global__ void pairs_count(const int* __restrict__ row_ptr, const int* __restrict__ col,
                             int n_nodes, int* __restrict__ cnt) {
@@ -292,6 +336,29 @@ extern "C" int rg_edge_features(const float* px, const float* py, const float* v
   if (blocks > 16384) blocks = 16384;
   edge_features_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(px, py, vx, vy, timestamp, src, dst,
                                                                 n_edges_dev, n_edges, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_pack_kinematics(const float* px, const float* py, const float* vx,
+                                  const float* vy, int n_nodes, void* kin, void* stream) {
+  RG_REQUIRE(n_nodes >= 0 && ((uintptr_t)kin & 15) == 0, RG_ERR_ARG,
+             "rg_pack_kinematics: n_nodes=%d, kin must be 16-B aligned", n_nodes);
+  if (n_nodes == 0) return RG_OK;
+  pack_kinematics_kernel<<<ceil_div(n_nodes, 256), 256, 0, (hipStream_t)stream>>>(
+      px, py, vx, vy, n_nodes, (float4*)kin);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_edge_features_packed(const void* kin, const int64_t* timestamp, const int* src,
+                                       const int* dst, const int* n_edges_dev, long n_edges,
+                                       float* out, void* stream) {
+  if (n_edges <= 0) return RG_OK;
+  long blocks = (n_edges + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  edge_features_packed_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(
+      (const float4*)kin, timestamp, src, dst, n_edges_dev, n_edges, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -401,15 +401,22 @@ def node_features(frame_arrays: dict, ball_degree, frame_ptr, n_frames, cfg) -> 
 
 
 def edge_features(frame_arrays: dict, src, dst, n_edges_dev, n_edges: int) -> torch.Tensor:
-    """compute_edge_features for edges src[p] -> dst[p] (rg_edge_features)."""
+    """compute_edge_features for edges src[p] -> dst[p]: the node kinematics packed once
+    (rg_pack_kinematics), then rg_edge_features_packed (two gathers per endpoint)."""
     lib = nat.lib()
     px = frame_arrays['meas_px']
-    out = torch.empty((max(n_edges, 1), 7), dtype=torch.float32, device=px.device)
-    nat.check(lib.rg_edge_features(
-        px.data_ptr(), frame_arrays['meas_py'].data_ptr(), frame_arrays['meas_vx'].data_ptr(),
-        frame_arrays['meas_vy'].data_ptr(), frame_arrays['meas_timestamp'].data_ptr(),
-        src.data_ptr(), dst.data_ptr(), nat.ptr(n_edges_dev), n_edges, out.data_ptr(),
-        nat.stream_ptr(px.device)), 'rg_edge_features')
+    dev = px.device
+    out = torch.empty((max(n_edges, 1), 7), dtype=torch.float32, device=dev)
+    n = int(px.shape[0])
+    kin = torch.empty((max(n, 1), 4), dtype=torch.float32, device=dev)
+    st = nat.stream_ptr(dev)
+    nat.check(lib.rg_pack_kinematics(px.data_ptr(), frame_arrays['meas_py'].data_ptr(),
+                                     frame_arrays['meas_vx'].data_ptr(),
+                                     frame_arrays['meas_vy'].data_ptr(), n, kin.data_ptr(), st),
+              'rg_pack_kinematics')
+    nat.check(lib.rg_edge_features_packed(
+        kin.data_ptr(), frame_arrays['meas_timestamp'].data_ptr(), src.data_ptr(), dst.data_ptr(),
+        nat.ptr(n_edges_dev), n_edges, out.data_ptr(), st), 'rg_edge_features_packed')
     return out
 
 

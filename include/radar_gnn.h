@@ -126,6 +126,15 @@ int rg_edge_features(const float* px, const float* py, const float* vx, const fl
                      const int64_t* timestamp, const int* src, const int* dst,
                      const int* n_edges_dev, long n_edges, float* out, void* stream);
 
+/* rg_edge_features from node kinematics packed once per batch: kin = float4[n_nodes]
+ * (px, py, vx, vy) from rg_pack_kinematics (16-B aligned).  Same results, two gathers
+ * per edge endpoint instead of five. */
+int rg_pack_kinematics(const float* px, const float* py, const float* vx, const float* vy,
+                       int n_nodes, void* kin, void* stream);
+int rg_edge_features_packed(const void* kin, const int64_t* timestamp, const int* src,
+                            const int* dst, const int* n_edges_dev, long n_edges, float* out,
+                            void* stream);
+
 /* Undirected link pairs of edge_formation (gnn_blocks.py:295-296):
  * nonzero(triu(adj,1)) row-major == CSR positions with col > row.
  * pair_ptr int32[n_nodes+1]; pair_src/pair_dst int32[capacity]; n_pairs int32[1]. */
