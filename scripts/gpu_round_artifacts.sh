@@ -10,7 +10,7 @@ PYTEST_ARGS="--timeout 300 --timeout-method thread" bash scripts/gpu_check.sh ||
 echo "== prof"; bash scripts/gpu_prof.sh || exit $?
 echo "== pmc"; bash scripts/gpu_pmc.sh || exit $?
 echo "== sq"; bash scripts/gpu_sq.sh || exit $?
-for c in c5 c4 cls; do
+for c in c5 c4 cls frontend; do
   echo "== preset $c"
   timeout -k 10 400 python bench.py --config $c > gpurun_out/presets/bench_$c.log 2>&1 || exit $?
   tail -1 gpurun_out/presets/bench_$c.log | cut -c1-200
