@@ -942,9 +942,19 @@ __global__ void grid_scatter_t(const float* __restrict__ px, const float* __rest
 // bit-identically from the coordinates), so the test reads two small L2-resident
 // arrays instead of a cache line of the bitset per pair, and only a missing bit costs
 // an atomic.
+// row j's position and kk-th key in one 16-B record, so knn_mark gathers one line per
+// pair instead of three (px[j], py[j], kth[j])
+__global__ void node_key_pack(const float* __restrict__ px, const float* __restrict__ py,
+                              const int2* __restrict__ kth, int n, int4* __restrict__ nk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int2 k = kth[i];
+    nk[i] = make_int4(__float_as_int(px[i]), __float_as_int(py[i]), k.x, k.y);
+  }
+}
+
 __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict__ knn_idx,
-                         const int* __restrict__ knn_cnt, const float* __restrict__ px,
-                         const float* __restrict__ py, const int2* __restrict__ kth, int K,
+                         const int* __restrict__ knn_cnt, const int4* __restrict__ nk, int K,
                          int n_nodes, uint32_t* __restrict__ bits, int W) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int i = (int)(t / K);
@@ -956,9 +966,10 @@ __global__ void knn_mark(const int* __restrict__ row_base, const int* __restrict
   const int jl = knn_idx[(size_t)i * K + s];
   if (jl == il || jl < 0) return;
   const int j = b + jl;
-  const float d = sqdist(px[j], py[j], px[i], py[i]);
-  const int2 kj = kth[j];
-  if (!key_less(__int_as_float(kj.x), kj.y, d, il)) return;  // (d, il) <= row j's kk-th key
+  const int4 rj = nk[j], ri = nk[i];
+  const float d = sqdist(__int_as_float(rj.x), __int_as_float(rj.y), __int_as_float(ri.x),
+                         __int_as_float(ri.y));
+  if (!key_less(__int_as_float(rj.z), rj.w, d, il)) return;  // (d, il) <= row j's kk-th key
   atomicOr(bits + (size_t)j * W + (il >> 5), 1u << (il & 31));
 }
 
@@ -1131,6 +1142,7 @@ struct GraphWs {
   int* cell_start_t;
   float4* pts_t;
   int* cursor_t;       // arrival counters of the column-major scatter
+  int4* nkey;          // per row: (x, y, kk-th key) for knn_mark
   int cpf;
   long n_cells;
 };
@@ -1171,7 +1183,9 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
   char* p_st = take((size_t)(n_cells + 1) * sizeof(int));
   char* p_pq = take((size_t)n_nodes * sizeof(float4));
   char* p_cv = take((size_t)n_cells * sizeof(int));
+  char* p_nk = take((size_t)n_nodes * sizeof(int4));
   if (ws) {
+    ws->nkey = (int4*)p_nk;
     ws->cursor_t = (int*)p_cv;
     ws->kth = (int2*)p_kt;
     ws->cell_cnt_t = (int*)p_ct;
@@ -1295,8 +1309,9 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   RG_LAUNCH_CHECK();
   if (mode != RG_GRAPH_RADIUS) {
     long tot = (long)n_nodes * K;
-    knn_mark<<<ceil_div(tot, 256), 256, 0, st>>>(ws.row_base, ws.knn_idx, ws.knn_cnt, px, py,
-                                                  ws.kth, K, n_nodes, ws.bits, W);
+    node_key_pack<<<ceil_div(n_nodes, 256), 256, 0, st>>>(px, py, ws.kth, n_nodes, ws.nkey);
+    knn_mark<<<ceil_div(tot, 256), 256, 0, st>>>(ws.row_base, ws.knn_idx, ws.knn_cnt, ws.nkey,
+                                                  K, n_nodes, ws.bits, W);
     RG_LAUNCH_CHECK();
   }
   row_count<<<ceil_div(n_nodes, 4), 256, 0, st>>>(ws.row_base, frame_ptr, ws.bits, W, n_nodes,
