@@ -979,19 +979,21 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
-// one wave per row: number of set bits in the row's valid columns
+// 16 lanes per row (a row of a 3 000-point frame is 94 words: one wave per row left
+// most lanes idle on the second pass): number of set bits in the row
 __global__ __launch_bounds__(256) void row_count(const int* __restrict__ row_base,
                                                  const int* __restrict__ frame_ptr_unused,
                                                  const uint32_t* __restrict__ bits, int W,
                                                  int n_nodes, int* __restrict__ cnt) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n_nodes) return;
+  const int sl = threadIdx.x & 15;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (row >= n_nodes) return;  // group-uniform
   const uint32_t* rb = bits + (size_t)row * W;
   int c = 0;
-  for (int w = lane; w < W; w += 64) c += __popc(rb[w]);
-  c = wave_sum(c);
-  if (lane == 0) cnt[row] = c;
+  for (int w = sl; w < W; w += 16) c += __popc(rb[w]);
+#pragma unroll
+  for (int d = 8; d > 0; d >>= 1) c += __shfl_xor(c, d, 16);
+  if (sl == 0) cnt[row] = c;
 }
 
 // one wave per row: emit ascending set columns as global node ids
@@ -1314,8 +1316,8 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
                                                   K, n_nodes, ws.bits, W);
     RG_LAUNCH_CHECK();
   }
-  row_count<<<ceil_div(n_nodes, 4), 256, 0, st>>>(ws.row_base, frame_ptr, ws.bits, W, n_nodes,
-                                                  ws.cnt);
+  row_count<<<ceil_div(n_nodes, 16), 256, 0, st>>>(ws.row_base, frame_ptr, ws.bits, W, n_nodes,
+                                                   ws.cnt);
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(ws.cnt, n_nodes, row_ptr, n_edges_out, ws.scan_ws, st);
   if (rc) return rc;
