@@ -996,35 +996,36 @@ __global__ __launch_bounds__(256) void row_count(const int* __restrict__ row_bas
   if (sl == 0) cnt[row] = c;
 }
 
-// one wave per row: emit ascending set columns as global node ids
+// 16 lanes per row: emit ascending set columns as global node ids (each pass of 16
+// words: popcounts, a 16-lane exclusive scan, every lane writes its word's columns)
 __global__ __launch_bounds__(256) void row_emit(const int* __restrict__ row_base,
                                                 const uint32_t* __restrict__ bits, int W,
                                                 int n_nodes, const int* __restrict__ row_ptr,
                                                 int* __restrict__ col, long cap) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n_nodes) return;
+  const int sl = threadIdx.x & 15;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (row >= n_nodes) return;  // group-uniform
   const uint32_t* rb = bits + (size_t)row * W;
   const int b = row_base[row];
   long pos = row_ptr[row];
   if ((long)row_ptr[row + 1] > cap) return;  // overflow: caller sees n_edges > capacity
-  for (int w0 = 0; w0 < W; w0 += 64) {
-    const int w = w0 + lane;
+  for (int w0 = 0; w0 < W; w0 += 16) {
+    const int w = w0 + sl;
     uint32_t word = w < W ? rb[w] : 0u;
-    int c = __popc(word);
+    const int c = __popc(word);
     int inc = c;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      int t = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += t;
+    for (int d = 1; d < 16; d <<= 1) {
+      const int t = __shfl_up(inc, d, 16);
+      if (sl >= d) inc += t;
     }
     long p = pos + inc - c;
     while (word) {
-      int bit = __ffs(word) - 1;
+      const int bit = __ffs(word) - 1;
       word &= word - 1;
       col[p++] = b + w * 32 + bit;
     }
-    pos += __shfl(inc, 63, 64);
+    pos += __shfl(inc, 15, 16);
   }
 }
 
@@ -1321,7 +1322,7 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(ws.cnt, n_nodes, row_ptr, n_edges_out, ws.scan_ws, st);
   if (rc) return rc;
-  row_emit<<<ceil_div(n_nodes, 4), 256, 0, st>>>(ws.row_base, ws.bits, W, n_nodes, row_ptr, col,
+  row_emit<<<ceil_div(n_nodes, 16), 256, 0, st>>>(ws.row_base, ws.bits, W, n_nodes, row_ptr, col,
                                                  col_capacity);
   RG_LAUNCH_CHECK();
   return RG_OK;
