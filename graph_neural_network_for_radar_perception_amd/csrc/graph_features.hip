@@ -181,15 +181,16 @@ __global__ __launch_bounds__(256) void pairs_emit(const int* __restrict__ row_pt
                                                   const int* __restrict__ pair_ptr,
                                                   int* __restrict__ ps, int* __restrict__ pd,
                                                   long cap) {
-  const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n_nodes; row += nw) {
+  // 16 lanes per row (a kNN row has ~k/2 + a few pairs: a wave per row left most idle)
+  const int lane = threadIdx.x & 15;
+  const int nw = gridDim.x * 16;
+  for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < n_nodes; row += nw) {
     const int e = row_ptr[row + 1];
     const int q0 = pair_ptr[row], q1 = pair_ptr[row + 1];
     if ((long)q1 > cap) continue;
     const int n = q1 - q0;
     const int start = e - n;  // cols > row are the row's suffix
-    for (int t = lane; t < n; t += 64) {
+    for (int t = lane; t < n; t += 16) {
       ps[q0 + t] = row;
       pd[q0 + t] = col[start + t];
     }
@@ -384,7 +385,7 @@ extern "C" int rg_link_pairs(const int* row_ptr, const int* col, int n_nodes, in
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(cnt, n_nodes, pair_ptr, n_pairs, sws, st);
   if (rc) return rc;
-  int blocks = ceil_div(n_nodes, 4);
+  int blocks = ceil_div(n_nodes, 16);
   if (blocks > 8192) blocks = 8192;
   pairs_emit<<<blocks, 256, 0, st>>>(row_ptr, col, n_nodes, pair_ptr, pair_src, pair_dst,
                                      pair_capacity);
