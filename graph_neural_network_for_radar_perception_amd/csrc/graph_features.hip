@@ -269,11 +269,12 @@ __global__ void dense_adj_set(const int* __restrict__ row_ptr, const int* __rest
 // destination of each destination-major edge)
 __global__ __launch_bounds__(256) void csr_rows_kernel(const int* __restrict__ row_ptr, int n_rows,
                                                        int* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n_rows; row += nw) {
+  // 16 lanes per row: graph rows hold tens of edges, so a 64-lane wave per row idled most lanes
+  const int lane = threadIdx.x & 15;
+  const int nw = gridDim.x * 16;
+  for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < n_rows; row += nw) {
     const int b = row_ptr[row], e = row_ptr[row + 1];
-    for (int p = b + lane; p < e; p += 64) out[p] = row;
+    for (int p = b + lane; p < e; p += 16) out[p] = row;
   }
 }
 
@@ -466,8 +467,8 @@ extern "C" int rg_gather_rows_f32(const float* in, const int* idx, long rows, in
 
 extern "C" int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream) {
   if (n_rows <= 0) return RG_OK;
-  int blocks = ceil_div(n_rows, 4);
-  if (blocks > 8192) blocks = 8192;
+  int blocks = ceil_div(n_rows, 16);
+  if (blocks > 16384) blocks = 16384;
   csr_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(row_ptr, n_rows, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
