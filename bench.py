@@ -5,9 +5,13 @@ already resident in HBM, through the whole hot path: kNN graph build + ball
 query, node / edge input features, node and edge encoders, L message-passing
 layers, the four task heads (graph_features.py:58-164 + gnn_detector.py:141-201).
 
-Default workload = BASELINE config 2: 64 frames x 3000 nodes per GPU, k = 32,
-L = 6, bf16 compute (fp32 accumulation / normalisation statistics), random-init
-weights of the yml architecture (no checkpoint is needed for throughput).
+Default workload = the metric's own configuration **M** (SURVEY.md §8(d)): 64 frames
+x 3000 nodes per GPU, the yml graph (k = 10, eps^2 = 25 -> E ~ 37.8k edges per frame),
+L = 7, **fp32** compute (the reference precision; parity 1e-4), the trained
+checkpoint's weights (`1718175257362`, committed as the `w/*` arrays of
+tests/golden/model_trained_N50.npz -- nothing is read from the reference at run time).
+The same run also times BASELINE config 2 (64 x 3000, k = 32, L = 6, bf16) as the extra
+key ``c2_bf16``.
 Multi-GPU (torchrun, one process per GPU): every rank owns its own 64 frames
 (frame-parallel, weak scaling, no collective in the timed region; barrier +
 max-over-ranks timing only).
@@ -43,10 +47,14 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}   # dense MFMA peaks (same do
 
 # workloads; k is unused by the pure radius graph
 PRESETS = {
+    # the metric's configuration (BASELINE.json metric "N~3k nodes, E~30k edges"; yml k = 10,
+    # L = 7, configuration_radarscenes_gnn.yml:14,58), fp32, trained weights
+    'm': dict(frames=64, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=5,
+              cpu_warm=2, dtype='fp32', weights='trained'),
     'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
-               cpu_warm=2),
+               cpu_warm=2, dtype='bf16', weights='random'),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
-               cpu_warm=1),
+               cpu_warm=1, dtype='bf16', weights='random'),
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
     'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
                cpu_warm=1),
@@ -67,8 +75,9 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--config', default='c2', choices=sorted(PRESETS),
-                   help='c2: BASELINE config 2 (default); c5: config 5 radius-graph stress; '
+    p.add_argument('--config', default='m', choices=sorted(PRESETS),
+                   help='m: the metric configuration (default; fp32, trained weights); '
+                        'c2: BASELINE config 2 (bf16); c5: config 5 radius-graph stress; '
                         'c4: config 4 training step (forward + backward + SGD, DDP); '
                         'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4); '
                         'frontend: the real-data front-end (SURVEY 8(f) rank 3)')
@@ -77,8 +86,12 @@ def parse():
     p.add_argument('--k', type=int, default=None)
     p.add_argument('--layers', type=int, default=None)
     p.add_argument('--dtype', default=None, choices=['bf16', 'fp32'],
-                   help='compute dtype (default bf16; fp32 for --config cls, the reference '
-                        'precision of the classifier)')
+                   help='compute dtype (default: the preset\'s -- fp32 for m / c4 / cls, '
+                        'bf16 for c2 / c5)')
+    p.add_argument('--weights', default=None, choices=['trained', 'random'],
+                   help='trained: the checkpoint committed in tests/golden (L = 7 only)')
+    p.add_argument('--no-extra', action='store_true',
+                   help='m: skip the extra BASELINE config 2 (bf16) measurement')
     p.add_argument('--cpu-frames', type=int, default=None,
                    help='CPU baseline sample (timed frames)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -88,7 +101,9 @@ def parse():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
     if a.dtype is None:
-        a.dtype = 'fp32' if a.config == 'cls' else 'bf16'
+        a.dtype = 'bf16' if a.config in ('c2', 'c5') else 'fp32'
+    if a.weights is None:
+        a.weights = 'random'
     return a
 
 
@@ -170,11 +185,66 @@ def scatter_aggregate_bench(gb, E, N, steps):
     return out
 
 
-def make_model(cfg, device):
+TRAINED_FIXTURE = os.path.join(REPO, 'tests', 'golden', 'model_trained_N50.npz')
+
+
+def model_state(cfg, weights: str) -> dict:
+    """CPU state_dict of Model_Training: the trained checkpoint (the `w/*` arrays of the
+    committed fixture, written by tests/golden/make_golden.py from the reference's
+    model_weights/gnn/1718175257362) or the seeded random init of the yml architecture."""
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
     torch.manual_seed(1234)
-    m = Model_Training(cfg, device).to(device)
-    return m.pred.eval().requires_grad_(False)
+    m = Model_Training(cfg, 'cpu')
+    if weights == 'trained':
+        d = np.load(TRAINED_FIXTURE)
+        sd = {k[2:]: torch.from_numpy(np.array(d[k])) for k in d.files if k.startswith('w/')}
+        m.load_state_dict(sd, strict=True)
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def make_model(cfg, device, sd):
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    m = Model_Training(cfg, 'cpu')
+    m.load_state_dict(sd, strict=True)
+    return m.to(device).pred.eval().requires_grad_(False)
+
+
+def _cgroup_cpu_limit():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs files), or None."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            return max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_threads() -> int:
+    """Every host core this process may use: the CPUs in its affinity
+    mask, capped by the cgroup CPU quota when one is set (more threads than the quota
+    only time-slice the same CPU time)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    lim = _cgroup_cpu_limit()
+    return min(n, lim) if lim else n
+
+
+T_START = time.perf_counter()
+
+
+def log(msg: str):
+    """Progress line on stderr (a long silent phase looks hung to the GPU harness)."""
+    print(f'[bench {time.perf_counter() - T_START:7.1f}s] {msg}', file=sys.stderr, flush=True)
 
 
 def event_durations(events):
@@ -226,17 +296,13 @@ def _cpu_model() -> str:
     return 'unknown'
 
 
-def cpu_baseline(args, cfg):
+def cpu_baseline(args, cfg, sd):
     """The oracle (numpy dense graph build + op-for-op torch fp32 forward, i.e. the
-    reference's own CPU algorithm) on a bounded sample of the same workload
-    (2 warm-up frames, median of the timed frames, graph build and
-    forward reported separately, plus a 1-thread forward on one frame)."""
+    reference's own CPU algorithm) on a bounded sample of the same workload, same
+    weights (2 warm-up frames, median of the timed frames, graph build
+    and forward reported separately, on every host core, plus a 1-thread forward)."""
     from oracle import gnn_forward_ref, graph_features_ref as gref
-    threads = min(16, os.cpu_count() or 1)
-    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
-    torch.manual_seed(1234)
-    model = Model_Training(cfg, 'cpu')
-    sd = {k: v.detach() for k, v in model.state_dict().items()}
+    threads = host_threads()
     warm = args.cpu_warm
     frames = [synthetic.make_frame(args.nodes, args.seed + 10**6 + i)
               for i in range(args.cpu_frames + warm)]
@@ -263,6 +329,8 @@ def cpu_baseline(args, cfg):
     tb, tf = [], []
     for i, fr in enumerate(frames):
         b_, f_ = one(fr)
+        log(f'cpu baseline frame {i}: build {b_ * 1e3:.0f} ms, forward {f_ * 1e3:.0f} ms '
+            f'({threads} threads)')
         if i >= warm:
             tb.append(b_)
             tf.append(f_)
@@ -270,7 +338,7 @@ def cpu_baseline(args, cfg):
     fwd_ms = float(np.median(tf)) * 1e3
     total_ms = float(np.median(np.array(tb) + np.array(tf))) * 1e3
     f1 = None
-    if args.config == 'c2':  # (a 1-thread pass over a 20k-node frame would take minutes)
+    if args.graph == 'knn':  # (a 1-thread pass over a 20k-node frame would take minutes)
         torch.set_num_threads(1)
         _, f1 = one(frames[0])
         torch.set_num_threads(threads)
@@ -278,7 +346,9 @@ def cpu_baseline(args, cfg):
             'graph_build_ms': round(build_ms, 1), 'forward_ms': round(fwd_ms, 1),
             'forward_only_frames_per_s': round(1e3 / fwd_ms, 4),
             'forward_1thread_ms': None if f1 is None else round(f1 * 1e3, 1),
-            'cpu_model': _cpu_model(),
+            'forward_1thread_frames_per_s': None if f1 is None else round(1.0 / f1, 4),
+            'cpu_model': _cpu_model(), 'os_cpu_count': os.cpu_count(),
+            'affinity_cpus': len(os.sched_getaffinity(0)), 'cgroup_cpu_limit': _cgroup_cpu_limit(),
             'sample': f'{len(tb)} frame(s) of {args.nodes} nodes, {graph_desc(args)}, '
                       f'L={args.layers} after {warm} warm-up frame(s): oracle graph build (dense '
                       f'numpy, graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
@@ -302,7 +372,7 @@ def cpu_train_baseline(args, cfg):
     args.cpu_frames single-frame steps after args.cpu_warm warm-up frames."""
     from oracle import graph_features_ref as gref, train_ref
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(1234)
     sd = {k: v.detach() for k, v in Model_Training(cfg, 'cpu').state_dict().items()}
@@ -394,7 +464,7 @@ def cpu_classifier_baseline(args, cfg, sd):
     reference's CPU algorithm) on a bounded sample: args.cpu_frames samples after
     args.cpu_warm warm-up samples, median per sample."""
     from oracle import classifier_ref
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     torch.set_num_threads(threads)
     times = []
     for i in range(args.cpu_warm + args.cpu_frames):
@@ -581,37 +651,37 @@ def frontend_main(args, world, rank, local):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist()
-    if not torch.cuda.is_available():
-        raise SystemExit('bench.py needs a HIP device')
-    if args.config == 'c4':
-        return train_main(args, world, rank, local)
-    if args.config == 'cls':
-        return cls_main(args, world, rank, local)
-    if args.config == 'frontend':
-        return frontend_main(args, world, rank, local)
-    dev = torch.device('cuda', torch.cuda.current_device())  # set from LOCAL_RANK in setup_dist
+def workload_name(args) -> str:
+    head = {'m': 'M (the metric configuration, SURVEY §8(d))',
+            'c2': 'BASELINE config 2', 'c5': 'BASELINE config 5'}.get(args.config, args.config)
+    return (f'{head}: {args.frames} frame(s) x {args.nodes} nodes per GPU, {graph_desc(args)}, '
+            f'L={args.layers}, {args.dtype}, {args.weights} weights; step = graph build + '
+            'node/edge features + encoders + message passing + 4 heads')
+
+
+def gnn_measure(args, world, dev, cfg, sd, scatter=True):
+    """Warm up, then time args.steps full steps (barrier + synchronize on both sides,
+    max over ranks), then the forward alone; per-kernel HIP-event durations and the
+    roofline of the conv layer kernel."""
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
     from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
-
-    cfg = default_config(graph_convolution_stem_channels=[64] * args.layers,
-                         k_number_nearest_points=args.k)
     from graph_neural_network_for_radar_perception_amd import _native as nat
+    rank = dist.get_rank() if world > 1 else 0
     mode = nat.GRAPH_RADIUS if args.graph == 'radius' else nat.GRAPH_KNN
-    model = make_model(cfg, dev)
+    model = make_model(cfg, dev, sd)
     seeds = rank_frame_seeds(rank, args.frames, args.seed)
     frames = [synthetic.make_frame(args.nodes, s) for s in seeds]
     clusters = [synthetic.cluster_lists(args.nodes) for _ in seeds]
     batch = FrameBatch.from_frames(frames, clusters, device=dev)
     pipe = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
+    log(f'{args.config}: {args.frames} frames generated; warm-up')
 
     with torch.no_grad():
         for _ in range(args.warmup):
             gb, out = pipe.step(batch)
         torch.cuda.synchronize()
         E = int(gb.n_edges_dev.item())
+        log(f'{args.config}: warm-up done, E = {E}; timing {args.steps} steps')
         # ---- timed region: K full steps -----------------------------------------
         events = []
         barrier(world)
@@ -624,17 +694,18 @@ def main():
         elapsed = max_over_ranks(time.perf_counter() - t0, world)
         durs = event_durations(events)
         # ---- forward only (graph + features already built) -----------------------
+        barrier(world)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
             pipe.forward(batch, gb)
         torch.cuda.synchronize()
+        barrier(world)
         fwd_elapsed = max_over_ranks(time.perf_counter() - t1, world)
-        scatter = scatter_aggregate_bench(gb, E, args.frames * args.nodes, max(args.steps, 5))
+        sc = (scatter_aggregate_bench(gb, E, args.frames * args.nodes, max(args.steps, 5))
+              if scatter else None)
 
     frames_total = sum_over_ranks(args.frames * args.steps, world)
-    value = frames_total / elapsed
-    ms_step = elapsed / args.steps * 1e3
     N = args.frames * args.nodes
     s = 2 if args.dtype == 'bf16' else 4
     C = 64
@@ -644,7 +715,7 @@ def main():
                       len(ms) // args.steps}
     peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
     if 'conv_fused' in durs:
-        # fused conv layer: gather x_i, x_j, e -> msg MLP -> MFMA segment sum -> update MLP
+        # fused conv layer: gather x_i, x_j, e -> msg MLP -> segment sum -> update MLP
         ms = float(np.mean(durs['conv_fused']))
         flops = 65536.0 * E + 16384.0 * N                   # per layer
         nbytes = E * (C * s + 8) + N * (2 * C * s + 4)     # e rows + (src,dst) once; x in/out once
@@ -653,7 +724,7 @@ def main():
         kern['conv_fused'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
                                   flops_per_launch=flops, bytes_per_launch=nbytes)
         kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
-        traffic, tsrc = pmc_traffic(args, 'fused_conv_kernel')
+        traffic, tsrc = pmc_traffic(args, 'fused_conv')
     else:
         # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
         ms = float(np.mean(durs['message_chain']))
@@ -664,15 +735,18 @@ def main():
         kern['message_chain'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
                                      flops_per_launch=flops, bytes_per_launch=nbytes)
         kname = 'message_chain (rg_mlp_chain GATHER3, gnn_blocks.py:104-113)'
-        traffic, tsrc = None, None
+        traffic, tsrc = pmc_traffic(args, 'chain_kernel')
         agg_ms = float(np.mean(durs['segment_reduce']))
         agg_bytes = E * C * s + N * C * s + (N + 1) * 4     # SURVEY §8(d) B_agg
         agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
         kern['segment_reduce'].update(algorithmic_gbs=round(agg_gbs, 1), bytes_per_launch=agg_bytes,
                                       hbm_frac=round(agg_gbs / HBM_PEAK_GBS, 4))
-    enc_ms = float(np.mean(durs['edge_encoder']))
-    enc_flops = 118272.0 * E
-    kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2))
+    if 'edge_encoder' in durs:
+        enc_ms = float(np.mean(durs['edge_encoder']))
+        enc_flops = 118272.0 * E
+        kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2),
+                                    flops_per_launch=enc_flops,
+                                    mfma_frac=round(enc_flops / (enc_ms * 1e-3) / 1e12 / peak_tf, 4))
     frac_mfma = tf / peak_tf
     frac_hbm = gbs / HBM_PEAK_GBS
     if frac_mfma >= frac_hbm:
@@ -683,32 +757,79 @@ def main():
         roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': traffic,
                 'mfma_frac': round(frac_mfma, 4)}
+    roof.update(avg_ms=round(ms, 4), timing='HIP events on the launch stream, timed region')
     if traffic is not None:
         roof.update(traffic_unit='bytes/launch', traffic_source=tsrc,
                     algorithmic_bytes=nbytes, traffic_over_algorithmic=round(traffic / nbytes, 3))
+    F = (84992.0 * N + 118272.0 * E + args.layers * (65536.0 * E + 16384.0 * N) + 99456.0 * N
+         + 33024.0 * (E / 2) + 9088.0 * (N / 5))       # SURVEY §8(d) forward flops
+    fwd_ms = fwd_elapsed / args.steps * 1e3
+    return {'value': frames_total / elapsed, 'elapsed': elapsed, 'ms_step': elapsed / args.steps * 1e3,
+            'forward_fps': frames_total / fwd_elapsed, 'forward_ms': fwd_ms, 'E': E,
+            'forward_tflops': F / (fwd_ms * 1e-3) / 1e12, 'roof': roof, 'kern': kern,
+            'scatter': sc}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    if not torch.cuda.is_available():
+        raise SystemExit('bench.py needs a HIP device')
+    if args.config == 'c4':
+        return train_main(args, world, rank, local)
+    if args.config == 'cls':
+        return cls_main(args, world, rank, local)
+    if args.config == 'frontend':
+        return frontend_main(args, world, rank, local)
+    if args.weights == 'trained' and args.layers != 7:
+        raise SystemExit('--weights trained needs --layers 7 (the checkpoint has 7 conv blocks)')
+    dev = torch.device('cuda', torch.cuda.current_device())  # set from LOCAL_RANK in setup_dist
+    cfg = default_config(graph_convolution_stem_channels=[64] * args.layers,
+                         k_number_nearest_points=args.k)
+    sd = model_state(cfg, args.weights)
+    log(f'config {args.config}, dtype {args.dtype}, weights {args.weights}')
+    r = gnn_measure(args, world, dev, cfg, sd)
+    log(f'{args.config}: {r["value"]:.1f} frames/s, {r["ms_step"]:.3f} ms/step')
     line = {
-        'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
-        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_step, 3),
+        'metric': METRIC, 'value': round(r['value'], 2), 'unit': 'frames/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(r['ms_step'], 3),
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
-        'data': 'synthetic RadarScenes-shaped frames (SURVEY.md §8(d), seeded), random-init '
-                'weights of the yml architecture',
-        'config': {'workload': f'BASELINE config {args.config[1:]}: {args.frames} frame(s) x '
-                               f'{args.nodes} nodes per GPU, {graph_desc(args)}, L={args.layers}; '
-                               'step = graph build + node/edge features + encoders + message '
-                               'passing + 4 heads',
+        'data': 'synthetic RadarScenes-shaped frames (SURVEY.md §8(d), seeded); '
+                + ('weights of the trained checkpoint 1718175257362 (committed fixture)'
+                   if args.weights == 'trained' else 'random-init weights of the yml architecture'),
+        'config': {'workload': workload_name(args),
                    'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes,
                    'graph': args.graph, 'k': args.k if args.graph == 'knn' else None,
-                   'eps2': args.eps2, 'layers': args.layers, 'edges_per_gpu': E,
+                   'eps2': args.eps2, 'layers': args.layers, 'edges_per_gpu': r['E'],
+                   'edges_per_frame': round(r['E'] / args.frames, 1),
                    'parallelism': f'frame-parallel x{world} (no collective in the step)'},
-        'forward_only_frames_per_s': round(frames_total / fwd_elapsed, 2),
-        'roofline': roof,
-        'scatter_aggregate': dict(scatter, kernel='rg_segment_reduce sum over the step\'s '
+        'forward_only_frames_per_s': round(r['forward_fps'], 2),
+        'forward_algorithmic_tflops': round(r['forward_tflops'], 2),
+        'roofline': r['roof'],
+        'scatter_aggregate': dict(r['scatter'], kernel='rg_segment_reduce sum over the step\'s '
                                   'destination-major CSR (standalone; fused into conv_fused in '
-                                  'the bf16 step)', bound='hbm', peak_gbs=HBM_PEAK_GBS),
-        'kernels': kern,
+                                  'the step)', bound='hbm', peak_gbs=HBM_PEAK_GBS),
+        'kernels': r['kern'],
     }
+    if args.config == 'm' and not args.no_extra:
+        # the same run also times BASELINE config 2 (bf16, random init) as an extra key
+        a2 = argparse.Namespace(**vars(args))
+        a2.config = 'c2'
+        for key, v in PRESETS['c2'].items():
+            setattr(a2, key, v)
+        cfg2 = default_config(graph_convolution_stem_channels=[64] * a2.layers,
+                              k_number_nearest_points=a2.k)
+        r2 = gnn_measure(a2, world, dev, cfg2, model_state(cfg2, a2.weights), scatter=False)
+        line['c2_bf16'] = {'value': round(r2['value'], 2), 'unit': 'frames/s',
+                           'ms_per_step': round(r2['ms_step'], 3), 'dtype': 'bf16',
+                           'workload': workload_name(a2), 'edges_per_gpu': r2['E'],
+                           'forward_only_frames_per_s': round(r2['forward_fps'], 2),
+                           'roofline': r2['roof'], 'kernels': r2['kern']}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(args, cfg)
+        log('cpu baseline')
+        cb = cpu_baseline(args, cfg, sd)
+        line['cpu_baseline'] = cb
+        line['gpu_over_cpu'] = round(line['value'] / cb['value'], 1)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,0 +1,518 @@
+// Register-resident float32 MLP chains on v_mfma_f32_32x32x2_f32 (exact f32 products,
+// the reference precision): the fp32 path's encoders, task heads and the per-node
+// projections of the fused f32 conv layer (conv_f32.hip).
+//
+// Same semantics as rg_mlp_chain with dtype RG_F32 (ffn_block chains: Linear ->
+// channel_normalization -> activation, common.py:185-220, gnn_blocks.py:19-389), for the
+// widths of the shipped architecture, every width a compile-time constant:
+//
+//  * one wave = 32 rows; Y^T = W . X^T, so lane (r = lane&31, h = lane>>5) holds row r's
+//    features {32m + 8g + 4h + t} in accumulator register 4g + t of M-tile m;
+//  * the k order of every packed layer (RG_PACK_F32_FAST) is k(s4, u, h) = 8 s4 + 4h + u,
+//    which is BOTH a float4 of a row loaded from memory and registers 4g..4g+3 of the
+//    previous layer's M-tile s4/4 (g = s4%4): layers chain in registers with no data
+//    movement at all;
+//  * channel_normalization (mean, unbiased std, correctly rounded sqrt / divide) is an
+//    in-lane sum plus one v_permlane32_swap per statistic;
+//  * one wave per SIMD (256-thread workgroups, up to 512 registers per lane): an f32 MFMA
+//    keeps the matrix pipe busy for 64 cycles, room for ~14 independent instructions of
+//    the same wave, so the epilogues and the next rows' loads hide behind the MFMAs;
+//  * layers whose packed weights fit (<= ~155 KiB in total) are staged in LDS once per
+//    persistent workgroup; larger chains (the 7 -> 256 -> 128 -> 128 -> 64 edge encoder is
+//    232 KiB of f32 weights) read the remaining layers' fragments from global memory
+//    (L2-resident, prefetched several k-steps ahead).
+#include "rg_common.h"
+
+namespace rg {
+namespace f32c {
+
+static constexpr float NORM_EPS = 1e-5f;  // constants.py:9
+static constexpr int FT = 256;            // 4 waves, one per SIMD
+
+// bytes of one RG_PACK_F32_FAST layer (fragments + accumulator-order bias)
+__host__ __device__ constexpr int fbytes(int K, int N) {
+  return (N / 32) * ((K + 7) / 8) * 1024 + N * 4;
+}
+__host__ __device__ constexpr int falign(int b) { return (b + 15) & ~15; }
+
+struct Layer {
+  const void* src;  // packed weights + bias (global)
+  const float* mu;
+  const float* sd;
+  int out;
+  int act;
+};
+
+struct Args {
+  Layer L[RG_MAX_LAYERS];
+  int nl;
+  long rows;
+  const int* rows_dev;
+  const float* in0;
+  int ld0, w0real;
+  const int* idx0;
+  const int* idx1;
+  float* out;
+  int ld_out, out_real;
+  int* zero_ptr;  // optional: zeroed by workgroup 0 (the next kernel's work counters)
+  int zero_n;
+};
+
+// input modes of layer 0 (k-step order 8 s4 + 4h + u)
+enum { IN_SMALL = 0,   // float32 rows of <= 8 features (encoders), one k-quad per lane half
+       IN_DENSE = 1,   // float32 rows, K0 % 8 == 0
+       IN_PAIR = 2 };  // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// the 16 bias values of M-tile m, lane half h (accumulator order, 4 x 16-B reads)
+__device__ __forceinline__ f32x16 bias_frag(const float* bias, int m, int h) {
+  return ld_bias_frag(bias, m, h);
+}
+
+// One layer: acc (holding the bias) += W . X^T over S4 k-quads.  bop(s4) returns the
+// f32x4 B operand of k-steps 4 s4 .. 4 s4 + 3.  A fragments (one f32x4 = 4 k-steps per
+// M-tile) are read PD quads ahead: from LDS one quad ahead, from global memory (L2)
+// four quads ahead.
+template <int S4, int MT, bool G, typename BOp>
+__device__ __forceinline__ void layer(f32x16 (&acc)[MT], const char* w, int lane, BOp&& bop) {
+  const f32x4* wa = (const f32x4*)w + lane;
+  constexpr int PD = G ? 4 : 1;
+  constexpr int NB = PD + 1;
+  f32x4 a[NB][MT];
+#pragma unroll
+  for (int s = 0; s < PD && s < S4; ++s)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) a[s][m] = wa[(m * S4 + s) * 64];
+#pragma unroll
+  for (int s4 = 0; s4 < S4; ++s4) {
+    if (s4 + PD < S4) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) a[(s4 + PD) % NB][m] = wa[(m * S4 + s4 + PD) * 64];
+    }
+    const f32x4 b = bop(s4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma(a[s4 % NB][m][u], b[u], acc[m]);
+    // one fence per k-quad: the compiler would otherwise hoist every fragment load of
+    // the fully unrolled layer (hundreds of registers, then scratch)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// channel_normalization (common.py:208-220): y = s (x - mean) / (std_unbiased + eps) + m
+// over the row's 32*MT features (lane pair (lane, lane^32) holds one row)
+template <int MT>
+__device__ __forceinline__ void channel_norm(f32x16 (&acc)[MT], float mu, float sd) {
+  constexpr int N = 32 * MT;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += acc[m][q];
+      s1 += acc[m][q + 1];
+    }
+  const float mean = add_xor32(s0 + s1) * (1.f / N);  // N is a power of two: exact
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      const float d0 = acc[m][q] - mean, d1 = acc[m][q + 1] - mean;
+      q0 = fmaf(d0, d0, q0);
+      q1 = fmaf(d1, d1, q1);
+    }
+  const float ss = add_xor32(q0 + q1);
+  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + NORM_EPS);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      acc[m][q] = __fadd_rn(__fmul_rn(sd, __fmul_rn(acc[m][q] - mean, inv)), mu);
+}
+
+template <int ACT, int MT>
+__device__ __forceinline__ void act_all(f32x16 (&acc)[MT]) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[m][q] = act_t<ACT>(acc[m][q]);
+}
+
+// SPEC: bits 0-7 the activation, bit 8 + l layer l normalised, bit 16 + l layer l
+// activated (else identity), bit 24 + l layer l's weights read from global memory
+// (else staged in LDS) -- all host-checked against the layer descriptors
+constexpr int spec(int act, int norm_mask, int act_mask, int gmask) {
+  return act | (norm_mask << 8) | (act_mask << 16) | (gmask << 24);
+}
+constexpr bool spec_norm(int sp, int l) { return ((sp >> (8 + l)) & 1) != 0; }
+constexpr bool spec_act(int sp, int l) { return ((sp >> (16 + l)) & 1) != 0; }
+constexpr bool spec_glob(int sp, int l) { return ((sp >> (24 + l)) & 1) != 0; }
+
+template <int SPEC, int LI, int MT>
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const float* nrm) {
+  if constexpr (spec_norm(SPEC, LI)) channel_norm<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1]);
+  if constexpr (spec_act(SPEC, LI)) act_all<(SPEC & 0xff), MT>(acc);
+}
+
+// LDS offsets: layers staged in LDS are packed back to back in layer order
+template <int SPEC, int LI, int K, int... Ns> struct LdsOff;
+template <int SPEC, int LI, int K> struct LdsOff<SPEC, LI, K> {
+  static constexpr int get(int) { return 0; }
+  static constexpr int total() { return 0; }
+};
+template <int SPEC, int LI, int K, int N, int... Rest> struct LdsOff<SPEC, LI, K, N, Rest...> {
+  static constexpr int mine() { return spec_glob(SPEC, LI) ? 0 : falign(fbytes(K, N)); }
+  static constexpr int get(int l) { return l == LI ? 0 : mine() + LdsOff<SPEC, LI + 1, N, Rest...>::get(l); }
+  static constexpr int total() { return mine() + LdsOff<SPEC, LI + 1, N, Rest...>::total(); }
+};
+
+template <int MT>
+__device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const Args& a, long row, int h) {
+  float* o = a.out + (size_t)row * a.ld_out;
+  const int out = a.out_real;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * m + 8 * g + 4 * h;
+      if (f0 + 4 <= out && (a.ld_out & 3) == 0) {
+        *(f32x4*)(o + f0) = (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2],
+                                    acc[m][4 * g + 3]};
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (f0 + t < out) o[f0 + t] = acc[m][4 * g + t];
+      }
+    }
+}
+
+// the weight image of layer LI: LDS (staged) or global
+template <int SPEC, int LI, int OFF>
+__device__ __forceinline__ const char* wbase(const Args& a, const char* lds) {
+  if constexpr (spec_glob(SPEC, LI)) return (const char*)a.L[LI].src;
+  else return lds + OFF;
+}
+
+// layers LI.. of the chain; `prev` holds the previous layer's activations (B operands)
+template <int SPEC, int LI, int K, int N, int... Rest, int PMT, typename Off>
+__device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT], const char* lds,
+                                         const float* nrm, long row, bool valid, int lane, Off) {
+  constexpr int S4 = K / 8, MT = N / 32;
+  static_assert(K == 32 * PMT, "chained width");
+  const int h = lane >> 5;
+  const char* w = wbase<SPEC, LI, Off::get(LI)>(a, lds);
+  const float* bias = (const float*)(w + MT * S4 * 1024);
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = bias_frag(bias, m, h);
+  layer<S4, MT, spec_glob(SPEC, LI)>(acc, w, lane, [&](int s4) {
+    const f32x16& p = prev[s4 >> 2];
+    const int q = 4 * (s4 & 3);
+    return (f32x4){p[q], p[q + 1], p[q + 2], p[q + 3]};
+  });
+  epilogue<SPEC, LI, MT>(acc, nrm);
+  if constexpr (sizeof...(Rest) > 0) {
+    run_rest<SPEC, LI + 1, N, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+  } else {
+    if (valid) store_out<MT>(acc, a, row, h);
+  }
+}
+
+template <int SPEC, int K0, int N0, int... Rest, typename Off>
+__device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 + 7) / 8], const char* lds,
+                                          const float* nrm, long row, bool valid, int lane, Off) {
+  constexpr int S4 = (K0 + 7) / 8, MT = N0 / 32;
+  const int h = lane >> 5;
+  const char* w = wbase<SPEC, 0, Off::get(0)>(a, lds);
+  const float* bias = (const float*)(w + MT * S4 * 1024);
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = bias_frag(bias, m, h);
+  layer<S4, MT, spec_glob(SPEC, 0)>(acc, w, lane, [&](int s4) { return bin[s4]; });
+  epilogue<SPEC, 0, MT>(acc, nrm);
+  if constexpr (sizeof...(Rest) > 0) {
+    run_rest<SPEC, 1, N0, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+  } else {
+    if (valid) store_out<MT>(acc, a, row, h);
+  }
+}
+
+// Encoders (graph_feature_encoding, gnn_blocks.py:19-42): layer 0 (<= 8 inputs, no
+// normalisation) fused tile by tile into layer 1 -- each 32-feature output tile of layer
+// 0 (4 MFMAs) is activated and consumed at once as 16 k-steps of layer 1, so layer 0's
+// 256-wide activation never exists in full.
+template <int SPEC, int K0, int N0, int N1, int... Rest, typename Off>
+__device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1], const char* lds,
+                                            const float* nrm, long row, bool valid, int lane, Off) {
+  static_assert(K0 <= 8, "fused first layer takes <= 8 inputs");
+  constexpr int MT0 = N0 / 32, S41 = N0 / 8, MT1 = N1 / 32;
+  const int h = lane >> 5;
+  const char* w0 = wbase<SPEC, 0, Off::get(0)>(a, lds);
+  const char* w1 = wbase<SPEC, 1, Off::get(1)>(a, lds);
+  const float* bias0 = (const float*)(w0 + MT0 * 1024);
+  const float* bias1 = (const float*)(w1 + MT1 * S41 * 1024);
+  const f32x4* wa0 = (const f32x4*)w0 + lane;
+  const f32x4* wa1 = (const f32x4*)w1 + lane;
+  constexpr bool G1 = spec_glob(SPEC, 1);
+  f32x16 acc[MT1];
+#pragma unroll
+  for (int m = 0; m < MT1; ++m) acc[m] = bias_frag(bias1, m, h);
+  const f32x4 b0 = bin[0];
+#pragma unroll
+  for (int m0 = 0; m0 < MT0; ++m0) {
+    // layer-1 A fragments of this layer-0 tile (k-quads 4 m0 .. 4 m0 + 3), issued first
+    f32x4 f[4][MT1];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int m = 0; m < MT1; ++m) f[g][m] = wa1[(m * S41 + 4 * m0 + g) * 64];
+    f32x16 t = bias_frag(bias0, m0, h);
+    const f32x4 a0 = wa0[m0 * 64];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t = mfma(a0[u], b0[u], t);
+    if constexpr (spec_act(SPEC, 0)) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = act_t<(SPEC & 0xff)>(t[q]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[m] = mfma(f[g][m][u], t[4 * g + u], acc[m]);
+    (void)G1;
+    __builtin_amdgcn_sched_barrier(0);  // bound the live fragments to one layer-0 tile
+  }
+  epilogue<SPEC, 1, MT1>(acc, nrm);
+  if constexpr (sizeof...(Rest) > 0) {
+    run_rest<SPEC, 2, N1, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+  } else {
+    if (valid) store_out<MT1>(acc, a, row, h);
+  }
+}
+
+template <int MODE, int K0, int SPEC, bool FUSE01, int... Ns>
+__global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[2 * RG_MAX_LAYERS];
+  using Off = LdsOff<SPEC, 0, K0, Ns...>;
+  constexpr int NL = sizeof...(Ns);
+  constexpr int S40 = (K0 + 7) / 8;
+  if (blockIdx.x == 0 && a.zero_ptr && (int)threadIdx.x < a.zero_n) a.zero_ptr[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int l = 0; l < RG_MAX_LAYERS; ++l) {
+      const bool n = l < NL && a.L[l].mu;
+      nrm[2 * l] = n ? *a.L[l].mu : 0.f;
+      nrm[2 * l + 1] = n ? *a.L[l].sd : 0.f;
+    }
+  }
+  // stage the LDS layers (static indices: a dynamically indexed a.L would go to scratch)
+  {
+    constexpr int Ks[NL] = {Ns...};
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      if (!spec_glob(SPEC, l)) {
+        const int K = l == 0 ? K0 : Ks[l - 1];
+        const int n = fbytes(K, Ks[l]) / 16;
+        const f32x4* src = (const f32x4*)a.L[l].src;
+        f32x4* dst = (f32x4*)(lds + Off::get(l));
+        for (int i = threadIdx.x; i < n; i += FT) dst[i] = src[i];
+      }
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
+  const long ntiles = (rows + 31) / 32;
+  const long tstride = (long)gridDim.x * (FT / 64);
+  // layer-0 operands of tile t (prefetched one tile ahead)
+  auto fetch = [&](long t, f32x4 (&b)[S40]) {
+    const long row = t * 32 + r;
+    const bool ok = t < ntiles && row < rows;
+    if constexpr (MODE == IN_SMALL) {
+      const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (ok && 4 * h + u < a.w0real) ? p[4 * h + u] : 0.f;
+      b[0] = (f32x4){v[0], v[1], v[2], v[3]};
+    } else if constexpr (MODE == IN_DENSE) {
+      const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 4 * h;
+#pragma unroll
+      for (int s = 0; s < S40; ++s) b[s] = ok ? *(const f32x4*)(p + 8 * s) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    } else {
+      const int i = ok ? a.idx0[row] : 0, j = ok ? a.idx1[row] : 0;
+      const float* pi = a.in0 + (size_t)i * a.ld0 + 4 * h;
+      const float* pj = a.in0 + (size_t)j * a.ld0 + 4 * h;
+#pragma unroll
+      for (int s = 0; s < S40; ++s) {
+        const f32x4 xi = *(const f32x4*)(pi + 8 * s), xj = *(const f32x4*)(pj + 8 * s);
+        b[s] = ok ? (f32x4){__fadd_rn(xi.x, xj.x), __fadd_rn(xi.y, xj.y), __fadd_rn(xi.z, xj.z),
+                            __fadd_rn(xi.w, xj.w)}
+                  : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  long tile = (long)blockIdx.x * (FT / 64) + wave;
+  f32x4 nb[S40];
+  fetch(tile, nb);
+  for (; tile < ntiles; tile += tstride) {
+    f32x4 b[S40];
+#pragma unroll
+    for (int s = 0; s < S40; ++s) b[s] = nb[s];
+    fetch(tile + tstride, nb);
+    const long row = tile * 32 + r;
+    const bool valid = row < rows;
+    if constexpr (FUSE01) run_chain01<SPEC, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
+    else run_chain<SPEC, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
+  }
+}
+
+template <int MODE, int K0, int SPEC, bool FUSE01, int... Ns>
+static int launch(const Args& a, hipStream_t st) {
+  using Off = LdsOff<SPEC, 0, K0, Ns...>;
+  constexpr int lds = Off::total();
+  static_assert(lds <= DYN_LDS_MAX, "LDS image too large: read more layers from global memory");
+  auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, Ns...>;
+  int dev = 0;
+  RG_CHECK_HIP(hipGetDevice(&dev));
+  static bool attr[64] = {};
+  if (dev < 64 && !attr[dev]) {  // per device (a process may drive several GPUs)
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     DYN_LDS_MAX));
+    attr[dev] = true;
+  }
+  const long tiles = (a.rows + 31) / 32;
+  long blocks = (tiles + 3) / 4;
+  const long cap = lds <= 76 * 1024 ? 512 : 256;  // persistent: workgroups that fit at once
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  kern<<<blocks, FT, lds, st>>>(a);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+struct Key {
+  int mode, k0, spec_lo, nl;  // spec_lo: act | norm | act masks (bits 0..23)
+  int n[RG_MAX_LAYERS];
+};
+
+static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<int> ns) {
+  if (k.mode != mode || k.k0 != k0 || k.spec_lo != (sp & 0xffffff) || k.nl != (int)ns.size())
+    return false;
+  int i = 0;
+  for (int v : ns)
+    if (k.n[i++] != v) return false;
+  return true;
+}
+
+static int dispatch(const Key& k, const Args& a, hipStream_t st) {
+  constexpr int L = ACT_LEAKY;
+#define RG_F32C(MODE, K0, SP, F01, ...) \
+  if (match(k, MODE, K0, SP, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, __VA_ARGS__>(a, st);
+  // edge encoder 7 -> 256 -> 128 -> 128 -> 64 (gnn_blocks.py:19-42, block 0 without norm):
+  // layers 0 + 1 (136 KiB) in LDS, layers 2 + 3 (96 KiB) from L2
+  RG_F32C(IN_SMALL, 7, spec(L, 0b1110, 0b1111, 0b1100), true, 256, 128, 128, 64)
+  // node encoder 6 -> 256 -> 128 -> 64
+  RG_F32C(IN_SMALL, 6, spec(L, 0b110, 0b111, 0b100), true, 256, 128, 64)
+  // per-node projections of the fused f32 conv layer: [W_xi; W_xj] x + [b; 0], 64 -> 256
+  RG_F32C(IN_DENSE, 64, spec(L, 0, 0, 0), false, 256)
+  // task heads: 3-block stem + FFN_TaskSpecificHead (ffn + bare Linear -> 7 / 2, padded)
+  RG_F32C(IN_DENSE, 64, spec(L, 0b1111, 0b1111, 0), false, 64, 64, 64, 64, 32)
+  RG_F32C(IN_PAIR, 64, spec(L, 0b1111, 0b1111, 0), false, 64, 64, 64, 64, 32)
+  // link edge_formation stem (1 block), object-class stem (3 blocks), object head
+  RG_F32C(IN_DENSE, 64, spec(L, 0b1, 0b1, 0), false, 64)
+  RG_F32C(IN_DENSE, 64, spec(L, 0b111, 0b111, 0), false, 64, 64, 64)
+  RG_F32C(IN_DENSE, 64, spec(L, 0b01, 0b01, 0), false, 64, 32)
+#undef RG_F32C
+  return RG_ERR_UNSUPPORTED;
+}
+
+}  // namespace f32c
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::f32c;
+
+// internal entry (conv_f32.hip): the per-node projection chain, also zeroing the conv's
+// work counters (zero_ptr) in the same launch
+int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                        int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                        const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
+                        void* stream);
+
+int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                        int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                        const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
+                        void* stream) {
+  RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_f32: n_layers");
+  RG_REQUIRE(zero_n <= FT, RG_ERR_ARG, "rg_mlp_chain_f32: zero_n");
+  Key k;
+  memset(&k, 0, sizeof(k));
+  Args a;
+  memset(&a, 0, sizeof(a));
+  if (in_mode == RG_IN_DENSE && w0 <= 8 && n_layers >= 2 && !layers[0].norm_mu)
+    k.mode = IN_SMALL;
+  else if (in_mode == RG_IN_DENSE)
+    k.mode = IN_DENSE;
+  else if (in_mode == RG_IN_PAIRADD)
+    k.mode = IN_PAIR;
+  else
+    return RG_ERR_UNSUPPORTED;
+  RG_REQUIRE(k.mode == IN_SMALL || (w0 % 8 == 0 && ld0 % 4 == 0), RG_ERR_UNSUPPORTED,
+             "rg_mlp_chain_f32: dense input width / stride must be multiples of 8 / 4");
+  k.k0 = w0;
+  k.nl = n_layers;
+  int nm = 0, am = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const rg_layer& s = layers[l];
+    RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_f32: layer %d weights", l);
+    if (s.save_pre || s.save_out || (s.flags & RG_LAYER_CENTERED)) return RG_ERR_UNSUPPORTED;
+    RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
+    RG_REQUIRE(l == 0 ? s.in_dim == w0 : s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG,
+               "rg_mlp_chain_f32: layer %d width", l);
+    if (l + 1 < n_layers && s.out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
+    if (s.norm_mu && s.out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
+    if (s.norm_mu) nm |= 1 << l;
+    if (s.act == ACT_LEAKY) am |= 1 << l;
+    else if (s.act != ACT_NONE) return RG_ERR_UNSUPPORTED;
+    k.n[l] = (s.out_dim + 31) / 32 * 32;
+    a.L[l].src = s.w_packed;
+    a.L[l].mu = s.norm_mu;
+    a.L[l].sd = s.norm_std;
+    a.L[l].out = s.out_dim;
+    a.L[l].act = s.act;
+  }
+  k.spec_lo = spec(ACT_LEAKY, nm, am, 0);
+  a.nl = n_layers;
+  a.rows = rows;
+  a.rows_dev = rows_dev;
+  a.in0 = in0;
+  a.ld0 = ld0;
+  a.w0real = w0;
+  a.idx0 = idx0;
+  a.idx1 = idx1;
+  a.out = out;
+  a.ld_out = ld_out;
+  a.out_real = layers[n_layers - 1].out_dim;
+  a.zero_ptr = zero_ptr;
+  a.zero_n = zero_n;
+  if (rows <= 0 && !zero_ptr) return RG_OK;
+  return dispatch(k, a, (hipStream_t)stream);
+}
+
+extern "C" int rg_mlp_chain_f32(const rg_layer* layers, int n_layers, long rows,
+                                const int* rows_dev, int in_mode, const float* in0, int ld0,
+                                int w0, const int* idx0, const int* idx1, float* out, int ld_out,
+                                void* stream) {
+  RG_REQUIRE(in_mode != RG_IN_PAIRADD || (idx0 && idx1), RG_ERR_ARG,
+             "rg_mlp_chain_f32: RG_IN_PAIRADD needs idx0 and idx1");
+  return rg_f32_chain_launch(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, idx0, idx1,
+                             out, ld_out, nullptr, 0, stream);
+}

@@ -1,0 +1,419 @@
+// Fused float32 residual_graph_conv_block (gnn_blocks.py:96-113) -- the reference
+// precision -- for the shipped widths (C = 64 node / edge channels, message MLP
+// 192 -> 128 -> 64, update 128 -> 64, channel_normalization + activation on every block,
+// aggregation add or mean).  Exact f32 products on v_mfma_f32_32x32x2_f32.
+//
+// One C-ABI call = two launches:
+//  1. projections (chain_f32.hip, 64 -> 256 per node): P[i] = W_xi x[i] + b1 and
+//     Q[j] = W_xj x[j], the x_i and x_j thirds of the first message layer, computed once
+//     per NODE instead of once per edge (msg0(cat(x_i, x_j, e)) = P[i] + Q[j] + W_e e);
+//     this launch also zeroes the work counters of launch 2;
+//  2. the fused layer: work block = 32 destination nodes and their incoming edges (one
+//     contiguous range of the destination-major CSR).  Per 32-edge tile a wave computes
+//        h = act(norm(P[dst] + Q[src] + W_e e))         128 MFMAs (K = 64, N = 128)
+//        m = act(norm(W_2 h + b2))                       128 MFMAs (K = 128, N = 64)
+//     (layer 2 takes layer 1's accumulators as its B operand in registers), then the
+//     segmented sum: the message tile goes through a wave-private LDS tile so that lane
+//     = feature, and every lane adds the tile's messages IN EDGE ORDER into a running
+//     sum, starting a new sum at each change of destination (the destination of an
+//     edge is wave-uniform: a scalar compare) -- the reference scatter_add_ order, no
+//     MFMA spent on the reduction.  After the block's last tile the aggregates (LDS,
+//     row = node) and x[node] are the update MLP's B operand; update + norm + act +
+//     residual, store.  Messages and aggregates never touch HBM.
+// One wave per SIMD (up to 512 registers): the f32 MFMA (64 cycles) leaves the issue
+// slots for the epilogues; the next tile's rows (P[dst], Q[src], e: 160 registers) are
+// loaded while the current tile computes, the tile after's indices one tile earlier.
+// Workgroups are persistent; block ids come from one atomic counter per XCD over that
+// XCD's contiguous eighth of the nodes (workgroup w runs on XCD w % 8), so each frame's
+// x, P and Q rows are gathered from one L2.
+#include "rg_common.h"
+
+namespace rg {
+namespace convf32 {
+
+static constexpr int FT = 256;       // 4 waves, one per SIMD
+static constexpr int NW = FT / 64;
+static constexpr int C = 64;         // node / edge / message / output channels
+static constexpr int HID = 128;      // msg_mlp_hidden_dim
+static constexpr int NBLK = 32;      // destination nodes per work block
+static constexpr int TS = 68;        // LDS row stride (floats) of the message half-tile
+static constexpr int AS = 68;        // LDS row stride (floats) of the aggregate rows
+static constexpr float NORM_EPS = 1e-5f;
+static constexpr int NXCD = 8;
+
+__host__ __device__ constexpr int fbytes(int K, int N) {
+  return (N / 32) * ((K + 7) / 8) * 1024 + N * 4;
+}
+static constexpr int W_E_OFF = 0;                                       // W_e: 64 -> 128
+static constexpr int W_2_OFF = (fbytes(C, HID) + 15) & ~15;             // W_2: 128 -> 64
+static constexpr int W_U_OFF = W_2_OFF + ((fbytes(HID, C) + 15) & ~15);  // W_u: 128 -> 64
+static constexpr int W_BYTES = W_U_OFF + ((fbytes(2 * C, C) + 15) & ~15);
+static constexpr int WAVE_LDS = (16 * TS + NBLK * AS) * 4;
+static constexpr int LDS_BYTES = W_BYTES + NW * WAVE_LDS;
+static_assert(LDS_BYTES <= DYN_LDS_MAX, "conv_f32 LDS");
+
+struct Args {
+  const float* x;
+  const float* e;
+  const float* pq;  // [N][256]: P (0..127) | Q (128..255)
+  const int* seg_ptr;
+  const int* src;
+  const int* dst;
+  float* x_out;
+  int* counters;  // [NXCD], zero at launch (zeroed by the projection launch)
+  const void* w[3];  // W_e, W_2, W_u (RG_PACK_F32_FAST)
+  const float* mu[3];
+  const float* sd[3];
+  int ldx, lde, ldpq, ldo;
+  int n_nodes, n_blocks;
+  int aggr_mean;
+};
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <int S4, int MT, typename BOp>
+__device__ __forceinline__ void layer(f32x16 (&acc)[MT], const char* w, int lane, BOp&& bop) {
+  const f32x4* wa = (const f32x4*)w + lane;
+  f32x4 a[2][MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) a[0][m] = wa[(m * S4) * 64];
+#pragma unroll
+  for (int s4 = 0; s4 < S4; ++s4) {
+    if (s4 + 1 < S4) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) a[(s4 + 1) & 1][m] = wa[(m * S4 + s4 + 1) * 64];
+    }
+    const f32x4 b = bop(s4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma(a[s4 & 1][m][u], b[u], acc[m]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// channel_normalization (common.py:208-220) + activation over a row's 32*MT features
+template <int MT>
+__device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], float mu, float sd, int act) {
+  constexpr int N = 32 * MT;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += acc[m][q];
+      s1 += acc[m][q + 1];
+    }
+  const float mean = add_xor32(s0 + s1) * (1.f / N);
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      const float d0 = acc[m][q] - mean, d1 = acc[m][q + 1] - mean;
+      q0 = fmaf(d0, d0, q0);
+      q1 = fmaf(d1, d1, q1);
+    }
+  const float ss = add_xor32(q0 + q1);
+  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + NORM_EPS);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      acc[m][q] = __fadd_rn(__fmul_rn(sd, __fmul_rn(acc[m][q] - mean, inv)), mu);
+  act_dispatch(act, [&](auto A) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = act_t<decltype(A)::value>(acc[m][q]);
+  });
+}
+
+struct Rows {
+  f32x4 p[16];  // P[dst]: features 32m + 8g + 4h .. +3 at [4m + g]
+  f32x4 q[16];  // Q[src]
+  f32x4 e[8];   // e[edge]: features 8 s4 + 4h .. +3 at [s4]
+};
+struct Idx {
+  int d, s;
+};
+
+__global__ __launch_bounds__(FT) void conv_f32_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[6];
+  __shared__ int acts[3];
+  if (threadIdx.x < 3) {
+    nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
+    nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
+  }
+  {
+    const int nb[3] = {fbytes(C, HID), fbytes(HID, C), fbytes(2 * C, C)};
+    const int off[3] = {W_E_OFF, W_2_OFF, W_U_OFF};
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      const f32x4* s = (const f32x4*)a.w[l];
+      f32x4* d = (f32x4*)(lds + off[l]);
+      for (int i = threadIdx.x; i < nb[l] / 16; i += FT) d[i] = s[i];
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  float* T = (float*)(lds + W_BYTES + wave * WAVE_LDS);  // [16][TS] message half-tile
+  float* Agg = T + 16 * TS;                             // [NBLK][AS] aggregates
+  const char* wE = lds + W_E_OFF;
+  const char* w2 = lds + W_2_OFF;
+  const char* wU = lds + W_U_OFF;
+  const float* bias2 = (const float*)(w2 + 2 * 16 * 1024);
+  const float* biasU = (const float*)(wU + 2 * 16 * 1024);
+  const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3], muU = nrm[4], sdU = nrm[5];
+  const int act = ACT_LEAKY;  // host-checked: all three blocks use the yml LeakyReLU
+  (void)acts;
+
+  // this workgroup's XCD range of blocks
+  const int xcd = blockIdx.x % NXCD;
+  const int blo = (int)((long)a.n_blocks * xcd / NXCD);
+  const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  int* ctr = a.counters + xcd;
+
+  auto load_idx = [&](int t0, int e1) {
+    const int p = min(t0 + r, e1 - 1);
+    return Idx{a.dst[p], a.src[p]};
+  };
+  auto load_rows = [&](int t0, int e1, const Idx& ix, Rows& R) {
+    const int p = min(t0 + r, e1 - 1);
+    const float* pp = a.pq + (size_t)ix.d * a.ldpq + 4 * h;
+    const float* pq = a.pq + (size_t)ix.s * a.ldpq + HID + 4 * h;
+    const float* pe = a.e + (size_t)p * a.lde + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      R.p[i] = *(const f32x4*)(pp + 8 * i);
+      R.q[i] = *(const f32x4*)(pq + 8 * i);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) R.e[s] = *(const f32x4*)(pe + 8 * s);
+  };
+
+  for (;;) {
+    int bi = 0;
+    if (lane == 0) bi = atomicAdd(ctr, 1);
+    const int blk = blo + __shfl(bi, 0, 64);
+    if (blk >= bhi) break;
+    const int n0 = blk * NBLK;
+    const int n1 = min(n0 + NBLK, a.n_nodes);
+    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+
+    // aggregates start at zero (nodes without incoming edges keep it, PyG semantics)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = lane + 64 * i;
+      *(f32x4*)(Agg + (idx >> 4) * AS + 4 * (idx & 15)) = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    float run = 0.f;  // lane = feature: the running sum of the current destination
+    int cur = -1;     // its slot (wave-uniform)
+
+    auto tile = [&](const Rows& R, int dcur, int t0, int e1) {
+      // ---- message layer 1: h = P[dst] + Q[src] + W_e e, then norm + act
+      f32x16 acc1[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 pv = R.p[4 * m + g], qv = R.q[4 * m + g];
+          acc1[m][4 * g + 0] = pv.x + qv.x;
+          acc1[m][4 * g + 1] = pv.y + qv.y;
+          acc1[m][4 * g + 2] = pv.z + qv.z;
+          acc1[m][4 * g + 3] = pv.w + qv.w;
+        }
+      layer<8, 4>(acc1, wE, lane, [&](int s4) { return R.e[s4]; });
+      norm_act<4>(acc1, mu0, sd0, act);
+      // ---- message layer 2 (B operand = layer 1's accumulators)
+      f32x16 acc2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
+      layer<16, 2>(acc2, w2, lane, [&](int s4) {
+        const f32x16& p = acc1[s4 >> 2];
+        const int q = 4 * (s4 & 3);
+        return (f32x4){p[q], p[q + 1], p[q + 2], p[q + 3]};
+      });
+      norm_act<2>(acc2, mu1, sd1, act);
+      // ---- segmented sum in edge order, 16 edges at a time through the LDS tile
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if ((r >> 4) == c) {
+          float* row = T + (r & 15) * TS + 4 * h;
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){acc2[m][4 * g], acc2[m][4 * g + 1],
+                                                        acc2[m][4 * g + 2], acc2[m][4 * g + 3]};
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int eo = 16 * c + j;
+          if (t0 + eo < e1) {
+            const float v = T[j * TS + lane];
+            const int slot = __builtin_amdgcn_readlane(dcur, eo) - n0;
+            run = slot == cur ? run + v : v;
+            Agg[slot * AS + lane] = run;
+            cur = slot;
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    };
+
+    if (e0 < e1) {
+      Idx iA = load_idx(e0, e1);
+      Idx iB = load_idx(e0 + 32, e1);
+      Rows RA, RB;
+      load_rows(e0, e1, iA, RA);
+      for (int t0 = e0;;) {
+        int dA = iA.d;
+        load_rows(t0 + 32, e1, iB, RB);
+        iA = load_idx(t0 + 64, e1);
+        tile(RA, dA, t0, e1);
+        t0 += 32;
+        if (t0 >= e1) break;
+        int dB = iB.d;
+        load_rows(t0 + 32, e1, iA, RA);
+        iB = load_idx(t0 + 64, e1);
+        tile(RB, dB, t0, e1);
+        t0 += 32;
+        if (t0 >= e1) break;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
+    const int node = n0 + r;
+    const bool nvalid = node < n1;
+    const float* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 4 * h;
+    f32x4 xb[8], ab[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) xb[s] = *(const f32x4*)(px + 8 * s);
+    float cnt = 1.f;
+    if (a.aggr_mean) {  // PyG mean: sum / max(count, 1)
+      const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
+      cnt = (float)(deg > 0 ? deg : 1);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      f32x4 v = *(const f32x4*)(Agg + r * AS + 8 * s + 4 * h);
+      if (a.aggr_mean) v = (f32x4){div_rn(v.x, cnt), div_rn(v.y, cnt), div_rn(v.z, cnt), div_rn(v.w, cnt)};
+      ab[s] = v;
+    }
+    f32x16 accu[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
+    layer<16, 2>(accu, wU, lane, [&](int s4) { return s4 < 8 ? xb[s4] : ab[s4 - 8]; });
+    norm_act<2>(accu, muU, sdU, act);
+    if (nvalid) {
+      float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 xr = xb[4 * m + g];  // x[node] features 32m + 8g + 4h .. +3
+          *(f32x4*)(po + 32 * m + 8 * g) =
+              (f32x4){__fadd_rn(xr.x, accu[m][4 * g]), __fadd_rn(xr.y, accu[m][4 * g + 1]),
+                      __fadd_rn(xr.z, accu[m][4 * g + 2]), __fadd_rn(xr.w, accu[m][4 * g + 3])};
+        }
+    }
+    // Agg / T are rewritten by the next block only after this wave's reads completed
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace convf32
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::convf32;
+
+int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                        int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                        const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
+                        void* stream);
+
+extern "C" size_t rg_conv_layer_f32_workspace_size(int n_nodes) {
+  return 256 + (size_t)(n_nodes > 0 ? n_nodes : 1) * 2 * HID * sizeof(float);
+}
+
+extern "C" int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx,
+                                 const float* e, int lde, const int* seg_ptr, const int* src,
+                                 const int* dst, int n_nodes, float* x_out, int ld_out,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const rg_layer& pq = layers[0];
+  const rg_layer& m0 = layers[1];
+  const rg_layer& m1 = layers[2];
+  const rg_layer& u = layers[3];
+  if (!(pq.in_dim == C && pq.out_dim == 2 * HID && m0.in_dim == C && m0.out_dim == HID &&
+        m1.in_dim == HID && m1.out_dim == C && u.in_dim == 2 * C && u.out_dim == C))
+    return RG_ERR_UNSUPPORTED;
+  if (aggr != RG_REDUCE_SUM && aggr != RG_REDUCE_MEAN) return RG_ERR_UNSUPPORTED;
+  if (pq.norm_mu || pq.act != ACT_NONE) return RG_ERR_UNSUPPORTED;
+  if (!m0.norm_mu || !m1.norm_mu || !u.norm_mu) return RG_ERR_UNSUPPORTED;
+  if (m0.act != ACT_LEAKY || m1.act != ACT_LEAKY || u.act != ACT_LEAKY) return RG_ERR_UNSUPPORTED;
+  RG_REQUIRE(ldx % 4 == 0 && lde % 4 == 0 && ld_out % 4 == 0, RG_ERR_UNSUPPORTED,
+             "rg_conv_layer_f32: row strides must be multiples of 4");
+  RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_f32: x_out must not alias x");
+  RG_REQUIRE(workspace_bytes >= rg_conv_layer_f32_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_conv_layer_f32: workspace too small");
+  if (n_nodes <= 0) return RG_OK;
+  Args a;
+  memset(&a, 0, sizeof(a));
+  a.counters = (int*)workspace;
+  float* pqbuf = (float*)((char*)workspace + 256);
+  // launch 1: P | Q for every node (+ zero the work counters)
+  int rc = rg_f32_chain_launch(&pq, 1, n_nodes, nullptr, RG_IN_DENSE, x, ldx, C, nullptr, nullptr,
+                               pqbuf, 2 * HID, a.counters, NXCD, stream);
+  if (rc) return rc;
+  a.x = x;
+  a.e = e;
+  a.pq = pqbuf;
+  a.seg_ptr = seg_ptr;
+  a.src = src;
+  a.dst = dst;
+  a.x_out = x_out;
+  a.w[0] = m0.w_packed;
+  a.w[1] = m1.w_packed;
+  a.w[2] = u.w_packed;
+  const rg_layer* ls[3] = {&m0, &m1, &u};
+  for (int l = 0; l < 3; ++l) {
+    a.mu[l] = ls[l]->norm_mu;
+    a.sd[l] = ls[l]->norm_std;
+  }
+  a.ldx = ldx;
+  a.lde = lde;
+  a.ldpq = 2 * HID;
+  a.ldo = ld_out;
+  a.n_nodes = n_nodes;
+  a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
+  a.aggr_mean = aggr == RG_REDUCE_MEAN;
+  int dev = 0;
+  RG_CHECK_HIP(hipGetDevice(&dev));
+  static bool attr[64] = {};
+  if (dev < 64 && !attr[dev]) {
+    RG_CHECK_HIP(hipFuncSetAttribute((const void*)conv_f32_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, DYN_LDS_MAX));
+    attr[dev] = true;
+  }
+  // one workgroup per CU (LDS); at least one per XCD counter
+  int blocks = 256;
+  const int need = (a.n_blocks + NW - 1) / NW;
+  if (blocks > need) blocks = need;
+  if (blocks < NXCD) blocks = NXCD;
+  conv_f32_kernel<<<blocks, FT, LDS_BYTES, st>>>(a);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

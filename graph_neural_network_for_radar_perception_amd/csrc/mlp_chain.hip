@@ -46,6 +46,8 @@ template <> struct Cfg<uint16_t> {
 __host__ __device__ inline int kpad(int k, int p) { return (k + p - 1) / p * p; }
 
 __host__ __device__ inline size_t frag_bytes(int in_dim, int out_dim, int dtype) {
+  if (dtype == RG_PACK_F32_FAST)
+    return (size_t)((out_dim + 31) / 32) * ((in_dim + 7) / 8) * 1024;
   if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD)
     return (size_t)((out_dim + 31) / 32) * ((in_dim + 15) / 16) * 64 * 8 * sizeof(uint16_t);
   const size_t mt = (size_t)(out_dim + 15) / 16;
@@ -53,8 +55,8 @@ __host__ __device__ inline size_t frag_bytes(int in_dim, int out_dim, int dtype)
   return mt * (kpad(in_dim, 32) / 32) * 64 * 8 * sizeof(uint16_t);
 }
 static size_t packed_bytes(int in_dim, int out_dim, int dtype) {
-  const int bpad =
-      (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD) ? 32 : 16;
+  const int bpad = (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN ||
+                    dtype == RG_PACK_FAST_UPD || dtype == RG_PACK_F32_FAST) ? 32 : 16;
   return frag_bytes(in_dim, out_dim, dtype) + (size_t)kpad(out_dim, bpad) * sizeof(float);
 }
 
@@ -153,6 +155,25 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
     }
   }
   P[t] = f32_to_bf16(v);
+}
+
+// RG_PACK_F32_FAST: [m][s4][lane][4] = W[32m + (lane&31)][8 s4 + 4 (lane>>5) + u]; the k
+// order is what both a row loaded from memory (one float4 per lane half and s4) and the
+// previous layer's 32x32 accumulators (register 4g + t of M-tile m' = k-step
+// 16 m' + 4g + t) supply, so one format serves every layer of an f32 chain
+__global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int out,
+                                     float* __restrict__ P, long total) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int S4 = (in + 7) / 8;
+  const int u = (int)(t & 3);
+  const int lane = (int)((t >> 2) & 63);
+  const long ms = t >> 8;
+  const int s4 = (int)(ms % S4);
+  const int m = (int)(ms / S4);
+  const int o = 32 * m + (lane & 31);
+  const int k = 8 * s4 + 4 * (lane >> 5) + u;
+  P[t] = (o < out && k < in) ? W[(size_t)o * in + k] : 0.f;
 }
 
 __global__ void pack_bias_kernel(const float* __restrict__ b, int out, int n, float* __restrict__ P) {
@@ -545,8 +566,8 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   dtype &= ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE);
   RG_REQUIRE(!transpose || dtype == RG_F32, RG_ERR_ARG,
              "rg_pack_linear: RG_PACK_TRANSPOSE applies to RG_F32");
-  RG_REQUIRE(!center || dtype >= RG_PACK_FAST_IN, RG_ERR_ARG,
-             "rg_pack_linear: RG_PACK_CENTERED applies to the RG_PACK_FAST_* formats");
+  RG_REQUIRE(!center || (dtype >= RG_PACK_FAST_IN && dtype <= RG_PACK_FAST_UPD), RG_ERR_ARG,
+             "rg_pack_linear: RG_PACK_CENTERED applies to the bf16 RG_PACK_FAST_* formats");
   if (dtype == RG_F32) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
     pack_f32_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
@@ -563,6 +584,10 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
     const int mem_steps = dtype == RG_PACK_FAST_IN ? ks : (dtype == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
     pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
                                                            center, (uint16_t*)packed, total);
+  } else if (dtype == RG_PACK_F32_FAST) {
+    long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
+    pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
+                                                               (float*)packed, total);
   } else {
     RG_REQUIRE(false, RG_ERR_ARG, "rg_pack_linear: bad dtype %d", dtype);
   }

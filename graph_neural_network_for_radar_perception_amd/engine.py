@@ -150,7 +150,7 @@ class ChainPlan:
         self.device = torch.device(device)
         self.in_dim = specs[0].in_dim
         self.out_dim = specs[-1].out_dim
-        self.use_fast = True   # try rg_mlp_chain_fast first (bf16 only)
+        self.use_fast = True   # try rg_mlp_chain_fast (bf16) / rg_mlp_chain_f32 (fp32) first
         self._pack()
 
     def _signature(self):
@@ -187,6 +187,7 @@ class ChainPlan:
                 self.specs[i], nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN))
             self.fast = fg[0][0]
         self.fast_ok = {}   # in_mode -> bool (shape has a compiled fast kernel)
+        self._f32 = None    # RG_PACK_F32_FAST layer array, packed on first fp32 fast call
         self.sig = self._signature()
 
     def refresh(self):
@@ -197,11 +198,33 @@ class ChainPlan:
         """Parameters were written behind torch's version counters (FusedSGD)."""
         self.sig = None
 
+    def _f32_layers(self):
+        """The chain packed RG_PACK_F32_FAST for rg_mlp_chain_f32 (lazily: training chains
+        never use it)."""
+        if self._f32 is None:
+            self._f32buf, groups = self._pack_buffer(lambda i: nat.RG_PACK_F32_FAST)
+            self._f32 = groups[0][0]
+        return self._f32
+
     def __call__(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
                  mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
                  idx0=None, idx1=None, residual=None, rows_dev=None):
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
+        if (self.use_fast and self.dt == nat.RG_F32 and mode in (nat.IN_DENSE, nat.IN_PAIRADD)
+                and residual is None and in0.dtype == torch.float32
+                and out.dtype == torch.float32 and len(self.specs) <= nat.MAX_LAYERS
+                and self.fast_ok.get(mode, True)):
+            rc = lib.rg_mlp_chain_f32(self._f32_layers(), len(self.specs), int(rows),
+                                      nat.ptr(rows_dev), mode, in0.data_ptr(), in0.stride(0), w0,
+                                      nat.ptr(idx0), nat.ptr(idx1), out.data_ptr(), out.stride(0),
+                                      st)
+            if rc == 0:
+                self.fast_ok[mode] = True
+                return out
+            if rc != nat.RG_ERR_UNSUPPORTED:
+                nat.check(rc, 'rg_mlp_chain_f32')
+            self.fast_ok[mode] = False
         if self.use_fast and self.fast is not None and self.fast_ok.get(mode, True):
             rc = lib.rg_mlp_chain_fast(
                 self.fast, len(self.specs), int(rows), nat.ptr(rows_dev), mode, _dt_code(in0),
@@ -439,10 +462,45 @@ class ConvPlan:
         self.use_fused = True   # bf16: one rg_conv_layer_fused launch per layer
         self._pack_fused()
 
+    def _pack_fused_f32(self):
+        """fp32: rg_conv_layer_f32's four RG_PACK_F32_FAST layers -- the per-node
+        projection [W_xi; W_xj] (+ [b; 0]), W_e (msg0's edge columns, with msg0's norm and
+        activation), msg1, upd."""
+        m0, m1 = self.msg.specs
+        u = self.upd.specs[0]
+        C = self.c_out
+        W = m0.weight.detach().to(torch.float32)
+        if W.shape[1] != 3 * C:
+            return
+        b = (m0.bias.detach().to(torch.float32) if m0.bias is not None
+             else torch.zeros(W.shape[0], dtype=torch.float32, device=W.device))
+        w_pq = torch.cat((W[:, :C], W[:, C:2 * C]), 0).contiguous()
+        b_pq = torch.cat((b, torch.zeros_like(b)), 0).contiguous()
+        pq = LayerSpec(w_pq, b_pq, None, None, 'none')
+        we = LayerSpec(W[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
+        specs = [pq, we, m1, u]
+        fmts = [nat.RG_PACK_F32_FAST] * 4
+        try:
+            self.fused_buf, offs = pack_specs(specs, fmts, self.device)
+        except RuntimeError:
+            return
+        self._fused_keep = (w_pq, b_pq, we.weight)   # packing is async: keep the sources
+        self.fused_layers = layer_array(specs, self.fused_buf.data_ptr(), offs, fmts)
+        self.fused_ws = None
+        self.fused = True
+        self.fused_sig = self._sig()
+
     def _pack_fused(self):
-        """bf16: the fused layer kernel (rg_conv_layer_fused) when the shapes fit."""
+        """bf16: the fused layer kernel (rg_conv_layer_fused) when the shapes fit;
+        fp32: rg_conv_layer_f32."""
         self.fused = None
-        if self.dtype != 'bf16' or self.res is not None or self.aggr == 'max':
+        if self.res is not None or self.aggr == 'max':
+            return
+        if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
+            return
+        if self.dtype == 'fp32':
+            return self._pack_fused_f32()
+        if self.dtype != 'bf16':
             return
         specs = self.msg.specs + self.upd.specs
         if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
@@ -484,6 +542,23 @@ class ConvPlan:
         if not self.use_fused or not self.fused or self.fused_ok is False:
             return False
         lib = nat.lib()
+        if self.dtype == 'fp32':
+            if x.dtype != torch.float32 or e.dtype != torch.float32:
+                return False
+            need = lib.rg_conv_layer_f32_workspace_size(g.n_nodes)
+            if self.fused_ws is None or self.fused_ws.numel() < need:
+                self.fused_ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            rc = lib.rg_conv_layer_f32(
+                self.fused_layers, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(),
+                e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
+                x_out.data_ptr(), x_out.stride(0), self.fused_ws.data_ptr(),
+                self.fused_ws.numel(), nat.stream_ptr(x.device))
+            if rc == nat.RG_ERR_UNSUPPORTED:
+                self.fused_ok = False
+                return False
+            nat.check(rc, 'rg_conv_layer_f32')
+            self.fused_ok = True
+            return True
         tbl, nb = g.conv_blocks()
         rc = lib.rg_conv_layer_fused_blocks(
             self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),

@@ -47,6 +47,11 @@ extern "C" {
 #define RG_PACK_FAST_IN 2
 #define RG_PACK_FAST_CHAIN 3
 #define RG_PACK_FAST_UPD 4 /* update layer of rg_conv_layer_fused: cat(x, aggregate) */
+/* float32 32x32x2 fragments of the register-resident f32 kernels (rg_mlp_chain_f32,
+ * rg_conv_layer_f32): fragment (m, s4) = 1 KiB at byte (m * K/8 + s4) * 1024, lane l's
+ * 16 B = W[32m + (l & 31)][8 s4 + 4 (l >> 5) + u], u = 0..3 (K padded to 8, N to 32),
+ * then the bias in accumulator order [m][h][16] (entry 4g + t = b[32m + 8g + 4h + t]) */
+#define RG_PACK_F32_FAST 5
 /* OR-ed into a RG_PACK_FAST_* format for a layer followed by channel_normalization:
  * the rows of W and b are shifted to zero mean over the outputs (W - 1 mean_o(W),
  * b - mean(b)).  The normalisation then sees (x - mean) directly -- it is invariant
@@ -231,6 +236,37 @@ int rg_mlp_chain_fast(const rg_layer* layers_host, int n_layers, long rows, cons
                       const void* in1, int ld1, int w1, const void* in2, int ld2, int w2,
                       const int* idx0, const int* idx1, const void* residual, int ld_res,
                       int res_dtype, void* out, int ld_out, int out_dtype, void* stream);
+
+/* Register-resident float32 chain (same semantics as rg_mlp_chain with dtype RG_F32,
+ * exact f32 products on v_mfma_f32_32x32x2_f32) for the widths of the shipped
+ * architecture: every layer packed RG_PACK_F32_FAST, no RG_LAYER_CENTERED.  in_mode
+ * RG_IN_DENSE (float32 rows; <= 8 features with an un-normalised first layer = the
+ * encoders, gnn_blocks.py:19-42) or RG_IN_PAIRADD (edge_formation, gnn_blocks.py:297).
+ * Returns RG_ERR_UNSUPPORTED (launching nothing) for shapes without an instantiation;
+ * the caller then uses rg_mlp_chain.  Replaces the ffn_block chains of common.py:185-220
+ * called from gnn_blocks.py:19-42 and :167-389. */
+int rg_mlp_chain_f32(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
+                     int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                     const int* idx1, float* out, int ld_out, void* stream);
+
+/* One fused FLOAT32 residual_graph_conv_block (gnn_blocks.py:96-113, the reference
+ * precision) for the shipped widths (C = 64, message MLP 192 -> 128 -> 64, update
+ * 128 -> 64, channel_normalization + LeakyReLU on every block), aggregation add or mean
+ * (the PyG propagate of gnn_blocks.py:57,106).  layers[4], all RG_PACK_F32_FAST:
+ *   [0] the per-node projection 64 -> 256: rows 0..127 = W_msg0[:, 0:64] (x_i columns),
+ *       rows 128..255 = W_msg0[:, 64:128] (x_j columns); bias = [b_msg0; 0]; no norm / act
+ *   [1] W_msg0[:, 128:192] (the edge columns) 64 -> 128, no bias, msg0's norm + act
+ *   [2] msg1 128 -> 64 (bias, norm, act)     [3] upd 128 -> 64 on cat(x, agg)
+ * seg_ptr / src / dst: destination-major CSR (sources ascending per segment); e rows in
+ * that order.  x_out[i] = x[i] + upd(cat(x[i], AGG_p msg(cat(x[i], x[src p], e[p])))),
+ * the sum in edge order.  workspace: rg_conv_layer_f32_workspace_size(n_nodes) bytes,
+ * no initialisation needed (two launches: projections, which also reset the block
+ * counters, then the fused layer); one workspace per stream. */
+size_t rg_conv_layer_f32_workspace_size(int n_nodes);
+int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx, const float* e,
+                      int lde, const int* seg_ptr, const int* src, const int* dst, int n_nodes,
+                      float* x_out, int ld_out, void* workspace, size_t workspace_bytes,
+                      void* stream);
 
 /* One fused residual_graph_conv_block (gnn_blocks.py:96-113) for the shipped
  * widths (node / edge channels 64, msg MLP 192->128->64, update 128->64, all with

@@ -248,6 +248,15 @@ def test_forward_fp32_matches_reference(cuda_device, name):
                    [c.to(dev) for c in cluster_lists(d)])
     for got, key in zip(out, ('node_cls', 'node_reg', 'link_cls', 'obj_cls')):
         np.testing.assert_allclose(got.cpu().numpy(), d[key], err_msg=key, **FP32_TOL)
+    # the fused f32 conv layer ran wherever the block shape allows it (add / mean, no
+    # residual projection), and the register-resident f32 chains for the encoders
+    plans = pred.plans('fp32')
+    for cv in plans.convs:
+        assert bool(cv.fused) == (cv.aggr != 'max' and cv.res is None), name
+        if cv.fused:
+            assert cv.fused_ok, name
+    if name != 'model_random_widths_N120':   # yml widths: an f32 instantiation exists
+        assert any(plans.edge_enc.fast_ok.values()), name
 
 
 @pytest.mark.parametrize('name', ['model_trained_N500', 'model_random_L6_N300_k32'])
