@@ -73,6 +73,11 @@ _SIGNATURES = {
     'rg_build_graph': (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
     'rg_node_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _P, _P]),
     'rg_edge_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
+    'rg_node_features_f64': (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _P, _P]),
+    'rg_edge_features_f64': (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
+    'rg_pairs_from_dense_adjacency_workspace_size': (_S, [_I]),
+    'rg_pairs_from_dense_adjacency': (_I, [_P, _I, _P, _P, _P, _P, _S, _P]),
+    'rg_pair_add_rows_f32': (_I, [_P, _I, _I, _P, _P, _L, _P, _I, _P]),
     'rg_pack_kinematics': (_I, [_P, _P, _P, _P, _I, _P, _P]),
     'rg_edge_features_packed': (_I, [_P, _P, _P, _P, _P, _L, _P, _P]),
     'rg_link_pairs_workspace_size': (_S, [_I]),
@@ -117,6 +122,10 @@ _SIGNATURES = {
                                         _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     'rg_conv_blocks_workspace_size': (_S, [_I]),
     'rg_conv_blocks': (_I, [_P, _I, _P, _P, _P, _S, _P]),
+    'rg_frame_norm_workspace_size': (_S, [_I, _I]),
+    'rg_frame_norm': (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
+    'rg_gather_i32': (_I, [_P, _P, _I, _P, _P]),
+    'rg_lower_bound_i32': (_I, [_P, _P, _L, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
     'rg_segment_reduce_ranges_workspace_size': (_S, [_L, _I, _I]),
     'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P, _S,

@@ -380,14 +380,7 @@ static int launch(const Args& a, hipStream_t st) {
   constexpr int lds = Off::total();
   static_assert(lds <= DYN_LDS_MAX, "LDS image too large: read more layers from global memory");
   auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, Ns...>;
-  int dev = 0;
-  RG_CHECK_HIP(hipGetDevice(&dev));
-  static bool attr[64] = {};
-  if (dev < 64 && !attr[dev]) {  // per device (a process may drive several GPUs)
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     DYN_LDS_MAX));
-    attr[dev] = true;
-  }
+  RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   const long tiles = (a.rows + 31) / 32;
   long blocks = (tiles + 3) / 4;
   const long cap = lds <= 76 * 1024 ? 512 : 256;  // persistent: workgroups that fit at once

@@ -630,12 +630,7 @@ static int launch(const FArgs& a, hipStream_t st) {
   for (int l = 0; l < a.nl; ++l)
     RG_REQUIRE(a.L[l].woff == Off::get(l), RG_ERR_ARG, "rg_mlp_chain_fast: LDS layout of layer %d", l);
   auto kern = fast_chain_kernel<MODE, IN_F32, W0, W1, SPEC, FT, Ns...>;
-  static bool attr = false;
-  if (!attr) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     DYN_LDS_MAX));
-    attr = true;
-  }
+  RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   const long tiles = (a.rows + 31) / 32;
   long blocks = (tiles + FW - 1) / FW;
   const int per_cu = (FT == 512 && a.total_bytes <= 76 * 1024) ? 2 : 1;

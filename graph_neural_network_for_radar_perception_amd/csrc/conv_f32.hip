@@ -400,14 +400,7 @@ extern "C" int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* 
   a.n_nodes = n_nodes;
   a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
-  int dev = 0;
-  RG_CHECK_HIP(hipGetDevice(&dev));
-  static bool attr[64] = {};
-  if (dev < 64 && !attr[dev]) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)conv_f32_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, DYN_LDS_MAX));
-    attr[dev] = true;
-  }
+  RG_ENSURE_LDS(conv_f32_kernel, DYN_LDS_MAX);
   // one workgroup per CU (LDS); at least one per XCD counter
   int blocks = 256;
   const int need = (a.n_blocks + NW - 1) / NW;

@@ -613,16 +613,18 @@ extern "C" int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_l
   const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY &&
                      (m0.flags & m1.flags & u.flags & RG_LAYER_CENTERED);
   auto kern = leaky ? fused_conv_kernel<ACT_LEAKY> : fused_conv_kernel<-1>;
-  static bool attr[2] = {false, false};
-  if (!attr[leaky]) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     DYN_LDS_MAX));
-    attr[leaky] = true;
-  }
+  RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   int blocks = 256;  // a block table has at least ceil(N / NB) entries
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
   kern<<<blocks, CT, lds, st>>>(a);
-  RG_LAUNCH_CHECK();
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) {
+    // a launch that did not run leaves the counters as they were; one that failed part
+    // way could leave them nonzero: re-zero so the next launch does not skip blocks
+    (void)hipMemsetAsync(workspace, 0, 2 * sizeof(int), st);
+    set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__, hipGetErrorString(le));
+    return RG_ERR_HIP;
+  }
   return RG_OK;
 }
 

@@ -24,15 +24,33 @@
 
 #include <stdarg.h>
 
+#include <mutex>
+#include <set>
+#include <tuple>
+
 namespace rg {
 
-static char g_err[1024];
+// per host thread: two threads driving two GPUs never see each other's message
+static thread_local char g_err[1024];
 
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+hipError_t ensure_max_lds(const void* kernel, int bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({kernel, dev, bytes})) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert({kernel, dev, bytes});
+  return e;
 }
 
 static constexpr int KNN_BLOCK = 256;

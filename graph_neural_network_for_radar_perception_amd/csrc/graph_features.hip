@@ -26,11 +26,15 @@ namespace rg {
 //   range_conf = (float64(r) - max_range) / (min_range - max_range)   (np.float64 scalars)
 //   th         = |atan2(py, px)| rounded to float32
 //   azi_conf   = (th - f32(max_az)) / f32(min_az - max_az)     (python-float scalars: weak -> f32)
+// OutT = float: the tensorized float32 features (datagen_gnn.py:122); OutT = double: the
+// float64 array compute_node_features itself returns (np.stack promotes the float32
+// columns exactly; t_norm, degree / 10 and range_conf are float64 computations)
+template <typename OutT>
 __global__ __launch_bounds__(256) void node_features_kernel(
     const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vr,
     const float* __restrict__ rcs, const int64_t* __restrict__ ts, const int* __restrict__ deg,
     const int* __restrict__ frame_ptr, double min_r, double max_r, float az_den, float max_az,
-    float* __restrict__ out) {
+    OutT* __restrict__ out) {
   const int f = blockIdx.y;
   const int b = frame_ptr[f], e = frame_ptr[f + 1];
   if (b + (int)blockIdx.x * 256 >= e) return;  // block-uniform: no chunk of this frame
@@ -61,13 +65,13 @@ __global__ __launch_bounds__(256) void node_features_kernel(
     const double rc = ((double)r - max_r) / (min_r - max_r);
     const float th = fabsf((float)atan2((double)y, (double)x));
     const float az = div_rn((th - max_az), az_den);
-    float* o = out + (size_t)i * 6;
-    o[0] = vr[i];
-    o[1] = rcs[i];
-    o[2] = (float)tn;
-    o[3] = (float)dg;
-    o[4] = (float)rc;
-    o[5] = az;
+    OutT* o = out + (size_t)i * 6;
+    o[0] = (OutT)vr[i];
+    o[1] = (OutT)rcs[i];
+    o[2] = (OutT)tn;
+    o[3] = (OutT)dg;
+    o[4] = (OutT)rc;
+    o[5] = (OutT)az;
   }
 }
 
@@ -115,6 +119,28 @@ __global__ __launch_bounds__(256) void edge_features_kernel(
     for (int i = threadIdx.x; i < n4; i += 256) o4[i] = stage4[i];
     for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) out[(size_t)b0 * 7 + i] = stage[i];
     __syncthreads();
+  }
+}
+
+// compute_edge_features' own float64 result (graph_features.py:147-164): columns 0-5 are
+// float32 computations promoted exactly by np.stack; dt = (t_s - t_d) * 1e-6 is int64 x
+// python float = float64
+__global__ __launch_bounds__(256) void edge_features_f64_kernel(
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ vx,
+    const float* __restrict__ vy, const int64_t* __restrict__ ts, const int* __restrict__ src,
+    const int* __restrict__ dst, long n_edges, double* __restrict__ out) {
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < n_edges; p += (long)gridDim.x * 256) {
+    const int s = src[p];
+    const int d = dst[p];
+    const float dx = div10_rn((px[s] - px[d]));
+    const float dy = div10_rn((py[s] - py[d]));
+    const float dl = div10_rn(sqrt_rn(((dx * dx) + (dy * dy))));
+    const float dvx = (vx[s] - vx[d]);
+    const float dvy = (vy[s] - vy[d]);
+    const float dv = sqrt_rn(((dvx * dvx) + (dvy * dvy)));
+    double* o = out + (size_t)p * 7;
+    o[0] = dx; o[1] = dy; o[2] = dl; o[3] = dvx; o[4] = dvy; o[5] = dv;
+    o[6] = (double)(ts[s] - ts[d]) * 1e-6;
   }
 }
 
@@ -323,9 +349,37 @@ extern "C" int rg_node_features(const float* px, const float* py, const float* v
   if (n_nodes == 0) return RG_OK;
   // chunks of 256 nodes per frame at the mean frame size (larger frames stride)
   const int chunks = max(1, min(1024, (int)((n_nodes / n_frames + 255) / 256)));
-  node_features_kernel<<<dim3(chunks, n_frames), 256, 0, (hipStream_t)stream>>>(
+  node_features_kernel<float><<<dim3(chunks, n_frames), 256, 0, (hipStream_t)stream>>>(
       px, py, vr, rcs, timestamp, ball_degree, frame_ptr, min_range, max_range,
       (float)(min_azimuth - max_azimuth), (float)max_azimuth, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_node_features_f64(const float* px, const float* py, const float* vr,
+                                    const float* rcs, const int64_t* timestamp,
+                                    const int* ball_degree, const int* frame_ptr, int n_nodes,
+                                    int n_frames, double min_range, double max_range,
+                                    double min_azimuth, double max_azimuth, double* out,
+                                    void* stream) {
+  RG_REQUIRE(n_frames >= 1 && n_nodes >= 0, RG_ERR_ARG, "rg_node_features_f64: bad sizes");
+  if (n_nodes == 0) return RG_OK;
+  const int chunks = max(1, min(1024, (int)((n_nodes / n_frames + 255) / 256)));
+  node_features_kernel<double><<<dim3(chunks, n_frames), 256, 0, (hipStream_t)stream>>>(
+      px, py, vr, rcs, timestamp, ball_degree, frame_ptr, min_range, max_range,
+      (float)(min_azimuth - max_azimuth), (float)max_azimuth, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_edge_features_f64(const float* px, const float* py, const float* vx,
+                                    const float* vy, const int64_t* timestamp, const int* src,
+                                    const int* dst, long n_edges, double* out, void* stream) {
+  if (n_edges <= 0) return RG_OK;
+  long blocks = (n_edges + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  edge_features_f64_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(px, py, vx, vy, timestamp, src,
+                                                                    dst, n_edges, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -476,6 +530,81 @@ extern "C" int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* strea
 
 extern "C" size_t rg_pairs_from_edge_index_workspace_size(long n_edges) {
   return 2 * align256((size_t)(n_edges + 1) * sizeof(int)) + align256(scan_workspace_bytes(n_edges));
+}
+
+// edge_formation's pairs from a dense adjacency (gnn_blocks.py:295-296): the row-major
+// flags of triu(adj, 1) -> exclusive scan -> scatter == torch.nonzero(..., as_tuple=True)
+__global__ void dense_pair_flags(const uint8_t* __restrict__ adj, int n, long nn,
+                                 int* __restrict__ flag) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nn) return;
+  const int i = (int)(t / n), j = (int)(t - (long)i * n);
+  flag[t] = (j > i && adj[t] != 0) ? 1 : 0;
+}
+__global__ void dense_pair_scatter(const uint8_t* __restrict__ adj, int n, long nn,
+                                   const int* __restrict__ pos, int* __restrict__ ps,
+                                   int* __restrict__ pd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nn) return;
+  const int i = (int)(t / n), j = (int)(t - (long)i * n);
+  if (j > i && adj[t] != 0) {
+    ps[pos[t]] = i;
+    pd[pos[t]] = j;
+  }
+}
+// out[r] = x[idx0[r]] + x[idx1[r]] (float32, one rounding: the reference's x[i] + x[j])
+__global__ void pair_add_rows_kernel(const float* __restrict__ x, int ldx, int w,
+                                     const int* __restrict__ i0, const int* __restrict__ i1,
+                                     long rows, float* __restrict__ out, int ldo) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * w) return;
+  const long r = t / w;
+  const int c = (int)(t - r * w);
+  out[r * ldo + c] = x[(size_t)i0[r] * ldx + c] + x[(size_t)i1[r] * ldx + c];
+}
+
+extern "C" size_t rg_pairs_from_dense_adjacency_workspace_size(int n_nodes) {
+  const long nn = (long)n_nodes * n_nodes;
+  return 2 * align256((size_t)(nn + 1) * sizeof(int)) + scan_workspace_bytes(nn);
+}
+
+extern "C" int rg_pairs_from_dense_adjacency(const void* adj, int n_nodes, int* pair_src,
+                                             int* pair_dst, int* n_pairs, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(n_nodes >= 0 && n_nodes <= 46340, RG_ERR_ARG,
+             "rg_pairs_from_dense_adjacency: n_nodes=%d outside 0..46340", n_nodes);
+  RG_REQUIRE(workspace_bytes >= rg_pairs_from_dense_adjacency_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_pairs_from_dense_adjacency: workspace too small");
+  const long nn = (long)n_nodes * n_nodes;
+  if (nn == 0) {
+    RG_CHECK_HIP(hipMemsetAsync(n_pairs, 0, sizeof(int), st));
+    return RG_OK;
+  }
+  char* w = (char*)workspace;
+  int* flag = (int*)w;
+  w += align256((size_t)(nn + 1) * sizeof(int));
+  int* pos = (int*)w;
+  w += align256((size_t)(nn + 1) * sizeof(int));
+  dense_pair_flags<<<ceil_div(nn, 256), 256, 0, st>>>((const uint8_t*)adj, n_nodes, nn, flag);
+  RG_LAUNCH_CHECK();
+  int rc = exclusive_scan(flag, nn, pos, n_pairs, w, st);
+  if (rc) return rc;
+  dense_pair_scatter<<<ceil_div(nn, 256), 256, 0, st>>>((const uint8_t*)adj, n_nodes, nn, pos,
+                                                        pair_src, pair_dst);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_pair_add_rows_f32(const float* x, int ldx, int w, const int* idx0,
+                                    const int* idx1, long rows, float* out, int ld_out,
+                                    void* stream) {
+  RG_REQUIRE(w >= 0 && rows >= 0, RG_ERR_ARG, "rg_pair_add_rows_f32: bad sizes");
+  if (rows == 0 || w == 0) return RG_OK;
+  pair_add_rows_kernel<<<ceil_div(rows * w, 256), 256, 0, (hipStream_t)stream>>>(
+      x, ldx, w, idx0, idx1, rows, out, ld_out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
 }
 
 extern "C" int rg_pairs_from_edge_index(const int64_t* edge_index, long n_edges, int* pair_src,

@@ -530,12 +530,7 @@ static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
   const size_t dbytes = (sizeof(ChainLayer) * RG_MAX_LAYERS + 15) & ~(size_t)15;
   const size_t lds = dbytes + (WLDS ? ((size_t)(a.wbytes + 15) & ~(size_t)15) : 0) +
                      (size_t)CH_WAVES * TR * a.sstride * sizeof(T);
-  static bool attr_set = false;
-  if (!attr_set) {
-    RG_CHECK_HIP(hipFuncSetAttribute((const void*)chain_kernel<T, WLDS>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT));
-    attr_set = true;
-  }
+  RG_ENSURE_LDS((chain_kernel<T, WLDS>), (int)LDS_LIMIT);
   const long tiles = (rows + TR - 1) / TR;
   long blocks = (tiles + CH_WAVES - 1) / CH_WAVES;
   // persistent grid: enough resident workgroups to fill 256 CUs

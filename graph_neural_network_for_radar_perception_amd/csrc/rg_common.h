@@ -18,6 +18,12 @@ namespace rg {
 // ---------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) once per (kernel, device): the
+// attribute is per device, and a process may drive several GPUs (thread-safe)
+hipError_t ensure_max_lds(const void* kernel, int bytes);
+
+#define RG_ENSURE_LDS(kern, bytes) RG_CHECK_HIP(::rg::ensure_max_lds((const void*)(kern), (bytes)))
+
 #define RG_CHECK_HIP(expr)                                                        \
   do {                                                                            \
     hipError_t _e = (expr);                                                       \

@@ -31,7 +31,8 @@ import torch
 import torch.nn as nn
 
 from . import _native as nat
-from .common import Activation, channel_normalization, ffn_block
+from .common import (Activation, channel_normalization, ffn_block, group_normalization,
+                     layer_normalization)
 
 DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16)}
 
@@ -58,6 +59,13 @@ class LayerSpec:
     mu: Optional[torch.Tensor]
     std: Optional[torch.Tensor]
     act: str
+    norm: str = 'channel'   # 'channel' (per row, fused) | 'layer' | 'group' (per frame)
+    groups: int = 1
+
+    @property
+    def frame_norm(self) -> bool:
+        """layer / group normalisation: statistics over a whole frame's rows."""
+        return self.mu is not None and self.norm != 'channel'
 
     @property
     def in_dim(self):
@@ -69,14 +77,18 @@ class LayerSpec:
 
 
 def _norm_params(norm):
+    """(mu, std, kind, groups) of a norm module (common.py:208-253)."""
     if norm is None:
-        return None, None
-    if not isinstance(norm, channel_normalization):
-        raise NotImplementedError(
-            f'{type(norm).__name__}: only channel_normalization (the shipped config, '
-            'configuration_radarscenes_gnn.yml:51) is fused in the HIP chain kernels; '
-            'layer/group normalisation need frame-wide statistics')
-    return norm.mu, norm.std
+        return None, None, 'channel', 1
+    if isinstance(norm, channel_normalization):
+        return norm.mu, norm.std, 'channel', 1
+    if isinstance(norm, layer_normalization):
+        return norm.mu, norm.std, 'layer', 1
+    if isinstance(norm, group_normalization):
+        if norm.num_groups is None or norm.num_groups < 1:
+            raise ValueError('group_normalization needs num_groups >= 1')
+        return norm.mu, norm.std, 'group', int(norm.num_groups)
+    raise NotImplementedError(f'{type(norm).__name__}')
 
 
 def specs_from_modules(mods) -> List[LayerSpec]:
@@ -94,8 +106,8 @@ def specs_from_modules(mods) -> List[LayerSpec]:
             lin, norm, act = m[0], (m[1] if len(m) > 1 else None), 'none'
         else:
             raise TypeError(f'cannot lower {type(m).__name__} to a chain layer')
-        mu, sd = _norm_params(norm)
-        out.append(LayerSpec(lin.weight, lin.bias, mu, sd, act))
+        mu, sd, kind, groups = _norm_params(norm)
+        out.append(LayerSpec(lin.weight, lin.bias, mu, sd, act, kind, groups))
     return out
 
 
@@ -151,7 +163,35 @@ class ChainPlan:
         self.in_dim = specs[0].in_dim
         self.out_dim = specs[-1].out_dim
         self.use_fast = True   # try rg_mlp_chain_fast (bf16) / rg_mlp_chain_f32 (fp32) first
+        self.pieces = None
+        if any(s.frame_norm for s in specs):
+            self._split_frame_norms()
+            return
         self._pack()
+
+    @property
+    def has_frame_norm(self) -> bool:
+        return self.pieces is not None
+
+    def _split_frame_norms(self):
+        """layer / group normalisation (common.py:223-253) normalise over a whole frame,
+        which no fused chain can see: the chain is cut after every such layer.  Each piece
+        is a ChainPlan whose last layer (when it carries a frame norm) is packed as a bare
+        Linear; rg_frame_norm then applies the norm + activation with per-frame stats."""
+        if self.dtype != 'fp32':
+            raise NotImplementedError('layer / group normalisation run in fp32 only')
+        self.pieces = []
+        cur = []
+        for sp in self.specs:
+            if sp.frame_norm:
+                cur.append(LayerSpec(sp.weight, sp.bias, None, None, 'none'))
+                self.pieces.append((ChainPlan(cur, self.dtype, self.device), sp))
+                cur = []
+            else:
+                cur.append(sp)
+        if cur:
+            self.pieces.append((ChainPlan(cur, self.dtype, self.device), None))
+        self.sig = self._signature()
 
     def _signature(self):
         sig = []
@@ -191,12 +231,61 @@ class ChainPlan:
         self.sig = self._signature()
 
     def refresh(self):
+        if self.pieces is not None:
+            for p, _ in self.pieces:
+                p.refresh()
+            return
         if self._signature() != self.sig:
             self._pack()
 
     def invalidate(self):
         """Parameters were written behind torch's version counters (FusedSGD)."""
         self.sig = None
+        if self.pieces is not None:
+            for p, _ in self.pieces:
+                p.invalidate()
+
+    def _call_pieces(self, rows, out, in0, w0, mode, in1, w1, in2, w2, idx0, idx1, residual,
+                     rows_dev, segs):
+        """Chain with frame-wide norms: pieces + rg_frame_norm.  segs = (seg_ptr int32
+        [n_seg+1] device, n_seg): the frames' row ranges; None = all rows one frame."""
+        lib = nat.lib()
+        dev = self.device
+        st = nat.stream_ptr(dev)
+        if segs is None:
+            if rows_dev is not None:
+                sp = torch.cat((torch.zeros(1, dtype=torch.int32, device=dev),
+                                rows_dev.reshape(1).to(torch.int32)))
+            else:
+                sp = torch.tensor([0, int(rows)], dtype=torch.int32, device=dev)
+            segs = (sp, 1)
+        seg_ptr, n_seg = segs
+        cur = (in0, w0, mode, in1, w1, in2, w2, idx0, idx1)
+        for pi, (plan, nspec) in enumerate(self.pieces):
+            last = pi == len(self.pieces) - 1
+            dst = out if last else torch.empty((out.shape[0], plan.out_dim), dtype=torch.float32,
+                                               device=dev)
+            a0, aw0, am, a1, aw1, a2, aw2, ai0, ai1 = cur
+            plan(rows, dst, a0, aw0, mode=am, in1=a1, w1=aw1, in2=a2, w2=aw2, idx0=ai0,
+                 idx1=ai1, residual=residual if (last and nspec is None) else None,
+                 rows_dev=rows_dev)
+            if nspec is not None:
+                groups = nspec.groups if nspec.norm == 'group' else 1
+                C = nspec.out_dim
+                if C % groups:
+                    raise RuntimeError(f'group_normalization: {C} channels not divisible by '
+                                       f'{groups} groups')
+                wsz = lib.rg_frame_norm_workspace_size(n_seg, groups)
+                ws = torch.empty(max(wsz, 1), dtype=torch.uint8, device=dev)
+                res = residual if last else None
+                nat.check(lib.rg_frame_norm(dst.data_ptr(), dst.stride(0), C, groups,
+                                            seg_ptr.data_ptr(), n_seg, nspec.mu.data_ptr(),
+                                            nspec.std.data_ptr(), nat.ACT[nspec.act], nat.ptr(res),
+                                            res.stride(0) if res is not None else 0,
+                                            dst.data_ptr(), dst.stride(0), ws.data_ptr(), wsz, st),
+                          'rg_frame_norm')
+            cur = (dst, plan.out_dim, nat.IN_DENSE, None, 0, None, 0, None, None)
+        return out
 
     def _f32_layers(self):
         """The chain packed RG_PACK_F32_FAST for rg_mlp_chain_f32 (lazily: training chains
@@ -208,7 +297,10 @@ class ChainPlan:
 
     def __call__(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
                  mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
-                 idx0=None, idx1=None, residual=None, rows_dev=None):
+                 idx0=None, idx1=None, residual=None, rows_dev=None, segs=None):
+        if self.pieces is not None:
+            return self._call_pieces(rows, out, in0, w0, mode, in1, w1, in2, w2, idx0, idx1,
+                                     residual, rows_dev, segs)
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
         if (self.use_fast and self.dt == nat.RG_F32 and mode in (nat.IN_DENSE, nat.IN_PAIRADD)
@@ -297,6 +389,44 @@ class DeviceGraph:
         self.n_edges = n_edges
         self.n_pairs = n_pairs
         self._conv_blocks = None
+        self.frame_ptr = None      # int32 [B+1] device node offsets of the frames (optional)
+        self.n_frames = None
+        self._segs = {}
+
+    def set_frames(self, frame_ptr: torch.Tensor, n_frames: int):
+        """Frame boundaries (node offsets); needed by layer / group normalisation, whose
+        statistics run over one frame's rows (common.py:223-253)."""
+        self.frame_ptr = frame_ptr.to(torch.int32).contiguous()
+        self.n_frames = int(n_frames)
+        self._segs = {}
+        return self
+
+    def segs(self, kind: str):
+        """(seg_ptr int32 [B+1] device, B): each frame's row range among the graph's
+        'node' rows, destination-major 'edge' rows or 'pair' rows (sorted by source)."""
+        if self.frame_ptr is None:
+            return None
+        if kind in self._segs:
+            return self._segs[kind]
+        lib = nat.lib()
+        dev = self.frame_ptr.device
+        st = nat.stream_ptr(dev)
+        B = self.n_frames
+        if kind == 'node':
+            out = self.frame_ptr
+        elif kind == 'edge':
+            out = torch.empty(B + 1, dtype=torch.int32, device=dev)
+            nat.check(lib.rg_gather_i32(self.seg_ptr.data_ptr(), self.frame_ptr.data_ptr(), B + 1,
+                                        out.data_ptr(), st), 'rg_gather_i32')
+        elif kind == 'pair':
+            out = torch.empty(B + 1, dtype=torch.int32, device=dev)
+            nat.check(lib.rg_lower_bound_i32(self.pair_src.data_ptr(), self.n_pairs_dev.data_ptr(),
+                                             self.pair_src.shape[0], self.frame_ptr.data_ptr(),
+                                             B + 1, out.data_ptr(), st), 'rg_lower_bound_i32')
+        else:
+            raise ValueError(kind)
+        self._segs[kind] = (out, B)
+        return self._segs[kind]
 
     # few 8-node runs per wave of the fused conv's 2 048-wave grid: dynamic scheduling of
     # whole runs leaves a tail of the heaviest runs (dense radius frames, BASELINE config 5)
@@ -496,6 +626,8 @@ class ConvPlan:
         self.fused = None
         if self.res is not None or self.aggr == 'max':
             return
+        if any(c.has_frame_norm for c in self.chains()):
+            return
         if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
             return
         if self.dtype == 'fp32':
@@ -590,6 +722,8 @@ class ModelPlans:
         self.link_pair = mk(list(pl.stem) + [pl.pred_cls.head[0], pl.pred_cls.head[1]])
         self.cls_stem = mk(list(pc.stem)) if len(pc.stem) else None
         self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
+        # layer / group normalisation anywhere: chains need each frame's row ranges
+        self.frame_norm = any(c.has_frame_norm for c in self.chains())
 
     def chains(self):
         out = [self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
@@ -625,6 +759,23 @@ class ForwardOutputs:
     x: torch.Tensor
     cluster_ptr: Optional[torch.Tensor] = None   # proposal branch: the clusters used
     cluster_idx: Optional[torch.Tensor] = None
+
+
+def cluster_segs(cluster_ptr, cluster_idx, n_clusters: int, frame_ptr, n_frames: int):
+    """Each frame's range of cluster rows: clusters come frame by frame, so the number of
+    clusters whose first member lies before frame f's first node is a binary search over
+    the first members (the predicate is monotone even if a frame's own clusters are not
+    sorted)."""
+    lib = nat.lib()
+    dev = cluster_ptr.device
+    st = nat.stream_ptr(dev)
+    first = torch.empty(n_clusters, dtype=torch.int32, device=dev)
+    nat.check(lib.rg_gather_i32(cluster_idx.data_ptr(), cluster_ptr.data_ptr(), n_clusters,
+                                first.data_ptr(), st), 'rg_gather_i32')
+    out = torch.empty(n_frames + 1, dtype=torch.int32, device=dev)
+    nat.check(lib.rg_lower_bound_i32(first.data_ptr(), None, n_clusters, frame_ptr.data_ptr(),
+                                     n_frames + 1, out.data_ptr(), st), 'rg_lower_bound_i32')
+    return out, n_frames
 
 
 def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst: torch.Tensor,
@@ -664,11 +815,18 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             buf[name] = t
         return t
 
+    if plans.frame_norm:
+        def segs(kind):
+            return g.segs(kind)
+    else:
+        def segs(kind):
+            return None
     x = alloc('x0', (N, plans.node_enc.out_dim), T)
-    plans.node_enc(N, x, node_feats, node_feats.shape[1])
+    plans.node_enc(N, x, node_feats, node_feats.shape[1], segs=segs('node'))
     e = alloc('e', (Ecap, plans.edge_enc.out_dim), T)
     mark('edge_encoder:start')
-    plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev)
+    plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
+                   segs=segs('edge'))
     mark('edge_encoder:end')
     for li, cv in enumerate(plans.convs):
         C = x.shape[1]
@@ -685,7 +843,7 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
         msg = alloc('msg', (Ecap, cv.c_msg), T)
         mark('message_chain:start')
         cv.msg(Ecap, msg, x, C, mode=nat.IN_GATHER3, in2=e, w2=e.shape[1], idx0=g.dst,
-               idx1=g.src, rows_dev=ne_dev)
+               idx1=g.src, rows_dev=ne_dev, segs=segs('edge'))
         mark('message_chain:end')
         agg = alloc('agg', (N, cv.c_msg), T)
         mark('segment_reduce:start')
@@ -693,30 +851,31 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
         mark('segment_reduce:end')
         if cv.res is not None:
             ident = alloc(f'id{li % 2}', (N, cv.c_out), T)
-            cv.res(N, ident, x, C)
+            cv.res(N, ident, x, C, segs=segs('node'))
         else:
             ident = x
-        cv.upd(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg, w1=cv.c_msg, residual=ident)
+        cv.upd(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg, w1=cv.c_msg, residual=ident,
+               segs=segs('node'))
         x = xn
     C = x.shape[1]
     f32 = torch.float32
     node_cls = torch.empty((N, plans.node_head.out_dim), dtype=f32, device=dev)
-    plans.node_head(N, node_cls, x, C)
+    plans.node_head(N, node_cls, x, C, segs=segs('node'))
     node_reg = torch.empty((N, plans.offset_head.out_dim), dtype=f32, device=dev)
-    plans.offset_head(N, node_reg, x, C)
+    plans.offset_head(N, node_reg, x, C, segs=segs('node'))
     if plans.link_node is not None:
         s = alloc('link_s', (N, plans.link_node.out_dim), T)
-        plans.link_node(N, s, x, C)
+        plans.link_node(N, s, x, C, segs=segs('node'))
     else:
         s = x
     ucap = n_pairs_cap if n_pairs_cap is not None else (g.n_pairs if g.n_pairs is not None
                                                         else g.pair_src.shape[0])
     link = torch.empty((ucap, plans.link_pair.out_dim), dtype=f32, device=dev)
     plans.link_pair(ucap, link, s, s.shape[1], mode=nat.IN_PAIRADD, idx0=g.pair_src,
-                    idx1=g.pair_dst, rows_dev=g.n_pairs_dev)
+                    idx1=g.pair_dst, rows_dev=g.n_pairs_dev, segs=segs('pair'))
     if plans.cls_stem is not None:
         h = alloc('cls_h', (N, plans.cls_stem.out_dim), T)
-        plans.cls_stem(N, h, x, C)
+        plans.cls_stem(N, h, x, C, segs=segs('node'))
     else:
         h = x
     if cluster_ptr is None:
@@ -724,7 +883,10 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
     pooled = alloc('pooled', (n_clusters, h.shape[1]), T)
     segment_reduce(h, cluster_ptr, n_clusters, 'max', pooled, idx=cluster_idx)
     obj = torch.empty((n_clusters, plans.cls_head.out_dim), dtype=f32, device=dev)
-    plans.cls_head(n_clusters, obj, pooled, pooled.shape[1])
+    csegs = None
+    if plans.frame_norm and g.frame_ptr is not None and n_clusters > 0:
+        csegs = cluster_segs(cluster_ptr, cluster_idx, n_clusters, g.frame_ptr, g.n_frames)
+    plans.cls_head(n_clusters, obj, pooled, pooled.shape[1], segs=csegs)
     return ForwardOutputs(node_cls, node_reg, link, obj, x, cluster_ptr, cluster_idx)
 
 
@@ -765,6 +927,77 @@ def run_blocks(mods, x: torch.Tensor, dtype: str = 'fp32') -> torch.Tensor:
     out = torch.empty((xin.shape[0], plan.out_dim), dtype=torch.float32, device=x.device)
     plan(xin.shape[0], out, xin, xin.shape[1])
     return out
+
+
+def pairs_from_dense_adjacency(adj_matrix: torch.Tensor):
+    """edge_formation's pairs (gnn_blocks.py:295-296: nonzero(triu(adj, 1)), row-major)
+    from a dense [N, N] adjacency on the device -> (pair_src int32, pair_dst int32, U).
+    One host synchronisation (U), where the reference's torch.nonzero synchronises too."""
+    _require_device(adj_matrix, 'adj_matrix')
+    lib = nat.lib()
+    dev = adj_matrix.device
+    n = int(adj_matrix.shape[0])
+    if adj_matrix.dim() != 2 or adj_matrix.shape[1] != n:
+        raise ValueError(f'adj_matrix must be square, got {tuple(adj_matrix.shape)}')
+    adj = adj_matrix.contiguous()
+    if adj.dtype not in (torch.bool, torch.uint8):
+        adj = (adj != 0).contiguous()
+    ws = torch.empty(lib.rg_pairs_from_dense_adjacency_workspace_size(n), dtype=torch.uint8,
+                     device=dev)
+    cap = max(n * (n - 1) // 2, 1)
+    ps = torch.empty(cap, dtype=torch.int32, device=dev)
+    pd = torch.empty(cap, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    nat.check(lib.rg_pairs_from_dense_adjacency(adj.data_ptr(), n, ps.data_ptr(), pd.data_ptr(),
+                                                cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                nat.stream_ptr(dev)),
+              'rg_pairs_from_dense_adjacency')
+    U = int(cnt.item())
+    return ps[:max(U, 1)], pd[:max(U, 1)], U
+
+
+def pair_add_rows(h: torch.Tensor, ps: torch.Tensor, pd: torch.Tensor, U: int) -> torch.Tensor:
+    """x[i] + x[j] for the pairs (gnn_blocks.py:297), float32 [U, C]."""
+    x = h.to(torch.float32).contiguous()
+    out = torch.empty((U, x.shape[1]), dtype=torch.float32, device=x.device)
+    nat.check(nat.lib().rg_pair_add_rows_f32(x.data_ptr(), x.stride(0), x.shape[1], ps.data_ptr(),
+                                             pd.data_ptr(), U, out.data_ptr(), out.stride(0),
+                                             nat.stream_ptr(x.device)), 'rg_pair_add_rows_f32')
+    return out
+
+
+def run_pair_chain(mods, h: torch.Tensor, ps: torch.Tensor, pd: torch.Tensor, U: int,
+                   dtype: str = 'fp32') -> torch.Tensor:
+    """ffn_block chain on the pair sums h[i] + h[j] (RG_IN_PAIRADD: the sum is formed in
+    the chain's operand load, never stored)."""
+    _require_device(h, 'input')
+    plan = _plan_for(mods, dtype, h.device)
+    x = h.to(torch.float32).contiguous()
+    out = torch.empty((U, plan.out_dim), dtype=torch.float32, device=h.device)
+    if U > 0:
+        plan(U, out, x, x.shape[1], mode=nat.IN_PAIRADD, idx0=ps, idx1=pd)
+    return out
+
+
+def run_cluster_head(stem_mods, head_mods, x: torch.Tensor, cluster_node_idx,
+                     dtype: str = 'fp32') -> torch.Tensor:
+    """object_classification.forward (gnn_blocks.py:378-389): stem, channel max over each
+    cluster's rows (rg_segment_reduce 'max' over a gathered CSR), head."""
+    _require_device(x, 'input')
+    dev = x.device
+    h = run_blocks(stem_mods, x, dtype) if stem_mods else x.to(torch.float32).contiguous()
+    lens = [int(c.numel()) for c in cluster_node_idx]
+    if any(n == 0 for n in lens):
+        # reference: torch.max over an empty selection raises
+        raise IndexError('max(): Expected reduction dim 0 to have non-zero size.')
+    ncl = len(lens)
+    ptr = torch.tensor([0] + lens, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+    idx = (torch.cat([c.reshape(-1).to(dev, torch.int64) for c in cluster_node_idx]).to(torch.int32)
+           if ncl else torch.zeros(1, dtype=torch.int32, device=dev))
+    pooled = torch.empty((ncl, h.shape[1]), dtype=torch.float32, device=dev)
+    if ncl:
+        segment_reduce(h, ptr, ncl, 'max', pooled, idx=idx.contiguous())
+    return run_blocks(head_mods, pooled, dtype)
 
 
 def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):

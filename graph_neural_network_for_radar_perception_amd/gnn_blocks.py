@@ -175,6 +175,14 @@ class edge_formation(nn.Module):
         self.stem = nn.Sequential(*[ffn_block(in_channels, in_channels, activation, norm_layer,
                                               num_groups) for _ in range(num_blocks)])
 
+    def forward(self, x: torch.Tensor, adj_matrix: torch.Tensor) -> torch.Tensor:
+        """gnn_blocks.py:292-298: stem, then x[i] + x[j] over nonzero(triu(adj, 1))."""
+        from . import engine
+        engine._require_device(x, 'x')
+        h = engine.run_blocks(list(self.stem), x) if len(self.stem) else x.float().contiguous()
+        ps, pd, U = engine.pairs_from_dense_adjacency(adj_matrix)
+        return engine.pair_add_rows(h, ps, pd, U)
+
 
 class link_predictions(nn.Module):
     """gnn_blocks.py:301-344."""
@@ -188,6 +196,17 @@ class link_predictions(nn.Module):
         self.pred_cls = FFN_TaskSpecificHead(stem_channels[-1], num_classes, activation,
                                              norm_layer, num_groups, CLS_MEAN, CLS_STD, CLS_BIAS)
 
+    def forward(self, x: torch.Tensor, adj_matrix: torch.Tensor) -> torch.Tensor:
+        """gnn_blocks.py:340-344: edge_formation -> stem -> head; the pair sum is formed in
+        the pair chain's operand load (RG_IN_PAIRADD)."""
+        from . import engine
+        engine._require_device(x, 'x')
+        ce = self.compute_edge
+        h = engine.run_blocks(list(ce.stem), x) if len(ce.stem) else x.float().contiguous()
+        ps, pd, U = engine.pairs_from_dense_adjacency(adj_matrix)
+        return engine.run_pair_chain(list(self.stem) + [self.pred_cls.head[0],
+                                                         self.pred_cls.head[1]], h, ps, pd, U)
+
 
 class object_classification(nn.Module):
     """gnn_blocks.py:347-389: node stem, channel max over each cluster, head."""
@@ -197,6 +216,13 @@ class object_classification(nn.Module):
         self.stem = _stem(in_channels, stem_channels, activation, norm_layer, num_groups)
         self.pred_cls = FFN_TaskSpecificHead(stem_channels[-1], num_classes, activation,
                                              norm_layer, num_groups, CLS_MEAN, CLS_STD, CLS_BIAS)
+
+    def forward(self, x: torch.Tensor, cluster_node_idx: List[torch.Tensor]) -> torch.Tensor:
+        """gnn_blocks.py:378-389: stem, channel max over each cluster's nodes, head."""
+        from . import engine
+        return engine.run_cluster_head(list(self.stem), [self.pred_cls.head[0],
+                                                          self.pred_cls.head[1]], x,
+                                       cluster_node_idx)
 
 
 class node_predictions(nn.Module):

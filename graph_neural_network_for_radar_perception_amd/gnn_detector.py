@@ -153,6 +153,8 @@ class Model_Inference(nn.Module):
                                                            edge_index, cluster_node_idx)
         N = nf.shape[0]
         g = engine.DeviceGraph.from_edge_index(ei, N)
+        g.set_frames(torch.tensor([0] + sizes, dtype=torch.int64).cumsum(0).to(torch.int32)
+                     .to(nf.device), len(sizes))
         E = g.n_edges
         e_dst = torch.empty((max(E, 1), ef.shape[1]), dtype=torch.float32, device=nf.device)
         if E > 0:

@@ -9,8 +9,10 @@ Drop-in functions (same names, arguments and result keys as
   compute_edge_features(data_dict, adj_list)             graph_features.py:147-164
 
 They take and return numpy arrays like the reference (one host round trip per
-call; float features come back as float32, the dtype the tensorization
-``datagen_gnn.py:120-124`` converts them to).  The batched device-side entry
+call) with the reference's dtypes: int64 indices, bool adjacency, float32 distances,
+and float64 node / edge features computed on the device exactly as numpy does
+(graph_features.py:144,164; the tensorization ``datagen_gnn.py:120-124`` then casts them
+to float32, which the batched device path below produces directly).  The batched device-side entry
 point for many frames is ``FrameBatch`` + ``build_graph_batch`` below, which
 keeps everything in HBM and never materialises an N x N matrix.
 """
@@ -90,7 +92,8 @@ def compute_radius_graph(data_dict: dict, eps: float) -> dict:
 
 def compute_node_features(data_dict, node_degree, include_region_confidence=False,
                           min_range=None, max_range=None, min_azimuth=None, max_azimuth=None):
-    """graph_features.py:117-144 on the GPU (float32 result)."""
+    """graph_features.py:117-144 on the GPU: float64 [N, 6] (or [N, 4] without the region
+    confidences), like the reference's np.stack."""
     dev = _device()
     d = _upload(data_dict, dev)
     n = int(d['meas_px'].shape[0])
@@ -103,21 +106,31 @@ def compute_node_features(data_dict, node_degree, include_region_confidence=Fals
         grid_min_th = 0.0 if min_azimuth is None else float(min_azimuth)
         grid_max_th = 1.0 if max_azimuth is None else float(max_azimuth)
 
-    out = engine.node_features(d, deg, fp, 1, _C)
+    out = torch.empty((n, 6), dtype=torch.float64, device=dev)
+    nat.check(nat.lib().rg_node_features_f64(
+        d['meas_px'].data_ptr(), d['meas_py'].data_ptr(), d['meas_vr'].data_ptr(),
+        d['meas_rcs'].data_ptr(), d['meas_timestamp'].data_ptr(), deg.data_ptr(), fp.data_ptr(),
+        n, 1, _C.grid_min_r, _C.grid_max_r, _C.grid_min_th, _C.grid_max_th, out.data_ptr(),
+        nat.stream_ptr(dev)), 'rg_node_features_f64')
     out = out if include_region_confidence else out[:, :4]
     return out.cpu().numpy()
 
 
 def compute_edge_features(data_dict, adj_list):
-    """graph_features.py:147-164 on the GPU (float32 result, edge order of adj_list)."""
+    """graph_features.py:147-164 on the GPU: float64 [E, 7] in the edge order of adj_list,
+    like the reference's np.stack (dt is a float64 product there)."""
     dev = _device()
     d = _upload(data_dict, dev)
     al = torch.from_numpy(np.asarray(adj_list).astype(np.int32)).to(dev)
     E = int(al.shape[1])
     src = al[0].contiguous()
     dst = al[1].contiguous()
-    out = engine.edge_features(d, src, dst, None, E)
-    return out[:E].cpu().numpy()
+    out = torch.empty((E, 7), dtype=torch.float64, device=dev)
+    nat.check(nat.lib().rg_edge_features_f64(
+        d['meas_px'].data_ptr(), d['meas_py'].data_ptr(), d['meas_vx'].data_ptr(),
+        d['meas_vy'].data_ptr(), d['meas_timestamp'].data_ptr(), src.data_ptr(), dst.data_ptr(),
+        E, out.data_ptr(), nat.stream_ptr(dev)), 'rg_edge_features_f64')
+    return out.cpu().numpy()
 
 
 # --------------------------------------------------------------------------- batched device API
@@ -203,6 +216,7 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
         if ws_cache is not None:
             ws_cache[cap_key] = cap
     g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
+    g.set_frames(batch.frame_ptr, batch.n_frames)
     nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)
     # destination-major edge (src = g.src[p] -> dst = g.dst[p])
     ef = engine.edge_features(batch.arrays, g.src, g.dst, ne, cap)

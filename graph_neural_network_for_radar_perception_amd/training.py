@@ -79,6 +79,10 @@ class TrainChain:
 
     def __init__(self, mods, device, ws: Workspaces):
         self.specs = specs_from_modules(mods)
+        if any(sp.frame_norm for sp in self.specs):
+            raise NotImplementedError(
+                'training with layer_normalization / group_normalization (frame-wide '
+                'statistics) has no native backward yet; inference supports them')
         if len(self.specs) > nat.MAX_LAYERS:
             raise NotImplementedError(f'chain of {len(self.specs)} layers > {nat.MAX_LAYERS}')
         self.plan = ChainPlan(self.specs, 'fp32', device)

@@ -131,6 +131,17 @@ int rg_edge_features(const float* px, const float* py, const float* vx, const fl
                      const int64_t* timestamp, const int* src, const int* dst,
                      const int* n_edges_dev, long n_edges, float* out, void* stream);
 
+/* The float64 arrays compute_node_features / compute_edge_features themselves return
+ * (graph_features.py:144,164: np.stack promotes the float32 columns exactly, while
+ * t_norm, degree/10, range_conf and dt are float64 computations), same layouts. */
+int rg_node_features_f64(const float* px, const float* py, const float* vr, const float* rcs,
+                         const int64_t* timestamp, const int* ball_degree, const int* frame_ptr,
+                         int n_nodes, int n_frames, double min_range, double max_range,
+                         double min_azimuth, double max_azimuth, double* out, void* stream);
+int rg_edge_features_f64(const float* px, const float* py, const float* vx, const float* vy,
+                         const int64_t* timestamp, const int* src, const int* dst, long n_edges,
+                         double* out, void* stream);
+
 /* rg_edge_features from node kinematics packed once per batch: kin = float4[n_nodes]
  * (px, py, vx, vy) from rg_pack_kinematics (16-B aligned).  Same results, two gathers
  * per edge endpoint instead of five. */
@@ -139,6 +150,18 @@ int rg_pack_kinematics(const float* px, const float* py, const float* vx, const 
 int rg_edge_features_packed(const void* kin, const int64_t* timestamp, const int* src,
                             const int* dst, const int* n_edges_dev, long n_edges, float* out,
                             void* stream);
+
+/* edge_formation's pairs from a DENSE adjacency (gnn_blocks.py:295-296: torch.nonzero(
+ * torch.triu(adj, 1), as_tuple=True), row-major): adj = uint8 / bool [n][n] (n <= 46340);
+ * pair_src / pair_dst int32[capacity >= number of pairs]; n_pairs int32[1] (device). */
+size_t rg_pairs_from_dense_adjacency_workspace_size(int n_nodes);
+int rg_pairs_from_dense_adjacency(const void* adj, int n_nodes, int* pair_src, int* pair_dst,
+                                  int* n_pairs, void* workspace, size_t workspace_bytes,
+                                  void* stream);
+/* out[r][0..w) = x[idx0[r]] + x[idx1[r]] in float32 (edge_formation's x[i] + x[j],
+ * gnn_blocks.py:297) */
+int rg_pair_add_rows_f32(const float* x, int ldx, int w, const int* idx0, const int* idx1,
+                         long rows, float* out, int ld_out, void* stream);
 
 /* Undirected link pairs of edge_formation (gnn_blocks.py:295-296):
  * nonzero(triu(adj,1)) row-major == CSR positions with col > row.
@@ -277,7 +300,9 @@ int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx,
  * RG_PACK_FAST_CHAIN, upd_layer RG_PACK_FAST_UPD.  Returns RG_ERR_UNSUPPORTED for
  * other shapes / aggregations (use rg_mlp_chain + rg_segment_reduce).
  * workspace: rg_conv_layer_workspace_size() bytes, ZEROED before the first call (block
- * counters; every completed launch leaves them zero again, so no per-call memset). */
+ * counters; every completed launch leaves them zero again, so no per-call memset; a
+ * failed launch re-zeroes them).  One workspace per stream: two launches in flight on
+ * different streams must not share it. */
 size_t rg_conv_layer_workspace_size(void);
 int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
                         const void* x, int ldx, const void* e, int lde, const int* seg_ptr,
@@ -298,6 +323,29 @@ int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_l
 size_t rg_conv_blocks_workspace_size(int n_nodes);
 int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------- frame-wide normalisations */
+
+/* layer_normalization (groups = 1) / group_normalization (groups = G) of
+ * modules/neural_net/common.py:223-253 over row segments (one segment = one frame's rows,
+ * the tensor the reference normalises) + the block's activation:
+ *   out[r][c] = [residual[r][c] +] act(std_param * (z[r][c] - mean_{s,g}) / (std_{s,g} + 1e-5)
+ *               + mu_param),
+ * mean / unbiased std over the segment's rows x group g's C/G features.  seg_ptr: device
+ * int32 [n_seg+1]; z and out float32 [rows][C] (may alias); residual optional (the conv
+ * block's identity, gnn_blocks.py:109).  Deterministic. */
+size_t rg_frame_norm_workspace_size(int n_seg, int groups);
+int rg_frame_norm(const float* z, int ldz, int C, int groups, const int* seg_ptr, int n_seg,
+                  const float* norm_mu, const float* norm_std, int act, const float* residual,
+                  int ld_res, float* out, int ld_out, void* workspace, size_t workspace_bytes,
+                  void* stream);
+/* out[t] = table[idx[t]] (device int32; per-frame edge offsets = seg_ptr[frame_ptr]) */
+int rg_gather_i32(const int* table, const int* idx, int n, int* out, void* stream);
+/* out[t] = first position p in sorted[0..n) with sorted[p] >= queries[t] (n from
+ * n_sorted_dev when non-NULL, capped at n_sorted): per-frame offsets of rows sorted by
+ * node (link pairs by source, clusters by first member) */
+int rg_lower_bound_i32(const int* sorted, const int* n_sorted_dev, long n_sorted,
+                       const int* queries, int n_queries, int* out, void* stream);
 
 /* ----------------------------------------------------- segment reductions */
 

@@ -388,6 +388,73 @@ def make_training_fixtures():
     print('training', {k: v for k, v in data.items() if k.startswith('s')})
 
 
+def make_norm_fixtures():
+    """layer_normalization / group_normalization (common.py:223-253; normalization is a
+    yml choice, configuration_radarscenes_gnn.yml:51-52): the reference's Model_Inference
+    forward frame by frame (its statistics run over a whole frame's rows: nodes, edges,
+    pairs or clusters) and one Model_Training step (loss.backward()) on a 2-frame batch."""
+    from modules.set_configurations.set_config_gnn import config
+    from modules.neural_net.gnn.gnn_detector import Model_Training
+    for norm, groups in (('layer_normalization', None), ('group_normalization', 4)):
+        cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+        cfg.norm_layer = norm
+        cfg.num_groups = groups
+        cfg.graph_convolution_stem_channels = [64, 64]
+        sizes, seeds = (120, 90), (9101, 9102)
+        torch.manual_seed(31)
+        model = Model_Training(cfg, 'cpu')
+        frames, graphs, labels = [], [], []
+        data = {}
+        for f, (n, sd_) in enumerate(zip(sizes, seeds)):
+            fr = synthetic.make_frame(n, sd_)
+            adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points)
+            lb = synthetic.make_labels(fr, adj['adj_list'], cfg.num_classes, sd_)
+            frames.append(fr)
+            graphs.append((adj, nf, ef))
+            labels.append(lb)
+            model.eval()
+            with torch.no_grad():
+                outs = model.pred(torch.from_numpy(nf).float(), torch.from_numpy(ef).float(),
+                                  torch.from_numpy(adj['adj_list']).long(),
+                                  torch.from_numpy(adj['adj_matrix']),
+                                  [torch.from_numpy(c) for c in lb['cluster_node_idx']])
+            for key, v in zip(('node_cls', 'node_reg', 'link_cls', 'obj_cls'), outs):
+                data[f'f{f}/{key}'] = v.numpy()
+            data[f'f{f}/node_features'] = nf.astype(np.float32)
+            data[f'f{f}/edge_features'] = ef.astype(np.float32)
+            data[f'f{f}/edge_index'] = adj['adj_list'].astype(np.int32)
+            data[f'f{f}/node_class'] = lb['node_class']
+            data[f'f{f}/node_offsets'] = lb['node_offsets']
+            data[f'f{f}/edge_class'] = lb['edge_class']
+            data[f'f{f}/cluster_ptr'] = np.cumsum([0] + [len(c) for c in lb['cluster_node_idx']]).astype(np.int64)
+            data[f'f{f}/cluster_idx'] = np.concatenate(lb['cluster_node_idx']).astype(np.int64)
+            data[f'f{f}/cluster_labels'] = lb['cluster_labels']
+        for k_, v in model.state_dict().items():
+            data['w/' + k_] = v.numpy()
+        lab = {'node_class': [torch.from_numpy(l['node_class']) for l in labels],
+               'node_offsets': [torch.from_numpy(l['node_offsets']) for l in labels],
+               'edge_class': [torch.from_numpy(l['edge_class']) for l in labels],
+               'cluster_node_idx': [[torch.from_numpy(c) for c in l['cluster_node_idx']] for l in labels],
+               'cluster_labels': [torch.from_numpy(l['cluster_labels']) for l in labels]}
+        model.train()
+        loss, acc = model(node_features=[torch.from_numpy(g[1]).float() for g in graphs],
+                          edge_features=[torch.from_numpy(g[2]).float() for g in graphs],
+                          edge_index=[torch.from_numpy(g[0]['adj_list']).long() for g in graphs],
+                          adj_matrix=[torch.from_numpy(g[0]['adj_matrix']) for g in graphs],
+                          labels=lab)
+        total = loss['loss_node_cls'] + loss['loss_node_reg'] + loss['loss_edge_cls'] + loss['loss_obj_cls']
+        total.backward()
+        for k_, v in loss.items():
+            data[f's1/{k_}'] = np.float64(v.item())
+        for name, p_ in model.named_parameters():
+            data['g1/' + name] = p_.grad.detach().numpy().copy()
+        data.update(n_frames=len(sizes), norm_layer=norm, num_groups=-1 if groups is None else groups,
+                    L=2)
+        tag = 'layer' if norm == 'layer_normalization' else 'group'
+        np.savez_compressed(os.path.join(HERE, f'norm_{tag}_2frames.npz'), **data)
+        print('norm', norm, {k: v for k, v in data.items() if k.startswith('s1')})
+
+
 def make_classifier_fixtures():
     """Cluster-level classifier GNN (modules/neural_net/classifier):
     the reference's own Model_Training(cfg) -- pred forward per sample and the loss over
@@ -457,11 +524,15 @@ def main():
     if '--training-only' in sys.argv:
         make_training_fixtures()
         return
+    if '--norm-only' in sys.argv:
+        make_norm_fixtures()
+        return
     if '--proposals-only' not in sys.argv:
         make_graph_fixtures()
         make_model_fixtures()
     make_proposal_fixtures()
     make_training_fixtures()
+    make_norm_fixtures()
     make_classifier_fixtures()
 
 

@@ -8,8 +8,8 @@ edge_index bit-exact):
                                                          depends on numpy's float32 arctan2
                                                          (SIMD/libm-specific): <= 4e-7 abs
   * fp32 forward outputs                               : |d| <= 1e-4 + 1e-4 |ref|
-  * bf16 forward outputs (BASELINE config 2 dtype)     : every |d| <= 0.5 + 0.1 |ref|, 99.9 % of
-                                                         elements |d| <= 0.1 + 0.05 |ref|, >= 97 %
+  * bf16 forward outputs (BASELINE config 2 dtype)     : |d_k| <= 8 u max(rms(ref_k), ||w_k||_1), u = 2^-8
+                                                         per output k (bf16_bound), >= 99.5 %
                                                          argmax agreement of class logits
 """
 import numpy as np
@@ -65,10 +65,19 @@ def test_graph_build_bit_exact(cuda_device, name):
     oracle = gref.compute_adjacency_information(fr, float(d['eps']), int(d['k']))
     np.testing.assert_array_equal(adj['adj_matrix'], oracle['adj_matrix'])
     np.testing.assert_array_equal(adj['distance_mat'], oracle['distance_mat'])
+    # float64 results like the reference's np.stack (graph_features.py:144,164)
     ef = gf.compute_edge_features(fr, adj['adj_list'])
-    np.testing.assert_array_equal(ef, d['edge_features'])
+    assert ef.dtype == np.float64
+    np.testing.assert_array_equal(ef, gref.compute_edge_features(fr, d['adj_list']))
+    np.testing.assert_array_equal(ef.astype(np.float32), d['edge_features'])
     nf = gf.compute_node_features(fr, adj['degree'], True, 0, GRID_MAX_R, 0, np.pi * 0.5)
+    assert nf.dtype == np.float64 and nf.shape[1] == 6
+    np.testing.assert_array_equal(nf[:, :5], d['node_features_f64'][:, :5])
+    np.testing.assert_allclose(nf[:, 5], d['node_features_f64'][:, 5], rtol=0, atol=4e-7)
     assert _node_features_close(nf, d['node_features'])
+    nf4 = gf.compute_node_features(fr, adj['degree'])
+    assert nf4.shape[1] == 4 and nf4.dtype == np.float64
+    np.testing.assert_array_equal(nf4, d['node_features_f64'][:, :4])
 
 
 def test_radius_graph_bit_exact(cuda_device):
@@ -259,8 +268,48 @@ def test_forward_fp32_matches_reference(cuda_device, name):
         assert any(plans.edge_enc.fast_ok.values()), name
 
 
+BF16_U = 2.0 ** -8   # bf16 unit roundoff (8 significant bits, round to nearest)
+HEAD_LAST = {'node_cls': 'predict_node.pred_cls.head.1.weight',
+             'node_reg': 'predict_offset.pred_offsets.head.1.weight',
+             'link_cls': 'predict_link.pred_cls.head.1.weight',
+             'obj_cls': 'predict_class.pred_cls.head.1.weight'}
+
+
+def bf16_bound(key, ref, pred):
+    """Per-output error bound of the bf16 path against the fp32 reference.
+
+    Every output is a final Linear w_k . h + b_k of channel-normalised activations h,
+    and the bf16 path perturbs h (and the packed weights) by a few units of bf16
+    roundoff relative to their own scale.  So the error of output k is bounded by
+    c * u * S_k, u = 2^-8 and S_k = max(rms(ref_k), ||w_k||_1): ||w_k||_1 is the largest
+    output an activation of magnitude <= 1 can produce (it floors the scale of outputs
+    that are small by cancellation, e.g. the 0.01-scale offsets of node_reg), rms(ref_k)
+    the scale of outputs that are large (logits ~5).  c = 8 (|d| <= 3.1 % of S_k): the
+    worst measured is 1.1 % (trained checkpoint, N = 500: the trained gains amplify the
+    rounding of the 7 bf16 node-state round trips), 0.06 % with the seeded random weights
+    at BASELINE config 2's full size (scripts/bf16_error.py)."""
+    mod = dict(pred.named_parameters())
+    w = mod[HEAD_LAST[key]].detach().float().cpu().numpy()
+    l1 = np.abs(w).sum(1)                         # [n_out]
+    rms = np.sqrt(np.mean(np.asarray(ref, np.float64) ** 2, axis=0))
+    return 8.0 * BF16_U * np.maximum(rms, l1)
+
+
+def assert_bf16_close(pred, key, got, ref):
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    bound = bf16_bound(key, ref, pred)
+    err = np.abs(got - ref)
+    worst = float((err / bound).max()) if err.size else 0.0
+    assert worst <= 1.0, (key, worst, float(err.max()))
+    if key != 'node_reg' and len(ref):
+        agree = float((got.argmax(-1) == ref.argmax(-1)).mean())
+        assert agree >= 0.995, (key, agree)
+
+
 @pytest.mark.parametrize('name', ['model_trained_N500', 'model_random_L6_N300_k32'])
 def test_forward_bf16_close_to_reference(cuda_device, name):
+    """bf16 forward vs the reference's fp32 golden outputs, within bf16_bound."""
     d = golden(name)
     pred, cfg = _model(name, cuda_device, 'bf16')
     dev = cuda_device
@@ -270,14 +319,52 @@ def test_forward_bf16_close_to_reference(cuda_device, name):
                    torch.from_numpy(d['edge_features']).to(dev), ei, None,
                    [c.to(dev) for c in cluster_lists(d)])
     for got, key in zip(out, ('node_cls', 'node_reg', 'link_cls', 'obj_cls')):
-        g = got.cpu().numpy()
-        ref = d[key]
-        err = np.abs(g - ref)
-        assert np.all(err <= 0.5 + 0.1 * np.abs(ref)), (key, err.max())
-        assert np.mean(err <= 0.1 + 0.05 * np.abs(ref)) >= 0.999, key
-        if key in ('node_cls', 'link_cls', 'obj_cls'):
-            agree = (g.argmax(-1) == ref.argmax(-1)).mean()
-            assert agree >= 0.97, (key, agree)
+        assert_bf16_close(pred, key, got.cpu().numpy(), d[key])
+
+
+def test_c2_full_size_bf16_within_bound(cuda_device):
+    """BASELINE config 2 at its full size -- 64 frames x 3000 nodes, k = 32, L = 6, the
+    bench's seeded random-init weights, the bench's own pipeline -- spot frames' four
+    outputs against the fp32 oracle within bf16_bound (the fused bf16 conv, the
+    register-resident bf16 chains and the graph build all in the loop)."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+    dev = cuda_device
+    B, N, K, L = 64, 3000, 32, 6
+    cfg = default_config(graph_convolution_stem_channels=[64] * L, k_number_nearest_points=K)
+    torch.manual_seed(1234)
+    m = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    pred = m.to(dev).pred.eval().requires_grad_(False)
+    frames = [synthetic.make_frame(N, synthetic.SEED0 + f) for f in range(B)]
+    clusters = [synthetic.cluster_lists(N) for _ in range(B)]
+    batch = FrameBatch.from_frames(frames, clusters, device=dev)
+    pipe = RadarGNNPipeline(pred, cfg, 'bf16')
+    with torch.no_grad():
+        gb, out = pipe.step(batch)
+    torch.cuda.synchronize()
+    assert all(cv.fused_ok for cv in pipe.plans.convs), 'fused bf16 conv not used'
+    U = int(gb.graph.n_pairs_dev.item())
+    ps = gb.graph.pair_src[:U].cpu().numpy()
+    link = out.link_cls[:U].cpu().numpy()
+    for f in (0, 21, 63):
+        g = gref.build_frame_graph(frames[f], 25.0, K, GRID_MAX_R)
+        with torch.no_grad():
+            ref = gnn_forward_ref.forward(sd, cfg, torch.from_numpy(g['node_features']),
+                                          torch.from_numpy(g['edge_features']),
+                                          torch.from_numpy(g['edge_index']), None,
+                                          [torch.from_numpy(c) for c in clusters[f]])
+        sl = slice(f * N, (f + 1) * N)
+        sel = (ps >= f * N) & (ps < (f + 1) * N)
+        ncl = len(clusters[f])
+        got = (out.node_cls[sl].cpu().numpy(), out.node_reg[sl].cpu().numpy(), link[sel],
+               out.obj_cls[f * ncl:(f + 1) * ncl].cpu().numpy())
+        for key, gt, rf in zip(('node_cls', 'node_reg', 'link_cls', 'obj_cls'), got, ref):
+            assert gt.shape == tuple(rf.shape), key
+            assert_bf16_close(pred, key, gt, rf.numpy())
 
 
 def test_conv_block_dropin(cuda_device):
