@@ -122,6 +122,9 @@ _SIGNATURES = {
                                         _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     'rg_conv_blocks_workspace_size': (_S, [_I]),
     'rg_conv_blocks': (_I, [_P, _I, _P, _P, _P, _S, _P]),
+    'rg_cluster_majority_label': (_I, [_P, _P, _P, _I, _I, _P, _P, _P]),
+    'rg_cross_entropy': (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
+    'rg_cross_entropy_backward': (_I, [_P, _I, _P, _I, _I, _P, _P, _I, _P]),
     'rg_frame_norm_workspace_size': (_S, [_I, _I]),
     'rg_frame_norm': (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
     'rg_gather_i32': (_I, [_P, _P, _I, _P, _P]),

@@ -245,6 +245,8 @@ class Model_Training(nn.Module):
     def __init__(self, net_config, device):
         super().__init__()
         self.pred = Model_Inference(net_config)
+        from .loss import Loss_Graph
+        self.loss = Loss_Graph(net_config, device)   # gnn_detector.py:423 (no parameters)
         self.device = device
         self.offset_mu = net_config.offset_mu
         self.offset_sigma = net_config.offset_sigma
@@ -346,3 +348,81 @@ def native_loss_graph(cfg, pred, lab):
     nat.check(lib.rg_loss_graph(ctypes.byref(a), losses.data_ptr(), acc.data_ptr(), ws.data_ptr(),
                                 ws.numel(), nat.stream_ptr(dev)), 'rg_loss_graph')
     return losses, acc
+
+
+class Model_Object_Classifier_Finetuning(nn.Module):
+    """gnn_detector.py:481-519: the detector with proposal extraction; the object head's
+    loss (Loss_Object_Class) on the proposals, whose ground truth is the majority node
+    class of each proposal (argmax(bincount(...)), gnn_detector.py:511-513).
+
+    The frames of a call run as one batch: the proposal forward (no grad) yields the
+    clusters; with gradients enabled the native training engine then runs the forward
+    tape over those clusters and the backward of the object loss alone (the other three
+    losses are weighted 0), so ``loss.backward()`` fills .grad of every parameter that
+    requires it -- after ``pred.freeze_layers_except_object_class_predictor()``
+    (set_param_for_finetuning_obj_classifier.py:34) only predict_class's."""
+
+    def __init__(self, net_config):
+        super().__init__()
+        self.pred = Model_Inference(net_config, extract_proposals=True,
+                                    eps=net_config.clustering_eps)
+        from .loss import Loss_Object_Class
+        self.loss = Loss_Object_Class(net_config)
+        self.net_config = net_config
+        self._train_engine = None
+
+    def train_engine(self):
+        from .training import TrainEngine
+        dev = next(self.parameters()).device
+        if self._train_engine is None or self._train_engine.device != dev:
+            self._train_engine = TrainEngine(self, dev)
+        return self._train_engine
+
+    def forward(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
+                other_features: List[torch.Tensor], edge_index: List[torch.Tensor],
+                adj_matrix: List[torch.Tensor], node_class_labels: List[torch.Tensor]):
+        from . import _native as nat
+        from .loss import cross_entropy_with_accuracy
+        dev = node_features[0].device
+        engine._require_device(node_features[0], 'node_features')
+        with torch.no_grad():
+            was = self.pred.training
+            self.pred.eval()
+            outs = self.pred.forward_frames(node_features, edge_features, edge_index, None,
+                                            other_features)
+            self.pred.train(was)
+        obj_pred, lists = outs[3], outs[4]
+        # proposals as one CSR over the batch (global node ids, frame order)
+        nf, ef, ei, cptr, cidx, ncl, sizes = _batch_frames(node_features, edge_features,
+                                                           edge_index, lists)
+        labels = torch.cat([t.to(dev, torch.int64).reshape(-1) for t in node_class_labels], 0)
+        gt = torch.empty(max(ncl, 1), dtype=torch.int64, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = nat.lib()
+        nat.check(lib.rg_cluster_majority_label(labels.contiguous().data_ptr(), cptr.data_ptr(),
+                                                cidx.data_ptr(), ncl, self.net_config.num_classes,
+                                                gt.data_ptr(), bad.data_ptr(),
+                                                nat.stream_ptr(dev)), 'rg_cluster_majority_label')
+        if int(bad.item()):
+            raise RuntimeError('node_class_labels outside [0, num_classes)')
+        gt = gt[:ncl]
+        if ncl == 0:
+            raise RuntimeError('no proposals in the batch (the reference stacks an empty list)')
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from .training import train_step_losses
+            N = nf.shape[0]
+            g = engine.DeviceGraph.from_edge_index(ei, N)
+            e_dst = _edges_dst_major(ef, g)
+            lab = {'node_class': torch.zeros(N, dtype=torch.int64, device=dev),
+                   'node_offsets': torch.zeros((N, 2), dtype=torch.float32, device=dev),
+                   'edge_class': torch.zeros(max(g.n_pairs, 1), dtype=torch.int64, device=dev),
+                   'cluster_labels': gt.contiguous(),
+                   'class_weights': torch.ones(self.net_config.num_classes, dtype=torch.float32,
+                                               device=dev),
+                   'loss_weights': (0.0, 0.0, 0.0, 1.0)}
+            eng = self.train_engine()
+            losses = train_step_losses(eng, (nf, e_dst, g, cptr, cidx, ncl, lab))
+            return losses[3], eng.last_acc[2]
+        loss, acc = cross_entropy_with_accuracy(obj_pred, gt)
+        return loss, acc
+

@@ -369,10 +369,10 @@ class TrainEngine:
         a.n_classes = outs[0].shape[1]
         a.mu_x, a.mu_y = float(cfg.offset_mu[0]), float(cfg.offset_mu[1])
         a.sigma_x, a.sigma_y = float(cfg.offset_sigma[0]), float(cfg.offset_sigma[1])
-        a.w_node_cls = float(cfg.node_cls_loss_weight)
-        a.w_node_reg = float(cfg.node_reg_loss_weight)
-        a.w_edge_cls = float(cfg.edge_cls_loss_weight)
-        a.w_obj_cls = float(cfg.obj_cls_loss_weight)
+        w = labels.get('loss_weights') or (cfg.node_cls_loss_weight, cfg.node_reg_loss_weight,
+                                           cfg.edge_cls_loss_weight, cfg.obj_cls_loss_weight)
+        # (finetuning passes (0, 0, 0, 1): Loss_Object_Class alone, loss.py:79-89)
+        a.w_node_cls, a.w_node_reg, a.w_edge_cls, a.w_obj_cls = (float(v) for v in w)
         return a
 
     # ------------------------------------------------------------------ backward

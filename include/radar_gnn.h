@@ -324,6 +324,22 @@ size_t rg_conv_blocks_workspace_size(int n_nodes);
 int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------- object-classifier finetuning */
+
+/* gnn_detector.py:511-513: out[c] = argmax(bincount(node_labels[members of c])) (first
+ * maximum) for the proposal clusters (cluster_ptr int32 [n+1], cluster_idx int32);
+ * *bad_label (device int32, caller-zeroed) is set when a label is outside [0, n_classes). */
+int rg_cluster_majority_label(const int64_t* node_labels, const int* cluster_ptr,
+                              const int* cluster_idx, int n_clusters, int n_classes,
+                              int64_t* out, int* bad_label, void* stream);
+/* Loss_Object_Class (loss.py:79-89): sum_r CE(logits_r, one_hot(label_r)) / n, and
+ * compute_accuracy (gnn_detector.py:24-28); loss, accuracy: device float32 [1] */
+int rg_cross_entropy(const float* logits, int ld, const int64_t* labels, int n, int nc,
+                     float* loss, float* accuracy, void* stream);
+/* its gradient: d_logits = g (softmax - one_hot) / n, g a device float32 scalar */
+int rg_cross_entropy_backward(const float* logits, int ld, const int64_t* labels, int n, int nc,
+                              const float* g, float* d_logits, int ld_d, void* stream);
+
 /* ------------------------------------------- frame-wide normalisations */
 
 /* layer_normalization (groups = 1) / group_normalization (groups = G) of

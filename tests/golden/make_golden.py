@@ -455,6 +455,59 @@ def make_norm_fixtures():
         print('norm', norm, {k: v for k, v in data.items() if k.startswith('s1')})
 
 
+def make_finetune_fixtures():
+    """Model_Object_Classifier_Finetuning (gnn_detector.py:481-519) with the trained
+    checkpoint, frozen except predict_class (set_param_for_finetuning_obj_classifier.py:31-34):
+    loss, accuracy and the predict_class gradients of one step on 2 frames (proposals from
+    the predicted offsets, majority-vote object labels), then the same in eval mode under
+    no_grad (the validation call of finetuning.py:85-96)."""
+    from modules.set_configurations.set_config_gnn import config
+    from modules.neural_net.gnn.gnn_detector import Model_Object_Classifier_Finetuning
+    cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+    torch.manual_seed(5)
+    model = Model_Object_Classifier_Finetuning(cfg)
+    sd = torch.load(CKPT, map_location='cpu', weights_only=True)
+    model.load_state_dict(sd)
+    model.pred.freeze_layers_except_object_class_predictor()
+    sizes, seeds = (300, 260), (9301, 9302)
+    data = {}
+    args = {k: [] for k in ('node_features', 'edge_features', 'other_features', 'edge_index',
+                            'adj_matrix', 'node_class_labels')}
+    for f, (n, sd_) in enumerate(zip(sizes, seeds)):
+        fr = synthetic.make_frame(n, sd_)
+        adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points)
+        lb = synthetic.make_labels(fr, adj['adj_list'], cfg.num_classes, sd_)
+        other = np.stack([fr['meas_px'], fr['meas_py'], fr['meas_vx'], fr['meas_vy']], -1).astype(np.float32)
+        args['node_features'].append(torch.from_numpy(nf).float())
+        args['edge_features'].append(torch.from_numpy(ef).float())
+        args['other_features'].append(torch.from_numpy(other))
+        args['edge_index'].append(torch.from_numpy(adj['adj_list']).long())
+        args['adj_matrix'].append(torch.from_numpy(adj['adj_matrix']))
+        args['node_class_labels'].append(torch.from_numpy(lb['node_class']))
+        data[f'f{f}/node_features'] = nf.astype(np.float32)
+        data[f'f{f}/edge_features'] = ef.astype(np.float32)
+        data[f'f{f}/edge_index'] = adj['adj_list'].astype(np.int32)
+        data[f'f{f}/other_features'] = other
+        data[f'f{f}/node_class'] = lb['node_class']
+    model.train()
+    loss, acc = model(**args)
+    loss.backward()
+    data['loss'] = np.float64(loss.item())
+    data['accuracy'] = np.float64(float(acc))
+    for name, p_ in model.named_parameters():
+        if p_.requires_grad:
+            data['g/' + name] = p_.grad.detach().numpy().copy()
+    model.eval()
+    with torch.no_grad():
+        loss_e, acc_e = model(**args)
+    data['eval_loss'] = np.float64(loss_e.item())
+    data['eval_accuracy'] = np.float64(float(acc_e))
+    data.update(n_frames=len(sizes))
+    np.savez_compressed(os.path.join(HERE, 'finetune_trained_2frames.npz'), **data)
+    print('finetune', data['loss'], data['accuracy'], data['eval_loss'],
+          sorted(k for k in data if k.startswith('g/')))
+
+
 def make_classifier_fixtures():
     """Cluster-level classifier GNN (modules/neural_net/classifier):
     the reference's own Model_Training(cfg) -- pred forward per sample and the loss over
@@ -527,12 +580,16 @@ def main():
     if '--norm-only' in sys.argv:
         make_norm_fixtures()
         return
+    if '--finetune-only' in sys.argv:
+        make_finetune_fixtures()
+        return
     if '--proposals-only' not in sys.argv:
         make_graph_fixtures()
         make_model_fixtures()
     make_proposal_fixtures()
     make_training_fixtures()
     make_norm_fixtures()
+    make_finetune_fixtures()
     make_classifier_fixtures()
 
 
