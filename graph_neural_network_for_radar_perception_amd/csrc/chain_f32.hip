@@ -153,8 +153,49 @@ constexpr bool spec_norm(int sp, int l) { return ((sp >> (8 + l)) & 1) != 0; }
 constexpr bool spec_act(int sp, int l) { return ((sp >> (16 + l)) & 1) != 0; }
 constexpr bool spec_glob(int sp, int l) { return ((sp >> (24 + l)) & 1) != 0; }
 
+// channel_normalization + LeakyReLU in five ops per feature: sum, x - mean, sum of
+// squares, y' = x a + b with the 0.505 of leaky(y) = 0.505 y + 0.495 |y| folded into a and
+// b, then |y'| C + y' (C = 0.495 / 0.505; a free |.| source modifier)
+template <int MT>
+__device__ __forceinline__ void channel_norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
+  constexpr int N = 32 * MT;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += acc[m][q];
+      s1 += acc[m][q + 1];
+    }
+  const float mean = add_xor32(s0 + s1) * (1.f / N);
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      acc[m][q] -= mean;
+      acc[m][q + 1] -= mean;
+      q0 = fmaf(acc[m][q], acc[m][q], q0);
+      q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
+    }
+  const float ss = add_xor32(q0 + q1);
+  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + NORM_EPS);
+  const float ga = LEAKY_PRE * (sd * inv), gb = LEAKY_PRE * mu;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float y = fmaf(acc[m][q], ga, gb);
+      acc[m][q] = fmaf(fabsf(y), LEAKY_C, y);
+    }
+}
+
 template <int SPEC, int LI, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const float* nrm) {
+  if constexpr (spec_norm(SPEC, LI) && spec_act(SPEC, LI) && (SPEC & 0xff) == ACT_LEAKY) {
+    channel_norm_leaky<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1]);
+    return;
+  }
   if constexpr (spec_norm(SPEC, LI)) channel_norm<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1]);
   if constexpr (spec_act(SPEC, LI)) act_all<(SPEC & 0xff), MT>(acc);
 }

@@ -28,6 +28,8 @@
 // x, P and Q rows are gathered from one L2.
 #include "rg_common.h"
 
+#include <stdlib.h>
+
 namespace rg {
 namespace convf32 {
 
@@ -333,6 +335,306 @@ __global__ __launch_bounds__(FT) void conv_f32_kernel(Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Two waves per SIMD (512-thread workgroups, <= 256 registers per wave): the second wave
+// of a SIMD issues its MFMAs while the first runs its epilogues or waits for its rows, so
+// the matrix pipe is fed without hand-interleaving.  LDS: W_e and W_2 (66 KiB) stay
+// resident; W_u (once per block) is read from L2; per wave an 8-edge message tile and
+// the block's 32 aggregate rows.  The channel_normalization + LeakyReLU epilogue is five
+// VALU ops per feature: sum, x - mean, sum of squares, y' = x a + b with the 0.505 of
+// leaky(y) = 0.505 y + 0.495 |y| folded into a and b, then |y'| C + y' (C = 0.495 / 0.505).
+#ifndef RG_CF32_PQLATE
+#define RG_CF32_PQLATE 0
+#endif
+#ifndef RG_CF32_PRIO
+#define RG_CF32_PRIO 0
+#endif
+#ifndef RG_CF32_EXP
+#define RG_CF32_EXP 0  // timing experiments only (wrong results): 1 no norm/act epilogues,
+                       // 2 no segmented sum, 3 no P/Q gathers, 4 = 1 + 2 + 3
+#endif
+static constexpr int FT2 = 512;
+static constexpr int NW2 = FT2 / 64;
+static constexpr int TR2 = 8;   // message rows per LDS pass
+static constexpr int W2_BYTES = W_U_OFF;  // W_e + W_2 staged; W_u streamed
+static constexpr int WAVE_LDS2 = (TR2 * TS + NBLK * AS) * 4;
+static constexpr int LDS_BYTES2 = W2_BYTES + NW2 * WAVE_LDS2;
+static_assert(LDS_BYTES2 <= DYN_LDS_MAX, "conv_f32 (2 waves / SIMD) LDS");
+static constexpr float LEAKY_PRE2 = 0.505f;
+static constexpr float LEAKY_C2 = 0.495f / 0.505f;
+
+// channel_normalization + LeakyReLU (common.py:208-220, 256-267), five ops per feature
+template <int MT>
+__device__ __forceinline__ void norm_leaky5(f32x16 (&acc)[MT], float mu, float sd) {
+  constexpr int N = 32 * MT;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += acc[m][q];
+      s1 += acc[m][q + 1];
+    }
+  const float mean = add_xor32(s0 + s1) * (1.f / N);
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      acc[m][q] -= mean;
+      acc[m][q + 1] -= mean;
+      q0 = fmaf(acc[m][q], acc[m][q], q0);
+      q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
+    }
+  const float ss = add_xor32(q0 + q1);
+  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + NORM_EPS);
+  const float ga = LEAKY_PRE2 * (sd * inv), gb = LEAKY_PRE2 * mu;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float y = fmaf(acc[m][q], ga, gb);
+      acc[m][q] = fmaf(fabsf(y), LEAKY_C2, y);
+    }
+}
+
+// layer with A fragments from global memory (L2), prefetched two k-quads ahead
+template <int S4, int MT, typename BOp>
+__device__ __forceinline__ void layer_g(f32x16 (&acc)[MT], const char* w, int lane, BOp&& bop) {
+  const f32x4* wa = (const f32x4*)w + lane;
+  constexpr int PD = 2, NB = PD + 1;
+  f32x4 a[NB][MT];
+#pragma unroll
+  for (int s = 0; s < PD; ++s)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) a[s][m] = wa[(m * S4 + s) * 64];
+#pragma unroll
+  for (int s4 = 0; s4 < S4; ++s4) {
+    if (s4 + PD < S4) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) a[(s4 + PD) % NB][m] = wa[(m * S4 + s4 + PD) * 64];
+    }
+    const f32x4 b = bop(s4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma(a[s4 % NB][m][u], b[u], acc[m]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[6];
+  if (threadIdx.x < 3) {
+    nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
+    nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
+  }
+  {
+    const int nb[2] = {fbytes(C, HID), fbytes(HID, C)};
+    const int off[2] = {W_E_OFF, W_2_OFF};
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const f32x4* s = (const f32x4*)a.w[l];
+      f32x4* d = (f32x4*)(lds + off[l]);
+      for (int i = threadIdx.x; i < nb[l] / 16; i += FT2) d[i] = s[i];
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+#if RG_CF32_PRIO
+  // the second wave of each SIMD (waves 4-7) yields the issue port: the pair drifts out
+  // of lock-step, so one wave's epilogue runs under the other's MFMAs
+  if (wave >= NW2 / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+  float* T = (float*)(lds + W2_BYTES + wave * WAVE_LDS2);  // [TR2][TS] message rows
+  float* Agg = T + TR2 * TS;                              // [NBLK][AS] aggregates
+  const char* wE = lds + W_E_OFF;
+  const char* w2 = lds + W_2_OFF;
+  const char* wU = (const char*)a.w[2];
+  const float* bias2 = (const float*)(w2 + 2 * 16 * 1024);
+  const float* biasU = (const float*)(wU + 2 * 16 * 1024);
+  const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3], muU = nrm[4], sdU = nrm[5];
+
+  const int xcd = blockIdx.x % NXCD;
+  const int blo = (int)((long)a.n_blocks * xcd / NXCD);
+  const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  int* ctr = a.counters + xcd;
+
+  for (;;) {
+    int bi = 0;
+    if (lane == 0) bi = atomicAdd(ctr, 1);
+    const int blk = blo + __shfl(bi, 0, 64);
+    if (blk >= bhi) break;
+    const int n0 = blk * NBLK;
+    const int n1 = min(n0 + NBLK, a.n_nodes);
+    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = lane + 64 * i;
+      *(f32x4*)(Agg + (idx >> 4) * AS + 4 * (idx & 15)) = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    float run = 0.f;
+    int cur = -1;
+    int pn = min(e0 + r, e1 - 1);
+    int dn = e0 < e1 ? a.dst[pn] : 0, sn = e0 < e1 ? a.src[pn] : 0;
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+      const int p = pn, d = dn, sj = sn;
+      // the next tile's indices now (their latency hides behind this tile)
+      pn = min(t0 + 32 + r, e1 - 1);
+      dn = a.dst[pn];
+      sn = a.src[pn];
+      // ---- layer 1: h = P[dst] + Q[src] + W_e e
+      f32x16 acc1[4];
+#if RG_CF32_PQLATE
+      // the MFMAs need only the e rows: P and Q arrive while they run and are added after
+      {
+        const float* pe = a.e + (size_t)p * a.lde + 4 * h;
+        const float* pp = a.pq + (size_t)d * a.ldpq + 4 * h;
+        const float* pq = a.pq + (size_t)sj * a.ldpq + HID + 4 * h;
+        f32x4 eb[8], pv[16], qv[16];
+#pragma unroll
+        for (int s4 = 0; s4 < 8; ++s4) eb[s4] = *(const f32x4*)(pe + 8 * s4);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          pv[i] = *(const f32x4*)(pp + 8 * i);
+          qv[i] = *(const f32x4*)(pq + 8 * i);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc1[m] = (f32x16){0.f};
+        layer<8, 4>(acc1, wE, lane, [&](int s4) { return eb[s4]; });
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              acc1[m][4 * g + t] += pv[4 * m + g][t] + qv[4 * m + g][t];
+      }
+#else
+      {
+        const float* pp = a.pq + (size_t)d * a.ldpq + 4 * h;
+        const float* pq = a.pq + (size_t)sj * a.ldpq + HID + 4 * h;
+        f32x4 pv[16], qv[16];
+        if (RG_CF32_EXP == 3 || RG_CF32_EXP == 4) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) pv[i] = qv[i] = (f32x4){1.f, 2.f, 3.f, (float)d};
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            pv[i] = *(const f32x4*)(pp + 8 * i);
+            qv[i] = *(const f32x4*)(pq + 8 * i);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc1[m][4 * g + t] = pv[4 * m + g][t] + qv[4 * m + g][t];
+      }
+      {
+        const float* pe = a.e + (size_t)p * a.lde + 4 * h;
+        f32x4 eb[8];
+#pragma unroll
+        for (int s4 = 0; s4 < 8; ++s4) eb[s4] = *(const f32x4*)(pe + 8 * s4);
+        layer<8, 4>(acc1, wE, lane, [&](int s4) { return eb[s4]; });
+      }
+#endif
+      if (RG_CF32_EXP != 1 && RG_CF32_EXP != 4) norm_leaky5<4>(acc1, mu0, sd0);
+      // ---- layer 2
+      f32x16 acc2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
+      layer<16, 2>(acc2, w2, lane, [&](int s4) {
+        const f32x16& q = acc1[s4 >> 2];
+        const int o = 4 * (s4 & 3);
+        return (f32x4){q[o], q[o + 1], q[o + 2], q[o + 3]};
+      });
+      if (RG_CF32_EXP != 1 && RG_CF32_EXP != 4) norm_leaky5<2>(acc2, mu1, sd1);
+      if (RG_CF32_EXP == 2 || RG_CF32_EXP == 4) {
+        // keep the messages live: fold them into the running sum without the LDS pass
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) run += acc2[m][q];
+        continue;
+      }
+      // ---- segmented sum in edge order, 8 edges per LDS pass
+#pragma unroll
+      for (int c = 0; c < 32 / TR2; ++c) {
+        if (t0 + TR2 * c >= e1) break;  // wave-uniform
+        if (r / TR2 == c) {
+          float* row = T + (r % TR2) * TS + 4 * h;
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){acc2[m][4 * g], acc2[m][4 * g + 1],
+                                                        acc2[m][4 * g + 2], acc2[m][4 * g + 3]};
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < TR2; ++j) {
+          const int eo = TR2 * c + j;
+          if (t0 + eo < e1) {
+            const float v = T[j * TS + lane];
+            const int slot = __builtin_amdgcn_readlane(d, eo) - n0;
+            run = slot == cur ? run + v : v;
+            Agg[slot * AS + lane] = run;
+            cur = slot;
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (RG_CF32_EXP == 2 || RG_CF32_EXP == 4) Agg[lane] = run;  // keep the messages live
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
+    const int node = n0 + r;
+    const bool nvalid = node < n1;
+    const float* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 4 * h;
+    f32x4 xb[8], ab[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) xb[s] = *(const f32x4*)(px + 8 * s);
+    float cnt = 1.f;
+    if (a.aggr_mean) {  // PyG mean: sum / max(count, 1)
+      const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
+      cnt = (float)(deg > 0 ? deg : 1);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      f32x4 v = *(const f32x4*)(Agg + r * AS + 8 * s + 4 * h);
+      if (a.aggr_mean) v = (f32x4){div_rn(v.x, cnt), div_rn(v.y, cnt), div_rn(v.z, cnt), div_rn(v.w, cnt)};
+      ab[s] = v;
+    }
+    f32x16 accu[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
+    layer_g<16, 2>(accu, wU, lane, [&](int s4) { return s4 < 8 ? xb[s4] : ab[s4 - 8]; });
+    norm_leaky5<2>(accu, muU, sdU);
+    if (nvalid) {
+      float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 xr = xb[4 * m + g];
+          *(f32x4*)(po + 32 * m + 8 * g) =
+              (f32x4){__fadd_rn(xr.x, accu[m][4 * g]), __fadd_rn(xr.y, accu[m][4 * g + 1]),
+                      __fadd_rn(xr.z, accu[m][4 * g + 2]), __fadd_rn(xr.w, accu[m][4 * g + 3])};
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace convf32
 }  // namespace rg
 
@@ -400,13 +702,21 @@ extern "C" int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* 
   a.n_nodes = n_nodes;
   a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
-  RG_ENSURE_LDS(conv_f32_kernel, DYN_LDS_MAX);
-  // one workgroup per CU (LDS); at least one per XCD counter
+  // one workgroup per CU (LDS); at least one per XCD counter.  RG_CONV_F32_WAVES=1 selects
+  // the one-wave-per-SIMD variant (timing comparison)
+  static const bool one_wave = getenv("RG_CONV_F32_WAVES") && atoi(getenv("RG_CONV_F32_WAVES")) == 1;
+  const int nw = one_wave ? NW : NW2;
   int blocks = 256;
-  const int need = (a.n_blocks + NW - 1) / NW;
+  const int need = (a.n_blocks + nw - 1) / nw;
   if (blocks > need) blocks = need;
   if (blocks < NXCD) blocks = NXCD;
-  conv_f32_kernel<<<blocks, FT, LDS_BYTES, st>>>(a);
+  if (one_wave) {
+    RG_ENSURE_LDS(conv_f32_kernel, DYN_LDS_MAX);
+    conv_f32_kernel<<<blocks, FT, LDS_BYTES, st>>>(a);
+  } else {
+    RG_ENSURE_LDS(conv_f32_kernel2, DYN_LDS_MAX);
+    conv_f32_kernel2<<<blocks, FT2, LDS_BYTES2, st>>>(a);
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
