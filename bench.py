@@ -714,17 +714,31 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         kern[name] = {'avg_ms': round(float(np.mean(ms)), 4), 'launches_per_step':
                       len(ms) // args.steps}
     peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
+    ref_tf = None
     if 'conv_fused' in durs:
-        # fused conv layer: gather x_i, x_j, e -> msg MLP -> segment sum -> update MLP
+        # fused conv layer: gather x_i, x_j, e -> msg MLP -> segment sum -> update MLP.
+        # Roofline flops = the dense work the kernel's algorithm needs:
+        #  fp32 (rg_conv_layer_f32): msg0 factorised, W_xi x_i + W_xj x_j once per NODE
+        #    (P | Q, 64 -> 256), per edge W_e e (64 -> 128) + msg1 (128 -> 64), per node the
+        #    update (128 -> 64): 32768 E + 49152 N
+        #  bf16 (rg_conv_layer_fused): per node P = W_xi x_i, per edge W_[xj,e] (128 -> 128)
+        #    + msg1, per node the update: 49152 E + 32768 N
+        # The reference form (SURVEY §8(d), msg0 over all 192 inputs per edge: 65536 E +
+        # 16384 N) is reported beside it as reference_form_tflops.
         ms = float(np.mean(durs['conv_fused']))
-        flops = 65536.0 * E + 16384.0 * N                   # per layer
+        ref_flops = 65536.0 * E + 16384.0 * N
+        flops = (32768.0 * E + 49152.0 * N) if args.dtype == 'fp32' else (49152.0 * E + 32768.0 * N)
         nbytes = E * (C * s + 8) + N * (2 * C * s + 4)     # e rows + (src,dst) once; x in/out once
         tf = flops / (ms * 1e-3) / 1e12
+        ref_tf = ref_flops / (ms * 1e-3) / 1e12
         gbs = nbytes / (ms * 1e-3) / 1e9
         kern['conv_fused'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
-                                  flops_per_launch=flops, bytes_per_launch=nbytes)
-        kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
-        traffic, tsrc = pmc_traffic(args, 'fused_conv')
+                                  flops_per_launch=flops, bytes_per_launch=nbytes,
+                                  reference_form_tflops=round(ref_tf, 2))
+        kname = ('conv_fused (rg_conv_layer_f32: per-node projection + fused layer launches, '
+                 'gnn_blocks.py:96-113)' if args.dtype == 'fp32' else
+                 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)')
+        traffic, tsrc = pmc_traffic(args, 'conv_f32' if args.dtype == 'fp32' else 'fused_conv')
     else:
         # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
         ms = float(np.mean(durs['message_chain']))
@@ -757,7 +771,10 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': traffic,
                 'mfma_frac': round(frac_mfma, 4)}
-    roof.update(avg_ms=round(ms, 4), timing='HIP events on the launch stream, timed region')
+    roof.update(avg_ms=round(ms, 4), timing='HIP events on the launch stream, timed region',
+                flops_per_launch=flops)
+    if ref_tf is not None:
+        roof['reference_form_tflops'] = round(ref_tf, 2)
     if traffic is not None:
         roof.update(traffic_unit='bytes/launch', traffic_source=tsrc,
                     algorithmic_bytes=nbytes, traffic_over_algorithmic=round(traffic / nbytes, 3))
