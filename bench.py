@@ -715,6 +715,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
                       len(ms) // args.steps}
     peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
     ref_tf = None
+    conv_exec, conv_peak = 1.0, MFMA_PEAK_TFLOPS[args.dtype]
     if 'conv_fused' in durs:
         # fused conv layer: gather x_i, x_j, e -> msg MLP -> segment sum -> update MLP.
         # Roofline flops = the dense work the kernel's algorithm needs:
@@ -725,9 +726,20 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         #    + msg1, per node the update: 49152 E + 32768 N
         # The reference form (SURVEY §8(d), msg0 over all 192 inputs per edge: 65536 E +
         # 16384 N) is reported beside it as reference_form_tflops.
+        #  fp32 x3 (rg_conv_layer_x3, the default): one launch = W_e e + msg1 per edge, the
+        #    update per node, and the NEXT layer's P | Q per node in L - 1 of the L launches
+        #    (the first layer's P | Q is its own launch, conv_proj): 32768 E + 16384 N +
+        #    32768 N (L - 1) / L on average
+        from graph_neural_network_for_radar_perception_amd import engine as _eng
         ms = float(np.mean(durs['conv_fused']))
         ref_flops = 65536.0 * E + 16384.0 * N
-        flops = (32768.0 * E + 49152.0 * N) if args.dtype == 'fp32' else (49152.0 * E + 32768.0 * N)
+        x3 = args.dtype == 'fp32' and _eng.F32_ARITH == 'x3'
+        if x3:
+            flops = 32768.0 * E + 16384.0 * N + 32768.0 * N * (args.layers - 1) / args.layers
+        elif args.dtype == 'fp32':
+            flops = 32768.0 * E + 49152.0 * N
+        else:
+            flops = 49152.0 * E + 32768.0 * N
         nbytes = E * (C * s + 8) + N * (2 * C * s + 4)     # e rows + (src,dst) once; x in/out once
         tf = flops / (ms * 1e-3) / 1e12
         ref_tf = ref_flops / (ms * 1e-3) / 1e12
@@ -735,10 +747,20 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         kern['conv_fused'].update(algorithmic_tflops=round(tf, 2), algorithmic_gbs=round(gbs, 1),
                                   flops_per_launch=flops, bytes_per_launch=nbytes,
                                   reference_form_tflops=round(ref_tf, 2))
-        kname = ('conv_fused (rg_conv_layer_f32: per-node projection + fused layer launches, '
-                 'gnn_blocks.py:96-113)' if args.dtype == 'fp32' else
-                 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)')
-        traffic, tsrc = pmc_traffic(args, 'conv_f32' if args.dtype == 'fp32' else 'fused_conv')
+        if x3:
+            kname = ('conv_fused (conv_x3_kernel = rg_conv_layer_x3: f32 products from exact '
+                     '3-term bf16 splits on v_mfma_f32_32x32x16_bf16, gnn_blocks.py:96-113)')
+            # roofline on the pipe it runs on: the bf16 matrix cores, which execute six bf16
+            # products per f32 product
+            conv_exec, conv_peak = 6.0, MFMA_PEAK_TFLOPS['bf16']
+            kern['conv_fused']['bf16_mfma_tflops'] = round(6 * tf, 2)
+        elif args.dtype == 'fp32':
+            kname = ('conv_fused (rg_conv_layer_f32: per-node projection + fused layer launches, '
+                     'gnn_blocks.py:96-113)')
+        else:
+            kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
+        traffic, tsrc = pmc_traffic(args, 'conv_x3' if x3 else (
+            'conv_f32' if args.dtype == 'fp32' else 'fused_conv'))
     else:
         # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
         ms = float(np.mean(durs['message_chain']))
@@ -761,12 +783,15 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2),
                                     flops_per_launch=enc_flops,
                                     mfma_frac=round(enc_flops / (enc_ms * 1e-3) / 1e12 / peak_tf, 4))
-    frac_mfma = tf / peak_tf
+    frac_mfma = conv_exec * tf / conv_peak
     frac_hbm = gbs / HBM_PEAK_GBS
     if frac_mfma >= frac_hbm:
-        roof = {'kernel': kname, 'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak_tf,
-                'unit': 'TFLOP/s', 'frac': round(frac_mfma, 4), 'traffic': traffic,
-                'hbm_frac': round(frac_hbm, 4)}
+        roof = {'kernel': kname, 'bound': 'mfma', 'achieved': round(conv_exec * tf, 2),
+                'peak': conv_peak, 'unit': 'TFLOP/s', 'frac': round(frac_mfma, 4),
+                'traffic': traffic, 'hbm_frac': round(frac_hbm, 4)}
+        if conv_exec != 1.0:
+            roof.update(f32_tflops=round(tf, 2), executed_per_f32_flop=conv_exec,
+                        f32_equivalent_peak=round(conv_peak / conv_exec, 1))
     else:
         roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': traffic,

@@ -25,6 +25,7 @@ RG_F32, RG_BF16 = 0, 1
 RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD, RG_PACK_F32_FAST = 2, 3, 4, 5
 RG_PACK_CENTERED = 0x100
 RG_PACK_TRANSPOSE = 0x200
+RG_PACK_X3 = 0x400
 RG_LAYER_CENTERED = 1
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
@@ -112,9 +113,15 @@ _SIGNATURES = {
                                _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
     'rg_mlp_chain_f32': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _P, _P,
                               _I, _P]),
+    'rg_mlp_chain_x3': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _P, _P,
+                             _I, _P]),
     'rg_conv_layer_f32_workspace_size': (_S, [_I]),
     'rg_conv_layer_f32': (_I, [ctypes.POINTER(rg_layer), _I, _P, _I, _P, _I, _P, _P, _P, _I, _P,
                                _I, _P, _S, _P]),
+    'rg_conv_layer_x3_workspace_size': (_S, [_I]),
+    'rg_conv_layer_x3': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I, _P,
+                              _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _S, _P]),
+    'rg_conv_proj_x3': (_I, [ctypes.POINTER(rg_layer), _P, _I, _I, _P, _P]),
     'rg_conv_layer_workspace_size': (_S, []),
     'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,
                                  _P, _I, _P, _P, _P, _I, _P, _I, _P, _P]),

@@ -26,7 +26,8 @@ FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-Wall',
 # per-source flags: the fused conv keeps its epilogue in scalar f32 (a packed v_pk_*_f32
 # beside MFMAs costs far more than two scalar ops, MI355X_MICROARCH.md "price of one
 # filler"); measured 3.5 % faster per conv layer than the packed build
-FILE_FLAGS = {'conv_fused.hip': ['-DRG_NO_PK', '-fno-slp-vectorize']}
+FILE_FLAGS = {'conv_fused.hip': ['-DRG_NO_PK', '-fno-slp-vectorize'],
+              'conv_x3.hip': ['-fno-slp-vectorize']}
 
 
 def _headers():

@@ -1,0 +1,479 @@
+// Float32 residual_graph_conv_block (gnn_blocks.py:96-113) on the bf16 matrix cores:
+// every f32 operand is split EXACTLY into three bf16 terms, v = v0 + v1 + v2 (round to
+// nearest even at each step: v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1); the
+// residues are exact in f32 and the third term holds the last 8 significant bits), and a
+// product a.b is formed from the six terms of weight <= 2,
+//     a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0,
+// on v_mfma_f32_32x32x16_bf16 with f32 accumulation.  The dropped terms a1 b2 + a2 b1 +
+// a2 b2 are below 2^-23 |a b|: each product carries about the error of one f32 rounding,
+// the accumulation is f32 -- the arithmetic of the reference's fp32 path, not of bf16.
+// Six 32-cycle bf16 MFMAs replace eight 64-cycle f32 MFMAs per 16-deep k-step (2.7x the
+// matrix rate of v_mfma_f32_32x32x2_f32, conv_f32.hip).
+//
+// One layer = ONE launch (rg_conv_layer_x3):
+//  * work block = 32 destination nodes and their incoming edges (destination-major CSR);
+//    workgroups are persistent and take blocks from one counter per XCD over that XCD's
+//    contiguous eighth of the nodes; the last workgroup out re-zeroes the counters;
+//  * per 32-edge tile a wave computes
+//        h = act(norm(P[dst] + Q[src] + W_e e))     P | Q = the per-node projections of
+//                                                   msg0's x_i / x_j columns (+ b1)
+//        m = act(norm(W_2 h + b2))                   (h stays in registers: layer 2's B)
+//    then the segmented sum: the message tile is transposed through a wave-private LDS
+//    tile (lane = feature) and summed IN EDGE ORDER into a running sum that starts anew
+//    at each change of destination (wave-uniform), the reference scatter_add_ order; a
+//    finished destination's sum is stored as one 256-B row to the aggregate scratch;
+//  * after the block's last tile: update MLP on cat(x, agg) (agg read back from L2),
+//    norm + act + residual -> x_out, and -- when the next layer is also this kernel --
+//    the NEXT layer's projections P' | Q' = W'_pq x_out (+ [b1'; 0]) from the same
+//    registers, so x_out is never re-read for them.
+// The first layer's projections come from rg_conv_proj_x3.
+#include "x3_common.h"
+
+namespace rg {
+namespace convx3 {
+
+using namespace ::rg::x3;
+
+static constexpr int C = 64;      // node / edge / message / output channels
+static constexpr int HID = 128;   // msg_mlp_hidden_dim
+static constexpr int PQW = 2 * HID;
+static constexpr int NBLK = 32;   // destination nodes per work block
+static constexpr int NXCD = 8;
+static constexpr int FT = 512;    // 8 waves: two per SIMD
+static constexpr int NW = FT / 64;
+static constexpr int TR = 8;      // message rows per LDS transposition pass
+static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
+#ifndef RG_CX3_EXP
+#define RG_CX3_EXP 0  // timing experiments only (wrong results): 1 no tile norm epilogues,
+                      // 2 no segmented sum, 3 no P / Q gathers, 4 no B splits (one plane
+                      // copied), 5 no tile MFMAs, 6 no update / projection phase
+#endif
+
+static constexpr int WE_OFF = 0;                                   // W_e 64 -> 128 (FAST_IN)
+static constexpr int W2_OFF = al16(x3_bytes(C, HID));              // W_2 128 -> 64 (FAST_CHAIN)
+static constexpr int W_LDS = W2_OFF + al16(x3_bytes(HID, C));
+static constexpr int T_BYTES = TR * TS * 4;
+static constexpr int LDS_BYTES = W_LDS + NW * T_BYTES;
+static_assert(LDS_BYTES <= DYN_LDS_MAX, "conv_x3 LDS");
+
+// timing experiments: keep a split alive without its MFMAs
+__device__ __forceinline__ float xor_first(const X3& b) {
+  return __uint_as_float(__builtin_bit_cast(u32x4, b.p0)[0] ^ __builtin_bit_cast(u32x4, b.p1)[0] ^
+                         __builtin_bit_cast(u32x4, b.p2)[0]);
+}
+// P' | Q' of 32 rows held in accumulator layout (xo[2]: features 32m + 8g + 4h + t at
+// register 4g + t of tile m) -> pq rows [256] f32; W'_pq packed FAST_CHAIN x3 (K = 64), read
+// from global memory (L2): the row's B operand is split once, then four passes of two
+// M-tiles keep the live registers bounded
+__device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WBuf& W, const float* bias,
+                                             float* pq_row, bool valid, int lane) {
+  const int h = lane >> 5;
+  X3 b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) b[s] = split_acc(xo[s >> 1], s & 1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[m] = ld_bias_frag(bias, 2 * q + m, h);
+    layer_x3<4, 2, 8>(acc, W, 2 * q, [&](int s) { return b[s]; });
+    if (valid) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(f32x4*)(pq_row + 64 * q + 32 * m + 8 * g + 4 * h) =
+              (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+    }
+  }
+}
+
+struct Args {
+  const float* x;
+  const float* e;
+  const float* pq;       // [N][256]: P | Q of this layer
+  const int* seg_ptr;
+  const int* src;
+  const int* dst;
+  float* x_out;
+  float* pq_out;         // [N][256] the next layer's P | Q, or null
+  float* agg;            // [N][64] aggregate scratch
+  int* counters;         // [NXCD] block counters + [1] done counter; zero at launch
+  const char* w[3];      // W_e (FAST_IN), W_2 (FAST_CHAIN), W_u (FAST_IN over cat(x, agg)), x3
+  const char* wpq;       // the next layer's projection (FAST_CHAIN x3) or null
+  const float* mu[3];
+  const float* sd[3];
+  int ldx, lde, ldo;
+  int n_nodes, n_blocks;
+  int aggr_mean;
+};
+
+__global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[6];
+  if (threadIdx.x < 3) {
+    nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
+    nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
+  }
+  {
+    const int nb[2] = {x3_bytes(C, HID), x3_bytes(HID, C)};
+    const int off[2] = {WE_OFF, W2_OFF};
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const u32x4* s = (const u32x4*)a.w[l];
+      u32x4* d = (u32x4*)(lds + off[l]);
+      for (int i = threadIdx.x; i < nb[l] / 16; i += FT) d[i] = s[i];
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  float* T = (float*)(lds + W_LDS + wave * T_BYTES);  // [TR][TS] message rows
+  const WLds wE{lds + WE_OFF + lane * 16, plane_bytes(C, HID)};
+  const WLds w2{lds + W2_OFF + lane * 16, plane_bytes(HID, C)};
+  const WBuf wU = wbuf(a.w[2], x3_bytes(2 * C, C), plane_bytes(2 * C, C), lane);
+  const WBuf wPQ = wbuf(a.wpq, a.wpq ? x3_bytes(C, PQW) : 0, plane_bytes(C, PQW), lane);
+  const float* bias2 = (const float*)(lds + W2_OFF + 3 * plane_bytes(HID, C));
+  const float* biasU = (const float*)(a.w[2] + 3 * plane_bytes(2 * C, C));
+  const float* biasPQ = a.wpq ? (const float*)(a.wpq + 3 * plane_bytes(C, PQW)) : nullptr;
+  const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3], muU = nrm[4], sdU = nrm[5];
+
+  const int xcd = blockIdx.x % NXCD;
+  const int blo = (int)((long)a.n_blocks * xcd / NXCD);
+  const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  int* ctr = a.counters + xcd;
+
+  for (;;) {
+    int bi = 0;
+    if (lane == 0) bi = atomicAdd(ctr, 1);
+    // readfirstlane, not a shuffle: the block id, its node / edge range and the segment
+    // state below are then provably wave-uniform (scalar registers and scalar branches)
+    const int blk = blo + __builtin_amdgcn_readfirstlane(bi);
+    if (blk >= bhi) break;
+    const int n0 = blk * NBLK;
+    const int n1 = min(n0 + NBLK, a.n_nodes);
+    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+    float run = 0.f;  // lane = feature: running sum of the current destination
+    int cur = -1;     // its slot (wave-uniform)
+    int pn = min(e0 + r, e1 - 1);
+    int dn = e0 < e1 ? a.dst[pn] : 0, sn = e0 < e1 ? a.src[pn] : 0;
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+      const int p = pn, d = dn, sj = sn;
+      pn = min(t0 + 32 + r, e1 - 1);  // the next tile's indices (latency behind this tile)
+      dn = a.dst[pn];
+      sn = a.src[pn];
+      // ---- layer 1: h = P[dst] + Q[src] + W_e e
+      f32x16 acc1[4];
+      {
+        const float* pp = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : d) * PQW + 4 * h;
+        const float* pq = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : sj) * PQW + HID + 4 * h;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 pv = *(const f32x4*)(pp + 32 * m + 8 * g);
+            acc1[m][4 * g + 0] = pv.x;
+            acc1[m][4 * g + 1] = pv.y;
+            acc1[m][4 * g + 2] = pv.z;
+            acc1[m][4 * g + 3] = pv.w;
+          }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 qv = *(const f32x4*)(pq + 32 * m + 8 * g);
+            acc1[m][4 * g + 0] += qv.x;
+            acc1[m][4 * g + 1] += qv.y;
+            acc1[m][4 * g + 2] += qv.z;
+            acc1[m][4 * g + 3] += qv.w;
+          }
+      }
+      {
+        const float* pe = a.e + (size_t)p * a.lde + 8 * h;
+        X3 eb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          eb[s] = split8(*(const f32x4*)(pe + 16 * s), *(const f32x4*)(pe + 16 * s + 4));
+        if constexpr (RG_CX3_EXP != 5) {
+          layer_x3<4, 4, 4>(acc1, wE, 0, [&](int s) { return eb[s]; });
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            acc1[s][0] += xor_first(eb[s]);
+        }
+      }
+      if constexpr (RG_CX3_EXP != 1) norm_leaky<4>(acc1, mu0, sd0);
+      // ---- layer 2 (B operand = layer 1's accumulators)
+      f32x16 acc2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
+      if constexpr (RG_CX3_EXP != 5) {
+        layer_x3<8, 2, 2>(acc2, w2, 0, [&](int s) { return split_acc(acc1[s >> 1], s & 1); });
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const X3 b = split_acc(acc1[s >> 1], s & 1);
+          acc2[s & 1][s] += xor_first(b);
+        }
+      }
+      if constexpr (RG_CX3_EXP != 1) norm_leaky<2>(acc2, mu1, sd1);
+      if constexpr (RG_CX3_EXP == 2) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) run += acc2[m][q];
+        cur = 0;
+        continue;
+      }
+      // ---- segmented sum in edge order, TR edges per LDS pass
+#pragma unroll
+      for (int c = 0; c < 32 / TR; ++c) {
+        if (t0 + TR * c >= e1) break;  // wave-uniform
+        if (r / TR == c) {
+          float* row = T + (r % TR) * TS + 4 * h;
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){acc2[m][4 * g], acc2[m][4 * g + 1],
+                                                        acc2[m][4 * g + 2], acc2[m][4 * g + 3]};
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        float v[TR];  // all rows of the pass in flight at once
+#pragma unroll
+        for (int j = 0; j < TR; ++j) v[j] = T[j * TS + lane];
+#pragma unroll
+        for (int j = 0; j < TR; ++j) {
+          const int eo = TR * c + j;
+          if (t0 + eo < e1) {
+            const int slot = __builtin_amdgcn_readlane(d, eo) - n0;
+            if (slot != cur) {
+              if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
+              run = v[j];
+              cur = slot;
+            } else {
+              run += v[j];
+            }
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
+    // the aggregate rows were written by this wave's lanes = features; read them back as
+    // rows (lane = node) from L2: stores complete (vmcnt 0), loads bypass L1 (nt)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+
+    if constexpr (RG_CX3_EXP == 6) {
+      if (n0 + r < n1) a.x_out[(size_t)(n0 + r) * a.ldo + h] = run;
+      continue;
+    }
+    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
+    const int node = n0 + r;
+    const bool nvalid = node < n1;
+    const int nrow = nvalid ? node : n0;
+    const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 0;
+    const float* px = a.x + (size_t)nrow * a.ldx;
+    f32x4 xb[4][2], ab[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      xb[s][0] = *(const f32x4*)(px + 16 * s + 8 * h);
+      xb[s][1] = *(const f32x4*)(px + 16 * s + 8 * h + 4);
+    }
+    {
+      const f32x4* pa = (const f32x4*)(a.agg + (size_t)nrow * C + 8 * h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        ab[s][0] = __builtin_nontemporal_load(pa + 4 * s);
+        ab[s][1] = __builtin_nontemporal_load(pa + 4 * s + 1);
+      }
+      // no incoming edges: PyG leaves the aggregate at zero; mean = sum / max(count, 1)
+      const float sc = deg > 0 ? (float)deg : 1.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          f32x4 v = deg > 0 ? ab[s][u] : (f32x4){0.f, 0.f, 0.f, 0.f};
+          if (a.aggr_mean) v = (f32x4){div_rn(v.x, sc), div_rn(v.y, sc), div_rn(v.z, sc), div_rn(v.w, sc)};
+          ab[s][u] = v;
+        }
+    }
+    f32x16 accu[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
+    layer_x3<8, 2, 2>(accu, wU, 0, [&](int s) {
+      return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
+    });
+    norm_leaky<2>(accu, muU, sdU);
+    {
+      const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 xr = *(const f32x4*)(pxr + 32 * m + 8 * g);
+          accu[m][4 * g + 0] = __fadd_rn(xr.x, accu[m][4 * g + 0]);
+          accu[m][4 * g + 1] = __fadd_rn(xr.y, accu[m][4 * g + 1]);
+          accu[m][4 * g + 2] = __fadd_rn(xr.z, accu[m][4 * g + 2]);
+          accu[m][4 * g + 3] = __fadd_rn(xr.w, accu[m][4 * g + 3]);
+        }
+    }
+    if (nvalid) {
+      float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(f32x4*)(po + 32 * m + 8 * g) = (f32x4){accu[m][4 * g], accu[m][4 * g + 1],
+                                                   accu[m][4 * g + 2], accu[m][4 * g + 3]};
+    }
+    if (a.pq_out) project_rows(accu, wPQ, biasPQ, a.pq_out + (size_t)nrow * PQW, nvalid, lane);
+  }
+  // the last workgroup out re-zeroes the counters for the next launch (stream order)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.counters + NXCD, 1) == (int)gridDim.x - 1) {
+#pragma unroll
+      for (int i = 0; i <= NXCD; ++i) a.counters[i] = 0;
+    }
+  }
+}
+
+// P | Q = W_pq x + [b1; 0] for dense float32 rows (the first layer's projections):
+// W_pq packed FAST_IN x3 (K = 64, N = 256), staged in LDS; one 32-row tile per wave
+static constexpr int PFT = 256;
+__global__ __launch_bounds__(PFT) void proj_x3_kernel(const float* x, int ldx, int n_nodes,
+                                                      const char* wpq, float* pq) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int NB = x3_bytes(C, PQW);
+  {
+    const u32x4* s = (const u32x4*)wpq;
+    u32x4* d = (u32x4*)lds;
+    for (int i = threadIdx.x; i < NB / 16; i += PFT) d[i] = s[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const float* bias = (const float*)(lds + 3 * plane_bytes(C, PQW));
+  const long ntiles = (n_nodes + 31) / 32;
+  for (long t = (long)blockIdx.x * (PFT / 64) + wave; t < ntiles; t += (long)gridDim.x * (PFT / 64)) {
+    const long row = t * 32 + r;
+    const bool valid = row < n_nodes;
+    const float* px = x + (size_t)(valid ? row : 0) * ldx + 8 * h;
+    f32x4 xb[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      xb[s][0] = *(const f32x4*)(px + 16 * s);
+      xb[s][1] = *(const f32x4*)(px + 16 * s + 4);
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f32x16 acc[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[m] = ld_bias_frag(bias, 4 * half + m, h);
+      layer_x3<4, 4, 8>(acc, WLds{lds + lane * 16, plane_bytes(C, PQW)}, 4 * half, [&](int s) { return split8(xb[s][0], xb[s][1]); });
+      if (valid) {
+        float* po = pq + (size_t)row * PQW + 128 * half + 4 * h;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *(f32x4*)(po + 32 * m + 8 * g) =
+                (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+      }
+    }
+  }
+}
+
+}  // namespace convx3
+}  // namespace rg
+
+using namespace rg;
+using namespace rg::convx3;
+
+extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
+  return 256 + (size_t)(n_nodes > 0 ? n_nodes : 1) * C * sizeof(float);
+}
+
+extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes,
+                               float* pq_out, void* stream) {
+  RG_REQUIRE(pq && pq->in_dim == C && pq->out_dim == PQW && !pq->norm_mu && pq->act == RG_ACT_NONE,
+             RG_ERR_UNSUPPORTED, "rg_conv_proj_x3: expects the 64 -> 256 projection");
+  RG_REQUIRE(ldx % 4 == 0, RG_ERR_UNSUPPORTED, "rg_conv_proj_x3: row stride must be a multiple of 4");
+  if (n_nodes <= 0) return RG_OK;
+  constexpr int lds = x3_bytes(C, PQW);
+  RG_ENSURE_LDS(proj_x3_kernel, lds);
+  const long tiles = (n_nodes + 31) / 32;
+  long blocks = (tiles + 3) / 4;
+  if (blocks > 256) blocks = 256;
+  proj_x3_kernel<<<blocks, PFT, lds, (hipStream_t)stream>>>(x, ldx, n_nodes,
+                                                           (const char*)pq->w_packed, pq_out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr,
+                                const float* x, int ldx, const float* e, int lde, const float* pq,
+                                const int* seg_ptr, const int* src, const int* dst, int n_nodes,
+                                float* x_out, int ld_out, float* pq_out, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  const rg_layer& m0 = layers[0];
+  const rg_layer& m1 = layers[1];
+  const rg_layer& u = layers[2];
+  if (!(m0.in_dim == C && m0.out_dim == HID && m1.in_dim == HID && m1.out_dim == C &&
+        u.in_dim == 2 * C && u.out_dim == C))
+    return RG_ERR_UNSUPPORTED;
+  if (aggr != RG_REDUCE_SUM && aggr != RG_REDUCE_MEAN) return RG_ERR_UNSUPPORTED;
+  if (!m0.norm_mu || !m1.norm_mu || !u.norm_mu) return RG_ERR_UNSUPPORTED;
+  if (m0.act != ACT_LEAKY || m1.act != ACT_LEAKY || u.act != ACT_LEAKY) return RG_ERR_UNSUPPORTED;
+  if ((m0.flags | m1.flags | u.flags) & RG_LAYER_CENTERED) return RG_ERR_UNSUPPORTED;
+  RG_REQUIRE(!next_pq == !pq_out, RG_ERR_ARG, "rg_conv_layer_x3: next_pq and pq_out go together");
+  RG_REQUIRE(!next_pq || (next_pq->in_dim == C && next_pq->out_dim == PQW && !next_pq->norm_mu &&
+                          next_pq->act == RG_ACT_NONE),
+             RG_ERR_UNSUPPORTED, "rg_conv_layer_x3: next_pq must be the 64 -> 256 projection");
+  RG_REQUIRE(ldx % 4 == 0 && lde % 4 == 0 && ld_out % 4 == 0, RG_ERR_UNSUPPORTED,
+             "rg_conv_layer_x3: row strides must be multiples of 4");
+  RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_x3: x_out must not alias x");
+  RG_REQUIRE(!pq_out || pq_out != pq, RG_ERR_ARG, "rg_conv_layer_x3: pq_out must not alias pq");
+  RG_REQUIRE(workspace_bytes >= rg_conv_layer_x3_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_conv_layer_x3: workspace too small");
+  if (n_nodes <= 0) return RG_OK;
+  Args a;
+  memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.e = e;
+  a.pq = pq;
+  a.seg_ptr = seg_ptr;
+  a.src = src;
+  a.dst = dst;
+  a.x_out = x_out;
+  a.pq_out = pq_out;
+  a.counters = (int*)workspace;
+  a.agg = (float*)((char*)workspace + 256);
+  a.w[0] = (const char*)m0.w_packed;
+  a.w[1] = (const char*)m1.w_packed;
+  a.w[2] = (const char*)u.w_packed;
+  a.wpq = next_pq ? (const char*)next_pq->w_packed : nullptr;
+  const rg_layer* ls[3] = {&m0, &m1, &u};
+  for (int l = 0; l < 3; ++l) {
+    a.mu[l] = ls[l]->norm_mu;
+    a.sd[l] = ls[l]->norm_std;
+  }
+  a.ldx = ldx;
+  a.lde = lde;
+  a.ldo = ld_out;
+  a.n_nodes = n_nodes;
+  a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
+  a.aggr_mean = aggr == RG_REDUCE_MEAN;
+  int blocks = 256;  // one workgroup per CU (LDS)
+  const int need = (a.n_blocks + NW - 1) / NW;
+  if (blocks > need) blocks = need;
+  if (blocks < NXCD) blocks = NXCD;
+  RG_ENSURE_LDS(conv_x3_kernel, LDS_BYTES);
+  conv_x3_kernel<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

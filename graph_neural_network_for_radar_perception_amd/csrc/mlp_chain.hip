@@ -55,6 +55,8 @@ __host__ __device__ inline size_t frag_bytes(int in_dim, int out_dim, int dtype)
   return mt * (kpad(in_dim, 32) / 32) * 64 * 8 * sizeof(uint16_t);
 }
 static size_t packed_bytes(int in_dim, int out_dim, int dtype) {
+  if (dtype & RG_PACK_X3)  // three bf16 planes, then the bias (accumulator order)
+    return 3 * frag_bytes(in_dim, out_dim, dtype & ~RG_PACK_X3) + (size_t)kpad(out_dim, 32) * sizeof(float);
   const int bpad = (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN ||
                     dtype == RG_PACK_FAST_UPD || dtype == RG_PACK_F32_FAST) ? 32 : 16;
   return frag_bytes(in_dim, out_dim, dtype) + (size_t)kpad(out_dim, bpad) * sizeof(float);
@@ -129,8 +131,10 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
 //            accumulator registers 8(s&1)..8(s&1)+7 of M-tile s>>1, no lane movement)
 // FAST_UPD  k-steps s < in/32 as FAST_IN (x[node] from memory), the rest as FAST_CHAIN
 //           offset by in/2 (aggregate from accumulators): the fused conv layer's update
+// plane p > 0 (RG_PACK_X3): the p-th bf16 term of the exact three-term split of each
+// weight, w = bf16(w) + bf16(w - w0) + bf16(w - w0 - w1) (conv_x3.hip)
 __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int mem_steps,
-                                 int center, uint16_t* __restrict__ P, long total) {
+                                 int center, int plane, uint16_t* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S = (in + 15) / 16;
@@ -154,6 +158,7 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
       v -= cs / (float)out;
     }
   }
+  for (int q = 0; q < plane; ++q) v -= bf16_to_f32(f32_to_bf16(v));  // exact residues
   P[t] = f32_to_bf16(v);
 }
 
@@ -551,11 +556,37 @@ extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
   return packed_bytes(in_dim, out_dim, dtype & ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE));
 }
 
+// RG_PACK_X3: three planes of one RG_PACK_FAST_* format
+static int pack_x3(const float* weight, const float* bias, int in_dim, int out_dim, int fmt,
+                   void* packed, hipStream_t st) {
+  RG_REQUIRE(fmt == RG_PACK_FAST_IN || fmt == RG_PACK_FAST_CHAIN || fmt == RG_PACK_FAST_UPD,
+             RG_ERR_ARG, "rg_pack_linear: RG_PACK_X3 applies to the RG_PACK_FAST_* formats");
+  const int ks = (in_dim + 15) / 16;
+  RG_REQUIRE(fmt != RG_PACK_FAST_UPD || in_dim % 64 == 0, RG_ERR_ARG,
+             "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
+  const int mem_steps = fmt == RG_PACK_FAST_IN ? ks : (fmt == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
+  const size_t fb = frag_bytes(in_dim, out_dim, fmt);
+  const long total = (long)fb / sizeof(uint16_t);
+  for (int p = 0; p < 3; ++p)
+    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps, 0, p,
+                                                           (uint16_t*)((char*)packed + p * fb), total);
+  const int nb = kpad(out_dim, 32);
+  pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, 0,
+                                                           (float*)((char*)packed + 3 * fb));
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim, int out_dim,
                               int dtype, void* packed, void* stream) {
   RG_REQUIRE(in_dim > 0 && out_dim > 0 && in_dim <= MAXW && out_dim <= MAXW, RG_ERR_UNSUPPORTED,
              "rg_pack_linear: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
   hipStream_t st = (hipStream_t)stream;
+  if (dtype & RG_PACK_X3) {
+    RG_REQUIRE(!(dtype & (RG_PACK_CENTERED | RG_PACK_TRANSPOSE)), RG_ERR_ARG,
+               "rg_pack_linear: RG_PACK_X3 does not combine with CENTERED / TRANSPOSE");
+    return pack_x3(weight, bias, in_dim, out_dim, dtype & ~RG_PACK_X3, packed, st);
+  }
   const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
   const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;
   dtype &= ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE);
@@ -578,7 +609,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
     const int mem_steps = dtype == RG_PACK_FAST_IN ? ks : (dtype == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
     pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
-                                                           center, (uint16_t*)packed, total);
+                                                           center, 0, (uint16_t*)packed, total);
   } else if (dtype == RG_PACK_F32_FAST) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
     pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,

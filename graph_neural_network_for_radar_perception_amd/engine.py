@@ -23,6 +23,7 @@ float32.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from dataclasses import dataclass
 from typing import List, Optional
@@ -35,6 +36,12 @@ from .common import (Activation, channel_normalization, ffn_block, group_normali
                      layer_normalization)
 
 DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16)}
+
+# Arithmetic of the fused fp32 conv layer: 'x3' = float32 products from exact three-term
+# bf16 splits on the bf16 matrix cores (rg_conv_layer_x3, one launch per layer, the next
+# layer's projections fused into the update); 'mfma_f32' = v_mfma_f32_32x32x2_f32
+# (rg_conv_layer_f32).  Both keep float32 accuracy (tests/test_gpu_f32.py runs both).
+F32_ARITH = os.environ.get('RG_F32_ARITH', 'x3')
 
 
 def _dt_code(t: torch.Tensor) -> int:
@@ -228,6 +235,8 @@ class ChainPlan:
             self.fast = fg[0][0]
         self.fast_ok = {}   # in_mode -> bool (shape has a compiled fast kernel)
         self._f32 = None    # RG_PACK_F32_FAST layer array, packed on first fp32 fast call
+        self._x3 = None     # RG_PACK_X3 layer array (rg_mlp_chain_x3), likewise
+        self.x3_ok = {}     # in_mode -> bool (shape has a compiled x3 kernel)
         self.sig = self._signature()
 
     def refresh(self):
@@ -287,6 +296,16 @@ class ChainPlan:
             cur = (dst, plan.out_dim, nat.IN_DENSE, None, 0, None, 0, None, None)
         return out
 
+    def _x3_layers(self):
+        """The chain packed RG_PACK_X3 (layer 0 FAST_IN, later FAST_CHAIN) for
+        rg_mlp_chain_x3 (lazily)."""
+        if self._x3 is None:
+            X3 = nat.RG_PACK_X3
+            self._x3buf, groups = self._pack_buffer(
+                lambda i: (nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN) | X3)
+            self._x3 = groups[0][0]
+        return self._x3
+
     def _f32_layers(self):
         """The chain packed RG_PACK_F32_FAST for rg_mlp_chain_f32 (lazily: training chains
         never use it)."""
@@ -303,10 +322,20 @@ class ChainPlan:
                                      residual, rows_dev, segs)
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
-        if (self.use_fast and self.dt == nat.RG_F32 and mode in (nat.IN_DENSE, nat.IN_PAIRADD)
-                and residual is None and in0.dtype == torch.float32
-                and out.dtype == torch.float32 and len(self.specs) <= nat.MAX_LAYERS
-                and self.fast_ok.get(mode, True)):
+        f32_fast = (self.use_fast and self.dt == nat.RG_F32 and mode in (nat.IN_DENSE, nat.IN_PAIRADD)
+                    and residual is None and in0.dtype == torch.float32
+                    and out.dtype == torch.float32 and len(self.specs) <= nat.MAX_LAYERS)
+        if f32_fast and F32_ARITH == 'x3' and self.x3_ok.get(mode, True):
+            rc = lib.rg_mlp_chain_x3(self._x3_layers(), len(self.specs), int(rows),
+                                     nat.ptr(rows_dev), mode, in0.data_ptr(), in0.stride(0), w0,
+                                     nat.ptr(idx0), nat.ptr(idx1), out.data_ptr(), out.stride(0), st)
+            if rc == 0:
+                self.x3_ok[mode] = True
+                return out
+            if rc != nat.RG_ERR_UNSUPPORTED:
+                nat.check(rc, 'rg_mlp_chain_x3')
+            self.x3_ok[mode] = False
+        if f32_fast and self.fast_ok.get(mode, True):
             rc = lib.rg_mlp_chain_f32(self._f32_layers(), len(self.specs), int(rows),
                                       nat.ptr(rows_dev), mode, in0.data_ptr(), in0.stride(0), w0,
                                       nat.ptr(idx0), nat.ptr(idx1), out.data_ptr(), out.stride(0),
@@ -590,6 +619,7 @@ class ConvPlan:
         self.c_out = self.upd.out_dim
         self.fused_ok = None
         self.use_fused = True   # bf16: one rg_conv_layer_fused launch per layer
+        self.f32_arith = F32_ARITH if dtype == 'fp32' else None
         self._pack_fused()
 
     def _pack_fused_f32(self):
@@ -609,14 +639,31 @@ class ConvPlan:
         pq = LayerSpec(w_pq, b_pq, None, None, 'none')
         we = LayerSpec(W[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
         specs = [pq, we, m1, u]
-        fmts = [nat.RG_PACK_F32_FAST] * 4
+        if self.f32_arith == 'x3':
+            X3 = nat.RG_PACK_X3
+            # [0] W_e, [1] msg1, [2] upd (cat(x, agg) read from memory), [3] P | Q from
+            # memory (first layer), [4] P | Q from the previous layer's registers
+            specs = [we, m1, u, pq, pq]
+            fmts = [nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3, nat.RG_PACK_FAST_IN | X3,
+                    nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3]
+        else:
+            fmts = [nat.RG_PACK_F32_FAST] * 4
         try:
             self.fused_buf, offs = pack_specs(specs, fmts, self.device)
         except RuntimeError:
             return
         self._fused_keep = (w_pq, b_pq, we.weight)   # packing is async: keep the sources
-        self.fused_layers = layer_array(specs, self.fused_buf.data_ptr(), offs, fmts)
-        self.fused_ws = None
+        base = self.fused_buf.data_ptr()
+        if self.f32_arith == 'x3':
+            self.fused_layers = layer_array(specs[:3], base, offs[:3], fmts[:3])
+            self.x3_pq_in = layer_array(specs[3:4], base, offs[3:4], fmts[3:4])
+            self.x3_pq_chain = layer_array(specs[4:5], base, offs[4:5], fmts[4:5])
+            self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_x3_workspace_size(0),
+                                        dtype=torch.uint8, device=self.device)
+            self.x3_pq = None   # projections of a standalone run_fused call
+        else:
+            self.fused_layers = layer_array(specs, base, offs, fmts)
+            self.fused_ws = None
         self.fused = True
         self.fused_sig = self._sig()
 
@@ -668,12 +715,54 @@ class ConvPlan:
             c.invalidate()
         self.fused_sig = None
 
+    @property
+    def x3(self) -> bool:
+        return bool(self.fused) and self.f32_arith == 'x3'
+
+    def x3_ready(self, x, e) -> bool:
+        return (self.use_fused and self.x3 and self.fused_ok is not False
+                and x.dtype == torch.float32 and e.dtype == torch.float32)
+
+    def project_x3(self, x, pq):
+        """P | Q of the first x3 layer (rg_conv_proj_x3)."""
+        nat.check(nat.lib().rg_conv_proj_x3(self.x3_pq_in, x.data_ptr(), x.stride(0), x.shape[0],
+                                            pq.data_ptr(), nat.stream_ptr(x.device)),
+                  'rg_conv_proj_x3')
+
+    def run_x3(self, x, e, g, x_out, pq, nxt=None, pq_out=None) -> bool:
+        """One rg_conv_layer_x3 launch; with nxt (the next ConvPlan, also x3) it also writes
+        the next layer's P | Q into pq_out."""
+        lib = nat.lib()
+        need = lib.rg_conv_layer_x3_workspace_size(g.n_nodes)
+        if self.fused_ws.numel() < need:
+            self.fused_ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
+        rc = lib.rg_conv_layer_x3(
+            self.fused_layers, nxt.x3_pq_chain if nxt is not None else None, nat.REDUCE[self.aggr],
+            x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0), pq.data_ptr(),
+            g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes, x_out.data_ptr(),
+            x_out.stride(0), nat.ptr(pq_out), self.fused_ws.data_ptr(), self.fused_ws.numel(),
+            nat.stream_ptr(x.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            self.fused_ok = False
+            return False
+        nat.check(rc, 'rg_conv_layer_x3')
+        self.fused_ok = True
+        return True
+
     def run_fused(self, x, e, g, x_out) -> bool:
         """One launch for the whole layer; False when the fused kernel does not
         cover this shape (the caller runs the unfused chain + reduce path)."""
         if not self.use_fused or not self.fused or self.fused_ok is False:
             return False
         lib = nat.lib()
+        if self.x3:
+            if not self.x3_ready(x, e):
+                return False
+            n = x.shape[0]
+            if self.x3_pq is None or self.x3_pq.shape[0] < n:
+                self.x3_pq = torch.empty((max(n, 1), 256), dtype=torch.float32, device=self.device)
+            self.project_x3(x, self.x3_pq)
+            return self.run_x3(x, e, g, x_out, self.x3_pq)
         if self.dtype == 'fp32':
             if x.dtype != torch.float32 or e.dtype != torch.float32:
                 return False
@@ -828,11 +917,34 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
     plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
                    segs=segs('edge'))
     mark('edge_encoder:end')
+    pq = None   # fp32 x3 layers: this layer's P | Q projections
     for li, cv in enumerate(plans.convs):
         C = x.shape[1]
         xn = alloc(f'x{(li + 1) % 2}' if li + 1 < len(plans.convs) else 'xL', (N, cv.c_out), T)
         if xn.data_ptr() == x.data_ptr():
             xn = alloc('xalt', (N, cv.c_out), T)
+        if cv.x3_ready(x, e):
+            if pq is None:
+                pq = alloc('pq0', (N, 256), torch.float32)
+                mark('conv_proj:start')
+                cv.project_x3(x, pq)
+                mark('conv_proj:end')
+            nxt = plans.convs[li + 1] if li + 1 < len(plans.convs) else None
+            if nxt is not None and not nxt.x3_ready(xn, e):
+                nxt = None
+            pq_next = None
+            if nxt is not None:   # ping-pong between the two projection buffers
+                pq_next = alloc('pq1', (N, 256), torch.float32)
+                if pq_next.data_ptr() == pq.data_ptr():
+                    pq_next = alloc('pq0', (N, 256), torch.float32)
+            mark('conv_fused:start')
+            if cv.run_x3(x, e, g, xn, pq, nxt, pq_next):
+                mark('conv_fused:end')
+                pq = pq_next
+                x = xn
+                continue
+            events and events.pop()
+            pq = None
         mark('conv_fused:start')
         fused = cv.run_fused(x, e, g, xn)
         if fused:

@@ -60,6 +60,12 @@ extern "C" {
 /* OR-ed into RG_F32: `weight` holds the TRANSPOSE of the packed layer, i.e. a row-major
  * [in_dim][out_dim] matrix (the backward data GEMM dX = dZ W packs W^T this way) */
 #define RG_PACK_TRANSPOSE 0x200
+/* OR-ed into a RG_PACK_FAST_* format: the exact three-term bf16 split of every weight,
+ * w = w0 + w1 + w2 (w0 = bf16(w), w1 = bf16(w - w0), w2 = bf16(w - w0 - w1), each residue
+ * exact in float32), as three planes of that format back to back, then the float32 bias in
+ * accumulator order -- the operand format of the float32 kernels on bf16 matrix cores
+ * (rg_conv_layer_x3) */
+#define RG_PACK_X3 0x400
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -272,6 +278,17 @@ int rg_mlp_chain_f32(const rg_layer* layers_host, int n_layers, long rows, const
                      int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                      const int* idx1, float* out, int ld_out, void* stream);
 
+/* The same float32 chains on the bf16 matrix cores: every product formed from the exact
+ * three-term bf16 splits of both operands (RG_PACK_X3, see rg_conv_layer_x3), f32
+ * accumulation -- float32 accuracy at 2.7x the f32 MFMA rate.  Layer 0 packed
+ * RG_PACK_FAST_IN | RG_PACK_X3, later layers RG_PACK_FAST_CHAIN | RG_PACK_X3, no
+ * RG_LAYER_CENTERED; in_mode and the rest as rg_mlp_chain_f32 (dense inputs of <= 8 features
+ * with an un-normalised first layer, or widths that are multiples of 16).  Returns
+ * RG_ERR_UNSUPPORTED (launching nothing) for shapes without an instantiation. */
+int rg_mlp_chain_x3(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
+                    int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                    const int* idx1, float* out, int ld_out, void* stream);
+
 /* One fused FLOAT32 residual_graph_conv_block (gnn_blocks.py:96-113, the reference
  * precision) for the shipped widths (C = 64, message MLP 192 -> 128 -> 64, update
  * 128 -> 64, channel_normalization + LeakyReLU on every block), aggregation add or mean
@@ -290,6 +307,31 @@ int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx,
                       int lde, const int* seg_ptr, const int* src, const int* dst, int n_nodes,
                       float* x_out, int ld_out, void* workspace, size_t workspace_bytes,
                       void* stream);
+
+/* The same FLOAT32 layer on the bf16 matrix cores: every product of the MLPs is formed
+ * from the exact three-term bf16 splits of both operands (six bf16 products of total
+ * weight <= 2 per product, f32 accumulation; dropped terms < 2^-23 |a b|), so the layer
+ * keeps float32 accuracy at 2.7x the matrix rate of the f32 MFMA path.  One launch per
+ * layer:
+ *   layers[3], all RG_PACK_X3: [0] W_msg0[:, 128:192] (edge columns, FAST_IN) with msg0's
+ *     norm + act, bias unused; [1] msg1 (FAST_CHAIN); [2] upd on cat(x, agg) (FAST_IN over
+ *     the 128 concatenated inputs)
+ *   pq        [n_nodes][256] float32: P | Q = W_msg0[:, 0:64] x + b_msg0 | W_msg0[:, 64:128] x,
+ *             from rg_conv_proj_x3 (first layer) or the previous layer's pq_out
+ *   next_pq   NULL, or the NEXT layer's projection (64 -> 256, FAST_CHAIN | X3, bias
+ *             [b_msg0'; 0]): then pq_out [n_nodes][256] receives it from x_out's registers
+ *   workspace rg_conv_layer_x3_workspace_size(n_nodes) bytes, block counters ZEROED before
+ *             the first call (every completed launch leaves them zero); one per stream.
+ * Same results contract as rg_conv_layer_f32 (sum in edge order, mean = sum / max(deg, 1)). */
+size_t rg_conv_layer_x3_workspace_size(int n_nodes);
+int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, const float* x,
+                     int ldx, const float* e, int lde, const float* pq, const int* seg_ptr,
+                     const int* src, const int* dst, int n_nodes, float* x_out, int ld_out,
+                     float* pq_out, void* workspace, size_t workspace_bytes, void* stream);
+/* P | Q of the first layer for dense float32 rows x [n_nodes][ldx >= 64]: pq layer packed
+ * RG_PACK_FAST_IN | RG_PACK_X3 (64 -> 256, bias [b_msg0; 0]). */
+int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes, float* pq_out,
+                    void* stream);
 
 /* One fused residual_graph_conv_block (gnn_blocks.py:96-113) for the shipped
  * widths (node / edge channels 64, msg MLP 192->128->64, update 128->64, all with

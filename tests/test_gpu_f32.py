@@ -32,12 +32,18 @@ def _torch_chain64(plan, x):
     return h
 
 
-def test_f32_fast_chains_used_and_exact(cuda_device):
-    """Every chain of the yml architecture in fp32 runs on rg_mlp_chain_f32 and agrees
-    with the generic f32 kernel and with a float64 evaluation (1e-4)."""
+@pytest.mark.parametrize('arith', ['x3', 'mfma_f32'])
+def test_f32_fast_chains_used_and_exact(cuda_device, arith, monkeypatch):
+    """Every chain of the yml architecture in fp32 runs on its register-resident kernel --
+    rg_mlp_chain_x3 (f32 products from exact three-term bf16 splits) or rg_mlp_chain_f32
+    (v_mfma_f32_32x32x2_f32) -- and agrees with the generic f32 kernel and with a float64
+    evaluation (1e-4)."""
     from graph_neural_network_for_radar_perception_amd import _native as nat
+    from graph_neural_network_for_radar_perception_amd import engine
     from graph_neural_network_for_radar_perception_amd.config import default_config
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    monkeypatch.setattr(engine, 'F32_ARITH', arith)
+    used = 'x3_ok' if arith == 'x3' else 'fast_ok'
     dev = cuda_device
     torch.manual_seed(5)
     cfg = default_config()
@@ -67,11 +73,13 @@ def test_f32_fast_chains_used_and_exact(cuda_device):
         for use_fast in (True, False):
             plan.use_fast = use_fast
             plan.fast_ok = {}
+            plan.x3_ok = {}
             out = torch.full((R, plan.out_dim), float('nan'), device=dev)
             plan(R, out, **kw)
             outs.append(out)
             if use_fast:
-                assert plan.fast_ok.get(kw.get('mode', nat.IN_DENSE)), 'f32 fast kernel not used'
+                assert getattr(plan, used).get(kw.get('mode', nat.IN_DENSE)), \
+                    f'{arith} chain kernel not used'
         plan.use_fast = True
         if kw.get('mode') == nat.IN_PAIRADD:
             xin = kw['in0'][idx0.long()] + kw['in0'][idx1.long()]
@@ -95,7 +103,7 @@ def test_f32_chain_rows_dev_and_empty(cuda_device):
     out = torch.full((500, 64), 7.0, device=dev)
     n = torch.tensor([123], dtype=torch.int32, device=dev)
     plan(500, out, x, 7, rows_dev=n)
-    assert plan.fast_ok.get(0)
+    assert plan.fast_ok.get(0) or plan.x3_ok.get(0)
     ref = _torch_chain64(plan, x[:123]).float()
     torch.testing.assert_close(out[:123], ref, **FP32_TOL)
     assert bool((out[123:] == 7.0).all())
@@ -110,12 +118,27 @@ def _graph(dev, sizes, k, seed0, cfg):
     return batch, gf.build_graph_batch(batch, cfg, k=k)
 
 
+def _conv_plan(m, arith, li=0):
+    """A fresh fp32 ConvPlan of block li with the given f32 arithmetic ('x3' | 'mfma_f32')."""
+    from graph_neural_network_for_radar_perception_amd import engine
+    old = engine.F32_ARITH
+    engine.F32_ARITH = arith
+    try:
+        cv = engine.ConvPlan(m.pred.pass_messages.conv_blk[li], 'fp32', next(m.parameters()).device)
+    finally:
+        engine.F32_ARITH = old
+    assert cv.f32_arith == arith
+    return cv
+
+
+@pytest.mark.parametrize('arith', ['x3', 'mfma_f32'])
 @pytest.mark.parametrize('aggr', ['add', 'mean'])
-def test_f32_fused_conv_matches_unfused_and_oracle(cuda_device, aggr):
-    """rg_conv_layer_f32 (per-node projections + message MLP + in-order segmented sum +
-    update in two launches) against the unfused f32 path (generic chain + rg_segment_reduce
-    + chain) and the oracle's residual_graph_conv_block, on a batched kNN graph with an
-    isolated-size frame (N = 1: no edges) and frames whose nodes straddle work blocks."""
+def test_f32_fused_conv_matches_unfused_and_oracle(cuda_device, aggr, arith):
+    """The fused float32 conv layer -- rg_conv_layer_x3 (f32 products from exact three-term
+    bf16 splits, one launch) and rg_conv_layer_f32 (v_mfma_f32_32x32x2_f32, two launches) --
+    against the unfused f32 path (generic chain + rg_segment_reduce + chain) and the
+    oracle's residual_graph_conv_block, on a batched kNN graph with an isolated-size frame
+    (N = 1: no edges) and frames whose nodes straddle work blocks."""
     from graph_neural_network_for_radar_perception_amd import engine
     from graph_neural_network_for_radar_perception_amd.config import default_config
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
@@ -124,7 +147,7 @@ def test_f32_fused_conv_matches_unfused_and_oracle(cuda_device, aggr):
                          k_number_nearest_points=10)
     torch.manual_seed(12)
     m = Model_Training(cfg, dev).to(dev).eval().requires_grad_(False)
-    cv = m.pred.plans('fp32').convs[0]
+    cv = _conv_plan(m, arith)
     assert cv.fused
     batch, gb = _graph(dev, [700, 1, 33, 1500, 64], 10, 90, cfg)
     g = gb.graph
@@ -150,7 +173,8 @@ def test_f32_fused_conv_matches_unfused_and_oracle(cuda_device, aggr):
         ctx = gnn_forward_ref._Ctx(sd, cfg)
         ref = gnn_forward_ref.conv_block(ctx, 'pass_messages.conv_blk.0', x.cpu(), e[:E].cpu(), ei)
     torch.testing.assert_close(out_f.cpu(), ref, **FP32_TOL)
-    # a second launch on the same workspace (counters reset by the projection launch)
+    # a second launch on the same workspace (counters reset by the launch itself (x3) or by
+    # the projection launch (mfma_f32))
     out_2 = torch.full((N, 64), float('nan'), device=dev)
     assert cv.run_fused(x, e, g, out_2)
     assert torch.equal(out_f, out_2)
@@ -218,7 +242,7 @@ def test_m_config_full_batch_fp32_matches_oracle(cuda_device):
     assert all(cv.fused_ok for cv in plans.convs), 'fused f32 conv not used'
     for c in (plans.node_enc, plans.edge_enc, plans.node_head, plans.offset_head,
               plans.link_pair, plans.cls_head):
-        assert any(c.fast_ok.values()), 'f32 fast chain not used'
+        assert any(c.fast_ok.values()) or any(c.x3_ok.values()), 'f32 fast chain not used'
     rp = gb.row_ptr.cpu().numpy()
     fptr = np.arange(0, B + 1) * N
     U = int(gb.graph.n_pairs_dev.item())

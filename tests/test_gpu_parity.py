@@ -265,7 +265,7 @@ def test_forward_fp32_matches_reference(cuda_device, name):
         if cv.fused:
             assert cv.fused_ok, name
     if name != 'model_random_widths_N120':   # yml widths: an f32 instantiation exists
-        assert any(plans.edge_enc.fast_ok.values()), name
+        assert any(plans.edge_enc.fast_ok.values()) or any(plans.edge_enc.x3_ok.values()), name
 
 
 BF16_U = 2.0 ** -8   # bf16 unit roundoff (8 significant bits, round to nearest)
