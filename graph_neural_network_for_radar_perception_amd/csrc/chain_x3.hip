@@ -23,6 +23,10 @@ namespace cx3 {
 
 using namespace ::rg::x3;
 
+#ifndef RG_X3_DB
+#define RG_X3_DB false  // double-buffered weight fragments in the chained layers (measured: no gain)
+#endif
+
 enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused into layer 1
        IN_DENSE = 1,   // float32 rows, K0 % 16 == 0
        IN_PAIR = 2 };  // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
@@ -151,8 +155,8 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[RT]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
-  layer_x3<KS, MT, MT, RT>(acc, src_of<S, LM, l>(a, lds, lane), 0,
-                           [&](int s, int t) { return split_acc(prev[t][s >> 1], s & 1); });
+  layer_x3<KS, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, l>(a, lds, lane), 0,
+                                 [&](int s, int t) { return split_acc(prev[t][s >> 1], s & 1); });
 #pragma unroll
   for (int t = 0; t < RT; ++t) epilogue<SPEC, l, MT>(acc[t], nrm);
   if constexpr (l + 1 < S::NL) {
@@ -174,8 +178,8 @@ __device__ __forceinline__ void run_first(const Args& a, const X3 (&b0)[RT][KS0]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
-  layer_x3<KS0, MT, MT, RT>(acc, src_of<S, LM, 0>(a, lds, lane), 0,
-                            [&](int s, int t) { return b0[t][s]; });
+  layer_x3<KS0, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, 0>(a, lds, lane), 0,
+                                  [&](int s, int t) { return b0[t][s]; });
 #pragma unroll
   for (int t = 0; t < RT; ++t) epilogue<SPEC, 0, MT>(acc[t], nrm);
   if constexpr (S::NL > 1) {
@@ -203,8 +207,23 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT1; ++m) acc[t][m] = ld_bias_frag(bias1, m, h);
+  // layer-1 A fragments of layer-0 tile m0 (k-steps 2 m0, 2 m0 + 1), read one tile ahead
+  auto lda1 = [&](int m0, bf16x8_t (&d)[2][MT1][3]) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int m = 0; m < MT1; ++m)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) d[hf][m][p] = W1(p, (m * KS1 + 2 * m0 + hf) * 1024);
+  };
+  // (measured: rolling this loop two tiles per iteration, 67 -> 47 KB of code, made the
+  // edge encoder 12 % slower)
+  bf16x8_t A1[2][2][MT1][3];
+  lda1(0, A1[0]);
 #pragma unroll
   for (int m0 = 0; m0 < MT0; ++m0) {
+    const int u = m0 & 1;
+    if (m0 + 1 < MT0) lda1(m0 + 1, A1[(u + 1) & 1]);
     f32x16 y[RT][1];
 #pragma unroll
     for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
@@ -218,12 +237,7 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
     // layer-1 k-steps 2 m0, 2 m0 + 1 from this tile
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      const int s = 2 * m0 + hf;
-      bf16x8_t A[MT1][3];
-#pragma unroll
-      for (int m = 0; m < MT1; ++m)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) A[m][p] = W1(p, (m * KS1 + s) * 1024);
+      const bf16x8_t(&A)[MT1][3] = A1[u][hf];
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const X3 b = split_acc(y[t][0], hf);
@@ -240,8 +254,8 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
 #pragma unroll
         for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int t = 0; t < RT; ++t) epilogue<SPEC, 1, MT1>(acc[t], nrm);

@@ -37,11 +37,37 @@ using namespace ::rg::x3;
 static constexpr int C = 64;      // node / edge / message / output channels
 static constexpr int HID = 128;   // msg_mlp_hidden_dim
 static constexpr int PQW = 2 * HID;
-static constexpr int NBLK = 32;   // destination nodes per work block
+#ifndef RG_CX3_NBLK
+#define RG_CX3_NBLK 32
+#endif
+#ifndef RG_CX3_DB1
+#define RG_CX3_DB1 0  // double-buffered A fragments in message layer 1 / layer 2
+#endif
+#ifndef RG_CX3_DB2
+#define RG_CX3_DB2 1
+#endif
+#ifndef RG_CX3_PRIO
+#define RG_CX3_PRIO 0
+#endif
+static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
+#ifndef RG_CX3_STAMP
+#define RG_CX3_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_cx3_stamp
+#endif
+#if RG_CX3_STAMP
+__device__ unsigned long long g_cx3_stamp[16];
+#define STAMP(i)                                            \
+  do {                                                      \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += _n - st_last;                              \
+    st_last = _n;                                           \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
 static constexpr int NXCD = 8;
 static constexpr int FT = 512;    // 8 waves: two per SIMD
 static constexpr int NW = FT / 64;
-static constexpr int TR = 8;      // message rows per LDS transposition pass
+static constexpr int TR = 16;     // message rows per LDS transposition pass
 static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
 #ifndef RG_CX3_EXP
 #define RG_CX3_EXP 0  // timing experiments only (wrong results): 1 no tile norm epilogues,
@@ -76,7 +102,7 @@ __device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WBuf& 
     f32x16 acc[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) acc[m] = ld_bias_frag(bias, 2 * q + m, h);
-    layer_x3<4, 2, 8>(acc, W, 2 * q, [&](int s) { return b[s]; });
+    layer_x3<4, 2, 8, true>(acc, W, 2 * q, [&](int s) { return b[s]; });
     if (valid) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -128,6 +154,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
+  if (RG_CX3_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   float* T = (float*)(lds + W_LDS + wave * T_BYTES);  // [TR][TS] message rows
   const WLds wE{lds + WE_OFF + lane * 16, plane_bytes(C, HID)};
   const WLds w2{lds + W2_OFF + lane * 16, plane_bytes(HID, C)};
@@ -143,6 +170,10 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
   int* ctr = a.counters + xcd;
 
+#if RG_CX3_STAMP
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     int bi = 0;
     if (lane == 0) bi = atomicAdd(ctr, 1);
@@ -153,15 +184,37 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     const int n0 = blk * NBLK;
     const int n1 = min(n0 + NBLK, a.n_nodes);
     const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
+    STAMP(0);  // block fetch
     float run = 0.f;  // lane = feature: running sum of the current destination
     int cur = -1;     // its slot (wave-uniform)
     int pn = min(e0 + r, e1 - 1);
     int dn = e0 < e1 ? a.dst[pn] : 0, sn = e0 < e1 ? a.src[pn] : 0;
+    f32x4 en[8];  // the next tile's e rows (k = 16 s + 8 h + 0..7 at [2 s], [2 s + 1])
+    auto load_e = [&](int q, f32x4 (&dst)[8]) {
+      const float* pe = a.e + (size_t)q * a.lde + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        dst[2 * s] = *(const f32x4*)(pe + 16 * s);
+        dst[2 * s + 1] = *(const f32x4*)(pe + 16 * s + 4);
+      }
+    };
+    if (e0 < e1) load_e(pn, en);
     for (int t0 = e0; t0 < e1; t0 += 32) {
-      const int p = pn, d = dn, sj = sn;
-      pn = min(t0 + 32 + r, e1 - 1);  // the next tile's indices (latency behind this tile)
+      const int d = dn, sj = sn;
+      X3 eb[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) eb[s] = split8(en[2 * s], en[2 * s + 1]);
+      // the next tile's indices and e rows now: their latency hides behind this tile (past
+      // the block's last edge the clamped index re-reads a row already in cache)
+      pn = min(t0 + 32 + r, e1 - 1);
       dn = a.dst[pn];
       sn = a.src[pn];
+      load_e(pn, en);
+      // destination-change mask of this tile's edges (bit j: edge t0 + j starts a segment)
+      const int dprev = __shfl_up(d, 1, 64);
+      const uint32_t smask =
+          (uint32_t)__ballot(r == 0 ? d - n0 != cur : d != dprev) &
+          (e1 - t0 >= 32 ? 0xffffffffu : ((1u << (e1 - t0)) - 1u));
       // ---- layer 1: h = P[dst] + Q[src] + W_e e
       f32x16 acc1[4];
       {
@@ -189,26 +242,23 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           }
       }
       {
-        const float* pe = a.e + (size_t)p * a.lde + 8 * h;
-        X3 eb[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          eb[s] = split8(*(const f32x4*)(pe + 16 * s), *(const f32x4*)(pe + 16 * s + 4));
         if constexpr (RG_CX3_EXP != 5) {
-          layer_x3<4, 4, 4>(acc1, wE, 0, [&](int s) { return eb[s]; });
+          layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0, [&](int s) { return eb[s]; });
         } else {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
             acc1[s][0] += xor_first(eb[s]);
         }
       }
+      STAMP(1);  // gathers + layer 1 issue
       if constexpr (RG_CX3_EXP != 1) norm_leaky<4>(acc1, mu0, sd0);
+      STAMP(2);  // norm 1 (waits for layer 1)
       // ---- layer 2 (B operand = layer 1's accumulators)
       f32x16 acc2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
       if constexpr (RG_CX3_EXP != 5) {
-        layer_x3<8, 2, 2>(acc2, w2, 0, [&](int s) { return split_acc(acc1[s >> 1], s & 1); });
+        layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0, [&](int s) { return split_acc(acc1[s >> 1], s & 1); });
       } else {
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
@@ -216,7 +266,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           acc2[s & 1][s] += xor_first(b);
         }
       }
+      STAMP(3);  // layer 2 issue
       if constexpr (RG_CX3_EXP != 1) norm_leaky<2>(acc2, mu1, sd1);
+      STAMP(4);  // norm 2
       if constexpr (RG_CX3_EXP == 2) {
 #pragma unroll
         for (int m = 0; m < 2; ++m)
@@ -247,11 +299,10 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         for (int j = 0; j < TR; ++j) {
           const int eo = TR * c + j;
           if (t0 + eo < e1) {
-            const int slot = __builtin_amdgcn_readlane(d, eo) - n0;
-            if (slot != cur) {
+            if ((smask >> eo) & 1u) {  // a new destination: flush the finished sum
               if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
               run = v[j];
-              cur = slot;
+              cur = __builtin_amdgcn_readlane(d, eo) - n0;
             } else {
               run += v[j];
             }
@@ -260,7 +311,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
       }
+      STAMP(5);  // segmented sum
     }
+    STAMP(9);  // tile loop exit
     if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
     // the aggregate rows were written by this wave's lanes = features; read them back as
     // rows (lane = node) from L2: stores complete (vmcnt 0), loads bypass L1 (nt)
@@ -303,10 +356,11 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     f32x16 accu[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
-    layer_x3<8, 2, 2>(accu, wU, 0, [&](int s) {
+    layer_x3<8, 2, 2, true>(accu, wU, 0, [&](int s) {
       return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
     });
     norm_leaky<2>(accu, muU, sdU);
+    STAMP(6);  // update loads + layer
     {
       const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
 #pragma unroll
@@ -329,8 +383,14 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           *(f32x4*)(po + 32 * m + 8 * g) = (f32x4){accu[m][4 * g], accu[m][4 * g + 1],
                                                    accu[m][4 * g + 2], accu[m][4 * g + 3]};
     }
+    STAMP(7);  // residual + store
     if (a.pq_out) project_rows(accu, wPQ, biasPQ, a.pq_out + (size_t)nrow * PQW, nvalid, lane);
+    STAMP(8);  // next layer's projections
   }
+#if RG_CX3_STAMP
+  if (lane == 0)
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_cx3_stamp[i], st_acc[i]);
+#endif
   // the last workgroup out re-zeroes the counters for the next launch (stream order)
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -393,6 +453,16 @@ __global__ __launch_bounds__(PFT) void proj_x3_kernel(const float* x, int ldx, i
 
 using namespace rg;
 using namespace rg::convx3;
+
+#if RG_CX3_STAMP
+// diagnostic builds only (not in radar_gnn.h): read and clear the phase sums
+extern "C" int rg_debug_cx3_stamps(unsigned long long* out_host) {
+  RG_CHECK_HIP(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_cx3_stamp), sizeof(g_cx3_stamp)));
+  static const unsigned long long z[16] = {0};
+  RG_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_cx3_stamp), z, sizeof(z)));
+  return RG_OK;
+}
+#endif
 
 extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
   return 256 + (size_t)(n_nodes > 0 ? n_nodes : 1) * C * sizeof(float);

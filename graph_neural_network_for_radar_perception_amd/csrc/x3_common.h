@@ -104,15 +104,26 @@ struct WMix {
 // MTW M-tiles; bop(s, t) returns the split B operand of k-step s, row tile t.  Per k-step
 // the A fragments are issued first and the B operands are split while they arrive; the
 // small terms go first.
-template <int KS, int MT, int MTW, int RT, typename WSrc, typename BOp>
+// DB: the A fragments of k-step s + 1 are issued before the MFMAs of step s (double
+// buffer: MT * 12 more registers, no wait on the fragment loads between k-steps).
+template <int KS, int MT, int MTW, int RT, bool DB = false, typename WSrc, typename BOp>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, int m0, BOp&& bop) {
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    bf16x8_t A[MT][3];
+  bf16x8_t Ab[DB ? 2 : 1][MT][3];
+  auto lda = [&](int s, bf16x8_t (&d)[MT][3]) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) A[m][p] = W(p, ((m0 + m) * KS + s) * 1024);
+      for (int p = 0; p < 3; ++p) d[m][p] = W(p, ((m0 + m) * KS + s) * 1024);
+  };
+  if constexpr (DB) lda(0, Ab[0]);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if constexpr (DB) {
+      if (s + 1 < KS) lda(s + 1, Ab[(s + 1) & 1]);
+    } else {
+      lda(s, Ab[0]);
+    }
+    const bf16x8_t(&A)[MT][3] = Ab[DB ? (s & 1) : 0];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const X3 b = bop(s, t);
@@ -133,43 +144,51 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
   }
 }
 // one row tile
-template <int KS, int MT, int MTW, typename WSrc, typename BOp>
+template <int KS, int MT, int MTW, bool DB = false, typename WSrc, typename BOp>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[MT], const WSrc& W, int m0, BOp&& bop) {
-  layer_x3<KS, MT, MTW, 1>(*reinterpret_cast<f32x16(*)[1][MT]>(&acc), W, m0,
-                           [&](int s, int) { return bop(s); });
+  layer_x3<KS, MT, MTW, 1, DB>(*reinterpret_cast<f32x16(*)[1][MT]>(&acc), W, m0,
+                               [&](int s, int) { return bop(s); });
 }
 
-// channel_normalization (common.py:208-220) + LeakyReLU (common.py:256-267, constants.py:10)
-// in five f32 ops per feature: sum, x - mean, sum of squares, y' = x a + b with the 0.505
-// of leaky(y) = 0.505 y + 0.495 |y| folded into a and b, then |y'| C + y'
 static constexpr float X3_NORM_EPS = 1e-5f;  // constants.py:9
 static constexpr float X3_LEAKY_PRE = 0.505f;
 static constexpr float X3_LEAKY_C = 0.495f / 0.505f;
 
+// row statistics of channel_normalization over the 32 MT features of a lane pair: eight
+// independent partial sums per statistic (short dependent chains: the epilogue sits on the
+// critical path between two layers), then one v_permlane32_swap each.  1 / (std + eps)
+// from the hardware sqrt and reciprocal (~1 ulp each, 2e-7 relative on the scale; the
+// float32 MFMA path keeps the correctly rounded sequences).
+template <int MT>
+__device__ __forceinline__ float2 row_stats(f32x16 (&acc)[MT]) {
+  constexpr int N = 32 * MT;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s[q & 7] += acc[m][q];
+  const float mean =
+      add_xor32(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * (1.f / N);
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc[m][q] -= mean;
+      v[q & 7] = fmaf(acc[m][q], acc[m][q], v[q & 7]);
+    }
+  const float ss = add_xor32(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+  const float inv =
+      __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
+  return make_float2(mean, inv);
+}
+
+// channel_normalization (common.py:208-220) + LeakyReLU (common.py:256-267, constants.py:10):
+// after the statistics, two fmas per feature -- y' = x a + b with the 0.505 of
+// leaky(y) = 0.505 y + 0.495 |y| folded into a and b, then |y'| C + y'
 template <int MT>
 __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
-  constexpr int N = 32 * MT;
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      s0 += acc[m][q];
-      s1 += acc[m][q + 1];
-    }
-  const float mean = add_xor32(s0 + s1) * (1.f / N);
-  float q0 = 0.f, q1 = 0.f;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      acc[m][q] -= mean;
-      acc[m][q + 1] -= mean;
-      q0 = fmaf(acc[m][q], acc[m][q], q0);
-      q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
-    }
-  const float ss = add_xor32(q0 + q1);
-  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + X3_NORM_EPS);
+  const float inv = row_stats<MT>(acc).y;  // acc now centred
   const float ga = X3_LEAKY_PRE * (sd * inv), gb = X3_LEAKY_PRE * mu;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -180,32 +199,10 @@ __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd
     }
 }
 
-// channel_normalization without activation / with a general activation
+// channel_normalization without activation
 template <int MT>
 __device__ __forceinline__ void norm_only(f32x16 (&acc)[MT], float mu, float sd) {
-  constexpr int N = 32 * MT;
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      s0 += acc[m][q];
-      s1 += acc[m][q + 1];
-    }
-  const float mean = add_xor32(s0 + s1) * (1.f / N);
-  float q0 = 0.f, q1 = 0.f;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int q = 0; q < 16; q += 2) {
-      acc[m][q] -= mean;
-      acc[m][q + 1] -= mean;
-      q0 = fmaf(acc[m][q], acc[m][q], q0);
-      q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
-    }
-  const float ss = add_xor32(q0 + q1);
-  const float inv = 1.f / (sqrtf(ss / (float)(N - 1)) + X3_NORM_EPS);
-  const float ga = sd * inv;
+  const float ga = sd * row_stats<MT>(acc).y;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
