@@ -31,9 +31,14 @@ enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused
        IN_DENSE = 1,   // float32 rows, K0 % 16 == 0
        IN_PAIR = 2 };  // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
 
-constexpr int spec(int norm_mask, int act_mask) { return norm_mask | (act_mask << 8); }
+// SPEC: bit l = layer l normalised, bit 8 + l = activated (LeakyReLU), bit 16 = every
+// normalised layer packed centred (RG_LAYER_CENTERED)
+constexpr int spec(int norm_mask, int act_mask, bool centred = false) {
+  return norm_mask | (act_mask << 8) | (centred ? 1 << 16 : 0);
+}
 constexpr bool sp_norm(int sp, int l) { return ((sp >> l) & 1) != 0; }
 constexpr bool sp_act(int sp, int l) { return ((sp >> (8 + l)) & 1) != 0; }
+constexpr bool sp_cent(int sp) { return ((sp >> 16) & 1) != 0; }
 constexpr int lmask(int m, int l) { return (m >> (3 * l)) & 7; }
 
 template <int K0, int... Ns>
@@ -103,9 +108,9 @@ __device__ __forceinline__ Src<LM, l> src_of(const Args& a, const char* lds, int
 template <int SPEC, int l, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const float* nrm) {
   if constexpr (sp_norm(SPEC, l) && sp_act(SPEC, l)) {
-    norm_leaky<MT>(acc, nrm[2 * l], nrm[2 * l + 1]);
+    norm_leaky<MT, sp_cent(SPEC)>(acc, nrm[2 * l], nrm[2 * l + 1]);
   } else if constexpr (sp_norm(SPEC, l)) {
-    norm_only<MT>(acc, nrm[2 * l], nrm[2 * l + 1]);
+    norm_only<MT, sp_cent(SPEC)>(acc, nrm[2 * l], nrm[2 * l + 1]);
   } else if constexpr (sp_act(SPEC, l)) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -389,16 +394,21 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   constexpr int EFT = RG_X3_ENC_RT == 2 ? 256 : 512;
   // edge encoder 7 -> 256 -> 128 -> 128 -> 64 (gnn_blocks.py:19-42, block 0 without norm):
   // LDS = layer 0 + planes 0, 1 of layer 1
-  RG_X3C(IN_SMALL, 7, spec(0b1110, 0b1111), 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 128, 64)
+  // (each shape twice: normalised layers packed centred -- the engine's choice -- or not)
+#define RG_X3C2(MODE, K0, NM, AM, LM, RT, FT, ...)                      \
+  RG_X3C(MODE, K0, spec(NM, AM, true), LM, RT, FT, __VA_ARGS__)         \
+  RG_X3C(MODE, K0, spec(NM, AM, false), LM, RT, FT, __VA_ARGS__)
+  RG_X3C2(IN_SMALL, 7, 0b1110, 0b1111, 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 128, 64)
   // node encoder 6 -> 256 -> 128 -> 64
-  RG_X3C(IN_SMALL, 6, spec(0b110, 0b111), 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 64)
+  RG_X3C2(IN_SMALL, 6, 0b110, 0b111, 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 64)
   // task heads: 3-block stem + FFN_TaskSpecificHead (ffn + bare Linear -> 7 / 2, padded)
-  RG_X3C(IN_DENSE, 64, spec(0b1111, 0b1111), ALL, 1, 512, 64, 64, 64, 64, 32)
-  RG_X3C(IN_PAIR, 64, spec(0b1111, 0b1111), ALL, 1, 512, 64, 64, 64, 64, 32)
+  RG_X3C2(IN_DENSE, 64, 0b1111, 0b1111, ALL, 1, 512, 64, 64, 64, 64, 32)
+  RG_X3C2(IN_PAIR, 64, 0b1111, 0b1111, ALL, 1, 512, 64, 64, 64, 64, 32)
   // link edge_formation stem (1 block), object-class stem (3 blocks), object head
-  RG_X3C(IN_DENSE, 64, spec(0b1, 0b1), ALL, 1, 512, 64)
-  RG_X3C(IN_DENSE, 64, spec(0b111, 0b111), ALL, 1, 512, 64, 64, 64)
-  RG_X3C(IN_DENSE, 64, spec(0b01, 0b01), ALL, 1, 512, 64, 32)
+  RG_X3C2(IN_DENSE, 64, 0b1, 0b1, ALL, 1, 512, 64)
+  RG_X3C2(IN_DENSE, 64, 0b111, 0b111, ALL, 1, 512, 64, 64, 64)
+  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, 512, 64, 32)
+#undef RG_X3C2
 #undef RG_X3C
   return RG_ERR_UNSUPPORTED;
 }
@@ -435,7 +445,7 @@ extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, 
   for (int l = 0; l < n_layers; ++l) {
     const rg_layer& s = layers[l];
     RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_x3: layer %d weights", l);
-    if (s.save_pre || s.save_out || (s.flags & RG_LAYER_CENTERED)) return RG_ERR_UNSUPPORTED;
+    if (s.save_pre || s.save_out) return RG_ERR_UNSUPPORTED;
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
     RG_REQUIRE(l == 0 ? s.in_dim == w0 : s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG,
                "rg_mlp_chain_x3: layer %d width", l);
@@ -449,7 +459,12 @@ extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, 
     a.L[l].mu = s.norm_mu;
     a.L[l].sd = s.norm_std;
   }
-  k.sp = spec(nm, am);
+  // every normalised layer centred, or none (an un-normalised layer's flag is irrelevant)
+  int cm = 0;
+  for (int l = 0; l < n_layers; ++l)
+    if (layers[l].norm_mu && (layers[l].flags & RG_LAYER_CENTERED)) cm |= 1 << l;
+  if (cm != 0 && cm != nm) return RG_ERR_UNSUPPORTED;
+  k.sp = spec(nm, am, cm != 0);
   a.rows = rows;
   a.rows_dev = rows_dev;
   a.in0 = in0;

@@ -65,7 +65,14 @@ __device__ unsigned long long g_cx3_stamp[16];
 #define STAMP(i) do {} while (0)
 #endif
 static constexpr int NXCD = 8;
-static constexpr int FT = 512;    // 8 waves: two per SIMD
+#ifndef RG_CX3_FT
+#define RG_CX3_FT 512
+#endif
+#ifndef RG_CX3_RPF
+#define RG_CX3_RPF 0  // the next tile's P / Q / e rows prefetched (160 registers: one wave
+                      // per SIMD, RG_CX3_FT = 256)
+#endif
+static constexpr int FT = RG_CX3_FT;  // 512: two waves per SIMD
 static constexpr int NW = FT / 64;
 static constexpr int TR = 16;     // message rows per LDS transposition pass
 static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
@@ -134,6 +141,7 @@ struct Args {
   int aggr_mean;
 };
 
+template <bool CENT>
 __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[6];
@@ -187,29 +195,55 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     STAMP(0);  // block fetch
     float run = 0.f;  // lane = feature: running sum of the current destination
     int cur = -1;     // its slot (wave-uniform)
-    int pn = min(e0 + r, e1 - 1);
-    int dn = e0 < e1 ? a.dst[pn] : 0, sn = e0 < e1 ? a.src[pn] : 0;
-    f32x4 en[8];  // the next tile's e rows (k = 16 s + 8 h + 0..7 at [2 s], [2 s + 1])
-    auto load_e = [&](int q, f32x4 (&dst)[8]) {
+    // one tile's gathered rows: P[dst] and Q[src] in accumulator order (features
+    // 32m + 8g + 4h .. +3 at [4m + g]), e[edge] in k order (16 s + 8 h .. +3, +4 .. +7 at
+    // [2s], [2s + 1])
+    struct Rows {
+      f32x4 p[16], q[16], e[8];
+    };
+    auto load_rows = [&](int q, int dq, int sq, Rows& w) {
+      const float* pp = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : dq) * PQW + 4 * h;
+      const float* pqq = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : sq) * PQW + HID + 4 * h;
       const float* pe = a.e + (size_t)q * a.lde + 8 * h;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        dst[2 * s] = *(const f32x4*)(pe + 16 * s);
-        dst[2 * s + 1] = *(const f32x4*)(pe + 16 * s + 4);
+      for (int i = 0; i < 16; ++i) w.p[i] = *(const f32x4*)(pp + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w.q[i] = *(const f32x4*)(pqq + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
+        w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
       }
     };
-    if (e0 < e1) load_e(pn, en);
+    // tile indices (past the block's last edge clamped: a re-read of a cached row)
+    auto tile_idx = [&](int t, int& q, int& dq, int& sq) {
+      q = min(t + r, e1 - 1);
+      dq = a.dst[q];
+      sq = a.src[q];
+    };
+    int p1 = 0, d1 = 0, s1 = 0, p2 = 0, d2 = 0, s2 = 0;
+    Rows nrows;
+    if (e0 < e1) {
+      tile_idx(e0, p1, d1, s1);
+      if constexpr (RG_CX3_RPF) {  // rows of tile 0 now, indices of tile 1
+        load_rows(p1, d1, s1, nrows);
+        tile_idx(e0 + 32, p2, d2, s2);
+      }
+    }
     for (int t0 = e0; t0 < e1; t0 += 32) {
-      const int d = dn, sj = sn;
-      X3 eb[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) eb[s] = split8(en[2 * s], en[2 * s + 1]);
-      // the next tile's indices and e rows now: their latency hides behind this tile (past
-      // the block's last edge the clamped index re-reads a row already in cache)
-      pn = min(t0 + 32 + r, e1 - 1);
-      dn = a.dst[pn];
-      sn = a.src[pn];
-      load_e(pn, en);
+      const int d = d1;
+      Rows rw;
+      if constexpr (RG_CX3_RPF) {
+        // rows of the next tile now (indices loaded one tile earlier), indices of the tile
+        // after: the whole gather latency hides behind this tile
+        rw = nrows;
+        load_rows(p2, d2, s2, nrows);
+        p1 = p2; d1 = d2; s1 = s2;
+        tile_idx(t0 + 64, p2, d2, s2);
+      } else {
+        load_rows(p1, d1, s1, rw);
+        tile_idx(t0 + 32, p1, d1, s1);  // the next tile's indices (latency behind this tile)
+      }
       // destination-change mask of this tile's edges (bit j: edge t0 + j starts a segment)
       const int dprev = __shfl_up(d, 1, 64);
       const uint32_t smask =
@@ -217,41 +251,24 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           (e1 - t0 >= 32 ? 0xffffffffu : ((1u << (e1 - t0)) - 1u));
       // ---- layer 1: h = P[dst] + Q[src] + W_e e
       f32x16 acc1[4];
-      {
-        const float* pp = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : d) * PQW + 4 * h;
-        const float* pq = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : sj) * PQW + HID + 4 * h;
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+      for (int m = 0; m < 4; ++m)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 pv = *(const f32x4*)(pp + 32 * m + 8 * g);
-            acc1[m][4 * g + 0] = pv.x;
-            acc1[m][4 * g + 1] = pv.y;
-            acc1[m][4 * g + 2] = pv.z;
-            acc1[m][4 * g + 3] = pv.w;
-          }
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 qv = *(const f32x4*)(pq + 32 * m + 8 * g);
-            acc1[m][4 * g + 0] += qv.x;
-            acc1[m][4 * g + 1] += qv.y;
-            acc1[m][4 * g + 2] += qv.z;
-            acc1[m][4 * g + 3] += qv.w;
-          }
-      }
+          for (int t = 0; t < 4; ++t) acc1[m][4 * g + t] = rw.p[4 * m + g][t] + rw.q[4 * m + g][t];
       {
         if constexpr (RG_CX3_EXP != 5) {
-          layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0, [&](int s) { return eb[s]; });
+          layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0,
+                                        [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
         } else {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
-            acc1[s][0] += xor_first(eb[s]);
+            acc1[s][0] += xor_first(split8(rw.e[2 * s], rw.e[2 * s + 1]));
         }
       }
       STAMP(1);  // gathers + layer 1 issue
-      if constexpr (RG_CX3_EXP != 1) norm_leaky<4>(acc1, mu0, sd0);
+      if constexpr (RG_CX3_EXP != 1) norm_leaky<4, CENT>(acc1, mu0, sd0);
       STAMP(2);  // norm 1 (waits for layer 1)
       // ---- layer 2 (B operand = layer 1's accumulators)
       f32x16 acc2[2];
@@ -267,7 +284,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         }
       }
       STAMP(3);  // layer 2 issue
-      if constexpr (RG_CX3_EXP != 1) norm_leaky<2>(acc2, mu1, sd1);
+      if constexpr (RG_CX3_EXP != 1) norm_leaky<2, CENT>(acc2, mu1, sd1);
       STAMP(4);  // norm 2
       if constexpr (RG_CX3_EXP == 2) {
 #pragma unroll
@@ -359,7 +376,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     layer_x3<8, 2, 2, true>(accu, wU, 0, [&](int s) {
       return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
     });
-    norm_leaky<2>(accu, muU, sdU);
+    norm_leaky<2, CENT>(accu, muU, sdU);
     STAMP(6);  // update loads + layer
     {
       const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
@@ -499,7 +516,10 @@ extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq,
   if (aggr != RG_REDUCE_SUM && aggr != RG_REDUCE_MEAN) return RG_ERR_UNSUPPORTED;
   if (!m0.norm_mu || !m1.norm_mu || !u.norm_mu) return RG_ERR_UNSUPPORTED;
   if (m0.act != ACT_LEAKY || m1.act != ACT_LEAKY || u.act != ACT_LEAKY) return RG_ERR_UNSUPPORTED;
-  if ((m0.flags | m1.flags | u.flags) & RG_LAYER_CENTERED) return RG_ERR_UNSUPPORTED;
+  // centred (RG_LAYER_CENTERED) on all three normalised layers -- and then on the
+  // projections, which are msg0's other columns -- or on none
+  const int cent = m0.flags & m1.flags & u.flags & RG_LAYER_CENTERED;
+  if (!cent && ((m0.flags | m1.flags | u.flags) & RG_LAYER_CENTERED)) return RG_ERR_UNSUPPORTED;
   RG_REQUIRE(!next_pq == !pq_out, RG_ERR_ARG, "rg_conv_layer_x3: next_pq and pq_out go together");
   RG_REQUIRE(!next_pq || (next_pq->in_dim == C && next_pq->out_dim == PQW && !next_pq->norm_mu &&
                           next_pq->act == RG_ACT_NONE),
@@ -542,8 +562,13 @@ extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq,
   const int need = (a.n_blocks + NW - 1) / NW;
   if (blocks > need) blocks = need;
   if (blocks < NXCD) blocks = NXCD;
-  RG_ENSURE_LDS(conv_x3_kernel, LDS_BYTES);
-  conv_x3_kernel<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
+  if (cent) {
+    RG_ENSURE_LDS(conv_x3_kernel<true>, LDS_BYTES);
+    conv_x3_kernel<true><<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
+  } else {
+    RG_ENSURE_LDS(conv_x3_kernel<false>, LDS_BYTES);
+    conv_x3_kernel<false><<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -558,7 +558,7 @@ extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
 
 // RG_PACK_X3: three planes of one RG_PACK_FAST_* format
 static int pack_x3(const float* weight, const float* bias, int in_dim, int out_dim, int fmt,
-                   void* packed, hipStream_t st) {
+                   int center, void* packed, hipStream_t st) {
   RG_REQUIRE(fmt == RG_PACK_FAST_IN || fmt == RG_PACK_FAST_CHAIN || fmt == RG_PACK_FAST_UPD,
              RG_ERR_ARG, "rg_pack_linear: RG_PACK_X3 applies to the RG_PACK_FAST_* formats");
   const int ks = (in_dim + 15) / 16;
@@ -568,10 +568,11 @@ static int pack_x3(const float* weight, const float* bias, int in_dim, int out_d
   const size_t fb = frag_bytes(in_dim, out_dim, fmt);
   const long total = (long)fb / sizeof(uint16_t);
   for (int p = 0; p < 3; ++p)
-    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps, 0, p,
+    pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
+                                                           center, p,
                                                            (uint16_t*)((char*)packed + p * fb), total);
   const int nb = kpad(out_dim, 32);
-  pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, 0,
+  pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, center,
                                                            (float*)((char*)packed + 3 * fb));
   RG_LAUNCH_CHECK();
   return RG_OK;
@@ -583,9 +584,10 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
              "rg_pack_linear: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
   hipStream_t st = (hipStream_t)stream;
   if (dtype & RG_PACK_X3) {
-    RG_REQUIRE(!(dtype & (RG_PACK_CENTERED | RG_PACK_TRANSPOSE)), RG_ERR_ARG,
-               "rg_pack_linear: RG_PACK_X3 does not combine with CENTERED / TRANSPOSE");
-    return pack_x3(weight, bias, in_dim, out_dim, dtype & ~RG_PACK_X3, packed, st);
+    RG_REQUIRE(!(dtype & RG_PACK_TRANSPOSE), RG_ERR_ARG,
+               "rg_pack_linear: RG_PACK_X3 does not combine with RG_PACK_TRANSPOSE");
+    return pack_x3(weight, bias, in_dim, out_dim, dtype & ~(RG_PACK_X3 | RG_PACK_CENTERED),
+                   (dtype & RG_PACK_CENTERED) ? 1 : 0, packed, st);
   }
   const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
   const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;

@@ -158,37 +158,47 @@ static constexpr float X3_LEAKY_C = 0.495f / 0.505f;
 // independent partial sums per statistic (short dependent chains: the epilogue sits on the
 // critical path between two layers), then one v_permlane32_swap each.  1 / (std + eps)
 // from the hardware sqrt and reciprocal (~1 ulp each, 2e-7 relative on the scale; the
-// float32 MFMA path keeps the correctly rounded sequences).
-template <int MT>
-__device__ __forceinline__ float2 row_stats(f32x16 (&acc)[MT]) {
+// float32 MFMA path keeps the correctly rounded sequences).  CENT: the layer's weights and
+// bias were packed zero-mean over the outputs (RG_LAYER_CENTERED), so the row mean of the
+// pre-activations is zero up to f32 rounding and its pass is skipped -- the normalisation
+// is invariant to the shift, and the centred form avoids the cancellation of x - mean.
+template <int MT, bool CENT>
+__device__ __forceinline__ float row_inv_std(f32x16 (&acc)[MT]) {
   constexpr int N = 32 * MT;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (!CENT) {
+    float s[8];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int i = 0; i < 8; ++i) s[i] = acc[0][i] + acc[0][i + 8];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) s[q & 7] += acc[m][q];
-  const float mean =
-      add_xor32(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * (1.f / N);
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int m = 1; m < MT; ++m)
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+      for (int q = 0; q < 16; ++q) s[q & 7] += acc[m][q];
+    const float mean =
+        add_xor32(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * (1.f / N);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      acc[m][q] -= mean;
-      v[q & 7] = fmaf(acc[m][q], acc[m][q], v[q & 7]);
-    }
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] -= mean;
+  }
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = acc[0][i] * acc[0][i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fmaf(acc[0][i + 8], acc[0][i + 8], v[i]);
+#pragma unroll
+  for (int m = 1; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q & 7] = fmaf(acc[m][q], acc[m][q], v[q & 7]);
   const float ss = add_xor32(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
-  const float inv =
-      __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
-  return make_float2(mean, inv);
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
 }
 
 // channel_normalization (common.py:208-220) + LeakyReLU (common.py:256-267, constants.py:10):
 // after the statistics, two fmas per feature -- y' = x a + b with the 0.505 of
 // leaky(y) = 0.505 y + 0.495 |y| folded into a and b, then |y'| C + y'
-template <int MT>
+template <int MT, bool CENT = false>
 __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
-  const float inv = row_stats<MT>(acc).y;  // acc now centred
+  const float inv = row_inv_std<MT, CENT>(acc);  // acc now centred
   const float ga = X3_LEAKY_PRE * (sd * inv), gb = X3_LEAKY_PRE * mu;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -200,9 +210,9 @@ __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd
 }
 
 // channel_normalization without activation
-template <int MT>
+template <int MT, bool CENT = false>
 __device__ __forceinline__ void norm_only(f32x16 (&acc)[MT], float mu, float sd) {
-  const float ga = sd * row_stats<MT>(acc).y;
+  const float ga = sd * row_inv_std<MT, CENT>(acc);
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll

@@ -301,8 +301,8 @@ class ChainPlan:
         rg_mlp_chain_x3 (lazily)."""
         if self._x3 is None:
             X3 = nat.RG_PACK_X3
-            self._x3buf, groups = self._pack_buffer(
-                lambda i: (nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN) | X3)
+            self._x3buf, groups = self._pack_buffer(lambda i: centered_fmt(
+                self.specs[i], (nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN) | X3))
             self._x3 = groups[0][0]
         return self._x3
 
@@ -640,12 +640,22 @@ class ConvPlan:
         we = LayerSpec(W[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
         specs = [pq, we, m1, u]
         if self.f32_arith == 'x3':
-            X3 = nat.RG_PACK_X3
+            X3, CEN = nat.RG_PACK_X3, nat.RG_PACK_CENTERED
+            # normalised layers packed zero-mean over their outputs (the kernel then skips
+            # the mean pass): msg0 is centred here as a whole -- its x_i, x_j and edge
+            # columns (P, Q, W_e) and its bias -- and msg1 / upd by the packer
+            Wc = W - W.mean(0, keepdim=True)
+            bc = b - b.mean()
+            pq = LayerSpec(torch.cat((Wc[:, :C], Wc[:, C:2 * C]), 0).contiguous(),
+                           torch.cat((bc, torch.zeros_like(bc)), 0).contiguous(), None, None, 'none')
+            we = LayerSpec(Wc[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
+            w_pq, b_pq = pq.weight, pq.bias
             # [0] W_e, [1] msg1, [2] upd (cat(x, agg) read from memory), [3] P | Q from
             # memory (first layer), [4] P | Q from the previous layer's registers
             specs = [we, m1, u, pq, pq]
-            fmts = [nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3, nat.RG_PACK_FAST_IN | X3,
-                    nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3]
+            fmts = [nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3 | CEN,
+                    nat.RG_PACK_FAST_IN | X3 | CEN, nat.RG_PACK_FAST_IN | X3,
+                    nat.RG_PACK_FAST_CHAIN | X3]
         else:
             fmts = [nat.RG_PACK_F32_FAST] * 4
         try:
@@ -656,6 +666,7 @@ class ConvPlan:
         base = self.fused_buf.data_ptr()
         if self.f32_arith == 'x3':
             self.fused_layers = layer_array(specs[:3], base, offs[:3], fmts[:3])
+            self.fused_layers[0].flags = nat.RG_LAYER_CENTERED   # centred on the host
             self.x3_pq_in = layer_array(specs[3:4], base, offs[3:4], fmts[3:4])
             self.x3_pq_chain = layer_array(specs[4:5], base, offs[4:5], fmts[4:5])
             self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_x3_workspace_size(0),
