@@ -40,6 +40,15 @@ struct X3 {
   bf16x8_t p0, p1, p2;
 };
 
+// v_cvt_pk_bf16_f32 (round to nearest even) as an opaque instruction: through the builtin
+// the compiler re-derives each element's bf16 with a second conversion instead of taking
+// it from the packed word (two extra instructions per pair)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // 8 consecutive k values of one row -> the three exact bf16 terms
 __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
   const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -47,13 +56,13 @@ __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float a = v[2 * i], b = v[2 * i + 1];
-    const uint32_t u0 = pack_bf16x2(a, b);
+    const uint32_t u0 = cvt_pk_bf16(a, b);
     const float ra = a - __uint_as_float(u0 << 16), rb = b - __uint_as_float(u0 & 0xffff0000u);
-    const uint32_t u1 = pack_bf16x2(ra, rb);
+    const uint32_t u1 = cvt_pk_bf16(ra, rb);
     const float sa = ra - __uint_as_float(u1 << 16), sb = rb - __uint_as_float(u1 & 0xffff0000u);
     w0[i] = u0;
     w1[i] = u1;
-    w2[i] = pack_bf16x2(sa, sb);
+    w2[i] = cvt_pk_bf16(sa, sb);
   }
   return X3{__builtin_bit_cast(bf16x8_t, w0), __builtin_bit_cast(bf16x8_t, w1),
             __builtin_bit_cast(bf16x8_t, w2)};
