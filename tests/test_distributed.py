@@ -6,7 +6,8 @@ its own frames, builds and runs them with no data-path collective, and only the 
 same helpers under two gloo processes and check (1) the shards are disjoint and cover
 the single-process frame set, (2) the reductions are the max / sum, and (3) the per-rank
 graphs (oracle restatement, CPU) concatenate to the single-process result, i.e. the
-sharding needs no exchange step.
+sharding needs no exchange step.  On a GPU box, test_frame_sharding_two_ranks_hip_pipeline
+runs the same sharding with the product HIP pipeline on every rank.
 """
 import os
 import socket
@@ -30,7 +31,7 @@ def _free_port():
 
 def _worker(rank, world, port, frames, nodes, out_dir):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
-                      RANK=str(rank), LOCAL_RANK=str(rank))
+                      RANK=str(rank), LOCAL_RANK=str(rank), RG_BENCH_BACKEND='gloo')
     import bench
     from graph_neural_network_for_radar_perception_amd import synthetic
     from oracle import graph_features_ref as gref
@@ -106,3 +107,64 @@ def test_gradient_allreduce_two_ranks_gloo(tmp_path):
         np.testing.assert_array_equal(d['g'], want)
         assert float(d['scale']) == 0.5
         np.testing.assert_array_equal(d['p'], np.zeros(4, np.float32))
+
+
+def _hip_worker(rank, world, port, frames, nodes, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), RG_BENCH_BACKEND='gloo')
+    import bench
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+    w, r, _ = bench.setup_dist()           # one process per "GPU" (both share cuda:0 here)
+    dev = torch.device('cuda', torch.cuda.current_device())
+    cfg = default_config()
+    model = bench.make_model(cfg, dev, bench.model_state(cfg, 'trained'))
+    seeds = bench.rank_frame_seeds(rank, frames, synthetic.SEED0)
+    fr = [synthetic.make_frame(nodes, s) for s in seeds]
+    cl = [synthetic.cluster_lists(nodes) for _ in seeds]
+    batch = FrameBatch.from_frames(fr, cl, device=dev)
+    with torch.no_grad():
+        gb, out = RadarGNNPipeline(model, cfg, 'fp32').step(batch)
+    torch.cuda.synchronize()
+    bench.barrier(w)
+    total = bench.sum_over_ranks(float(len(seeds)), w)
+    np.savez(os.path.join(out_dir, f'hip{rank}.npz'), seeds=np.array(seeds),
+             node_cls=out.node_cls.cpu().numpy(), node_reg=out.node_reg.cpu().numpy(),
+             n_edges=int(gb.n_edges_dev.item()), total=total)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_frame_sharding_two_ranks_hip_pipeline(tmp_path, cuda_device):
+    """bench.py's multi-rank path with the PRODUCT pipeline on every rank: two processes
+    (gloo for the bookkeeping collectives, both on the one card of the test box), each
+    building and running its own frames through the HIP graph build + fp32 forward.  The
+    ranks' outputs, concatenated, equal one process running all frames: frame sharding
+    needs no data-path exchange, and the batched union is exact per frame."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+    import bench
+    world, frames, nodes = 2, 3, 700
+    mp.spawn(_hip_worker, args=(world, _free_port(), frames, nodes, str(tmp_path)),
+             nprocs=world, join=True)
+    res = [np.load(tmp_path / f'hip{r}.npz') for r in range(world)]
+    seeds = np.concatenate([x['seeds'] for x in res])
+    assert len(set(seeds.tolist())) == world * frames
+    assert all(float(x['total']) == world * frames for x in res)
+    dev = cuda_device
+    cfg = default_config()
+    model = bench.make_model(cfg, dev, bench.model_state(cfg, 'trained'))
+    fr = [synthetic.make_frame(nodes, int(s)) for s in seeds]
+    cl = [synthetic.cluster_lists(nodes) for _ in seeds]
+    with torch.no_grad():
+        gb, out = RadarGNNPipeline(model, cfg, 'fp32').step(FrameBatch.from_frames(fr, cl, device=dev))
+    assert int(gb.n_edges_dev.item()) == sum(int(x['n_edges']) for x in res)
+    np.testing.assert_array_equal(np.concatenate([x['node_cls'] for x in res]),
+                                  out.node_cls.cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate([x['node_reg'] for x in res]),
+                                  out.node_reg.cpu().numpy())
