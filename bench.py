@@ -17,8 +17,8 @@ Multi-GPU (torchrun, one process per GPU): every rank owns its own 64 frames
 max-over-ranks timing only).
 
 ``--config c5``: BASELINE config 5 (dense-scene stress): one frame of 20,000 nodes per GPU,
-pure radius graph (compute_ball_query semantics, eps^2 = 2.5 -> E ~ 400k), L = 7; the
-half-precision type is bf16 (the MFMA path has no separate fp16 build).
+pure radius graph (compute_ball_query semantics, eps^2 = 2.5 -> E ~ 400k), L = 7, fp16
+operands (v_mfma_f32_32x32x16_f16, f32 accumulation) as the config names.
 
 Prints ONE JSON line (rank 0).
 """
@@ -42,7 +42,7 @@ from graph_neural_network_for_radar_perception_amd.config import default_config 
 
 METRIC = json.load(open(os.path.join(REPO, 'BASELINE.json')))['metric']
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp32': 157.3}   # dense MFMA peaks (same doc)
+MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense MFMA peaks (same doc)
 
 
 # workloads; k is unused by the pure radius graph
@@ -54,7 +54,7 @@ PRESETS = {
     'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
                cpu_warm=2, dtype='bf16', weights='random'),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
-               cpu_warm=1, dtype='bf16', weights='random'),
+               cpu_warm=1, dtype='fp16', weights='random'),
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
     'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
                cpu_warm=1),
@@ -85,9 +85,9 @@ def parse():
     p.add_argument('--nodes', type=int, default=None)
     p.add_argument('--k', type=int, default=None)
     p.add_argument('--layers', type=int, default=None)
-    p.add_argument('--dtype', default=None, choices=['bf16', 'fp32'],
+    p.add_argument('--dtype', default=None, choices=['bf16', 'fp16', 'fp32'],
                    help='compute dtype (default: the preset\'s -- fp32 for m / c4 / cls, '
-                        'bf16 for c2 / c5)')
+                        'bf16 for c2, fp16 for c5)')
     p.add_argument('--weights', default=None, choices=['trained', 'random'],
                    help='trained: the checkpoint committed in tests/golden (L = 7 only)')
     p.add_argument('--no-extra', action='store_true',
@@ -101,7 +101,7 @@ def parse():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
     if a.dtype is None:
-        a.dtype = 'bf16' if a.config in ('c2', 'c5') else 'fp32'
+        a.dtype = {'c2': 'bf16', 'c5': 'fp16'}.get(a.config, 'fp32')
     if a.weights is None:
         a.weights = 'random'
     return a
@@ -707,7 +707,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
 
     frames_total = sum_over_ranks(args.frames * args.steps, world)
     N = args.frames * args.nodes
-    s = 2 if args.dtype == 'bf16' else 4
+    s = 2 if args.dtype in ('bf16', 'fp16') else 4
     C = 64
     kern = {}
     for name, ms in durs.items():

@@ -21,12 +21,14 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('RG_LIBRARY') or os.path.join(PKG, 'lib', 'libradargnn.so')
 HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 
-RG_F32, RG_BF16 = 0, 1
+RG_F32, RG_BF16, RG_F16 = 0, 1, 6
 RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD, RG_PACK_F32_FAST = 2, 3, 4, 5
 RG_PACK_CENTERED = 0x100
 RG_PACK_TRANSPOSE = 0x200
 RG_PACK_X3 = 0x400
+RG_PACK_F16 = 0x800
 RG_LAYER_CENTERED = 1
+RG_LAYER_F16 = 2
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
 GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2

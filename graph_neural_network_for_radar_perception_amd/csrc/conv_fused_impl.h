@@ -1,0 +1,568 @@
+// Fused residual_graph_conv_block on 16-bit operands: the kernel of conv_fused.hip, compiled
+// once per operand type (RG_HALF_F16 = 0: bf16 in namespace rg::conv; 1: IEEE fp16 in
+// rg::conv_f16).  No include guard: conv_fused.hip includes it twice.
+namespace rg {
+namespace RG_CONV_NS {
+
+using HT = ::rg::H16<RG_HALF_F16 != 0>;  // the 16-bit operand type (bf16 / fp16)
+
+typedef HT::v8 bf16x8_t;  // (named for the bf16 build; fp16 lanes in the fp16 build)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef RG_CONV_PFX
+#define RG_CONV_PFX 0  // 1: the next block's x rows for P are loaded one block ahead
+#endif
+
+#ifndef RG_CONV_CT
+#define RG_CONV_CT 512  // threads per workgroup (8 waves, 2 per SIMD)
+#endif
+static constexpr int CT = RG_CONV_CT;
+static constexpr int CW = CT / 64;
+static constexpr int NB = 8;         // destination nodes per work block
+static constexpr int C = 64;         // node / edge / message / output channels
+static constexpr int HID = 128;      // msg_mlp_hidden_dim
+// wave-private LDS: P (NB x HID f32), message tile (32 x C bf16), slots (32 int)
+static constexpr int WAVE_LDS = NB * HID * 4 + 32 * C * 2 + 128;
+static constexpr float NORM_EPS = 1e-5f;
+
+struct CLayer {
+  int woff, bytes, out, act, centered;
+  const float* mu;
+  const float* sd;
+  const void* src;
+};
+
+struct CArgs {
+  CLayer L[3];  // msg0 (192->128), msg1 (128->64), upd (128->64)
+  int total_bytes;
+  int aggr_mean;
+  int n_nodes;
+  int n_blocks;
+  const uint16_t* x;
+  const uint16_t* e;
+  const int* seg_ptr;
+  const int* src;
+  const int* dst;
+  uint16_t* x_out;
+  int* counter;
+  int ldx, lde, ldo;
+  // optional edge-balanced work blocks (rg_conv_blocks): block b = nodes
+  // [blk_nodes[b], blk_nodes[b + 1]), at most NB, *n_blk_dev blocks; null: b = 8-node run
+  const int* blk_nodes;
+  const int* n_blk_dev;
+};
+
+__device__ __forceinline__ uint32_t bf2(float a, float b) { return HT::pack2(a, b); }
+__device__ __forceinline__ bf16x8_t ld_bf8(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *(const u32x4*)p);
+}
+__device__ __forceinline__ bf16x8_t zero_bf8() {
+  return __builtin_bit_cast(bf16x8_t, (u32x4){0u, 0u, 0u, 0u});
+}
+
+// k-steps [S0, S0 + KS) of a packed 32x32x16 layer with KT k-steps in total
+// (fragment (m, s) at byte (m * KT + s) * 1024); acc holds the initial values.
+// Software pipelined: the A fragments of step s+1 are read from LDS while the MFMAs of
+// step s issue, so an MFMA never waits for the LDS read that feeds it; one scheduling
+// fence per step keeps the compiler from hoisting the whole layer's fragments.
+#ifndef RG_CONV_PFD
+#define RG_CONV_PFD 1  // A-fragment prefetch distance (k-steps) for layers with MT <= 2
+#endif
+
+#ifndef RG_CONV_PFD4
+#define RG_CONV_PFD4 1  // the same for the 4-tile first message layer
+#endif
+
+template <int KS, int MT, int KT, int S0>
+__device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
+                                           int lane) {
+  const char* wl = w + lane * 16;
+  // narrow layers (MT <= 2) issue only MT MFMAs per k-step, less than an LDS round trip:
+  // their fragments are read PD steps ahead (registers: (PD + 1) * MT fragments)
+  constexpr int PD = MT <= 2 ? RG_CONV_PFD : RG_CONV_PFD4;
+  bf16x8_t f[KS][MT];
+#pragma unroll
+  for (int s = 0; s < PD && s < KS; ++s)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) f[s][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s) * 1024));
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + PD < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        f[s + PD][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s + PD) * 1024));
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = HT::mfma(f[s][m], b[s], acc[m]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// channel_normalization (common.py:208-220) + activation (rg_common.h)
+// (every block is normalised; with ACT >= 0 every block uses ACT and was packed
+// RG_PACK_CENTERED: host-checked)
+// (mu, sd = the layer's channel_normalization scalars, staged in LDS once per kernel)
+template <int ACT, int MT>
+__device__ __forceinline__ void norm_act(f32x16 (&acc)[MT], const CLayer& L, float mu, float sd) {
+#ifndef RG_NO_FUSED_LEAKY
+  if constexpr (ACT == ACT_LEAKY) {  // centred (host-checked): norm + leaky in two fmas
+    channel_norm_leaky_centered<MT>(acc, mu, sd, NORM_EPS);
+    return;
+  }
+#endif
+  if constexpr (ACT >= 0) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
+  else if (L.centered) channel_norm_pk_centered<MT>(acc, mu, sd, NORM_EPS);
+  else channel_norm_pk<MT>(acc, mu, sd, NORM_EPS);
+  if constexpr (ACT >= 0) act_pk_all<ACT, MT>(acc);
+  else act_dispatch(L.act, [&](auto A) { act_pk_all<decltype(A)::value, MT>(acc); });
+}
+
+template <int MT>
+__device__ __forceinline__ void pack_acc(const f32x16 (&acc)[MT], bf16x8_t* nb) {
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int q = 8 * hf;
+      nb[2 * m + hf] = __builtin_bit_cast(
+          bf16x8_t, (u32x4){bf2(acc[m][q + 0], acc[m][q + 1]), bf2(acc[m][q + 2], acc[m][q + 3]),
+                            bf2(acc[m][q + 4], acc[m][q + 5]), bf2(acc[m][q + 6], acc[m][q + 7])});
+    }
+}
+
+// XOR swizzle of the 4-feature granules of message-tile row `row` (64 bf16 = 128 B per
+// row).  Row stores (ds_write_b64, lane = row) and transposed reads (ds_read_b64_tr_b16,
+// 4 rows x 8 granules per half-wave) are both bank-conflict free: granule g of row r
+// lives at g ^ swz(r), swz a bijection on 0..15 whose bit 3 differs for rows r, r + 2.
+__device__ __forceinline__ int swz(int row) {
+  return (row & 7) | ((((row >> 1) ^ (row >> 3)) & 1) << 3);
+}
+
+template <int ACT>
+__global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[6];  // (mu, sd) of the three channel_normalizations
+  if (threadIdx.x == 0) {  // static layer indices: a dynamic a.L[i] would copy a to scratch
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      nrm[2 * l] = *a.L[l].mu;
+      nrm[2 * l + 1] = *a.L[l].sd;
+    }
+  }
+  // stage weights (static indices)
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const u32x4* src = (const u32x4*)a.L[l].src;
+    u32x4* dstp = (u32x4*)(lds + a.L[l].woff);
+    const int n = a.L[l].bytes / 16;
+    for (int i = threadIdx.x; i < n; i += CT) dstp[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+#ifdef RG_CONV_PRIO
+  // static priority for the second-dispatched half of the waves (MI355X_MICROARCH.md,
+  // "two waves per SIMD", item 4)
+  if (wave >= CW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+  // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
+  char* wbase = lds + a.total_bytes + wave * WAVE_LDS;
+  float* P = (float*)wbase;
+  uint16_t* tile = (uint16_t*)(wbase + NB * HID * 4);
+  int* slots = (int*)((char*)tile + 32 * C * 2);
+  const char* w0 = lds + a.L[0].woff;
+  const char* w1 = lds + a.L[1].woff;
+  const char* w2 = lds + a.L[2].woff;
+  const float* bias0 = (const float*)(w0 + 4 * 12 * 1024);
+  const float* bias1 = (const float*)(w1 + 2 * 8 * 1024);
+  const float* bias2 = (const float*)(w2 + 2 * 8 * 1024);
+
+  // block ids come from an atomic counter (dynamic balance); the NEXT block's id and
+  // edge range are fetched at the start of the current block, so a block starts with
+  // two dependent global round trips (indices -> rows) instead of four
+  const int n_blocks = a.blk_nodes ? *a.n_blk_dev : a.n_blocks;
+  // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
+  auto block_nodes = [&](int b, int& n0, int& n1) {
+    if (a.blk_nodes) {
+      n0 = a.blk_nodes[b];
+      n1 = a.blk_nodes[b + 1];
+    } else {
+      n0 = b * NB;
+      n1 = min(n0 + NB, a.n_nodes);
+    }
+  };
+  int blk = 0;
+  if (lane == 0) blk = atomicAdd(a.counter, 1);
+  blk = __shfl(blk, 0, 64);
+  int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
+  if (blk < n_blocks) {
+    block_nodes(blk, bn0, bn1);
+    e0 = a.seg_ptr[bn0];
+    e1 = a.seg_ptr[bn1];
+  }
+#if RG_CONV_PFX
+  // x rows of the block's nodes for P, loaded one block ahead (the block start otherwise
+  // waits a full global round trip before its first MFMA)
+  bf16x8_t bxn[4];
+  {
+    const uint16_t* px = a.x + (size_t)min(bn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
+  }
+#endif
+  while (blk < n_blocks) {
+    const int n0 = bn0;
+    const int n1 = bn1;
+    int nxt_raw = 0;
+    if (lane == 0) nxt_raw = atomicAdd(a.counter, 1);
+    f32x16 agg[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
+
+    // ---- edge tiles, software pipelined: while tile t computes, the rows of tile t+1
+    //      (x[src], e) and the indices of tile t+2 are in flight.  The loop is unrolled
+    //      by two with separate A / B registers for rows AND indices, so no loaded value
+    //      is ever copied (a copy would wait for the load and serialise the pipeline).
+    //      Lanes past the end of the block's edges load the last edge (finite data) and
+    //      aggregate into the unused slot 31.
+    struct Idx { int di, sj; };
+    auto load_idx = [&](int t0) {
+      const int p = min(t0 + r, e1 - 1);
+      return Idx{a.dst[p], a.src[p]};
+    };
+    auto load_rows = [&](int t0, const Idx& ix, bf16x8_t (&bb)[8]) {
+      const int p = min(t0 + r, e1 - 1);
+      const uint16_t* pj = a.x + (size_t)ix.sj * a.ldx + 8 * h;
+      const uint16_t* pe = a.e + (size_t)p * a.lde + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bb[s] = ld_bf8(pj + 16 * s);
+        bb[4 + s] = ld_bf8(pe + 16 * s);
+      }
+    };
+    auto compute = [&](const bf16x8_t (&b)[8], int slot, int t0) {
+      const bool valid = t0 + r < e1;
+      f32x16 acc1[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * HID, m, h);
+      mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
+      if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
+      bf16x8_t b2[8];
+      pack_acc<4>(acc1, b2);
+      f32x16 acc2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias1, m, h);
+      mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
+      if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1], nrm[2], nrm[3]);
+      if (RG_CONV_EXP == 3) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) agg[m] += acc2[m];
+        return;
+      }
+      // ---- message tile M -> LDS rows [edge][feature] (8-B stores of 4 features)
+      const int sr = swz(r);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint2 wv;
+          wv.x = bf2(acc2[m][4 * g + 0], acc2[m][4 * g + 1]);
+          wv.y = bf2(acc2[m][4 * g + 2], acc2[m][4 * g + 3]);
+          const int gr = (8 * m + 2 * g + h) ^ sr;
+          *(uint2*)(tile + r * C + 4 * gr) = wv;
+        }
+      if (h == 0) slots[r] = valid ? slot : 31;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
+      // A = M (features x edges) via ds_read_b64_tr_b16: lane 4q+p of each 16-lane
+      // group G addresses row (edge) row0+q, granule col0/4+p; lane i of the group
+      // receives column (feature) col0+i of the 4 rows.
+      const int G = (lane >> 4) & 3, q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        // B = S (k = edge 16s + 8h + j, col = slot r): one-hot bf16
+        const int4 sa = *(const int4*)(slots + 16 * s + 8 * h);
+        const int4 sb = *(const int4*)(slots + 16 * s + 8 * h + 4);
+        const uint32_t one = HT::ONE;
+        u32x4 sv;
+        sv[0] = (sa.x == r ? one : 0u) | ((sa.y == r ? one : 0u) << 16);
+        sv[1] = (sa.z == r ? one : 0u) | ((sa.w == r ? one : 0u) << 16);
+        sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
+        sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
+        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
+        const int row_lo = 16 * s + 8 * (G >> 1) + q4, row_hi = row_lo + 4;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int gcol = 8 * m + 4 * (G & 1) + p4;
+          typedef short v4s __attribute__((ext_vector_type(4)));
+          typedef __attribute__((address_space(3))) v4s lds_v4s;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s*)(tile + row_lo * C + 4 * (gcol ^ swz(row_lo))));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s*)(tile + row_hi * C + 4 * (gcol ^ swz(row_hi))));
+          const bf16x8_t mf = __builtin_bit_cast(
+              bf16x8_t, (short __attribute__((ext_vector_type(8)))){lo[0], lo[1], lo[2], lo[3],
+                                                                  hi[0], hi[1], hi[2], hi[3]});
+          agg[m] = HT::mfma(mf, sf, agg[m]);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    };
+
+    bf16x8_t bA[8], bB[8];
+    Idx iA{0, 0}, iB{0, 0};
+    if (e0 < e1) {
+      iA = load_idx(e0);
+      iB = load_idx(e0 + 32);  // clamped: harmless when the block has one tile
+    }
+    // ---- P[node] = W1[:, x_i part] x[node] + b1 for the block's nodes: the x_i = x[dst]
+    //      third of the message MLP's first layer is the same for every edge into a node,
+    //      so it is computed once per node here instead of once per edge
+    {
+#if RG_CONV_PFX
+      bf16x8_t bx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bx[s] = bxn[s];
+#else
+      const int node = min(n0 + r, n1 - 1);
+      const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
+      bf16x8_t bx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
+#endif
+      f32x16 accp[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
+      // tile 0's rows go out while P is computed (their indices were issued above)
+      if (e0 < e1) load_rows(e0, iA, bA);
+      mfma_steps<4, 4, 12, 0>(bx, accp, w0, lane);
+      if (r < NB) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          f32x4* pw = (f32x4*)(P + r * HID + (2 * m + h) * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pw[q] = (f32x4){accp[m][4 * q], accp[m][4 * q + 1], accp[m][4 * q + 2], accp[m][4 * q + 3]};
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the whole wave
+      __builtin_amdgcn_wave_barrier();
+    }
+
+    const int nxt = __shfl(nxt_raw, 0, 64);
+    int ne0 = 0, ne1 = 0, nn0 = 0, nn1 = 0;
+    if (nxt < n_blocks) {
+      block_nodes(nxt, nn0, nn1);
+      ne0 = a.seg_ptr[nn0];
+      ne1 = a.seg_ptr[nn1];
+    }
+#if RG_CONV_PFX
+    {
+      const uint16_t* px = a.x + (size_t)min(nn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
+    }
+#endif
+
+    // The next tile's rows and the tile after's indices are loaded UNCONDITIONALLY
+    // (clamped to the block's last edge: past the end every lane reads one row): a load
+    // under a branch leaves the compiler unsure how many loads are in flight at the
+    // join, and it then waits for the freshly issued prefetch before this tile's MFMAs.
+    if (e0 < e1) {
+      for (int t0 = e0;;) {
+        const int slotA = iA.di - n0;
+        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iB, bB);
+        iA = load_idx(t0 + 64);
+        compute(bA, slotA, t0);
+        t0 += 32;
+        if (t0 >= e1) break;
+        const int slotB = iB.di - n0;
+        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iA, bA);
+        iB = load_idx(t0 + 64);
+        compute(RG_CONV_EXP != 1 ? bB : bA, slotB, t0);
+        t0 += 32;
+        if (t0 >= e1) break;
+      }
+    }
+    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
+    const int node = n0 + r;
+    const bool nvalid = r < NB && node < n1;
+    if (a.aggr_mean) {
+      // PyG mean: sum / max(count, 1)
+      const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
+      const float cnt = (float)(deg > 0 ? deg : 1);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) agg[m][q] = div_rn(agg[m][q], cnt);
+    }
+    bf16x8_t bu[8];
+    const uint16_t* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bu[s] = ld_bf8(px + 16 * s);
+    pack_acc<2>(agg, bu + 4);
+    f32x16 accu[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(bias2, m, h);
+    mfma_steps<8, 2, 8, 0>(bu, accu, w2, lane);
+    norm_act<ACT, 2>(accu, a.L[2], nrm[4], nrm[5]);
+    if (nvalid) {
+      uint16_t* po = a.x_out + (size_t)node * a.ldo;
+      const uint16_t* pr = a.x + (size_t)node * a.ldx;
+      // all residual loads first: interleaved with the stores, each load would wait
+      // for the previous store (possible aliasing) -- eight serial round trips
+      uint2 rv[2][4];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) rv[m][g] = *(const uint2*)(pr + 32 * m + 8 * g + 4 * h);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int f0 = 32 * m + 8 * g + 4 * h;
+          const uint2 r2 = rv[m][g];
+          const float v0 = __fadd_rn(HT::lo(r2.x), accu[m][4 * g + 0]);
+          const float v1 = __fadd_rn(HT::hi(r2.x), accu[m][4 * g + 1]);
+          const float v2 = __fadd_rn(HT::lo(r2.y), accu[m][4 * g + 2]);
+          const float v3 = __fadd_rn(HT::hi(r2.y), accu[m][4 * g + 3]);
+          uint2 o;
+          o.x = bf2(v0, v1);
+          o.y = bf2(v2, v3);
+          *(uint2*)(po + f0) = o;
+        }
+    }
+    blk = nxt;
+    e0 = ne0;
+    e1 = ne1;
+    bn0 = nn0;
+    bn1 = nn1;
+  }
+  // the last workgroup out re-zeroes the block counter for the next launch (no memset
+  // per layer: each cost a ~10 us stream gap).  Every wave's final counter atomic has
+  // returned before its workgroup reaches the barrier, so when `done` reaches the grid
+  // size no workgroup can touch the counter again.
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(a.counter + 1, 1) == (int)gridDim.x - 1) {
+      atomicExch(a.counter, 0);
+      atomicExch(a.counter + 1, 0);
+    }
+  }
+}
+
+// Edge-balanced work blocks: each run of NB nodes is split at node boundaries wherever
+// its running edge count would pass `cap` (a single node is never split), so no work
+// block holds many more edges than the mean share of a wave.  cap = max(CAP_MIN, E / 4096)
+// (4096 = two blocks per wave of the 256 x 8-wave grid): a 20 000-node radius frame
+// (~160 edges per 8 nodes, hubs of ~100) is cut to ~4-tile blocks, while a C2 batch
+// (~300 edges per 8 nodes, cap 1 778) keeps its 8-node runs.
+static constexpr int CAP_MIN = 128;
+
+__device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes) {
+  return max(CAP_MIN, seg_ptr[n_nodes] / 4096);
+}
+
+template <bool EMIT>
+__global__ void conv_blocks_kernel(const int* __restrict__ seg_ptr, int n_nodes,
+                                   int* __restrict__ cnt, const int* __restrict__ off,
+                                   int* __restrict__ blk_nodes) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb8 = (n_nodes + NB - 1) / NB;
+  if (b >= nb8) return;
+  const int cap = block_cap(seg_ptr, n_nodes);
+  const int n0 = b * NB, n1 = min(n0 + NB, n_nodes);
+  int c = 0, acc = 0, o = EMIT ? off[b] : 0;
+  for (int n = n0; n < n1; ++n) {
+    const int d = seg_ptr[n + 1] - seg_ptr[n];
+    if (n == n0 || (acc > 0 && acc + d > cap)) {
+      if (EMIT) blk_nodes[o + c] = n;
+      ++c;
+      acc = 0;
+    }
+    acc += d;
+  }
+  if (!EMIT) cnt[b] = c;
+  if (EMIT && b == nb8 - 1) blk_nodes[o + c] = n_nodes;  // sentinel
+}
+
+// the C-ABI entry of this operand type (rg_conv_layer_fused_blocks dispatches on RG_LAYER_F16)
+static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_layer,
+                                          int aggr, const void* x, int ldx, const void* e,
+                                          int lde, const int* seg_ptr, const int* src,
+                                          const int* dst, int n_nodes, void* x_out, int ld_out,
+                                          const int* blk_nodes, const int* n_blocks_dev,
+                                          void* workspace, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const rg_layer& m0 = msg_layers[0];
+  const rg_layer& m1 = msg_layers[1];
+  const rg_layer& u = *upd_layer;
+  if (!(m0.in_dim == 3 * C && m0.out_dim == HID && m1.in_dim == HID && m1.out_dim == C &&
+        u.in_dim == 2 * C && u.out_dim == C))
+    return RG_ERR_UNSUPPORTED;
+  if (aggr != RG_REDUCE_SUM && aggr != RG_REDUCE_MEAN) return RG_ERR_UNSUPPORTED;
+  if (!m0.norm_mu || !m1.norm_mu || !u.norm_mu) return RG_ERR_UNSUPPORTED;  // norm assumed
+  RG_REQUIRE(ldx % 8 == 0 && lde % 8 == 0 && ld_out % 8 == 0, RG_ERR_UNSUPPORTED,
+             "rg_conv_layer_fused: strides must be multiples of 8");
+  RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_fused: x_out must not alias x");
+  CArgs a;
+  memset(&a, 0, sizeof(a));
+  const rg_layer* ls[3] = {&m0, &m1, &u};
+  const int fmts[3] = {RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD};
+  int off = 0;
+  for (int l = 0; l < 3; ++l) {
+    a.L[l].src = ls[l]->w_packed;
+    a.L[l].mu = ls[l]->norm_mu;
+    a.L[l].sd = ls[l]->norm_std;
+    a.L[l].woff = off;
+    a.L[l].bytes = (int)rg_packed_linear_bytes(ls[l]->in_dim, ls[l]->out_dim, fmts[l]);
+    a.L[l].out = ls[l]->out_dim;
+    a.L[l].act = ls[l]->act;
+    a.L[l].centered = (ls[l]->flags & RG_LAYER_CENTERED) ? 1 : 0;
+    off += (a.L[l].bytes + 15) & ~15;
+  }
+  a.total_bytes = off;
+  a.aggr_mean = aggr == RG_REDUCE_MEAN;
+  a.n_nodes = n_nodes;
+  a.n_blocks = (n_nodes + NB - 1) / NB;
+  a.x = (const uint16_t*)x;
+  a.e = (const uint16_t*)e;
+  a.seg_ptr = seg_ptr;
+  a.src = src;
+  a.dst = dst;
+  a.x_out = (uint16_t*)x_out;
+  a.counter = (int*)workspace;  // [0] next block, [1] workgroups done: zero between launches
+  a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
+  RG_REQUIRE((blk_nodes == nullptr) == (n_blocks_dev == nullptr), RG_ERR_ARG,
+             "rg_conv_layer_fused_blocks: block table and count go together");
+  a.blk_nodes = blk_nodes;
+  a.n_blk_dev = n_blocks_dev;
+  if (n_nodes <= 0) return RG_OK;
+  const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
+  RG_REQUIRE(lds <= DYN_LDS_MAX, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
+  // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
+  // blocks selects the compile-time variant; anything else dispatches per layer
+  const bool leaky = m0.act == ACT_LEAKY && m1.act == ACT_LEAKY && u.act == ACT_LEAKY &&
+                     (m0.flags & m1.flags & u.flags & RG_LAYER_CENTERED);
+  auto kern = leaky ? fused_conv_kernel<ACT_LEAKY> : fused_conv_kernel<-1>;
+  RG_ENSURE_LDS(kern, DYN_LDS_MAX);
+  int blocks = 256;  // a block table has at least ceil(N / NB) entries
+  if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
+  kern<<<blocks, CT, lds, st>>>(a);
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) {
+    // a launch that did not run leaves the counters as they were; one that failed part
+    // way could leave them nonzero: re-zero so the next launch does not skip blocks
+    (void)hipMemsetAsync(workspace, 0, 2 * sizeof(int), st);
+    set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__, hipGetErrorString(le));
+    return RG_ERR_HIP;
+  }
+  return RG_OK;
+}
+
+}  // namespace RG_CONV_NS
+}  // namespace rg

@@ -133,8 +133,10 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
 //           offset by in/2 (aggregate from accumulators): the fused conv layer's update
 // plane p > 0 (RG_PACK_X3): the p-th bf16 term of the exact three-term split of each
 // weight, w = bf16(w) + bf16(w - w0) + bf16(w - w0 - w1) (conv_x3.hip)
+// f16 (RG_PACK_F16): IEEE fp16 fragments instead of bf16
 __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, int mem_steps,
-                                 int center, int plane, uint16_t* __restrict__ P, long total) {
+                                 int center, int plane, int f16, uint16_t* __restrict__ P,
+                                 long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S = (in + 15) / 16;
@@ -159,7 +161,7 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
     }
   }
   for (int q = 0; q < plane; ++q) v -= bf16_to_f32(f32_to_bf16(v));  // exact residues
-  P[t] = f32_to_bf16(v);
+  P[t] = f16 ? f32_to_f16(v) : f32_to_bf16(v);
 }
 
 // RG_PACK_F32_FAST: [m][s4][lane][4] = W[32m + (lane&31)][8 s4 + 4 (lane>>5) + u]; the k
@@ -553,7 +555,7 @@ static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
 using namespace rg;
 
 extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
-  return packed_bytes(in_dim, out_dim, dtype & ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE));
+  return packed_bytes(in_dim, out_dim, dtype & ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE | RG_PACK_F16));
 }
 
 // RG_PACK_X3: three planes of one RG_PACK_FAST_* format
@@ -569,7 +571,7 @@ static int pack_x3(const float* weight, const float* bias, int in_dim, int out_d
   const long total = (long)fb / sizeof(uint16_t);
   for (int p = 0; p < 3; ++p)
     pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
-                                                           center, p,
+                                                           center, p, 0,
                                                            (uint16_t*)((char*)packed + p * fb), total);
   const int nb = kpad(out_dim, 32);
   pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb, center,
@@ -583,6 +585,11 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   RG_REQUIRE(in_dim > 0 && out_dim > 0 && in_dim <= MAXW && out_dim <= MAXW, RG_ERR_UNSUPPORTED,
              "rg_pack_linear: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
   hipStream_t st = (hipStream_t)stream;
+  const int f16 = (dtype & RG_PACK_F16) ? 1 : 0;
+  dtype &= ~RG_PACK_F16;
+  RG_REQUIRE(!f16 || ((dtype & ~RG_PACK_CENTERED) >= RG_PACK_FAST_IN &&
+                      (dtype & ~RG_PACK_CENTERED) <= RG_PACK_FAST_UPD),
+             RG_ERR_ARG, "rg_pack_linear: RG_PACK_F16 applies to the RG_PACK_FAST_* formats");
   if (dtype & RG_PACK_X3) {
     RG_REQUIRE(!(dtype & RG_PACK_TRANSPOSE), RG_ERR_ARG,
                "rg_pack_linear: RG_PACK_X3 does not combine with RG_PACK_TRANSPOSE");
@@ -611,7 +618,8 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
     const int mem_steps = dtype == RG_PACK_FAST_IN ? ks : (dtype == RG_PACK_FAST_CHAIN ? 0 : ks / 2);
     pack_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, mem_steps,
-                                                           center, 0, (uint16_t*)packed, total);
+                                                           center, 0, f16, (uint16_t*)packed,
+                                                           total);
   } else if (dtype == RG_PACK_F32_FAST) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
     pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,

@@ -89,6 +89,59 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
+// ---------------------------------------------------------------------------
+// The two 16-bit operand types of the half-precision kernels (chain_fast.hip,
+// conv_fused.hip, segment_reduce.hip): bf16 (8-bit exponent) and IEEE fp16 (5-bit
+// exponent, 3 more mantissa bits; BASELINE config 5).  Same 32x32x16 MFMA shape and rate.
+// Conversions from f32 round to nearest even (v_cvt_pk_bf16_f32 / v_cvt_f16_f32).
+// ---------------------------------------------------------------------------
+typedef _Float16 f16x2_hw __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_f16x2(float lo, float hi) {
+  const f16x2_hw v = {(_Float16)lo, (_Float16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  return (float)__builtin_bit_cast(_Float16, h);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+template <bool F16>
+struct H16;
+template <>
+struct H16<false> {  // bf16
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ uint32_t pack2(float a, float b) { return pack_bf16x2(a, b); }
+  // the low / high element of a packed pair as f32
+  static __device__ __forceinline__ float lo(uint32_t u) { return __uint_as_float(u << 16); }
+  static __device__ __forceinline__ float hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+  template <int D>
+  static __device__ __forceinline__ float half(uint32_t u, int which) { return which ? hi(u) : lo(u); }
+  static __device__ __forceinline__ float to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+  static __device__ __forceinline__ uint16_t from_f32(float f) { return f32_to_bf16(f); }
+  static __device__ __forceinline__ f32x16 mfma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static constexpr uint16_t ONE = 0x3f80;
+};
+template <>
+struct H16<true> {  // IEEE fp16
+  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ uint32_t pack2(float a, float b) { return pack_f16x2(a, b); }
+  static __device__ __forceinline__ float lo(uint32_t u) { return f16_to_f32((uint16_t)(u & 0xffffu)); }
+  static __device__ __forceinline__ float hi(uint32_t u) { return f16_to_f32((uint16_t)(u >> 16)); }
+  template <int D>
+  static __device__ __forceinline__ float half(uint32_t u, int which) { return which ? hi(u) : lo(u); }
+  static __device__ __forceinline__ float to_f32(uint16_t h) { return f16_to_f32(h); }
+  static __device__ __forceinline__ uint16_t from_f32(float f) { return f32_to_f16(f); }
+  static __device__ __forceinline__ f32x16 mfma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static constexpr uint16_t ONE = 0x3c00;
+};
+
+
 // activation codes (Activation, common.py:256-267)
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2, ACT_SWISH = 3 };
 

@@ -35,13 +35,14 @@ __device__ __forceinline__ raw_t<TS, VEC> load_raw(const TS* __restrict__ p) {
   return *(const raw_t<TS, VEC>*)p;
 }
 
+// element types: float, uint16_t = bf16 bits, _Float16 = IEEE fp16
 template <typename TS, int VEC>
 __device__ __forceinline__ float chan(const raw_t<TS, VEC>& x, int i) {
   if constexpr (sizeof(TS) == 4) {
     return __uint_as_float(((const uint32_t*)&x)[i]);
   } else {
     const uint32_t w = ((const uint32_t*)&x)[i >> 1];
-    return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+    return H16<std::is_same_v<TS, _Float16>>::template half<0>(w, i & 1);
   }
 }
 
@@ -51,10 +52,12 @@ __device__ __forceinline__ void store_vec(TO* __restrict__ o, const float (&a)[V
 #pragma unroll
     for (int i = 0; i < VEC; i += 4) *(f32x4*)(o + i) = (f32x4){a[i], a[i + 1], a[i + 2], a[i + 3]};
   } else if constexpr (VEC == 8) {
-    *(uint4*)o = (uint4){pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]),
-                         pack_bf16x2(a[6], a[7])};
+    using H = H16<std::is_same_v<TO, _Float16>>;
+    *(uint4*)o = (uint4){H::pack2(a[0], a[1]), H::pack2(a[2], a[3]), H::pack2(a[4], a[5]),
+                         H::pack2(a[6], a[7])};
   } else {
-    *(uint2*)o = (uint2){pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3])};
+    using H = H16<std::is_same_v<TO, _Float16>>;
+    *(uint2*)o = (uint2){H::pack2(a[0], a[1]), H::pack2(a[2], a[3])};
   }
 }
 
@@ -187,6 +190,16 @@ static int launch_any(int op, int src_dtype, int out_dtype, bool v8, hipStream_t
     launch_seg<uint16_t, uint16_t, 4>(op, st, g);
   else if (src_dtype == RG_F32 && out_dtype == RG_BF16)
     launch_seg<float, uint16_t, 4>(op, st, g);
+  else if (src_dtype == RG_F16 && out_dtype == RG_F32 && v8)
+    launch_seg<_Float16, float, 8>(op, st, g);
+  else if (src_dtype == RG_F16 && out_dtype == RG_F32)
+    launch_seg<_Float16, float, 4>(op, st, g);
+  else if (src_dtype == RG_F16 && out_dtype == RG_F16 && v8)
+    launch_seg<_Float16, _Float16, 8>(op, st, g);
+  else if (src_dtype == RG_F16 && out_dtype == RG_F16)
+    launch_seg<_Float16, _Float16, 4>(op, st, g);
+  else if (src_dtype == RG_F32 && out_dtype == RG_F16)
+    launch_seg<float, _Float16, 4>(op, st, g);
   else
     RG_REQUIRE(false, RG_ERR_ARG, "rg_segment_reduce: bad dtypes");
   RG_LAUNCH_CHECK();
@@ -223,7 +236,7 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
 static int bm_ld(int C) { return (C + 7) / 8 * 8; }
 
 extern "C" size_t rg_segment_reduce_ranges_workspace_size(long n_rows, int C, int src_dtype) {
-  const size_t es = src_dtype == RG_BF16 ? 2 : 4;
+  const size_t es = (src_dtype == RG_BF16 || src_dtype == RG_F16) ? 2 : 4;
   return ((size_t)(n_rows + RANGE_BLOCK - 1) / RANGE_BLOCK) * bm_ld(C) * es + 256;
 }
 

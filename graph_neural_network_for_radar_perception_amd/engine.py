@@ -35,7 +35,15 @@ from . import _native as nat
 from .common import (Activation, channel_normalization, ffn_block, group_normalization,
                      layer_normalization)
 
-DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16)}
+DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16),
+          'fp16': (nat.RG_F16, torch.float16)}
+# the 16-bit compute dtypes: register-resident fast chains and the fused conv only (the yml
+# widths); 'fp16' = IEEE binary16 operands (BASELINE config 5), packed with RG_PACK_F16
+HALF = ('bf16', 'fp16')
+
+
+def _half_flag(dtype: str) -> int:
+    return nat.RG_PACK_F16 if dtype == 'fp16' else 0
 
 # Arithmetic of the fused fp32 conv layer: 'x3' = float32 products from exact three-term
 # bf16 splits on the bf16 matrix cores (rg_conv_layer_x3, one launch per layer, the next
@@ -49,6 +57,8 @@ def _dt_code(t: torch.Tensor) -> int:
         return nat.RG_F32
     if t.dtype == torch.bfloat16:
         return nat.RG_BF16
+    if t.dtype == torch.float16:
+        return nat.RG_F16
     raise TypeError(f'unsupported tensor dtype {t.dtype}')
 
 
@@ -146,8 +156,9 @@ def centered_fmt(spec: LayerSpec, fmt: int) -> int:
 def layer_array(specs: List[LayerSpec], base: int, offs: List[int], fmts=None):
     arr = (nat.rg_layer * len(specs))()
     for i, s in enumerate(specs):
-        arr[i].flags = (nat.RG_LAYER_CENTERED
-                        if fmts is not None and fmts[i] & nat.RG_PACK_CENTERED else 0)
+        arr[i].flags = ((nat.RG_LAYER_CENTERED
+                         if fmts is not None and fmts[i] & nat.RG_PACK_CENTERED else 0)
+                        | (nat.RG_LAYER_F16 if fmts is not None and fmts[i] & nat.RG_PACK_F16 else 0))
         arr[i].w_packed = base + offs[i]
         arr[i].norm_mu = nat.ptr(s.mu.detach()) if s.mu is not None else None
         arr[i].norm_std = nat.ptr(s.std.detach()) if s.std is not None else None
@@ -226,12 +237,15 @@ class ChainPlan:
             for t in (s.weight, s.bias, s.mu, s.std):
                 if t is not None:
                     _require_device(t, 'model parameter')
-        self.buf, self.groups = self._pack_buffer(lambda i: self.dt)
-        # bf16: also the register-resident 32x32x16 formats of rg_mlp_chain_fast
+        # the generic chain kernel (fp32 / bf16; fp16 runs on the fast chains only)
+        self.buf, self.groups = (self._pack_buffer(lambda i: self.dt) if self.dtype != 'fp16'
+                                 else (None, None))
+        # 16-bit: also the register-resident 32x32x16 formats of rg_mlp_chain_fast
         self.fast = None
-        if self.dt == nat.RG_BF16 and len(self.specs) <= nat.MAX_LAYERS:
+        if self.dtype in HALF and len(self.specs) <= nat.MAX_LAYERS:
+            hf = _half_flag(self.dtype)
             self.fast_buf, fg = self._pack_buffer(lambda i: centered_fmt(
-                self.specs[i], nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN))
+                self.specs[i], (nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN) | hf))
             self.fast = fg[0][0]
         self.fast_ok = {}   # in_mode -> bool (shape has a compiled fast kernel)
         self._f32 = None    # RG_PACK_F32_FAST layer array, packed on first fp32 fast call
@@ -362,6 +376,11 @@ class ChainPlan:
             if rc != nat.RG_ERR_UNSUPPORTED:
                 nat.check(rc, 'rg_mlp_chain_fast')
             self.fast_ok[mode] = False
+        if self.groups is None:
+            raise NotImplementedError(
+                f'fp16 chains run on the register-resident fast kernels only, which have no '
+                f'instantiation for this chain (widths {[s.out_dim for s in self.specs]}, input '
+                f'mode {mode}); use fp32 or bf16')
         cur_in, cur_w, cur_mode = in0, w0, mode
         for gi, (arr, n, gout) in enumerate(self.groups):
             last = gi == len(self.groups) - 1
@@ -690,12 +709,13 @@ class ConvPlan:
             return
         if self.dtype == 'fp32':
             return self._pack_fused_f32()
-        if self.dtype != 'bf16':
+        if self.dtype not in HALF:
             return
         specs = self.msg.specs + self.upd.specs
         if len(self.msg.specs) != 2 or len(self.upd.specs) != 1:
             return
-        fmts = [centered_fmt(sp, f) for sp, f in
+        hf = _half_flag(self.dtype)
+        fmts = [centered_fmt(sp, f | hf) for sp, f in
                 zip(specs, [nat.RG_PACK_FAST_IN, nat.RG_PACK_FAST_CHAIN, nat.RG_PACK_FAST_UPD])]
         try:
             self.fused_buf, offs = pack_specs(specs, fmts, self.device)
@@ -1045,7 +1065,7 @@ def run_blocks(mods, x: torch.Tensor, dtype: str = 'fp32') -> torch.Tensor:
     _require_device(x, 'input')
     plan = _plan_for(mods, dtype, x.device)
     xin = x.contiguous()
-    if xin.dtype not in (torch.float32, torch.bfloat16):
+    if xin.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         xin = xin.float()
     out = torch.empty((xin.shape[0], plan.out_dim), dtype=torch.float32, device=x.device)
     plan(xin.shape[0], out, xin, xin.shape[1])

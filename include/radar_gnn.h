@@ -42,6 +42,7 @@ extern "C" {
 /* element types */
 #define RG_F32 0
 #define RG_BF16 1
+#define RG_F16 6 /* IEEE binary16: the fp16 path (BASELINE config 5) of the 16-bit kernels */
 /* packed-weight formats of rg_pack_linear: RG_F32 / RG_BF16 for rg_mlp_chain, and
  * the two 32x32x16 bf16 formats of rg_mlp_chain_fast (first layer / chained layers) */
 #define RG_PACK_FAST_IN 2
@@ -66,6 +67,9 @@ extern "C" {
  * accumulator order -- the operand format of the float32 kernels on bf16 matrix cores
  * (rg_conv_layer_x3) */
 #define RG_PACK_X3 0x400
+/* OR-ed into a RG_PACK_FAST_* format: IEEE fp16 fragments instead of bf16 (round to nearest
+ * even); mark such layers RG_LAYER_F16 -- the 16-bit kernels then take fp16 operands */
+#define RG_PACK_F16 0x800
 
 /* activations (modules/neural_net/common.py:256-267) */
 #define RG_ACT_NONE 0
@@ -234,6 +238,8 @@ typedef struct rg_layer {
 } rg_layer;
 
 #define RG_LAYER_CENTERED 1 /* w_packed was packed with RG_PACK_CENTERED */
+#define RG_LAYER_F16 2      /* w_packed holds fp16 fragments (RG_PACK_F16): the fast chain /
+                               fused conv then read and write RG_F16 activations */
 
 #define RG_MAX_LAYERS 8
 
