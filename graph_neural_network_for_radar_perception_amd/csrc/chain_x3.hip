@@ -24,7 +24,7 @@ namespace cx3 {
 using namespace ::rg::x3;
 
 #ifndef RG_X3_DB
-#define RG_X3_DB false  // double-buffered weight fragments in the chained layers (measured: no gain)
+#define RG_X3_DB true  // double-buffered weight fragments in the chained layers (M: edge encoder 1.52 -> 1.45 ms)
 #endif
 
 enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused into layer 1

@@ -75,7 +75,8 @@ extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, i
   return RG_OK;
 }
 
-extern "C" size_t rg_conv_layer_workspace_size(void) { return 256; }
+static_assert((rg::conv::CTR_STRIDE * rg::conv::NQ + 1) * sizeof(int) <= 2048, "conv workspace");
+extern "C" size_t rg_conv_layer_workspace_size(void) { return 2048; }
 
 extern "C" int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_layer,
                                           int aggr, const void* x, int ldx, const void* e,
@@ -101,3 +102,10 @@ extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* u
                                     dst, n_nodes, x_out, ld_out, nullptr, nullptr, workspace,
                                     stream);
 }
+
+#if RG_CONV_STAMP
+// diagnostic build only (not in radar_gnn.h): read and reset the per-phase stamp sums
+extern "C" int rg_debug_conv_stamps(int f16, unsigned long long* out_host) {
+  return f16 ? rg::conv_f16::conv_stamps(out_host) : rg::conv::conv_stamps(out_host);
+}
+#endif

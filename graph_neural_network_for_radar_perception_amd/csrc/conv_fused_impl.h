@@ -24,6 +24,28 @@ static constexpr int HID = 128;      // msg_mlp_hidden_dim
 // wave-private LDS: P (NB x HID f32), message tile (32 x C bf16), slots (32 int)
 static constexpr int WAVE_LDS = NB * HID * 4 + 32 * C * 2 + 128;
 static constexpr float NORM_EPS = 1e-5f;
+// Work-block heads: one per XCD (workgroup b runs on XCD b % 8), each on a 128-B line of
+// its own.  One shared head saturates at ~88 dequeues/us (MI355X_MICROARCH.md, dequeue):
+// measured here, both the C2 and C5 layers ran at exactly one block per ~22 ns with it.
+static constexpr int NQ = 8;
+static constexpr int CTR_STRIDE = 32;
+
+#ifndef RG_CONV_STAMP
+#define RG_CONV_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_conv_stamp
+#endif
+#if RG_CONV_STAMP
+// [0] staging [1] block head + P [2] edge tiles [3] update + store [4] blocks [5] tiles
+// [6] end-of-kernel wait [8] min start [9] max end (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_conv_stamp[16];
+#define CSTAMP(i)                                              \
+  do {                                                         \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += _n - st_last;                                 \
+    st_last = _n;                                              \
+  } while (0)
+#else
+#define CSTAMP(i) do {} while (0)
+#endif
 
 struct CLayer {
   int woff, bytes, out, act, centered;
@@ -44,7 +66,7 @@ struct CArgs {
   const int* src;
   const int* dst;
   uint16_t* x_out;
-  int* counter;
+  int* counter;  // NQ block heads, one per XCD, CTR_STRIDE ints apart, then the done counter
   int ldx, lde, ldo;
   // optional edge-balanced work blocks (rg_conv_blocks): block b = nodes
   // [blk_nodes[b], blk_nodes[b + 1]), at most NB, *n_blk_dev blocks; null: b = 8-node run
@@ -142,6 +164,11 @@ __device__ __forceinline__ int swz(int row) {
 template <int ACT>
 __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+#if RG_CONV_STAMP
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ float nrm[6];  // (mu, sd) of the three channel_normalizations
   if (threadIdx.x == 0) {  // static layer indices: a dynamic a.L[i] would copy a to scratch
 #pragma unroll
@@ -159,6 +186,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     for (int i = threadIdx.x; i < n; i += CT) dstp[i] = src[i];
   }
   __syncthreads();
+  CSTAMP(0);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
 #ifdef RG_CONV_PRIO
@@ -182,6 +210,12 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // edge range are fetched at the start of the current block, so a block starts with
   // two dependent global round trips (indices -> rows) instead of four
   const int n_blocks = a.blk_nodes ? *a.n_blk_dev : a.n_blocks;
+  // this XCD's share of the blocks: contiguous destination ranges (its L2 then holds the
+  // neighbourhoods it gathers), dequeued from its own head
+  const int xcd = blockIdx.x % NQ;
+  const int blo = (int)((long)n_blocks * xcd / NQ);
+  const int bhi = (int)((long)n_blocks * (xcd + 1) / NQ);
+  int* const head = a.counter + CTR_STRIDE * xcd;
   // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
   auto block_nodes = [&](int b, int& n0, int& n1) {
     if (a.blk_nodes) {
@@ -193,10 +227,10 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     }
   };
   int blk = 0;
-  if (lane == 0) blk = atomicAdd(a.counter, 1);
-  blk = __shfl(blk, 0, 64);
+  if (lane == 0) blk = atomicAdd(head, 1);
+  blk = blo + __shfl(blk, 0, 64);
   int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
-  if (blk < n_blocks) {
+  if (blk < bhi) {
     block_nodes(blk, bn0, bn1);
     e0 = a.seg_ptr[bn0];
     e1 = a.seg_ptr[bn1];
@@ -211,11 +245,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
   }
 #endif
-  while (blk < n_blocks) {
+  while (blk < bhi) {
     const int n0 = bn0;
     const int n1 = bn1;
     int nxt_raw = 0;
-    if (lane == 0) nxt_raw = atomicAdd(a.counter, 1);
+    if (lane == 0) nxt_raw = atomicAdd(head, 1);
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
@@ -352,10 +386,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): P visible to the whole wave
       __builtin_amdgcn_wave_barrier();
     }
+    CSTAMP(1);
 
-    const int nxt = __shfl(nxt_raw, 0, 64);
+    const int nxt = blo + __shfl(nxt_raw, 0, 64);
     int ne0 = 0, ne1 = 0, nn0 = 0, nn1 = 0;
-    if (nxt < n_blocks) {
+    if (nxt < bhi) {
       block_nodes(nxt, nn0, nn1);
       ne0 = a.seg_ptr[nn0];
       ne1 = a.seg_ptr[nn1];
@@ -388,6 +423,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
         if (t0 >= e1) break;
       }
     }
+#if RG_CONV_STAMP
+    CSTAMP(2);
+    st_acc[4] += 1;
+    st_acc[5] += (e1 - e0 + 31) / 32;
+#endif
     // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
     const int node = n0 + r;
     const bool nvalid = r < NB && node < n1;
@@ -436,6 +476,10 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
           *(uint2*)(po + f0) = o;
         }
     }
+#if RG_CONV_STAMP
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    CSTAMP(3);
     blk = nxt;
     e0 = ne0;
     e1 = ne1;
@@ -447,10 +491,18 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // returned before its workgroup reaches the barrier, so when `done` reaches the grid
   // size no workgroup can touch the counter again.
   __syncthreads();
+#if RG_CONV_STAMP
+  CSTAMP(6);
+  if (lane == 0) {
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_conv_stamp[i], st_acc[i]);
+    atomicMin(&g_conv_stamp[8], st_rt0);
+    atomicMax(&g_conv_stamp[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+#endif
   if (threadIdx.x == 0) {
-    if (atomicAdd(a.counter + 1, 1) == (int)gridDim.x - 1) {
-      atomicExch(a.counter, 0);
-      atomicExch(a.counter + 1, 0);
+    if (atomicAdd(a.counter + CTR_STRIDE * NQ, 1) == (int)gridDim.x - 1) {
+#pragma unroll
+      for (int q = 0; q <= NQ; ++q) atomicExch(a.counter + CTR_STRIDE * q, 0);
     }
   }
 }
@@ -489,6 +541,16 @@ __global__ void conv_blocks_kernel(const int* __restrict__ seg_ptr, int n_nodes,
   if (!EMIT) cnt[b] = c;
   if (EMIT && b == nb8 - 1) blk_nodes[o + c] = n_nodes;  // sentinel
 }
+
+#if RG_CONV_STAMP
+static int conv_stamps(unsigned long long* out_host) {
+  RG_CHECK_HIP(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_conv_stamp), sizeof(g_conv_stamp)));
+  unsigned long long z[16] = {0};
+  z[8] = ~0ull;
+  RG_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_conv_stamp), z, sizeof(z)));
+  return RG_OK;
+}
+#endif
 
 // the C-ABI entry of this operand type (rg_conv_layer_fused_blocks dispatches on RG_LAYER_F16)
 static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_layer,
@@ -535,7 +597,7 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
   a.src = src;
   a.dst = dst;
   a.x_out = (uint16_t*)x_out;
-  a.counter = (int*)workspace;  // [0] next block, [1] workgroups done: zero between launches
+  a.counter = (int*)workspace;  // NQ heads + workgroups done: zero between launches
   a.ldx = ldx; a.lde = lde; a.ldo = ld_out;
   RG_REQUIRE((blk_nodes == nullptr) == (n_blocks_dev == nullptr), RG_ERR_ARG,
              "rg_conv_layer_fused_blocks: block table and count go together");
@@ -552,12 +614,13 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
   RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   int blocks = 256;  // a block table has at least ceil(N / NB) entries
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
+  blocks = (blocks + NQ - 1) / NQ * NQ;  // every head has workgroups of its own
   kern<<<blocks, CT, lds, st>>>(a);
   const hipError_t le = hipGetLastError();
   if (le != hipSuccess) {
     // a launch that did not run leaves the counters as they were; one that failed part
     // way could leave them nonzero: re-zero so the next launch does not skip blocks
-    (void)hipMemsetAsync(workspace, 0, 2 * sizeof(int), st);
+    (void)hipMemsetAsync(workspace, 0, (CTR_STRIDE * NQ + 1) * sizeof(int), st);
     set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__, hipGetErrorString(le));
     return RG_ERR_HIP;
   }

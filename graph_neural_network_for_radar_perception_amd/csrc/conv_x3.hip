@@ -69,6 +69,8 @@ __device__ unsigned long long g_cx3_stamp[16];
 #define STAMP(i) do {} while (0)
 #endif
 static constexpr int NXCD = 8;
+static constexpr int CTR_STRIDE = 32;  // block counters one 128-B line apart (per-line atomics)
+static constexpr int CTR_BYTES = 2048; // counter area at the front of the workspace
 #ifndef RG_CX3_FT
 #define RG_CX3_FT 512
 #endif
@@ -78,7 +80,10 @@ static constexpr int NXCD = 8;
 #endif
 static constexpr int FT = RG_CX3_FT;  // 512: two waves per SIMD
 static constexpr int NW = FT / 64;
-static constexpr int TR = 16;     // message rows per LDS transposition pass
+#ifndef RG_CX3_WU_LDS
+#define RG_CX3_WU_LDS 0  // W_u staged in LDS too, 4-row passes (M: 0.650 vs 0.638 ms/layer, slower)
+#endif
+static constexpr int TR = RG_CX3_WU_LDS ? 4 : 16;  // message rows per LDS transposition pass
 static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
 #ifndef RG_CX3_EXP
 #define RG_CX3_EXP 0  // timing experiments only (wrong results): 1 no tile norm epilogues,
@@ -88,7 +93,8 @@ static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
 
 static constexpr int WE_OFF = 0;                                   // W_e 64 -> 128 (FAST_IN)
 static constexpr int W2_OFF = al16(x3_bytes(C, HID));              // W_2 128 -> 64 (FAST_CHAIN)
-static constexpr int W_LDS = W2_OFF + al16(x3_bytes(HID, C));
+static constexpr int WU_OFF = W2_OFF + al16(x3_bytes(HID, C));   // W_u (FAST_IN), optional
+static constexpr int W_LDS = WU_OFF + (RG_CX3_WU_LDS ? al16(x3_bytes(2 * C, C)) : 0);
 static constexpr int T_BYTES = TR * TS * 4;
 static constexpr int LDS_BYTES = W_LDS + NW * T_BYTES;
 static_assert(LDS_BYTES <= DYN_LDS_MAX, "conv_x3 LDS");
@@ -135,7 +141,7 @@ struct Args {
   float* x_out;
   float* pq_out;         // [N][256] the next layer's P | Q, or null
   float* agg;            // [N][64] aggregate scratch
-  int* counters;         // [NXCD] block counters + [1] done counter; zero at launch
+  int* counters;         // NXCD block counters + done counter, CTR_STRIDE apart; zero at launch
   const char* w[3];      // W_e (FAST_IN), W_2 (FAST_CHAIN), W_u (FAST_IN over cat(x, agg)), x3
   const char* wpq;       // the next layer's projection (FAST_CHAIN x3) or null
   const float* mu[3];
@@ -154,10 +160,10 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
   }
   {
-    const int nb[2] = {x3_bytes(C, HID), x3_bytes(HID, C)};
-    const int off[2] = {WE_OFF, W2_OFF};
+    const int nb[3] = {x3_bytes(C, HID), x3_bytes(HID, C), x3_bytes(2 * C, C)};
+    const int off[3] = {WE_OFF, W2_OFF, WU_OFF};
 #pragma unroll
-    for (int l = 0; l < 2; ++l) {
+    for (int l = 0; l < (RG_CX3_WU_LDS ? 3 : 2); ++l) {
       const u32x4* s = (const u32x4*)a.w[l];
       u32x4* d = (u32x4*)(lds + off[l]);
       for (int i = threadIdx.x; i < nb[l] / 16; i += FT) d[i] = s[i];
@@ -170,7 +176,11 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   float* T = (float*)(lds + W_LDS + wave * T_BYTES);  // [TR][TS] message rows
   const WLds wE{lds + WE_OFF + lane * 16, plane_bytes(C, HID)};
   const WLds w2{lds + W2_OFF + lane * 16, plane_bytes(HID, C)};
+#if RG_CX3_WU_LDS
+  const WLds wU{lds + WU_OFF + lane * 16, plane_bytes(2 * C, C)};
+#else
   const WBuf wU = wbuf(a.w[2], x3_bytes(2 * C, C), plane_bytes(2 * C, C), lane);
+#endif
   const WBuf wPQ = wbuf(a.wpq, a.wpq ? x3_bytes(C, PQW) : 0, plane_bytes(C, PQW), lane);
   const float* bias2 = (const float*)(lds + W2_OFF + 3 * plane_bytes(HID, C));
   const float* biasU = (const float*)(a.w[2] + 3 * plane_bytes(2 * C, C));
@@ -204,7 +214,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
 #else
   const int blo = (int)((long)a.n_blocks * xcd / NXCD);
   const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
-  int* ctr = a.counters + xcd;
+  int* ctr = a.counters + CTR_STRIDE * xcd;
 #endif
 
 #if RG_CX3_STAMP
@@ -448,9 +458,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(a.counters + NXCD, 1) == (int)gridDim.x - 1) {
+    if (atomicAdd(a.counters + CTR_STRIDE * NXCD, 1) == (int)gridDim.x - 1) {
 #pragma unroll
-      for (int i = 0; i <= NXCD; ++i) a.counters[i] = 0;
+      for (int i = 0; i <= NXCD; ++i) a.counters[CTR_STRIDE * i] = 0;
     }
   }
 }
@@ -518,7 +528,8 @@ extern "C" int rg_debug_cx3_stamps(unsigned long long* out_host) {
 #endif
 
 extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
-  return 256 + (size_t)(n_nodes > 0 ? n_nodes : 1) * C * sizeof(float);
+  static_assert((CTR_STRIDE * NXCD + 1) * sizeof(int) <= CTR_BYTES, "counter area");
+  return CTR_BYTES + (size_t)(n_nodes > 0 ? n_nodes : 1) * C * sizeof(float);
 }
 
 extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes,
@@ -578,7 +589,7 @@ extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq,
   a.x_out = x_out;
   a.pq_out = pq_out;
   a.counters = (int*)workspace;
-  a.agg = (float*)((char*)workspace + 256);
+  a.agg = (float*)((char*)workspace + CTR_BYTES);
   a.w[0] = (const char*)m0.w_packed;
   a.w[1] = (const char*)m1.w_packed;
   a.w[2] = (const char*)u.w_packed;
