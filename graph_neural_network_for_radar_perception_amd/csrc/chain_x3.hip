@@ -146,11 +146,39 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
   }
 }
 
-// layers l.. of the chain; prev = the previous layer's activations (RT row tiles)
-template <typename S, int SPEC, int LM, int l, int RT, int PMT>
+#ifndef RG_X3_JIT
+#define RG_X3_JIT 1  // a normalised layer's scale + act applied in the next layer's B operand
+#endif
+// what layer l leaves pending for the next one (split_acc_pend): 1 norm + LeakyReLU,
+// 2 norm only, 0 nothing (its epilogue, if any, runs in full)
+template <int SPEC, int l>
+constexpr int pend_kind() {
+  return !RG_X3_JIT ? 0 : (sp_norm(SPEC, l) && sp_act(SPEC, l)) ? 1 : sp_norm(SPEC, l) ? 2 : 0;
+}
+// layer l's epilogue when a next layer follows: statistics only for a pending kind
+template <int SPEC, int l, int MT, int RT>
+__device__ __forceinline__ void epilogue_pend(f32x16 (&acc)[RT][MT], const float* nrm,
+                                              Pend (&pn)[RT]) {
+  constexpr int K = pend_kind<SPEC, l>();
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    if constexpr (K == 1) {
+      pn[t] = pend_norm_leaky<MT, sp_cent(SPEC)>(acc[t], nrm[2 * l], nrm[2 * l + 1]);
+    } else if constexpr (K == 2) {
+      pn[t] = pend_norm_only<MT, sp_cent(SPEC)>(acc[t], nrm[2 * l], nrm[2 * l + 1]);
+    } else {
+      epilogue<SPEC, l, MT>(acc[t], nrm);
+      pn[t] = Pend{0.f, 0.f};
+    }
+  }
+}
+
+// layers l.. of the chain; prev = the previous layer's activations (RT row tiles), with
+// the previous layer's norm / act still pending (PEND) where pend_kind says so
+template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND>
 __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[RT][PMT],
-                                         const char* lds, const float* nrm, long row0, long rows,
-                                         int lane) {
+                                         const Pend (&pend)[RT], const char* lds, const float* nrm,
+                                         long row0, long rows, int lane) {
   constexpr int N = S::N[l], MT = N / 32, KS = S::K(l) / 16;
   static_assert(S::K(l) == 32 * PMT, "chained width");
   const int h = lane >> 5;
@@ -160,13 +188,17 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[RT]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
-  layer_x3<KS, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, l>(a, lds, lane), 0,
-                                 [&](int s, int t) { return split_acc(prev[t][s >> 1], s & 1); });
-#pragma unroll
-  for (int t = 0; t < RT; ++t) epilogue<SPEC, l, MT>(acc[t], nrm);
+  layer_x3<KS, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, l>(a, lds, lane), 0, [&](int s, int t) {
+    return split_acc_pend<PEND>(prev[t][s >> 1], s & 1, pend[t]);
+  });
   if constexpr (l + 1 < S::NL) {
-    run_rest<S, SPEC, LM, l + 1, RT, MT>(a, acc, lds, nrm, row0, rows, lane);
+    Pend pn[RT];
+    epilogue_pend<SPEC, l, MT, RT>(acc, nrm, pn);
+    run_rest<S, SPEC, LM, l + 1, RT, MT, pend_kind<SPEC, l>()>(a, acc, pn, lds, nrm, row0, rows,
+                                                              lane);
   } else {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) epilogue<SPEC, l, MT>(acc[t], nrm);
     store_rows<RT, MT>(acc, a, row0, rows, lane);
   }
 }
@@ -185,11 +217,13 @@ __device__ __forceinline__ void run_first(const Args& a, const X3 (&b0)[RT][KS0]
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
   layer_x3<KS0, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, 0>(a, lds, lane), 0,
                                   [&](int s, int t) { return b0[t][s]; });
-#pragma unroll
-  for (int t = 0; t < RT; ++t) epilogue<SPEC, 0, MT>(acc[t], nrm);
   if constexpr (S::NL > 1) {
-    run_rest<S, SPEC, LM, 1, RT, MT>(a, acc, lds, nrm, row0, rows, lane);
+    Pend pn[RT];
+    epilogue_pend<SPEC, 0, MT, RT>(acc, nrm, pn);
+    run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
   } else {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) epilogue<SPEC, 0, MT>(acc[t], nrm);
     store_rows<RT, MT>(acc, a, row0, rows, lane);
   }
 }
@@ -262,11 +296,13 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-#pragma unroll
-  for (int t = 0; t < RT; ++t) epilogue<SPEC, 1, MT1>(acc[t], nrm);
   if constexpr (S::NL > 2) {
-    run_rest<S, SPEC, LM, 2, RT, MT1>(a, acc, lds, nrm, row0, rows, lane);
+    Pend pn[RT];
+    epilogue_pend<SPEC, 1, MT1, RT>(acc, nrm, pn);
+    run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>()>(a, acc, pn, lds, nrm, row0, rows, lane);
   } else {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) epilogue<SPEC, 1, MT1>(acc[t], nrm);
     store_rows<RT, MT1>(acc, a, row0, rows, lane);
   }
 }

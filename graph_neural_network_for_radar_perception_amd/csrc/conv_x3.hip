@@ -80,6 +80,12 @@ static constexpr int CTR_BYTES = 2048; // counter area at the front of the works
 #endif
 static constexpr int FT = RG_CX3_FT;  // 512: two waves per SIMD
 static constexpr int NW = FT / 64;
+#ifndef RG_CX3_JIT
+#define RG_CX3_JIT 1  // message layer 1's norm scale + act applied in layer 2's B operand
+#endif
+#ifndef RG_CX3_NODE_KERNEL
+#define RG_CX3_NODE_KERNEL 1  // the update / projection phase as a second launch (LDS weights)
+#endif
 #ifndef RG_CX3_WU_LDS
 #define RG_CX3_WU_LDS 0  // W_u staged in LDS too, 4-row passes (M: 0.650 vs 0.638 ms/layer, slower)
 #endif
@@ -108,7 +114,8 @@ __device__ __forceinline__ float xor_first(const X3& b) {
 // register 4g + t of tile m) -> pq rows [256] f32; W'_pq packed FAST_CHAIN x3 (K = 64), read
 // from global memory (L2): the row's B operand is split once, then four passes of two
 // M-tiles keep the live registers bounded
-__device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WBuf& W, const float* bias,
+template <typename WSrc>
+__device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WSrc& W, const float* bias,
                                              float* pq_row, bool valid, int lane) {
   const int h = lane >> 5;
   X3 b[4];
@@ -151,7 +158,76 @@ struct Args {
   int aggr_mean;
 };
 
-template <bool CENT>
+// ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109) for the 32
+//      nodes n0 .. n1 - 1 (lane r = node), then -- when a.pq_out is set -- the next layer's
+//      projections from the same registers
+template <bool CENT, typename WU, typename WP>
+__device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const WU& wU,
+                                            const float* biasU, const WP& wPQ,
+                                            const float* biasPQ, float muU, float sdU, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int node = n0 + r;
+  const bool nvalid = node < n1;
+  const int nrow = nvalid ? node : n0;
+  const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 0;
+  const float* px = a.x + (size_t)nrow * a.ldx;
+  f32x4 xb[4][2], ab[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    xb[s][0] = *(const f32x4*)(px + 16 * s + 8 * h);
+    xb[s][1] = *(const f32x4*)(px + 16 * s + 8 * h + 4);
+  }
+  {
+    const f32x4* pa = (const f32x4*)(a.agg + (size_t)nrow * C + 8 * h);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ab[s][0] = __builtin_nontemporal_load(pa + 4 * s);
+      ab[s][1] = __builtin_nontemporal_load(pa + 4 * s + 1);
+    }
+    // no incoming edges: PyG leaves the aggregate at zero; mean = sum / max(count, 1)
+    const float sc = deg > 0 ? (float)deg : 1.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x4 v = deg > 0 ? ab[s][u] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (a.aggr_mean) v = (f32x4){div_rn(v.x, sc), div_rn(v.y, sc), div_rn(v.z, sc), div_rn(v.w, sc)};
+        ab[s][u] = v;
+      }
+  }
+  f32x16 accu[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
+  layer_x3<8, 2, 2, true>(accu, wU, 0, [&](int s) {
+    return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
+  });
+  norm_leaky<2, CENT>(accu, muU, sdU);
+  {
+    const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 xr = *(const f32x4*)(pxr + 32 * m + 8 * g);
+        accu[m][4 * g + 0] = __fadd_rn(xr.x, accu[m][4 * g + 0]);
+        accu[m][4 * g + 1] = __fadd_rn(xr.y, accu[m][4 * g + 1]);
+        accu[m][4 * g + 2] = __fadd_rn(xr.z, accu[m][4 * g + 2]);
+        accu[m][4 * g + 3] = __fadd_rn(xr.w, accu[m][4 * g + 3]);
+      }
+  }
+  if (nvalid) {
+    float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(f32x4*)(po + 32 * m + 8 * g) = (f32x4){accu[m][4 * g], accu[m][4 * g + 1],
+                                                 accu[m][4 * g + 2], accu[m][4 * g + 3]};
+  }
+  if (a.pq_out) project_rows(accu, wPQ, biasPQ, a.pq_out + (size_t)nrow * PQW, nvalid, lane);
+}
+
+template <bool CENT, bool NODE>
 __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[6];
@@ -314,14 +390,24 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         }
       }
       STAMP(1);  // gathers + layer 1 issue
+#if RG_CX3_JIT
+      // norm 1's statistics now; its scale + LeakyReLU inside layer 2's B operand
+      const Pend pn1 = pend_norm_leaky<4, CENT>(acc1, mu0, sd0);
+#else
       if constexpr (RG_CX3_EXP != 1) norm_leaky<4, CENT>(acc1, mu0, sd0);
+#endif
       STAMP(2);  // norm 1 (waits for layer 1)
       // ---- layer 2 (B operand = layer 1's accumulators)
       f32x16 acc2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
       if constexpr (RG_CX3_EXP != 5) {
+#if RG_CX3_JIT
+        layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0,
+                                      [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
+#else
         layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0, [&](int s) { return split_acc(acc1[s >> 1], s & 1); });
+#endif
       } else {
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
@@ -380,74 +466,15 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
     // the aggregate rows were written by this wave's lanes = features; read them back as
     // rows (lane = node) from L2: stores complete (vmcnt 0), loads bypass L1 (nt)
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    if constexpr (NODE) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 
     if constexpr (RG_CX3_EXP == 6) {
       if (n0 + r < n1) a.x_out[(size_t)(n0 + r) * a.ldo + h] = run;
       continue;
     }
-    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
-    const int node = n0 + r;
-    const bool nvalid = node < n1;
-    const int nrow = nvalid ? node : n0;
-    const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 0;
-    const float* px = a.x + (size_t)nrow * a.ldx;
-    f32x4 xb[4][2], ab[4][2];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      xb[s][0] = *(const f32x4*)(px + 16 * s + 8 * h);
-      xb[s][1] = *(const f32x4*)(px + 16 * s + 8 * h + 4);
+    if constexpr (NODE) {
+      node_update<CENT>(a, n0, n1, wU, biasU, wPQ, biasPQ, muU, sdU, lane);
     }
-    {
-      const f32x4* pa = (const f32x4*)(a.agg + (size_t)nrow * C + 8 * h);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        ab[s][0] = __builtin_nontemporal_load(pa + 4 * s);
-        ab[s][1] = __builtin_nontemporal_load(pa + 4 * s + 1);
-      }
-      // no incoming edges: PyG leaves the aggregate at zero; mean = sum / max(count, 1)
-      const float sc = deg > 0 ? (float)deg : 1.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          f32x4 v = deg > 0 ? ab[s][u] : (f32x4){0.f, 0.f, 0.f, 0.f};
-          if (a.aggr_mean) v = (f32x4){div_rn(v.x, sc), div_rn(v.y, sc), div_rn(v.z, sc), div_rn(v.w, sc)};
-          ab[s][u] = v;
-        }
-    }
-    f32x16 accu[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
-    layer_x3<8, 2, 2, true>(accu, wU, 0, [&](int s) {
-      return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
-    });
-    norm_leaky<2, CENT>(accu, muU, sdU);
-    STAMP(6);  // update loads + layer
-    {
-      const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 xr = *(const f32x4*)(pxr + 32 * m + 8 * g);
-          accu[m][4 * g + 0] = __fadd_rn(xr.x, accu[m][4 * g + 0]);
-          accu[m][4 * g + 1] = __fadd_rn(xr.y, accu[m][4 * g + 1]);
-          accu[m][4 * g + 2] = __fadd_rn(xr.z, accu[m][4 * g + 2]);
-          accu[m][4 * g + 3] = __fadd_rn(xr.w, accu[m][4 * g + 3]);
-        }
-    }
-    if (nvalid) {
-      float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(f32x4*)(po + 32 * m + 8 * g) = (f32x4){accu[m][4 * g], accu[m][4 * g + 1],
-                                                   accu[m][4 * g + 2], accu[m][4 * g + 3]};
-    }
-    STAMP(7);  // residual + store
-    if (a.pq_out) project_rows(accu, wPQ, biasPQ, a.pq_out + (size_t)nrow * PQW, nvalid, lane);
     STAMP(8);  // next layer's projections
   }
 #if RG_CX3_STAMP
@@ -463,6 +490,46 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       for (int i = 0; i <= NXCD; ++i) a.counters[CTR_STRIDE * i] = 0;
     }
   }
+}
+
+// The node phase as a launch of its own (RG_CX3_NODE_KERNEL): W_u and W'_pq both staged in
+// LDS (145 KB), one 32-node tile per wave and step; the aggregate rows come from the
+// edge launch's scratch.  In the single-launch layer the same phase runs at each block's
+// end with both weight images read from L2 (the edge weights fill the LDS).
+static constexpr int NU_OFF = 0;
+static constexpr int NPQ_OFF = al16(x3_bytes(2 * C, C));
+static constexpr int NODE_LDS = NPQ_OFF + al16(x3_bytes(C, PQW));
+static_assert(NODE_LDS <= DYN_LDS_MAX, "node_x3 LDS");
+template <bool CENT>
+__global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[2];
+  if (threadIdx.x == 0) {
+    nrm[0] = *a.mu[2];
+    nrm[1] = *a.sd[2];
+  }
+  {
+    const int nb[2] = {x3_bytes(2 * C, C), a.wpq ? x3_bytes(C, PQW) : 0};
+    const char* src[2] = {a.w[2], a.wpq};
+    const int off[2] = {NU_OFF, NPQ_OFF};
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const u32x4* sp = (const u32x4*)src[l];
+      u32x4* d = (u32x4*)(lds + off[l]);
+      for (int i = threadIdx.x; i < nb[l] / 16; i += 512) d[i] = sp[i];
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const WLds wU{lds + NU_OFF + lane * 16, plane_bytes(2 * C, C)};
+  const WLds wPQ{lds + NPQ_OFF + lane * 16, plane_bytes(C, PQW)};
+  const float* biasU = (const float*)(lds + NU_OFF + 3 * plane_bytes(2 * C, C));
+  const float* biasPQ = (const float*)(lds + NPQ_OFF + 3 * plane_bytes(C, PQW));
+  const float muU = nrm[0], sdU = nrm[1];
+  const int ntiles = (a.n_nodes + 31) / 32;
+  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8)
+    node_update<CENT>(a, 32 * t, min(32 * t + 32, a.n_nodes), wU, biasU, wPQ, biasPQ, muU, sdU,
+                      lane);
 }
 
 // P | Q = W_pq x + [b1; 0] for dense float32 rows (the first layer's projections):
@@ -609,13 +676,18 @@ extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq,
   const int need = (a.n_blocks + NW - 1) / NW;
   if (blocks > need) blocks = (need + NXCD - 1) / NXCD * NXCD;
   if (blocks < NXCD) blocks = NXCD;
-  if (cent) {
-    RG_ENSURE_LDS(conv_x3_kernel<true>, LDS_BYTES);
-    conv_x3_kernel<true><<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
-  } else {
-    RG_ENSURE_LDS(conv_x3_kernel<false>, LDS_BYTES);
-    conv_x3_kernel<false><<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
-  }
+  constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
+  auto edge = cent ? conv_x3_kernel<true, NODE> : conv_x3_kernel<false, NODE>;
+  RG_ENSURE_LDS(edge, LDS_BYTES);
+  edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
   RG_LAUNCH_CHECK();
+  if constexpr (!NODE) {
+    auto node = cent ? node_x3_kernel<true> : node_x3_kernel<false>;
+    RG_ENSURE_LDS(node, NODE_LDS);
+    const int tiles = (n_nodes + 31) / 32;
+    const int nblk = (tiles + 7) / 8 < 256 ? (tiles + 7) / 8 : 256;
+    node<<<nblk, 512, NODE_LDS, (hipStream_t)stream>>>(a);
+    RG_LAUNCH_CHECK();
+  }
   return RG_OK;
 }

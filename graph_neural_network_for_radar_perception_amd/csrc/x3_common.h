@@ -49,20 +49,54 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
   return r;
 }
 
-// 8 consecutive k values of one row -> the three exact bf16 terms
+#ifndef RG_X3_PIPE
+#define RG_X3_PIPE 1  // layer_x3 computes the B operand of k-step s + 1 beside step s's MFMAs
+#endif
+#ifndef RG_X3_PKNORM
+#define RG_X3_PKNORM 0  // 1: row statistics and scale in v_pk_fma_f32 (M: no gain, conv 1% slower)
+#endif
+#ifndef RG_X3_SPLIT
+#define RG_X3_SPLIT 0  // split8 residues: 0 scalar v_sub_f32, 1 f32x2 (compiler), 2 forced v_pk_add_f32
+#endif
+
+// the two f32 values of a packed bf16 pair
+__device__ __forceinline__ f32x2 unpk(uint32_t u) {
+  return (f32x2){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// a - b on a register pair as ONE v_pk_add_f32 (the compiler otherwise keeps the
+// residues of split8 scalar: two v_add_f32 per pair)
+__device__ __forceinline__ f32x2 sub_pk(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// 8 consecutive k values of one row -> the three exact bf16 terms (the residues of a
+// pair in one v_pk_add_f32)
 __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
-  const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const f32x2 v[4] = {{lo.x, lo.y}, {lo.z, lo.w}, {hi.x, hi.y}, {hi.z, hi.w}};
   u32x4 w0, w1, w2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float a = v[2 * i], b = v[2 * i + 1];
-    const uint32_t u0 = cvt_pk_bf16(a, b);
-    const float ra = a - __uint_as_float(u0 << 16), rb = b - __uint_as_float(u0 & 0xffff0000u);
-    const uint32_t u1 = cvt_pk_bf16(ra, rb);
-    const float sa = ra - __uint_as_float(u1 << 16), sb = rb - __uint_as_float(u1 & 0xffff0000u);
+    const uint32_t u0 = cvt_pk_bf16(v[i].x, v[i].y);
+#if RG_X3_SPLIT == 2
+    const f32x2 r = sub_pk(v[i], unpk(u0));
+    const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
+    const f32x2 t = sub_pk(r, unpk(u1));
+#elif RG_X3_SPLIT == 1
+    const f32x2 r = add2(v[i], -unpk(u0));
+    const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
+    const f32x2 t = add2(r, -unpk(u1));
+#else
+    const f32x2 u0f = unpk(u0);
+    const f32x2 r = {v[i].x - u0f.x, v[i].y - u0f.y};
+    const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
+    const f32x2 u1f = unpk(u1);
+    const f32x2 t = {r.x - u1f.x, r.y - u1f.y};
+#endif
     w0[i] = u0;
     w1[i] = u1;
-    w2[i] = cvt_pk_bf16(sa, sb);
+    w2[i] = cvt_pk_bf16(t.x, t.y);
   }
   return X3{__builtin_bit_cast(bf16x8_t, w0), __builtin_bit_cast(bf16x8_t, w1),
             __builtin_bit_cast(bf16x8_t, w2)};
@@ -125,6 +159,13 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
       for (int p = 0; p < 3; ++p) d[m][p] = W(p, ((m0 + m) * KS + s) * 1024);
   };
   if constexpr (DB) lda(0, Ab[0]);
+  // B operands one k-step ahead (RG_X3_PIPE): the split of step s + 1 is independent of
+  // step s's MFMAs, so its VALU work can issue in their shadow instead of between them
+  X3 bq[RG_X3_PIPE ? RT : 1];
+  if constexpr (RG_X3_PIPE) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) bq[t] = bop(0, t);
+  }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if constexpr (DB) {
@@ -133,9 +174,16 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
       lda(s, Ab[0]);
     }
     const bf16x8_t(&A)[MT][3] = Ab[DB ? (s & 1) : 0];
+    X3 bn[RG_X3_PIPE ? RT : 1];
+    if constexpr (RG_X3_PIPE) {
+      if (s + 1 < KS) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) bn[t] = bop(s + 1, t);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
-      const X3 b = bop(s, t);
+      const X3 b = RG_X3_PIPE ? bq[t] : bop(s, t);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[t][m] = mf(A[m][2], b.p0, acc[t][m]);
 #pragma unroll
@@ -148,6 +196,12 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
       for (int m = 0; m < MT; ++m) acc[t][m] = mf(A[m][0], b.p1, acc[t][m]);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
+    }
+    if constexpr (RG_X3_PIPE) {
+      if (s + 1 < KS) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) bq[t] = bn[t];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -189,16 +243,31 @@ __device__ __forceinline__ float row_inv_std(f32x16 (&acc)[MT]) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[m][q] -= mean;
   }
-  float v[8];
+#if !RG_X3_PKNORM
+  float u[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = acc[0][i] * acc[0][i];
+  for (int i = 0; i < 8; ++i) u[i] = acc[0][i] * acc[0][i];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = fmaf(acc[0][i + 8], acc[0][i + 8], v[i]);
+  for (int i = 0; i < 8; ++i) u[i] = fmaf(acc[0][i + 8], acc[0][i + 8], u[i]);
 #pragma unroll
   for (int m = 1; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q & 7] = fmaf(acc[m][q], acc[m][q], v[q & 7]);
-  const float ss = add_xor32(((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7])));
+    for (int q = 0; q < 16; ++q) u[q & 7] = fmaf(acc[m][q], acc[m][q], u[q & 7]);
+  const float ss = add_xor32(((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7])));
+#else
+  // sum of squares in four packed partial sums (v_pk_fma_f32: two features per instruction)
+  f32x2 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = mul2(pair(acc[0], i), pair(acc[0], i));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = fma2(pair(acc[0], i + 4), pair(acc[0], i + 4), v[i]);
+#pragma unroll
+  for (int m = 1; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i & 3] = fma2(pair(acc[m], i), pair(acc[m], i), v[i & 3]);
+  const f32x2 w = add2(add2(v[0], v[1]), add2(v[2], v[3]));
+  const float ss = add_xor32(w.x + w.y);
+#endif
   return __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
 }
 
@@ -209,12 +278,17 @@ template <int MT, bool CENT = false>
 __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
   const float inv = row_inv_std<MT, CENT>(acc);  // acc now centred
   const float ga = X3_LEAKY_PRE * (sd * inv), gb = X3_LEAKY_PRE * mu;
+  const f32x2 ga2 = {ga, ga}, gb2 = {gb, gb};
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float y = fmaf(acc[m][q], ga, gb);
-      acc[m][q] = fmaf(fabsf(y), X3_LEAKY_C, y);
+    for (int i = 0; i < 8; ++i) {
+#if RG_X3_PKNORM
+      const f32x2 y = fma2(pair(acc[m], i), ga2, gb2);
+#else
+      const f32x2 y = {fmaf(acc[m][2 * i], ga, gb), fmaf(acc[m][2 * i + 1], ga, gb)};
+#endif
+      set_pair(acc[m], i, (f32x2){fmaf(fabsf(y.x), X3_LEAKY_C, y.x), fmaf(fabsf(y.y), X3_LEAKY_C, y.y)});
     }
 }
 
@@ -222,10 +296,44 @@ __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd
 template <int MT, bool CENT = false>
 __device__ __forceinline__ void norm_only(f32x16 (&acc)[MT], float mu, float sd) {
   const float ga = sd * row_inv_std<MT, CENT>(acc);
+  const f32x2 ga2 = {ga, ga}, mu2 = {mu, mu};
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[m][q] = fmaf(acc[m][q], ga, mu);
+    for (int i = 0; i < 8; ++i) set_pair(acc[m], i, fma2(pair(acc[m], i), ga2, mu2));
+}
+
+// A normalised layer's scale and activation applied when the NEXT layer reads it, eight
+// values per k-step (its B operand), instead of over the whole tile between the layers:
+// that VALU work then issues beside the next layer's MFMAs (layer_x3's one-step-ahead B).
+// PEND 1: norm + LeakyReLU (ga, gb as in norm_leaky), 2: norm only, 0: nothing pending.
+struct Pend {
+  float ga, gb;
+};
+template <int MT, bool CENT>
+__device__ __forceinline__ Pend pend_norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
+  const float inv = row_inv_std<MT, CENT>(acc);
+  return Pend{X3_LEAKY_PRE * (sd * inv), X3_LEAKY_PRE * mu};
+}
+template <int MT, bool CENT>
+__device__ __forceinline__ Pend pend_norm_only(f32x16 (&acc)[MT], float mu, float sd) {
+  return Pend{sd * row_inv_std<MT, CENT>(acc), mu};
+}
+template <int PEND>
+__device__ __forceinline__ X3 split_acc_pend(const f32x16& t, int hf, Pend p) {
+  if constexpr (PEND == 0) {
+    return split_acc(t, hf);
+  } else {
+    const int q = 8 * hf;
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float y = fmaf(t[q + i], p.ga, p.gb);
+      if constexpr (PEND == 1) y = fmaf(fabsf(y), X3_LEAKY_C, y);
+      v[i] = y;
+    }
+    return split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]});
+  }
 }
 
 }  // namespace x3
