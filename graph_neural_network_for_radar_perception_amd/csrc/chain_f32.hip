@@ -360,10 +360,7 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
     for (int l = 0; l < NL; ++l) {
       if (!spec_glob(SPEC, l)) {
         const int K = l == 0 ? K0 : Ks[l - 1];
-        const int n = fbytes(K, Ks[l]) / 16;
-        const f32x4* src = (const f32x4*)a.L[l].src;
-        f32x4* dst = (f32x4*)(lds + Off::get(l));
-        for (int i = threadIdx.x; i < n; i += FT) dst[i] = src[i];
+        stage_lds<FT>(lds + Off::get(l), a.L[l].src, fbytes(K, Ks[l]));
       }
     }
   }

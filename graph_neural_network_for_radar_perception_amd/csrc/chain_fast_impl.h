@@ -535,10 +535,7 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
 #pragma unroll
   for (int l = 0; l < RG_MAX_LAYERS; ++l) {
     if (l < a.nl) {
-      const u32x4* src = (const u32x4*)a.L[l].src;
-      u32x4* dst = (u32x4*)(lds + a.L[l].woff);
-      const int n = a.L[l].bytes / 16;
-      for (int i = threadIdx.x; i < n; i += FT) dst[i] = src[i];
+      stage_lds<FT>(lds + a.L[l].woff, a.L[l].src, a.L[l].bytes);
     }
   }
   __syncthreads();

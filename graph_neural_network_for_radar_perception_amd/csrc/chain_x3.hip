@@ -329,9 +329,7 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       if ((m >> p) & 1) {
-        const u32x4* src = (const u32x4*)(a.L[l].src + p * S::pl(l));
-        u32x4* dst = (u32x4*)(lds + S::woff(LM, l) + slot * S::pl(l));
-        for (int i = threadIdx.x; i < S::pl(l) / 16; i += FT) dst[i] = src[i];
+        stage_lds<FT>(lds + S::woff(LM, l) + slot * S::pl(l), a.L[l].src + p * S::pl(l), S::pl(l));
         ++slot;
       }
     }

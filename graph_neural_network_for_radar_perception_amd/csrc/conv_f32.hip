@@ -155,9 +155,7 @@ __global__ __launch_bounds__(FT) void conv_f32_kernel(Args a) {
     const int off[3] = {W_E_OFF, W_2_OFF, W_U_OFF};
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
-      const f32x4* s = (const f32x4*)a.w[l];
-      f32x4* d = (f32x4*)(lds + off[l]);
-      for (int i = threadIdx.x; i < nb[l] / 16; i += FT) d[i] = s[i];
+      stage_lds<FT>(lds + off[l], a.w[l], nb[l]);
     }
   }
   __syncthreads();
@@ -435,9 +433,7 @@ __global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
     const int off[2] = {W_E_OFF, W_2_OFF};
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
-      const f32x4* s = (const f32x4*)a.w[l];
-      f32x4* d = (f32x4*)(lds + off[l]);
-      for (int i = threadIdx.x; i < nb[l] / 16; i += FT2) d[i] = s[i];
+      stage_lds<FT2>(lds + off[l], a.w[l], nb[l]);
     }
   }
   __syncthreads();

@@ -180,10 +180,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // stage weights (static indices)
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
-    const u32x4* src = (const u32x4*)a.L[l].src;
-    u32x4* dstp = (u32x4*)(lds + a.L[l].woff);
-    const int n = a.L[l].bytes / 16;
-    for (int i = threadIdx.x; i < n; i += CT) dstp[i] = src[i];
+    stage_lds<CT>(lds + a.L[l].woff, a.L[l].src, a.L[l].bytes);
   }
   __syncthreads();
   CSTAMP(0);

@@ -240,9 +240,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     const int off[3] = {WE_OFF, W2_OFF, WU_OFF};
 #pragma unroll
     for (int l = 0; l < (RG_CX3_WU_LDS ? 3 : 2); ++l) {
-      const u32x4* s = (const u32x4*)a.w[l];
-      u32x4* d = (u32x4*)(lds + off[l]);
-      for (int i = threadIdx.x; i < nb[l] / 16; i += FT) d[i] = s[i];
+      stage_lds<FT>(lds + off[l], a.w[l], nb[l]);
     }
   }
   __syncthreads();
@@ -514,9 +512,7 @@ __global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
     const int off[2] = {NU_OFF, NPQ_OFF};
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
-      const u32x4* sp = (const u32x4*)src[l];
-      u32x4* d = (u32x4*)(lds + off[l]);
-      for (int i = threadIdx.x; i < nb[l] / 16; i += 512) d[i] = sp[i];
+      stage_lds<512>(lds + off[l], src[l], nb[l]);
     }
   }
   __syncthreads();
@@ -539,11 +535,7 @@ __global__ __launch_bounds__(PFT) void proj_x3_kernel(const float* x, int ldx, i
                                                       const char* wpq, float* pq) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int NB = x3_bytes(C, PQW);
-  {
-    const u32x4* s = (const u32x4*)wpq;
-    u32x4* d = (u32x4*)lds;
-    for (int i = threadIdx.x; i < NB / 16; i += PFT) d[i] = s[i];
-  }
+  stage_lds<PFT>(lds, wpq, NB);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;

@@ -488,9 +488,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
     // stage every layer's packed weights (+bias) into LDS once per workgroup
     for (int l = 0; l < a.nl; ++l) {
       const int nb = (l + 1 < a.nl ? sL[l + 1].woff : a.wbytes) - sL[l].woff;
-      const u32x4* src = (const u32x4*)sL[l].w;
-      u32x4* dst = (u32x4*)(wimg + sL[l].woff);
-      for (int i = threadIdx.x; i < nb / 16; i += CH_THREADS) dst[i] = src[i];
+      stage_lds<CH_THREADS>(wimg + sL[l].woff, sL[l].w, nb);
     }
     __syncthreads();
   }

@@ -180,6 +180,26 @@ __device__ __forceinline__ void act_dispatch(int act, F&& f) {
 // ---------------------------------------------------------------------------
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// Global -> LDS copy of a weight image by a whole workgroup of NT threads, UNR 16-B loads
+// in flight per thread.  (A plain load-store loop waits one full memory round trip per
+// 16 B per thread: 145 KB staged by 512 threads was 18 serial round trips.)
+template <int NT, int UNR = 8>
+__device__ __forceinline__ void stage_lds(void* lds_dst, const void* gsrc, int bytes) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u* s = (const v4u*)gsrc;
+  v4u* d = (v4u*)lds_dst;
+  const int n = bytes / 16;
+  int i = threadIdx.x;
+  for (; i + (UNR - 1) * NT < n; i += UNR * NT) {
+    v4u v[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) v[k] = s[i + k * NT];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) d[i + k * NT] = v[k];
+  }
+  for (; i < n; i += NT) d[i] = s[i];
+}
+
 // x[lane] + x[lane ^ 32] with v_permlane32_swap (a VALU lane exchange on gfx950; the
 // generic __shfl_xor goes through ds_bpermute and an LDS round trip on the critical path)
 __device__ __forceinline__ float add_xor32(float x) {

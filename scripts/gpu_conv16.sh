@@ -18,6 +18,7 @@ print(' ', sys.argv[1], 'value', d['value'], 'ms', d['ms_per_step'], {k: v['avg_
 PY
 done
 export RG_LIBRARY=graph_neural_network_for_radar_perception_amd/lib/variants/libradargnn_cstamp.so
+[ -f $RG_LIBRARY ] || exit 0
 for c in c5 c2; do
   timeout -k 10 200 python scripts/conv_stamps.py $c > gpurun_out/c16/st_$c.txt 2>&1 || exit $?
   echo "stamps $c"; tail -n 7 gpurun_out/c16/st_$c.txt
