@@ -95,6 +95,9 @@ def parse():
     p.add_argument('--cpu-frames', type=int, default=None,
                    help='CPU baseline sample (timed frames)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--fine-events', action='store_true',
+                   help='time every launch with its own HIP event pair (adds ~10 us of stream '
+                        'gap per pair to the timed steps)')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
@@ -247,6 +250,15 @@ def log(msg: str):
     print(f'[bench {time.perf_counter() - T_START:7.1f}s] {msg}', file=sys.stderr, flush=True)
 
 
+class EventList(list):
+    """(name, event) pairs; coarse: engine.forward_batched records one pair around the
+    whole conv stack ('conv_stack') instead of one per launch."""
+
+    def __init__(self, coarse: bool = False):
+        super().__init__()
+        self.coarse = coarse
+
+
 def event_durations(events):
     """(name:start, name:end) event pairs -> {name: [ms, ...]}"""
     out, open_ = {}, {}
@@ -263,7 +275,9 @@ def pmc_traffic(args, kernel_substr):
     """HBM bytes per launch of the roofline kernel from the newest committed PMC table
     (profiles/rNN_pmc_traffic.json, written by scripts/pmc_traffic.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command), or None when
-    no table was collected for this workload."""
+    no table was collected for this workload.  kernel_substr: a name substring, or
+    [(substring, weight), ...] summed (every part must be in the table)."""
+    parts = [(kernel_substr, 1.0)] if isinstance(kernel_substr, str) else list(kernel_substr)
     import glob
     want = {'frames': args.frames, 'nodes': args.nodes, 'k': args.k, 'layers': args.layers,
             'dtype': args.dtype}
@@ -274,9 +288,15 @@ def pmc_traffic(args, kernel_substr):
         doc = json.load(open(path))
         if doc.get('workload') != want:
             continue
-        for name, rec in doc['kernels'].items():
-            if kernel_substr in name:
-                return float(rec['traffic_bytes']), os.path.relpath(path, REPO)
+        total, found = 0.0, 0
+        for sub, w in parts:
+            for name, rec in doc['kernels'].items():
+                if sub in name:
+                    total += w * float(rec['traffic_bytes'])
+                    found += 1
+                    break
+        if found == len(parts):
+            return total, os.path.relpath(path, REPO)
     return None, None
 
 
@@ -683,7 +703,10 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         E = int(gb.n_edges_dev.item())
         log(f'{args.config}: warm-up done, E = {E}; timing {args.steps} steps')
         # ---- timed region: K full steps -----------------------------------------
-        events = []
+        # coarse events: one pair around the edge encoder and one around the conv stack
+        # per step (a pair per launch cost ~10 us of stream gap each); --fine-events
+        # times every launch
+        events = EventList(coarse=not args.fine_events)
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -693,6 +716,8 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         barrier(world)
         elapsed = max_over_ranks(time.perf_counter() - t0, world)
         durs = event_durations(events)
+        if 'conv_stack' in durs:  # per-layer launch time = span / layers
+            durs['conv_fused'] = [ms / args.layers for ms in durs.pop('conv_stack')]
         # ---- forward only (graph + features already built) -----------------------
         barrier(world)
         torch.cuda.synchronize()
@@ -726,15 +751,18 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         #    + msg1, per node the update: 49152 E + 32768 N
         # The reference form (SURVEY §8(d), msg0 over all 192 inputs per edge: 65536 E +
         # 16384 N) is reported beside it as reference_form_tflops.
-        #  fp32 x3 (rg_conv_layer_x3, the default): one launch = W_e e + msg1 per edge, the
-        #    update per node, and the NEXT layer's P | Q per node in L - 1 of the L launches
-        #    (the first layer's P | Q is its own launch, conv_proj): 32768 E + 16384 N +
-        #    32768 N (L - 1) / L on average
+        #  fp32 x3 (rg_conv_layer_x3, the default): one layer = W_e e + msg1 per edge, the
+        #    update per node, and the NEXT layer's P | Q per node (the first layer's P | Q
+        #    is rg_conv_proj_x3): timed as one span over the whole stack (proj + L layers),
+        #    so per layer 32768 E + 16384 N + 32768 N
+        #    (--fine-events: the layer launches alone, 32768 E + 16384 N + 32768 N (L-1)/L)
         from graph_neural_network_for_radar_perception_amd import engine as _eng
         ms = float(np.mean(durs['conv_fused']))
         ref_flops = 65536.0 * E + 16384.0 * N
         x3 = args.dtype == 'fp32' and _eng.F32_ARITH == 'x3'
-        if x3:
+        if x3 and not args.fine_events:
+            flops = 32768.0 * E + 49152.0 * N
+        elif x3:
             flops = 32768.0 * E + 16384.0 * N + 32768.0 * N * (args.layers - 1) / args.layers
         elif args.dtype == 'fp32':
             flops = 32768.0 * E + 49152.0 * N
@@ -759,8 +787,14 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
                      'gnn_blocks.py:96-113)')
         else:
             kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
-        traffic, tsrc = pmc_traffic(args, 'conv_x3' if x3 else (
-            'conv_f32' if args.dtype == 'fp32' else 'fused_conv'))
+        if x3 and not args.fine_events:  # one layer of the stack: edge + node launches + proj / L
+            tparts = [('conv_x3_kernel', 1.0), ('node_x3_kernel', 1.0),
+                      ('proj_x3_kernel', 1.0 / args.layers)]
+        elif x3:
+            tparts = [('conv_x3_kernel', 1.0), ('node_x3_kernel', 1.0)]
+        else:
+            tparts = 'conv_f32' if args.dtype == 'fp32' else 'fused_conv'
+        traffic, tsrc = pmc_traffic(args, tparts)
     else:
         # message chain: gather x_i, x_j, e -> 192->128->64 MLP (norm + act) -> messages
         ms = float(np.mean(durs['message_chain']))
@@ -796,7 +830,10 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         roof = {'kernel': kname, 'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'frac': round(frac_hbm, 4), 'traffic': traffic,
                 'mfma_frac': round(frac_mfma, 4)}
-    roof.update(avg_ms=round(ms, 4), timing='HIP events on the launch stream, timed region',
+    roof.update(avg_ms=round(ms, 4),
+                timing=('HIP events on the launch stream, timed region: ' +
+                        ('one pair per launch' if args.fine_events else
+                         'one pair around the conv stack per step, avg = span / layers')),
                 flops_per_launch=flops)
     if ref_tf is not None:
         roof['reference_form_tflops'] = round(ref_tf, 2)
