@@ -21,8 +21,11 @@ static constexpr int CW = CT / 64;
 static constexpr int NB = 8;         // destination nodes per work block
 static constexpr int C = 64;         // node / edge / message / output channels
 static constexpr int HID = 128;      // msg_mlp_hidden_dim
-// wave-private LDS: P (NB x HID f32), message tile (32 x C bf16), slots (32 int)
-static constexpr int WAVE_LDS = NB * HID * 4 + 32 * C * 2 + 128;
+// wave-private LDS: P (NB rows of HID f32, row stride PST: the 4-float pad puts the rows of
+// different nodes on different banks -- at HID they all mapped to the same four), message
+// tile (32 x C bf16), slots (32 int)
+static constexpr int PST = HID + 4;
+static constexpr int WAVE_LDS = NB * PST * 4 + 32 * C * 2 + 128;
 static constexpr float NORM_EPS = 1e-5f;
 // Work-block heads: one per XCD (workgroup b runs on XCD b % 8), each on a 128-B line of
 // its own.  One shared head saturates at ~88 dequeues/us (MI355X_MICROARCH.md, dequeue):
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
   char* wbase = lds + a.total_bytes + wave * WAVE_LDS;
   float* P = (float*)wbase;
-  uint16_t* tile = (uint16_t*)(wbase + NB * HID * 4);
+  uint16_t* tile = (uint16_t*)(wbase + NB * PST * 4);
   int* slots = (int*)((char*)tile + 32 * C * 2);
   const char* w0 = lds + a.L[0].woff;
   const char* w1 = lds + a.L[1].woff;
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       f32x16 acc1[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * HID, m, h);
+        acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * PST, m, h);
       mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
       if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
       bf16x8_t b2[8];
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       if (r < NB) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          f32x4* pw = (f32x4*)(P + r * HID + (2 * m + h) * 16);
+          f32x4* pw = (f32x4*)(P + r * PST + (2 * m + h) * 16);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             pw[q] = (f32x4){accp[m][4 * q], accp[m][4 * q + 1], accp[m][4 * q + 2], accp[m][4 * q + 3]};

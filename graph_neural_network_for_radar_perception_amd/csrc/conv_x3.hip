@@ -83,6 +83,9 @@ static constexpr int NW = FT / 64;
 #ifndef RG_CX3_JIT
 #define RG_CX3_JIT 1  // message layer 1's norm scale + act applied in layer 2's B operand
 #endif
+#ifndef RG_CX3_NODE_PF
+#define RG_CX3_NODE_PF 0  // 1: node launch loads the next tile's rows while a tile computes (M: slower, 256 VGPRs)
+#endif
 #ifndef RG_CX3_NODE_KERNEL
 #define RG_CX3_NODE_KERNEL 1  // the update / projection phase as a second launch (LDS weights)
 #endif
@@ -158,39 +161,54 @@ struct Args {
   int aggr_mean;
 };
 
+// the rows the node phase of nodes n0 .. n1 - 1 reads first (lane r = node): the segment
+// bounds (degree), x[node] and agg[node] in k order (features 16 s + 8 h .. + 7)
+struct NodeRows {
+  int s0, s1;
+  f32x4 xb[4][2], ab[4][2];
+};
+__device__ __forceinline__ void load_node_rows(const Args& a, int n0, int n1, int lane,
+                                               NodeRows& w) {
+  const int r = lane & 31, h = lane >> 5;
+  const int node = n0 + r;
+  const int nrow = node < n1 ? node : n0;
+  w.s0 = a.seg_ptr[nrow];
+  w.s1 = a.seg_ptr[nrow + 1];
+  const float* px = a.x + (size_t)nrow * a.ldx;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w.xb[s][0] = *(const f32x4*)(px + 16 * s + 8 * h);
+    w.xb[s][1] = *(const f32x4*)(px + 16 * s + 8 * h + 4);
+  }
+  const f32x4* pa = (const f32x4*)(a.agg + (size_t)nrow * C + 8 * h);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w.ab[s][0] = __builtin_nontemporal_load(pa + 4 * s);
+    w.ab[s][1] = __builtin_nontemporal_load(pa + 4 * s + 1);
+  }
+}
+
 // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109) for the 32
-//      nodes n0 .. n1 - 1 (lane r = node), then -- when a.pq_out is set -- the next layer's
-//      projections from the same registers
+//      nodes n0 .. n1 - 1 (lane r = node) from their loaded rows, then -- when a.pq_out is
+//      set -- the next layer's projections from the same registers
 template <bool CENT, typename WU, typename WP>
-__device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const WU& wU,
-                                            const float* biasU, const WP& wPQ,
-                                            const float* biasPQ, float muU, float sdU, int lane) {
+__device__ __forceinline__ void node_compute(const Args& a, const NodeRows& w, int n0, int n1,
+                                             const WU& wU, const float* biasU, const WP& wPQ,
+                                             const float* biasPQ, float muU, float sdU, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int node = n0 + r;
   const bool nvalid = node < n1;
   const int nrow = nvalid ? node : n0;
-  const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 0;
-  const float* px = a.x + (size_t)nrow * a.ldx;
-  f32x4 xb[4][2], ab[4][2];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    xb[s][0] = *(const f32x4*)(px + 16 * s + 8 * h);
-    xb[s][1] = *(const f32x4*)(px + 16 * s + 8 * h + 4);
-  }
+  const int deg = nvalid ? w.s1 - w.s0 : 0;
+  f32x4 ab[4][2];
   {
-    const f32x4* pa = (const f32x4*)(a.agg + (size_t)nrow * C + 8 * h);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      ab[s][0] = __builtin_nontemporal_load(pa + 4 * s);
-      ab[s][1] = __builtin_nontemporal_load(pa + 4 * s + 1);
-    }
     // no incoming edges: PyG leaves the aggregate at zero; mean = sum / max(count, 1)
     const float sc = deg > 0 ? (float)deg : 1.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        f32x4 v = deg > 0 ? ab[s][u] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        f32x4 v = deg > 0 ? w.ab[s][u] : (f32x4){0.f, 0.f, 0.f, 0.f};
         if (a.aggr_mean) v = (f32x4){div_rn(v.x, sc), div_rn(v.y, sc), div_rn(v.z, sc), div_rn(v.w, sc)};
         ab[s][u] = v;
       }
@@ -199,11 +217,11 @@ __device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const
 #pragma unroll
   for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
   layer_x3<8, 2, 2, true>(accu, wU, 0, [&](int s) {
-    return s < 4 ? split8(xb[s][0], xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
+    return s < 4 ? split8(w.xb[s][0], w.xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
   });
   norm_leaky<2, CENT>(accu, muU, sdU);
   {
-    const float* pxr = px + 4 * h;  // x[node] in accumulator order for the residual
+    const float* pxr = a.x + (size_t)nrow * a.ldx + 4 * h;  // x[node] in accumulator order
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -225,6 +243,15 @@ __device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const
                                                  accu[m][4 * g + 2], accu[m][4 * g + 3]};
   }
   if (a.pq_out) project_rows(accu, wPQ, biasPQ, a.pq_out + (size_t)nrow * PQW, nvalid, lane);
+}
+
+template <bool CENT, typename WU, typename WP>
+__device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const WU& wU,
+                                            const float* biasU, const WP& wPQ,
+                                            const float* biasPQ, float muU, float sdU, int lane) {
+  NodeRows w;
+  load_node_rows(a, n0, n1, lane, w);
+  node_compute<CENT>(a, w, n0, n1, wU, biasU, wPQ, biasPQ, muU, sdU, lane);
 }
 
 template <bool CENT, bool NODE>
@@ -523,9 +550,30 @@ __global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
   const float* biasPQ = (const float*)(lds + NPQ_OFF + 3 * plane_bytes(C, PQW));
   const float muU = nrm[0], sdU = nrm[1];
   const int ntiles = (a.n_nodes + 31) / 32;
-  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8)
+  const int stride = gridDim.x * 8;
+  // the next tile's rows are loaded while this one computes; unrolled by two with separate
+  // row buffers (a register copy of a loaded value would wait for the load)
+#if !RG_CX3_NODE_PF
+  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += stride)
     node_update<CENT>(a, 32 * t, min(32 * t + 32, a.n_nodes), wU, biasU, wPQ, biasPQ, muU, sdU,
                       lane);
+  return;
+#endif
+  NodeRows rA, rB;
+  int t = blockIdx.x * 8 + wave;
+  auto tile_end = [&](int tt) { return min(32 * tt + 32, a.n_nodes); };
+  if (t < ntiles) load_node_rows(a, 32 * t, tile_end(t), lane, rA);
+  while (t < ntiles) {
+    int tn = t + stride;
+    if (tn < ntiles) load_node_rows(a, 32 * tn, tile_end(tn), lane, rB);
+    node_compute<CENT>(a, rA, 32 * t, tile_end(t), wU, biasU, wPQ, biasPQ, muU, sdU, lane);
+    t = tn;
+    if (t >= ntiles) break;
+    tn = t + stride;
+    if (tn < ntiles) load_node_rows(a, 32 * tn, tile_end(tn), lane, rA);
+    node_compute<CENT>(a, rB, 32 * t, tile_end(t), wU, biasU, wPQ, biasPQ, muU, sdU, lane);
+    t = tn;
+  }
 }
 
 // P | Q = W_pq x + [b1; 0] for dense float32 rows (the first layer's projections):
