@@ -88,6 +88,7 @@ _SIGNATURES = {
     'rg_pairs_from_edge_index_workspace_size': (_S, [_L]),
     'rg_pairs_from_edge_index': (_I, [_P, _L, _P, _P, _P, _P, _S, _P]),
     'rg_csr_rows': (_I, [_P, _I, _P, _P]),
+    'rg_csr_clamp': (_I, [_P, _I, _P, _L, _P, _P]),
     # real-data front-end (frontend.hip)
     'rg_frontend_sync': (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P,
                               _P, _P]),

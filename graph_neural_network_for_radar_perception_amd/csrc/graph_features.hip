@@ -528,6 +528,42 @@ extern "C" int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* strea
   return RG_OK;
 }
 
+// Capacity guard of a radius graph built into a capacity that was not checked on the host
+// first: need[0] = the true edge count; when it exceeds cap, the CSR is cut at the last row
+// boundary <= cap (rows past it were not written by row_emit) and n_edges = that boundary,
+// so every consumer stays inside the arrays.  One workgroup.
+__global__ __launch_bounds__(1024) void csr_clamp_kernel(int* __restrict__ row_ptr, int n,
+                                                          int* __restrict__ n_edges, long cap,
+                                                          int* __restrict__ need) {
+  __shared__ int cut;
+  const int E = *n_edges;
+  if (threadIdx.x == 0) need[0] = E;
+  if ((long)E <= cap) return;  // uniform
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n;  // the largest j with row_ptr[j] <= cap (row_ptr[0] = 0)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((long)row_ptr[mid] <= cap) lo = mid;
+      else hi = mid - 1;
+    }
+    cut = row_ptr[lo];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i <= n; i += blockDim.x)
+    if (row_ptr[i] > cut) row_ptr[i] = cut;
+  if (threadIdx.x == 0) *n_edges = cut;
+}
+
+extern "C" int rg_csr_clamp(int* row_ptr, int n_rows, int* n_edges_dev, long capacity,
+                            int* need_out, void* stream) {
+  RG_REQUIRE(row_ptr && n_edges_dev && need_out && n_rows >= 0, RG_ERR_ARG,
+             "rg_csr_clamp: null argument");
+  csr_clamp_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(row_ptr, n_rows, n_edges_dev, capacity,
+                                                       need_out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" size_t rg_pairs_from_edge_index_workspace_size(long n_edges) {
   return 2 * align256((size_t)(n_edges + 1) * sizeof(int)) + align256(scan_workspace_bytes(n_edges));
 }

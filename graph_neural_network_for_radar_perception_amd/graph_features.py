@@ -185,9 +185,24 @@ class GraphBatch:
     graph: engine.DeviceGraph    # destination-major view + link pairs
     node_features: torch.Tensor  # float32 [N, 6]
     edge_features: torch.Tensor  # float32 [cap, 7], destination-major order
+    # radius graphs built into an unchecked capacity: device int32[1] = the true edge count
+    # (rg_csr_clamp); None when the capacity was checked on the host (or is exact, kNN)
+    need_dev: Optional[torch.Tensor] = None
+
+    def check_capacity(self):
+        """Raise if this graph was cut to its capacity (a radius graph built without a host
+        sync whose edges outgrew the capacity that sufficed before): every output computed
+        from it is invalid.  Host sync."""
+        if self.need_dev is not None:
+            need = int(self.need_dev.item())
+            if need > self.capacity:
+                raise RuntimeError(f'radius graph needed {need} edges but was built into a '
+                                   f'capacity of {self.capacity}; this step\'s outputs are '
+                                   f'invalid (the next build uses a larger capacity)')
 
     def edge_index(self) -> torch.Tensor:
         """int64 [2, E] in the reference's np.where order (host sync for E)."""
+        self.check_capacity()
         E = int(self.n_edges_dev.item())
         return torch.stack((self.graph.dst[:E], self.col[:E]), 0).to(torch.int64)
 
@@ -199,15 +214,29 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
     link pairs."""
     k = cfg.k_number_nearest_points if k is None else k
     eps2 = cfg.ball_query_eps_square if eps2 is None else eps2
-    # radius graphs have no a-priori edge bound: the capacity that sufficed last time
-    # (kept in ws_cache) is tried first, then checked (one host sync) and rebuilt if short
+    # radius graphs have no a-priori edge bound.  First build (nothing cached): built,
+    # checked with one host sync and rebuilt if short.  Later builds use the cached
+    # capacity WITHOUT a host sync: rg_csr_clamp keeps an overflowing graph in bounds and
+    # records the true edge count, read back asynchronously (pinned copy + event) and
+    # checked at the next build -- a short capacity grows there -- and by
+    # GraphBatch.check_capacity() (called by edge_index() / RadarGNNPipeline.trim()).
     cap_key = ('radius_cap', mode, float(eps2))
+    pend_key = ('radius_need', mode, float(eps2))
     cap0 = ws_cache.get(cap_key) if (ws_cache is not None and mode != nat.GRAPH_KNN) else None
+    if cap0 is not None:
+        pend = ws_cache.get(pend_key)
+        if pend is not None and pend[1].query():  # the previous build's count has landed
+            need = int(pend[0][0])
+            if need > cap0:
+                cap0 = need + need // 4
+                ws_cache[cap_key] = cap0
+            ws_cache.pop(pend_key)
     row_ptr, col, deg, ne, cap = engine.build_graph(batch.arrays['meas_px'],
                                                     batch.arrays['meas_py'], batch.frame_ptr,
                                                     batch.frame_sizes, k, eps2, mode,
                                                     edge_capacity=cap0, ws_cache=ws_cache)
-    if mode != nat.GRAPH_KNN:
+    need_dev = None
+    if mode != nat.GRAPH_KNN and cap0 is None:
         E = int(ne.item())
         if E > cap:
             row_ptr, col, deg, ne, cap = engine.build_graph(
@@ -215,9 +244,19 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
                 batch.frame_sizes, k, eps2, mode, edge_capacity=E, ws_cache=ws_cache)
         if ws_cache is not None:
             ws_cache[cap_key] = cap
+    elif mode != nat.GRAPH_KNN:
+        need_dev = torch.empty(1, dtype=torch.int32, device=row_ptr.device)
+        nat.check(nat.lib().rg_csr_clamp(row_ptr.data_ptr(), batch.n_nodes, ne.data_ptr(), cap,
+                                         need_dev.data_ptr(), nat.stream_ptr(row_ptr.device)),
+                  'rg_csr_clamp')
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(need_dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(row_ptr.device))
+        ws_cache[pend_key] = (host, ev)
     g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
     g.set_frames(batch.frame_ptr, batch.n_frames)
     nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)
     # destination-major edge (src = g.src[p] -> dst = g.dst[p])
     ef = engine.edge_features(batch.arrays, g.src, g.dst, ne, cap)
-    return GraphBatch(row_ptr, col, deg, ne, cap, g, nf, ef)
+    return GraphBatch(row_ptr, col, deg, ne, cap, g, nf, ef, need_dev)

@@ -3,9 +3,10 @@ input features -> GNN forward -> four task heads, on one GPU.
 
 One ``step`` = ``datagen_gnn.py:104-124`` (graph + features) for every frame of
 the batch followed by ``Model_Inference.forward`` (gnn_detector.py:141-201) over
-the batch, with no host synchronisation inside (capacities are exact upper
-bounds for kNN graphs), so a step can be timed with HIP events or captured in a
-HIP graph.
+the batch, with no host synchronisation inside: capacities are exact upper
+bounds for kNN graphs, and a radius graph syncs once, on its first build, then
+reuses that capacity behind a device-side guard (rg_csr_clamp; checked lazily,
+GraphBatch.check_capacity).  A step can be timed with HIP events.
 """
 from __future__ import annotations
 
@@ -50,6 +51,8 @@ class RadarGNNPipeline:
 
     @staticmethod
     def trim(gb: GraphBatch, out: engine.ForwardOutputs):
-        """Host-synchronising view of the outputs at their true sizes."""
+        """Host-synchronising view of the outputs at their true sizes (raises if a radius
+        graph built without a host sync outgrew its capacity: GraphBatch.check_capacity)."""
+        gb.check_capacity()
         U = int(gb.graph.n_pairs_dev.item())
         return out.node_cls, out.node_reg, out.link_cls[:U], out.obj_cls

@@ -191,6 +191,16 @@ int rg_pairs_from_edge_index(const int64_t* edge_index, long n_edges, int* pair_
 /* out[p] = row of CSR position p (edge_index[0]; destination of a dst-major edge). */
 int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream);
 
+/* Capacity guard for a graph built by rg_build_graph into a capacity the host has not
+ * checked (radius graphs without a host sync, graph_features.py:build_graph_batch):
+ * need_out[0] = the true edge count (device int32); if it exceeds capacity, row_ptr is cut
+ * at the last row boundary <= capacity (the rows rg_build_graph left unwritten become
+ * empty) and *n_edges_dev = that boundary, so every consumer stays in bounds.  The host
+ * reads need_out later (no sync on the launch path) and treats the step as invalid when
+ * need_out[0] > capacity. */
+int rg_csr_clamp(int* row_ptr, int n_rows, int* n_edges_dev, long capacity, int* need_out,
+                 void* stream);
+
 /* Destination-major CSR of an arbitrary edge_index (int64[2][E], reference order):
  * dst_ptr int32[n_nodes+1]; perm int32[E] (dst-major position -> reference
  * position), ordered by (dst, src, reference position); src_sorted int32[E]. */
