@@ -530,8 +530,10 @@ extern "C" int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* strea
 
 // Capacity guard of a radius graph built into a capacity that was not checked on the host
 // first: need[0] = the true edge count; when it exceeds cap, the CSR is cut at the last row
-// boundary <= cap (rows past it were not written by row_emit) and n_edges = that boundary,
-// so every consumer stays inside the arrays.  One workgroup.
+// boundary <= cap / 2 (rows past cap were not written by row_emit; and a cut graph is no
+// longer symmetric, so its i < j link pairs are bounded only by its edge count, while the
+// pair arrays hold cap / 2 + 1) and n_edges = that boundary, so every consumer stays
+// inside its arrays.  One workgroup.
 __global__ __launch_bounds__(1024) void csr_clamp_kernel(int* __restrict__ row_ptr, int n,
                                                           int* __restrict__ n_edges, long cap,
                                                           int* __restrict__ need) {
@@ -540,10 +542,10 @@ __global__ __launch_bounds__(1024) void csr_clamp_kernel(int* __restrict__ row_p
   if (threadIdx.x == 0) need[0] = E;
   if ((long)E <= cap) return;  // uniform
   if (threadIdx.x == 0) {
-    int lo = 0, hi = n;  // the largest j with row_ptr[j] <= cap (row_ptr[0] = 0)
+    int lo = 0, hi = n;  // the largest j with row_ptr[j] <= cap / 2 (row_ptr[0] = 0)
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if ((long)row_ptr[mid] <= cap) lo = mid;
+      if ((long)row_ptr[mid] <= cap / 2) lo = mid;
       else hi = mid - 1;
     }
     cut = row_ptr[lo];

@@ -1,5 +1,6 @@
 // Exclusive prefix sums (int32) used by every CSR builder in the library.
-// Three launches: per-block sums -> scan of the block sums -> add offsets.
+// Small arrays: one launch (scan_small); larger: three launches, per-block sums -> scan of
+// the block sums -> add offsets.
 #include "rg_common.h"
 #include "scan.h"
 
@@ -91,12 +92,63 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_apply(const int* __restrict__
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) out[n] = ex;
 }
 
+// n <= SMALL_N: ONE launch of one 1024-thread workgroup, 32 consecutive elements per
+// thread (all its loads in flight at once).  The three-launch form costs ~15 us of launch
+// floor for what is a few us of work on the small arrays of the graph builders (a 20k-node
+// frame's row counts, the grid cells).
+static constexpr int SMALL_T = 1024;
+static constexpr int SMALL_I = 32;
+static constexpr long SMALL_N = (long)SMALL_T * SMALL_I;
+
+__global__ __launch_bounds__(SMALL_T) void scan_small(const int* __restrict__ in, long n,
+                                                      int* __restrict__ out,
+                                                      int* __restrict__ total_out) {
+  __shared__ int wsum[SMALL_T / 64];
+  const long base = (long)threadIdx.x * SMALL_I;
+  int v[SMALL_I];
+  int s = 0;
+#pragma unroll
+  for (int t = 0; t < SMALL_I; ++t) {
+    const long i = base + t;
+    v[t] = i < n ? in[i] : 0;
+  }
+#pragma unroll
+  for (int t = 0; t < SMALL_I; ++t) s += v[t];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int inc = wave_incl_scan(s);
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < SMALL_T / 64; ++w) {
+    const int x = wsum[w];
+    if (w < wid) off += x;
+    tot += x;
+  }
+  int ex = off + inc - s;
+#pragma unroll
+  for (int t = 0; t < SMALL_I; ++t) {
+    const long i = base + t;
+    if (i < n) out[i] = ex;
+    ex += v[t];
+  }
+  if (threadIdx.x == 0) {
+    out[n] = tot;
+    if (total_out) *total_out = tot;
+  }
+}
+
 size_t scan_workspace_bytes(long n) {
   long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   return (size_t)((nb + 1 + 63) / 64 * 64) * sizeof(int);
 }
 
 int exclusive_scan(const int* in, long n, int* out, int* total_out, void* ws, hipStream_t st) {
+  if (n <= SMALL_N) {
+    scan_small<<<1, SMALL_T, 0, st>>>(in, n, out, total_out);
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
   long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (nb == 0) nb = 1;
   int* sums = (int*)ws;

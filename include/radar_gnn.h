@@ -194,10 +194,10 @@ int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream);
 /* Capacity guard for a graph built by rg_build_graph into a capacity the host has not
  * checked (radius graphs without a host sync, graph_features.py:build_graph_batch):
  * need_out[0] = the true edge count (device int32); if it exceeds capacity, row_ptr is cut
- * at the last row boundary <= capacity (the rows rg_build_graph left unwritten become
- * empty) and *n_edges_dev = that boundary, so every consumer stays in bounds.  The host
+ * at a row boundary (the rows rg_build_graph left unwritten become empty) and *n_edges_dev = that boundary, so every consumer stays in bounds.  The host
  * reads need_out later (no sync on the launch path) and treats the step as invalid when
- * need_out[0] > capacity. */
+ * need_out[0] > capacity.  (The cut is at the last boundary <= capacity / 2: a cut graph is
+ * not symmetric, and the link-pair arrays hold capacity / 2 + 1 pairs.) */
 int rg_csr_clamp(int* row_ptr, int n_rows, int* n_edges_dev, long capacity, int* need_out,
                  void* stream);
 

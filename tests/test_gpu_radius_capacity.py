@@ -62,7 +62,8 @@ def test_radius_short_capacity_is_guarded_then_grows(cuda_device):
         assert int(gb.need_dev.item()) == E
         rp = gb.row_ptr.cpu().numpy()
         ne = int(gb.n_edges_dev.item())
-        assert ne <= short and rp[-1] == ne and np.all(np.diff(rp) >= 0)
+        assert ne <= short // 2 and rp[-1] == ne and np.all(np.diff(rp) >= 0)
+        assert int(gb.graph.n_pairs_dev.item()) <= gb.capacity // 2 + 1
         with pytest.raises(RuntimeError, match='capacity'):
             gb.check_capacity()
         with pytest.raises(RuntimeError, match='capacity'):
