@@ -92,30 +92,54 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_apply(const int* __restrict__
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) out[n] = ex;
 }
 
-// n <= SMALL_N: ONE launch of one 1024-thread workgroup, 32 consecutive elements per
-// thread (all its loads in flight at once).  The three-launch form costs ~15 us of launch
-// floor for what is a few us of work on the small arrays of the graph builders (a 20k-node
-// frame's row counts, the grid cells).
+// n <= SMALL_N: ONE launch of one 1024-thread workgroup.  Wave w owns the contiguous chunk
+// [2048 w, 2048 w + 2048): coalesced loads into LDS, then lane l scans the 32 consecutive
+// elements 32 l .. 32 l + 31 of its chunk serially in registers (LDS rows padded by one
+// word per 32: conflict-free), one wave scan of the lane sums, the 16 chunk totals through
+// LDS, and coalesced stores.  The three-launch form costs ~15 us of launch floor for a few
+// us of work on the graph builders' small arrays.
 static constexpr int SMALL_T = 1024;
 static constexpr int SMALL_I = 32;
 static constexpr long SMALL_N = (long)SMALL_T * SMALL_I;
+static constexpr int CHUNK = 64 * SMALL_I;           // elements per wave
+static constexpr int CHUNK_P = CHUNK + CHUNK / 32;   // padded LDS words per wave
+
+__device__ __forceinline__ int pad32(int j) { return j + (j >> 5); }
 
 __global__ __launch_bounds__(SMALL_T) void scan_small(const int* __restrict__ in, long n,
                                                       int* __restrict__ out,
                                                       int* __restrict__ total_out) {
-  __shared__ int wsum[SMALL_T / 64];
-  const long base = (long)threadIdx.x * SMALL_I;
+  extern __shared__ int sm[];  // SMALL_T / 64 chunk totals, then the padded chunks
+  int* wsum = sm;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int* ch = sm + SMALL_T / 64 + wid * CHUNK_P;
+  const long base = (long)wid * CHUNK;
+  {
+    int v[SMALL_I];
+#pragma unroll
+    for (int k = 0; k < SMALL_I; ++k) {
+      const long i = base + 64 * k + lane;
+      v[k] = i < n ? in[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < SMALL_I; ++k) ch[pad32(64 * k + lane)] = v[k];
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's chunk is in LDS
+  __builtin_amdgcn_wave_barrier();
   int v[SMALL_I];
   int s = 0;
 #pragma unroll
   for (int t = 0; t < SMALL_I; ++t) {
-    const long i = base + t;
-    v[t] = i < n ? in[i] : 0;
+    v[t] = ch[pad32(SMALL_I * lane + t)];
   }
 #pragma unroll
-  for (int t = 0; t < SMALL_I; ++t) s += v[t];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int t = 0; t < SMALL_I; ++t) {
+    const int x = v[t];
+    v[t] = s;
+    s += x;
+  }
   const int inc = wave_incl_scan(s);
+  const int lane_off = inc - s;
   if (lane == 63) wsum[wid] = inc;
   __syncthreads();
   int off = 0, tot = 0;
@@ -125,18 +149,21 @@ __global__ __launch_bounds__(SMALL_T) void scan_small(const int* __restrict__ in
     if (w < wid) off += x;
     tot += x;
   }
-  int ex = off + inc - s;
 #pragma unroll
-  for (int t = 0; t < SMALL_I; ++t) {
-    const long i = base + t;
-    if (i < n) out[i] = ex;
-    ex += v[t];
+  for (int t = 0; t < SMALL_I; ++t) ch[pad32(SMALL_I * lane + t)] = off + lane_off + v[t];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < SMALL_I; ++k) {
+    const long i = base + 64 * k + lane;
+    if (i < n) out[i] = ch[pad32(64 * k + lane)];
   }
   if (threadIdx.x == 0) {
     out[n] = tot;
     if (total_out) *total_out = tot;
   }
 }
+static constexpr int SMALL_LDS = (SMALL_T / 64 + (SMALL_T / 64) * CHUNK_P) * 4;
 
 size_t scan_workspace_bytes(long n) {
   long nb = (n + SCAN_TILE - 1) / SCAN_TILE;
@@ -145,7 +172,8 @@ size_t scan_workspace_bytes(long n) {
 
 int exclusive_scan(const int* in, long n, int* out, int* total_out, void* ws, hipStream_t st) {
   if (n <= SMALL_N) {
-    scan_small<<<1, SMALL_T, 0, st>>>(in, n, out, total_out);
+    RG_ENSURE_LDS(scan_small, SMALL_LDS);
+    scan_small<<<1, SMALL_T, SMALL_LDS, st>>>(in, n, out, total_out);
     RG_LAUNCH_CHECK();
     return RG_OK;
   }
