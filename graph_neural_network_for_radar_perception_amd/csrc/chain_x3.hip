@@ -24,7 +24,8 @@ namespace cx3 {
 using namespace ::rg::x3;
 
 #ifndef RG_X3_DB
-#define RG_X3_DB true  // double-buffered weight fragments in the chained layers (M: edge encoder 1.52 -> 1.45 ms)
+#define RG_X3_DB 1  // weight fragments read this many k-steps ahead in the chained layers
+                    // (1 vs 0, M: edge encoder 1.52 -> 1.45 ms)
 #endif
 
 enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused into layer 1

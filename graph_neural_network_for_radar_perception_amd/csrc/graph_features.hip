@@ -40,8 +40,21 @@ __global__ __launch_bounds__(256) void node_features_kernel(
   if (b + (int)blockIdx.x * 256 >= e) return;  // block-uniform: no chunk of this frame
   __shared__ long long smin[256], smax[256];
   long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000ULL;
-  for (int i = b + threadIdx.x; i < e; i += 256) {
-    long long t = ts[i];
+  // eight loads in flight per thread (a one-load loop over a 20 000-node frame waited 79
+  // L2 round trips per thread)
+  int i0 = b + threadIdx.x;
+  for (; i0 + 7 * 256 < e; i0 += 8 * 256) {
+    long long t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = ts[i0 + u * 256];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mn = t[u] < mn ? t[u] : mn;
+      mx = t[u] > mx ? t[u] : mx;
+    }
+  }
+  for (int i = i0; i < e; i += 256) {
+    const long long t = ts[i];
     mn = t < mn ? t : mn;
     mx = t > mx ? t : mx;
   }

@@ -149,16 +149,21 @@ struct WMix {
 // small terms go first.
 // DB: the A fragments of k-step s + 1 are issued before the MFMAs of step s (double
 // buffer: MT * 12 more registers, no wait on the fragment loads between k-steps).
-template <int KS, int MT, int MTW, int RT, bool DB = false, typename WSrc, typename BOp>
+template <int KS, int MT, int MTW, int RT, int DB = 0, typename WSrc, typename BOp>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, int m0, BOp&& bop) {
-  bf16x8_t Ab[DB ? 2 : 1][MT][3];
+  // DB: A fragments read DB k-steps ahead (a ring of DB + 1 buffers); 0: at their step
+  constexpr int NBUF = DB + 1;
+  bf16x8_t Ab[NBUF][MT][3];
   auto lda = [&](int s, bf16x8_t (&d)[MT][3]) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int p = 0; p < 3; ++p) d[m][p] = W(p, ((m0 + m) * KS + s) * 1024);
   };
-  if constexpr (DB) lda(0, Ab[0]);
+  if constexpr (DB > 0) {
+#pragma unroll
+    for (int q = 0; q < DB && q < KS; ++q) lda(q, Ab[q % NBUF]);
+  }
   // B operands one k-step ahead (RG_X3_PIPE): the split of step s + 1 is independent of
   // step s's MFMAs, so its VALU work can issue in their shadow instead of between them
   X3 bq[RG_X3_PIPE ? RT : 1];
@@ -168,12 +173,12 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
   }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    if constexpr (DB) {
-      if (s + 1 < KS) lda(s + 1, Ab[(s + 1) & 1]);
+    if constexpr (DB > 0) {
+      if (s + DB < KS) lda(s + DB, Ab[(s + DB) % NBUF]);
     } else {
       lda(s, Ab[0]);
     }
-    const bf16x8_t(&A)[MT][3] = Ab[DB ? (s & 1) : 0];
+    const bf16x8_t(&A)[MT][3] = Ab[DB > 0 ? s % NBUF : 0];
     X3 bn[RG_X3_PIPE ? RT : 1];
     if constexpr (RG_X3_PIPE) {
       if (s + 1 < KS) {
@@ -207,7 +212,7 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
   }
 }
 // one row tile
-template <int KS, int MT, int MTW, bool DB = false, typename WSrc, typename BOp>
+template <int KS, int MT, int MTW, int DB = 0, typename WSrc, typename BOp>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[MT], const WSrc& W, int m0, BOp&& bop) {
   layer_x3<KS, MT, MTW, 1, DB>(*reinterpret_cast<f32x16(*)[1][MT]>(&acc), W, m0,
                                [&](int s, int) { return bop(s); });
