@@ -32,6 +32,8 @@ def main():
     ap.add_argument('--k', type=int, default=32)
     ap.add_argument('--layers', type=int, default=6)
     ap.add_argument('--dtype', default='bf16')
+    ap.add_argument('--graph', default='knn', help='radius: the workload key adds graph + eps2')
+    ap.add_argument('--eps2', type=float, default=25.0)
     a = ap.parse_args()
     fetch, nf = per_kernel(os.path.join(a.pmc_dir, 'FETCH_SIZE_counter_collection.csv'))
     write, _ = per_kernel(os.path.join(a.pmc_dir, 'WRITE_SIZE_counter_collection.csv'))
@@ -42,8 +44,10 @@ def main():
         kernels[name] = {'launches': nf.get(name, 0), 'fetch_bytes_raw': round(fb),
                          'fetch_bytes': round(2 * fb), 'write_bytes': round(wb),
                          'traffic_bytes': round(2 * fb + wb)}
-    doc = {'workload': {'frames': a.frames, 'nodes': a.nodes, 'k': a.k, 'layers': a.layers,
-                        'dtype': a.dtype},
+    wl = {'frames': a.frames, 'nodes': a.nodes, 'k': a.k, 'layers': a.layers, 'dtype': a.dtype}
+    if a.graph != 'knn':
+        wl.update(graph=a.graph, eps2=a.eps2)
+    doc = {'workload': wl,
            'correction': 'fetch_bytes = 2 x FETCH_SIZE (gfx950 wide-read undercount); '
                          'write_bytes = WRITE_SIZE; both KiB -> bytes',
            'kernels': kernels}
