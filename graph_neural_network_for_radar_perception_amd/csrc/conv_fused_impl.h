@@ -33,6 +33,12 @@ static constexpr float NORM_EPS = 1e-5f;
 static constexpr int NQ = 8;
 static constexpr int CTR_STRIDE = 32;
 
+#ifndef RG_CONV_LUT
+#define RG_CONV_LUT 1  // one-hot segment matrix from a 256-entry LDS table (0: per-edge compares)
+#endif
+// the one-hot table: entry b = eight 16-bit ONEs / zeros for the bits of b (4 KiB of LDS)
+static constexpr int LUT_BYTES = RG_CONV_LUT ? 256 * 16 : 0;
+
 #ifndef RG_CONV_STAMP
 #define RG_CONV_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_conv_stamp
 #endif
@@ -185,6 +191,15 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   for (int l = 0; l < 3; ++l) {
     stage_lds<CT>(lds + a.L[l].woff, a.L[l].src, a.L[l].bytes);
   }
+#if RG_CONV_LUT
+  for (int b = threadIdx.x; b < 256; b += CT) {
+    u32x4 e;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      e[i] = (((b >> (2 * i)) & 1) ? HT::ONE : 0u) | ((((b >> (2 * i + 1)) & 1) ? HT::ONE : 0u) << 16);
+    *(u32x4*)(lds + a.total_bytes + 16 * b) = e;
+  }
+#endif
   __syncthreads();
   CSTAMP(0);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -195,7 +210,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   if (wave >= CW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
-  char* wbase = lds + a.total_bytes + wave * WAVE_LDS;
+  const u32x4* lut = (const u32x4*)(lds + a.total_bytes);
+  char* wbase = lds + a.total_bytes + LUT_BYTES + wave * WAVE_LDS;
   float* P = (float*)wbase;
   uint16_t* tile = (uint16_t*)(wbase + NB * PST * 4);
   int* slots = (int*)((char*)tile + 32 * C * 2);
@@ -250,6 +266,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     const int n1 = bn1;
     int nxt_raw = 0;
     if (lane == 0) nxt_raw = atomicAdd(head, 1);
+#if RG_CONV_LUT
+    // the block's node r (= one-hot column / slot r) owns the CSR range [sst, sen); lanes
+    // past the block's nodes get an empty range (clamped loads, no branch)
+    const int sst = a.seg_ptr[min(n0 + r, n1)], sen = a.seg_ptr[min(n0 + r + 1, n1)];
+#endif
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
@@ -307,7 +328,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
           const int gr = (8 * m + 2 * g + h) ^ sr;
           *(uint2*)(tile + r * C + 4 * gr) = wv;
         }
+#if RG_CONV_LUT
+      // slot r's edges in this tile: bits [sst - t0, sen - t0) of a 32-bit mask (edges past
+      // the block's end belong to no slot)
+      const int lo_b = min(max(sst - t0, 0), 32), hi_b = min(max(sen - t0, 0), 32);
+      const uint32_t mhi = hi_b >= 32 ? 0xffffffffu : ((1u << hi_b) - 1u);
+      const uint32_t mlo = lo_b >= 32 ? 0xffffffffu : ((1u << lo_b) - 1u);
+      const uint32_t smask = mhi & ~mlo;
+      (void)valid;
+#else
       if (h == 0) slots[r] = valid ? slot : 31;
+#endif
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
@@ -318,6 +349,9 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // B = S (k = edge 16s + 8h + j, col = slot r): one-hot bf16
+#if RG_CONV_LUT
+        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, lut[(smask >> (16 * s + 8 * h)) & 0xffu]);
+#else
         const int4 sa = *(const int4*)(slots + 16 * s + 8 * h);
         const int4 sb = *(const int4*)(slots + 16 * s + 8 * h + 4);
         const uint32_t one = HT::ONE;
@@ -327,6 +361,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
         sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
         sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
         const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
+#endif
         const int row_lo = 16 * s + 8 * (G >> 1) + q4, row_hi = row_lo + 4;
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -604,7 +639,7 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
   a.blk_nodes = blk_nodes;
   a.n_blk_dev = n_blocks_dev;
   if (n_nodes <= 0) return RG_OK;
-  const size_t lds = (size_t)off + (size_t)CW * WAVE_LDS;
+  const size_t lds = (size_t)off + LUT_BYTES + (size_t)CW * WAVE_LDS;
   RG_REQUIRE(lds <= DYN_LDS_MAX, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
   // the yml activation (LeakyReLU, configuration_radarscenes_gnn.yml:50) on all three
   // blocks selects the compile-time variant; anything else dispatches per layer

@@ -368,13 +368,18 @@ __device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], f
   const float inv = inv_std_bf16(ss, N, eps);
   const float gs = LEAKY_PRE * (sd * inv);
   const f32x2 gs2 = {gs, gs}, mu2 = {LEAKY_PRE * mu, LEAKY_PRE * mu};
+  // all of a tile's packed fmas first, then the scalar ones: a v_fma_f32 reading a
+  // v_pk_fma_f32 result right after it costs an s_nop (gfx950 hazard) -- one per pair
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < MT; ++m) {
+    f32x2 y[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const f32x2 y = fma2(pair(acc[m], i), gs2, mu2);
-      set_pair(acc[m], i, (f32x2){fmaf(fabsf(y.x), LEAKY_C, y.x), fmaf(fabsf(y.y), LEAKY_C, y.y)});
-    }
+    for (int i = 0; i < 8; ++i) y[i] = fma2(pair(acc[m], i), gs2, mu2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      set_pair(acc[m], i, (f32x2){fmaf(fabsf(y[i].x), LEAKY_C, y[i].x),
+                                  fmaf(fabsf(y[i].y), LEAKY_C, y[i].y)});
+  }
 }
 
 template <int ACT, int MT>
