@@ -89,6 +89,9 @@ static constexpr int NW = FT / 64;
 #ifndef RG_CX3_NODE_KERNEL
 #define RG_CX3_NODE_KERNEL 1  // the update / projection phase as a second launch (LDS weights)
 #endif
+#ifndef RG_CX3_LATE
+#define RG_CX3_LATE 0  // 1: the next tile's rows loaded right after this tile's layer 2 (M: 0.62 -> 0.84 ms, rejected)
+#endif
 #ifndef RG_CX3_WU_LDS
 #define RG_CX3_WU_LDS 0  // W_u staged in LDS too, 4-row passes (M: 0.650 vs 0.638 ms/layer, slower)
 #endif
@@ -370,17 +373,24 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     };
     int p1 = 0, d1 = 0, s1 = 0, p2 = 0, d2 = 0, s2 = 0;
     Rows nrows;
+    Rows rw;       // RG_CX3_LATE: loop-carried, loaded in the previous tile's second half
+    int dcur = 0;  // RG_CX3_LATE: the destinations of the rows in rw
     if (e0 < e1) {
       tile_idx(e0, p1, d1, s1);
       if constexpr (RG_CX3_RPF) {  // rows of tile 0 now, indices of tile 1
         load_rows(p1, d1, s1, nrows);
         tile_idx(e0 + 32, p2, d2, s2);
+      } else if constexpr (RG_CX3_LATE) {
+        load_rows(p1, d1, s1, rw);
+        dcur = d1;
+        tile_idx(e0 + 32, p1, d1, s1);
       }
     }
     for (int t0 = e0; t0 < e1; t0 += 32) {
-      const int d = d1;
-      Rows rw;
-      if constexpr (RG_CX3_RPF) {
+      const int d = RG_CX3_LATE ? dcur : d1;
+      if constexpr (RG_CX3_LATE) {
+        // rows already in flight since the previous tile's second half
+      } else if constexpr (RG_CX3_RPF) {
         // rows of the next tile now (indices loaded one tile earlier), indices of the tile
         // after: the whole gather latency hides behind this tile
         rw = nrows;
@@ -438,6 +448,15 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         for (int s = 0; s < 8; ++s) {
           const X3 b = split_acc(acc1[s >> 1], s & 1);
           acc2[s & 1][s] += xor_first(b);
+        }
+      }
+      if constexpr (RG_CX3_LATE) {
+        // acc1 and this tile's rows are dead: the next tile's rows go out now and arrive
+        // behind norm 2 and the segmented sum (no registers beyond the rows' own)
+        if (t0 + 32 < e1) {
+          load_rows(p1, d1, s1, rw);
+          dcur = d1;
+          tile_idx(t0 + 64, p1, d1, s1);
         }
       }
       STAMP(3);  // layer 2 issue

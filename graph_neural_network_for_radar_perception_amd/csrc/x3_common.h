@@ -56,7 +56,8 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 #define RG_X3_PKNORM 0  // 1: row statistics and scale in v_pk_fma_f32 (M: no gain, conv 1% slower)
 #endif
 #ifndef RG_X3_SPLIT
-#define RG_X3_SPLIT 0  // split8 residues: 0 scalar v_sub_f32, 1 f32x2 (compiler), 2 forced v_pk_add_f32
+#define RG_X3_SPLIT 0  // split8: 0 pair by pair, 3 stage by stage (no s_nop pads; measured flat),
+                       // 1 f32x2 residues (compiler), 2 forced v_pk_add_f32 residues
 #endif
 
 // the two f32 values of a packed bf16 pair
@@ -77,7 +78,7 @@ __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
   const f32x2 v[4] = {{lo.x, lo.y}, {lo.z, lo.w}, {hi.x, hi.y}, {hi.z, hi.w}};
   u32x4 w0, w1, w2;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4 && RG_X3_SPLIT != 3; ++i) {
     const uint32_t u0 = cvt_pk_bf16(v[i].x, v[i].y);
 #if RG_X3_SPLIT == 2
     const f32x2 r = sub_pk(v[i], unpk(u0));
@@ -87,17 +88,41 @@ __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
     const f32x2 r = add2(v[i], -unpk(u0));
     const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
     const f32x2 t = add2(r, -unpk(u1));
-#else
+#elif RG_X3_SPLIT == 0
     const f32x2 u0f = unpk(u0);
     const f32x2 r = {v[i].x - u0f.x, v[i].y - u0f.y};
     const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
     const f32x2 u1f = unpk(u1);
     const f32x2 t = {r.x - u1f.x, r.y - u1f.y};
 #endif
+#if RG_X3_SPLIT != 3
     w0[i] = u0;
     w1[i] = u1;
     w2[i] = cvt_pk_bf16(t.x, t.y);
+#endif
   }
+#if RG_X3_SPLIT == 3
+  // stage by stage over the four pairs: every read of a conversion result is three
+  // instructions after it (right after an inline-asm conversion the compiler pads an
+  // s_nop: 43 per conv tile)
+  f32x2 r[4], t[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w0[i] = cvt_pk_bf16(v[i].x, v[i].y);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 u = unpk(w0[i]);
+    r[i] = (f32x2){v[i].x - u.x, v[i].y - u.y};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w1[i] = cvt_pk_bf16(r[i].x, r[i].y);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 u = unpk(w1[i]);
+    t[i] = (f32x2){r[i].x - u.x, r[i].y - u.y};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w2[i] = cvt_pk_bf16(t[i].x, t[i].y);
+#endif
   return X3{__builtin_bit_cast(bf16x8_t, w0), __builtin_bit_cast(bf16x8_t, w1),
             __builtin_bit_cast(bf16x8_t, w2)};
 }
