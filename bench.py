@@ -446,13 +446,35 @@ def train_main(args, world, rank, local):
     E = int(gb.n_edges_dev.item())
     barrier(world)
     torch.cuda.synchronize()
+    events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        losses, acc, gb = trainer.step(batch, labels)
+        losses, acc, gb = trainer.step(batch, labels, events=events)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     frames_total = sum_over_ranks(args.frames * args.steps, world)
+    durs = event_durations(events)
+    # roofline of the forward tape (the step's largest phase: the f32 row-MLP chain kernel
+    # writing every layer's pre-norm / activation rows): the model's forward flops in the
+    # form the training forward computes them (message MLP over all 192 inputs per edge,
+    # SURVEY §8(d)) on the f32 MFMA peak (v_mfma_f32_16x16x4_f32); the backward beside it
+    # at twice those flops (dX and dW per layer)
+    N = args.frames * args.nodes
+    U = int(gb.graph.n_pairs_dev.item())
+    Fw = (84992.0 * N + 118272.0 * E + args.layers * (65536.0 * E + 16384.0 * N) + 99456.0 * N
+          + 33024.0 * U + 9088.0 * (N / 5))
+    fwd_ms = float(np.mean(durs['train_forward']))
+    bwd_ms = float(np.mean(durs['train_backward']))
+    roof = {'kernel': 'training forward tape (rg_mlp_chain f32 with save_pre / save_out, '
+                      'gnn_detector.py:428-478 + loss.py:37-76)',
+            'bound': 'mfma', 'achieved': round(Fw / (fwd_ms * 1e-3) / 1e12, 2),
+            'peak': MFMA_PEAK_TFLOPS['fp32'], 'unit': 'TFLOP/s',
+            'frac': round(Fw / (fwd_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS['fp32'], 4),
+            'traffic': None, 'avg_ms': round(fwd_ms, 4), 'flops_per_launch': Fw,
+            'timing': 'HIP events on the launch stream around the forward of every timed step',
+            'backward_ms': round(bwd_ms, 4),
+            'backward_tflops': round(2 * Fw / (bwd_ms * 1e-3) / 1e12, 2)}
     line = {
         'metric': 'radar frames/sec training (BASELINE config 4: yml k=10, L=7, batch 8/GPU, '
                   'SGD momentum 0.9, DDP gradient all-reduce over RCCL)',
@@ -469,7 +491,7 @@ def train_main(args, world, rank, local):
                    'layers': args.layers, 'edges_per_gpu': E,
                    'parallelism': f'data-parallel x{world} (one flat-gradient all-reduce per step)'},
         'last_losses': [round(float(x), 5) for x in losses.cpu()],
-        'roofline': None,
+        'roofline': roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_train_baseline(args, cfg)

@@ -616,10 +616,20 @@ class RadarGNNTrainer:
         g = gb.graph
         g.n_edges = int(gb.n_edges_dev.item())      # host sizes for the backward's launches
         g.n_pairs = int(g.n_pairs_dev.item())
+        def mark(name):  # one HIP event pair per phase (bench.py's c4 roofline)
+            if events is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(torch.cuda.current_stream(self.engine.device))
+                events.append((name, ev))
+
+        mark('train_forward:start')
         losses, acc, tape = self.engine.forward(gb.node_features, gb.edge_features, g,
                                                 batch.cluster_ptr, batch.cluster_idx,
                                                 batch.n_clusters, labels)
+        mark('train_forward:end')
+        mark('train_backward:start')
         self.engine.backward(tape, self.ones)
+        mark('train_backward:end')
         scale = allreduce_gradients(self.engine.flat_grad, self.world)
         self.opt.step(self.engine.flat_grad, grad_scale=scale)
         return losses, acc, gb
