@@ -21,7 +21,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('RG_LIBRARY') or os.path.join(PKG, 'lib', 'libradargnn.so')
 HEADER = os.path.join(os.path.dirname(PKG), 'include', 'radar_gnn.h')
 
-RG_F32, RG_BF16, RG_F16 = 0, 1, 6
+RG_F32, RG_BF16, RG_F16, RG_F32X3 = 0, 1, 6, 7
 RG_PACK_FAST_IN, RG_PACK_FAST_CHAIN, RG_PACK_FAST_UPD, RG_PACK_F32_FAST = 2, 3, 4, 5
 RG_PACK_CENTERED = 0x100
 RG_PACK_TRANSPOSE = 0x200

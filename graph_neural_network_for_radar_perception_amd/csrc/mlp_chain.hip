@@ -23,6 +23,7 @@
 // dtype RG_F32 : v_mfma_f32_16x16x4_f32  (exact f32 products, k-ordered fma chain)
 // dtype RG_BF16: v_mfma_f32_16x16x32_bf16 (bf16 operands, f32 accumulate and epilogue)
 #include "rg_common.h"
+#include "x3_common.h"
 
 namespace rg {
 
@@ -110,8 +111,10 @@ __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, in
   P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k]) : 0.f;
 }
 
-__global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
-                                 uint16_t* __restrict__ P, long total) {
+// plane p > 0: the p-th term of the exact three-term bf16 split (RG_PACK_X3 | RG_BF16, the
+// generic chain's f32 arithmetic on bf16 products); transpose: W holds the [in][out] matrix
+__global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out, int plane,
+                                 int transpose, uint16_t* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S = kpad(in, 32) / 32;
@@ -122,7 +125,10 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out,
   const int m = (int)(ms / S);
   const int o = 16 * m + (lane & 15);
   const int k = 32 * s + 8 * (lane >> 4) + j;
-  P[t] = (o < out && k < in) ? f32_to_bf16(W[(size_t)o * in + k]) : (uint16_t)0;
+  float v = 0.f;
+  if (o < out && k < in) v = transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k];
+  for (int q = 0; q < plane; ++q) v -= bf16_to_f32(f32_to_bf16(v));  // exact residues
+  P[t] = f32_to_bf16(v);
 }
 
 // 32x32x16 fragments: [m][s][lane][8] = W[32m + (lane&31)][k(s, lane>>5, j)] with
@@ -370,6 +376,36 @@ template <> struct Mfma<uint16_t> {
   }
 };
 
+// float32 arithmetic on the bf16 matrix cores (RG_F32X3): the f32 slab's 8 k values per
+// lane split exactly into three bf16 terms (x3_common.h), weights pre-split into three
+// planes of the 16x16x32 fragment format; six products of weight <= 2 per k-step
+struct MfmaX3 {
+  static __device__ __forceinline__ void run(f32x4 (&acc)[16], const float* slab,
+                                             const uint16_t* P, int mt, int K, int lane, int SS,
+                                             size_t pl) {
+    const int S = kpad(K, 32) / 32;
+    const float* brow = slab + (lane & 15) * SS + 8 * (lane >> 4);
+    for (int s = 0; s < S; ++s) {
+      const x3::X3 b = x3::split8(*(const f32x4*)(brow + 32 * s), *(const f32x4*)(brow + 32 * s + 4));
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m < mt) {
+          const uint16_t* pa = P + (((size_t)m * S + s) * 64 + lane) * 8;
+          const bf16x8_t a0 = __builtin_bit_cast(bf16x8_t, *(const u32x4*)pa);
+          const bf16x8_t a1 = __builtin_bit_cast(bf16x8_t, *(const u32x4*)(pa + pl));
+          const bf16x8_t a2 = __builtin_bit_cast(bf16x8_t, *(const u32x4*)(pa + 2 * pl));
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b.p0, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b.p1, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b.p2, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b.p0, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b.p1, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b.p0, acc[m], 0, 0, 0);
+        }
+      }
+    }
+  }
+};
+
 // bias (already in acc) -> channel_normalization -> activation; features >= out -> 0.
 // Lane (r, g) holds features 16m + 4g + e of row r; the row's other features
 // sit in lanes r^16, r^32, r^48.
@@ -468,7 +504,7 @@ __device__ __forceinline__ void save_rows(const f32x4 (&acc)[16], float* dst, lo
   }
 }
 
-template <typename T, bool WLDS>
+template <typename T, bool WLDS, bool X3 = false>
 __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // layer descriptors: copied with static indices (a dynamically indexed kernel
@@ -495,7 +531,8 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
   const long ntiles = (rows + TR - 1) / TR;
   const int dt = sizeof(T) == 4 ? RG_F32 : RG_BF16;
-  const int K0p = kpad(sL[0].in, Cfg<T>::KPAD);
+  constexpr int KP = X3 ? 32 : Cfg<T>::KPAD;  // k-step depth of the slab's zero padding
+  const int K0p = kpad(sL[0].in, KP);
   for (long tile = (long)blockIdx.x * CH_WAVES + wave; tile < ntiles;
        tile += (long)gridDim.x * CH_WAVES) {
     const long r0 = tile * TR;
@@ -505,11 +542,15 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
       const ChainLayer L = sL[l];
       const int mt = (L.out + 15) / 16;
       const T* P = WLDS ? (const T*)(wimg + L.woff) : (const T*)L.w;
-      const float* bias = (const float*)((const char*)P + frag_bytes(L.in, L.out, dt));
+      const size_t fb = frag_bytes(L.in, L.out, X3 ? RG_BF16 : dt);
+      const float* bias = (const float*)((const char*)P + (X3 ? 3 * fb : fb));
 #pragma unroll
       for (int m = 0; m < 16; ++m)
         if (m < mt) acc[m] = *(const f32x4*)(bias + 16 * m + 4 * g);
-      Mfma<T>::run(acc, slab, P, mt, L.in, lane, a.sstride);
+      if constexpr (X3)
+        MfmaX3::run(acc, slab, (const uint16_t*)P, mt, L.in, lane, a.sstride, fb / sizeof(uint16_t));
+      else
+        Mfma<T>::run(acc, slab, P, mt, L.in, lane, a.sstride);
       if (L.save_pre && r0 + r < rows) save_rows(acc, L.save_pre, r0 + r, mt, L.out, g);
       epilogue(acc, L, mt, g);
       if (L.save_out && r0 + r < rows) save_rows(acc, L.save_out, r0 + r, mt, L.out, g);
@@ -520,7 +561,7 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
           if (m < mt) st4_slab<T>(row + 16 * m + 4 * g, acc[m]);
         // zero the next layer's K padding beyond the 16*mt features written above
         // (bf16 k-steps are 32 deep: an odd tile count leaves 16 stale columns)
-        if (kpad(L.out, Cfg<T>::KPAD) > 16 * mt)
+        if (kpad(L.out, KP) > 16 * mt)
           st4_slab<T>(row + 16 * mt + 4 * g, (f32x4){0.f, 0.f, 0.f, 0.f});
       } else {
         const long row = r0 + r;
@@ -530,12 +571,12 @@ __global__ __launch_bounds__(CH_THREADS) void chain_kernel(ChainArgs a) {
   }
 }
 
-template <typename T, bool WLDS>
+template <typename T, bool WLDS, bool X3 = false>
 static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
   const size_t dbytes = (sizeof(ChainLayer) * RG_MAX_LAYERS + 15) & ~(size_t)15;
   const size_t lds = dbytes + (WLDS ? ((size_t)(a.wbytes + 15) & ~(size_t)15) : 0) +
                      (size_t)CH_WAVES * TR * a.sstride * sizeof(T);
-  RG_ENSURE_LDS((chain_kernel<T, WLDS>), (int)LDS_LIMIT);
+  RG_ENSURE_LDS((chain_kernel<T, WLDS, X3>), (int)LDS_LIMIT);
   const long tiles = (rows + TR - 1) / TR;
   long blocks = (tiles + CH_WAVES - 1) / CH_WAVES;
   // persistent grid: enough resident workgroups to fill 256 CUs
@@ -543,7 +584,7 @@ static int launch_chain(const ChainArgs& a, long rows, hipStream_t st) {
   const long cap = 256L * per_cu * (WLDS ? 1 : 4);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  chain_kernel<T, WLDS><<<blocks, CH_THREADS, lds, st>>>(a);
+  chain_kernel<T, WLDS, X3><<<blocks, CH_THREADS, lds, st>>>(a);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -556,11 +597,27 @@ extern "C" size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype) {
   return packed_bytes(in_dim, out_dim, dtype & ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE | RG_PACK_F16));
 }
 
-// RG_PACK_X3: three planes of one RG_PACK_FAST_* format
+// RG_PACK_X3: three planes of one RG_PACK_FAST_* format, or of RG_BF16 (the generic chain's
+// 16x16x32 fragments; transpose allowed), then the f32 bias
 static int pack_x3(const float* weight, const float* bias, int in_dim, int out_dim, int fmt,
-                   int center, void* packed, hipStream_t st) {
+                   int center, int transpose, void* packed, hipStream_t st) {
+  if (fmt == RG_BF16) {
+    RG_REQUIRE(!center, RG_ERR_ARG, "rg_pack_linear: RG_PACK_CENTERED applies to the fast formats");
+    const size_t fb = frag_bytes(in_dim, out_dim, RG_BF16);
+    const long total = (long)fb / sizeof(uint16_t);
+    for (int p = 0; p < 3; ++p)
+      pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(
+          weight, in_dim, out_dim, p, transpose, (uint16_t*)((char*)packed + p * fb), total);
+    const int nb = kpad(out_dim, 32);
+    pack_bias_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(bias, out_dim, nb,
+                                                        (float*)((char*)packed + 3 * fb));
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
+  RG_REQUIRE(!transpose, RG_ERR_ARG,
+             "rg_pack_linear: RG_PACK_X3 with RG_PACK_TRANSPOSE applies to RG_BF16");
   RG_REQUIRE(fmt == RG_PACK_FAST_IN || fmt == RG_PACK_FAST_CHAIN || fmt == RG_PACK_FAST_UPD,
-             RG_ERR_ARG, "rg_pack_linear: RG_PACK_X3 applies to the RG_PACK_FAST_* formats");
+             RG_ERR_ARG, "rg_pack_linear: RG_PACK_X3 applies to RG_BF16 and the RG_PACK_FAST_* formats");
   const int ks = (in_dim + 15) / 16;
   RG_REQUIRE(fmt != RG_PACK_FAST_UPD || in_dim % 64 == 0, RG_ERR_ARG,
              "RG_PACK_FAST_UPD needs in_dim = 2*C with C a multiple of 32");
@@ -589,10 +646,10 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                       (dtype & ~RG_PACK_CENTERED) <= RG_PACK_FAST_UPD),
              RG_ERR_ARG, "rg_pack_linear: RG_PACK_F16 applies to the RG_PACK_FAST_* formats");
   if (dtype & RG_PACK_X3) {
-    RG_REQUIRE(!(dtype & RG_PACK_TRANSPOSE), RG_ERR_ARG,
-               "rg_pack_linear: RG_PACK_X3 does not combine with RG_PACK_TRANSPOSE");
-    return pack_x3(weight, bias, in_dim, out_dim, dtype & ~(RG_PACK_X3 | RG_PACK_CENTERED),
-                   (dtype & RG_PACK_CENTERED) ? 1 : 0, packed, st);
+    return pack_x3(weight, bias, in_dim, out_dim,
+                   dtype & ~(RG_PACK_X3 | RG_PACK_CENTERED | RG_PACK_TRANSPOSE),
+                   (dtype & RG_PACK_CENTERED) ? 1 : 0, (dtype & RG_PACK_TRANSPOSE) ? 1 : 0, packed,
+                   st);
   }
   const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
   const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;
@@ -607,7 +664,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                                                           (float*)packed, total);
   } else if (dtype == RG_BF16) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
-    pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
+    pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, 0, 0,
                                                            (uint16_t*)packed, total);
   } else if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
@@ -643,7 +700,10 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
                             int ld_out, int out_dtype, void* stream) {
   RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG,
              "rg_mlp_chain: n_layers=%d outside 1..%d", n_layers, RG_MAX_LAYERS);
-  RG_REQUIRE(dtype == RG_F32 || dtype == RG_BF16, RG_ERR_ARG, "rg_mlp_chain: bad dtype");
+  RG_REQUIRE(dtype == RG_F32 || dtype == RG_BF16 || dtype == RG_F32X3, RG_ERR_ARG,
+             "rg_mlp_chain: bad dtype");
+  const bool x3 = dtype == RG_F32X3;
+  const int wfmt = x3 ? (RG_BF16 | RG_PACK_X3) : dtype;  // the layers' packed format
   RG_REQUIRE(in_dtype == RG_F32 || in_dtype == RG_BF16, RG_ERR_ARG, "rg_mlp_chain: bad in_dtype");
   RG_REQUIRE(out_dtype == RG_F32 || out_dtype == RG_BF16, RG_ERR_ARG, "rg_mlp_chain: bad out_dtype");
   RG_REQUIRE(in_mode >= RG_IN_DENSE && in_mode <= RG_IN_PAIRADD, RG_ERR_ARG, "bad in_mode");
@@ -669,8 +729,8 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
                "rg_mlp_chain: layer %d in_dim %d does not match its input", l, s.in_dim);
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG,
                "rg_mlp_chain: layer %d norm needs mu, std and out_dim >= 2", l);
-    RG_REQUIRE((!s.save_pre && !s.save_out) || dtype == RG_F32, RG_ERR_ARG,
-               "rg_mlp_chain: training tapes (save_pre / save_out) need dtype RG_F32");
+    RG_REQUIRE((!s.save_pre && !s.save_out) || dtype == RG_F32 || x3, RG_ERR_ARG,
+               "rg_mlp_chain: training tapes (save_pre / save_out) need dtype RG_F32 / RG_F32X3");
     a.L[l].w = s.w_packed;
     a.L[l].save_pre = s.save_pre;
     a.L[l].save_out = s.save_out;
@@ -680,7 +740,7 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
     a.L[l].out = s.out_dim;
     a.L[l].act = s.act;
     a.L[l].woff = (int)woff;
-    woff += packed_bytes(s.in_dim, s.out_dim, dtype);
+    woff += packed_bytes(s.in_dim, s.out_dim, wfmt);
   }
   a.wbytes = (int)woff;
   a.nl = n_layers;
@@ -695,14 +755,17 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
   if (rows <= 0) return RG_OK;
   hipStream_t st = (hipStream_t)stream;
   const size_t dbytes = (sizeof(ChainLayer) * RG_MAX_LAYERS + 15) & ~(size_t)15;
-  if (dtype == RG_F32) {
+  if (dtype == RG_F32 || x3) {
     // f32 slab rows sized to the chain's widest input (kpad 64 + 8 keeps the B reads
     // conflict-free): single large layers (the training backward's W^T) then fit in LDS
     int kmax = layers[0].in_dim;
     for (int l = 0; l + 1 < n_layers; ++l) kmax = layers[l].out_dim > kmax ? layers[l].out_dim : kmax;
     a.sstride = kpad(kmax, 64) + 8;
     const size_t slabs = (size_t)CH_WAVES * TR * a.sstride * sizeof(float);
-    if (dbytes + woff + slabs <= LDS_LIMIT) return launch_chain<float, true>(a, rows, st);
+    const bool fits = dbytes + woff + slabs <= LDS_LIMIT;
+    if (x3) return fits ? launch_chain<float, true, true>(a, rows, st)
+                        : launch_chain<float, false, true>(a, rows, st);
+    if (fits) return launch_chain<float, true>(a, rows, st);
     return launch_chain<float, false>(a, rows, st);
   }
   a.sstride = Cfg<uint16_t>::STRIDE;

@@ -43,6 +43,9 @@ extern "C" {
 #define RG_F32 0
 #define RG_BF16 1
 #define RG_F16 6 /* IEEE binary16: the fp16 path (BASELINE config 5) of the 16-bit kernels */
+#define RG_F32X3 7 /* rg_mlp_chain: float32 arithmetic on the bf16 matrix cores (every product
+                      from exact three-term bf16 splits, f32 accumulation); layers packed
+                      RG_BF16 | RG_PACK_X3; training tapes allowed */
 /* packed-weight formats of rg_pack_linear: RG_F32 / RG_BF16 for rg_mlp_chain, and
  * the two 32x32x16 bf16 formats of rg_mlp_chain_fast (first layer / chained layers) */
 #define RG_PACK_FAST_IN 2

@@ -266,3 +266,79 @@ def test_m_config_full_batch_fp32_matches_oracle(cuda_device):
         ncl = len(clusters[f])
         np.testing.assert_allclose(out.obj_cls[f * ncl:(f + 1) * ncl].cpu().numpy(),
                                    ref[3].numpy(), **FP32_TOL)
+
+
+def test_generic_chain_f32x3_matches_f32(cuda_device):
+    """rg_mlp_chain RG_F32X3 (layers packed RG_BF16 | RG_PACK_X3: three exact bf16 planes,
+    products from exact activation splits, f32 accumulation) against the same chain on the
+    exact f32 MFMA (RG_F32), GATHER3 input, norm + LeakyReLU, training tapes on: outputs and
+    both tapes agree to 2e-5 of their scale; the backward's transposed x3 packing (dX = dZ W)
+    likewise."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    lib = nat.lib()
+    dev = cuda_device
+    st = nat.stream_ptr(dev)
+    g = torch.Generator().manual_seed(5)
+    N, E, C = 900, 5000, 64
+    dims = [(3 * C, 128), (128, 64)]
+    ws = [(torch.randn(o, i, generator=g) / i ** 0.5).to(dev) for i, o in dims]
+    bs = [(0.1 * torch.randn(o, generator=g)).to(dev) for _, o in dims]
+    mus = [torch.tensor([0.2], device=dev), torch.tensor([-0.1], device=dev)]
+    sds = [torch.tensor([1.3], device=dev), torch.tensor([0.7], device=dev)]
+    x = torch.randn(N, C, generator=g).to(dev)
+    e = torch.randn(E, C, generator=g).to(dev)
+    src = torch.randint(0, N, (E,), generator=g, dtype=torch.int32).to(dev)
+    dst = torch.randint(0, N, (E,), generator=g, dtype=torch.int32).to(dev)
+
+    def run(dtype, fmt):
+        bufs, arr = [], (nat.rg_layer * 2)()
+        tapes = []
+        for l, ((i, o), w, b) in enumerate(zip(dims, ws, bs)):
+            buf = torch.empty(lib.rg_packed_linear_bytes(i, o, fmt), dtype=torch.uint8, device=dev)
+            nat.check(lib.rg_pack_linear(w.data_ptr(), b.data_ptr(), i, o, fmt, buf.data_ptr(), st),
+                      'rg_pack_linear')
+            bufs.append(buf)
+            z = torch.empty(E, o, device=dev)
+            a = torch.empty(E, o, device=dev)
+            tapes.append((z, a))
+            arr[l].w_packed = buf.data_ptr()
+            arr[l].norm_mu = mus[l].data_ptr()
+            arr[l].norm_std = sds[l].data_ptr()
+            arr[l].in_dim, arr[l].out_dim = i, o
+            arr[l].act = nat.ACT['leakyrelu']
+            arr[l].save_pre, arr[l].save_out = z.data_ptr(), a.data_ptr()
+        out = torch.empty(E, 64, device=dev)
+        nat.check(lib.rg_mlp_chain(dtype, arr, 2, E, None, nat.IN_GATHER3, nat.RG_F32,
+                                   x.data_ptr(), x.stride(0), C, None, 0, 0, e.data_ptr(),
+                                   e.stride(0), C, dst.data_ptr(), src.data_ptr(), None, 0,
+                                   nat.RG_F32, out.data_ptr(), out.stride(0), nat.RG_F32, st),
+                  'rg_mlp_chain')
+        torch.cuda.synchronize()
+        return out, tapes
+
+    o32, t32 = run(nat.RG_F32, nat.RG_F32)
+    ox3, tx3 = run(nat.RG_F32X3, nat.RG_BF16 | nat.RG_PACK_X3)
+    for a, b in [(o32, ox3)] + [p for pair in zip(t32, tx3) for p in zip(*pair)]:
+        scale = float(a.abs().max())
+        assert float((a - b).abs().max()) <= 2e-5 * max(scale, 1.0)
+    # dX = dZ W with transposed packing, as the training backward runs it
+    dz = torch.randn(E, 128, generator=g).to(dev)
+    outs = []
+    for dtype, fmt in ((nat.RG_F32, nat.RG_F32), (nat.RG_F32X3, nat.RG_BF16 | nat.RG_PACK_X3)):
+        buf = torch.empty(lib.rg_packed_linear_bytes(128, 3 * C, fmt), dtype=torch.uint8, device=dev)
+        nat.check(lib.rg_pack_linear(ws[0].data_ptr(), None, 128, 3 * C, fmt | nat.RG_PACK_TRANSPOSE,
+                                     buf.data_ptr(), st), 'rg_pack_linear')
+        arr = (nat.rg_layer * 1)()
+        arr[0].w_packed = buf.data_ptr()
+        arr[0].in_dim, arr[0].out_dim = 128, 3 * C
+        arr[0].act = nat.ACT['none']
+        dx = torch.empty(E, 3 * C, device=dev)
+        nat.check(lib.rg_mlp_chain(dtype, arr, 1, E, None, nat.IN_DENSE, nat.RG_F32, dz.data_ptr(),
+                                   dz.stride(0), 128, None, 0, 0, None, 0, 0, None, None, None,
+                                   0, nat.RG_F32, dx.data_ptr(), dx.stride(0), nat.RG_F32, st),
+                  'rg_mlp_chain')
+        outs.append(dx)
+    torch.cuda.synchronize()
+    ref = (dz.double() @ ws[0].double()).float()
+    for dx in outs:
+        assert float((dx - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
