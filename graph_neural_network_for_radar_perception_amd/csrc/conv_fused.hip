@@ -48,9 +48,51 @@
 using namespace rg;
 using namespace rg::conv;
 
+#ifndef RG_CONV_LPT
+#define RG_CONV_LPT 1  // 0: blocks in node order (timing comparison)
+#endif
+// Each XCD's share of the blocks (the fused kernel's ranges [n*x/NQ, n*(x+1)/NQ) of the
+// dequeue order) sorted by tile count, largest first: the waves then finish on the
+// smallest blocks (greedy longest-first), instead of on whatever blocks come last in node
+// order -- a 20 000-node frame is only ~2.3 blocks of 1-4 tiles per wave, and its launch
+// tail (waves idle until the last block ends) was a third of the wave time.  Order within
+// a size class is arbitrary: every node's result is independent of the schedule.
+__global__ __launch_bounds__(256) void conv_blocks_lpt(const int* __restrict__ bounds,
+                                                       const int* __restrict__ seg_ptr,
+                                                       const int* __restrict__ n_blocks_dev,
+                                                       int* __restrict__ pairs) {
+  constexpr int NBIN = 64;
+  __shared__ int hist[NBIN];
+  const int nb = *n_blocks_dev;
+  const int lo = (int)((long)nb * blockIdx.x / NQ), hi = (int)((long)nb * (blockIdx.x + 1) / NQ);
+  if (threadIdx.x < NBIN) hist[threadIdx.x] = 0;
+  __syncthreads();
+  auto bin = [&](int b) {  // bin 0 = the most tiles
+    const int t = (seg_ptr[bounds[b + 1]] - seg_ptr[bounds[b]] + 31) / 32;
+    return NBIN - 1 - min(t, NBIN - 1);
+  };
+  for (int b = lo + threadIdx.x; b < hi; b += blockDim.x) atomicAdd(&hist[bin(b)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < NBIN; ++i) {
+      const int c = hist[i];
+      hist[i] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (int b = lo + threadIdx.x; b < hi; b += blockDim.x) {
+    const int pos = RG_CONV_LPT ? lo + atomicAdd(&hist[bin(b)], 1) : b;
+    pairs[2 * pos] = bounds[b];
+    pairs[2 * pos + 1] = bounds[b + 1];
+  }
+}
+
 extern "C" size_t rg_conv_blocks_workspace_size(int n_nodes) {
   const long nb8 = ((long)n_nodes + NB - 1) / NB;
-  return 2 * ((size_t)((nb8 + 1) * sizeof(int) + 255) / 256 * 256) + scan_workspace_bytes(nb8);
+  return 2 * ((size_t)((nb8 + 1) * sizeof(int) + 255) / 256 * 256) +
+         ((size_t)((n_nodes + 1) * sizeof(int)) + 255) / 256 * 256 + scan_workspace_bytes(nb8);
 }
 
 extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
@@ -63,14 +105,17 @@ extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, i
   const size_t arr = ((size_t)(nb8 + 1) * sizeof(int) + 255) / 256 * 256;
   int* cnt = (int*)workspace;                 // sub-blocks per 8-node run
   int* off = (int*)((char*)workspace + arr);  // their exclusive scan
-  void* sws = (char*)workspace + 2 * arr;
+  int* bounds = (int*)((char*)workspace + 2 * arr);  // block boundaries in node order
+  void* sws = (char*)workspace + 2 * arr + ((size_t)((n_nodes + 1) * sizeof(int)) + 255) / 256 * 256;
   conv_blocks_kernel<false><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, cnt, nullptr,
                                                                 nullptr);
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(cnt, nb8, off, n_blocks, sws, st);
   if (rc) return rc;
   conv_blocks_kernel<true><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, nullptr, off,
-                                                               blk_nodes);
+                                                               bounds);
+  RG_LAUNCH_CHECK();
+  conv_blocks_lpt<<<NQ, 256, 0, st>>>(bounds, seg_ptr, n_blocks, blk_nodes);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

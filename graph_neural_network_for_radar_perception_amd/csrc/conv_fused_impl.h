@@ -78,7 +78,8 @@ struct CArgs {
   int* counter;  // NQ block heads, one per XCD, CTR_STRIDE ints apart, then the done counter
   int ldx, lde, ldo;
   // optional edge-balanced work blocks (rg_conv_blocks): block b = nodes
-  // [blk_nodes[b], blk_nodes[b + 1]), at most NB, *n_blk_dev blocks; null: b = 8-node run
+  // [blk_nodes[2b], blk_nodes[2b + 1]), at most NB, *n_blk_dev blocks (each XCD's share
+  // largest first, rg_conv_blocks); null: b = 8-node run
   const int* blk_nodes;
   const int* n_blk_dev;
 };
@@ -235,8 +236,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
   auto block_nodes = [&](int b, int& n0, int& n1) {
     if (a.blk_nodes) {
-      n0 = a.blk_nodes[b];
-      n1 = a.blk_nodes[b + 1];
+      n0 = a.blk_nodes[2 * b];
+      n1 = a.blk_nodes[2 * b + 1];
     } else {
       n0 = b * NB;
       n1 = min(n0 + NB, a.n_nodes);

@@ -490,7 +490,7 @@ class DeviceGraph:
         if self._conv_blocks is None:
             lib = nat.lib()
             dev = self.seg_ptr.device
-            tbl = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            tbl = torch.empty(2 * n + 2, dtype=torch.int32, device=dev)  # (first, end) pairs
             nb = torch.empty(1, dtype=torch.int32, device=dev)
             ws = torch.empty(lib.rg_conv_blocks_workspace_size(n), dtype=torch.uint8, device=dev)
             nat.check(lib.rg_conv_blocks(self.seg_ptr.data_ptr(), n, tbl.data_ptr(), nb.data_ptr(),

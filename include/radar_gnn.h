@@ -370,7 +370,7 @@ int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, i
                         const int* src, const int* dst, int n_nodes, void* x_out, int ld_out,
                         void* workspace, void* stream);
 /* The same layer over edge-balanced work blocks: block b = destination nodes
- * [blk_nodes[b], blk_nodes[b+1]), *n_blocks_dev blocks (both from rg_conv_blocks; both
+ * [blk_nodes[2b], blk_nodes[2b+1]), *n_blocks_dev blocks (both from rg_conv_blocks; both
  * NULL = runs of 8 nodes, i.e. rg_conv_layer_fused).  Same results, better balance for
  * graphs with few, skewed-degree runs (dense radius frames). */
 int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
@@ -380,7 +380,9 @@ int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_l
                                const int* n_blocks_dev, void* workspace, void* stream);
 /* Work blocks for rg_conv_layer_fused_blocks from the destination-major seg_ptr[N+1]:
  * every run of 8 nodes, split at node boundaries where its edge count would pass
- * max(128, E / 4096).  blk_nodes: int32[N + 1] capacity; n_blocks: int32[1] (device). */
+ * max(128, E / 4096); written as (first node, end node) pairs in dequeue order, each of
+ * the 8 XCD shares sorted by edge tiles, largest first.  blk_nodes: int32[2N] capacity;
+ * n_blocks: int32[1] (device). */
 size_t rg_conv_blocks_workspace_size(int n_nodes);
 int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
                    void* workspace, size_t workspace_bytes, void* stream);

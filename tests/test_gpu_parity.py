@@ -751,10 +751,11 @@ def test_fused_conv_layer_matches_unfused(cuda_device, aggr):
 
 def test_fused_conv_block_table_bit_identical(cuda_device):
     """Edge-balanced work blocks (rg_conv_blocks + rg_conv_layer_fused_blocks) on a
-    skewed-degree radius graph: the table covers every node once, in order, in runs of
-    <= 8 nodes split only where the edge cap is passed, and the layer output is
-    bit-identical to the plain 8-node schedule (each destination still sums its edges in
-    CSR order inside one block)."""
+    skewed-degree radius graph: the (first, end) node pairs cover every node once, in runs
+    of <= 8 nodes split only where the edge cap is passed, each XCD's share of the dequeue
+    order sorted by tile count (largest first), and the layer output is bit-identical to
+    the plain 8-node schedule (each destination still sums its edges in CSR order inside
+    one block)."""
     from graph_neural_network_for_radar_perception_amd import synthetic
     from graph_neural_network_for_radar_perception_amd.config import default_config
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
@@ -775,8 +776,15 @@ def test_fused_conv_block_table_bit_identical(cuda_device):
     tbl, nb = g.conv_blocks()
     assert tbl is not None
     nbk = int(nb.item())
-    t = tbl[:nbk + 1].cpu().numpy()
+    pairs = tbl[:2 * nbk].cpu().numpy().reshape(nbk, 2)
     seg = g.seg_ptr.cpu().numpy()
+    tiles = (seg[pairs[:, 1]] - seg[pairs[:, 0]] + 31) // 32
+    for x in range(8):                                      # per-XCD share: largest first
+        lo, hi = nbk * x // 8, nbk * (x + 1) // 8
+        assert np.all(np.diff(tiles[lo:hi]) <= 0)
+    order = np.argsort(pairs[:, 0], kind='stable')
+    t = np.concatenate([pairs[order, 0], pairs[order[-1:], 1]])
+    assert np.all(pairs[order[:-1], 1] == pairs[order[1:], 0])  # contiguous cover
     assert t[0] == 0 and t[-1] == N and np.all(np.diff(t) >= 1) and np.all(np.diff(t) <= 8)
     assert set(range(0, N, 8)) <= set(t.tolist())          # only splits of the 8-node runs
     cap = max(128, int(seg[N]) // 4096)
