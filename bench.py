@@ -836,9 +836,15 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     if 'edge_encoder' in durs:
         enc_ms = float(np.mean(durs['edge_encoder']))
         enc_flops = 118272.0 * E
-        kern['edge_encoder'].update(algorithmic_tflops=round(enc_flops / (enc_ms * 1e-3) / 1e12, 2),
-                                    flops_per_launch=enc_flops,
-                                    mfma_frac=round(enc_flops / (enc_ms * 1e-3) / 1e12 / peak_tf, 4))
+        enc_tf = enc_flops / (enc_ms * 1e-3) / 1e12
+        kern['edge_encoder'].update(algorithmic_tflops=round(enc_tf, 2), flops_per_launch=enc_flops)
+        from graph_neural_network_for_radar_perception_amd import engine as _eng
+        if args.dtype == 'fp32' and _eng.F32_ARITH == 'x3':
+            # chain_x3_kernel: six bf16 products per f32 product on the bf16 matrix cores
+            kern['edge_encoder'].update(bf16_mfma_tflops=round(6 * enc_tf, 2),
+                                        mfma_frac=round(6 * enc_tf / MFMA_PEAK_TFLOPS['bf16'], 4))
+        else:
+            kern['edge_encoder']['mfma_frac'] = round(enc_tf / peak_tf, 4)
     frac_mfma = conv_exec * tf / conv_peak
     frac_hbm = gbs / HBM_PEAK_GBS
     if frac_mfma >= frac_hbm:

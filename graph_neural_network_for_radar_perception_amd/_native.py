@@ -124,6 +124,10 @@ _SIGNATURES = {
     'rg_conv_layer_x3_workspace_size': (_S, [_I]),
     'rg_conv_layer_x3': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I, _P,
                               _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _S, _P]),
+    'rg_conv_layer_x3_blocks': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P,
+                                     _I, _P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _S, _P]),
+    'rg_conv_x3_blocks_bytes': (_S, [_I]),
+    'rg_conv_x3_blocks': (_I, [_P, _I, _P, _P]),
     'rg_conv_proj_x3': (_I, [ctypes.POINTER(rg_layer), _P, _I, _I, _P, _P]),
     'rg_conv_layer_workspace_size': (_S, []),
     'rg_conv_layer_fused': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P, _I,

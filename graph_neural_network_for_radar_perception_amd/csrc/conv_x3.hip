@@ -69,6 +69,14 @@ __device__ unsigned long long g_cx3_stamp[16];
 #define STAMP(i) do {} while (0)
 #endif
 static constexpr int NXCD = 8;
+static constexpr int TBL_HDR = 16;  // block table: NXCD + 1 block offsets, padded, then pairs
+#ifndef RG_CX3_TAIL
+#define RG_CX3_TAIL 15  // percent of each XCD's nodes cut into TAILN-node blocks (launch tail)
+#endif
+#ifndef RG_CX3_TAILN
+#define RG_CX3_TAILN 8
+#endif
+static constexpr int TAILN = RG_CX3_TAILN;
 static constexpr int CTR_STRIDE = 32;  // block counters one 128-B line apart (per-line atomics)
 static constexpr int CTR_BYTES = 2048; // counter area at the front of the workspace
 #ifndef RG_CX3_FT
@@ -145,6 +153,7 @@ __device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WSrc& 
 }
 
 struct Args {
+  const int* table;      // optional work-block table (rg_conv_x3_blocks), else NBLK-node runs
   const float* x;
   const float* e;
   const float* pq;       // [N][256]: P | Q of this layer
@@ -316,13 +325,16 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   int nb0 = __builtin_amdgcn_readfirstlane(wlo);
   const int nend = __builtin_amdgcn_readfirstlane(whi);
 #else
-  const int blo = (int)((long)a.n_blocks * xcd / NXCD);
-  const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  // with a block table: this XCD's blocks are table[xcd] .. table[xcd + 1] of the (first,
+  // end) node pairs at table + TBL_HDR, largest first
+  const int blo = a.table ? a.table[xcd] : (int)((long)a.n_blocks * xcd / NXCD);
+  const int bhi = a.table ? a.table[xcd + 1] : (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  const int* pairs = a.table ? a.table + TBL_HDR : nullptr;
   int* ctr = a.counters + CTR_STRIDE * xcd;
 #endif
 
 #if RG_CX3_STAMP
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
@@ -338,8 +350,8 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     // state below are then provably wave-uniform (scalar registers and scalar branches)
     const int blk = blo + __builtin_amdgcn_readfirstlane(bi);
     if (blk >= bhi) break;
-    const int n0 = blk * NBLK;
-    const int n1 = min(n0 + NBLK, a.n_nodes);
+    const int n0 = pairs ? pairs[2 * blk] : blk * NBLK;
+    const int n1 = pairs ? pairs[2 * blk + 1] : min(n0 + NBLK, a.n_nodes);
 #endif
     const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
     STAMP(0);  // block fetch
@@ -521,12 +533,13 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     }
     STAMP(8);  // next layer's projections
   }
-#if RG_CX3_STAMP
-  if (lane == 0)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_cx3_stamp[i], st_acc[i]);
-#endif
   // the last workgroup out re-zeroes the counters for the next launch (stream order)
   __syncthreads();
+#if RG_CX3_STAMP
+  STAMP(10);  // end-of-launch wait (this wave idle until its workgroup's last wave is done)
+  if (lane == 0)
+    for (int i = 0; i < 11; ++i) atomicAdd(&g_cx3_stamp[i], st_acc[i]);
+#endif
   if (threadIdx.x == 0) {
     __threadfence();
     if (atomicAdd(a.counters + CTR_STRIDE * NXCD, 1) == (int)gridDim.x - 1) {
@@ -675,11 +688,122 @@ extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int 
   return RG_OK;
 }
 
+// Work blocks of the edge launch for one graph: XCD x's share of the nodes
+// [N x / 8, N (x + 1) / 8) -- its frames' rows in one L2 -- as 32-node runs over the first
+// (100 - RG_CX3_TAIL) % and TAILN-node runs over the rest, all ordered by edge tiles, largest
+// first: the waves take the big blocks first and end on the small ones, so the launch tail
+// (waves idle until the last block of their workgroup ends: 14 % of the wave time with
+// 32-node blocks only, M) shrinks to a few tiles.  Order and size change no result: each
+// destination's messages are summed in CSR order within one block.
+__host__ __device__ inline void x3_share(int n, int x, int& a0, int& sp, int& b0) {
+  a0 = (int)((long)n * x / NXCD);
+  b0 = (int)((long)n * (x + 1) / NXCD);
+  sp = a0 + (int)((long)(b0 - a0) * (100 - RG_CX3_TAIL) / 100 / NBLK) * NBLK;
+}
+__host__ __device__ inline int x3_share_blocks(int n, int x) {
+  int a0, sp, b0;
+  x3_share(n, x, a0, sp, b0);
+  return (sp - a0 + NBLK - 1) / NBLK + (b0 - sp + TAILN - 1) / TAILN;
+}
+__global__ __launch_bounds__(256) void conv_x3_blocks_kernel(const int* __restrict__ seg_ptr,
+                                                             int n, int* __restrict__ table) {
+  constexpr int NBIN = 64;
+  __shared__ int hist[NBIN];
+  const int x = blockIdx.x;
+  int off = 0;
+  for (int xx = 0; xx < x; ++xx) off += x3_share_blocks(n, xx);
+  int a0, sp, b0;
+  x3_share(n, x, a0, sp, b0);
+  const int nmain = (sp - a0 + NBLK - 1) / NBLK;
+  const int m = nmain + (b0 - sp + TAILN - 1) / TAILN;
+  if (threadIdx.x == 0) {
+    table[x] = off;
+    if (x == NXCD - 1) table[NXCD] = off + m;
+  }
+  if (threadIdx.x < NBIN) hist[threadIdx.x] = 0;
+  __syncthreads();
+  auto block = [&](int i, int& n0, int& n1) {
+    if (i < nmain) {
+      n0 = a0 + NBLK * i;
+      n1 = min(n0 + NBLK, sp);
+    } else {
+      n0 = sp + TAILN * (i - nmain);
+      n1 = min(n0 + TAILN, b0);
+    }
+    const int t = (seg_ptr[n1] - seg_ptr[n0] + 31) / 32;
+    return NBIN - 1 - min(t, NBIN - 1);  // bin 0 = the most tiles
+  };
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    int n0, n1;
+    atomicAdd(&hist[block(i, n0, n1)], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < NBIN; ++i) {
+      const int c = hist[i];
+      hist[i] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  int* pairs = table + TBL_HDR;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    int n0, n1;
+    const int pos = off + atomicAdd(&hist[block(i, n0, n1)], 1);
+    pairs[2 * pos] = n0;
+    pairs[2 * pos + 1] = n1;
+  }
+}
+
+static int x3_total_blocks(int n) {
+  int t = 0;
+  for (int x = 0; x < NXCD; ++x) t += x3_share_blocks(n, x);
+  return t;
+}
+
+extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
+  return (size_t)(TBL_HDR + 2 * x3_total_blocks(n_nodes > 0 ? n_nodes : 1)) * sizeof(int);
+}
+
+extern "C" int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream) {
+  RG_REQUIRE(seg_ptr && table && n_nodes >= 1, RG_ERR_ARG, "rg_conv_x3_blocks: bad argument");
+  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, const float* x,
+                         int ldx, const float* e, int lde, const float* pq, const int* seg_ptr,
+                         const int* src, const int* dst, int n_nodes, float* x_out, int ld_out,
+                         float* pq_out, const int* table, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
 extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr,
                                 const float* x, int ldx, const float* e, int lde, const float* pq,
                                 const int* seg_ptr, const int* src, const int* dst, int n_nodes,
                                 float* x_out, int ld_out, float* pq_out, void* workspace,
                                 size_t workspace_bytes, void* stream) {
+  return conv_layer_x3(layers, next_pq, aggr, x, ldx, e, lde, pq, seg_ptr, src, dst, n_nodes,
+                       x_out, ld_out, pq_out, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int rg_conv_layer_x3_blocks(const rg_layer* layers, const rg_layer* next_pq, int aggr,
+                                       const float* x, int ldx, const float* e, int lde,
+                                       const float* pq, const int* seg_ptr, const int* src,
+                                       const int* dst, int n_nodes, float* x_out, int ld_out,
+                                       float* pq_out, const int* table, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  RG_REQUIRE(table, RG_ERR_ARG, "rg_conv_layer_x3_blocks: table from rg_conv_x3_blocks");
+  return conv_layer_x3(layers, next_pq, aggr, x, ldx, e, lde, pq, seg_ptr, src, dst, n_nodes,
+                       x_out, ld_out, pq_out, table, workspace, workspace_bytes, stream);
+}
+
+static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr,
+                         const float* x, int ldx, const float* e, int lde, const float* pq,
+                         const int* seg_ptr, const int* src, const int* dst, int n_nodes,
+                         float* x_out, int ld_out, float* pq_out, const int* table,
+                         void* workspace, size_t workspace_bytes, void* stream) {
   const rg_layer& m0 = layers[0];
   const rg_layer& m1 = layers[1];
   const rg_layer& u = layers[2];
@@ -729,7 +853,8 @@ extern "C" int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq,
   a.lde = lde;
   a.ldo = ld_out;
   a.n_nodes = n_nodes;
-  a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
+  a.n_blocks = table ? x3_total_blocks(n_nodes) : (n_nodes + NBLK - 1) / NBLK;
+  a.table = table;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
   int blocks = 256;  // one workgroup per CU (LDS); a multiple of the 8 XCDs
   const int need = (a.n_blocks + NW - 1) / NW;

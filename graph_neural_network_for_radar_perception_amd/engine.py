@@ -50,6 +50,9 @@ def _half_flag(dtype: str) -> int:
 # layer's projections fused into the update); 'mfma_f32' = v_mfma_f32_32x32x2_f32
 # (rg_conv_layer_f32).  Both keep float32 accuracy (tests/test_gpu_f32.py runs both).
 F32_ARITH = os.environ.get('RG_F32_ARITH', 'x3')
+# x3 conv over the per-graph work-block table (rg_conv_x3_blocks: LPT order, 8-node tail);
+# '0' = plain 32-node runs (same results)
+CONV_X3_TABLE = os.environ.get('RG_CONV_X3_TABLE', '1') != '0'
 
 
 def _dt_code(t: torch.Tensor) -> int:
@@ -437,6 +440,7 @@ class DeviceGraph:
         self.n_edges = n_edges
         self.n_pairs = n_pairs
         self._conv_blocks = None
+        self._conv_x3_blocks = None
         self.frame_ptr = None      # int32 [B+1] device node offsets of the frames (optional)
         self.n_frames = None
         self._segs = {}
@@ -498,6 +502,22 @@ class DeviceGraph:
                       'rg_conv_blocks')
             self._conv_blocks = (tbl, nb)
         return self._conv_blocks
+
+    def conv_x3_blocks(self):
+        """The rg_conv_x3_blocks work-block table of this graph for rg_conv_layer_x3_blocks
+        (one launch, built once per graph), or None with CONV_X3_TABLE off."""
+        n = self.n_nodes
+        if n == 0 or not CONV_X3_TABLE:
+            return None
+        if self._conv_x3_blocks is None:
+            lib = nat.lib()
+            dev = self.seg_ptr.device
+            tbl = torch.empty((lib.rg_conv_x3_blocks_bytes(n) + 3) // 4, dtype=torch.int32,
+                              device=dev)
+            nat.check(lib.rg_conv_x3_blocks(self.seg_ptr.data_ptr(), n, tbl.data_ptr(),
+                                            nat.stream_ptr(dev)), 'rg_conv_x3_blocks')
+            self._conv_x3_blocks = tbl
+        return self._conv_x3_blocks
 
     @staticmethod
     def from_edge_index(edge_index: torch.Tensor, n_nodes: int, count_pairs: bool = True):
@@ -767,12 +787,16 @@ class ConvPlan:
         need = lib.rg_conv_layer_x3_workspace_size(g.n_nodes)
         if self.fused_ws.numel() < need:
             self.fused_ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
-        rc = lib.rg_conv_layer_x3(
-            self.fused_layers, nxt.x3_pq_chain if nxt is not None else None, nat.REDUCE[self.aggr],
-            x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0), pq.data_ptr(),
-            g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes, x_out.data_ptr(),
-            x_out.stride(0), nat.ptr(pq_out), self.fused_ws.data_ptr(), self.fused_ws.numel(),
-            nat.stream_ptr(x.device))
+        tbl = g.conv_x3_blocks()
+        args = (self.fused_layers, nxt.x3_pq_chain if nxt is not None else None,
+                nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
+                pq.data_ptr(), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
+                x_out.data_ptr(), x_out.stride(0), nat.ptr(pq_out))
+        tail = (self.fused_ws.data_ptr(), self.fused_ws.numel(), nat.stream_ptr(x.device))
+        if tbl is not None:
+            rc = lib.rg_conv_layer_x3_blocks(*args, tbl.data_ptr(), *tail)
+        else:
+            rc = lib.rg_conv_layer_x3(*args, *tail)
         if rc == nat.RG_ERR_UNSUPPORTED:
             self.fused_ok = False
             return False

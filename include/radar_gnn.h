@@ -347,6 +347,18 @@ int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, 
                      int ldx, const float* e, int lde, const float* pq, const int* seg_ptr,
                      const int* src, const int* dst, int n_nodes, float* x_out, int ld_out,
                      float* pq_out, void* workspace, size_t workspace_bytes, void* stream);
+/* The same layer over a work-block table from rg_conv_x3_blocks (built once per graph): each
+ * XCD's eighth of the nodes in 32-node blocks, its last 15 % in 8-node blocks, ordered by
+ * edge tiles, largest first, so the launch ends on small blocks.  Same results. */
+int rg_conv_layer_x3_blocks(const rg_layer* layers, const rg_layer* next_pq, int aggr,
+                            const float* x, int ldx, const float* e, int lde, const float* pq,
+                            const int* seg_ptr, const int* src, const int* dst, int n_nodes,
+                            float* x_out, int ld_out, float* pq_out, const int* table,
+                            void* workspace, size_t workspace_bytes, void* stream);
+/* table: rg_conv_x3_blocks_bytes(n_nodes) bytes of device memory -- int32 block offsets per
+ * XCD [9] (padded to 16), then (first node, end node) pairs -- from seg_ptr[n_nodes + 1]. */
+size_t rg_conv_x3_blocks_bytes(int n_nodes);
+int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream);
 /* P | Q of the first layer for dense float32 rows x [n_nodes][ldx >= 64]: pq layer packed
  * RG_PACK_FAST_IN | RG_PACK_X3 (64 -> 256, bias [b_msg0; 0]). */
 int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes, float* pq_out,

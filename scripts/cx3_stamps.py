@@ -35,9 +35,9 @@ with torch.no_grad():
         pipe.forward(batch, gb)
     torch.cuda.synchronize()
     fn(buf)
-v = np.array(buf[:10], dtype=np.float64)
+v = np.array(buf[:11], dtype=np.float64)
 names = ['block fetch', 'gathers+layer1', 'norm1', 'layer2', 'norm2', 'segsum', 'update',
-         'residual+store', 'projection', 'tile-loop exit']
+         'residual+store', 'projection', 'tile-loop exit', 'end wait']
 tot = v.sum()
 for n, x in zip(names, v):
     print(f'{n:16s} {x / tot * 100:6.1f} %  {x / 3 / 7 / 2048 / 1e3:9.1f} k cycles per wave-launch')
