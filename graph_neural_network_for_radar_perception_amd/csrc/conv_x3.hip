@@ -98,7 +98,12 @@ static constexpr int NW = FT / 64;
 #define RG_CX3_NODE_KERNEL 1  // the update / projection phase as a second launch (LDS weights)
 #endif
 #ifndef RG_CX3_LATE
-#define RG_CX3_LATE 0  // 1: the next tile's rows loaded right after this tile's layer 2 (M: 0.62 -> 0.84 ms, rejected)
+#define RG_CX3_LATE 4  // 4: the next tile's e rows (streamed from HBM, 32 registers) loaded right after this
+                      // tile's layer 2, P / Q rows (L2 / MALL) at the tile start (M: -1.4..-2.2 %);
+                      // 1: all its rows there (M: 0.62 -> 0.84 ms, spills); 0: all at the tile start
+#endif
+#ifndef RG_CX3_ENT
+#define RG_CX3_ENT 0  // 1: non-temporal e loads (M: +2.7 %, rejected)
 #endif
 #ifndef RG_CX3_WU_LDS
 #define RG_CX3_WU_LDS 0  // W_u staged in LDS too, 4-row passes (M: 0.650 vs 0.638 ms/layer, slower)
@@ -377,6 +382,27 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
       }
     };
+    auto load_pq = [&](int dq, int sq, Rows& w) {
+      const float* pp = a.pq + (size_t)dq * PQW + 4 * h;
+      const float* pqq = a.pq + (size_t)sq * PQW + HID + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w.p[i] = *(const f32x4*)(pp + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w.q[i] = *(const f32x4*)(pqq + 8 * i);
+    };
+    auto load_e = [&](int q, Rows& w) {
+      const float* pe = a.e + (size_t)q * a.lde + 8 * h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#if RG_CX3_ENT  // streamed once per layer: non-temporal (keeps the reused P | Q rows in L2)
+        w.e[2 * i] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i));
+        w.e[2 * i + 1] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i + 4));
+#else
+        w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
+        w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
+#endif
+      }
+    };
     // tile indices (past the block's last edge clamped: a re-read of a cached row)
     auto tile_idx = [&](int t, int& q, int& dq, int& sq) {
       q = min(t + r, e1 - 1);
@@ -387,11 +413,17 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     Rows nrows;
     Rows rw;       // RG_CX3_LATE: loop-carried, loaded in the previous tile's second half
     int dcur = 0;  // RG_CX3_LATE: the destinations of the rows in rw
+    int scur = 0;  // RG_CX3_LATE 4: their sources
     if (e0 < e1) {
       tile_idx(e0, p1, d1, s1);
       if constexpr (RG_CX3_RPF) {  // rows of tile 0 now, indices of tile 1
         load_rows(p1, d1, s1, nrows);
         tile_idx(e0 + 32, p2, d2, s2);
+      } else if constexpr (RG_CX3_LATE == 4) {
+        load_e(p1, rw);
+        dcur = d1;
+        scur = s1;
+        tile_idx(e0 + 32, p1, d1, s1);
       } else if constexpr (RG_CX3_LATE) {
         load_rows(p1, d1, s1, rw);
         dcur = d1;
@@ -400,7 +432,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     }
     for (int t0 = e0; t0 < e1; t0 += 32) {
       const int d = RG_CX3_LATE ? dcur : d1;
-      if constexpr (RG_CX3_LATE) {
+      if constexpr (RG_CX3_LATE == 4) {
+        load_pq(d, scur, rw);  // e already in flight since the previous tile's second half
+      } else if constexpr (RG_CX3_LATE) {
         // rows already in flight since the previous tile's second half
       } else if constexpr (RG_CX3_RPF) {
         // rows of the next tile now (indices loaded one tile earlier), indices of the tile
@@ -465,8 +499,14 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       if constexpr (RG_CX3_LATE) {
         // acc1 and this tile's rows are dead: the next tile's rows go out now and arrive
         // behind norm 2 and the segmented sum (no registers beyond the rows' own)
+        if constexpr (RG_CX3_LATE == 4) __builtin_amdgcn_sched_barrier(0);
         if (t0 + 32 < e1) {
-          load_rows(p1, d1, s1, rw);
+          if constexpr (RG_CX3_LATE == 4) {
+            load_e(p1, rw);
+            scur = s1;
+          } else {
+            load_rows(p1, d1, s1, rw);
+          }
           dcur = d1;
           tile_idx(t0 + 64, p1, d1, s1);
         }
