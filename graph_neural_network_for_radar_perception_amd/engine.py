@@ -482,7 +482,7 @@ class DeviceGraph:
 
     # few 8-node runs per wave of the fused conv's 2 048-wave grid: dynamic scheduling of
     # whole runs leaves a tail of the heaviest runs (dense radius frames, BASELINE config 5)
-    CONV_BLOCK_TABLE_MAX_RUNS = 4 * 2048
+    CONV_BLOCK_TABLE_MAX_RUNS = int(os.environ.get('RG_CONV_TABLE_MAX_RUNS', 4 * 2048))
 
     def conv_blocks(self):
         """(blk_nodes, n_blocks_dev) of rg_conv_blocks -- edge-balanced work blocks for
