@@ -33,6 +33,11 @@ static constexpr float NORM_EPS = 1e-5f;
 static constexpr int NQ = 8;
 static constexpr int CTR_STRIDE = 32;
 
+#ifndef RG_CONV_STEAL
+#define RG_CONV_STEAL 0  // 1: a wave whose XCD queue drained takes blocks from the others
+                         // (C2 -0.5 %, C5 +23 %: stealers saturate the heads of small blocks)
+#endif
+
 #ifndef RG_CONV_LUT
 #define RG_CONV_LUT 1  // one-hot segment matrix from a 256-entry LDS table (0: per-edge compares)
 #endif
@@ -230,9 +235,25 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // this XCD's share of the blocks: contiguous destination ranges (its L2 then holds the
   // neighbourhoods it gathers), dequeued from its own head
   const int xcd = blockIdx.x % NQ;
-  const int blo = (int)((long)n_blocks * xcd / NQ);
-  const int bhi = (int)((long)n_blocks * (xcd + 1) / NQ);
-  int* const head = a.counter + CTR_STRIDE * xcd;
+  int blo = (int)((long)n_blocks * xcd / NQ);
+  int bhi = (int)((long)n_blocks * (xcd + 1) / NQ);
+  int* head = a.counter + CTR_STRIDE * xcd;
+  // this XCD's queue drained: take blocks from the other XCDs' queues (their tails; the
+  // rows are cold in this L2, but the launch no longer waits on the slowest XCD); -1: done
+  int steal = 0;
+  auto steal_next = [&]() -> int {
+    while (RG_CONV_STEAL && ++steal < NQ) {
+      const int x2 = (xcd + steal) % NQ;
+      blo = (int)((long)n_blocks * x2 / NQ);
+      bhi = (int)((long)n_blocks * (x2 + 1) / NQ);
+      head = a.counter + CTR_STRIDE * x2;
+      int b = 0;
+      if (lane == 0) b = atomicAdd(head, 1);
+      b = blo + __shfl(b, 0, 64);
+      if (b < bhi) return b;
+    }
+    return -1;
+  };
   // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
   auto block_nodes = [&](int b, int& n0, int& n1) {
     if (a.blk_nodes) {
@@ -247,7 +268,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   if (lane == 0) blk = atomicAdd(head, 1);
   blk = blo + __shfl(blk, 0, 64);
   int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
-  if (blk < bhi) {
+  if (blk >= bhi) blk = steal_next();
+  if (blk >= 0) {
     block_nodes(blk, bn0, bn1);
     e0 = a.seg_ptr[bn0];
     e1 = a.seg_ptr[bn1];
@@ -262,7 +284,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
   }
 #endif
-  while (blk < bhi) {
+  while (blk >= 0) {
     const int n0 = bn0;
     const int n1 = bn1;
     int nxt_raw = 0;
@@ -424,9 +446,10 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     }
     CSTAMP(1);
 
-    const int nxt = blo + __shfl(nxt_raw, 0, 64);
+    int nxt = blo + __shfl(nxt_raw, 0, 64);
+    if (nxt >= bhi) nxt = steal_next();
     int ne0 = 0, ne1 = 0, nn0 = 0, nn1 = 0;
-    if (nxt < bhi) {
+    if (nxt >= 0) {
       block_nodes(nxt, nn0, nn1);
       ne0 = a.seg_ptr[nn0];
       ne1 = a.seg_ptr[nn1];

@@ -102,6 +102,11 @@ static constexpr int NW = FT / 64;
                       // tile's layer 2, P / Q rows (L2 / MALL) at the tile start (M: -1.4..-2.2 %);
                       // 1: all its rows there (M: 0.62 -> 0.84 ms, spills); 0: all at the tile start
 #endif
+#ifndef RG_CX3_STEAL
+#define RG_CX3_STEAL 1  // a wave whose XCD queue drained takes blocks from the others (M: conv
+                       // -1.1 %; only with >= 2 blocks per wave: on C5's small blocks the
+                       // 16-bit conv lost 23 % to stealers saturating the other heads)
+#endif
 #ifndef RG_CX3_ENT
 #define RG_CX3_ENT 0  // 1: non-temporal e loads (M: +2.7 %, rejected)
 #endif
@@ -175,6 +180,7 @@ struct Args {
   const float* sd[3];
   int ldx, lde, ldo;
   int n_nodes, n_blocks;
+  int steal;  // RG_CX3_STEAL and >= 2 blocks per wave (small graphs: the heads would saturate)
   int aggr_mean;
 };
 
@@ -332,10 +338,11 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
 #else
   // with a block table: this XCD's blocks are table[xcd] .. table[xcd + 1] of the (first,
   // end) node pairs at table + TBL_HDR, largest first
-  const int blo = a.table ? a.table[xcd] : (int)((long)a.n_blocks * xcd / NXCD);
-  const int bhi = a.table ? a.table[xcd + 1] : (int)((long)a.n_blocks * (xcd + 1) / NXCD);
+  auto xlo = [&](int x) { return a.table ? a.table[x] : (int)((long)a.n_blocks * x / NXCD); };
+  int blo = xlo(xcd), bhi = xlo(xcd + 1);
   const int* pairs = a.table ? a.table + TBL_HDR : nullptr;
   int* ctr = a.counters + CTR_STRIDE * xcd;
+  int steal = 0;  // RG_CX3_STEAL: other XCDs' queues visited after this one drained
 #endif
 
 #if RG_CX3_STAMP
@@ -354,7 +361,15 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     // readfirstlane, not a shuffle: the block id, its node / edge range and the segment
     // state below are then provably wave-uniform (scalar registers and scalar branches)
     const int blk = blo + __builtin_amdgcn_readfirstlane(bi);
-    if (blk >= bhi) break;
+    if (blk >= bhi) {
+      if (!RG_CX3_STEAL || !a.steal || ++steal >= NXCD) break;
+      // this XCD's queue is empty: take the tail of the next one (cold rows, only at the end)
+      const int x2 = (xcd + steal) % NXCD;
+      blo = xlo(x2);
+      bhi = xlo(x2 + 1);
+      ctr = a.counters + CTR_STRIDE * x2;
+      continue;
+    }
     const int n0 = pairs ? pairs[2 * blk] : blk * NBLK;
     const int n1 = pairs ? pairs[2 * blk + 1] : min(n0 + NBLK, a.n_nodes);
 #endif
@@ -900,6 +915,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   const int need = (a.n_blocks + NW - 1) / NW;
   if (blocks > need) blocks = (need + NXCD - 1) / NXCD * NXCD;
   if (blocks < NXCD) blocks = NXCD;
+  a.steal = a.n_blocks >= 2 * blocks * NW;
   constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
   auto edge = cent ? conv_x3_kernel<true, NODE> : conv_x3_kernel<false, NODE>;
   RG_ENSURE_LDS(edge, LDS_BYTES);
