@@ -37,6 +37,9 @@ using namespace ::rg::x3;
 static constexpr int C = 64;      // node / edge / message / output channels
 static constexpr int HID = 128;   // msg_mlp_hidden_dim
 static constexpr int PQW = 2 * HID;
+#ifndef RG_CX3_PQNT
+#define RG_CX3_PQNT 0  // non-temporal P | Q stores (M: +3 %, rejected)
+#endif
 #ifndef RG_CX3_NBLK
 #define RG_CX3_NBLK 32
 #endif
@@ -118,7 +121,8 @@ static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
 #ifndef RG_CX3_EXP
 #define RG_CX3_EXP 0  // timing experiments only (wrong results): 1 no tile norm epilogues,
                       // 2 no segmented sum, 3 no P / Q gathers, 4 no B splits (one plane
-                      // copied), 5 no tile MFMAs, 6 no update / projection phase
+                      // copied), 5 no tile MFMAs, 6 no update / projection phase,
+                      // 7 no P | Q stores
 #endif
 
 static constexpr int WE_OFF = 0;                                   // W_e 64 -> 128 (FAST_IN)
@@ -151,13 +155,18 @@ __device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WSrc& 
 #pragma unroll
     for (int m = 0; m < 2; ++m) acc[m] = ld_bias_frag(bias, 2 * q + m, h);
     layer_x3<4, 2, 8, true>(acc, W, 2 * q, [&](int s) { return b[s]; });
-    if (valid) {
+    if (valid && RG_CX3_EXP != 7) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(f32x4*)(pq_row + 64 * q + 32 * m + 8 * g + 4 * h) =
-              (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = {acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+#if RG_CX3_PQNT
+          __builtin_nontemporal_store(v, (f32x4*)(pq_row + 64 * q + 32 * m + 8 * g + 4 * h));
+#else
+          *(f32x4*)(pq_row + 64 * q + 32 * m + 8 * g + 4 * h) = v;
+#endif
+        }
     }
   }
 }
