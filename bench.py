@@ -162,7 +162,8 @@ def scatter_aggregate_bench(gb, E, N, steps):
     CSR, messages E x 64 already in HBM (synthetic values).  It is the aggregation of the
     unfused paths (fp32, and bf16 shapes the fused kernel does not take); the default bf16
     step fuses it into rg_conv_layer_fused.  Algorithmic bytes per launch:
-    E*C*s_msg + N*C*s_out + (N+1)*4.  Timed with HIP events on the stream it runs on."""
+    E*C*s_msg + N*C*s_out + (N+1)*4.  Timed with HIP events on the stream it runs on
+    (torch's current stream: engine.segment_reduce launches there)."""
     from graph_neural_network_for_radar_perception_amd import engine
     C = 64
     out = {}
@@ -172,14 +173,15 @@ def scatter_aggregate_bench(gb, E, N, steps):
         agg = torch.empty((N, C), dtype=tdt, device=seg.device)
         for _ in range(2):
             engine.segment_reduce(msg, seg, N, 'add', agg)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(steps)]
-        for a, b in evs:
-            a.record()
+        # one event pair around `steps` back-to-back launches (a pair per launch adds its
+        # own stream gap to every timed launch), avg = span / steps
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(steps):
             engine.segment_reduce(msg, seg, N, 'add', agg)
-            b.record()
+        b.record()
         torch.cuda.synchronize()
-        ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        ms = a.elapsed_time(b) / steps
         nbytes = E * C * s + N * C * s + (N + 1) * 4
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {'avg_ms': round(ms, 4), 'bytes_per_launch': nbytes,

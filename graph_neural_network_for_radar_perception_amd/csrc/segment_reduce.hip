@@ -29,10 +29,18 @@ static constexpr int RANGE_BLOCK = 32;   // rows per block maximum (range max-po
 template <typename TS, int VEC>
 using raw_t = std::conditional_t<sizeof(TS) == 4 || VEC == 8, uint4, uint2>;
 
-template <typename TS, int VEC>
+template <typename TS, int VEC, bool NT = false>
 __device__ __forceinline__ raw_t<TS, VEC> load_raw(const TS* __restrict__ p) {
   static_assert(sizeof(TS) == 2 || VEC == 4, "f32 rows: 4 channels per lane");
-  return *(const raw_t<TS, VEC>*)p;
+  if constexpr (NT) {
+    constexpr int W = sizeof(raw_t<TS, VEC>) / 4;
+    typedef uint32_t vw __attribute__((ext_vector_type(W)));
+    const vw v = __builtin_nontemporal_load((const vw*)p);
+    raw_t<TS, VEC> r;
+    __builtin_memcpy(&r, &v, sizeof(r));
+    return r;
+  } else
+    return *(const raw_t<TS, VEC>*)p;
 }
 
 // element types: float, uint16_t = bf16 bits, _Float16 = IEEE fp16
@@ -63,17 +71,16 @@ __device__ __forceinline__ void store_vec(TO* __restrict__ o, const float (&a)[V
 
 // rows [b, e) of src (row(p) = idx ? idx[p] : p) folded into a[]: U = 8 row loads in
 // flight, indices past e clamped to e - 1 (cache hits) and masked out of the fold
-template <typename TS, int VEC, int OP>
+template <typename TS, int VEC, int OP, int U = 8, bool NT = false>
 __device__ __forceinline__ void fold_rows(const TS* __restrict__ src, int ld, const int* __restrict__ idx,
                                           int c, int b, int e, float (&a)[VEC]) {
-  constexpr int U = 8;
   for (int p = b; p < e; p += U) {
     raw_t<TS, VEC> x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = p + u < e ? p + u : e - 1;
       const size_t row = idx ? (size_t)idx[q] : (size_t)q;
-      x[u] = load_raw<TS, VEC>(src + row * ld + c);
+      x[u] = load_raw<TS, VEC, NT>(src + row * ld + c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -93,7 +100,7 @@ __device__ __forceinline__ void fold_rows(const TS* __restrict__ src, int ld, co
 // of the range max-pool.  bm (max only): 32-row block maxima of src; a long range then
 // reads its head rows, its whole blocks from bm and its tail rows (exact: max is
 // order-free).
-template <typename TS, typename TO, int OP, int VEC>
+template <typename TS, typename TO, int OP, int VEC, int U = 8, bool NT = false>
 __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
                                                              const int* __restrict__ seg_end,
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
         fold_rows<TS, VEC, OP>(bm, ld_bm, nullptr, c, hb, te, a);
         fold_rows<TS, VEC, OP>(src, ld_src, nullptr, c, te * RANGE_BLOCK, e, a);
       } else {
-        fold_rows<TS, VEC, OP>(src, ld_src, idx, c, b, e, a);
+        fold_rows<TS, VEC, OP, U, NT>(src, ld_src, idx, c, b, e, a);
       }
       if (OP == RG_REDUCE_MAX) {
         if (e == b)
@@ -141,6 +148,71 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
       }
       store_vec<TO, VEC>(out + (size_t)s * ld_out + c, a);
     }
+  }
+}
+
+// Short destination segments (kNN graphs: ~13 rows of 128 B per bf16 segment) leave the
+// one-segment-per-group kernel a seg_ptr -> rows round trip per 1.6 KiB.  This variant
+// gives each lane group G consecutive segments as ONE contiguous row stream
+// [seg_ptr[s0], seg_ptr[s0 + G]) (destination-major messages are contiguous): 8 row loads
+// in flight across segment boundaries, a finished segment stored and the sum restarted at
+// each boundary (segment pointers held one per lane of the group, read by shuffle).  Each
+// segment is still summed from its first row in order: bit-identical to the kernel above.
+// Sum / mean, no row index, C a multiple of 64.
+template <typename TS, typename TO, int OP, int VEC, int G, bool NT>
+__global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restrict__ src, int ld_src,
+                                                             const int* __restrict__ seg_ptr,
+                                                             int n_seg, int C, TO* __restrict__ out,
+                                                             int ld_out) {
+  constexpr int LPS = 64 / VEC;
+  constexpr int GPB = 256 / LPS;
+  constexpr int U = 8;
+  static_assert(G <= LPS, "one segment pointer per lane of the group");
+  const int g = threadIdx.x % LPS;
+  const int s0 = (blockIdx.x * GPB + threadIdx.x / LPS) * G;
+  if (s0 >= n_seg) return;
+  const int ns = min(G, n_seg - s0);
+  const int my_ptr = seg_ptr[s0 + min(g, ns)];
+  const int p_end = seg_ptr[s0 + ns];
+  // ptr_at(j) is called with j uniform over the lane group (all its lanes active)
+  auto ptr_at = [&](int j) { return j >= ns ? p_end : __shfl(my_ptr, j, LPS); };
+  const int p_beg = ptr_at(0);
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + VEC * g;
+    float a[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) a[i] = 0.f;
+    int s = 0, b_cur = p_beg, e_cur = ptr_at(1);
+    auto finish = [&]() {
+      if (OP == RG_REDUCE_MEAN) {
+        const float n = (float)(e_cur - b_cur > 0 ? e_cur - b_cur : 1);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) a[i] = __fdiv_rn(a[i], n);
+      }
+      store_vec<TO, VEC>(out + (size_t)(s0 + s) * ld_out + c, a);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) a[i] = 0.f;
+      ++s;
+      b_cur = e_cur;
+      e_cur = ptr_at(s + 1);
+    };
+    for (int p = p_beg; p < p_end; p += U) {
+      raw_t<TS, VEC> x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = p + u < p_end ? p + u : p_end - 1;
+        x[u] = load_raw<TS, VEC, NT>(src + (size_t)q * ld_src + c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (p + u < p_end) {
+          while (p + u >= e_cur) finish();
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) a[i] = __fadd_rn(a[i], chan<TS, VEC>(x[u], i));
+        }
+      }
+    }
+    while (s < ns) finish();
   }
 }
 
@@ -166,7 +238,21 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
 #define RG_SEG_ARGS                                                                         \
   (const TS*)g.src, g.ld_src, g.seg_ptr, g.seg_end, g.idx, g.uni, g.n_uni, (const TS*)g.bm,   \
       g.ld_bm, g.n_seg, g.C, (TO*)g.out, g.ld_out
-  if (op == RG_REDUCE_SUM)
+  // sum / mean over a plain CSR: the streaming kernel, two segments per lane group,
+  // non-temporal row loads (M's CSR, bf16: 0.56 -> 0.70 of HBM; scripts/seg_variants.py).
+  // RG_SEG_STREAM=0 selects the one-segment-per-group kernel (A/B measurement knob).
+  static const bool stream_on = !getenv("RG_SEG_STREAM") || atoi(getenv("RG_SEG_STREAM")) != 0;
+  constexpr int GPB = 256 / (64 / VEC);
+  constexpr int G = 2;
+  if (stream_on && op != RG_REDUCE_MAX && !g.idx && !g.seg_end && g.uni == 0 && g.C % 64 == 0) {
+    const int grid_s = ceil_div(ceil_div(g.n_seg, G), GPB);
+#define RG_STREAM_ARGS (const TS*)g.src, g.ld_src, g.seg_ptr, g.n_seg, g.C, (TO*)g.out, g.ld_out
+    if (op == RG_REDUCE_SUM)
+      segment_stream_kernel<TS, TO, RG_REDUCE_SUM, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
+    else
+      segment_stream_kernel<TS, TO, RG_REDUCE_MEAN, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
+#undef RG_STREAM_ARGS
+  } else if (op == RG_REDUCE_SUM)
     segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
   else if (op == RG_REDUCE_MEAN)
     segment_reduce_kernel<TS, TO, RG_REDUCE_MEAN, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
