@@ -769,8 +769,12 @@ __host__ __device__ inline int x3_share_blocks(int n, int x) {
   x3_share(n, x, a0, sp, b0);
   return (sp - a0 + NBLK - 1) / NBLK + (b0 - sp + TAILN - 1) / TAILN;
 }
+// order (RG_CX3_ORDER, measurement knob): 0 = every block by edge tiles, largest first;
+// 1 = the 32-node blocks in node order (consecutive blocks share their frame's rows in
+// L2), then the tail blocks largest first; 2 = every block in node order
 __global__ __launch_bounds__(256) void conv_x3_blocks_kernel(const int* __restrict__ seg_ptr,
-                                                             int n, int* __restrict__ table) {
+                                                             int n, int* __restrict__ table,
+                                                             int order) {
   constexpr int NBIN = 64;
   __shared__ int hist[NBIN];
   const int x = blockIdx.x;
@@ -797,7 +801,8 @@ __global__ __launch_bounds__(256) void conv_x3_blocks_kernel(const int* __restri
     const int t = (seg_ptr[n1] - seg_ptr[n0] + 31) / 32;
     return NBIN - 1 - min(t, NBIN - 1);  // bin 0 = the most tiles
   };
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+  const int sorted0 = order == 0 ? 0 : order == 1 ? nmain : m;  // blocks [sorted0, m) sorted
+  for (int i = sorted0 + threadIdx.x; i < m; i += blockDim.x) {
     int n0, n1;
     atomicAdd(&hist[block(i, n0, n1)], 1);
   }
@@ -814,7 +819,8 @@ __global__ __launch_bounds__(256) void conv_x3_blocks_kernel(const int* __restri
   int* pairs = table + TBL_HDR;
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     int n0, n1;
-    const int pos = off + atomicAdd(&hist[block(i, n0, n1)], 1);
+    const int bin = block(i, n0, n1);
+    const int pos = off + (i < sorted0 ? i : sorted0 + atomicAdd(&hist[bin], 1));
     pairs[2 * pos] = n0;
     pairs[2 * pos + 1] = n1;
   }
@@ -832,7 +838,8 @@ extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
 
 extern "C" int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream) {
   RG_REQUIRE(seg_ptr && table && n_nodes >= 1, RG_ERR_ARG, "rg_conv_x3_blocks: bad argument");
-  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table);
+  static const int order = getenv("RG_CX3_ORDER") ? atoi(getenv("RG_CX3_ORDER")) : 0;
+  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table, order);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
