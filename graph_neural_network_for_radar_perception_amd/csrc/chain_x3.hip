@@ -422,6 +422,10 @@ static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<
 #define RG_X3_ENC_RT 2  // row tiles per wave of the encoders (1 wave / SIMD at 2)
 #endif
 
+#ifndef RG_X3_HEAD_RT
+#define RG_X3_HEAD_RT 1  // row tiles per wave of the 5-layer task-head chains (two waves / SIMD at 1)
+#endif
+
 static int dispatch(const Key& k, const Args& a, hipStream_t st) {
 #define RG_X3C(MODE, K0, SP, LM, RT, FT, ...) \
   if (match(k, MODE, K0, SP, {__VA_ARGS__})) return launch<MODE, SP, LM, RT, FT, K0, __VA_ARGS__>(a, st);
@@ -437,8 +441,9 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   // node encoder 6 -> 256 -> 128 -> 64
   RG_X3C2(IN_SMALL, 6, 0b110, 0b111, 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 64)
   // task heads: 3-block stem + FFN_TaskSpecificHead (ffn + bare Linear -> 7 / 2, padded)
-  RG_X3C2(IN_DENSE, 64, 0b1111, 0b1111, ALL, 1, 512, 64, 64, 64, 64, 32)
-  RG_X3C2(IN_PAIR, 64, 0b1111, 0b1111, ALL, 1, 512, 64, 64, 64, 64, 32)
+  constexpr int HFT = RG_X3_HEAD_RT == 1 ? 512 : 256;
+  RG_X3C2(IN_DENSE, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
+  RG_X3C2(IN_PAIR, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
   // link edge_formation stem (1 block), object-class stem (3 blocks), object head
   RG_X3C2(IN_DENSE, 64, 0b1, 0b1, ALL, 1, 512, 64)
   RG_X3C2(IN_DENSE, 64, 0b111, 0b111, ALL, 1, 512, 64, 64, 64)

@@ -620,9 +620,13 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
 static constexpr int NU_OFF = 0;
 static constexpr int NPQ_OFF = al16(x3_bytes(2 * C, C));
 static constexpr int NODE_LDS = NPQ_OFF + al16(x3_bytes(C, PQW));
+#ifndef RG_CX3_NODE_FT
+#define RG_CX3_NODE_FT 512  // node launch workgroup: 8 waves = two per SIMD (170 VGPRs)
+#endif
+static constexpr int NFT = RG_CX3_NODE_FT, NW_NODE = NFT / 64;
 static_assert(NODE_LDS <= DYN_LDS_MAX, "node_x3 LDS");
 template <bool CENT>
-__global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
+__global__ __launch_bounds__(NFT) void node_x3_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[2];
   if (threadIdx.x == 0) {
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
     const int off[2] = {NU_OFF, NPQ_OFF};
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
-      stage_lds<512>(lds + off[l], src[l], nb[l]);
+      stage_lds<NFT>(lds + off[l], src[l], nb[l]);
     }
   }
   __syncthreads();
@@ -646,17 +650,17 @@ __global__ __launch_bounds__(512) void node_x3_kernel(Args a) {
   const float* biasPQ = (const float*)(lds + NPQ_OFF + 3 * plane_bytes(C, PQW));
   const float muU = nrm[0], sdU = nrm[1];
   const int ntiles = (a.n_nodes + 31) / 32;
-  const int stride = gridDim.x * 8;
+  const int stride = gridDim.x * NW_NODE;
   // the next tile's rows are loaded while this one computes; unrolled by two with separate
   // row buffers (a register copy of a loaded value would wait for the load)
 #if !RG_CX3_NODE_PF
-  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += stride)
+  for (int t = blockIdx.x * NW_NODE + wave; t < ntiles; t += stride)
     node_update<CENT>(a, 32 * t, min(32 * t + 32, a.n_nodes), wU, biasU, wPQ, biasPQ, muU, sdU,
                       lane);
   return;
 #endif
   NodeRows rA, rB;
-  int t = blockIdx.x * 8 + wave;
+  int t = blockIdx.x * NW_NODE + wave;
   auto tile_end = [&](int tt) { return min(32 * tt + 32, a.n_nodes); };
   if (t < ntiles) load_node_rows(a, 32 * t, tile_end(t), lane, rA);
   while (t < ntiles) {
@@ -941,8 +945,8 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
     auto node = cent ? node_x3_kernel<true> : node_x3_kernel<false>;
     RG_ENSURE_LDS(node, NODE_LDS);
     const int tiles = (n_nodes + 31) / 32;
-    const int nblk = (tiles + 7) / 8 < 256 ? (tiles + 7) / 8 : 256;
-    node<<<nblk, 512, NODE_LDS, (hipStream_t)stream>>>(a);
+    const int nblk = (tiles + NW_NODE - 1) / NW_NODE < 256 ? (tiles + NW_NODE - 1) / NW_NODE : 256;
+    node<<<nblk, NFT, NODE_LDS, (hipStream_t)stream>>>(a);
     RG_LAUNCH_CHECK();
   }
   return RG_OK;
