@@ -107,13 +107,18 @@ extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, i
   int* off = (int*)((char*)workspace + arr);  // their exclusive scan
   int* bounds = (int*)((char*)workspace + 2 * arr);  // block boundaries in node order
   void* sws = (char*)workspace + 2 * arr + ((size_t)((n_nodes + 1) * sizeof(int)) + 255) / 256 * 256;
+  // block edge cap max(cap_min, E / cap_div); RG_CONV_CAP_MIN / RG_CONV_CAP_DIV are
+  // measurement knobs
+  static const int cap_min = getenv("RG_CONV_CAP_MIN") ? atoi(getenv("RG_CONV_CAP_MIN")) : CAP_MIN;
+  static const int cap_div = getenv("RG_CONV_CAP_DIV") ? atoi(getenv("RG_CONV_CAP_DIV")) : 4096;
+  RG_REQUIRE(cap_min >= 1 && cap_div >= 1, RG_ERR_ARG, "rg_conv_blocks: bad RG_CONV_CAP_*");
   conv_blocks_kernel<false><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, cnt, nullptr,
-                                                                nullptr);
+                                                                nullptr, cap_min, cap_div);
   RG_LAUNCH_CHECK();
   int rc = exclusive_scan(cnt, nb8, off, n_blocks, sws, st);
   if (rc) return rc;
   conv_blocks_kernel<true><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, nullptr, off,
-                                                               bounds);
+                                                               bounds, cap_min, cap_div);
   RG_LAUNCH_CHECK();
   conv_blocks_lpt<<<NQ, 256, 0, st>>>(bounds, seg_ptr, n_blocks, blk_nodes);
   RG_LAUNCH_CHECK();

@@ -574,18 +574,19 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 // (~300 edges per 8 nodes, cap 1 778) keeps its 8-node runs.
 static constexpr int CAP_MIN = 128;
 
-__device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes) {
-  return max(CAP_MIN, seg_ptr[n_nodes] / 4096);
+__device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes, int cap_min,
+                                         int cap_div) {
+  return max(cap_min, seg_ptr[n_nodes] / cap_div);
 }
 
 template <bool EMIT>
 __global__ void conv_blocks_kernel(const int* __restrict__ seg_ptr, int n_nodes,
                                    int* __restrict__ cnt, const int* __restrict__ off,
-                                   int* __restrict__ blk_nodes) {
+                                   int* __restrict__ blk_nodes, int cap_min, int cap_div) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int nb8 = (n_nodes + NB - 1) / NB;
   if (b >= nb8) return;
-  const int cap = block_cap(seg_ptr, n_nodes);
+  const int cap = block_cap(seg_ptr, n_nodes, cap_min, cap_div);
   const int n0 = b * NB, n1 = min(n0 + NB, n_nodes);
   int c = 0, acc = 0, o = EMIT ? off[b] : 0;
   for (int n = n0; n < n1; ++n) {

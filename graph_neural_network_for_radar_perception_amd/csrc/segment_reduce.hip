@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
 // in flight across segment boundaries, a finished segment stored and the sum restarted at
 // each boundary (segment pointers held one per lane of the group, read by shuffle).  Each
 // segment is still summed from its first row in order: bit-identical to the kernel above.
-// Sum / mean, no row index, C a multiple of 64.
+// Sum / mean / max, no row index, C a multiple of 64.
 template <typename TS, typename TO, int OP, int VEC, int G, bool NT>
 __global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
@@ -179,19 +179,23 @@ __global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restric
   const int p_beg = ptr_at(0);
   for (int c0 = 0; c0 < C; c0 += 64) {
     const int c = c0 + VEC * g;
+    constexpr float A0 = OP == RG_REDUCE_MAX ? -__builtin_inff() : 0.f;
     float a[VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) a[i] = 0.f;
+    for (int i = 0; i < VEC; ++i) a[i] = A0;
     int s = 0, b_cur = p_beg, e_cur = ptr_at(1);
     auto finish = [&]() {
       if (OP == RG_REDUCE_MEAN) {
         const float n = (float)(e_cur - b_cur > 0 ? e_cur - b_cur : 1);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) a[i] = __fdiv_rn(a[i], n);
+      } else if (OP == RG_REDUCE_MAX && e_cur == b_cur) {  // empty segment -> 0
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) a[i] = 0.f;
       }
       store_vec<TO, VEC>(out + (size_t)(s0 + s) * ld_out + c, a);
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) a[i] = 0.f;
+      for (int i = 0; i < VEC; ++i) a[i] = A0;
       ++s;
       b_cur = e_cur;
       e_cur = ptr_at(s + 1);
@@ -208,7 +212,10 @@ __global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restric
         if (p + u < p_end) {
           while (p + u >= e_cur) finish();
 #pragma unroll
-          for (int i = 0; i < VEC; ++i) a[i] = __fadd_rn(a[i], chan<TS, VEC>(x[u], i));
+          for (int i = 0; i < VEC; ++i) {
+            const float v = chan<TS, VEC>(x[u], i);
+            a[i] = OP == RG_REDUCE_MAX ? fmaxf(a[i], v) : __fadd_rn(a[i], v);
+          }
         }
       }
     }
@@ -238,19 +245,21 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
 #define RG_SEG_ARGS                                                                         \
   (const TS*)g.src, g.ld_src, g.seg_ptr, g.seg_end, g.idx, g.uni, g.n_uni, (const TS*)g.bm,   \
       g.ld_bm, g.n_seg, g.C, (TO*)g.out, g.ld_out
-  // sum / mean over a plain CSR: the streaming kernel, two segments per lane group,
+  // sum / mean / max over a plain CSR: the streaming kernel, two segments per lane group,
   // non-temporal row loads (M's CSR, bf16: 0.56 -> 0.70 of HBM; scripts/seg_variants.py).
   // RG_SEG_STREAM=0 selects the one-segment-per-group kernel (A/B measurement knob).
   static const bool stream_on = !getenv("RG_SEG_STREAM") || atoi(getenv("RG_SEG_STREAM")) != 0;
   constexpr int GPB = 256 / (64 / VEC);
   constexpr int G = 2;
-  if (stream_on && op != RG_REDUCE_MAX && !g.idx && !g.seg_end && g.uni == 0 && g.C % 64 == 0) {
+  if (stream_on && !g.idx && !g.seg_end && !g.bm && g.uni == 0 && g.C % 64 == 0) {
     const int grid_s = ceil_div(ceil_div(g.n_seg, G), GPB);
 #define RG_STREAM_ARGS (const TS*)g.src, g.ld_src, g.seg_ptr, g.n_seg, g.C, (TO*)g.out, g.ld_out
     if (op == RG_REDUCE_SUM)
       segment_stream_kernel<TS, TO, RG_REDUCE_SUM, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
-    else
+    else if (op == RG_REDUCE_MEAN)
       segment_stream_kernel<TS, TO, RG_REDUCE_MEAN, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
+    else
+      segment_stream_kernel<TS, TO, RG_REDUCE_MAX, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
 #undef RG_STREAM_ARGS
   } else if (op == RG_REDUCE_SUM)
     segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
