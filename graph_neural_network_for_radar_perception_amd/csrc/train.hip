@@ -331,9 +331,16 @@ static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
   g.ot = (out_dim + 64 * g.ow - 1) / (64 * g.ow);
   g.it = (in_dim + 16 * g.nt - 1) / (16 * g.nt);
   const long blocks = (rows + GR - 1) / GR;
-  long want = 256 / (g.ot * g.it);  // ~one workgroup per CU
+  // two workgroups per CU (one's row staging overlaps another's MFMAs: the kernel stages
+  // single-buffered) and chunks of >= 8 staged blocks of GR rows -- c4 backward 20.4 ->
+  // 17.0 ms against one workgroup per CU and >= 32 blocks; RG_GRAD_WG_PER_CU /
+  // RG_GRAD_MIN_BLOCKS are the measurement knobs
+  static const int wg_cu = getenv("RG_GRAD_WG_PER_CU") ? atoi(getenv("RG_GRAD_WG_PER_CU")) : 2;
+  static const int min_blk = getenv("RG_GRAD_MIN_BLOCKS") ? atoi(getenv("RG_GRAD_MIN_BLOCKS")) : 8;
+  long want = 256L * (wg_cu > 0 ? wg_cu : 1) / (g.ot * g.it);
   if (want < 1) want = 1;
-  if (want > (blocks + 31) / 32) want = (blocks + 31) / 32;  // >= 1024 rows per chunk
+  const long mb = min_blk > 0 ? min_blk : 1;
+  if (want > (blocks + mb - 1) / mb) want = (blocks + mb - 1) / mb;
   if (want < 1) want = 1;
   g.rpc = ((blocks + want - 1) / want) * GR;
   g.nchunk = (int)((rows + g.rpc - 1) / g.rpc);
