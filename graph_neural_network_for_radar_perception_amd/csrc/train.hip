@@ -436,14 +436,36 @@ __global__ __launch_bounds__(256) void gather_segsum_kernel(
   for (int v = blockIdx.x * 4 + wave; v < n_nodes; v += gridDim.x * 4) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int b = ptr[v], e = ptr[v + 1];
-    for (int k = b; k < e; ++k) {
-      const int row = list ? list[k] : k;
-      const float sc = scale ? scale[row] : 1.f;
-      const float* p = src + (size_t)row * ld_src + col0;
+    // U list entries, then U rows in flight (indices past e clamped to e - 1 and masked);
+    // the rows are still added in list order
+    constexpr int U = 8;
+    for (int k = b; k < e; k += U) {
+      int rw[U];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = lane + 64 * j;
-        if (f < width) acc[j] += scale ? p[f] * sc : p[f];
+      for (int u = 0; u < U; ++u) {
+        const int q = k + u < e ? k + u : e - 1;
+        rw[u] = list ? list[q] : q;
+      }
+      float sc[U], x[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        sc[u] = scale ? scale[rw[u]] : 1.f;
+        const float* p = src + (size_t)rw[u] * ld_src + col0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int f = lane + 64 * j;
+          x[u][j] = f < width ? p[f] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u < e) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int f = lane + 64 * j;
+            if (f < width) acc[j] += scale ? x[u][j] * sc[u] : x[u][j];
+          }
+        }
       }
     }
 #pragma unroll
