@@ -332,11 +332,11 @@ static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
   g.it = (in_dim + 16 * g.nt - 1) / (16 * g.nt);
   const long blocks = (rows + GR - 1) / GR;
   // two workgroups per CU (one's row staging overlaps another's MFMAs: the kernel stages
-  // single-buffered) and chunks of >= 8 staged blocks of GR rows -- c4 backward 20.4 ->
-  // 17.0 ms against one workgroup per CU and >= 32 blocks; RG_GRAD_WG_PER_CU /
-  // RG_GRAD_MIN_BLOCKS are the measurement knobs
+  // single-buffered) and chunks of >= 4 staged blocks of GR rows (the partials' reduction
+  // keeps eight loads in flight) -- c4 backward 20.4 -> 15.5 ms against one workgroup per
+  // CU and >= 32 blocks; RG_GRAD_WG_PER_CU / RG_GRAD_MIN_BLOCKS are the measurement knobs
   static const int wg_cu = getenv("RG_GRAD_WG_PER_CU") ? atoi(getenv("RG_GRAD_WG_PER_CU")) : 2;
-  static const int min_blk = getenv("RG_GRAD_MIN_BLOCKS") ? atoi(getenv("RG_GRAD_MIN_BLOCKS")) : 8;
+  static const int min_blk = getenv("RG_GRAD_MIN_BLOCKS") ? atoi(getenv("RG_GRAD_MIN_BLOCKS")) : 4;
   long want = 256L * (wg_cu > 0 ? wg_cu : 1) / (g.ot * g.it);
   if (want < 1) want = 1;
   const long mb = min_blk > 0 ? min_blk : 1;
@@ -373,9 +373,11 @@ __global__ __launch_bounds__(256) void linear_grad_reduce(
     const int ot = o / oc, oo = o % oc;
     if (i < in_dim) {
       const int it = i / ic, ii = i % ic;
+#pragma unroll 8  // eight partial loads in flight; still added in chunk order
       for (int c = wave; c < nchunk; c += 4)
         s += part[((size_t)(c * ot_n + ot) * it_n + it) * oc * ic + (size_t)oo * ic + ii];
     } else {
+#pragma unroll 8
       for (int c = wave; c < nchunk; c += 4) s += part_b[((size_t)c * ot_n + ot) * oc + oo];
     }
   }
@@ -436,36 +438,14 @@ __global__ __launch_bounds__(256) void gather_segsum_kernel(
   for (int v = blockIdx.x * 4 + wave; v < n_nodes; v += gridDim.x * 4) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int b = ptr[v], e = ptr[v + 1];
-    // U list entries, then U rows in flight (indices past e clamped to e - 1 and masked);
-    // the rows are still added in list order
-    constexpr int U = 8;
-    for (int k = b; k < e; k += U) {
-      int rw[U];
+    for (int k = b; k < e; ++k) {
+      const int row = list ? list[k] : k;
+      const float sc = scale ? scale[row] : 1.f;
+      const float* p = src + (size_t)row * ld_src + col0;
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int q = k + u < e ? k + u : e - 1;
-        rw[u] = list ? list[q] : q;
-      }
-      float sc[U], x[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        sc[u] = scale ? scale[rw[u]] : 1.f;
-        const float* p = src + (size_t)rw[u] * ld_src + col0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int f = lane + 64 * j;
-          x[u][j] = f < width ? p[f] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (k + u < e) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int f = lane + 64 * j;
-            if (f < width) acc[j] += scale ? x[u][j] * sc[u] : x[u][j];
-          }
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int f = lane + 64 * j;
+        if (f < width) acc[j] += scale ? p[f] * sc : p[f];
       }
     }
 #pragma unroll
