@@ -25,6 +25,7 @@ namespace rg {
 namespace train {
 
 static constexpr int PARTS = 512;          // fixed grid of the partial-sum kernels
+static constexpr int FFN_PARTS_MAX = 4096;  // ffn_backward grid bound (workspace size)
 static constexpr float NORM_EPS = 1e-5f;   // constants.py:9
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -153,13 +154,13 @@ __global__ __launch_bounds__(256) void ffn_backward_kernel(
 }
 
 // sum of PARTS (s, m) partials in a fixed order, added to the parameter gradients
-__global__ __launch_bounds__(256) void ffn_param_reduce(const float* __restrict__ part,
+__global__ __launch_bounds__(256) void ffn_param_reduce(const float* __restrict__ part, int parts,
                                                         float* __restrict__ d_mu,
                                                         float* __restrict__ d_sd) {
   __shared__ float red[4][2];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   float s = 0.f, m = 0.f;
-  for (int i = t; i < PARTS; i += 256) {
+  for (int i = t; i < parts; i += 256) {
     s += part[2 * i];
     m += part[2 * i + 1];
   }
@@ -656,7 +657,9 @@ using namespace rg;
 using namespace rg::train;
 
 // ----------------------------------------------------------------------------- C ABI
-extern "C" size_t rg_ffn_backward_workspace_size(void) { return (size_t)PARTS * 2 * sizeof(float); }
+extern "C" size_t rg_ffn_backward_workspace_size(void) {
+  return (size_t)FFN_PARTS_MAX * 2 * sizeof(float);
+}
 
 extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
                                int has_norm, const float* mu, const float* std_, int act,
@@ -669,21 +672,26 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
   if (rows <= 0) return RG_OK;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)workspace;
+  // 2048 workgroups (8 waves per SIMD: each 16-lane group's row loop is one dependent
+  // load -> compute -> store chain; 512 left it latency-bound, c4 backward -0.7 ms);
+  // RG_FFN_PARTS is the measurement knob
+  static const int parts_env = getenv("RG_FFN_PARTS") ? atoi(getenv("RG_FFN_PARTS")) : 2048;
+  const int parts = parts_env < 1 ? 1 : parts_env > FFN_PARTS_MAX ? FFN_PARTS_MAX : parts_env;
   if (C <= 16)
-    ffn_backward_kernel<1><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+    ffn_backward_kernel<1><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
                                                   act, dz, lddz, part);
   else if (C <= 64)
-    ffn_backward_kernel<4><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+    ffn_backward_kernel<4><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
                                                   act, dz, lddz, part);
   else if (C <= 128)
-    ffn_backward_kernel<8><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+    ffn_backward_kernel<8><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
                                                   act, dz, lddz, part);
   else
-    ffn_backward_kernel<16><<<PARTS, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
+    ffn_backward_kernel<16><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
                                                    act, dz, lddz, part);
   RG_LAUNCH_CHECK();
   if (has_norm) {
-    ffn_param_reduce<<<1, 256, 0, st>>>(part, d_mu, d_std);
+    ffn_param_reduce<<<1, 256, 0, st>>>(part, parts, d_mu, d_std);
     RG_LAUNCH_CHECK();
   }
   return RG_OK;
