@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out/c4g
 for r in 1 2; do
-  for v in "" "RG_FFN_PARTS=512 RG_GRAD_WG_PER_CU=1 RG_GRAD_MIN_BLOCKS=32"; do
+  for v in ""; do
     env $v timeout -k 10 300 python bench.py --config c4 --no-cpu-baseline > gpurun_out/c4g/o.log 2> gpurun_out/c4g/o.err
     rc=$?; [ $rc -ne 0 ] && { echo "[$v] rc=$rc"; tail -5 gpurun_out/c4g/o.err; exit $rc; }
     python - "$v" <<'PY'
