@@ -95,15 +95,15 @@ struct ChainArgs {
 // ------------------------------------------------------------------ packing
 // f32 : [m][s4][lane][4] = W[16m + (lane&15)][16*s4 + 4*(lane>>4) + t]
 // bf16: [m][s ][lane][8] = W[16m + (lane&15)][32*s  + 8*(lane>>4) + j]
-// weights, then (bias != nullptr) the nb bias entries that follow them in the image: one
-// launch per packed f32 layer (the training step repacks every layer after each SGD step)
+// weights, then the nb bias entries that follow them in the image (zeros without a bias):
+// one launch per packed f32 layer (the training step repacks every layer after each SGD step)
 __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, int transpose,
                                 float* __restrict__ P, long total,
                                 const float* __restrict__ bias = nullptr, int nb = 0) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) {
     const long i = t - total;
-    if (i < nb) P[t] = i < out ? bias[i] : 0.f;
+    if (i < nb) P[t] = (bias && i < out) ? bias[i] : 0.f;
     return;
   }
   const int S4 = kpad(in, 16) / 16;
@@ -665,7 +665,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
              "rg_pack_linear: RG_PACK_TRANSPOSE applies to RG_F32");
   RG_REQUIRE(!center || (dtype >= RG_PACK_FAST_IN && dtype <= RG_PACK_FAST_UPD), RG_ERR_ARG,
              "rg_pack_linear: RG_PACK_CENTERED applies to the bf16 RG_PACK_FAST_* formats");
-  if (dtype == RG_F32 && bias) {
+  if (dtype == RG_F32) {
     // weights and bias in one launch (the bias follows the weights: pb below)
     const long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
     const int nb = kpad(out_dim, 16);
@@ -674,11 +674,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
     RG_LAUNCH_CHECK();
     return RG_OK;
   }
-  if (dtype == RG_F32) {
-    long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
-    pack_f32_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
-                                                          (float*)packed, total);
-  } else if (dtype == RG_BF16) {
+  if (dtype == RG_BF16) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, 0, 0,
                                                            (uint16_t*)packed, total);
