@@ -110,10 +110,47 @@ def parse():
     return a
 
 
-def setup_dist():
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE from a launcher): start N child
+    processes of this same script, one per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N,
+    rendezvous on 127.0.0.1), and return the worst exit code.  Called before this process
+    makes any HIP call; the children are new processes (no exec of a GPU process).  Rank 0
+    prints the JSON line to the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    # a rank that fails would leave the others waiting in a collective: stop them
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            return bad[0]
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.2)
+
+
+def setup_dist(expect_world=None):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if expect_world is not None and world != expect_world:
+        raise SystemExit(f'bench.py --gpus {expect_world} but WORLD_SIZE={world}: run it '
+                         f'directly (it starts the ranks itself) or under torch.distributed.run '
+                         f'with --nproc-per-node {expect_world}')
     if torch.cuda.is_available():
         # one GPU per rank; modulo the visible count only so that a rehearsal of the
         # multi-rank logic can share one card (RG_BENCH_BACKEND=gloo)
@@ -149,6 +186,16 @@ def sum_over_ranks(x: float, world: int) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=_reduce_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def per_rank_counts(x: int, world: int):
+    """Every rank's count (rank order), e.g. the frames each rank processed."""
+    if world == 1:
+        return [int(x)]
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_reduce_device())
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [int(v.item()) for v in out]
 
 
 def rank_frame_seeds(rank: int, frames: int, seed0: int):
@@ -456,6 +503,7 @@ def train_main(args, world, rank, local):
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     frames_total = sum_over_ranks(args.frames * args.steps, world)
+    rank_frames = per_rank_counts(args.frames * args.steps, world)
     durs = event_durations(events)
     # roofline of the forward tape (the step's largest phase: the f32 row-MLP chain kernel
     # writing every layer's pre-norm / activation rows): the model's forward flops in the
@@ -491,7 +539,9 @@ def train_main(args, world, rank, local):
                                'forward tape + Loss_Graph + backward + all-reduce + SGD',
                    'frames_per_gpu': args.frames, 'nodes_per_frame': args.nodes, 'k': args.k,
                    'layers': args.layers, 'edges_per_gpu': E,
-                   'parallelism': f'data-parallel x{world} (one flat-gradient all-reduce per step)'},
+                   'parallelism': f'data-parallel x{world} (one flat-gradient all-reduce per step)',
+                   'frames_per_rank_timed': rank_frames,
+                   'backend': dist.get_backend() if world > 1 else None},
         'last_losses': [round(float(x), 5) for x in losses.cpu()],
         'roofline': roof,
     }
@@ -755,6 +805,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
               if scatter else None)
 
     frames_total = sum_over_ranks(args.frames * args.steps, world)
+    rank_frames = per_rank_counts(args.frames * args.steps, world)
     N = args.frames * args.nodes
     s = 2 if args.dtype in ('bf16', 'fp16') else 4
     C = 64
@@ -876,12 +927,14 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     return {'value': frames_total / elapsed, 'elapsed': elapsed, 'ms_step': elapsed / args.steps * 1e3,
             'forward_fps': frames_total / fwd_elapsed, 'forward_ms': fwd_ms, 'E': E,
             'forward_tflops': F / (fwd_ms * 1e-3) / 1e12, 'roof': roof, 'kern': kern,
-            'scatter': sc}
+            'scatter': sc, 'rank_frames': rank_frames}
 
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
+    world, rank, local = setup_dist(args.gpus)
     if not torch.cuda.is_available():
         raise SystemExit('bench.py needs a HIP device')
     if args.config == 'c4':
@@ -911,7 +964,9 @@ def main():
                    'graph': args.graph, 'k': args.k if args.graph == 'knn' else None,
                    'eps2': args.eps2, 'layers': args.layers, 'edges_per_gpu': r['E'],
                    'edges_per_frame': round(r['E'] / args.frames, 1),
-                   'parallelism': f'frame-parallel x{world} (no collective in the step)'},
+                   'parallelism': f'frame-parallel x{world} (no collective in the step)',
+                   'frames_per_rank_timed': r['rank_frames'],
+                   'backend': dist.get_backend() if world > 1 else None},
         'forward_only_frames_per_s': round(r['forward_fps'], 2),
         'forward_algorithmic_tflops': round(r['forward_tflops'], 2),
         'roofline': r['roof'],

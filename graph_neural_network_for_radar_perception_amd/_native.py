@@ -78,8 +78,9 @@ _SIGNATURES = {
     'rg_edge_features': (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
     'rg_node_features_f64': (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _P, _P]),
     'rg_edge_features_f64': (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _P, _P]),
-    'rg_pairs_from_dense_adjacency_workspace_size': (_S, [_I]),
-    'rg_pairs_from_dense_adjacency': (_I, [_P, _I, _P, _P, _P, _P, _S, _P]),
+    'rg_dense_pair_rows_workspace_size': (_S, [_I]),
+    'rg_dense_pair_rows': (_I, [_P, _I, _P, _P, _P, _S, _P]),
+    'rg_dense_pair_emit': (_I, [_P, _I, _P, _P, _P, _P]),
     'rg_pair_add_rows_f32': (_I, [_P, _I, _I, _P, _P, _L, _P, _I, _P]),
     'rg_pack_kinematics': (_I, [_P, _P, _P, _P, _I, _P, _P]),
     'rg_edge_features_packed': (_I, [_P, _P, _P, _P, _P, _L, _P, _P]),

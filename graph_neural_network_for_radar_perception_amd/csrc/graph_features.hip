@@ -583,24 +583,42 @@ extern "C" size_t rg_pairs_from_edge_index_workspace_size(long n_edges) {
   return 2 * align256((size_t)(n_edges + 1) * sizeof(int)) + align256(scan_workspace_bytes(n_edges));
 }
 
-// edge_formation's pairs from a dense adjacency (gnn_blocks.py:295-296): the row-major
-// flags of triu(adj, 1) -> exclusive scan -> scatter == torch.nonzero(..., as_tuple=True)
-__global__ void dense_pair_flags(const uint8_t* __restrict__ adj, int n, long nn,
-                                 int* __restrict__ flag) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nn) return;
-  const int i = (int)(t / n), j = (int)(t - (long)i * n);
-  flag[t] = (j > i && adj[t] != 0) ? 1 : 0;
+// edge_formation's pairs from a dense adjacency (gnn_blocks.py:295-296: torch.nonzero(
+// torch.triu(adj, 1)), row-major) in two passes over the rows, one wave per row: count
+// the set entries right of the diagonal, exclusive scan of the row counts (the caller sizes
+// the pair arrays from the total), then emit each row's pairs in column order (ballot +
+// popcount prefix per 64-column chunk).  Workspace O(n), not O(n^2).
+__global__ __launch_bounds__(256) void dense_pair_row_count(const uint8_t* __restrict__ adj,
+                                                             int n, int* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int i = (int)(((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= n) return;  // wave-uniform
+  const uint8_t* row = adj + (size_t)i * n;
+  int c = 0;
+  for (int j = i + 1 + lane; j < n; j += 64) c += row[j] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) cnt[i] = c;
 }
-__global__ void dense_pair_scatter(const uint8_t* __restrict__ adj, int n, long nn,
-                                   const int* __restrict__ pos, int* __restrict__ ps,
-                                   int* __restrict__ pd) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nn) return;
-  const int i = (int)(t / n), j = (int)(t - (long)i * n);
-  if (j > i && adj[t] != 0) {
-    ps[pos[t]] = i;
-    pd[pos[t]] = j;
+__global__ __launch_bounds__(256) void dense_pair_row_emit(const uint8_t* __restrict__ adj, int n,
+                                                            const int* __restrict__ row_ptr,
+                                                            int* __restrict__ ps,
+                                                            int* __restrict__ pd) {
+  const int lane = threadIdx.x & 63;
+  const int i = (int)(((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= n) return;  // wave-uniform
+  const uint8_t* row = adj + (size_t)i * n;
+  int pos = row_ptr[i];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int j0 = i + 1; j0 < n; j0 += 64) {
+    const int j = j0 + lane;
+    const bool set = j < n && row[j] != 0;
+    const unsigned long long m = __ballot(set);
+    if (set) {
+      const int p = pos + __popcll(m & below);
+      ps[p] = i;
+      pd[p] = j;
+    }
+    pos += __popcll(m);
   }
 }
 // out[r] = x[idx0[r]] + x[idx1[r]] (float32, one rounding: the reference's x[i] + x[j])
@@ -614,35 +632,40 @@ __global__ void pair_add_rows_kernel(const float* __restrict__ x, int ldx, int w
   out[r * ldo + c] = x[(size_t)i0[r] * ldx + c] + x[(size_t)i1[r] * ldx + c];
 }
 
-extern "C" size_t rg_pairs_from_dense_adjacency_workspace_size(int n_nodes) {
-  const long nn = (long)n_nodes * n_nodes;
-  return 2 * align256((size_t)(nn + 1) * sizeof(int)) + scan_workspace_bytes(nn);
+extern "C" size_t rg_dense_pair_rows_workspace_size(int n_nodes) {
+  return align256((size_t)(n_nodes + 1) * sizeof(int)) + scan_workspace_bytes(n_nodes);
 }
 
-extern "C" int rg_pairs_from_dense_adjacency(const void* adj, int n_nodes, int* pair_src,
-                                             int* pair_dst, int* n_pairs, void* workspace,
-                                             size_t workspace_bytes, void* stream) {
+extern "C" int rg_dense_pair_rows(const void* adj, int n_nodes, int* row_ptr, int* n_pairs,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   RG_REQUIRE(n_nodes >= 0 && n_nodes <= 46340, RG_ERR_ARG,
-             "rg_pairs_from_dense_adjacency: n_nodes=%d outside 0..46340", n_nodes);
-  RG_REQUIRE(workspace_bytes >= rg_pairs_from_dense_adjacency_workspace_size(n_nodes), RG_ERR_ARG,
-             "rg_pairs_from_dense_adjacency: workspace too small");
-  const long nn = (long)n_nodes * n_nodes;
-  if (nn == 0) {
+             "rg_dense_pair_rows: n_nodes=%d outside 0..46340", n_nodes);
+  RG_REQUIRE(adj || n_nodes == 0, RG_ERR_ARG, "rg_dense_pair_rows: null adjacency");
+  RG_REQUIRE(workspace_bytes >= rg_dense_pair_rows_workspace_size(n_nodes), RG_ERR_ARG,
+             "rg_dense_pair_rows: workspace too small");
+  if (n_nodes == 0) {
+    RG_CHECK_HIP(hipMemsetAsync(row_ptr, 0, sizeof(int), st));
     RG_CHECK_HIP(hipMemsetAsync(n_pairs, 0, sizeof(int), st));
     return RG_OK;
   }
   char* w = (char*)workspace;
-  int* flag = (int*)w;
-  w += align256((size_t)(nn + 1) * sizeof(int));
-  int* pos = (int*)w;
-  w += align256((size_t)(nn + 1) * sizeof(int));
-  dense_pair_flags<<<ceil_div(nn, 256), 256, 0, st>>>((const uint8_t*)adj, n_nodes, nn, flag);
+  int* cnt = (int*)w;
+  w += align256((size_t)(n_nodes + 1) * sizeof(int));
+  dense_pair_row_count<<<ceil_div((long)n_nodes * 64, 256), 256, 0, st>>>((const uint8_t*)adj,
+                                                                           n_nodes, cnt);
   RG_LAUNCH_CHECK();
-  int rc = exclusive_scan(flag, nn, pos, n_pairs, w, st);
-  if (rc) return rc;
-  dense_pair_scatter<<<ceil_div(nn, 256), 256, 0, st>>>((const uint8_t*)adj, n_nodes, nn, pos,
-                                                        pair_src, pair_dst);
+  return exclusive_scan(cnt, n_nodes, row_ptr, n_pairs, w, st);
+}
+
+extern "C" int rg_dense_pair_emit(const void* adj, int n_nodes, const int* row_ptr, int* pair_src,
+                                  int* pair_dst, void* stream) {
+  RG_REQUIRE(n_nodes >= 0 && n_nodes <= 46340, RG_ERR_ARG,
+             "rg_dense_pair_emit: n_nodes=%d outside 0..46340", n_nodes);
+  if (n_nodes == 0) return RG_OK;
+  RG_REQUIRE(adj && row_ptr && pair_src && pair_dst, RG_ERR_ARG, "rg_dense_pair_emit: null argument");
+  dense_pair_row_emit<<<ceil_div((long)n_nodes * 64, 256), 256, 0, (hipStream_t)stream>>>(
+      (const uint8_t*)adj, n_nodes, row_ptr, pair_src, pair_dst);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

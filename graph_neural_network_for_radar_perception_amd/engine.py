@@ -669,7 +669,13 @@ class ConvPlan:
         u = self.upd.specs[0]
         C = self.c_out
         W = m0.weight.detach().to(torch.float32)
-        if W.shape[1] != 3 * C:
+        # both fused f32 kernels are compiled for the yml block only (conv_x3.hip /
+        # conv_f32.hip: C = 64, msg_mlp_hidden_dim = 128, edge embedding 64, every layer
+        # channel-normalised + LeakyReLU); any other block runs the unfused chains
+        if not (C == 64 and W.shape == (128, 3 * C) and m1.weight.shape == (C, 128)
+                and u.weight.shape == (C, 2 * C)):
+            return
+        if any(sp.mu is None or sp.act != 'leakyrelu' for sp in (m0, m1, u)):
             return
         b = (m0.bias.detach().to(torch.float32) if m0.bias is not None
              else torch.zeros(W.shape[0], dtype=torch.float32, device=W.device))
@@ -774,11 +780,16 @@ class ConvPlan:
         return (self.use_fused and self.x3 and self.fused_ok is not False
                 and x.dtype == torch.float32 and e.dtype == torch.float32)
 
-    def project_x3(self, x, pq):
-        """P | Q of the first x3 layer (rg_conv_proj_x3)."""
-        nat.check(nat.lib().rg_conv_proj_x3(self.x3_pq_in, x.data_ptr(), x.stride(0), x.shape[0],
-                                            pq.data_ptr(), nat.stream_ptr(x.device)),
-                  'rg_conv_proj_x3')
+    def project_x3(self, x, pq) -> bool:
+        """P | Q of the first x3 layer (rg_conv_proj_x3); False when the kernel does not
+        take this layer (the caller then runs the layer unfused)."""
+        rc = nat.lib().rg_conv_proj_x3(self.x3_pq_in, x.data_ptr(), x.stride(0), x.shape[0],
+                                       pq.data_ptr(), nat.stream_ptr(x.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            self.fused_ok = False
+            return False
+        nat.check(rc, 'rg_conv_proj_x3')
+        return True
 
     def run_x3(self, x, e, g, x_out, pq, nxt=None, pq_out=None) -> bool:
         """One rg_conv_layer_x3 launch; with nxt (the next ConvPlan, also x3) it also writes
@@ -816,7 +827,8 @@ class ConvPlan:
             n = x.shape[0]
             if self.x3_pq is None or self.x3_pq.shape[0] < n:
                 self.x3_pq = torch.empty((max(n, 1), 256), dtype=torch.float32, device=self.device)
-            self.project_x3(x, self.x3_pq)
+            if not self.project_x3(x, self.x3_pq):
+                return False
             return self.run_x3(x, e, g, x_out, self.x3_pq)
         if self.dtype == 'fp32':
             if x.dtype != torch.float32 or e.dtype != torch.float32:
@@ -989,8 +1001,10 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             if pq is None:
                 pq = alloc('pq0', (N, 256), torch.float32)
                 mark('conv_proj:start')
-                cv.project_x3(x, pq)
+                if not cv.project_x3(x, pq):
+                    pq = None
                 mark('conv_proj:end')
+        if cv.x3_ready(x, e):
             nxt = plans.convs[li + 1] if li + 1 < len(plans.convs) else None
             if nxt is not None and not nxt.x3_ready(xn, e):
                 nxt = None
@@ -1117,7 +1131,8 @@ def run_blocks(mods, x: torch.Tensor, dtype: str = 'fp32') -> torch.Tensor:
 def pairs_from_dense_adjacency(adj_matrix: torch.Tensor):
     """edge_formation's pairs (gnn_blocks.py:295-296: nonzero(triu(adj, 1)), row-major)
     from a dense [N, N] adjacency on the device -> (pair_src int32, pair_dst int32, U).
-    One host synchronisation (U), where the reference's torch.nonzero synchronises too."""
+    One host synchronisation (U, which sizes the pair arrays), where the reference's
+    torch.nonzero synchronises too; scratch is O(N) beside the N x N bool input."""
     _require_device(adj_matrix, 'adj_matrix')
     lib = nat.lib()
     dev = adj_matrix.device
@@ -1127,17 +1142,17 @@ def pairs_from_dense_adjacency(adj_matrix: torch.Tensor):
     adj = adj_matrix.contiguous()
     if adj.dtype not in (torch.bool, torch.uint8):
         adj = (adj != 0).contiguous()
-    ws = torch.empty(lib.rg_pairs_from_dense_adjacency_workspace_size(n), dtype=torch.uint8,
-                     device=dev)
-    cap = max(n * (n - 1) // 2, 1)
-    ps = torch.empty(cap, dtype=torch.int32, device=dev)
-    pd = torch.empty(cap, dtype=torch.int32, device=dev)
+    st = nat.stream_ptr(dev)
+    ws = torch.empty(lib.rg_dense_pair_rows_workspace_size(n), dtype=torch.uint8, device=dev)
+    row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
     cnt = torch.empty(1, dtype=torch.int32, device=dev)
-    nat.check(lib.rg_pairs_from_dense_adjacency(adj.data_ptr(), n, ps.data_ptr(), pd.data_ptr(),
-                                                cnt.data_ptr(), ws.data_ptr(), ws.numel(),
-                                                nat.stream_ptr(dev)),
-              'rg_pairs_from_dense_adjacency')
+    nat.check(lib.rg_dense_pair_rows(adj.data_ptr(), n, row_ptr.data_ptr(), cnt.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), st), 'rg_dense_pair_rows')
     U = int(cnt.item())
+    ps = torch.empty(max(U, 1), dtype=torch.int32, device=dev)
+    pd = torch.empty(max(U, 1), dtype=torch.int32, device=dev)
+    nat.check(lib.rg_dense_pair_emit(adj.data_ptr(), n, row_ptr.data_ptr(), ps.data_ptr(),
+                                     pd.data_ptr(), st), 'rg_dense_pair_emit')
     return ps[:max(U, 1)], pd[:max(U, 1)], U
 
 

@@ -59,6 +59,43 @@ def _batch_frames(node_features: List[torch.Tensor], edge_features: List[torch.T
     return nf, ef, ei, cptr, cidx.contiguous(), len(lens), sizes
 
 
+class _Recompute:
+    """What the backward of a grad-enabled inference call needs: the model and the
+    batched inputs (node rows, destination-major edge rows, graph, object clusters)."""
+
+    def __init__(self, model, batch):
+        self.model = model
+        self.batch = batch
+
+
+class _DetectorOutputs(torch.autograd.Function):
+    """The four outputs of a Model_Inference call made with autograd enabled, as an
+    autograd node over every parameter.
+
+    The forward values are the inference kernels' (compute_dtype).  backward() re-runs the
+    forward in float32 with the training tape (training.TrainEngine.forward_tape: the same
+    kernels Model_Training trains with) and back-propagates the incoming output gradients
+    through it (TrainEngine.backward_outputs), i.e. recomputation instead of keeping a tape
+    alive for callers that never call backward (the reference's evaluation loops)."""
+
+    @staticmethod
+    def forward(ctx, rec, node_cls, node_reg, link_cls, obj_cls, *params):
+        ctx.rec = rec
+        ctx.n_params = len(params)
+        return node_cls.clone(), node_reg.clone(), link_cls.clone(), obj_cls.clone()
+
+    @staticmethod
+    def backward(ctx, *grads):
+        rec = ctx.rec
+        eng = rec.model.train_engine()
+        outs, T = eng.forward_tape(*rec.batch)
+        eng.backward_outputs(T, *eng.output_grad_buffers(T, grads))
+        ctx.rec = None
+        pgrads = tuple(eng.grads[id(p)].clone() for p in eng.params)
+        assert len(pgrads) == ctx.n_params
+        return (None, None, None, None, None) + pgrads
+
+
 class Model_Inference(nn.Module):
     """gnn_detector.py:31-201."""
 
@@ -118,6 +155,18 @@ class Model_Inference(nn.Module):
         """Re-pack every plan on next use (weights written outside torch, FusedSGD)."""
         for p in self._plans.values():
             p.invalidate()
+        if getattr(self, '_train_engine', None) is not None:
+            self._train_engine.invalidate()
+
+    def train_engine(self):
+        """The float32 tape + backward of this model (backward of grad-enabled calls)."""
+        from .training import TrainEngine
+        dev = next(self.parameters()).device
+        eng = getattr(self, '_train_engine', None)
+        if eng is None or eng.device != dev:
+            eng = TrainEngine(self, dev)
+            self._train_engine = eng
+        return eng
 
     def plans(self, dtype: Optional[str] = None) -> engine.ModelPlans:
         dtype = dtype or self.compute_dtype
@@ -140,11 +189,6 @@ class Model_Inference(nn.Module):
         ``cluster_node_idx=None`` the object head runs on the proposal clusters
         (gnn_detector.py:164-187; needs ``other_features`` and extract_proposals) and a
         fifth value, the per-frame cluster member lists, is returned."""
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                'Model_Inference.forward has no autograd graph: train through '
-                'Model_Training.forward (native forward tape + backward, training.py), or run '
-                'inference under torch.no_grad()')
         engine._require_device(node_features[0], 'node_features')
         proposals = cluster_node_idx is None
         if proposals:
@@ -178,6 +222,15 @@ class Model_Inference(nn.Module):
         out = engine.forward_batched(self.plans(), nf, e_dst, g, cptr, cidx, ncl,
                                      n_pairs_cap=g.n_pairs, clusters_fn=clusters_fn)
         res = (out.node_cls, out.node_reg, out.link_cls[:g.n_pairs], out.obj_cls)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # the reference's evaluation callers run the detector with autograd on
+            # (set_param_for_inference_gnn.py:36 returns detector_train.pred.eval(); no
+            # no_grad in output.py:88-94, segmentation_accuracy.py:66-72,
+            # detection_accuracy.py:85): attach a native backward to the outputs
+            if proposals:
+                cptr, cidx, ncl = out.cluster_ptr, out.cluster_idx, out.obj_cls.shape[0]
+            res = _DetectorOutputs.apply(_Recompute(self, (nf, e_dst, g, cptr, cidx, ncl)),
+                                         *res, *self.parameters())
         if not proposals:
             return res
         # per-frame member lists with frame-local indices, int64 (gnn_detector.py:180-184):
@@ -278,11 +331,17 @@ class Model_Training(nn.Module):
                         on_update=self.invalidate_plans)
 
     def _labels(self, labels, dev):
-        return {'node_class': torch.cat(labels['node_class'], 0).to(dev, torch.int64).contiguous(),
-                'node_offsets': torch.cat(labels['node_offsets'], 0).to(dev, torch.float32).contiguous(),
-                'edge_class': torch.cat(labels['edge_class'], 0).to(dev, torch.int64).contiguous(),
-                'cluster_labels': torch.cat(labels['cluster_labels'], 0).to(dev, torch.int64).contiguous(),
-                'class_weights': self.class_weights.to(dev).contiguous()}
+        from .loss import check_class_labels
+        lab = {'node_class': torch.cat(labels['node_class'], 0).to(dev, torch.int64).contiguous(),
+               'node_offsets': torch.cat(labels['node_offsets'], 0).to(dev, torch.float32).contiguous(),
+               'edge_class': torch.cat(labels['edge_class'], 0).to(dev, torch.int64).contiguous(),
+               'cluster_labels': torch.cat(labels['cluster_labels'], 0).to(dev, torch.int64).contiguous(),
+               'class_weights': self.class_weights.to(dev).contiguous()}
+        c = self.net_config
+        check_class_labels([(lab['node_class'], c.num_classes),
+                            (lab['edge_class'], c.num_edge_classes),
+                            (lab['cluster_labels'], c.num_classes)])
+        return lab
 
     def forward(self, node_features: List[torch.Tensor], edge_features: List[torch.Tensor],
                 edge_index: List[torch.Tensor], adj_matrix: List[torch.Tensor],

@@ -224,13 +224,17 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
     pend_key = ('radius_need', mode, float(eps2))
     cap0 = ws_cache.get(cap_key) if (ws_cache is not None and mode != nat.GRAPH_KNN) else None
     if cap0 is not None:
-        pend = ws_cache.get(pend_key)
-        if pend is not None and pend[1].query():  # the previous build's count has landed
-            need = int(pend[0][0])
+        # every earlier build's count that has landed grows the capacity (the largest
+        # one); counts still in flight stay queued, so a host running ahead of the GPU
+        # loses none of them
+        pend = ws_cache.get(pend_key, [])
+        landed = [h for h, ev in pend if ev.query()]
+        if landed:
+            need = max(int(h[0]) for h in landed)
             if need > cap0:
                 cap0 = need + need // 4
                 ws_cache[cap_key] = cap0
-            ws_cache.pop(pend_key)
+            ws_cache[pend_key] = [(h, ev) for h, ev in pend if not any(h is x for x in landed)]
     row_ptr, col, deg, ne, cap = engine.build_graph(batch.arrays['meas_px'],
                                                     batch.arrays['meas_py'], batch.frame_ptr,
                                                     batch.frame_sizes, k, eps2, mode,
@@ -253,7 +257,7 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
         host.copy_(need_dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(row_ptr.device))
-        ws_cache[pend_key] = (host, ev)
+        ws_cache.setdefault(pend_key, []).append((host, ev))
     g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
     g.set_frames(batch.frame_ptr, batch.n_frames)
     nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)

@@ -57,6 +57,23 @@ class _LossGraphFn(torch.autograd.Function):
         return (None, None) + tuple(d)
 
 
+def check_class_labels(pairs):
+    """The range check torch.nn.functional.one_hot does on the reference's targets
+    (loss.py:59-73): pairs = [(int64 labels on the device, number of classes), ...].  The
+    native loss indexes its logits rows with the labels, so an out-of-range label must not
+    reach it.  One host synchronisation for all of them (one_hot synchronises too)."""
+    live = [(t, n) for t, n in pairs if t.numel()]
+    if not live:
+        return
+    ext = torch.stack([v for t, _ in live for v in (t.min(), t.max())]).cpu().tolist()
+    for i, (_, n) in enumerate(live):
+        lo, hi = ext[2 * i], ext[2 * i + 1]
+        if lo < 0:
+            raise RuntimeError('Class values must be non-negative.')
+        if hi >= n:
+            raise RuntimeError('Class values must be smaller than num_classes.')
+
+
 class Loss_Graph(nn.Module):
     """loss.py:9-76: focal edge loss, class-weighted node CE (sum / N), 0.5 MSE on the
     normalised offsets, object CE, each times its yml weight."""
@@ -80,6 +97,9 @@ class Loss_Graph(nn.Module):
                   'edge_class': gt.edge_class_logits.to(dev, torch.int64).contiguous(),
                   'cluster_labels': gt.obj_class_logits.to(dev, torch.int64).contiguous(),
                   'class_weights': self.class_weights.to(dev).contiguous()}
+        check_class_labels([(labels['node_class'], pred.node_class_logits.shape[1]),
+                            (labels['edge_class'], pred.edge_class_logits.shape[1]),
+                            (labels['cluster_labels'], pred.obj_class_logits.shape[1])])
         losses = _LossGraphFn.apply(self.net_config, labels, pred.node_class_logits,
                                     pred.node_reg_deltas, pred.edge_class_logits,
                                     pred.obj_class_logits)
@@ -138,8 +158,5 @@ class Loss_Object_Class(nn.Module):
     def forward(self, pred_obj_class_logits, gt_obj_class_logits):
         if not pred_obj_class_logits.is_cuda:
             raise RuntimeError('Loss_Object_Class: the native loss runs on a HIP device')
-        if int(gt_obj_class_logits.numel()) and (int(gt_obj_class_logits.max()) >= self.num_classes
-                                                 or int(gt_obj_class_logits.min()) < 0):
-            # torch.nn.functional.one_hot raises on out-of-range classes
-            raise RuntimeError('Class values must be smaller than num_classes.')
+        check_class_labels([(gt_obj_class_logits.to(torch.int64), self.num_classes)])
         return cross_entropy_with_accuracy(pred_obj_class_logits, gt_obj_class_logits)[0]

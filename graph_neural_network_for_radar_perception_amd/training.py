@@ -255,11 +255,13 @@ class TrainConv:
 
 
 class TrainEngine:
-    """Forward-with-tape and backward of a whole Model_Inference (``pred``)."""
+    """Forward-with-tape and backward of a whole Model_Inference: ``model`` is a
+    Model_Training / finetuning wrapper (its ``pred``) or a Model_Inference itself (the
+    grad-enabled inference callers, gnn_detector._DetectorOutputs)."""
 
     def __init__(self, model_training, device):
         self.model = model_training
-        pred = model_training.pred
+        pred = getattr(model_training, 'pred', model_training)
         self.device = torch.device(device)
         self.ws = Workspaces(self.device)
         mk = lambda mods: TrainChain(mods, self.device, self.ws)  # noqa: E731
@@ -289,8 +291,22 @@ class TrainEngine:
         node_offsets f32 [N,2] (raw), edge_class int64 [U] (pair order), cluster_labels
         int64 [Ncl].  Returns (losses f32 [4], accuracies f32 [3], tape)."""
         lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        outs, T = self.forward_tape(nf, e_dst, g, cptr, cidx, ncl)
+        N, U = g.n_nodes, g.n_pairs
+        losses = torch.empty(4, dtype=torch.float32, device=self.device)
+        acc = torch.empty(3, dtype=torch.float32, device=self.device)
+        args = self._loss_args(outs, labels, N, U, ncl)
+        ws = self.ws.get('loss', lib.rg_loss_workspace_size(N, U, ncl))
+        nat.check(lib.rg_loss_graph(ctypes.byref(args), losses.data_ptr(), acc.data_ptr(),
+                                    ws.data_ptr(), ws.numel(), st), 'rg_loss_graph')
+        T.update(labels=labels, args=args)
+        return losses, acc, T
+
+    def forward_tape(self, nf, e_dst, g: engine.DeviceGraph, cptr, cidx, ncl: int):
+        """Model_Inference.forward (gnn_detector.py:141-201) in float32 with the tape.
+        Returns ((node_cls, node_reg, link_cls [U], obj_cls [Ncl]), tape)."""
         dev = self.device
-        st = nat.stream_ptr(dev)
         f32 = dict(dtype=torch.float32, device=dev)
         N, E, U = g.n_nodes, g.n_edges, g.n_pairs
         T = {}
@@ -346,15 +362,8 @@ class TrainEngine:
         obj = torch.empty((max(ncl, 1), self.cls_head.out_dim), **f32)
         T['cls_head'] = self.cls_head.forward(ncl, obj, pooled, pooled.shape[1])
         outs = (node_cls, node_reg, link[:U], obj[:ncl])
-        losses = torch.empty(4, **f32)
-        acc = torch.empty(3, **f32)
-        args = self._loss_args(outs, labels, N, U, ncl)
-        ws = self.ws.get('loss', lib.rg_loss_workspace_size(N, U, ncl))
-        nat.check(lib.rg_loss_graph(ctypes.byref(args), losses.data_ptr(), acc.data_ptr(),
-                                    ws.data_ptr(), ws.numel(), st), 'rg_loss_graph')
-        T.update(g=g, cptr=cptr, cidx=cidx, ncl=ncl, outs=outs, labels=labels, args=args,
-                 N=N, E=E, U=U)
-        return losses, acc, T
+        T.update(g=g, cptr=cptr, cidx=cidx, ncl=ncl, outs=outs, N=N, E=E, U=U)
+        return outs, T
 
     def _loss_args(self, outs, labels, N, U, ncl):
         cfg = self.model.net_config
@@ -379,13 +388,8 @@ class TrainEngine:
     def backward(self, T: dict, g_losses: torch.Tensor, zero_grads: bool = True):
         """Gradients of sum_i g_losses[i] * losses[i] into self.flat_grad."""
         lib = nat.lib()
-        dev = self.device
-        st = nat.stream_ptr(dev)
-        f32 = dict(dtype=torch.float32, device=dev)
-        if zero_grads:
-            self.flat_grad.zero_()
-        G = self.grads
-        g, N, E, U, ncl = T['g'], T['N'], T['E'], T['U'], T['ncl']
+        f32 = dict(dtype=torch.float32, device=self.device)
+        U, ncl = T['U'], T['ncl']
         node_cls, node_reg, link, obj = T['outs']
         d_nc = torch.empty_like(node_cls)
         d_nr = torch.empty_like(node_reg)
@@ -394,7 +398,34 @@ class TrainEngine:
         gl = g_losses.detach().to(torch.float32).contiguous()
         nat.check(lib.rg_loss_graph_backward(ctypes.byref(T['args']), gl.data_ptr(),
                                              d_nc.data_ptr(), d_nr.data_ptr(), d_l.data_ptr(),
-                                             d_o.data_ptr(), st), 'rg_loss_graph_backward')
+                                             d_o.data_ptr(), nat.stream_ptr(self.device)),
+                  'rg_loss_graph_backward')
+        self.backward_outputs(T, d_nc, d_nr, d_l, d_o, zero_grads)
+
+    def output_grad_buffers(self, T: dict, grads):
+        """Gradients of the four outputs (None = zero) as the dense f32 buffers
+        backward_outputs consumes (link / object rows padded to >= 1 row)."""
+        f32 = dict(dtype=torch.float32, device=self.device)
+        rows = (T['N'], T['N'], max(T['U'], 1), max(T['ncl'], 1))
+        out = []
+        for gr, o, r in zip(grads, T['outs'], rows):
+            buf = torch.zeros((r, o.shape[1]), **f32)
+            if gr is not None and o.shape[0] > 0:
+                buf[:o.shape[0]].copy_(gr)
+            out.append(buf)
+        return out
+
+    def backward_outputs(self, T: dict, d_nc, d_nr, d_l, d_o, zero_grads: bool = True):
+        """Gradients of sum(d_nc * node_cls) + sum(d_nr * node_reg) + sum(d_l * link_cls) +
+        sum(d_o * obj_cls) into self.flat_grad (the d_* buffers are consumed)."""
+        lib = nat.lib()
+        dev = self.device
+        st = nat.stream_ptr(dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        if zero_grads:
+            self.flat_grad.zero_()
+        G = self.grads
+        g, N, E, U, ncl = T['g'], T['N'], T['E'], T['U'], T['ncl']
         x = T['xs'][-1]
         C = x.shape[1]
         dx = torch.zeros((N, C), **f32)

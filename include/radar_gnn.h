@@ -165,12 +165,18 @@ int rg_edge_features_packed(const void* kin, const int64_t* timestamp, const int
                             void* stream);
 
 /* edge_formation's pairs from a DENSE adjacency (gnn_blocks.py:295-296: torch.nonzero(
- * torch.triu(adj, 1), as_tuple=True), row-major): adj = uint8 / bool [n][n] (n <= 46340);
- * pair_src / pair_dst int32[capacity >= number of pairs]; n_pairs int32[1] (device). */
-size_t rg_pairs_from_dense_adjacency_workspace_size(int n_nodes);
-int rg_pairs_from_dense_adjacency(const void* adj, int n_nodes, int* pair_src, int* pair_dst,
-                                  int* n_pairs, void* workspace, size_t workspace_bytes,
-                                  void* stream);
+ * torch.triu(adj, 1), as_tuple=True), row-major), in two calls so the caller sizes the
+ * pair arrays from the count (the one host synchronisation, where torch.nonzero syncs too):
+ *   rg_dense_pair_rows: adj = uint8 / bool [n][n] (n <= 46340) -> row_ptr int32[n + 1]
+ *     (exclusive scan of each row's entries right of the diagonal), n_pairs int32[1];
+ *     workspace O(n);
+ *   rg_dense_pair_emit: pair_src / pair_dst int32[n_pairs], rows in order, columns
+ *     ascending. */
+size_t rg_dense_pair_rows_workspace_size(int n_nodes);
+int rg_dense_pair_rows(const void* adj, int n_nodes, int* row_ptr, int* n_pairs, void* workspace,
+                       size_t workspace_bytes, void* stream);
+int rg_dense_pair_emit(const void* adj, int n_nodes, const int* row_ptr, int* pair_src,
+                       int* pair_dst, void* stream);
 /* out[r][0..w) = x[idx0[r]] + x[idx1[r]] in float32 (edge_formation's x[i] + x[j],
  * gnn_blocks.py:297) */
 int rg_pair_add_rows_f32(const float* x, int ldx, int w, const int* idx0, const int* idx1,

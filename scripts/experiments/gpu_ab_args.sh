@@ -1,7 +1,7 @@
 #!/bin/bash
 # same-box A/B of two bench argument sets, interleaved: A_ARGS vs B_ARGS (and environment
 # assignments A_ENV / B_ENV), ROUNDS times
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/ab
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in A B; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # c4 (training step): sweep the weight-gradient kernel's grid (RG_GRAD_WG_PER_CU /
 # RG_GRAD_MIN_BLOCKS), interleaved
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/c4g
 for r in 1 2; do
   for v in ""; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # C5: sweep the 16-bit conv's block edge cap (RG_CONV_CAP_MIN / RG_CONV_CAP_DIV), interleaved
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/cap
 for r in 1 2; do
   for v in "" "RG_CONV_CAP_MIN=64" "RG_CONV_CAP_MIN=64 RG_CONV_CAP_DIV=8192" "RG_CONV_CAP_MIN=32 RG_CONV_CAP_DIV=16384" "RG_CONV_CAP_DIV=2048" "RG_CONV_CAP_MIN=256"; do

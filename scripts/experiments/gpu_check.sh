@@ -2,7 +2,7 @@
 # GPU validation pass used with gpurun: smoke -> gpu tests -> short bench.
 # Stops at the first crash-like exit (fault/abort/timeout); test failures
 # (pytest exit 1) still let the bench run.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log

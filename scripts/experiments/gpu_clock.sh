@@ -1,6 +1,6 @@
 #!/bin/bash
 # effective shader clock per kernel: GRBM_GUI_ACTIVE cycles / kernel-trace duration
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 OUT=gpurun_out/clock
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # effective clock per kernel: GRBM_GUI_ACTIVE (summed over 8 XCDs) / 8 / duration, with a
 # kernel-trace pass for the durations (separate runs)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 OUT=${OUT:-gpurun_out/clk}
 mkdir -p $OUT
 export TMPDIR=/tmp

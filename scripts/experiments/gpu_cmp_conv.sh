@@ -1,6 +1,6 @@
 #!/bin/bash
 # f32 conv variants: parity tests, then the M bench with each variant
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_f32.py \
   tests/test_gpu_parity.py -k "f32 or fp32 or pipeline or training" > gpurun_out/pytest_c.log 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # full GPU suite, then the C5 / C2 / M bench lines and the 16-bit conv phase stamps
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/c16
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then

@@ -2,7 +2,7 @@
 # Round evidence in one GPU call: the default bench line (M + the C2 extra, CPU baseline),
 # a rocprofv3 kernel-trace/stats pass, FETCH/WRITE_SIZE passes and SQ counter passes of the
 # M bench (each its own run).  Outputs under gpurun_out/ev/.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
 timeout -k 10 600 python bench.py > gpurun_out/ev/bench.log 2> gpurun_out/ev/bench.err

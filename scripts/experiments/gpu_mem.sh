@@ -1,6 +1,6 @@
 #!/bin/bash
 # memory-path counters (L2 hit rate, TA busy, L1->L2 latency) of the bench kernels
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/mem
 export TMPDIR=/tmp
 i=0

@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic counters for the bench command: FETCH_SIZE and WRITE_SIZE in
 # separate passes (they do not fit one TCC pass on gfx950), kernel trace only.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # FETCH_SIZE / WRITE_SIZE passes (separate runs) of the bench for each config in CONFIGS;
 # outputs under gpurun_out/pmc_<config>/
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export TMPDIR=/tmp
 for cfg in ${CONFIGS:-c2 c5}; do
   mkdir -p gpurun_out/pmc_$cfg

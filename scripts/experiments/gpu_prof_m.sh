@@ -1,6 +1,6 @@
 #!/bin/bash
 # M-config profile: kernel trace + stats, then two SQ counter passes (separate runs)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/prof_m gpurun_out/sq_m
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_m -o run \

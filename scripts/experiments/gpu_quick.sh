@@ -1,6 +1,6 @@
 #!/bin/bash
 # quick loop: f32 GPU tests (x3 + mfma_f32) then the M bench kernel times
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/q
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_f32.py ${QTESTS} > gpurun_out/q/pytest.log 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-2 check: new f32 kernels' tests, the fp32 forward parity, bench M, bf16 C2 error stats
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_f32.py \

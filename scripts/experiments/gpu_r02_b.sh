@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-2 check b: smoke + new GPU tests (norms, blocks, f32) + graph / bf16 parity subsets
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

@@ -3,7 +3,7 @@
 # baseline), rocprofv3 kernel stats, HBM traffic counters, SQ counters, and the other
 # presets' bench lines.  Everything lands under gpurun_out/; copy what is judged into
 # profiles/ (scripts/collect_round.py).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 set -o pipefail
 mkdir -p gpurun_out/presets
 PYTEST_ARGS="--timeout 300 --timeout-method thread" bash scripts/gpu_check.sh || exit $?

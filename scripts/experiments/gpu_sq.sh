@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters (issue / stall breakdown) of the bench kernels, two passes.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/sq
 export TMPDIR=/tmp
 rocprofv3 -L > gpurun_out/sq/counters.txt 2>&1 || true

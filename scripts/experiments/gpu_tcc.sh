@@ -1,6 +1,6 @@
 #!/bin/bash
 # L2 (TCC) hit / miss and TCP/TA counters of the M bench, separate passes
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 OUT=${OUT:-gpurun_out/tcc}
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # run the given GPU test files (default: the whole -m gpu suite) in one process
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/t
 export TMPDIR=/tmp
 FILES="${@:-tests}"

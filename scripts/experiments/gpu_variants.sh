@@ -1,7 +1,7 @@
 #!/bin/bash
 # time library variants (lib/variants/libradargnn_<v>.so) on the M bench: VARIANTS="a b";
 # ROUNDS (default 2) interleaved passes over base + variants, to see clock drift
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/var
 for r in $(seq 1 ${ROUNDS:-2}); do
 for v in base ${VARIANTS}; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # x3 fp32 path check: f32 GPU tests + fp32 forward parity, then the M bench (no CPU
 # baseline) and a kernel-trace/stats pass of the same command
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out/x3
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_f32.py \

@@ -168,3 +168,72 @@ def test_frame_sharding_two_ranks_hip_pipeline(tmp_path, cuda_device):
                                   out.node_cls.cpu().numpy())
     np.testing.assert_array_equal(np.concatenate([x['node_reg'] for x in res]),
                                   out.node_reg.cpu().numpy())
+
+
+def _run_bench(args, timeout=240):
+    import json
+    import subprocess
+    env = dict(os.environ, RG_BENCH_BACKEND='gloo')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py')] + args, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout       # rank 0 alone prints the line
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_gpus2_launches_two_ranks(cuda_device):
+    """`python bench.py --gpus 2` (no launcher in the environment) starts two ranks itself:
+    the line reports n_gpus 2 and the value counts both ranks' frames (weak scaling; gloo
+    for the timing collectives so both ranks can share the test box's one card)."""
+    line = _run_bench(['--gpus', '2', '--steps', '2', '--warmup', '1', '--frames', '4',
+                       '--no-cpu-baseline', '--no-extra'])
+    assert line['n_gpus'] == 2
+    assert line['config']['frames_per_rank_timed'] == [8, 8]
+    assert line['config']['backend'] == 'gloo'
+    # value = frames of all ranks / max-over-ranks elapsed = 16 / (steps * ms_per_step)
+    assert abs(line['value'] - 16.0 / (2 * line['ms_per_step'] * 1e-3)) <= 0.01 * line['value']
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_c4_gpus2_allreduce_path(cuda_device):
+    """`bench.py --config c4 --gpus 2`: data-parallel training through the launcher path,
+    the flat-gradient all-reduce (training.allreduce_gradients) on every step."""
+    line = _run_bench(['--config', 'c4', '--gpus', '2', '--steps', '2', '--warmup', '1',
+                       '--frames', '2', '--nodes', '500', '--no-cpu-baseline'])
+    assert line['n_gpus'] == 2
+    assert line['config']['frames_per_rank_timed'] == [4, 4]
+    assert all(np.isfinite(line['last_losses']))
+
+
+def _world_check_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), RG_BENCH_BACKEND='gloo')
+    import bench
+    try:
+        bench.setup_dist(world + 1)
+        ok = False
+    except SystemExit:
+        ok = True
+    w, r, _ = bench.setup_dist(world)
+    counts = bench.per_rank_counts(10 * (rank + 1), w)
+    np.savez(os.path.join(out_dir, f'wc{rank}.npz'), ok=ok, counts=np.array(counts))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_setup_dist_checks_world_and_gathers_counts(tmp_path):
+    """--gpus N under a launcher that started a different number of ranks is refused; the
+    per-rank frame counts of the line are gathered in rank order."""
+    world = 2
+    mp.spawn(_world_check_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+             join=True)
+    for r in range(world):
+        d = np.load(tmp_path / f'wc{r}.npz')
+        assert bool(d['ok'])
+        np.testing.assert_array_equal(d['counts'], [10, 20])

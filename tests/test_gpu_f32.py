@@ -7,6 +7,8 @@ Tolerances: f32 kernels vs float64 evaluation of the same f32 weights / inputs
 |d| <= 1e-4 + 1e-4 |ref| (north_star's fp32 bound); fused vs unfused f32 conv layer
 |d| <= 2e-5 + 2e-5 |ref| (same arithmetic up to summation order inside the GEMMs).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -271,17 +273,19 @@ def test_f32_fused_conv_deterministic_and_isolated_nodes(cuda_device):
     torch.testing.assert_close(outs[0].cpu(), ref, **FP32_TOL)
 
 
+@pytest.mark.timeout(600)
 def test_m_config_full_batch_fp32_matches_oracle(cuda_device):
     """The metric configuration M at full size (64 frames x 3000 nodes, k = 10, L = 7,
-    trained weights, the bench's own pipeline): edge count, and spot frames' four outputs
-    against the oracle at 1e-4; the fused conv and the f32 fast chains are the ones used."""
+    trained weights, the bench's own pipeline): every frame's edge count and four outputs
+    against the oracle, with the worst error over all 64 frames reported as a fraction of
+    the 1e-4 bound and held to <= 0.5 of it; the fused conv and the f32 fast chains are the
+    ones used."""
     from graph_neural_network_for_radar_perception_amd import synthetic
     from graph_neural_network_for_radar_perception_amd.config import default_config
     from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
     from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
     from oracle import graph_features_ref as gref
-    import os
     dev = cuda_device
     cfg = default_config()
     d = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'model_trained_N50.npz'))
@@ -307,9 +311,15 @@ def test_m_config_full_batch_fp32_matches_oracle(cuda_device):
     U = int(gb.graph.n_pairs_dev.item())
     link = out.link_cls[:U].cpu().numpy()
     pair_src = gb.graph.pair_src[:U].cpu().numpy()
+    got = {'node_cls': out.node_cls.cpu().numpy(), 'node_reg': out.node_reg.cpu().numpy(),
+           'obj_cls': out.obj_cls.cpu().numpy()}
     gmax = float(np.sqrt(np.float64(100 ** 2 + 50 ** 2)))
     sdc = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
-    for f in (0, 37, 63):
+    keys = ('node_cls', 'node_reg', 'link_cls', 'obj_cls')
+    # worst |d| / (atol + rtol |ref|) per output over ALL 64 frames (1.0 = the 1e-4 bound)
+    worst = {k: 0.0 for k in keys}
+    maxabs = {k: 0.0 for k in keys}
+    for f in range(B):
         g = gref.build_frame_graph(frames[f], 25.0, 10, gmax)
         assert rp[fptr[f + 1]] - rp[fptr[f]] == g['edge_index'].shape[1]
         with torch.no_grad():
@@ -318,13 +328,59 @@ def test_m_config_full_batch_fp32_matches_oracle(cuda_device):
                                           torch.from_numpy(g['edge_index']), None,
                                           [torch.from_numpy(c) for c in clusters[f]])
         sl = slice(f * N, (f + 1) * N)
-        np.testing.assert_allclose(out.node_cls[sl].cpu().numpy(), ref[0].numpy(), **FP32_TOL)
-        np.testing.assert_allclose(out.node_reg[sl].cpu().numpy(), ref[1].numpy(), **FP32_TOL)
-        sel = (pair_src >= f * N) & (pair_src < (f + 1) * N)
-        np.testing.assert_allclose(link[sel], ref[2].numpy(), **FP32_TOL)
         ncl = len(clusters[f])
-        np.testing.assert_allclose(out.obj_cls[f * ncl:(f + 1) * ncl].cpu().numpy(),
-                                   ref[3].numpy(), **FP32_TOL)
+        sel = (pair_src >= f * N) & (pair_src < (f + 1) * N)
+        pairs = {'node_cls': got['node_cls'][sl], 'node_reg': got['node_reg'][sl],
+                 'link_cls': link[sel], 'obj_cls': got['obj_cls'][f * ncl:(f + 1) * ncl]}
+        for k, r in zip(keys, ref):
+            r = r.numpy()
+            assert pairs[k].shape == r.shape, (f, k)
+            d = np.abs(pairs[k].astype(np.float64) - r)
+            worst[k] = max(worst[k], float((d / (1e-4 + 1e-4 * np.abs(r))).max()))
+            maxabs[k] = max(maxabs[k], float(d.max()))
+    report = {'frames': B, 'nodes': N, 'worst_over_bound': worst, 'max_abs_err': maxabs}
+    print('M parity headroom (1.0 = the 1e-4 bound):', report)
+    path = os.environ.get('RG_PARITY_REPORT')
+    if path:
+        import json
+        with open(path, 'w') as fh:
+            json.dump(report, fh, indent=1)
+    # headroom: a regression has to double the error before it reaches the 1e-4 bound
+    assert all(v <= 0.5 for v in worst.values()), report
+
+
+@pytest.mark.parametrize('over', [dict(graph_convolution_stem_channels=[128, 128]),
+                                  dict(graph_convolution_stem_channels=[64, 64],
+                                       msg_mlp_hidden_dim=96)])
+def test_f32_non_yml_conv_widths_match_oracle(cuda_device, over):
+    """fp32 models whose conv blocks are NOT the compiled fused shape (C = 64, hidden 128):
+    a 128-wide block without a residual projection, and a 96-wide message hidden layer.
+    The fused f32 conv is not planned for them (ConvPlan.fused is None), the unfused chains
+    run, and the forward equals the oracle at 1e-4 (these raised before)."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from oracle import graph_features_ref as gref
+    dev = cuda_device
+    cfg = default_config(**over)
+    torch.manual_seed(31)
+    m = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    pred = m.to(dev).pred.eval().requires_grad_(False)
+    gmax = float(np.sqrt(np.float64(100 ** 2 + 50 ** 2)))
+    fr = synthetic.make_frame(400, 4242)
+    g = gref.build_frame_graph(fr, 25.0, 10, gmax)
+    cl = [torch.from_numpy(c) for c in synthetic.cluster_lists(400)]
+    args = (torch.from_numpy(g['node_features']), torch.from_numpy(g['edge_features']),
+            torch.from_numpy(g['edge_index']))
+    with torch.no_grad():
+        out = pred(*(a.to(dev) for a in args), None, [c.to(dev) for c in cl])
+        ref = gnn_forward_ref.forward(sd, cfg, *args, None, cl)
+    for cv in pred.plans('fp32').convs:
+        if cv.c_out != 64 or cv.msg.specs[0].out_dim != 128:
+            assert not cv.fused
+    for o, r in zip(out, ref):
+        np.testing.assert_allclose(o.cpu().numpy(), r.numpy(), **FP32_TOL)
 
 
 def test_generic_chain_f32x3_matches_f32(cuda_device):
