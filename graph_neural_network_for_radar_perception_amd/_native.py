@@ -142,6 +142,9 @@ _SIGNATURES = {
     'rg_cross_entropy_backward': (_I, [_P, _I, _P, _I, _I, _P, _P, _I, _P]),
     'rg_frame_norm_workspace_size': (_S, [_I, _I]),
     'rg_frame_norm': (_I, [_P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _S, _P]),
+    'rg_frame_norm_backward_workspace_size': (_S, [_I, _I]),
+    'rg_frame_norm_backward': (_I, [_P, _I, _P, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P,
+                                    _P, _S, _P]),
     'rg_gather_i32': (_I, [_P, _P, _I, _P, _P]),
     'rg_lower_bound_i32': (_I, [_P, _P, _L, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),

@@ -115,6 +115,160 @@ __global__ __launch_bounds__(BT) void apply_kernel(const float* __restrict__ z, 
   }
 }
 
+// ------------------------------------------------------------------ backward
+// Training through layer / group normalisation (the reference's loss.backward() over
+// common.py:223-253).  Per segment s and group g with n = rows x C/G elements, from the
+// saved pre-norm rows z and the output gradient da:
+//   d = z - mean,  r = 1 / (std + eps),  n_ = d r,  y = s n_ + m,  gy = da act'(y),
+//   gn = s gy;   d_std_param += sum gy n_,  d_mu_param += sum gy   (over every element)
+//   dz = r (gn - mean(gn)) - r^2 (sum gn d) d / ((n - 1) std)     (torch.std: unbiased)
+// Pass 1 recomputes the statistics as the forward does; pass 2 sums (gn, gn d, d) per
+// (segment, chunk, group) and (gy n_, gy) per (segment, chunk) in float64; a finalize
+// turns them into per-(segment, group) coefficients and the two parameter gradients
+// (fixed order); pass 3 writes dz.  Deterministic.
+__device__ __forceinline__ float act_grad_y(float y, int act) {
+  if (act == ACT_LEAKY) return y > 0.f ? 1.f : 0.01f;  // torch: self > 0 ? grad : grad * slope
+  if (act == ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == ACT_SWISH) {
+    const float sg = 1.f / (1.f + expf(-y));
+    return sg * (1.f + y * (1.f - sg));
+  }
+  return 1.f;
+}
+
+__global__ __launch_bounds__(BT) void bpartial_kernel(const float* __restrict__ z, int ldz,
+                                                      const float* __restrict__ da, int ldda,
+                                                      int C, int G, const int* __restrict__ seg_ptr,
+                                                      const float* __restrict__ stats,
+                                                      const float* __restrict__ mu_p,
+                                                      const float* __restrict__ sd_p, int act,
+                                                      double* __restrict__ gpart,
+                                                      double* __restrict__ ppart) {
+  const int chunk = blockIdx.x, s = blockIdx.y;
+  long r0, r1;
+  seg_rows(seg_ptr, s, chunk, r0, r1);
+  const int cg = C / G;
+  const float mu = *mu_p, sd = *sd_p;
+  __shared__ double sh[3][BT];
+  double pn = 0.0, pm = 0.0;  // sum gy n_, sum gy over every group of the chunk
+  for (int g = 0; g < G; ++g) {
+    const float mean = stats[2 * ((size_t)s * G + g)];
+    const float sdev = stats[2 * ((size_t)s * G + g) + 1];
+    double a = 0.0, b = 0.0, c = 0.0;
+    const long n = (r1 - r0) * cg;
+    for (long t = threadIdx.x; t < n; t += BT) {
+      const long r = r0 + t / cg;
+      const int col = g * cg + (int)(t % cg);
+      const float x = z[(size_t)r * ldz + col];
+      const float d = x - mean;
+      const float nn = div_rn(d, sdev + NORM_EPS);
+      const float y = __fadd_rn(__fmul_rn(sd, nn), mu);
+      const float gy = da[(size_t)r * ldda + col] * act_grad_y(y, act);
+      const float gn = sd * gy;
+      a += (double)gn;
+      b += (double)gn * (double)d;
+      c += (double)d;
+      pn += (double)gy * (double)nn;
+      pm += (double)gy;
+    }
+    sh[0][threadIdx.x] = a;
+    sh[1][threadIdx.x] = b;
+    sh[2][threadIdx.x] = c;
+    __syncthreads();
+    for (int w = BT / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w)
+        for (int k = 0; k < 3; ++k) sh[k][threadIdx.x] += sh[k][threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      double* p = gpart + (((size_t)s * CHUNKS + chunk) * G + g) * 3;
+      p[0] = sh[0][0];
+      p[1] = sh[1][0];
+      p[2] = sh[2][0];
+    }
+    __syncthreads();
+  }
+  sh[0][threadIdx.x] = pn;
+  sh[1][threadIdx.x] = pm;
+  __syncthreads();
+  for (int w = BT / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + w];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ppart[((size_t)s * CHUNKS + chunk) * 2] = sh[0][0];
+    ppart[((size_t)s * CHUNKS + chunk) * 2 + 1] = sh[1][0];
+  }
+}
+
+// coef[s][g] = (r, r mean(gn), r^2 (sum gn d) / ((n - 1) std) - ... folded: see apply);
+// the parameter gradients over every (segment, chunk) in a fixed order (one thread)
+__global__ void bfinal_kernel(const double* __restrict__ gpart, const double* __restrict__ ppart,
+                              const int* __restrict__ seg_ptr, int n_seg, int C, int G,
+                              const float* __restrict__ stats, float* __restrict__ coef,
+                              float* __restrict__ d_mu, float* __restrict__ d_sd) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n_seg * G) {
+    const int s = t / G, g = t % G;
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int k = 0; k < CHUNKS; ++k) {
+      const double* p = gpart + (((size_t)s * CHUNKS + k) * G + g) * 3;
+      a += p[0];
+      b += p[1];
+      c += p[2];
+    }
+    const double n = (double)(seg_ptr[s + 1] - seg_ptr[s]) * (C / G);
+    const double sdev = (double)stats[2 * t + 1];
+    const double r = 1.0 / (double)(stats[2 * t + 1] + NORM_EPS);
+    const double k2 = sdev > 0.0 ? r * r * b / ((n - 1.0) * sdev) : 0.0;
+    // dz = r gn - k2 d - mean(r gn - k2 d) = r gn - k2 d - (r a - k2 c) / n
+    coef[3 * t] = (float)r;
+    coef[3 * t + 1] = (float)k2;
+    coef[3 * t + 2] = (float)((r * a - k2 * c) / n);
+  }
+  if (t == 0 && d_mu && d_sd) {
+    double pn = 0.0, pm = 0.0;
+    for (long k = 0; k < (long)n_seg * CHUNKS; ++k) {
+      pn += ppart[2 * k];
+      pm += ppart[2 * k + 1];
+    }
+    *d_sd += (float)pn;
+    *d_mu += (float)pm;
+  }
+}
+
+__global__ __launch_bounds__(BT) void bapply_kernel(const float* __restrict__ z, int ldz,
+                                                    const float* __restrict__ da, int ldda, int C,
+                                                    int G, const int* __restrict__ seg_ptr,
+                                                    const float* __restrict__ stats,
+                                                    const float* __restrict__ coef,
+                                                    const float* __restrict__ mu_p,
+                                                    const float* __restrict__ sd_p, int act,
+                                                    float* __restrict__ dz, int lddz) {
+  const int chunk = blockIdx.x, s = blockIdx.y;
+  long r0, r1;
+  seg_rows(seg_ptr, s, chunk, r0, r1);
+  const int cg = C / G;
+  const float mu = *mu_p, sd = *sd_p;
+  const long n = (r1 - r0) * C;
+  for (long t = threadIdx.x; t < n; t += BT) {
+    const long r = r0 + t / C;
+    const int col = (int)(t % C);
+    const size_t sg = (size_t)s * G + col / cg;
+    const float mean = stats[2 * sg], sdev = stats[2 * sg + 1];
+    const float x = z[(size_t)r * ldz + col];
+    const float d = x - mean;
+    const float nn = div_rn(d, sdev + NORM_EPS);
+    const float y = __fadd_rn(__fmul_rn(sd, nn), mu);
+    const float gn = sd * (da[(size_t)r * ldda + col] * act_grad_y(y, act));
+    const float* k = coef + 3 * sg;
+    dz[(size_t)r * lddz + col] = k[0] * gn - k[1] * d - k[2];
+  }
+}
+
 }  // namespace fnorm
 }  // namespace rg
 
@@ -153,6 +307,56 @@ extern "C" int rg_frame_norm(const float* z, int ldz, int C, int groups, const i
                                  : apply_kernel<ACT_NONE>;
   kern<<<grid, BT, 0, st>>>(z, ldz, C, groups, seg_ptr, stats, norm_mu, norm_std, residual, ld_res,
                             out, ld_out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+extern "C" size_t rg_frame_norm_backward_workspace_size(int n_seg, int groups) {
+  return rg_frame_norm_workspace_size(n_seg, groups) +
+         al256((size_t)n_seg * CHUNKS * groups * 3 * sizeof(double)) +
+         al256((size_t)n_seg * CHUNKS * 2 * sizeof(double)) +
+         al256((size_t)n_seg * groups * 3 * sizeof(float));
+}
+
+extern "C" int rg_frame_norm_backward(const float* z, int ldz, const float* da, int ldda, int C,
+                                      int groups, const int* seg_ptr, int n_seg,
+                                      const float* norm_mu, const float* norm_std, int act,
+                                      float* dz, int lddz, float* d_mu, float* d_std,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RG_REQUIRE(C >= 1 && groups >= 1 && groups <= MAXG && C % groups == 0, RG_ERR_ARG,
+             "rg_frame_norm_backward: C=%d groups=%d", C, groups);
+  RG_REQUIRE(n_seg >= 0 && norm_mu && norm_std && z && da && dz, RG_ERR_ARG,
+             "rg_frame_norm_backward: arguments");
+  RG_REQUIRE(act >= ACT_NONE && act <= ACT_SWISH, RG_ERR_ARG, "rg_frame_norm_backward: act %d", act);
+  RG_REQUIRE(workspace_bytes >= rg_frame_norm_backward_workspace_size(n_seg, groups), RG_ERR_ARG,
+             "rg_frame_norm_backward: workspace too small");
+  if (n_seg == 0) return RG_OK;
+  char* w = (char*)workspace;
+  double* partial = (double*)w;
+  float* stats = (float*)(w + al256((size_t)n_seg * CHUNKS * groups * 2 * sizeof(double)));
+  w += rg_frame_norm_workspace_size(n_seg, groups);
+  double* gpart = (double*)w;
+  w += al256((size_t)n_seg * CHUNKS * groups * 3 * sizeof(double));
+  double* ppart = (double*)w;
+  w += al256((size_t)n_seg * CHUNKS * 2 * sizeof(double));
+  float* coef = (float*)w;
+  const dim3 grid(CHUNKS, n_seg);
+  partial_kernel<<<grid, BT, 0, st>>>(z, ldz, C, groups, seg_ptr, partial);
+  RG_LAUNCH_CHECK();
+  finalize_kernel<<<ceil_div((long)n_seg * groups, 256), 256, 0, st>>>(partial, seg_ptr, n_seg, C,
+                                                                       groups, stats);
+  RG_LAUNCH_CHECK();
+  bpartial_kernel<<<grid, BT, 0, st>>>(z, ldz, da, ldda, C, groups, seg_ptr, stats, norm_mu,
+                                       norm_std, act, gpart, ppart);
+  RG_LAUNCH_CHECK();
+  bfinal_kernel<<<ceil_div((long)n_seg * groups, 256), 256, 0, st>>>(
+      gpart, ppart, seg_ptr, n_seg, C, groups, stats, coef, d_mu, d_std);
+  RG_LAUNCH_CHECK();
+  bapply_kernel<<<grid, BT, 0, st>>>(z, ldz, da, ldda, C, groups, seg_ptr, stats, coef, norm_mu,
+                                     norm_std, act, dz, lddz);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -197,8 +197,7 @@ class Model_Inference(nn.Module):
                                                            edge_index, cluster_node_idx)
         N = nf.shape[0]
         g = engine.DeviceGraph.from_edge_index(ei, N)
-        g.set_frames(torch.tensor([0] + sizes, dtype=torch.int64).cumsum(0).to(torch.int32)
-                     .to(nf.device), len(sizes))
+        _set_frames(g, sizes)
         E = g.n_edges
         e_dst = torch.empty((max(E, 1), ef.shape[1]), dtype=torch.float32, device=nf.device)
         if E > 0:
@@ -352,9 +351,10 @@ class Model_Training(nn.Module):
         names = ('loss_node_cls', 'loss_node_reg', 'loss_edge_cls', 'loss_obj_cls')
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             from .training import train_step_losses
-            nf, ef, ei, cptr, cidx, ncl, _ = _batch_frames(node_features, edge_features, edge_index,
-                                                           labels['cluster_node_idx'])
+            nf, ef, ei, cptr, cidx, ncl, sizes = _batch_frames(node_features, edge_features,
+                                                               edge_index, labels['cluster_node_idx'])
             g = engine.DeviceGraph.from_edge_index(ei, nf.shape[0])
+            _set_frames(g, sizes)
             e_dst = _edges_dst_major(ef, g)
             eng = self.train_engine()
             losses = train_step_losses(eng, (nf, e_dst, g, cptr, cidx, ncl, lab))
@@ -366,6 +366,14 @@ class Model_Training(nn.Module):
         acc = {'segment_accuracy': acc_t[0], 'edge_accuracy': acc_t[1],
                'object_accuracy': acc_t[2]}
         return loss, acc
+
+
+def _set_frames(g: engine.DeviceGraph, sizes: List[int]):
+    """Frame boundaries of a batched graph (layer / group normalisation statistics run
+    over one frame's rows, common.py:223-253)."""
+    dev = g.seg_ptr.device
+    g.set_frames(torch.tensor([0] + list(sizes), dtype=torch.int64).cumsum(0).to(torch.int32)
+                 .to(dev), len(sizes))
 
 
 def _edges_dst_major(ef: torch.Tensor, g: engine.DeviceGraph) -> torch.Tensor:
@@ -471,6 +479,7 @@ class Model_Object_Classifier_Finetuning(nn.Module):
             from .training import train_step_losses
             N = nf.shape[0]
             g = engine.DeviceGraph.from_edge_index(ei, N)
+            _set_frames(g, sizes)
             e_dst = _edges_dst_major(ef, g)
             lab = {'node_class': torch.zeros(N, dtype=torch.int64, device=dev),
                    'node_offsets': torch.zeros((N, 2), dtype=torch.float32, device=dev),

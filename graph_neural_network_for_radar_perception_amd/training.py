@@ -33,7 +33,7 @@ import torch
 
 from . import _native as nat
 from . import engine
-from .engine import ChainPlan, specs_from_modules
+from .engine import ChainPlan, LayerSpec, specs_from_modules
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -71,6 +71,7 @@ class ChainTape:
     idx1: Optional[torch.Tensor]
     z: List[torch.Tensor]
     a: List[torch.Tensor]
+    segs: Optional[tuple] = None   # (seg_ptr, n_seg) of the frames' rows (frame-wide norms)
 
 
 class TrainChain:
@@ -79,13 +80,16 @@ class TrainChain:
 
     def __init__(self, mods, device, ws: Workspaces):
         self.specs = specs_from_modules(mods)
-        if any(sp.frame_norm for sp in self.specs):
-            raise NotImplementedError(
-                'training with layer_normalization / group_normalization (frame-wide '
-                'statistics) has no native backward yet; inference supports them')
         if len(self.specs) > nat.MAX_LAYERS:
             raise NotImplementedError(f'chain of {len(self.specs)} layers > {nat.MAX_LAYERS}')
-        self.plan = ChainPlan(self.specs, 'fp32', device)
+        # layer / group normalisation (common.py:223-253) normalises a whole frame, which
+        # the row-wise chain kernel cannot see: such a layer is packed as a bare Linear (its
+        # launch writes the pre-norm rows z), rg_frame_norm applies the norm + activation
+        # over each frame's rows and rg_frame_norm_backward differentiates it
+        self.frame_norm = any(sp.frame_norm for sp in self.specs)
+        packed = [LayerSpec(sp.weight, sp.bias, None, None, 'none') if sp.frame_norm else sp
+                  for sp in self.specs]
+        self.plan = ChainPlan(packed, 'fp32', device)
         self.device = torch.device(device)
         self.ws = ws
         self._tsig = None
@@ -139,12 +143,20 @@ class TrainChain:
         return 400 + wb + slabs <= 160 * 1024 - 2048
 
     # ------------------------------------------------------------------ forward
+    def _segs(self, rows: int, segs):
+        """(seg_ptr, n_seg) of the frames' rows; None = all rows one frame."""
+        if segs is not None:
+            return segs
+        return (torch.tensor([0, int(rows)], dtype=torch.int32, device=self.device), 1)
+
     def forward(self, rows: int, out: torch.Tensor, in0: torch.Tensor, w0: int,
                 mode: int = nat.IN_DENSE, in1=None, w1: int = 0, in2=None, w2: int = 0,
-                idx0=None, idx1=None, residual=None) -> ChainTape:
+                idx0=None, idx1=None, residual=None, segs=None) -> ChainTape:
         """One launch for the chain when its weights fit in LDS, else one launch per
         layer (the tape holds every layer's output anyway, so splitting costs one extra
-        read of each intermediate instead of re-reading the weights from L2 per tile)."""
+        read of each intermediate instead of re-reading the weights from L2 per tile).
+        Chains with a frame-wide norm run one launch per layer, each such layer followed
+        by rg_frame_norm over the frames' rows (segs)."""
         self.plan.refresh()
         lib = nat.lib()
         dev = self.device
@@ -154,7 +166,11 @@ class TrainChain:
             zi = torch.empty((max(rows, 1), self.specs[i].out_dim), dtype=torch.float32, device=dev)
             z.append(zi)
             a.append(torch.empty_like(zi))
-        groups = [list(range(n))] if self._fits_lds(self.specs) else [[i] for i in range(n)]
+        if self.frame_norm:
+            segs = self._segs(rows, segs)
+            groups = [[i] for i in range(n)]
+        else:
+            groups = [list(range(n))] if self._fits_lds(self.specs) else [[i] for i in range(n)]
         st = nat.stream_ptr(dev)
         for gi, grp in enumerate(groups):
             arr = (nat.rg_layer * len(grp))()
@@ -171,7 +187,8 @@ class TrainChain:
                 m_, i0, w0_, i1, w1_, i2, w2_, x0, x1 = (nat.IN_DENSE, prev, prev.shape[1], None, 0,
                                                          None, 0, None, None)
             dst = out if last else a[grp[-1]]
-            res = residual if last else None
+            fn = self.specs[grp[-1]] if self.specs[grp[-1]].frame_norm else None
+            res = residual if (last and fn is None) else None
             rc = lib.rg_mlp_chain(
                 nat.RG_F32, arr, len(grp), int(rows), None, m_, nat.RG_F32, i0.data_ptr(),
                 i0.stride(0), w0_,
@@ -181,7 +198,23 @@ class TrainChain:
                 nat.ptr(res), res.stride(0) if res is not None else 0, nat.RG_F32,
                 dst.data_ptr(), dst.stride(0), nat.RG_F32, st)
             nat.check(rc, 'rg_mlp_chain (training tape)')
-        return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a)
+            if fn is not None and rows > 0:
+                zi = z[grp[-1]]
+                groups_n = fn.groups if fn.norm == 'group' else 1
+                if fn.out_dim % groups_n:
+                    raise RuntimeError(f'group_normalization: {fn.out_dim} channels not '
+                                       f'divisible by {groups_n} groups')
+                seg_ptr, n_seg = segs
+                res = residual if last else None
+                wsz = lib.rg_frame_norm_workspace_size(n_seg, groups_n)
+                wsb = self.ws.get('fnorm', wsz)
+                nat.check(lib.rg_frame_norm(zi.data_ptr(), zi.stride(0), fn.out_dim, groups_n,
+                                            seg_ptr.data_ptr(), n_seg, fn.mu.data_ptr(),
+                                            fn.std.data_ptr(), nat.ACT[fn.act], nat.ptr(res),
+                                            res.stride(0) if res is not None else 0,
+                                            dst.data_ptr(), dst.stride(0), wsb.data_ptr(), wsz, st),
+                          'rg_frame_norm (training tape)')
+        return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a, segs)
 
     # ------------------------------------------------------------------ backward
     def backward(self, tape: ChainTape, d_out: torch.Tensor, grads: Dict[int, torch.Tensor],
@@ -200,7 +233,18 @@ class TrainChain:
             sp = self.specs[l]
             act = nat.ACT[sp.act]
             has_norm = sp.mu is not None
-            if has_norm or act != 0:
+            if sp.frame_norm:
+                seg_ptr, n_seg = tape.segs
+                groups_n = sp.groups if sp.norm == 'group' else 1
+                wsz = lib.rg_frame_norm_backward_workspace_size(n_seg, groups_n)
+                wsb = self.ws.get('fnorm_bwd', wsz)
+                nat.check(lib.rg_frame_norm_backward(
+                    tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0),
+                    sp.out_dim, groups_n, seg_ptr.data_ptr(), n_seg, sp.mu.data_ptr(),
+                    sp.std.data_ptr(), act, dA.data_ptr(), dA.stride(0),
+                    nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))), wsb.data_ptr(),
+                    wsz, st), 'rg_frame_norm_backward')
+            elif has_norm or act != 0:
                 ws = self.ws.get('ffn', lib.rg_ffn_backward_workspace_size())
                 nat.check(lib.rg_ffn_backward(
                     tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0), rows,
@@ -242,9 +286,8 @@ class TrainChain:
 class TrainConv:
     def __init__(self, blk, device, ws):
         self.aggr = blk.aggr
-        if self.aggr not in ('add', 'sum', 'mean'):
-            raise NotImplementedError(f'training with aggregation {self.aggr!r} (the shipped '
-                                      'configuration uses add, configuration_radarscenes_gnn.yml:55)')
+        if self.aggr not in ('add', 'sum', 'mean', 'max'):
+            raise NotImplementedError(f'training with aggregation {self.aggr!r}')
         self.msg = TrainChain(list(blk.msg), device, ws)
         self.upd = TrainChain(list(blk.upd), device, ws)
         self.res = (TrainChain([blk.residual_connection], device, ws)
@@ -275,6 +318,8 @@ class TrainEngine:
         self.link_pair = mk(list(pl.stem) + [pl.pred_cls.head[0], pl.pred_cls.head[1]])
         self.cls_stem = mk(list(pc.stem)) if len(pc.stem) else None
         self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
+        # layer / group normalisation anywhere: the tape needs each frame's row ranges
+        self.frame_norm = any(c.frame_norm for c in self.chains())
         # flat gradient buffer: one view per parameter (one bucket for the DDP all-reduce)
         self.params = [p for p in model_training.parameters()]
         n = sum(p.numel() for p in self.params)
@@ -309,11 +354,21 @@ class TrainEngine:
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         N, E, U = g.n_nodes, g.n_edges, g.n_pairs
+        if self.frame_norm:
+            if g.frame_ptr is None:
+                raise ValueError('layer / group normalisation needs the batch\'s frame '
+                                 'boundaries (DeviceGraph.set_frames)')
+
+            def segs(kind):
+                return g.segs(kind)
+        else:
+            def segs(kind):
+                return None
         T = {}
         x = torch.empty((N, self.node_enc.out_dim), **f32)
-        T['node_enc'] = self.node_enc.forward(N, x, nf, nf.shape[1])
+        T['node_enc'] = self.node_enc.forward(N, x, nf, nf.shape[1], segs=segs('node'))
         e = torch.empty((max(E, 1), self.edge_enc.out_dim), **f32)
-        T['edge_enc'] = self.edge_enc.forward(E, e, e_dst, e_dst.shape[1])
+        T['edge_enc'] = self.edge_enc.forward(E, e, e_dst, e_dst.shape[1], segs=segs('edge'))
         xs = [x]
         T['conv'] = []
         for cv in self.convs:
@@ -321,46 +376,51 @@ class TrainEngine:
             ct = {}
             msg = torch.empty((max(E, 1), cv.msg.out_dim), **f32)
             ct['msg'] = cv.msg.forward(E, msg, x, C, mode=nat.IN_GATHER3, in2=e, w2=e.shape[1],
-                                       idx0=g.dst, idx1=g.src)
+                                       idx0=g.dst, idx1=g.src, segs=segs('edge'))
+            ct['msg_out'] = msg   # aggregation 'max': its backward needs the messages
             agg = torch.empty((N, cv.msg.out_dim), **f32)
             engine.segment_reduce(msg, g.seg_ptr, N, cv.aggr, agg)
             ct['agg'] = agg
             if cv.res is not None:
                 ident = torch.empty((N, cv.upd.out_dim), **f32)
-                ct['res'] = cv.res.forward(N, ident, x, C)
+                ct['res'] = cv.res.forward(N, ident, x, C, segs=segs('node'))
             else:
                 ident = x
             xn = torch.empty((N, cv.upd.out_dim), **f32)
             ct['upd'] = cv.upd.forward(N, xn, x, C, mode=nat.IN_CONCAT2, in1=agg,
-                                       w1=cv.msg.out_dim, residual=ident)
+                                       w1=cv.msg.out_dim, residual=ident, segs=segs('node'))
             T['conv'].append(ct)
             x = xn
             xs.append(x)
         T['xs'] = xs
         C = x.shape[1]
         node_cls = torch.empty((N, self.node_head.out_dim), **f32)
-        T['node_head'] = self.node_head.forward(N, node_cls, x, C)
+        T['node_head'] = self.node_head.forward(N, node_cls, x, C, segs=segs('node'))
         node_reg = torch.empty((N, self.offset_head.out_dim), **f32)
-        T['offset_head'] = self.offset_head.forward(N, node_reg, x, C)
+        T['offset_head'] = self.offset_head.forward(N, node_reg, x, C, segs=segs('node'))
         if self.link_node is not None:
             s = torch.empty((N, self.link_node.out_dim), **f32)
-            T['link_node'] = self.link_node.forward(N, s, x, C)
+            T['link_node'] = self.link_node.forward(N, s, x, C, segs=segs('node'))
         else:
             s = x
         T['s'] = s
         link = torch.empty((max(U, 1), self.link_pair.out_dim), **f32)
         T['link_pair'] = self.link_pair.forward(U, link, s, s.shape[1], mode=nat.IN_PAIRADD,
-                                                idx0=g.pair_src, idx1=g.pair_dst)
+                                                idx0=g.pair_src, idx1=g.pair_dst,
+                                                segs=segs('pair'))
         if self.cls_stem is not None:
             h = torch.empty((N, self.cls_stem.out_dim), **f32)
-            T['cls_stem'] = self.cls_stem.forward(N, h, x, C)
+            T['cls_stem'] = self.cls_stem.forward(N, h, x, C, segs=segs('node'))
         else:
             h = x
         T['h'] = h
         pooled = torch.empty((max(ncl, 1), h.shape[1]), **f32)
         engine.segment_reduce(h, cptr, ncl, 'max', pooled, idx=cidx)
         obj = torch.empty((max(ncl, 1), self.cls_head.out_dim), **f32)
-        T['cls_head'] = self.cls_head.forward(ncl, obj, pooled, pooled.shape[1])
+        csegs = None
+        if self.frame_norm and ncl > 0:
+            csegs = engine.cluster_segs(cptr, cidx, ncl, g.frame_ptr, g.n_frames)
+        T['cls_head'] = self.cls_head.forward(ncl, obj, pooled, pooled.shape[1], segs=csegs)
         outs = (node_cls, node_reg, link[:U], obj[:ncl])
         T.update(g=g, cptr=cptr, cidx=cidx, ncl=ncl, outs=outs, N=N, E=E, U=U)
         return outs, T
@@ -473,10 +533,19 @@ class TrainEngine:
                 dx_new = dx   # identity: d x += d x_out (already in dx)
             # d x += first half of the update input gradient
             self._add_cols(d_updin, 0, Cin, dx_new)
-            # d msg[p] = d agg[dst[p]] (mean: / count)
+            # d msg[p] = d agg[dst[p]] (mean: / count; max: to the maximal messages, ties
+            # sharing, torch's scatter_reduce amax backward)
             d_msg = torch.empty((max(E, 1), Cm), **f32)
-            scale = self._mean_scale(g, N) if cv.aggr == 'mean' else None
-            self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
+            if cv.aggr == 'max':
+                if E > 0:
+                    m = ct['msg_out']
+                    nat.check(lib.rg_segment_amax_backward(
+                        m.data_ptr(), m.stride(0), Cm, g.seg_ptr.data_ptr(), N,
+                        d_updin[:, Cin:].data_ptr(), d_updin.stride(0), d_msg.data_ptr(),
+                        d_msg.stride(0), st), 'rg_segment_amax_backward')
+            else:
+                scale = self._mean_scale(g, N) if cv.aggr == 'mean' else None
+                self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
             dG = torch.empty((max(E, 1), cv.msg.in_dim), **f32)
             cv.msg.backward(ct['msg'], d_msg, G, din=dG)
             # x_i = x[dst]: segment sums over the destination-major CSR

@@ -436,6 +436,17 @@ int rg_frame_norm(const float* z, int ldz, int C, int groups, const int* seg_ptr
                   const float* norm_mu, const float* norm_std, int act, const float* residual,
                   int ld_res, float* out, int ld_out, void* workspace, size_t workspace_bytes,
                   void* stream);
+/* Backward of rg_frame_norm (training through common.py:223-253, loss.backward()): from
+ * the saved pre-norm rows z and the gradient da of the activation output, writes
+ * dz = d out / d z (float32 [rows][C]) and ADDS the gradients of the scalar std / mu
+ * parameters to *d_std / *d_mu (device float32[1] each, nullable together).  The segment
+ * statistics are recomputed as rg_frame_norm computes them; every sum runs in float64 in
+ * a fixed order (deterministic). */
+size_t rg_frame_norm_backward_workspace_size(int n_seg, int groups);
+int rg_frame_norm_backward(const float* z, int ldz, const float* da, int ldda, int C, int groups,
+                           const int* seg_ptr, int n_seg, const float* norm_mu,
+                           const float* norm_std, int act, float* dz, int lddz, float* d_mu,
+                           float* d_std, void* workspace, size_t workspace_bytes, void* stream);
 /* out[t] = table[idx[t]] (device int32; per-frame edge offsets = seg_ptr[frame_ptr]) */
 int rg_gather_i32(const int* table, const int* idx, int n, int* out, void* stream);
 /* out[t] = first position p in sorted[0..n) with sorted[p] >= queries[t] (n from

@@ -455,6 +455,60 @@ def make_norm_fixtures():
         print('norm', norm, {k: v for k, v in data.items() if k.startswith('s1')})
 
 
+def make_max_training_fixture():
+    """Training with aggregation 'max' (gnn_blocks.py:57: MessagePassing(aggr=cfg.aggregation)
+    trains any aggregation through autograd): the reference's Model_Training, 2 conv blocks,
+    one loss.backward() on a 2-frame batch -> losses and every parameter gradient."""
+    from modules.set_configurations.set_config_gnn import config
+    from modules.neural_net.gnn.gnn_detector import Model_Training
+    cfg = config(os.path.join(REF, 'configuration_radarscenes_gnn.yml'))
+    cfg.aggregation = 'max'
+    cfg.graph_convolution_stem_channels = [64, 64]
+    sizes, seeds = (150, 110), (9201, 9202)
+    torch.manual_seed(41)
+    model = Model_Training(cfg, 'cpu')
+    data, graphs, labels = {}, [], []
+    for f, (n, sd_) in enumerate(zip(sizes, seeds)):
+        fr = synthetic.make_frame(n, sd_)
+        adj, nf, ef = _ref_graph(fr, cfg.ball_query_eps_square, cfg.k_number_nearest_points)
+        lb = synthetic.make_labels(fr, adj['adj_list'], cfg.num_classes, sd_)
+        graphs.append((adj, nf, ef))
+        labels.append(lb)
+        data[f'f{f}/node_features'] = nf.astype(np.float32)
+        data[f'f{f}/edge_features'] = ef.astype(np.float32)
+        data[f'f{f}/edge_index'] = adj['adj_list'].astype(np.int32)
+        data[f'f{f}/node_class'] = lb['node_class']
+        data[f'f{f}/node_offsets'] = lb['node_offsets']
+        data[f'f{f}/edge_class'] = lb['edge_class']
+        data[f'f{f}/cluster_ptr'] = np.cumsum([0] + [len(c) for c in lb['cluster_node_idx']]).astype(np.int64)
+        data[f'f{f}/cluster_idx'] = np.concatenate(lb['cluster_node_idx']).astype(np.int64)
+        data[f'f{f}/cluster_labels'] = lb['cluster_labels']
+    for k_, v in model.state_dict().items():
+        data['w/' + k_] = v.numpy()
+    lab = {'node_class': [torch.from_numpy(l['node_class']) for l in labels],
+           'node_offsets': [torch.from_numpy(l['node_offsets']) for l in labels],
+           'edge_class': [torch.from_numpy(l['edge_class']) for l in labels],
+           'cluster_node_idx': [[torch.from_numpy(c) for c in l['cluster_node_idx']] for l in labels],
+           'cluster_labels': [torch.from_numpy(l['cluster_labels']) for l in labels]}
+    model.train()
+    loss, acc = model(node_features=[torch.from_numpy(g[1]).float() for g in graphs],
+                      edge_features=[torch.from_numpy(g[2]).float() for g in graphs],
+                      edge_index=[torch.from_numpy(g[0]['adj_list']).long() for g in graphs],
+                      adj_matrix=[torch.from_numpy(g[0]['adj_matrix']) for g in graphs],
+                      labels=lab)
+    total = loss['loss_node_cls'] + loss['loss_node_reg'] + loss['loss_edge_cls'] + loss['loss_obj_cls']
+    total.backward()
+    for k_, v in loss.items():
+        data[f's1/{k_}'] = np.float64(v.item())
+    for k_, v in acc.items():
+        data[f's1/{k_}'] = np.float64(float(v))
+    for name, p_ in model.named_parameters():
+        data['g1/' + name] = p_.grad.detach().numpy().copy()
+    data.update(n_frames=len(sizes), aggregation='max', L=2)
+    np.savez_compressed(os.path.join(HERE, 'train_max_2frames.npz'), **data)
+    print('max training', {k: v for k, v in data.items() if k.startswith('s1')})
+
+
 def make_finetune_fixtures():
     """Model_Object_Classifier_Finetuning (gnn_detector.py:481-519) with the trained
     checkpoint, frozen except predict_class (set_param_for_finetuning_obj_classifier.py:31-34):
@@ -583,12 +637,16 @@ def main():
     if '--finetune-only' in sys.argv:
         make_finetune_fixtures()
         return
+    if '--max-training-only' in sys.argv:
+        make_max_training_fixture()
+        return
     if '--proposals-only' not in sys.argv:
         make_graph_fixtures()
         make_model_fixtures()
     make_proposal_fixtures()
     make_training_fixtures()
     make_norm_fixtures()
+    make_max_training_fixture()
     make_finetune_fixtures()
     make_classifier_fixtures()
 
