@@ -117,6 +117,8 @@ _SIGNATURES = {
                                _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
     'rg_mlp_chain_f32': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _P, _P,
                               _I, _P]),
+    'rg_mlp_chain_f32_ex': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _I, _I,
+                                 _P, _I, _I, _P, _P, _P, _I, _P, _I, _P]),
     'rg_mlp_chain_x3': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _P, _P,
                              _I, _P]),
     'rg_conv_layer_f32_workspace_size': (_S, [_I]),

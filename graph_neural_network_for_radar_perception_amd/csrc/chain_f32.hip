@@ -41,6 +41,8 @@ struct Layer {
   const float* sd;
   int out;
   int act;
+  float* zs;        // training tape (TAPE kernels): z = x W^T + b, float32 [rows][out]
+  float* as;        // and the activation output a, float32 [rows][out]
 };
 
 struct Args {
@@ -50,8 +52,14 @@ struct Args {
   const int* rows_dev;
   const float* in0;
   int ld0, w0real;
+  const float* in1;  // IN_CONCAT2: second part of the row (the aggregate)
+  int ld1;
+  const float* in2;  // IN_GATHER3: third part (the encoded edge rows)
+  int ld2;
   const int* idx0;
   const int* idx1;
+  const float* res;  // optional residual added to the chain output (identity, gnn_blocks.py:109)
+  int ld_res;
   float* out;
   int ld_out, out_real;
   int* zero_ptr;  // optional: zeroed by workgroup 0 (the next kernel's work counters)
@@ -59,9 +67,35 @@ struct Args {
 };
 
 // input modes of layer 0 (k-step order 8 s4 + 4h + u)
-enum { IN_SMALL = 0,   // float32 rows of <= 8 features (encoders), one k-quad per lane half
-       IN_DENSE = 1,   // float32 rows, K0 % 8 == 0
-       IN_PAIR = 2 };  // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
+enum { IN_SMALL = 0,    // float32 rows of <= 8 features (encoders), one k-quad per lane half
+       IN_DENSE = 1,    // float32 rows, K0 % 8 == 0
+       IN_PAIR = 2,     // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
+       IN_GATHER3 = 3,  // cat(x[idx0[r]], x[idx1[r]], e[r]): the message MLP input
+                        // (x_i, x_j, edge; gnn_blocks.py:112-113), 64 + 64 + 64 features
+       IN_CONCAT2 = 4 };  // cat(x[r], agg[r]): the update MLP input (gnn_blocks.py:108), 64 + 64
+static constexpr int GW = 64;  // part width of the gather / concat modes (the yml widths)
+
+// training tape: the 32 rows' features of accumulator tiles -> [rows][out] float32 (only the
+// `out` real columns of a padded last layer)
+template <int MT>
+__device__ __forceinline__ void tape_rows(const f32x16 (&acc)[MT], float* base, int out, long row,
+                                          int h) {
+  float* o = base + (size_t)row * out;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int f0 = 32 * m + 8 * g + 4 * h;
+      if (f0 + 4 <= out && (out & 3) == 0) {
+        *(f32x4*)(o + f0) = (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2],
+                                    acc[m][4 * g + 3]};
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (f0 + t < out) o[f0 + t] = acc[m][4 * g + t];
+      }
+    }
+}
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -215,19 +249,25 @@ template <int SPEC, int LI, int K, int N, int... Rest> struct LdsOff<SPEC, LI, K
 template <int MT>
 __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const Args& a, long row, int h) {
   float* o = a.out + (size_t)row * a.ld_out;
+  const float* rs = a.res ? a.res + (size_t)row * a.ld_res : nullptr;
   const int out = a.out_real;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int f0 = 32 * m + 8 * g + 4 * h;
-      if (f0 + 4 <= out && (a.ld_out & 3) == 0) {
-        *(f32x4*)(o + f0) = (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2],
-                                    acc[m][4 * g + 3]};
+      if (f0 + 4 <= out && (a.ld_out & 3) == 0 && (!rs || (a.ld_res & 3) == 0)) {
+        f32x4 v = {acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+        if (rs) {  // identity + upd(...) (gnn_blocks.py:109), one rounding per element
+          const f32x4 x = *(const f32x4*)(rs + f0);
+          v = (f32x4){__fadd_rn(x.x, v.x), __fadd_rn(x.y, v.y), __fadd_rn(x.z, v.z),
+                      __fadd_rn(x.w, v.w)};
+        }
+        *(f32x4*)(o + f0) = v;
       } else {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          if (f0 + t < out) o[f0 + t] = acc[m][4 * g + t];
+          if (f0 + t < out) o[f0 + t] = rs ? __fadd_rn(rs[f0 + t], acc[m][4 * g + t]) : acc[m][4 * g + t];
       }
     }
 }
@@ -239,8 +279,9 @@ __device__ __forceinline__ const char* wbase(const Args& a, const char* lds) {
   else return lds + OFF;
 }
 
-// layers LI.. of the chain; `prev` holds the previous layer's activations (B operands)
-template <int SPEC, int LI, int K, int N, int... Rest, int PMT, typename Off>
+// layers LI.. of the chain; `prev` holds the previous layer's activations (B operands).
+// TAPE: every layer's z (before its epilogue) and a (after it) also go to the tape.
+template <int SPEC, bool TAPE, int LI, int K, int N, int... Rest, int PMT, typename Off>
 __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT], const char* lds,
                                          const float* nrm, long row, bool valid, int lane, Off) {
   constexpr int S4 = K / 8, MT = N / 32;
@@ -256,15 +297,21 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT
     const int q = 4 * (s4 & 3);
     return (f32x4){p[q], p[q + 1], p[q + 2], p[q + 3]};
   });
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT>(acc, a.L[LI].zs, a.L[LI].out, row, h);
+  }
   epilogue<SPEC, LI, MT>(acc, nrm);
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
+  }
   if constexpr (sizeof...(Rest) > 0) {
-    run_rest<SPEC, LI + 1, N, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+    run_rest<SPEC, TAPE, LI + 1, N, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
   } else {
     if (valid) store_out<MT>(acc, a, row, h);
   }
 }
 
-template <int SPEC, int K0, int N0, int... Rest, typename Off>
+template <int SPEC, bool TAPE, int K0, int N0, int... Rest, typename Off>
 __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 + 7) / 8], const char* lds,
                                           const float* nrm, long row, bool valid, int lane, Off) {
   constexpr int S4 = (K0 + 7) / 8, MT = N0 / 32;
@@ -275,9 +322,15 @@ __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = bias_frag(bias, m, h);
   layer<S4, MT, spec_glob(SPEC, 0)>(acc, w, lane, [&](int s4) { return bin[s4]; });
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT>(acc, a.L[0].zs, a.L[0].out, row, h);
+  }
   epilogue<SPEC, 0, MT>(acc, nrm);
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
+  }
   if constexpr (sizeof...(Rest) > 0) {
-    run_rest<SPEC, 1, N0, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+    run_rest<SPEC, TAPE, 1, N0, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
   } else {
     if (valid) store_out<MT>(acc, a, row, h);
   }
@@ -287,7 +340,7 @@ __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 
 // normalisation) fused tile by tile into layer 1 -- each 32-feature output tile of layer
 // 0 (4 MFMAs) is activated and consumed at once as 16 k-steps of layer 1, so layer 0's
 // 256-wide activation never exists in full.
-template <int SPEC, int K0, int N0, int N1, int... Rest, typename Off>
+template <int SPEC, bool TAPE, int K0, int N0, int N1, int... Rest, typename Off>
 __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1], const char* lds,
                                             const float* nrm, long row, bool valid, int lane, Off) {
   static_assert(K0 <= 8, "fused first layer takes <= 8 inputs");
@@ -316,9 +369,21 @@ __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1]
     const f32x4 a0 = wa0[m0 * 64];
 #pragma unroll
     for (int u = 0; u < 4; ++u) t = mfma(a0[u], b0[u], t);
+    if constexpr (TAPE) {  // layer 0's z / a one 32-feature tile at a time
+      if (valid) {
+        f32x16 one[1] = {t};
+        tape_rows<1>(one, a.L[0].zs + 32 * m0, a.L[0].out, row, h);
+      }
+    }
     if constexpr (spec_act(SPEC, 0)) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) t[q] = act_t<(SPEC & 0xff)>(t[q]);
+    }
+    if constexpr (TAPE) {
+      if (valid) {
+        f32x16 one[1] = {t};
+        tape_rows<1>(one, a.L[0].as + 32 * m0, a.L[0].out, row, h);
+      }
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -329,15 +394,21 @@ __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1]
     (void)G1;
     __builtin_amdgcn_sched_barrier(0);  // bound the live fragments to one layer-0 tile
   }
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT1>(acc, a.L[1].zs, a.L[1].out, row, h);
+  }
   epilogue<SPEC, 1, MT1>(acc, nrm);
+  if constexpr (TAPE) {
+    if (valid) tape_rows<MT1>(acc, a.L[1].as, a.L[1].out, row, h);
+  }
   if constexpr (sizeof...(Rest) > 0) {
-    run_rest<SPEC, 2, N1, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
+    run_rest<SPEC, TAPE, 2, N1, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
   } else {
     if (valid) store_out<MT1>(acc, a, row, h);
   }
 }
 
-template <int MODE, int K0, int SPEC, bool FUSE01, int... Ns>
+template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int... Ns>
 __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[2 * RG_MAX_LAYERS];
@@ -384,6 +455,32 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
       const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 4 * h;
 #pragma unroll
       for (int s = 0; s < S40; ++s) b[s] = ok ? *(const f32x4*)(p + 8 * s) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    } else if constexpr (MODE == IN_GATHER3) {
+      // k-quad s: x[idx0] features 8 s + 4 h (s < 8), x[idx1] (8 <= s < 16), e (s >= 16)
+      static_assert(K0 == 3 * GW, "gather3 width");
+      const long rr = ok ? row : 0;
+      const float* pi = a.in0 + (size_t)(ok ? a.idx0[rr] : 0) * a.ld0 + 4 * h;
+      const float* pj = a.in0 + (size_t)(ok ? a.idx1[rr] : 0) * a.ld0 + 4 * h;
+      const float* pe = a.in2 + (size_t)rr * a.ld2 + 4 * h;
+#pragma unroll
+      for (int s = 0; s < S40; ++s) {
+        const float* p = s < GW / 8 ? pi + 8 * s : s < GW / 4 ? pj + 8 * (s - GW / 8) : pe + 8 * (s - GW / 4);
+        b[s] = *(const f32x4*)p;
+      }
+      if (!ok) {
+#pragma unroll
+        for (int s = 0; s < S40; ++s) b[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    } else if constexpr (MODE == IN_CONCAT2) {
+      static_assert(K0 == 2 * GW, "concat2 width");
+      const long rr = ok ? row : 0;
+      const float* p0 = a.in0 + (size_t)rr * a.ld0 + 4 * h;
+      const float* p1 = a.in1 + (size_t)rr * a.ld1 + 4 * h;
+#pragma unroll
+      for (int s = 0; s < S40; ++s) {
+        const f32x4 v = *(const f32x4*)(s < GW / 8 ? p0 + 8 * s : p1 + 8 * (s - GW / 8));
+        b[s] = ok ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
     } else {
       const int i = ok ? a.idx0[row] : 0, j = ok ? a.idx1[row] : 0;
       const float* pi = a.in0 + (size_t)i * a.ld0 + 4 * h;
@@ -407,17 +504,17 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
     fetch(tile + tstride, nb);
     const long row = tile * 32 + r;
     const bool valid = row < rows;
-    if constexpr (FUSE01) run_chain01<SPEC, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
-    else run_chain<SPEC, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
+    if constexpr (FUSE01) run_chain01<SPEC, TAPE, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
+    else run_chain<SPEC, TAPE, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
   }
 }
 
-template <int MODE, int K0, int SPEC, bool FUSE01, int... Ns>
+template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int... Ns>
 static int launch(const Args& a, hipStream_t st) {
   using Off = LdsOff<SPEC, 0, K0, Ns...>;
   constexpr int lds = Off::total();
   static_assert(lds <= DYN_LDS_MAX, "LDS image too large: read more layers from global memory");
-  auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, Ns...>;
+  auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, TAPE, Ns...>;
   RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   const long tiles = (a.rows + 31) / 32;
   long blocks = (tiles + 3) / 4;
@@ -431,11 +528,13 @@ static int launch(const Args& a, hipStream_t st) {
 
 struct Key {
   int mode, k0, spec_lo, nl;  // spec_lo: act | norm | act masks (bits 0..23)
+  int tape;                   // training tape (every layer's save_pre / save_out)
   int n[RG_MAX_LAYERS];
 };
 
-static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<int> ns) {
-  if (k.mode != mode || k.k0 != k0 || k.spec_lo != (sp & 0xffffff) || k.nl != (int)ns.size())
+static bool match(const Key& k, int mode, int k0, int sp, bool tape, std::initializer_list<int> ns) {
+  if (k.mode != mode || k.k0 != k0 || k.spec_lo != (sp & 0xffffff) || k.nl != (int)ns.size() ||
+      k.tape != (int)tape)
     return false;
   int i = 0;
   for (int v : ns)
@@ -446,7 +545,10 @@ static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<
 static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   constexpr int L = ACT_LEAKY;
 #define RG_F32C(MODE, K0, SP, F01, ...) \
-  if (match(k, MODE, K0, SP, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, __VA_ARGS__>(a, st);
+  if (match(k, MODE, K0, SP, false, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, false, __VA_ARGS__>(a, st);
+  // training forward (rg_mlp_chain_f32_ex with every layer's save_pre / save_out set)
+#define RG_F32T(MODE, K0, SP, F01, ...) \
+  if (match(k, MODE, K0, SP, true, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, true, __VA_ARGS__>(a, st);
   // edge encoder 7 -> 256 -> 128 -> 128 -> 64 (gnn_blocks.py:19-42, block 0 without norm):
   // layers 0 + 1 (136 KiB) in LDS, layers 2 + 3 (96 KiB) from L2
   RG_F32C(IN_SMALL, 7, spec(L, 0b1110, 0b1111, 0b1100), true, 256, 128, 128, 64)
@@ -461,7 +563,22 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   RG_F32C(IN_DENSE, 64, spec(L, 0b1, 0b1, 0), false, 64)
   RG_F32C(IN_DENSE, 64, spec(L, 0b111, 0b111, 0), false, 64, 64, 64)
   RG_F32C(IN_DENSE, 64, spec(L, 0b01, 0b01, 0), false, 64, 32)
+  // ---- training tapes of the yml architecture (Model_Training.forward, training.py)
+  // message MLP 192 -> 128 -> 64 on cat(x_i, x_j, e) (gnn_blocks.py:104-113), 131 KiB in LDS
+  RG_F32T(IN_GATHER3, 192, spec(L, 0b11, 0b11, 0), false, 128, 64)
+  // update MLP 128 -> 64 on cat(x, agg), + identity
+  RG_F32T(IN_CONCAT2, 128, spec(L, 0b1, 0b1, 0), false, 64)
+  // encoders (layer 0's tape written one 32-feature tile at a time)
+  RG_F32T(IN_SMALL, 7, spec(L, 0b1110, 0b1111, 0b1100), true, 256, 128, 128, 64)
+  RG_F32T(IN_SMALL, 6, spec(L, 0b110, 0b111, 0b100), true, 256, 128, 64)
+  // task heads, link pairs, link / object stems, object head
+  RG_F32T(IN_DENSE, 64, spec(L, 0b1111, 0b1111, 0), false, 64, 64, 64, 64, 32)
+  RG_F32T(IN_PAIR, 64, spec(L, 0b1111, 0b1111, 0), false, 64, 64, 64, 64, 32)
+  RG_F32T(IN_DENSE, 64, spec(L, 0b1, 0b1, 0), false, 64)
+  RG_F32T(IN_DENSE, 64, spec(L, 0b111, 0b111, 0), false, 64, 64, 64)
+  RG_F32T(IN_DENSE, 64, spec(L, 0b01, 0b01, 0), false, 64, 32)
 #undef RG_F32C
+#undef RG_F32T
   return RG_ERR_UNSUPPORTED;
 }
 
@@ -478,35 +595,50 @@ int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const i
                         const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
                         void* stream);
 
-int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
-                        int in_mode, const float* in0, int ld0, int w0, const int* idx0,
-                        const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
-                        void* stream) {
+static int f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                            int in_mode, const float* in0, int ld0, int w0, const float* in1,
+                            int ld1, int w1, const float* in2, int ld2, int w2, const int* idx0,
+                            const int* idx1, const float* res, int ld_res, float* out, int ld_out,
+                            int* zero_ptr, int zero_n, void* stream) {
   RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_f32: n_layers");
   RG_REQUIRE(zero_n <= FT, RG_ERR_ARG, "rg_mlp_chain_f32: zero_n");
   Key k;
   memset(&k, 0, sizeof(k));
   Args a;
   memset(&a, 0, sizeof(a));
-  if (in_mode == RG_IN_DENSE && w0 <= 8 && n_layers >= 2 && !layers[0].norm_mu)
+  int k0 = w0;
+  if (in_mode == RG_IN_DENSE && w0 <= 8 && n_layers >= 2 && !layers[0].norm_mu) {
     k.mode = IN_SMALL;
-  else if (in_mode == RG_IN_DENSE)
+  } else if (in_mode == RG_IN_DENSE) {
     k.mode = IN_DENSE;
-  else if (in_mode == RG_IN_PAIRADD)
+  } else if (in_mode == RG_IN_PAIRADD) {
     k.mode = IN_PAIR;
-  else
+  } else if (in_mode == RG_IN_GATHER3) {
+    if (w0 != GW || w2 != GW || !in2 || !idx0 || !idx1 || ld2 % 4) return RG_ERR_UNSUPPORTED;
+    k.mode = IN_GATHER3;
+    k0 = 2 * w0 + w2;
+  } else if (in_mode == RG_IN_CONCAT2) {
+    if (w0 != GW || w1 != GW || !in1 || ld1 % 4) return RG_ERR_UNSUPPORTED;
+    k.mode = IN_CONCAT2;
+    k0 = w0 + w1;
+  } else {
     return RG_ERR_UNSUPPORTED;
+  }
   RG_REQUIRE(k.mode == IN_SMALL || (w0 % 8 == 0 && ld0 % 4 == 0), RG_ERR_UNSUPPORTED,
              "rg_mlp_chain_f32: dense input width / stride must be multiples of 8 / 4");
-  k.k0 = w0;
+  k.k0 = k0;
   k.nl = n_layers;
+  // training tape: every layer saves (z, a) or none does
+  k.tape = layers[0].save_pre != nullptr;
   int nm = 0, am = 0;
   for (int l = 0; l < n_layers; ++l) {
     const rg_layer& s = layers[l];
     RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_f32: layer %d weights", l);
-    if (s.save_pre || s.save_out || (s.flags & RG_LAYER_CENTERED)) return RG_ERR_UNSUPPORTED;
+    if (s.flags & RG_LAYER_CENTERED) return RG_ERR_UNSUPPORTED;
+    if ((s.save_pre != nullptr) != (bool)k.tape || (s.save_out != nullptr) != (bool)k.tape)
+      return RG_ERR_UNSUPPORTED;
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
-    RG_REQUIRE(l == 0 ? s.in_dim == w0 : s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG,
+    RG_REQUIRE(l == 0 ? s.in_dim == k0 : s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG,
                "rg_mlp_chain_f32: layer %d width", l);
     if (l + 1 < n_layers && s.out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
     if (s.norm_mu && s.out_dim % 32 != 0) return RG_ERR_UNSUPPORTED;
@@ -519,6 +651,8 @@ int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const i
     a.L[l].sd = s.norm_std;
     a.L[l].out = s.out_dim;
     a.L[l].act = s.act;
+    a.L[l].zs = s.save_pre;
+    a.L[l].as = s.save_out;
   }
   k.spec_lo = spec(ACT_LEAKY, nm, am, 0);
   a.nl = n_layers;
@@ -527,8 +661,14 @@ int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const i
   a.in0 = in0;
   a.ld0 = ld0;
   a.w0real = w0;
+  a.in1 = in1;
+  a.ld1 = ld1;
+  a.in2 = in2;
+  a.ld2 = ld2;
   a.idx0 = idx0;
   a.idx1 = idx1;
+  a.res = res;
+  a.ld_res = ld_res;
   a.out = out;
   a.ld_out = ld_out;
   a.out_real = layers[n_layers - 1].out_dim;
@@ -538,12 +678,34 @@ int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const i
   return dispatch(k, a, (hipStream_t)stream);
 }
 
+int rg_f32_chain_launch(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                        int in_mode, const float* in0, int ld0, int w0, const int* idx0,
+                        const int* idx1, float* out, int ld_out, int* zero_ptr, int zero_n,
+                        void* stream) {
+  return f32_chain_launch(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, nullptr, 0, 0,
+                          nullptr, 0, 0, idx0, idx1, nullptr, 0, out, ld_out, zero_ptr, zero_n,
+                          stream);
+}
+
 extern "C" int rg_mlp_chain_f32(const rg_layer* layers, int n_layers, long rows,
                                 const int* rows_dev, int in_mode, const float* in0, int ld0,
                                 int w0, const int* idx0, const int* idx1, float* out, int ld_out,
                                 void* stream) {
   RG_REQUIRE(in_mode != RG_IN_PAIRADD || (idx0 && idx1), RG_ERR_ARG,
              "rg_mlp_chain_f32: RG_IN_PAIRADD needs idx0 and idx1");
+  if (in_mode != RG_IN_DENSE && in_mode != RG_IN_PAIRADD) return RG_ERR_UNSUPPORTED;
   return rg_f32_chain_launch(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, idx0, idx1,
                              out, ld_out, nullptr, 0, stream);
+}
+
+extern "C" int rg_mlp_chain_f32_ex(const rg_layer* layers, int n_layers, long rows,
+                                   const int* rows_dev, int in_mode, const float* in0, int ld0,
+                                   int w0, const float* in1, int ld1, int w1, const float* in2,
+                                   int ld2, int w2, const int* idx0, const int* idx1,
+                                   const float* residual, int ld_res, float* out, int ld_out,
+                                   void* stream) {
+  RG_REQUIRE((in_mode != RG_IN_PAIRADD && in_mode != RG_IN_GATHER3) || (idx0 && idx1), RG_ERR_ARG,
+             "rg_mlp_chain_f32_ex: gathered input modes need idx0 and idx1");
+  return f32_chain_launch(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, in1, ld1, w1, in2,
+                          ld2, w2, idx0, idx1, residual, ld_res, out, ld_out, nullptr, 0, stream);
 }

@@ -56,6 +56,12 @@ static constexpr int PQW = 2 * HID;
 #ifndef RG_CX3_PRIO
 #define RG_CX3_PRIO 0
 #endif
+#ifndef RG_CX3_STAGGER
+#define RG_CX3_STAGGER 0  // waves 4-7 (each SIMD's second wave) start after N x s_sleep(127)
+                          // (~8k cycles each): the two waves of a SIMD run the same tile
+                          // program, and in lockstep their MFMA phases collide while their
+                          // gather / norm phases leave the matrix pipe idle
+#endif
 static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
 #ifndef RG_CX3_STAMP
 #define RG_CX3_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_cx3_stamp
@@ -306,6 +312,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   if (RG_CX3_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (RG_CX3_STAGGER && wave >= NW / 2) {
+    for (int i = 0; i < RG_CX3_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   float* T = (float*)(lds + W_LDS + wave * T_BYTES);  // [TR][TS] message rows
   const WLds wE{lds + WE_OFF + lane * 16, plane_bytes(C, HID)};
   const WLds w2{lds + W2_OFF + lane * 16, plane_bytes(HID, C)};

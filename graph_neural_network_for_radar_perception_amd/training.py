@@ -26,6 +26,7 @@ counts (loss.py:59-73 on the concatenated predictions), so batching is exact.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -34,6 +35,11 @@ import torch
 from . import _native as nat
 from . import engine
 from .engine import ChainPlan, LayerSpec, specs_from_modules
+
+
+# training forward on the register-resident f32 chains (rg_mlp_chain_f32_ex with tapes)
+# where the shape has an instantiation; '0' = the generic chain kernel for every chain
+TAPE_F32_FAST = os.environ.get('RG_TRAIN_F32FAST', '1') != '0'
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -90,6 +96,7 @@ class TrainChain:
         packed = [LayerSpec(sp.weight, sp.bias, None, None, 'none') if sp.frame_norm else sp
                   for sp in self.specs]
         self.plan = ChainPlan(packed, 'fp32', device)
+        self._fast_ok = {}   # input mode -> the register-resident tape kernel took the chain
         self.device = torch.device(device)
         self.ws = ws
         self._tsig = None
@@ -166,12 +173,33 @@ class TrainChain:
             zi = torch.empty((max(rows, 1), self.specs[i].out_dim), dtype=torch.float32, device=dev)
             z.append(zi)
             a.append(torch.empty_like(zi))
+        st = nat.stream_ptr(dev)
+        if not self.frame_norm and TAPE_F32_FAST and self._fast_ok.get(mode, True):
+            # the register-resident f32 chain with its tape (rg_mlp_chain_f32_ex, exact f32
+            # products on v_mfma_f32_32x32x2_f32): one launch, activations in registers
+            src = self.plan._f32_layers()
+            arr = (nat.rg_layer * n)()
+            for i in range(n):
+                ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(src[i]), ctypes.sizeof(nat.rg_layer))
+                arr[i].save_pre = z[i].data_ptr()
+                arr[i].save_out = a[i].data_ptr()
+            rc = lib.rg_mlp_chain_f32_ex(
+                arr, n, int(rows), None, mode, in0.data_ptr(), in0.stride(0), w0,
+                nat.ptr(in1), in1.stride(0) if in1 is not None else 0, w1,
+                nat.ptr(in2), in2.stride(0) if in2 is not None else 0, w2,
+                nat.ptr(idx0), nat.ptr(idx1), nat.ptr(residual),
+                residual.stride(0) if residual is not None else 0, out.data_ptr(), out.stride(0), st)
+            if rc == 0:
+                self._fast_ok[mode] = True
+                return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a, segs)
+            if rc != nat.RG_ERR_UNSUPPORTED:
+                nat.check(rc, 'rg_mlp_chain_f32_ex (training tape)')
+            self._fast_ok[mode] = False
         if self.frame_norm:
             segs = self._segs(rows, segs)
             groups = [[i] for i in range(n)]
         else:
             groups = [list(range(n))] if self._fits_lds(self.specs) else [[i] for i in range(n)]
-        st = nat.stream_ptr(dev)
         for gi, grp in enumerate(groups):
             arr = (nat.rg_layer * len(grp))()
             for j, i in enumerate(grp):

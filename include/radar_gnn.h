@@ -302,6 +302,18 @@ int rg_mlp_chain_fast(const rg_layer* layers_host, int n_layers, long rows, cons
 int rg_mlp_chain_f32(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
                      int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                      const int* idx1, float* out, int ld_out, void* stream);
+/* rg_mlp_chain_f32 with every input mode and the training tape: in_mode also
+ * RG_IN_GATHER3 (cat(in0[idx0], in0[idx1], in2) with 64-wide parts: the message MLP,
+ * gnn_blocks.py:104-113) and RG_IN_CONCAT2 (cat(in0, in1), 64 + 64: the update MLP,
+ * :108); optional residual (out = residual + chain, :109); when every layer's save_pre /
+ * save_out is set, each layer's z and a rows are written as rg_mlp_chain writes them (the
+ * training forward of training.py:66-85).  RG_ERR_UNSUPPORTED (launching nothing) for
+ * shapes without an instantiation. */
+int rg_mlp_chain_f32_ex(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
+                        int in_mode, const float* in0, int ld0, int w0, const float* in1, int ld1,
+                        int w1, const float* in2, int ld2, int w2, const int* idx0,
+                        const int* idx1, const float* residual, int ld_res, float* out,
+                        int ld_out, void* stream);
 
 /* The same float32 chains on the bf16 matrix cores: every product formed from the exact
  * three-term bf16 splits of both operands (RG_PACK_X3, see rg_conv_layer_x3), f32

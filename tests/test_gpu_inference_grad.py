@@ -12,8 +12,8 @@ evaluation harness:
 The parameters still require grad and there is no torch.no_grad(): the outputs must
 equal the reference run (fixtures made by the reference itself, 1e-4), work with the
 callers' softmax / max / .detach().cpu().numpy(), and carry a backward whose parameter
-gradients equal autograd through the oracle (2e-4 x max|g| per tensor, the training
-tests' bound; tests/test_gpu_training.py).
+gradients agree with autograd through the oracle as closely as float32 allows (the
+float64-referenced bound of tests/test_gpu_training.py).
 """
 import numpy as np
 import pytest
@@ -36,25 +36,39 @@ def _detector(name, dev):
     return detector_train.pred.eval()
 
 
-def _grad_close(got, want, name, rel=2e-4):
-    got = np.asarray(got, np.float64)
-    want = np.asarray(want, np.float64)
-    tol = rel * float(np.max(np.abs(want))) + (1e-6 if want.size == 1 else 1e-7)
-    err = float(np.max(np.abs(got - want))) if want.size else 0.0
-    assert err <= tol, f'{name}: max |d| {err:.3e} > {tol:.3e}'
-
-
-def _oracle_grads(name, d, lists, weights):
-    """autograd through the oracle's op-for-op forward (CPU, float32) of
-    sum_k <weights_k, output_k>."""
+def _oracle_grads(name, d, lists, weights, dtype=torch.float32):
+    """autograd through the oracle's op-for-op forward (CPU) of sum_k <weights_k, output_k>,
+    in float32 or float64 (the stand-in for exact arithmetic)."""
     from oracle import gnn_forward_ref as ref
-    sd = {k: v.detach().clone().requires_grad_(True) for k, v in model_state_dict(name).items()}
-    out = ref.forward(sd, model_cfg(name), torch.from_numpy(d['node_features']),
-                      torch.from_numpy(d['edge_features']),
-                      torch.from_numpy(d['edge_index'].astype(np.int64)), None, lists)
-    total = sum((o * w).sum() for o, w in zip(out, weights))
-    total.backward()
-    return {k: v.grad for k, v in sd.items()}
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        sd = {k: v.detach().clone().to(dtype).requires_grad_(True)
+              for k, v in model_state_dict(name).items()}
+        out = ref.forward(sd, model_cfg(name), torch.from_numpy(d['node_features']).to(dtype),
+                          torch.from_numpy(d['edge_features']).to(dtype),
+                          torch.from_numpy(d['edge_index'].astype(np.int64)), None, lists)
+        total = sum((o * w.to(dtype)).sum() for o, w in zip(out, weights))
+        total.backward()
+        return {k: v.grad for k, v in sd.items()}
+    finally:
+        torch.set_default_dtype(prev)
+
+
+def _check_grads(model, name, d, lists, weights):
+    """Every parameter gradient at least as close to the float64 oracle as float32 allows
+    (the bound of tests/test_gpu_training.py::test_training_grads_match_oracle_larger): per
+    tensor max|g - g64| / max|g64| <= max(10 x the float32 oracle's own error, 1e-5) and
+    <= 1e-2."""
+    g32 = _oracle_grads(name, d, lists, weights, torch.float32)
+    g64 = _oracle_grads(name, d, lists, weights, torch.float64)
+    for pname, p in model.named_parameters():
+        assert p.grad is not None, pname
+        ref = g64['pred.' + pname].numpy()
+        scale = float(np.max(np.abs(ref))) + 1e-30
+        ours = float(np.max(np.abs(p.grad.double().cpu().numpy() - ref))) / scale
+        orc = float(np.max(np.abs(g32['pred.' + pname].double().numpy() - ref))) / scale
+        assert ours <= max(10 * orc, 1e-5) and ours <= 1e-2, (pname, ours, orc)
 
 
 def _weights(out, seed):
@@ -86,10 +100,7 @@ def test_grad_enabled_cluster_lists_match_reference(cuda_device):
     w = _weights(out, 3)
     total = sum((o * wi.to(dev)).sum() for o, wi in zip(out, w))
     total.backward()
-    want = _oracle_grads(name, d, cluster_lists(d), w)
-    for pname, p in detector.named_parameters():
-        assert p.grad is not None, pname
-        _grad_close(p.grad.cpu().numpy(), want['pred.' + pname].numpy(), pname)
+    _check_grads(detector, name, d, cluster_lists(d), w)
 
 
 @pytest.mark.parametrize('tag', ['off', 'links'])
@@ -139,10 +150,7 @@ def test_grad_enabled_proposals_like_reference_callers(cuda_device, tag):
     w = _weights(outs, 5)
     total = sum((o * wi.to(dev)).sum() for o, wi in zip(outs, w))
     total.backward()
-    lists = [c.cpu() for c in cluster_members_list]
-    want = _oracle_grads(name, d, lists, w)
-    for pname, p in detector.named_parameters():
-        _grad_close(p.grad.cpu().numpy(), want['pred.' + pname].numpy(), pname)
+    _check_grads(detector, name, d, [c.cpu() for c in cluster_members_list], w)
 
 
 def test_grad_enabled_frozen_layers_only_object_head_gets_grads(cuda_device):
