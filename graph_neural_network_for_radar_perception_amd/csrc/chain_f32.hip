@@ -224,8 +224,46 @@ __device__ __forceinline__ void channel_norm_leaky(f32x16 (&acc)[MT], float mu, 
     }
 }
 
-template <int SPEC, int LI, int MT>
+// channel_normalization in the reference's operation order (common.py:215-220:
+// (x - mean) / (std + eps), then std_param * . + mu_param, correctly rounded sqrt and
+// divide) -- the training tape's epilogue, so the saved activations are the values the
+// backward's recomputation (rg_ffn_backward) assumes
+template <int MT>
+__device__ __forceinline__ void channel_norm_ref(f32x16 (&acc)[MT], float mu, float sd) {
+  constexpr int N = 32 * MT;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      s0 += acc[m][q];
+      s1 += acc[m][q + 1];
+    }
+  const float mean = add_xor32(s0 + s1) * (1.f / N);  // N is a power of two: exact
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+      acc[m][q] -= mean;
+      acc[m][q + 1] -= mean;
+      q0 = fmaf(acc[m][q], acc[m][q], q0);
+      q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
+    }
+  const float den = __fadd_rn(__fsqrt_rn(__fdiv_rn(add_xor32(q0 + q1), (float)(N - 1))), NORM_EPS);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[m][q] = __fadd_rn(__fmul_rn(sd, __fdiv_rn(acc[m][q], den)), mu);
+}
+
+template <int SPEC, int LI, int MT, bool TAPE = false>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const float* nrm) {
+  if constexpr (TAPE) {
+    if constexpr (spec_norm(SPEC, LI)) channel_norm_ref<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1]);
+    if constexpr (spec_act(SPEC, LI)) act_all<(SPEC & 0xff), MT>(acc);
+    return;
+  }
   if constexpr (spec_norm(SPEC, LI) && spec_act(SPEC, LI) && (SPEC & 0xff) == ACT_LEAKY) {
     channel_norm_leaky<MT>(acc, nrm[2 * LI], nrm[2 * LI + 1]);
     return;
@@ -300,7 +338,7 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT
   if constexpr (TAPE) {
     if (valid) tape_rows<MT>(acc, a.L[LI].zs, a.L[LI].out, row, h);
   }
-  epilogue<SPEC, LI, MT>(acc, nrm);
+  epilogue<SPEC, LI, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
     if (valid) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
   }
@@ -325,7 +363,7 @@ __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 
   if constexpr (TAPE) {
     if (valid) tape_rows<MT>(acc, a.L[0].zs, a.L[0].out, row, h);
   }
-  epilogue<SPEC, 0, MT>(acc, nrm);
+  epilogue<SPEC, 0, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
     if (valid) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
   }
@@ -397,7 +435,7 @@ __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1]
   if constexpr (TAPE) {
     if (valid) tape_rows<MT1>(acc, a.L[1].zs, a.L[1].out, row, h);
   }
-  epilogue<SPEC, 1, MT1>(acc, nrm);
+  epilogue<SPEC, 1, MT1, TAPE>(acc, nrm);
   if constexpr (TAPE) {
     if (valid) tape_rows<MT1>(acc, a.L[1].as, a.L[1].out, row, h);
   }
@@ -577,6 +615,14 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   RG_F32T(IN_DENSE, 64, spec(L, 0b1, 0b1, 0), false, 64)
   RG_F32T(IN_DENSE, 64, spec(L, 0b111, 0b111, 0), false, 64, 64, 64)
   RG_F32T(IN_DENSE, 64, spec(L, 0b01, 0b01, 0), false, 64, 32)
+  // the backward's data GEMMs dX = dZ W (weights packed RG_PACK_F32_FAST | RG_PACK_TRANSPOSE,
+  // one bare layer, optionally accumulating through the residual input): message layers
+  // 64 -> 128 and 128 -> 192, update 64 -> 128, stems 64 -> 64, encoder layers
+  RG_F32C(IN_DENSE, 64, spec(L, 0, 0, 0), false, 64)
+  RG_F32C(IN_DENSE, 64, spec(L, 0, 0, 0), false, 128)
+  RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 128)
+  RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 192)
+  RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 256)
 #undef RG_F32C
 #undef RG_F32T
   return RG_ERR_UNSUPPORTED;

@@ -181,7 +181,7 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
 // order is what both a row loaded from memory (one float4 per lane half and s4) and the
 // previous layer's 32x32 accumulators (register 4g + t of M-tile m' = k-step
 // 16 m' + 4g + t) supply, so one format serves every layer of an f32 chain
-__global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int out,
+__global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int out, int transpose,
                                      float* __restrict__ P, long total) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
@@ -193,7 +193,8 @@ __global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int ou
   const int m = (int)(ms / S4);
   const int o = 32 * m + (lane & 31);
   const int k = 8 * s4 + 4 * (lane >> 5) + u;
-  P[t] = (o < out && k < in) ? W[(size_t)o * in + k] : 0.f;
+  // transpose: W is the [in][out] weight of the forward layer, packed as its transpose
+  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k]) : 0.f;
 }
 
 __global__ void pack_bias_kernel(const float* __restrict__ b, int out, int n, float* __restrict__ P) {
@@ -661,8 +662,8 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   const int center = (dtype & RG_PACK_CENTERED) ? 1 : 0;
   const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;
   dtype &= ~(RG_PACK_CENTERED | RG_PACK_TRANSPOSE);
-  RG_REQUIRE(!transpose || dtype == RG_F32, RG_ERR_ARG,
-             "rg_pack_linear: RG_PACK_TRANSPOSE applies to RG_F32");
+  RG_REQUIRE(!transpose || dtype == RG_F32 || dtype == RG_PACK_F32_FAST, RG_ERR_ARG,
+             "rg_pack_linear: RG_PACK_TRANSPOSE applies to RG_F32 and RG_PACK_F32_FAST");
   RG_REQUIRE(!center || (dtype >= RG_PACK_FAST_IN && dtype <= RG_PACK_FAST_UPD), RG_ERR_ARG,
              "rg_pack_linear: RG_PACK_CENTERED applies to the bf16 RG_PACK_FAST_* formats");
   if (dtype == RG_F32) {
@@ -689,7 +690,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
                                                            total);
   } else if (dtype == RG_PACK_F32_FAST) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(float);
-    pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim,
+    pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
                                                                (float*)packed, total);
   } else {
     RG_REQUIRE(false, RG_ERR_ARG, "rg_pack_linear: bad dtype %d", dtype);

@@ -97,6 +97,7 @@ class TrainChain:
                   for sp in self.specs]
         self.plan = ChainPlan(packed, 'fp32', device)
         self._fast_ok = {}   # input mode -> the register-resident tape kernel took the chain
+        self._dx_ok = {}     # layer -> the register-resident kernel took its dX = dZ W
         self.device = torch.device(device)
         self.ws = ws
         self._tsig = None
@@ -111,33 +112,63 @@ class TrainChain:
         self._tsig = None
 
     def _transposed(self):
-        """W^T of every layer packed as an RG_F32 layer (no bias / norm / activation):
-        the data GEMM of the backward, dX = dZ W, on the chain kernel."""
+        """W^T of every layer (no bias / norm / activation) for the data GEMM of the
+        backward, dX = dZ W: per layer (generic RG_F32 image, register-resident
+        RG_PACK_F32_FAST image), both packed transposed."""
         sig = self.plan.sig
         if self._tsig == sig:
             return self._tarr
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
-        fmt = nat.RG_F32 | nat.RG_PACK_TRANSPOSE
-        sizes = [lib.rg_packed_linear_bytes(s.out_dim, s.in_dim, nat.RG_F32) for s in self.specs]
+        fmts = (nat.RG_F32, nat.RG_PACK_F32_FAST)
         offs, tot = [], 0
-        for sz in sizes:
-            offs.append(tot)
-            tot += (sz + 255) // 256 * 256
+        for s in self.specs:
+            o = []
+            for f in fmts:
+                o.append(tot)
+                tot += (lib.rg_packed_linear_bytes(s.out_dim, s.in_dim, f) + 255) // 256 * 256
+            offs.append(o)
         self._tbuf = torch.empty(tot, dtype=torch.uint8, device=self.device)
         self._tarr = []
-        for s, off in zip(self.specs, offs):
+        for s, o in zip(self.specs, offs):
             w = s.weight.detach()
-            nat.check(lib.rg_pack_linear(w.data_ptr(), None, s.out_dim, s.in_dim, fmt,
-                                         self._tbuf.data_ptr() + off, st), 'rg_pack_linear')
-            arr = (nat.rg_layer * 1)()
-            arr[0].w_packed = self._tbuf.data_ptr() + off
-            arr[0].in_dim = s.out_dim
-            arr[0].out_dim = s.in_dim
-            arr[0].act = nat.ACT['none']
-            self._tarr.append(arr)
+            pair = []
+            for f, off in zip(fmts, o):
+                nat.check(lib.rg_pack_linear(w.data_ptr(), None, s.out_dim, s.in_dim,
+                                             f | nat.RG_PACK_TRANSPOSE, self._tbuf.data_ptr() + off,
+                                             st), 'rg_pack_linear')
+                arr = (nat.rg_layer * 1)()
+                arr[0].w_packed = self._tbuf.data_ptr() + off
+                arr[0].in_dim = s.out_dim
+                arr[0].out_dim = s.in_dim
+                arr[0].act = nat.ACT['none']
+                pair.append(arr)
+            self._tarr.append(tuple(pair))
         self._tsig = sig
         return self._tarr
+
+    def _dx(self, l: int, rows: int, dZ, out, res):
+        """out = dZ W_l (+ res): the register-resident f32 kernel where it has the shape,
+        else the generic chain kernel."""
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        gen, fast = self._transposed()[l]
+        if TAPE_F32_FAST and self._dx_ok.get(l, True):
+            rc = lib.rg_mlp_chain_f32_ex(fast, 1, rows, None, nat.IN_DENSE, dZ.data_ptr(),
+                                         dZ.stride(0), dZ.shape[1], None, 0, 0, None, 0, 0, None,
+                                         None, nat.ptr(res), res.stride(0) if res is not None else 0,
+                                         out.data_ptr(), out.stride(0), st)
+            if rc == 0:
+                self._dx_ok[l] = True
+                return
+            if rc != nat.RG_ERR_UNSUPPORTED:
+                nat.check(rc, 'rg_mlp_chain_f32_ex (dX = dZ W)')
+            self._dx_ok[l] = False
+        nat.check(lib.rg_mlp_chain(
+            nat.RG_F32, gen, 1, rows, None, nat.IN_DENSE, nat.RG_F32, dZ.data_ptr(),
+            dZ.stride(0), dZ.shape[1], None, 0, 0, None, 0, 0, None, None,
+            nat.ptr(res), res.stride(0) if res is not None else 0, nat.RG_F32,
+            out.data_ptr(), out.stride(0), nat.RG_F32, st), 'rg_mlp_chain (dX = dZ W)')
 
     def _fits_lds(self, layers) -> bool:
         """Whether rg_mlp_chain stages these f32 layers' weights in LDS (its rule:
@@ -255,7 +286,6 @@ class TrainChain:
         rows = tape.rows
         if rows <= 0:
             return
-        tarr = self._transposed()
         dA = d_out
         for l in range(len(self.specs) - 1, -1, -1):
             sp = self.specs[l]
@@ -303,11 +333,7 @@ class TrainChain:
             else:
                 out = torch.empty((rows, sp.in_dim), dtype=torch.float32, device=self.device)
                 res = None
-            nat.check(lib.rg_mlp_chain(
-                nat.RG_F32, tarr[l], 1, rows, None, nat.IN_DENSE, nat.RG_F32, dZ.data_ptr(),
-                dZ.stride(0), sp.out_dim, None, 0, 0, None, 0, 0, None, None,
-                nat.ptr(res), res.stride(0) if res is not None else 0, nat.RG_F32,
-                out.data_ptr(), out.stride(0), nat.RG_F32, st), 'rg_mlp_chain (dX = dZ W)')
+            self._dx(l, rows, dZ, out, res)
             dA = out
 
 
