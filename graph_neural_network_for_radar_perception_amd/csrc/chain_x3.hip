@@ -459,6 +459,11 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
 using namespace rg;
 using namespace rg::cx3;
 
+// enc_x3.hip: the encoders with their weights streamed through an LDS ring
+int rg_enc_ring_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
+                   const float* in0, int ld0, int w0, float* out, int ld_out, int norm_mask,
+                   int act_mask, int centred, void* stream);
+
 extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
                                int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                                const int* idx1, float* out, int ld_out, void* stream) {
@@ -505,6 +510,11 @@ extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, 
     if (layers[l].norm_mu && (layers[l].flags & RG_LAYER_CENTERED)) cm |= 1 << l;
   if (cm != 0 && cm != nm) return RG_ERR_UNSUPPORTED;
   k.sp = spec(nm, am, cm != 0);
+  if (k.mode == IN_SMALL) {
+    const int rc = rg_enc_ring_x3(layers, n_layers, rows, rows_dev, in0, ld0, w0, out, ld_out, nm,
+                                  am, cm != 0, stream);
+    if (rc != RG_ERR_UNSUPPORTED) return rc;
+  }
   a.rows = rows;
   a.rows_dev = rows_dev;
   a.in0 = in0;

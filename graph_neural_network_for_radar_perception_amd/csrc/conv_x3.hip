@@ -119,6 +119,11 @@ static constexpr int NW = FT / 64;
 #ifndef RG_CX3_ENT
 #define RG_CX3_ENT 0  // 1: non-temporal e loads (M: +2.7 %, rejected)
 #endif
+#ifndef RG_CX3_QLATE
+#define RG_CX3_QLATE 0  // 1: layer 1 accumulates onto P[dst] only and Q[src] (the random gather
+                        // from L2 / MALL) is added after its MFMAs, so the gather's latency
+                        // sits behind the 96 layer-1 MFMAs instead of in front of them
+#endif
 #ifndef RG_CX3_WU_LDS
 #define RG_CX3_WU_LDS 0  // W_u staged in LDS too, 4-row passes (M: 0.650 vs 0.638 ms/layer, slower)
 #endif
@@ -492,7 +497,8 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc1[m][4 * g + t] = rw.p[4 * m + g][t] + rw.q[4 * m + g][t];
+          for (int t = 0; t < 4; ++t)
+            acc1[m][4 * g + t] = RG_CX3_QLATE ? rw.p[4 * m + g][t] : rw.p[4 * m + g][t] + rw.q[4 * m + g][t];
       {
         if constexpr (RG_CX3_EXP != 5) {
           layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0,
@@ -502,6 +508,14 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           for (int s = 0; s < 4; ++s)
             acc1[s][0] += xor_first(split8(rw.e[2 * s], rw.e[2 * s + 1]));
         }
+      }
+      if constexpr (RG_CX3_QLATE) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc1[m][4 * g + t] += rw.q[4 * m + g][t];
       }
       STAMP(1);  // gathers + layer 1 issue
 #if RG_CX3_JIT
@@ -949,7 +963,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   auto edge = cent ? conv_x3_kernel<true, NODE> : conv_x3_kernel<false, NODE>;
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
-  RG_LAUNCH_CHECK();
+  RG_LAUNCH_CHECK_ZERO(a.counters, CTR_BYTES, stream);
   if constexpr (!NODE) {
     auto node = cent ? node_x3_kernel<true> : node_x3_kernel<false>;
     RG_ENSURE_LDS(node, NODE_LDS);

@@ -52,6 +52,19 @@ hipError_t ensure_max_lds(const void* kernel, int bytes);
     }                                                                             \
   } while (0)
 
+// a launch whose work counters are re-zeroed by its own last workgroup: when the launch
+// fails, re-zero them on the stream so the next launch on this workspace starts from zero
+#define RG_LAUNCH_CHECK_ZERO(ctr, bytes, stream)                                  \
+  do {                                                                            \
+    hipError_t _e = hipGetLastError();                                            \
+    if (_e != hipSuccess) {                                                       \
+      ::rg::set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__,            \
+                      hipGetErrorString(_e));                                     \
+      (void)hipMemsetAsync((ctr), 0, (bytes), (hipStream_t)(stream));             \
+      return RG_ERR_HIP;                                                          \
+    }                                                                             \
+  } while (0)
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------------------

@@ -714,12 +714,11 @@ class ConvPlan:
             self.fused_layers[0].flags = nat.RG_LAYER_CENTERED   # centred on the host
             self.x3_pq_in = layer_array(specs[3:4], base, offs[3:4], fmts[3:4])
             self.x3_pq_chain = layer_array(specs[4:5], base, offs[4:5], fmts[4:5])
-            self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_x3_workspace_size(0),
-                                        dtype=torch.uint8, device=self.device)
+            self._ws = {}
             self.x3_pq = None   # projections of a standalone run_fused call
         else:
             self.fused_layers = layer_array(specs, base, offs, fmts)
-            self.fused_ws = None
+            self._ws = {}
         self.fused = True
         self.fused_sig = self._sig()
 
@@ -750,13 +749,22 @@ class ConvPlan:
         base = self.fused_buf.data_ptr()
         self.fused_msg = layer_array(specs[:2], base, offs[:2], fmts[:2])
         self.fused_upd = layer_array(specs[2:], base, offs[2:], fmts[2:])
-        self.fused_ws = torch.zeros(nat.lib().rg_conv_layer_workspace_size(), dtype=torch.uint8,
-                                    device=self.device)
+        self._ws = {}
         self.fused = True
         self.fused_sig = self._sig()
 
     def _sig(self):
         return tuple(c._signature() for c in self.chains())
+
+    def workspace(self, need: int, stream: int) -> torch.Tensor:
+        """The fused conv workspace of one HIP stream (zeroed when allocated: its leading
+        work counters must be zero at a launch and each launch's last workgroup re-zeroes
+        them, so two streams never share one)."""
+        ws = self._ws.get(stream)
+        if ws is None or ws.numel() < need:
+            ws = torch.zeros(max(int(need), 1), dtype=torch.uint8, device=self.device)
+            self._ws[stream] = ws
+        return ws
 
     def chains(self):
         return [c for c in (self.msg, self.upd, self.res) if c is not None]
@@ -795,15 +803,14 @@ class ConvPlan:
         """One rg_conv_layer_x3 launch; with nxt (the next ConvPlan, also x3) it also writes
         the next layer's P | Q into pq_out."""
         lib = nat.lib()
-        need = lib.rg_conv_layer_x3_workspace_size(g.n_nodes)
-        if self.fused_ws.numel() < need:
-            self.fused_ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
+        st = nat.stream_ptr(x.device)
+        ws = self.workspace(lib.rg_conv_layer_x3_workspace_size(g.n_nodes), st)
         tbl = g.conv_x3_blocks()
         args = (self.fused_layers, nxt.x3_pq_chain if nxt is not None else None,
                 nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
                 pq.data_ptr(), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
                 x_out.data_ptr(), x_out.stride(0), nat.ptr(pq_out))
-        tail = (self.fused_ws.data_ptr(), self.fused_ws.numel(), nat.stream_ptr(x.device))
+        tail = (ws.data_ptr(), ws.numel(), st)
         if tbl is not None:
             rc = lib.rg_conv_layer_x3_blocks(*args, tbl.data_ptr(), *tail)
         else:
@@ -833,14 +840,12 @@ class ConvPlan:
         if self.dtype == 'fp32':
             if x.dtype != torch.float32 or e.dtype != torch.float32:
                 return False
-            need = lib.rg_conv_layer_f32_workspace_size(g.n_nodes)
-            if self.fused_ws is None or self.fused_ws.numel() < need:
-                self.fused_ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            st = nat.stream_ptr(x.device)
+            ws = self.workspace(lib.rg_conv_layer_f32_workspace_size(g.n_nodes), st)
             rc = lib.rg_conv_layer_f32(
                 self.fused_layers, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(),
                 e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
-                x_out.data_ptr(), x_out.stride(0), self.fused_ws.data_ptr(),
-                self.fused_ws.numel(), nat.stream_ptr(x.device))
+                x_out.data_ptr(), x_out.stride(0), ws.data_ptr(), ws.numel(), st)
             if rc == nat.RG_ERR_UNSUPPORTED:
                 self.fused_ok = False
                 return False
@@ -848,11 +853,13 @@ class ConvPlan:
             self.fused_ok = True
             return True
         tbl, nb = g.conv_blocks()
+        st = nat.stream_ptr(x.device)
+        ws = self.workspace(lib.rg_conv_layer_workspace_size(), st)
         rc = lib.rg_conv_layer_fused_blocks(
             self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),
             e.data_ptr(), e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
             g.n_nodes, x_out.data_ptr(), x_out.stride(0), nat.ptr(tbl), nat.ptr(nb),
-            self.fused_ws.data_ptr(), nat.stream_ptr(x.device))
+            ws.data_ptr(), st)
         if rc == nat.RG_ERR_UNSUPPORTED:
             self.fused_ok = False
             return False

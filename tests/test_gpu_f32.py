@@ -112,6 +112,43 @@ def test_f32_chain_rows_dev_and_empty(cuda_device):
     plan(0, out[:0], x[:0], 7)
 
 
+@pytest.mark.parametrize('R', [1, 3001, 140_000])
+def test_x3_encoder_ring_bit_identical(cuda_device, R, monkeypatch):
+    """The encoders with their weights streamed through an LDS ring (enc_x3.hip, the default
+    for the yml encoder shapes) are bit-identical to the register-resident chain_x3 encoders
+    (same products, same summation order per output) -- one row, a partial pass and several
+    passes per workgroup -- and match a float64 evaluation at 1e-4; rows_dev bounds the
+    rows written."""
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    dev = cuda_device
+    torch.manual_seed(11)
+    m = Model_Training(default_config(), dev).to(dev).eval().requires_grad_(False)
+    plans = m.pred.plans('fp32')
+    g = torch.Generator(device='cpu').manual_seed(R)
+    for plan, w in ((plans.node_enc, 6), (plans.edge_enc, 7)):
+        x = (torch.randn(R, w, generator=g) * 2).to(dev)
+        outs = []
+        for ring in ('1', '0'):
+            monkeypatch.setenv('RG_X3_RING', ring)
+            plan.x3_ok = {}
+            out = torch.full((R, plan.out_dim), float('nan'), device=dev)
+            plan(R, out, x, w)
+            assert plan.x3_ok.get(0), 'x3 encoder not used'
+            outs.append(out)
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+        sel = torch.arange(0, R, max(1, R // 4000), device=dev)
+        torch.testing.assert_close(outs[0][sel], _torch_chain64(plan, x[sel]).float(), **FP32_TOL)
+        monkeypatch.setenv('RG_X3_RING', '1')
+        if R > 1:
+            n = torch.tensor([R // 2 + 5], dtype=torch.int32, device=dev)
+            out = torch.full((R, plan.out_dim), 7.0, device=dev)
+            plan(R, out, x, w, rows_dev=n)
+            assert torch.equal(out[:R // 2 + 5], outs[1][:R // 2 + 5])
+            assert bool((out[R // 2 + 5:] == 7.0).all())
+
+
 def _graph(dev, sizes, k, seed0, cfg):
     from graph_neural_network_for_radar_perception_amd import synthetic
     from graph_neural_network_for_radar_perception_amd import graph_features as gf
