@@ -119,6 +119,10 @@ static constexpr int NW = FT / 64;
 #ifndef RG_CX3_ENT
 #define RG_CX3_ENT 0  // 1: non-temporal e loads (M: +2.7 %, rejected)
 #endif
+#ifndef RG_CX3_MO
+#define RG_CX3_MO 0  // bit 0: message layer 1, bit 1: layer 2 issued M-tile by M-tile (layer_x3_mo:
+                     // 24 registers of A fragments instead of 48; bit-identical)
+#endif
 #ifndef RG_CX3_QLATE
 #define RG_CX3_QLATE 0  // 1: layer 1 accumulates onto P[dst] only and Q[src] (the random gather
                         // from L2 / MALL) is added after its MFMAs, so the gather's latency
@@ -501,8 +505,11 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
             acc1[m][4 * g + t] = RG_CX3_QLATE ? rw.p[4 * m + g][t] : rw.p[4 * m + g][t] + rw.q[4 * m + g][t];
       {
         if constexpr (RG_CX3_EXP != 5) {
-          layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0,
-                                        [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
+          if constexpr (RG_CX3_MO & 1)
+            layer_x3_mo<4, 4>(acc1, wE, 0, [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
+          else
+            layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0,
+                                          [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
         } else {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
@@ -531,8 +538,11 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
       if constexpr (RG_CX3_EXP != 5) {
 #if RG_CX3_JIT
-        layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0,
-                                      [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
+        if constexpr ((RG_CX3_MO & 2) != 0)
+          layer_x3_mo<8, 2>(acc2, w2, 0, [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
+        else
+          layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0,
+                                        [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
 #else
         layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0, [&](int s) { return split_acc(acc1[s >> 1], s & 1); });
 #endif

@@ -236,6 +236,40 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// The same products in the same order per accumulator as layer_x3 (one row tile), issued
+// M-tile by M-tile: the six MFMAs of tile m chain on acc[m] back to back, and only two
+// M-tiles' A fragments are live (the next tile's three are read while the current tile's
+// MFMAs run: 24 registers instead of MT * 12).  Bit-identical to layer_x3.
+template <int KS, int MT, typename WSrc, typename BOp>
+__device__ __forceinline__ void layer_x3_mo(f32x16 (&acc)[MT], const WSrc& W, int m0, BOp&& bop) {
+  auto lda = [&](int s, int m, bf16x8_t (&d)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) d[p] = W(p, ((m0 + m) * KS + s) * 1024);
+  };
+  X3 bq = bop(0);
+  bf16x8_t A[2][3];
+  lda(0, 0, A[0]);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    X3 bn;
+    if (s + 1 < KS) bn = bop(s + 1);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int u = (s * MT + m) & 1;
+      if (m + 1 < MT) lda(s, m + 1, A[u ^ 1]);
+      else if (s + 1 < KS) lda(s + 1, 0, A[u ^ 1]);
+      acc[m] = mf(A[u][2], bq.p0, acc[m]);
+      acc[m] = mf(A[u][1], bq.p1, acc[m]);
+      acc[m] = mf(A[u][0], bq.p2, acc[m]);
+      acc[m] = mf(A[u][1], bq.p0, acc[m]);
+      acc[m] = mf(A[u][0], bq.p1, acc[m]);
+      acc[m] = mf(A[u][0], bq.p0, acc[m]);
+    }
+    if (s + 1 < KS) bq = bn;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // one row tile
 template <int KS, int MT, int MTW, int DB = 0, typename WSrc, typename BOp>
 __device__ __forceinline__ void layer_x3(f32x16 (&acc)[MT], const WSrc& W, int m0, BOp&& bop) {
