@@ -123,6 +123,10 @@ static constexpr int NW = FT / 64;
 #define RG_CX3_MO 0  // bit 0: message layer 1, bit 1: layer 2 issued M-tile by M-tile (layer_x3_mo:
                      // 24 registers of A fragments instead of 48; bit-identical)
 #endif
+#ifndef RG_CX3_RESREG
+#define RG_CX3_RESREG 1  // the update's residual x[node] from the rows in registers
+                         // (v_permlane32_swap) instead of a second load of x (M: flat, -0.3 %)
+#endif
 #ifndef RG_CX3_QLATE
 #define RG_CX3_QLATE 0  // 1: layer 1 accumulates onto P[dst] only and Q[src] (the random gather
                         // from L2 / MALL) is added after its MFMAs, so the gather's latency
@@ -267,6 +271,25 @@ __device__ __forceinline__ void node_compute(const Args& a, const NodeRows& w, i
     return s < 4 ? split8(w.xb[s][0], w.xb[s][1]) : split8(ab[s - 4][0], ab[s - 4][1]);
   });
   norm_leaky<2, CENT>(accu, muU, sdU);
+#if RG_CX3_RESREG
+  {
+    // the residual x[node] in accumulator order (features 32 m + 8 g + 4 h + t) from the
+    // k-order rows already in registers (features 16 s + 8 h + 4 u + t): the value lives in
+    // lane half g & 1 at xb[2 m + (g >> 1)][h].  v_permlane32_swap(vdst = xb[s][0],
+    // src = xb[s][1]) swaps vdst's lanes 32-63 with src's lanes 0-31, which leaves every
+    // lane's even-g value in the new vdst and its odd-g value in the new src -- no reload
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.xb[s][0][t]),
+                                                         __float_as_uint(w.xb[s][1][t]), false, false);
+        const int m = s >> 1, g0 = 2 * (s & 1);
+        accu[m][4 * g0 + t] = __fadd_rn(__uint_as_float(sw[0]), accu[m][4 * g0 + t]);
+        accu[m][4 * (g0 + 1) + t] = __fadd_rn(__uint_as_float(sw[1]), accu[m][4 * (g0 + 1) + t]);
+      }
+  }
+#else
   {
     const float* pxr = a.x + (size_t)nrow * a.ldx + 4 * h;  // x[node] in accumulator order
 #pragma unroll
@@ -280,6 +303,7 @@ __device__ __forceinline__ void node_compute(const Args& a, const NodeRows& w, i
         accu[m][4 * g + 3] = __fadd_rn(xr.w, accu[m][4 * g + 3]);
       }
   }
+#endif
   if (nvalid) {
     float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
 #pragma unroll

@@ -31,9 +31,11 @@ typedef __attribute__((address_space(3))) void* lds_as3;
 
 static constexpr int SLOT = 24 * 1024;  // one chunk
 #ifndef RG_ENC_NSLOT
-#define RG_ENC_NSLOT 2
+#define RG_ENC_NSLOT 3  // 3: chunk q + 1 is already visible while chunk q is consumed, so the
+                        // first fragments of the next chunk are read before its boundary
 #endif
 static constexpr int NSLOT = RG_ENC_NSLOT;
+static constexpr bool XPF = NSLOT >= 3;  // cross-chunk fragment prefetch
 
 constexpr int spec(int norm_mask, int act_mask, bool centred) {
   return norm_mask | (act_mask << 8) | (centred ? 1 << 16 : 0);
@@ -88,6 +90,7 @@ struct Ring {
   const char* w[S::NL];  // the layers' x3 images
   char* lds;
   const char* slot;  // current chunk's slot + lane * 16
+  const char* nslot; // the next chunk's slot + lane * 16 (visible when XPF)
   long q;            // next chunk to consume
   long total;        // chunks this workgroup consumes
   int wave, lane;
@@ -120,24 +123,31 @@ struct Ring {
       __builtin_amdgcn_global_load_lds((const void*)g, (lds_as3)(dst + b * 1024), 16, 0, 0);
     }
   }
-  // chunk boundary: this wave's copies of the chunk are complete (vmcnt 0), the barrier
-  // makes every wave's copies visible and frees the slot of the chunk before (every wave
-  // is past it); then the next chunk's copy is issued.  hook() runs between the barrier and
-  // the issue (register work whose loads must not wait for the new copies), after() behind it.
+  // chunk boundary of chunk q: this wave's copies issued so far are complete (vmcnt 0: chunk
+  // q + NSLOT - 2, which makes chunk q ready with two slots and q + 1 ready with three), the
+  // barrier makes every wave's copies visible and frees the slot of chunk q - 1 (every wave
+  // is past it); then chunk q + NSLOT - 1 is issued into that slot.  hook() runs between the
+  // barrier and the issue (register work whose loads must not wait for the new copies),
+  // after() behind it.
   template <typename Hook, typename After>
   __device__ __forceinline__ void begin(Hook&& hook, After&& after) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     hook();
-    issue(q + 1);
+    issue(q + NSLOT - 1);
     after();
     slot = lds + (int)(q % NSLOT) * SLOT + lane * 16;
+    nslot = lds + (int)((q + 1) % NSLOT) * SLOT + lane * 16;
     ++q;
   }
-  // fragment (k-step j of the chunk, M-tile m, plane p)
+  // fragment (k-step j of the chunk, M-tile m, plane p) of the current / the next chunk
   template <int MT>
   __device__ __forceinline__ bf16x8_t frag(int j, int m, int p) const {
     return ld_bf8(slot + ((j * MT + m) * 3 + p) * 1024);
+  }
+  template <int MT>
+  __device__ __forceinline__ bf16x8_t frag_next(int j, int m, int p) const {
+    return ld_bf8(nslot + ((j * MT + m) * 3 + p) * 1024);
   }
 };
 
@@ -210,16 +220,23 @@ __device__ __forceinline__ void run_rest(Ring<S, W>& ring, const f32x16 (&prev)[
       } else {
         ring.begin(Nop{}, Nop{});
       }
+      if (s == 0 || !XPF) {  // else read during the previous chunk's last k-step
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) Ab[s & 1][m][p] = ring.template frag<MT>(j, m, p);
+          for (int p = 0; p < 3; ++p) Ab[s & 1][m][p] = ring.template frag<MT>(j, m, p);
+      }
     }
     if (j + 1 < KPC) {  // the next k-step's fragments from the same slot
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int p = 0; p < 3; ++p) Ab[(s + 1) & 1][m][p] = ring.template frag<MT>(j + 1, m, p);
+    } else if (XPF && s + 1 < KS) {  // the next chunk's first k-step (visible already)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) Ab[(s + 1) & 1][m][p] = ring.template frag_next<MT>(0, m, p);
     }
     X3 bn[RT];
     if (s + 1 < KS) {
@@ -298,12 +315,14 @@ __global__ __launch_bounds__(64 * W) void enc_ring_kernel(Args a) {
   for (int l = 0; l < NL; ++l) ring.w[l] = a.w[l];
   ring.lds = lds;
   ring.slot = lds;
+  ring.nslot = lds;
   ring.q = 0;
   ring.total = my_pass * NCH;
   ring.wave = wave;
   ring.lane = lane;
   __syncthreads();  // the resident images are staged
-  ring.issue(0);
+#pragma unroll
+  for (int i = 0; i + 1 < NSLOT; ++i) ring.issue(i);
   const WLds W0{lds + S::W0_OFF + lane * 16, S::pl(0)};
 
   // the next pass's inputs (lane r = row; lanes h = 0 hold the <= 8 features)
@@ -351,6 +370,7 @@ __global__ __launch_bounds__(64 * W) void enc_ring_kernel(Args a) {
     for (int t = 0; t < RT; ++t)
 #pragma unroll
       for (int m = 0; m < MT1; ++m) acc1[t][m] = ld_bias_frag(bias1, m, h);
+    bf16x8_t An[MT1][3];  // XPF: the next chunk's first-k-step fragments
 #pragma unroll
     for (int m0 = 0; m0 < MT0; ++m0) {
       if (m0 == 0) {
@@ -369,7 +389,8 @@ __global__ __launch_bounds__(64 * W) void enc_ring_kernel(Args a) {
 #pragma unroll
       for (int m = 0; m < MT1; ++m)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) A[0][m][p] = ring.template frag<MT1>(0, m, p);
+        for (int p = 0; p < 3; ++p)
+          A[0][m][p] = (XPF && m0 > 0) ? An[m][p] : ring.template frag<MT1>(0, m, p);
       f32x16 y[RT][1];
 #pragma unroll
       for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
@@ -386,6 +407,12 @@ __global__ __launch_bounds__(64 * W) void enc_ring_kernel(Args a) {
         for (int p = 0; p < 3; ++p) A[1][m][p] = ring.template frag<MT1>(1, m, p);
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
+        if (XPF && hf == 1 && m0 + 1 < MT0) {  // the next chunk's first k-step (visible)
+#pragma unroll
+          for (int m = 0; m < MT1; ++m)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) An[m][p] = ring.template frag_next<MT1>(0, m, p);
+        }
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
           const X3 b = split_acc(y[t][0], hf);

@@ -106,3 +106,19 @@ def classifier_samples(d):
                  osz=torch.from_numpy(d[f's{i}/object_size']),
                  gt=torch.from_numpy(d[f's{i}/object_class']),
                  logits=d[f's{i}/logits']) for i in range(n)]
+
+
+def grad_within_f32_bound(ours: float, orc: float) -> bool:
+    """Per-tensor gradient bound against a float64 evaluation of the same model:
+    ours = max|g - g64| / max|g64| of the GPU gradient, orc = the same for the float32 oracle.
+
+    ours <= max(10 orc, 2e-4): at least as close to float64 as float32 allows, with the floor
+    of the reference's own training-step fixture (2e-4 of max|g|,
+    test_gpu_training.py::test_training_steps_match_reference) -- gradients through the
+    cluster max-pool route to the maximal node, and a near-tie (~1e-7 relative) resolved
+    differently by two float32 evaluations moves one node's contribution (measured: 1.5e-4
+    on the first node-encoder weight, 1e-6 for the oracle's own evaluation order);
+    ours <= max(1e-2, 2 orc): an absolute cap, except on tensors where float32 itself is
+    worse (the norm mu / std parameter gradients are sums over every row and feature with
+    heavy cancellation: the float32 oracle is 2e-2 .. 2e-1 off float64 on some of them)."""
+    return ours <= max(10 * orc, 2e-4) and ours <= max(1e-2, 2 * orc)
