@@ -229,6 +229,20 @@ __device__ __forceinline__ void run_first(const Args& a, const X3 (&b0)[RT][KS0]
   }
 }
 
+#ifndef RG_X3_K0SLOT
+#define RG_X3_K0SLOT 0  // encoders' layer 0 (<= 8 inputs) as 3 MFMAs instead of 6 (slot packing)
+#endif
+// Layer 0 of <= 8 inputs fills only half of a 16-deep k-step, so the six products of the
+// x3 form fit three MFMAs when the lane halves carry different terms: lanes h = 0 hold
+// (w_p, b_0) and lanes h = 1 (w_q, b_r) for k = 0..7 of the same row, with
+// (p | q, r) = (0 | 0, 1), (1 | 0, 2), (2 | 1, 1): a0 b0 + a0 b1, a1 b0 + a0 b2, a2 b0 + a1 b1.
+// A: plane P0[f] (h = 0) / P1[f] (h = 1) of the x3 image's k = 0..7 half (lane & 31 of the
+// fragment); B: the row's split, plane 0 (h = 0) / Q1[f] (h = 1).
+__device__ __forceinline__ bf16x8_t k0slot_b(const X3& x, int f, int h) {
+  const bf16x8_t hi = f == 1 ? x.p2 : x.p1;
+  return h ? hi : x.p0;
+}
+
 // encoders: layer 0 (one k-step of <= 8 inputs, no normalisation) fused tile by tile into
 // layer 1: tile m0 of layer 0 is layer 1's k-steps 2 m0 and 2 m0 + 1
 template <typename S, int SPEC, int LM, int RT>
@@ -267,7 +281,24 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
     f32x16 y[RT][1];
 #pragma unroll
     for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
-    layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
+    if constexpr (RG_X3_K0SLOT) {
+      static_assert(lmask(LM, 0) == 7, "slot layer 0 reads every plane from LDS");
+      const char* w0l = lds + S::woff(LM, 0) + m0 * 1024 + (lane & 31) * 16;
+      bf16x8_t A0[3];
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const int pl = h ? (f == 2 ? 1 : 0) : f;
+        A0[f] = ld_bf8(w0l + pl * S::pl(0));
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        y[t][0] = mf(A0[2], k0slot_b(b0[t][0], 2, h), y[t][0]);
+        y[t][0] = mf(A0[1], k0slot_b(b0[t][0], 1, h), y[t][0]);
+        y[t][0] = mf(A0[0], k0slot_b(b0[t][0], 0, h), y[t][0]);
+      }
+    } else {
+      layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
+    }
     if constexpr (sp_act(SPEC, 0)) {
 #pragma unroll
       for (int t = 0; t < RT; ++t)
@@ -356,7 +387,8 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
         const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (ok && h == 0 && j < a.w0real) ? p[j] : 0.f;
+        // both lane halves hold the row with RG_X3_K0SLOT (each carries other split terms)
+        for (int j = 0; j < 8; ++j) v[j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
         b0[t][0] = split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]});
       } else if constexpr (MODE == IN_DENSE) {
         const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 8 * h;
