@@ -237,3 +237,48 @@ def test_setup_dist_checks_world_and_gathers_counts(tmp_path):
         d = np.load(tmp_path / f'wc{r}.npz')
         assert bool(d['ok'])
         np.testing.assert_array_equal(d['counts'], [10, 20])
+
+
+_RCCL_PROBE = r'''
+import os, sys, json
+import torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+from graph_neural_network_for_radar_perception_amd import training
+torch.cuda.set_device(0)
+dist.init_process_group('nccl', world_size=1, rank=0)
+assert dist.get_backend() == 'nccl'
+# the training step's one flat-gradient bucket (training.allreduce_gradients) and the
+# construction-time broadcast, on device tensors through RCCL
+flat = torch.linspace(-1.0, 1.0, 463144, device='cuda')
+ref = flat.clone()
+dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+training.broadcast_parameters(flat, 1)
+dist.broadcast(flat, 0)
+# bench.py's timing reductions (max / sum over ranks of a device scalar) and its barrier
+t = torch.tensor([3.5], dtype=torch.float64, device='cuda')
+dist.all_reduce(t, op=dist.ReduceOp.MAX)
+dist.barrier()
+torch.cuda.synchronize()
+print(json.dumps({'equal': bool(torch.equal(flat, ref)), 'max': float(t.item()),
+                  'rccl': torch.cuda.nccl.version() if hasattr(torch.cuda, 'nccl') else None}))
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_collectives_on_device(cuda_device):
+    """The RCCL ('nccl' backend) branch of the multi-GPU path on the hardware: a one-rank
+    process group initialises on the MI355X and the collectives the data path uses -- the
+    flat-gradient all-reduce of training.allreduce_gradients, the parameter broadcast, the
+    bench's max-over-ranks and barrier -- run on device tensors (sum / max over one rank is
+    the identity).  Multi-rank RCCL needs one card per rank (the driver's 8-GPU run)."""
+    import json
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()),
+               WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    r = subprocess.run([sys.executable, '-c', _RCCL_PROBE, REPO], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    assert out['equal'] and out['max'] == 3.5, out
