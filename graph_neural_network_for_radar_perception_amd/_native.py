@@ -33,7 +33,7 @@ RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
 GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2
 REDUCE = {'add': 0, 'sum': 0, 'mean': 1, 'max': 2}
-IN_DENSE, IN_CONCAT2, IN_GATHER3, IN_PAIRADD = 0, 1, 2, 3
+IN_DENSE, IN_CONCAT2, IN_GATHER3, IN_PAIRADD, IN_PAIRPRE = 0, 1, 2, 3, 4
 MAX_LAYERS = 8
 
 

@@ -30,7 +30,9 @@ using namespace ::rg::x3;
 
 enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused into layer 1
        IN_DENSE = 1,   // float32 rows, K0 % 16 == 0
-       IN_PAIR = 2 };  // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
+       IN_PAIR = 2,    // float32 x[idx0[r]] + x[idx1[r]] (edge_formation, gnn_blocks.py:297)
+       IN_PAIRPRE = 3 };  // layer 0's pre-activation t[idx0[r]] + t[idx1[r]] + b0 from per-node
+                          // rows t = W0 x (RG_IN_PAIRPRE: layer 0's weights are not read)
 
 // SPEC: bit l = layer l normalised, bit 8 + l = activated (LeakyReLU), bit 16 = every
 // normalised layer packed centred (RG_LAYER_CENTERED)
@@ -229,6 +231,43 @@ __device__ __forceinline__ void run_first(const Args& a, const X3 (&b0)[RT][KS0]
   }
 }
 
+// RG_IN_PAIRPRE: layer 0 is linear before its norm, W0 (x_i + x_j) + b0 = t_i + t_j + b0 with
+// t = W0 x per NODE (rg_mlp_chain_x3 over the nodes, a bare last layer): the pair chain starts
+// from the gathered sum -- no layer-0 MFMAs and no split of the pair input (the link head's
+// pairs outnumber the nodes ~6x)
+template <typename S, int SPEC, int LM, int RT>
+__device__ __forceinline__ void run_pre(const Args& a, const char* lds, const float* nrm, long row0,
+                                        long rows, int lane) {
+  constexpr int N = S::N[0], MT = N / 32;
+  static_assert(S::K(0) == N, "per-node rows t have layer 0's output width");
+  const int r = lane & 31, h = lane >> 5;
+  const float* bias = (const float*)(lds + S::boff(LM, 0));
+  f32x16 acc[RT][MT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const long row = row0 + 32 * t + r;
+    const bool ok = row < rows;
+    const int i = ok ? a.idx0[row] : 0, j = ok ? a.idx1[row] : 0;
+    const float* pi = a.in0 + (size_t)i * a.ld0 + 4 * h;
+    const float* pj = a.in0 + (size_t)j * a.ld0 + 4 * h;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const f32x16 b = ld_bias_frag(bias, m, h);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 ti = *(const f32x4*)(pi + 32 * m + 8 * g);
+        const f32x4 tj = *(const f32x4*)(pj + 32 * m + 8 * g);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[t][m][4 * g + u] = __fadd_rn(__fadd_rn(ti[u], tj[u]), b[4 * g + u]);
+      }
+    }
+  }
+  static_assert(S::NL > 1, "a pair chain continues after layer 0");
+  Pend pn[RT];
+  epilogue_pend<SPEC, 0, MT, RT>(acc, nrm, pn);
+  run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
+}
+
 #ifndef RG_X3_K0SLOT
 #define RG_X3_K0SLOT 0  // encoders' layer 0 (<= 8 inputs) as 3 MFMAs instead of 6 (slot packing)
 #endif
@@ -343,7 +382,7 @@ template <int MODE, int SPEC, int LM, int RT, int FT, int K0, int... Ns>
 __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
   using S = Shape<K0, Ns...>;
   constexpr int NL = S::NL;
-  constexpr int KS0 = MODE == IN_SMALL ? 1 : K0 / 16;
+  constexpr int KS0 = (MODE == IN_SMALL || MODE == IN_PAIRPRE) ? 1 : K0 / 16;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[2 * RG_MAX_LAYERS];
   if (threadIdx.x == 0) {
@@ -378,6 +417,9 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
   const long tstride = (long)gridDim.x * (FT / 64);
   for (long tile = (long)blockIdx.x * (FT / 64) + wave; tile < ntiles; tile += tstride) {
     const long row0 = tile * TROWS;
+    if constexpr (MODE == IN_PAIRPRE) {
+      run_pre<S, SPEC, LM, RT>(a, lds, nrm, row0, rows, lane);
+    } else {
     X3 b0[RT][KS0];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -417,6 +459,7 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
       run_fused01<S, SPEC, LM, RT>(a, b0, lds, nrm, row0, rows, lane);
     else
       run_first<S, SPEC, LM, RT, KS0>(a, b0, lds, nrm, row0, rows, lane);
+    }
   }
 }
 
@@ -476,6 +519,12 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   constexpr int HFT = RG_X3_HEAD_RT == 1 ? 512 : 256;
   RG_X3C2(IN_DENSE, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
   RG_X3C2(IN_PAIR, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
+  // the same link chain from per-node pre-projections (layer 0's planes are not staged), and
+  // the per-node rows t: the compute_edge stem block + the bare layer 0 of the pair chain, or
+  // the bare layer alone (no stem)
+  RG_X3C2(IN_PAIRPRE, 64, 0b1111, 0b1111, ALL & ~07, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
+  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, 512, 64, 64)
+  RG_X3C2(IN_DENSE, 64, 0, 0, ALL, 1, 512, 64)
   // link edge_formation stem (1 block), object-class stem (3 blocks), object head
   RG_X3C2(IN_DENSE, 64, 0b1, 0b1, ALL, 1, 512, 64)
   RG_X3C2(IN_DENSE, 64, 0b111, 0b111, ALL, 1, 512, 64, 64, 64)
@@ -500,8 +549,10 @@ extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, 
                                int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                                const int* idx1, float* out, int ld_out, void* stream) {
   RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_x3: n_layers");
-  RG_REQUIRE(in_mode != RG_IN_PAIRADD || (idx0 && idx1), RG_ERR_ARG,
-             "rg_mlp_chain_x3: RG_IN_PAIRADD needs idx0 and idx1");
+  RG_REQUIRE((in_mode != RG_IN_PAIRADD && in_mode != RG_IN_PAIRPRE) || (idx0 && idx1), RG_ERR_ARG,
+             "rg_mlp_chain_x3: RG_IN_PAIRADD / RG_IN_PAIRPRE need idx0 and idx1");
+  RG_REQUIRE(in_mode != RG_IN_PAIRPRE || (w0 == layers[0].out_dim && ld0 % 4 == 0), RG_ERR_ARG,
+             "rg_mlp_chain_x3: RG_IN_PAIRPRE rows have layer 0's output width (stride % 4)");
   Key k;
   memset(&k, 0, sizeof(k));
   Args a;
@@ -512,6 +563,8 @@ extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, 
     k.mode = IN_DENSE;
   else if (in_mode == RG_IN_PAIRADD)
     k.mode = IN_PAIR;
+  else if (in_mode == RG_IN_PAIRPRE)
+    k.mode = IN_PAIRPRE;
   else
     return RG_ERR_UNSUPPORTED;
   RG_REQUIRE(k.mode == IN_SMALL || (w0 % 16 == 0 && ld0 % 4 == 0), RG_ERR_UNSUPPORTED,

@@ -50,6 +50,8 @@ def _half_flag(dtype: str) -> int:
 # layer's projections fused into the update); 'mfma_f32' = v_mfma_f32_32x32x2_f32
 # (rg_conv_layer_f32).  Both keep float32 accuracy (tests/test_gpu_f32.py runs both).
 F32_ARITH = os.environ.get('RG_F32_ARITH', 'x3')
+# fp32 link head with its first Linear per node (ModelPlans.link_pairs_pre); '0' = per pair
+LINK_PRE = os.environ.get('RG_LINK_PRE', '1') != '0'
 # x3 conv over the per-graph work-block table (rg_conv_x3_blocks: LPT order, 8-node tail);
 # '0' = plain 32-node runs (same results)
 CONV_X3_TABLE = os.environ.get('RG_CONV_X3_TABLE', '1') != '0'
@@ -887,18 +889,52 @@ class ModelPlans:
         self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
         # layer / group normalisation anywhere: chains need each frame's row ranges
         self.frame_norm = any(c.has_frame_norm for c in self.chains())
+        # fp32 link head: the pair chain's first Linear is applied per NODE (t = W0 s, a bare
+        # last layer after the compute_edge stem) and the pairs start from t_i + t_j + b0
+        # (RG_IN_PAIRPRE, link_pairs_pre); None: the pairs run the whole chain (RG_IN_PAIRADD)
+        self.link_pre = None
+        first = self.link_pair.specs[0]
+        if (dtype == 'fp32' and LINK_PRE and not self.frame_norm and first.mu is not None
+                and len(self.link_pair.specs) > 1):
+            bare = LayerSpec(first.weight, None, None, None, 'none')
+            stem = list(self.link_node.specs) if self.link_node is not None else []
+            self.link_pre = ChainPlan(stem + [bare], dtype, device)
 
     def chains(self):
         out = [self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
                self.cls_head]
-        out += [c for c in (self.link_node, self.cls_stem) if c is not None]
+        out += [c for c in (self.link_node, self.cls_stem, getattr(self, 'link_pre', None))
+                if c is not None]
         for cv in self.convs:
             out += cv.chains()
         return out
 
+    def link_pairs_pre(self, N, x, C, ucap, link, g) -> bool:
+        """The link head through RG_IN_PAIRPRE: t = [stem ->] W0 x per node, then the pair
+        chain from t[i] + t[j] + b0 (gnn_blocks.py:292-297, 340-344: W0 (s_i + s_j) + b0 =
+        W0 s_i + W0 s_j + b0).  False when the x3 kernels have no instantiation for it."""
+        lp, pair = self.link_pre, self.link_pair
+        if lp is None or lp.x3_ok.get('pre') is False:
+            return False
+        t = torch.empty((max(N, 1), lp.out_dim), dtype=torch.float32, device=x.device)
+        lp(N, t, x, C)
+        if not lp.x3_ok.get(nat.IN_DENSE):
+            lp.x3_ok['pre'] = False
+            return False
+        lib = nat.lib()
+        rc = lib.rg_mlp_chain_x3(pair._x3_layers(), len(pair.specs), int(ucap),
+                                 nat.ptr(g.n_pairs_dev), nat.IN_PAIRPRE, t.data_ptr(), t.stride(0),
+                                 lp.out_dim, g.pair_src.data_ptr(), g.pair_dst.data_ptr(),
+                                 link.data_ptr(), link.stride(0), nat.stream_ptr(x.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            lp.x3_ok['pre'] = False
+            return False
+        nat.check(rc, 'rg_mlp_chain_x3 (RG_IN_PAIRPRE)')
+        return True
+
     def refresh(self):
         for c in (self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
-                  self.cls_head, self.link_node, self.cls_stem):
+                  self.cls_head, self.link_node, self.cls_stem, self.link_pre):
             if c is not None:
                 c.refresh()
         for cv in self.convs:
@@ -906,7 +942,7 @@ class ModelPlans:
 
     def invalidate(self):
         for c in (self.node_enc, self.edge_enc, self.node_head, self.offset_head, self.link_pair,
-                  self.cls_head, self.link_node, self.cls_stem):
+                  self.cls_head, self.link_node, self.cls_stem, self.link_pre):
             if c is not None:
                 c.invalidate()
         for cv in self.convs:
@@ -1069,16 +1105,17 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
     plans.node_head(N, node_cls, x, C, segs=segs('node'))
     node_reg = torch.empty((N, plans.offset_head.out_dim), dtype=f32, device=dev)
     plans.offset_head(N, node_reg, x, C, segs=segs('node'))
-    if plans.link_node is not None:
-        s = alloc('link_s', (N, plans.link_node.out_dim), T)
-        plans.link_node(N, s, x, C, segs=segs('node'))
-    else:
-        s = x
     ucap = n_pairs_cap if n_pairs_cap is not None else (g.n_pairs if g.n_pairs is not None
                                                         else g.pair_src.shape[0])
     link = torch.empty((ucap, plans.link_pair.out_dim), dtype=f32, device=dev)
-    plans.link_pair(ucap, link, s, s.shape[1], mode=nat.IN_PAIRADD, idx0=g.pair_src,
-                    idx1=g.pair_dst, rows_dev=g.n_pairs_dev, segs=segs('pair'))
+    if not (x.dtype == f32 and plans.link_pairs_pre(N, x, C, ucap, link, g)):
+        if plans.link_node is not None:
+            s = alloc('link_s', (N, plans.link_node.out_dim), T)
+            plans.link_node(N, s, x, C, segs=segs('node'))
+        else:
+            s = x
+        plans.link_pair(ucap, link, s, s.shape[1], mode=nat.IN_PAIRADD, idx0=g.pair_src,
+                        idx1=g.pair_dst, rows_dev=g.n_pairs_dev, segs=segs('pair'))
     if plans.cls_stem is not None:
         h = alloc('cls_h', (N, plans.cls_stem.out_dim), T)
         plans.cls_stem(N, h, x, C, segs=segs('node'))

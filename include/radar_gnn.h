@@ -96,6 +96,9 @@ extern "C" {
 #define RG_IN_GATHER3 2 /* row r <- cat(in0[idx0[r]], in0[idx1[r]], in2[r])
                            = cat(x_i, x_j, e) of MessagePassing.message, gnn_blocks.py:113 */
 #define RG_IN_PAIRADD 3 /* row r <- in0[idx0[r]] + in0[idx1[r]]  gnn_blocks.py:297   */
+#define RG_IN_PAIRPRE 4 /* rg_mlp_chain_x3 only: layer 0's pre-activation <- in0[idx0[r]] +
+                           in0[idx1[r]] + b0, in0 = per-node rows W0 x (layer 0 is linear
+                           before its norm, gnn_blocks.py:292-297); layer 0's weights unread */
 
 const char* rg_last_error(void);
 int rg_version(void);

@@ -114,8 +114,8 @@ def test_f32_chain_rows_dev_and_empty(cuda_device):
 
 @pytest.mark.parametrize('R', [1, 3001, 140_000])
 def test_x3_encoder_ring_bit_identical(cuda_device, R, monkeypatch):
-    """The encoders with their weights streamed through an LDS ring (enc_x3.hip, the default
-    for the yml encoder shapes) are bit-identical to the register-resident chain_x3 encoders
+    """The encoders with their weights streamed through an LDS ring (enc_x3.hip,
+    RG_X3_RING=1; measured slower, off by default) are bit-identical to the register-resident chain_x3 encoders
     (same products, same summation order per output) -- one row, a partial pass and several
     passes per workgroup -- and match a float64 evaluation at 1e-4; rows_dev bounds the
     rows written."""
@@ -497,3 +497,33 @@ def test_generic_chain_f32x3_matches_f32(cuda_device):
     ref = (dz.double() @ ws[0].double()).float()
     for dx in outs:
         assert float((dx - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+
+
+def test_link_head_per_node_first_layer(cuda_device, monkeypatch):
+    """fp32 link head through RG_IN_PAIRPRE (ModelPlans.link_pairs_pre: the pair chain's first
+    Linear applied per node, W0 (s_i + s_j) + b0 = W0 s_i + W0 s_j + b0) against the per-pair
+    chain (RG_IN_PAIRADD) on the trained model at M-frame size: the link logits agree at the
+    fp32 bound, and the per-node path is the one that ran."""
+    from graph_neural_network_for_radar_perception_amd import engine, synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+    import bench
+    dev = cuda_device
+    cfg = default_config()
+    frames = [synthetic.make_frame(3000, 700 + i) for i in range(3)]
+    clusters = [synthetic.cluster_lists(3000) for _ in range(3)]
+    batch = FrameBatch.from_frames(frames, clusters, device=dev)
+    outs = {}
+    for pre in (True, False):
+        monkeypatch.setattr(engine, 'LINK_PRE', pre)
+        model = bench.make_model(cfg, dev, bench.model_state(cfg, 'trained'))
+        with torch.no_grad():
+            gb, out = RadarGNNPipeline(model, cfg, 'fp32').step(batch)
+        plans = model.plans('fp32')
+        if pre:
+            assert plans.link_pre is not None and plans.link_pre.x3_ok.get('pre') is not False
+        else:
+            assert plans.link_pre is None
+        outs[pre] = RadarGNNPipeline.trim(gb, out)[2]
+    torch.testing.assert_close(outs[True], outs[False], **FP32_TOL)
