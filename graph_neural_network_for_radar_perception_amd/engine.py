@@ -83,6 +83,8 @@ class LayerSpec:
     act: str
     norm: str = 'channel'   # 'channel' (per row, fused) | 'layer' | 'group' (per frame)
     groups: int = 1
+    center: bool = False    # pack zero-mean over the outputs although this layer has no norm
+                            # (its outputs are summed into a normalised pre-activation later)
 
     @property
     def frame_norm(self) -> bool:
@@ -155,7 +157,7 @@ def pack_specs(specs: List[LayerSpec], fmts: List[int], device):
 def centered_fmt(spec: LayerSpec, fmt: int) -> int:
     """Fast formats of a normalised layer are packed zero-mean over the outputs
     (RG_PACK_CENTERED): the kernels' channel_normalization then skips its mean pass."""
-    return fmt | nat.RG_PACK_CENTERED if spec.mu is not None else fmt
+    return fmt | nat.RG_PACK_CENTERED if (spec.mu is not None or spec.center) else fmt
 
 
 def layer_array(specs: List[LayerSpec], base: int, offs: List[int], fmts=None):
@@ -896,7 +898,9 @@ class ModelPlans:
         first = self.link_pair.specs[0]
         if (dtype == 'fp32' and LINK_PRE and not self.frame_norm and first.mu is not None
                 and len(self.link_pair.specs) > 1):
-            bare = LayerSpec(first.weight, None, None, None, 'none')
+            # t packed zero-mean over the outputs like the pair chain's (centred) layer 0,
+            # whose centred bias completes t_i + t_j + b0 to a zero-mean pre-activation
+            bare = LayerSpec(first.weight, None, None, None, 'none', center=True)
             stem = list(self.link_node.specs) if self.link_node is not None else []
             self.link_pre = ChainPlan(stem + [bare], dtype, device)
 
@@ -930,6 +934,7 @@ class ModelPlans:
             lp.x3_ok['pre'] = False
             return False
         nat.check(rc, 'rg_mlp_chain_x3 (RG_IN_PAIRPRE)')
+        pair.x3_ok[nat.IN_PAIRPRE] = True
         return True
 
     def refresh(self):
