@@ -31,29 +31,34 @@ def run(tag, dev):
     sum((o * wi.to(dev)).sum() for o, wi in zip(outs, w)).backward()
     g32 = T._oracle_grads(name, d, lists, w, torch.float32)
     g64 = T._oracle_grads(name, d, lists, w, torch.float64)
+    envs = T._kink_envelope(name, d, lists, w)
     rows = {}
     for pname, p in det.named_parameters():
-        ref = g64['pred.' + pname].numpy()
+        key = 'pred.' + pname
+        ref = g64[key].numpy()
+        env = envs[key]
         scale = float(np.max(np.abs(ref))) + 1e-30
-        ours = float(np.max(np.abs(p.grad.double().cpu().numpy() - ref))) / scale
-        orc = float(np.max(np.abs(g32['pred.' + pname].double().numpy() - ref))) / scale
-        rows[pname] = (ours, orc)
+        diff = np.abs(p.grad.double().cpu().numpy() - ref)
+        ours = float(np.max(np.maximum(diff - env, 0.0))) / scale
+        orc = float(np.max(np.abs(g32[key].double().numpy() - ref))) / scale
+        rows[pname] = (ours, orc, float(np.max(diff)) / scale, float(np.max(env)) / scale)
     return rows, [len(l) for l in lists]
 
 
 def main():
     dev = torch.device('cuda', 0)
     res = {}
-    for fast in (True, False):
+    for fast, dxf in ((True, True), (True, False), (False, True)):
         training.TAPE_F32_FAST = fast
-        for tag in ('off', 'links'):
-            for rep in range(2):
+        training.DX_F32_FAST = dxf
+        for tag in ('off',):
+            for rep in range(1):
                 rows, sizes = run(tag, dev)
-                key = f'fast{int(fast)}/{tag}/{rep}'
+                key = f'tape{int(fast)}/dx{int(dxf)}/{tag}/{rep}'
                 worst = sorted(rows.items(), key=lambda kv: -kv[1][0] / max(kv[1][1], 1e-7))[:6]
                 res[key] = {'clusters': len(sizes), 'worst_ratio': worst,
                             'max_ours': max(v[0] for v in rows.values())}
-                print(key, 'clusters', len(sizes), 'worst', [(k, f'{a:.2e}', f'{b:.2e}') for k, (a, b) in worst[:3]],
+                print(key, 'clusters', len(sizes), 'worst', [(k, ', '.join(f'{v:.2e}' for v in r)) for k, r in worst[:3]],
                       flush=True)
     os.makedirs(os.path.join(REPO, 'gpurun_out'), exist_ok=True)
     json.dump(res, open(os.path.join(REPO, 'gpurun_out', 'grad_diag.json'), 'w'), indent=1)

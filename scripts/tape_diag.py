@@ -53,6 +53,8 @@ def tapes(fast, dev):
             for i, (z, a) in enumerate(zip(tape.z, tape.a)):
                 rows.append((f'conv{l}.{part}.z{i}', z))
                 rows.append((f'conv{l}.{part}.a{i}', a))
+    for l, ct in enumerate(tp['conv']):
+        rows.append((f'conv{l}.msg_out', ct['msg_out']))
     for i, o in enumerate(tp['outs']):
         rows.append((f'out{i}', o))
     return rows, tp
@@ -74,6 +76,24 @@ def main():
         worst = int(d.max(1).values.argmax()) if d.numel() else -1
         print(f'{n1:22s} rows {rows:7d} maxrel {float(d.max()) / scale:9.2e} worst row {worst}',
               flush=True)
+    # max aggregation: where do the two tapes route a destination's gradient differently?
+    g = tf['g']
+    seg = g.seg_ptr.cpu().numpy()
+    eng = None
+    for l, (cf, cg) in enumerate(zip(tf['conv'], tg['conv'])):
+        mf, mg = cf['msg_out'].cpu().double().numpy(), cg['msg_out'].cpu().double().numpy()
+        flips, gaps = 0, []
+        for n in range(tf['N']):
+            a, b = int(seg[n]), int(seg[n + 1])
+            if b - a < 2:
+                continue
+            sf, sg = mf[a:b], mg[a:b]
+            af, ag = sf.argmax(0), sg.argmax(0)
+            for c in np.nonzero(af != ag)[0]:
+                top = np.sort(sg[:, c])[-2:]
+                flips += 1
+                gaps.append((top[1] - top[0]) / (abs(top[1]) + 1e-30))
+        print(f'conv{l} argmax flips {flips} rel gaps {sorted(gaps)[:5]}', flush=True)
 
 
 if __name__ == '__main__':

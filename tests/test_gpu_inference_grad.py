@@ -55,18 +55,81 @@ def _oracle_grads(name, d, lists, weights, dtype=torch.float32):
         torch.set_default_dtype(prev)
 
 
+# pre-activations within this fraction of their tensor's max |x| count as at the kink (the
+# float32 tapes differ from each other by <= 2.5e-6 of max |x|, scripts/tape_diag.py)
+KINK_TAU = 1e-5
+
+
+def _kink_envelope(name, d, lists, weights):
+    """relu / leakyrelu are not differentiable at 0: a pre-activation within float32 rounding
+    of 0 may land on either side in two valid float32 evaluations, which changes the slope
+    its gradient passes by (1 - slope) (measured on proposals_model_trained_N300: one message
+    pre-activation of conv block 6 flips between the register-resident and the generic tape,
+    moving conv block 6's first message weight gradient by 1.5e-3 of its max,
+    scripts/bwd_diag.py). Returns per parameter sum_e |J_e^T (1 - slope) gy_e|, the float64
+    first-order change of its gradient summed over every pre-activation e with
+    |x_e| <= KINK_TAU max|x| (J_e^T: the backward from that element; one batched backward
+    per activation call) -- a bound on any subset of such flips."""
+    from oracle import gnn_forward_ref as ref
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    rec = []
+    act = ref._act
+
+    def recording(x, a):
+        y = act(x, a)
+        rec.append((x, y, a))
+        return y
+
+    ref._act = recording
+    try:
+        sd = {k: v.detach().clone().double().requires_grad_(True)
+              for k, v in model_state_dict(name).items()}
+        out = ref.forward(sd, model_cfg(name), torch.from_numpy(d['node_features']).double(),
+                          torch.from_numpy(d['edge_features']).double(),
+                          torch.from_numpy(d['edge_index'].astype(np.int64)), None, lists)
+        total = sum((o * w.double()).sum() for o, w in zip(out, weights))
+        params = list(sd.values())
+        gys = torch.autograd.grad(total, [y for _, y, _ in rec], retain_graph=True,
+                                  allow_unused=True)
+        env = {k: torch.zeros_like(v) for k, v in sd.items()}
+        for (x, _, a), gy in zip(rec, gys):
+            if gy is None or a == 'swish' or x.numel() == 0:
+                continue
+            near = (x.abs() <= KINK_TAU * x.abs().max()).nonzero()
+            if len(near) == 0:
+                continue
+            slope = ref.LEAKY_SLOPE if a == 'leakyrelu' else 0.0
+            V = torch.zeros((len(near),) + tuple(x.shape))
+            for b, e in enumerate(near.tolist()):
+                V[(b, *e)] = gy[tuple(e)] * (1.0 - slope)
+            grads = torch.autograd.grad(x, params, grad_outputs=V, is_grads_batched=True,
+                                        retain_graph=True, allow_unused=True)
+            for k, gb in zip(sd, grads):
+                if gb is not None:
+                    env[k] += gb.abs().sum(0)
+        return {k: v.numpy() for k, v in env.items()}
+    finally:
+        ref._act = act
+        torch.set_default_dtype(prev)
+
+
 def _check_grads(model, name, d, lists, weights):
     """Every parameter gradient at least as close to the float64 oracle as float32 allows
     (conftest.grad_within_f32_bound: per tensor max|g - g64| / max|g64| <= max(10 x the
-    float32 oracle's own error, 2e-4) and <= max(1e-2, 2 x that error))."""
+    float32 oracle's own error, 2e-4) and <= max(1e-2, 2 x that error)), |g - g64| taken
+    beyond the kink envelope (_kink_envelope) elementwise."""
     g32 = _oracle_grads(name, d, lists, weights, torch.float32)
     g64 = _oracle_grads(name, d, lists, weights, torch.float64)
+    env = _kink_envelope(name, d, lists, weights)
     for pname, p in model.named_parameters():
         assert p.grad is not None, pname
-        ref = g64['pred.' + pname].numpy()
+        key = 'pred.' + pname
+        ref = g64[key].numpy()
         scale = float(np.max(np.abs(ref))) + 1e-30
-        ours = float(np.max(np.abs(p.grad.double().cpu().numpy() - ref))) / scale
-        orc = float(np.max(np.abs(g32['pred.' + pname].double().numpy() - ref))) / scale
+        diff = np.abs(p.grad.double().cpu().numpy() - ref)
+        ours = float(np.max(np.maximum(diff - env[key], 0.0))) / scale
+        orc = float(np.max(np.abs(g32[key].double().numpy() - ref))) / scale
         assert grad_within_f32_bound(ours, orc), (pname, ours, orc)
 
 
