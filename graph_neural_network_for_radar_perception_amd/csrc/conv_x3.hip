@@ -27,6 +27,8 @@
 //    the NEXT layer's projections P' | Q' = W'_pq x_out (+ [b1'; 0]) from the same
 //    registers, so x_out is never re-read for them.
 // The first layer's projections come from rg_conv_proj_x3.
+#include <type_traits>
+
 #include "x3_common.h"
 
 namespace rg {
@@ -325,7 +327,11 @@ __device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const
   node_compute<CENT>(a, w, n0, n1, wU, biasU, wPQ, biasPQ, muU, sdU, lane);
 }
 
-template <bool CENT, bool NODE>
+// ESPL: e is the edge encoder's output pre-split (RG_LAYER_E_SPLIT, rg_mlp_chain_x3_split):
+// row q at (char*)e + q lde holds, per k-step s, the three bf16 planes of its 16 features
+// (FAST_CHAIN k order) in 96 B, so layer 1's B operand is three plain 16-B loads per
+// k-step and W_e is packed FAST_CHAIN
+template <bool CENT, bool NODE, bool ESPL>
 __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[6];
@@ -431,22 +437,57 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     // one tile's gathered rows: P[dst] and Q[src] in accumulator order (features
     // 32m + 8g + 4h .. +3 at [4m + g]), e[edge] in k order (16 s + 8 h .. +3, +4 .. +7 at
     // [2s], [2s + 1])
-    struct Rows {
+    struct RowsF {
       f32x4 p[16], q[16], e[8];
+    };
+    struct RowsS {  // ESPL: e[2 s + plane] = the 16 B of k-step s, planes 0 and 1
+      f32x4 p[16], q[16];
+      u32x4 e[8];
+    };
+    using Rows = std::conditional_t<ESPL, RowsS, RowsF>;
+    // this lane's 16 B of row q, plane pl, k-step s in the pre-split layout
+    auto esp = [&](int q, int pl, int s) {
+      return (const u32x4*)((const char*)a.e + (size_t)q * a.lde + 96 * s + 32 * pl + 16 * h);
+    };
+    // layer 1's B operand of k-step s (ESPL: plane 2 loaded here, one k-step ahead of its
+    // MFMAs -- its lines came into L2 with planes 0 and 1 a tile earlier)
+    auto eop = [&](const Rows& w, int s, int q) {
+      if constexpr (ESPL)
+        return X3{__builtin_bit_cast(bf16x8_t, w.e[2 * s]), __builtin_bit_cast(bf16x8_t, w.e[2 * s + 1]),
+                  __builtin_bit_cast(bf16x8_t, *esp(q, 2, s))};
+      else
+        return split8(w.e[2 * s], w.e[2 * s + 1]);
+    };
+    // (ESPL: planes 0 and 1 -- as many registers as the float32 rows; plane 2 is read at
+    // layer 1, eop)
+    auto load_e = [&](int q, Rows& w) {
+      if constexpr (ESPL) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) w.e[2 * s + pl] = *esp(q, pl, s);
+      } else {
+        const float* pe = a.e + (size_t)q * a.lde + 8 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#if RG_CX3_ENT  // streamed once per layer: non-temporal (keeps the reused P | Q rows in L2)
+          w.e[2 * i] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i));
+          w.e[2 * i + 1] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i + 4));
+#else
+          w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
+          w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
+#endif
+        }
+      }
     };
     auto load_rows = [&](int q, int dq, int sq, Rows& w) {
       const float* pp = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : dq) * PQW + 4 * h;
       const float* pqq = a.pq + (size_t)(RG_CX3_EXP == 3 ? n0 : sq) * PQW + HID + 4 * h;
-      const float* pe = a.e + (size_t)q * a.lde + 8 * h;
 #pragma unroll
       for (int i = 0; i < 16; ++i) w.p[i] = *(const f32x4*)(pp + 8 * i);
 #pragma unroll
       for (int i = 0; i < 16; ++i) w.q[i] = *(const f32x4*)(pqq + 8 * i);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
-        w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
-      }
+      load_e(q, w);
     };
     auto load_pq = [&](int dq, int sq, Rows& w) {
       const float* pp = a.pq + (size_t)dq * PQW + 4 * h;
@@ -455,19 +496,6 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       for (int i = 0; i < 16; ++i) w.p[i] = *(const f32x4*)(pp + 8 * i);
 #pragma unroll
       for (int i = 0; i < 16; ++i) w.q[i] = *(const f32x4*)(pqq + 8 * i);
-    };
-    auto load_e = [&](int q, Rows& w) {
-      const float* pe = a.e + (size_t)q * a.lde + 8 * h;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#if RG_CX3_ENT  // streamed once per layer: non-temporal (keeps the reused P | Q rows in L2)
-        w.e[2 * i] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i));
-        w.e[2 * i + 1] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i + 4));
-#else
-        w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
-        w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
-#endif
-      }
     };
     // tile indices (past the block's last edge clamped: a re-read of a cached row)
     auto tile_idx = [&](int t, int& q, int& dq, int& sq) {
@@ -519,6 +547,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
           (uint32_t)__ballot(r == 0 ? d - n0 != cur : d != dprev) &
           (e1 - t0 >= 32 ? 0xffffffffu : ((1u << (e1 - t0)) - 1u));
       // ---- layer 1: h = P[dst] + Q[src] + W_e e
+      const int qt = min(t0 + r, e1 - 1);  // this lane's edge (tile_idx)
       f32x16 acc1[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -530,14 +559,13 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       {
         if constexpr (RG_CX3_EXP != 5) {
           if constexpr (RG_CX3_MO & 1)
-            layer_x3_mo<4, 4>(acc1, wE, 0, [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
+            layer_x3_mo<4, 4>(acc1, wE, 0, [&](int s) { return eop(rw, s, qt); });
           else
-            layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0,
-                                          [&](int s) { return split8(rw.e[2 * s], rw.e[2 * s + 1]); });
+            layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0, [&](int s) { return eop(rw, s, qt); });
         } else {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
-            acc1[s][0] += xor_first(split8(rw.e[2 * s], rw.e[2 * s + 1]));
+            acc1[s][0] += xor_first(eop(rw, s, qt));
         }
       }
       if constexpr (RG_CX3_QLATE) {
@@ -953,8 +981,11 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   RG_REQUIRE(!next_pq || (next_pq->in_dim == C && next_pq->out_dim == PQW && !next_pq->norm_mu &&
                           next_pq->act == RG_ACT_NONE),
              RG_ERR_UNSUPPORTED, "rg_conv_layer_x3: next_pq must be the 64 -> 256 projection");
-  RG_REQUIRE(ldx % 4 == 0 && lde % 4 == 0 && ld_out % 4 == 0, RG_ERR_UNSUPPORTED,
-             "rg_conv_layer_x3: row strides must be multiples of 4");
+  // RG_LAYER_E_SPLIT: e = the pre-split planes (rg_mlp_chain_x3_split), lde in BYTES
+  const bool espl = (m0.flags & RG_LAYER_E_SPLIT) != 0;
+  RG_REQUIRE(ldx % 4 == 0 && ld_out % 4 == 0 && (espl ? lde % 16 == 0 && lde >= 384 : lde % 4 == 0),
+             RG_ERR_UNSUPPORTED,
+             "rg_conv_layer_x3: row strides must be multiples of 4 (pre-split e: 16 bytes, >= 384)");
   RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_x3: x_out must not alias x");
   RG_REQUIRE(!pq_out || pq_out != pq, RG_ERR_ARG, "rg_conv_layer_x3: pq_out must not alias pq");
   RG_REQUIRE(workspace_bytes >= rg_conv_layer_x3_workspace_size(n_nodes), RG_ERR_ARG,
@@ -994,7 +1025,8 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   if (blocks < NXCD) blocks = NXCD;
   a.steal = a.n_blocks >= 2 * blocks * NW;
   constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
-  auto edge = cent ? conv_x3_kernel<true, NODE> : conv_x3_kernel<false, NODE>;
+  auto edge = cent ? (espl ? conv_x3_kernel<true, NODE, true> : conv_x3_kernel<true, NODE, false>)
+                   : (espl ? conv_x3_kernel<false, NODE, true> : conv_x3_kernel<false, NODE, false>);
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
   RG_LAUNCH_CHECK_ZERO(a.counters, CTR_BYTES, stream);

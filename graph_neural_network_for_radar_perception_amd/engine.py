@@ -52,6 +52,11 @@ def _half_flag(dtype: str) -> int:
 F32_ARITH = os.environ.get('RG_F32_ARITH', 'x3')
 # fp32 link head with its first Linear per node (ModelPlans.link_pairs_pre); '0' = per pair
 LINK_PRE = os.environ.get('RG_LINK_PRE', '1') != '0'
+# fp32 x3 stack: '1' = the edge encoder writes e pre-split (rg_mlp_chain_x3_split, 384 B per
+# edge) and no conv layer re-splits it.  Measured slower on M (conv layer 0.592 -> 0.651 ms,
+# encoder 1.40 -> 1.49 ms: the e rows are the edge launch's only HBM stream and grow by half),
+# so float32 e by default
+E_SPLIT = os.environ.get('RG_E_SPLIT', '0') != '0'
 # x3 conv over the per-graph work-block table (rg_conv_x3_blocks: LPT order, 8-node tail);
 # '0' = plain 32-node runs (same results)
 CONV_X3_TABLE = os.environ.get('RG_CONV_X3_TABLE', '1') != '0'
@@ -326,6 +331,25 @@ class ChainPlan:
                 self.specs[i], (nat.RG_PACK_FAST_IN if i == 0 else nat.RG_PACK_FAST_CHAIN) | X3))
             self._x3 = groups[0][0]
         return self._x3
+
+    def x3_split(self, rows: int, out_split: torch.Tensor, in0: torch.Tensor, w0: int,
+                 rows_dev=None) -> bool:
+        """The chain over dense float32 rows with its output pre-split
+        (rg_mlp_chain_x3_split: uint8 [rows][6 x out_dim]); False when no x3 kernel takes it."""
+        if (self.pieces is not None or not self.use_fast or self.dt != nat.RG_F32
+                or F32_ARITH != 'x3' or self.x3_ok.get('split', True) is False
+                or in0.dtype != torch.float32 or len(self.specs) > nat.MAX_LAYERS):
+            return False
+        rc = nat.lib().rg_mlp_chain_x3_split(self._x3_layers(), len(self.specs), int(rows),
+                                             nat.ptr(rows_dev), in0.data_ptr(), in0.stride(0), w0,
+                                             out_split.data_ptr(), out_split.stride(0),
+                                             nat.stream_ptr(self.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            self.x3_ok['split'] = False
+            return False
+        nat.check(rc, 'rg_mlp_chain_x3_split')
+        self.x3_ok['split'] = True
+        return True
 
     def _f32_layers(self):
         """The chain packed RG_PACK_F32_FAST for rg_mlp_chain_f32 (lazily: training chains
@@ -700,11 +724,12 @@ class ConvPlan:
             we = LayerSpec(Wc[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
             w_pq, b_pq = pq.weight, pq.bias
             # [0] W_e, [1] msg1, [2] upd (cat(x, agg) read from memory), [3] P | Q from
-            # memory (first layer), [4] P | Q from the previous layer's registers
-            specs = [we, m1, u, pq, pq]
+            # memory (first layer), [4] P | Q from the previous layer's registers, [5] W_e
+            # for the pre-split e rows (rg_mlp_chain_x3_split: FAST_CHAIN k order)
+            specs = [we, m1, u, pq, pq, we]
             fmts = [nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3 | CEN,
                     nat.RG_PACK_FAST_IN | X3 | CEN, nat.RG_PACK_FAST_IN | X3,
-                    nat.RG_PACK_FAST_CHAIN | X3]
+                    nat.RG_PACK_FAST_CHAIN | X3, nat.RG_PACK_FAST_CHAIN | X3]
         else:
             fmts = [nat.RG_PACK_F32_FAST] * 4
         try:
@@ -716,6 +741,8 @@ class ConvPlan:
         if self.f32_arith == 'x3':
             self.fused_layers = layer_array(specs[:3], base, offs[:3], fmts[:3])
             self.fused_layers[0].flags = nat.RG_LAYER_CENTERED   # centred on the host
+            self.fused_layers_esplit = layer_array(specs[:3], base, [offs[5]] + offs[1:3], fmts[:3])
+            self.fused_layers_esplit[0].flags = nat.RG_LAYER_CENTERED | nat.RG_LAYER_E_SPLIT
             self.x3_pq_in = layer_array(specs[3:4], base, offs[3:4], fmts[3:4])
             self.x3_pq_chain = layer_array(specs[4:5], base, offs[4:5], fmts[4:5])
             self._ws = {}
@@ -789,8 +816,9 @@ class ConvPlan:
         return bool(self.fused) and self.f32_arith == 'x3'
 
     def x3_ready(self, x, e) -> bool:
+        """e: float32 rows, or the pre-split rows of rg_mlp_chain_x3_split (uint8 [E][384])."""
         return (self.use_fused and self.x3 and self.fused_ok is not False
-                and x.dtype == torch.float32 and e.dtype == torch.float32)
+                and x.dtype == torch.float32 and e.dtype in (torch.float32, torch.uint8))
 
     def project_x3(self, x, pq) -> bool:
         """P | Q of the first x3 layer (rg_conv_proj_x3); False when the kernel does not
@@ -810,7 +838,9 @@ class ConvPlan:
         st = nat.stream_ptr(x.device)
         ws = self.workspace(lib.rg_conv_layer_x3_workspace_size(g.n_nodes), st)
         tbl = g.conv_x3_blocks()
-        args = (self.fused_layers, nxt.x3_pq_chain if nxt is not None else None,
+        # pre-split e (uint8 rows of rg_mlp_chain_x3_split): its W_e image, stride in bytes
+        layers = self.fused_layers_esplit if e.dtype == torch.uint8 else self.fused_layers
+        args = (layers, nxt.x3_pq_chain if nxt is not None else None,
                 nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
                 pq.data_ptr(), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
                 x_out.data_ptr(), x_out.stride(0), nat.ptr(pq_out))
@@ -1032,11 +1062,29 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             return None
     x = alloc('x0', (N, plans.node_enc.out_dim), T)
     plans.node_enc(N, x, node_feats, node_feats.shape[1], segs=segs('node'))
-    e = alloc('e', (Ecap, plans.edge_enc.out_dim), T)
     mark('edge_encoder:start', True)
-    plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
-                   segs=segs('edge'))
+    e = None
+    Ce = plans.edge_enc.out_dim
+    if (E_SPLIT and T == torch.float32 and Ce == 64 and plans.convs
+            and all(cv.x3 and cv.use_fused and cv.fused_ok is not False for cv in plans.convs)):
+        # every layer on the x3 conv: the encoder writes e pre-split once (three bf16 planes
+        # per row) and no layer re-splits it
+        es = alloc('e_split', (Ecap, 6 * Ce), torch.uint8)
+        if plans.edge_enc.x3_split(Ecap, es, edge_feats_dst, edge_feats_dst.shape[1],
+                                   rows_dev=ne_dev):
+            e = es
+    if e is None:
+        e = alloc('e', (Ecap, Ce), T)
+        plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
+                       segs=segs('edge'))
     mark('edge_encoder:end', True)
+
+    def e_f32():
+        """float32 e for a layer the x3 conv did not take (after a pre-split encode)."""
+        ef = alloc('e', (Ecap, Ce), T)
+        plans.edge_enc(Ecap, ef, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
+                       segs=segs('edge'))
+        return ef
     mark('conv_stack:start', True)
     n_fused = 0
     pq = None   # fp32 x3 layers: this layer's P | Q projections
@@ -1071,6 +1119,8 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             if events and not coarse:
                 events.pop()
             pq = None
+        if e.dtype == torch.uint8:
+            e = e_f32()
         mark('conv_fused:start')
         fused = cv.run_fused(x, e, g, xn)
         if fused:

@@ -40,6 +40,8 @@ from .engine import ChainPlan, LayerSpec, specs_from_modules
 # training forward on the register-resident f32 chains (rg_mlp_chain_f32_ex with tapes)
 # where the shape has an instantiation; '0' = the generic chain kernel for every chain
 TAPE_F32_FAST = os.environ.get('RG_TRAIN_F32FAST', '1') != '0'
+# the backward's data GEMMs dX = dZ W on the register-resident f32 kernel ('0': generic)
+DX_F32_FAST = os.environ.get('RG_TRAIN_DX_FAST', '1') != '0'
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -153,7 +155,7 @@ class TrainChain:
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
         gen, fast = self._transposed()[l]
-        if TAPE_F32_FAST and self._dx_ok.get(l, True):
+        if TAPE_F32_FAST and DX_F32_FAST and self._dx_ok.get(l, True):
             rc = lib.rg_mlp_chain_f32_ex(fast, 1, rows, None, nat.IN_DENSE, dZ.data_ptr(),
                                          dZ.stride(0), dZ.shape[1], None, 0, 0, None, 0, 0, None,
                                          None, nat.ptr(res), res.stride(0) if res is not None else 0,
