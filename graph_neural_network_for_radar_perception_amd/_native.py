@@ -141,6 +141,9 @@ _SIGNATURES = {
                                         _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     'rg_conv_blocks_workspace_size': (_S, [_I]),
     'rg_conv_blocks': (_I, [_P, _I, _P, _P, _P, _S, _P]),
+    'rg_conv_wave_nodes': (_I, [_P, _I, _I, _P, _P]),
+    'rg_conv_layer_fused_waves': (_I, [ctypes.POINTER(rg_layer), ctypes.POINTER(rg_layer), _I, _P,
+                                       _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _P]),
     'rg_cluster_majority_label': (_I, [_P, _P, _P, _I, _I, _P, _P, _P]),
     'rg_cross_entropy': (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
     'rg_cross_entropy_backward': (_I, [_P, _I, _P, _I, _I, _P, _P, _I, _P]),

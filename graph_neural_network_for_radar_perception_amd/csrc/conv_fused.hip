@@ -140,7 +140,32 @@ extern "C" int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_l
              RG_ERR_ARG, "rg_conv_layer_fused: every layer packed with the same 16-bit type");
   auto fn = f16 ? rg::conv_f16::conv_fused_entry : rg::conv::conv_fused_entry;
   return fn(msg_layers, upd_layer, aggr, x, ldx, e, lde, seg_ptr, src, dst, n_nodes, x_out, ld_out,
-            blk_nodes, n_blocks_dev, workspace, stream);
+            blk_nodes, n_blocks_dev, nullptr, 0, workspace, stream);
+}
+
+extern "C" int rg_conv_wave_nodes(const int* seg_ptr, int n_nodes, int n_waves, int* wave_nodes,
+                                  void* stream) {
+  RG_REQUIRE(seg_ptr && wave_nodes && n_nodes >= 1 && n_waves >= 1, RG_ERR_ARG,
+             "rg_conv_wave_nodes: bad argument");
+  conv_wave_nodes_kernel<<<(n_waves + 1 + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      seg_ptr, n_nodes, n_waves, wave_nodes);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_conv_layer_fused_waves(const rg_layer* msg_layers, const rg_layer* upd_layer,
+                                         int aggr, const void* x, int ldx, const void* e, int lde,
+                                         const int* seg_ptr, const int* src, const int* dst,
+                                         int n_nodes, void* x_out, int ld_out,
+                                         const int* wave_nodes, int n_waves, void* workspace,
+                                         void* stream) {
+  RG_REQUIRE(wave_nodes, RG_ERR_ARG, "rg_conv_layer_fused_waves: wave_nodes from rg_conv_wave_nodes");
+  const int f16 = msg_layers[0].flags & msg_layers[1].flags & upd_layer->flags & RG_LAYER_F16;
+  RG_REQUIRE(f16 || !((msg_layers[0].flags | msg_layers[1].flags | upd_layer->flags) & RG_LAYER_F16),
+             RG_ERR_ARG, "rg_conv_layer_fused: every layer packed with the same 16-bit type");
+  auto fn = f16 ? rg::conv_f16::conv_fused_entry : rg::conv::conv_fused_entry;
+  return fn(msg_layers, upd_layer, aggr, x, ldx, e, lde, seg_ptr, src, dst, n_nodes, x_out, ld_out,
+            nullptr, nullptr, wave_nodes, n_waves, workspace, stream);
 }
 
 extern "C" int rg_conv_layer_fused(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,

@@ -87,6 +87,11 @@ struct CArgs {
   // largest first, rg_conv_blocks); null: b = 8-node run
   const int* blk_nodes;
   const int* n_blk_dev;
+  // optional static schedule (rg_conv_wave_nodes): wave rank w owns the nodes
+  // [wave_nodes[w], wave_nodes[w + 1]) -- equal shares of degree + WAVE_NODE_COST -- and walks
+  // them in NB-node blocks; no work counters.  Ranks are XCD-major (workgroup b is on XCD
+  // b % NQ), so an XCD's waves hold one contiguous node range.
+  const int* wave_nodes;
 };
 
 __device__ __forceinline__ uint32_t bf2(float a, float b) { return HT::pack2(a, b); }
@@ -265,12 +270,21 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     }
   };
   int blk = 0;
-  if (lane == 0) blk = atomicAdd(head, 1);
-  blk = blo + __shfl(blk, 0, 64);
   int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
-  if (blk >= bhi) blk = steal_next();
+  int s_hi = 0;  // static schedule: the end of this wave's node range
+  if (a.wave_nodes) {
+    const int rank = (blockIdx.x % NQ) * (int)(gridDim.x / NQ) * CW + (blockIdx.x / NQ) * CW + wave;
+    bn0 = a.wave_nodes[rank];
+    s_hi = a.wave_nodes[rank + 1];
+    bn1 = min(bn0 + NB, s_hi);
+    blk = bn0 < s_hi ? 0 : -1;
+  } else {
+    if (lane == 0) blk = atomicAdd(head, 1);
+    blk = blo + __shfl(blk, 0, 64);
+    if (blk >= bhi) blk = steal_next();
+    if (blk >= 0) block_nodes(blk, bn0, bn1);
+  }
   if (blk >= 0) {
-    block_nodes(blk, bn0, bn1);
     e0 = a.seg_ptr[bn0];
     e1 = a.seg_ptr[bn1];
   }
@@ -288,7 +302,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     const int n0 = bn0;
     const int n1 = bn1;
     int nxt_raw = 0;
-    if (lane == 0) nxt_raw = atomicAdd(head, 1);
+    if (!a.wave_nodes && lane == 0) nxt_raw = atomicAdd(head, 1);
 #if RG_CONV_LUT
     // the block's node r (= one-hot column / slot r) owns the CSR range [sst, sen); lanes
     // past the block's nodes get an empty range (clamped loads, no branch)
@@ -446,11 +460,18 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     }
     CSTAMP(1);
 
-    int nxt = blo + __shfl(nxt_raw, 0, 64);
-    if (nxt >= bhi) nxt = steal_next();
+    int nxt = 0;
     int ne0 = 0, ne1 = 0, nn0 = 0, nn1 = 0;
+    if (a.wave_nodes) {
+      nn0 = n1;
+      nn1 = min(n1 + NB, s_hi);
+      nxt = nn0 < s_hi ? 0 : -1;
+    } else {
+      nxt = blo + __shfl(nxt_raw, 0, 64);
+      if (nxt >= bhi) nxt = steal_next();
+      if (nxt >= 0) block_nodes(nxt, nn0, nn1);
+    }
     if (nxt >= 0) {
-      block_nodes(nxt, nn0, nn1);
       ne0 = a.seg_ptr[nn0];
       ne1 = a.seg_ptr[nn1];
     }
@@ -579,6 +600,25 @@ __device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes, int ca
   return max(cap_min, seg_ptr[n_nodes] / cap_div);
 }
 
+// the static schedule's per-node cost in edge units: the block head (P) and update of an
+// NB-node block cost about one edge tile's MFMAs, 32 edges / NB nodes
+static constexpr int WAVE_NODE_COST = 4;
+__global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_nodes, int n_waves,
+                                       int* __restrict__ wave_nodes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_waves) return;
+  // first node n with cost(n) = seg_ptr[n] + WAVE_NODE_COST n >= total i / n_waves
+  const long total = (long)seg_ptr[n_nodes] + (long)WAVE_NODE_COST * n_nodes;
+  const long target = total * i / n_waves;
+  int lo = 0, hi = n_nodes;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((long)seg_ptr[mid] + (long)WAVE_NODE_COST * mid < target) lo = mid + 1;
+    else hi = mid;
+  }
+  wave_nodes[i] = i == n_waves ? n_nodes : lo;
+}
+
 template <bool EMIT>
 __global__ void conv_blocks_kernel(const int* __restrict__ seg_ptr, int n_nodes,
                                    int* __restrict__ cnt, const int* __restrict__ off,
@@ -618,6 +658,7 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
                                           int lde, const int* seg_ptr, const int* src,
                                           const int* dst, int n_nodes, void* x_out, int ld_out,
                                           const int* blk_nodes, const int* n_blocks_dev,
+                                          const int* wave_nodes, int n_waves,
                                           void* workspace, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const rg_layer& m0 = msg_layers[0];
@@ -663,6 +704,10 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
              "rg_conv_layer_fused_blocks: block table and count go together");
   a.blk_nodes = blk_nodes;
   a.n_blk_dev = n_blocks_dev;
+  RG_REQUIRE(!wave_nodes || (!blk_nodes && n_waves >= CW * NQ && n_waves % (CW * NQ) == 0),
+             RG_ERR_ARG, "rg_conv_layer_fused_waves: n_waves %d must be a multiple of %d", n_waves,
+             CW * NQ);
+  a.wave_nodes = wave_nodes;
   if (n_nodes <= 0) return RG_OK;
   const size_t lds = (size_t)off + LUT_BYTES + (size_t)CW * WAVE_LDS;
   RG_REQUIRE(lds <= DYN_LDS_MAX, RG_ERR_UNSUPPORTED, "rg_conv_layer_fused: LDS %zu", lds);
@@ -675,6 +720,7 @@ static int conv_fused_entry(const rg_layer* msg_layers, const rg_layer* upd_laye
   int blocks = 256;  // a block table has at least ceil(N / NB) entries
   if (blocks * CW > a.n_blocks) blocks = (a.n_blocks + CW - 1) / CW;
   blocks = (blocks + NQ - 1) / NQ * NQ;  // every head has workgroups of its own
+  if (wave_nodes) blocks = n_waves / CW;  // one workgroup per CW ranks of the schedule
   kern<<<blocks, CT, lds, st>>>(a);
   const hipError_t le = hipGetLastError();
   if (le != hipSuccess) {

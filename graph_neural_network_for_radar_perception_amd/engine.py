@@ -468,6 +468,7 @@ class DeviceGraph:
         self.n_edges = n_edges
         self.n_pairs = n_pairs
         self._conv_blocks = None
+        self._conv_waves = None
         self._conv_x3_blocks = None
         self.frame_ptr = None      # int32 [B+1] device node offsets of the frames (optional)
         self.n_frames = None
@@ -530,6 +531,25 @@ class DeviceGraph:
                       'rg_conv_blocks')
             self._conv_blocks = (tbl, nb)
         return self._conv_blocks
+
+    # the 16-bit fused conv's static schedule (rg_conv_wave_nodes) for the same small graphs:
+    # equal per-wave shares instead of dequeued blocks ('0': the block table)
+    CONV_WAVES = int(os.environ.get('RG_CONV_WAVES', 2048))
+
+    def conv_waves(self):
+        """wave_nodes [CONV_WAVES + 1] of rg_conv_wave_nodes for rg_conv_layer_fused_waves, or
+        None (large graphs: the dynamic 8-node schedule; or CONV_WAVES = 0)."""
+        n = self.n_nodes
+        if (n == 0 or self.CONV_WAVES <= 0 or (n + 7) // 8 >= self.CONV_BLOCK_TABLE_MAX_RUNS):
+            return None
+        if self._conv_waves is None:
+            dev = self.seg_ptr.device
+            wn = torch.empty(self.CONV_WAVES + 1, dtype=torch.int32, device=dev)
+            nat.check(nat.lib().rg_conv_wave_nodes(self.seg_ptr.data_ptr(), n, self.CONV_WAVES,
+                                                   wn.data_ptr(), nat.stream_ptr(dev)),
+                      'rg_conv_wave_nodes')
+            self._conv_waves = wn
+        return self._conv_waves
 
     def conv_x3_blocks(self):
         """The rg_conv_x3_blocks work-block table of this graph for rg_conv_layer_x3_blocks
@@ -886,14 +906,22 @@ class ConvPlan:
             nat.check(rc, 'rg_conv_layer_f32')
             self.fused_ok = True
             return True
-        tbl, nb = g.conv_blocks()
         st = nat.stream_ptr(x.device)
         ws = self.workspace(lib.rg_conv_layer_workspace_size(), st)
-        rc = lib.rg_conv_layer_fused_blocks(
-            self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),
-            e.data_ptr(), e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
-            g.n_nodes, x_out.data_ptr(), x_out.stride(0), nat.ptr(tbl), nat.ptr(nb),
-            ws.data_ptr(), st)
+        wn = g.conv_waves()
+        if wn is not None:
+            rc = lib.rg_conv_layer_fused_waves(
+                self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),
+                e.data_ptr(), e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(),
+                g.dst.data_ptr(), g.n_nodes, x_out.data_ptr(), x_out.stride(0), wn.data_ptr(),
+                wn.numel() - 1, ws.data_ptr(), st)
+        else:
+            tbl, nb = g.conv_blocks()
+            rc = lib.rg_conv_layer_fused_blocks(
+                self.fused_msg, self.fused_upd, nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0),
+                e.data_ptr(), e.stride(0), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(),
+                g.n_nodes, x_out.data_ptr(), x_out.stride(0), nat.ptr(tbl), nat.ptr(nb),
+                ws.data_ptr(), st)
         if rc == nat.RG_ERR_UNSUPPORTED:
             self.fused_ok = False
             return False

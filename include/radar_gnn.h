@@ -436,6 +436,20 @@ int rg_conv_layer_fused_blocks(const rg_layer* msg_layers, const rg_layer* upd_l
 size_t rg_conv_blocks_workspace_size(int n_nodes);
 int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, int* n_blocks,
                    void* workspace, size_t workspace_bytes, void* stream);
+/* A static schedule for the same layer: wave rank w of an n_waves-wave grid (n_waves a
+ * multiple of 64: 8 waves per workgroup, 8 XCDs) owns the destination nodes
+ * [wave_nodes[w], wave_nodes[w+1]), equal shares of degree + 4 per node (the block head and
+ * update in edge units), and walks them in 8-node blocks with no work counters -- no
+ * dequeue latency and no tail of whole blocks (one dense frame: BASELINE config 5).
+ * wave_nodes: int32[n_waves + 1] (device), from rg_conv_wave_nodes once per graph.  Same
+ * results as rg_conv_layer_fused (each destination's edges summed in CSR order by one wave). */
+int rg_conv_wave_nodes(const int* seg_ptr, int n_nodes, int n_waves, int* wave_nodes,
+                       void* stream);
+int rg_conv_layer_fused_waves(const rg_layer* msg_layers, const rg_layer* upd_layer, int aggr,
+                              const void* x, int ldx, const void* e, int lde,
+                              const int* seg_ptr, const int* src, const int* dst, int n_nodes,
+                              void* x_out, int ld_out, const int* wave_nodes, int n_waves,
+                              void* workspace, void* stream);
 
 /* ------------------------------------------- object-classifier finetuning */
 
