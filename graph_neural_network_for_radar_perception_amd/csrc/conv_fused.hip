@@ -147,8 +147,10 @@ extern "C" int rg_conv_wave_nodes(const int* seg_ptr, int n_nodes, int n_waves, 
                                   void* stream) {
   RG_REQUIRE(seg_ptr && wave_nodes && n_nodes >= 1 && n_waves >= 1, RG_ERR_ARG,
              "rg_conv_wave_nodes: bad argument");
+  static const int cost = getenv("RG_CONV_NODE_COST") ? atoi(getenv("RG_CONV_NODE_COST"))
+                                                     : rg::conv::WAVE_NODE_COST;
   conv_wave_nodes_kernel<<<(n_waves + 1 + 255) / 256, 256, 0, (hipStream_t)stream>>>(
-      seg_ptr, n_nodes, n_waves, wave_nodes);
+      seg_ptr, n_nodes, n_waves, cost, wave_nodes);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -600,20 +600,20 @@ __device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes, int ca
   return max(cap_min, seg_ptr[n_nodes] / cap_div);
 }
 
-// the static schedule's per-node cost in edge units: the block head (P) and update of an
-// NB-node block cost about one edge tile's MFMAs, 32 edges / NB nodes
+// the static schedule's per-node cost in edge units (the block head (P) and update of an
+// NB-node block, per node; RG_CONV_NODE_COST overrides it for measurement)
 static constexpr int WAVE_NODE_COST = 4;
 __global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_nodes, int n_waves,
-                                       int* __restrict__ wave_nodes) {
+                                       int node_cost, int* __restrict__ wave_nodes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n_waves) return;
-  // first node n with cost(n) = seg_ptr[n] + WAVE_NODE_COST n >= total i / n_waves
-  const long total = (long)seg_ptr[n_nodes] + (long)WAVE_NODE_COST * n_nodes;
+  // first node n with cost(n) = seg_ptr[n] + node_cost n >= total i / n_waves
+  const long total = (long)seg_ptr[n_nodes] + (long)node_cost * n_nodes;
   const long target = total * i / n_waves;
   int lo = 0, hi = n_nodes;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if ((long)seg_ptr[mid] + (long)WAVE_NODE_COST * mid < target) lo = mid + 1;
+    if ((long)seg_ptr[mid] + (long)node_cost * mid < target) lo = mid + 1;
     else hi = mid;
   }
   wave_nodes[i] = i == n_waves ? n_nodes : lo;

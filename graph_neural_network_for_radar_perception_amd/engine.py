@@ -535,12 +535,13 @@ class DeviceGraph:
     # the 16-bit fused conv's static schedule (rg_conv_wave_nodes) for the same small graphs:
     # equal per-wave shares instead of dequeued blocks ('0': the block table)
     CONV_WAVES = int(os.environ.get('RG_CONV_WAVES', 2048))
+    CONV_WAVES_MAX_RUNS = int(os.environ.get('RG_CONV_WAVES_MAX_RUNS', 4 * 2048))
 
     def conv_waves(self):
         """wave_nodes [CONV_WAVES + 1] of rg_conv_wave_nodes for rg_conv_layer_fused_waves, or
         None (large graphs: the dynamic 8-node schedule; or CONV_WAVES = 0)."""
         n = self.n_nodes
-        if (n == 0 or self.CONV_WAVES <= 0 or (n + 7) // 8 >= self.CONV_BLOCK_TABLE_MAX_RUNS):
+        if n == 0 or self.CONV_WAVES <= 0 or (n + 7) // 8 >= self.CONV_WAVES_MAX_RUNS:
             return None
         if self._conv_waves is None:
             dev = self.seg_ptr.device
