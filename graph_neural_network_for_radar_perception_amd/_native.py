@@ -49,6 +49,12 @@ class rg_layer(ctypes.Structure):
                 ('save_pre', ctypes.c_void_p), ('save_out', ctypes.c_void_p)]
 
 
+class rg_pack_job(ctypes.Structure):
+    _fields_ = [('weight', ctypes.c_void_p), ('bias', ctypes.c_void_p),
+                ('packed', ctypes.c_void_p), ('in_dim', ctypes.c_int),
+                ('out_dim', ctypes.c_int), ('fmt', ctypes.c_int), ('transpose', ctypes.c_int)]
+
+
 class rg_loss_args(ctypes.Structure):
     _fields_ = [('node_cls', ctypes.c_void_p), ('node_reg', ctypes.c_void_p),
                 ('link', ctypes.c_void_p), ('obj', ctypes.c_void_p),
@@ -112,6 +118,7 @@ _SIGNATURES = {
     'rg_gather_rows_f32': (_I, [_P, _P, _L, _I, _P, _P]),
     'rg_packed_linear_bytes': (_S, [_I, _I, _I]),
     'rg_pack_linear': (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    'rg_pack_linear_jobs': (_I, [_P, _I, _P]),
     'rg_mlp_chain': (_I, [_I, ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,
                           _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
     'rg_mlp_chain_fast': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,

@@ -705,6 +705,56 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   return RG_OK;
 }
 
+// rg_pack_linear_jobs: blockIdx.y = job, a grid-stride loop over its weights then its bias
+// (RG_F32: plain, padded to 16; RG_PACK_F32_FAST: accumulator order, padded to 32) -- the same
+// element formulas as pack_f32_kernel / pack_f32_fast_kernel / pack_bias_frag_kernel
+__global__ void pack_jobs_kernel(const rg_pack_job* __restrict__ jobs) {
+  const rg_pack_job j = jobs[blockIdx.y];
+  const bool fast = j.fmt == RG_PACK_F32_FAST;
+  const long total = (long)frag_bytes(j.in_dim, j.out_dim, j.fmt) / sizeof(float);
+  const int nb = kpad(j.out_dim, fast ? 32 : 16);
+  float* P = (float*)j.packed;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total + nb;
+       t += (long)gridDim.x * blockDim.x) {
+    if (t >= total) {
+      const int i = (int)(t - total);
+      int f = i;
+      if (fast) {
+        const int m = i >> 5, h = (i >> 4) & 1, g = (i >> 2) & 3, q = i & 3;
+        f = 32 * m + 8 * g + 4 * h + q;
+      }
+      P[t] = (j.bias && f < j.out_dim) ? j.bias[f] : 0.f;
+      continue;
+    }
+    const int e = (int)(t & 3);
+    const int lane = (int)((t >> 2) & 63);
+    const long ms = t >> 8;
+    int o, k;
+    if (fast) {
+      const int S4 = (j.in_dim + 7) / 8;
+      o = 32 * (int)(ms / S4) + (lane & 31);
+      k = 8 * (int)(ms % S4) + 4 * (lane >> 5) + e;
+    } else {
+      const int S4 = kpad(j.in_dim, 16) / 16;
+      o = 16 * (int)(ms / S4) + (lane & 15);
+      k = 16 * (int)(ms % S4) + 4 * (lane >> 4) + e;
+    }
+    P[t] = (o < j.out_dim && k < j.in_dim)
+               ? (j.transpose ? j.weight[(size_t)k * j.out_dim + o] : j.weight[(size_t)o * j.in_dim + k])
+               : 0.f;
+  }
+}
+
+extern "C" int rg_pack_linear_jobs(const rg_pack_job* jobs, int n_jobs, void* stream) {
+  RG_REQUIRE(n_jobs >= 0 && n_jobs <= 65535 && (jobs || n_jobs == 0), RG_ERR_ARG,
+             "rg_pack_linear_jobs: %d jobs", n_jobs);
+  if (n_jobs == 0) return RG_OK;
+  // 64 blocks of 256 per job: the largest f32 image (256 x 256 + bias) in four passes
+  pack_jobs_kernel<<<dim3(64, n_jobs), 256, 0, (hipStream_t)stream>>>(jobs);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, long rows,
                             const int* rows_dev, int in_mode, int in_dtype, const void* in0,
                             int ld0, int w0, const void* in1, int ld1, int w1, const void* in2,

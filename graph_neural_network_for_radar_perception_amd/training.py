@@ -42,6 +42,8 @@ from .engine import ChainPlan, LayerSpec, specs_from_modules
 TAPE_F32_FAST = os.environ.get('RG_TRAIN_F32FAST', '1') != '0'
 # the backward's data GEMMs dX = dZ W on the register-resident f32 kernel ('0': generic)
 DX_F32_FAST = os.environ.get('RG_TRAIN_DX_FAST', '1') != '0'
+# after an optimizer step, re-pack every f32 image in place in one launch ('0': per chain)
+REPACK_JOBS = os.environ.get('RG_TRAIN_REPACK_JOBS', '1') != '0'
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -112,6 +114,38 @@ class TrainChain:
     def invalidate(self):
         self.plan.sig = None
         self._tsig = None
+
+    def pack_jobs(self):
+        """rg_pack_job entries that re-write every packed image of this chain in place (the
+        generic and register-resident f32 images and their transposes), or None when the
+        chain is not fully packed yet or packs something else (frame-norm pieces)."""
+        p = self.plan
+        if p.pieces is not None or p.sig is None or p.dt != nat.RG_F32:
+            return None
+        jobs = []
+
+        def job(w, b, dst, i, o, fmt, tr):
+            j = nat.rg_pack_job()
+            j.weight, j.bias, j.packed = w.data_ptr(), nat.ptr(b), dst
+            j.in_dim, j.out_dim, j.fmt, j.transpose = i, o, fmt, tr
+            jobs.append(j)
+
+        for g0, (arr, n, _) in zip(range(0, len(p.specs), nat.MAX_LAYERS), p.groups):
+            for i in range(n):
+                s = p.specs[g0 + i]
+                job(s.weight.detach(), None if s.bias is None else s.bias.detach(), arr[i].w_packed,
+                    s.in_dim, s.out_dim, nat.RG_F32, 0)
+        if p._f32 is not None:
+            for i, s in enumerate(p.specs):
+                job(s.weight.detach(), None if s.bias is None else s.bias.detach(),
+                    p._f32[i].w_packed, s.in_dim, s.out_dim, nat.RG_PACK_F32_FAST, 0)
+        if self._tsig is not None and self._tsig == p.sig:
+            for s, pair in zip(self.specs, self._tarr):
+                for fmt, arr in zip((nat.RG_F32, nat.RG_PACK_F32_FAST), pair):
+                    job(s.weight.detach(), None, arr[0].w_packed, s.out_dim, s.in_dim, fmt, 1)
+        else:
+            self._tsig = None   # transposes not packed yet: packed on first use
+        return jobs
 
     def _transposed(self):
         """W^T of every layer (no bias / norm / activation) for the data GEMM of the
@@ -624,9 +658,33 @@ class TrainEngine:
         return out
 
     def invalidate(self):
-        """Parameters changed behind torch's version counters (FusedSGD): re-pack."""
+        """Parameters changed behind torch's version counters (FusedSGD): re-pack.  When
+        every chain holds only float32 images already packed, they are re-written in place by
+        ONE rg_pack_linear_jobs launch (~200 images: one launch instead of three per image);
+        otherwise each chain re-packs on its next use."""
+        if REPACK_JOBS and self._repack_in_place():
+            return
         for c in self.chains():
             c.invalidate()
+
+    def _repack_in_place(self) -> bool:
+        jobs = []
+        for c in self.chains():
+            j = c.pack_jobs()
+            if j is None:
+                return False
+            jobs += j
+        key = tuple((j.weight, j.bias, j.packed, j.in_dim, j.out_dim, j.fmt, j.transpose)
+                    for j in jobs)
+        if getattr(self, '_repack_key', None) != key:
+            arr = (nat.rg_pack_job * len(jobs))(*jobs)
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self._repack_dev = host.to(self.device)
+            self._repack_key = key
+        nat.check(nat.lib().rg_pack_linear_jobs(self._repack_dev.data_ptr(), len(jobs),
+                                                nat.stream_ptr(self.device)),
+                  'rg_pack_linear_jobs')
+        return True
 
     # ------------------------------------------------------------------ helpers
     def _segsum(self, src, col0, width, ptr, lst, scale, out, accumulate):

@@ -243,6 +243,19 @@ size_t rg_packed_linear_bytes(int in_dim, int out_dim, int dtype);
 int rg_pack_linear(const float* weight, const float* bias, int in_dim, int out_dim, int dtype,
                    void* packed, void* stream);
 
+/* Many float32 packs in ONE launch (the training step re-packs every layer's images after
+ * each optimizer step: `optimizer.step()` at training.py:80 changes every nn.Linear).  Each
+ * job is what rg_pack_linear(weight, bias, in_dim, out_dim, fmt | (transpose ?
+ * RG_PACK_TRANSPOSE : 0), packed) writes, for fmt RG_F32 or RG_PACK_F32_FAST.  jobs: a
+ * DEVICE array of n_jobs entries (built once; the weights are read at launch time). */
+typedef struct rg_pack_job {
+  const float* weight;  /* [out][in] ([in][out] with transpose) */
+  const float* bias;    /* [out] or NULL */
+  void* packed;         /* rg_packed_linear_bytes(in_dim, out_dim, fmt) bytes */
+  int in_dim, out_dim, fmt, transpose;
+} rg_pack_job;
+int rg_pack_linear_jobs(const rg_pack_job* jobs, int n_jobs, void* stream);
+
 /* One ffn_block (common.py:185-205): Linear -> [channel_normalization] -> activation. */
 typedef struct rg_layer {
   const void* w_packed;  /* rg_pack_linear output (weights + bias)             */

@@ -236,6 +236,50 @@ def test_trainer_step_matches_oracle(cuda_device):
         np.testing.assert_allclose(got[k].cpu().numpy(), v.numpy(), rtol=1e-5, atol=2e-7, err_msg=k)
 
 
+def test_trainer_repack_in_place_bit_identical(cuda_device, monkeypatch):
+    """After each fused SGD step the engine re-writes every packed float32 image in place with
+    ONE rg_pack_linear_jobs launch (training.REPACK_JOBS): three trainer steps give
+    bit-identical losses and weights to re-packing chain by chain, and the in-place path is
+    the one taken."""
+    from graph_neural_network_for_radar_perception_amd import synthetic, training
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    from graph_neural_network_for_radar_perception_amd.graph_features import (FrameBatch,
+                                                                                build_graph_batch)
+    from graph_neural_network_for_radar_perception_amd.training import RadarGNNTrainer
+    cfg = default_config()
+    torch.manual_seed(23)
+    sd = {k: v.detach().clone() for k, v in Model_Training(cfg, 'cpu').state_dict().items()}
+    frames = [synthetic.make_frame(n, 8400 + i) for i, n in enumerate([700, 300])]
+    gb = build_graph_batch(FrameBatch.from_frames(frames, device=cuda_device), cfg)
+    rp = gb.row_ptr.cpu().numpy().astype(np.int64)
+    col = gb.col[:int(rp[-1])].cpu().numpy().astype(np.int64)
+    lab_np, clusters = synthetic.batch_labels(frames, rp, col, cfg.num_classes)
+    lab = {k: torch.from_numpy(v).to(cuda_device) for k, v in lab_np.items()}
+    lab['class_weights'] = torch.tensor(cfg.class_weights_dyn, device=cuda_device)
+    batch = FrameBatch.from_frames(frames, clusters, device=cuda_device)
+    runs = []
+    for jobs in (True, False):
+        monkeypatch.setattr(training, 'REPACK_JOBS', jobs)
+        m = Model_Training(cfg, 'cpu')
+        m.load_state_dict(sd)
+        m = m.to(cuda_device).train()
+        tr = RadarGNNTrainer(m, cfg, world=1)
+        calls = []
+        orig = training.TrainEngine._repack_in_place
+        monkeypatch.setattr(training.TrainEngine, '_repack_in_place',
+                            lambda self: calls.append(orig(self)) or calls[-1])
+        losses = [torch.stack([torch.as_tensor(v) for v in tr.step(batch, lab)[0]]).cpu()
+                  for _ in range(3)]
+        monkeypatch.setattr(training.TrainEngine, '_repack_in_place', orig)
+        if jobs:
+            assert calls and all(calls), calls    # every step re-packed in place
+        runs.append((losses, tr.opt.flat.detach().clone().cpu()))
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert torch.equal(a, b)
+    assert torch.equal(runs[0][1], runs[1][1])
+
+
 def test_f32_tape_kernel_matches_generic(cuda_device, monkeypatch):
     """The register-resident training tape (rg_mlp_chain_f32_ex with save_pre / save_out,
     exact f32 products) against the generic f32 chain kernel, chain by chain on random rows
