@@ -53,6 +53,10 @@ PRESETS = {
               cpu_warm=2, dtype='fp32', weights='trained'),
     'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
                cpu_warm=2, dtype='bf16', weights='random'),
+    # BASELINE config 3: 512 frames of C2's shape frame-parallel over 8 GPUs, forward only --
+    # 64 frames per rank (weak scaling: --gpus 8 processes 512), no collective in the step
+    'c3': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
+               cpu_warm=2, dtype='bf16', weights='random'),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
                cpu_warm=1, dtype='fp16', weights='random'),
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
@@ -77,7 +81,9 @@ def parse():
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--config', default='m', choices=sorted(PRESETS),
                    help='m: the metric configuration (default; fp32, trained weights); '
-                        'c2: BASELINE config 2 (bf16); c5: config 5 radius-graph stress; '
+                        'c2: BASELINE config 2 (bf16); c3: config 3 (C2 frames, 64 per GPU, '
+                        'frame-parallel over --gpus, forward only); '
+                        'c5: config 5 radius-graph stress; '
                         'c4: config 4 training step (forward + backward + SGD, DDP); '
                         'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4); '
                         'frontend: the real-data front-end (SURVEY 8(f) rank 3)')
@@ -104,7 +110,7 @@ def parse():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
     if a.dtype is None:
-        a.dtype = {'c2': 'bf16', 'c5': 'fp16'}.get(a.config, 'fp32')
+        a.dtype = {'c2': 'bf16', 'c3': 'bf16', 'c5': 'fp16'}.get(a.config, 'fp32')
     if a.weights is None:
         a.weights = 'random'
     return a
@@ -747,7 +753,10 @@ def frontend_main(args, world, rank, local):
 
 def workload_name(args) -> str:
     head = {'m': 'M (the metric configuration, SURVEY §8(d))',
-            'c2': 'BASELINE config 2', 'c5': 'BASELINE config 5'}.get(args.config, args.config)
+            'c2': 'BASELINE config 2', 'c5': 'BASELINE config 5',
+            'c3': f'BASELINE config 3 ({args.frames * max(args.gpus, 1)} frames frame-parallel '
+                  f'over {max(args.gpus, 1)} GPU(s), forward only, no collective in the step)'
+            }.get(args.config, args.config)
     return (f'{head}: {args.frames} frame(s) x {args.nodes} nodes per GPU, {graph_desc(args)}, '
             f'L={args.layers}, {args.dtype}, {args.weights} weights; step = graph build + '
             'node/edge features + encoders + message passing + 4 heads')

@@ -159,14 +159,13 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
 // each boundary (segment pointers held one per lane of the group, read by shuffle).  Each
 // segment is still summed from its first row in order: bit-identical to the kernel above.
 // Sum / mean / max, no row index, C a multiple of 64.
-template <typename TS, typename TO, int OP, int VEC, int G, bool NT>
+template <typename TS, typename TO, int OP, int VEC, int G, bool NT, int U = 8>
 __global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
                                                              int n_seg, int C, TO* __restrict__ out,
                                                              int ld_out) {
   constexpr int LPS = 64 / VEC;
   constexpr int GPB = 256 / LPS;
-  constexpr int U = 8;
   static_assert(G <= LPS, "one segment pointer per lane of the group");
   const int g = threadIdx.x % LPS;
   const int s0 = (blockIdx.x * GPB + threadIdx.x / LPS) * G;
@@ -245,21 +244,48 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
 #define RG_SEG_ARGS                                                                         \
   (const TS*)g.src, g.ld_src, g.seg_ptr, g.seg_end, g.idx, g.uni, g.n_uni, (const TS*)g.bm,   \
       g.ld_bm, g.n_seg, g.C, (TO*)g.out, g.ld_out
-  // sum / mean / max over a plain CSR: the streaming kernel, two segments per lane group,
-  // non-temporal row loads (M's CSR, bf16: 0.56 -> 0.70 of HBM; scripts/seg_variants.py).
+  // sum / mean / max over a plain CSR: the streaming kernel, non-temporal row loads (M's
+  // CSR, bf16: 0.56 -> 0.70 of HBM with two segments per group; scripts/seg_variants.py).
   // RG_SEG_STREAM=0 selects the one-segment-per-group kernel (A/B measurement knob).
   static const bool stream_on = !getenv("RG_SEG_STREAM") || atoi(getenv("RG_SEG_STREAM")) != 0;
+  // (segments per lane group G, rows in flight per lane U): measured on C5's radius CSR (one
+  // 20 000-node frame, 20 rows per segment on average, 63 at most) and on M's kNN CSR
+  // (192 000 segments of ~13 rows), scripts/seg_few.py: (1, 8) beat (2, 8) on both -- more
+  // waves, and a wave waits for its longest segment either way.  RG_SEG_CFG="G,U" selects
+  // another compiled pair (A/B knob, read per launch: the parity test sweeps it).
   constexpr int GPB = 256 / (64 / VEC);
-  constexpr int G = 2;
   if (stream_on && !g.idx && !g.seg_end && !g.bm && g.uni == 0 && g.C % 64 == 0) {
-    const int grid_s = ceil_div(ceil_div(g.n_seg, G), GPB);
+    int G = 1, U = 8;
+    if (const char* cfg = getenv("RG_SEG_CFG")) sscanf(cfg, "%d,%d", &G, &U);
 #define RG_STREAM_ARGS (const TS*)g.src, g.ld_src, g.seg_ptr, g.n_seg, g.C, (TO*)g.out, g.ld_out
-    if (op == RG_REDUCE_SUM)
-      segment_stream_kernel<TS, TO, RG_REDUCE_SUM, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
-    else if (op == RG_REDUCE_MEAN)
-      segment_stream_kernel<TS, TO, RG_REDUCE_MEAN, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
+#define RG_STREAM(G_, U_)                                                                        \
+  {                                                                                              \
+    const int grid_s = ceil_div(ceil_div(g.n_seg, G_), GPB);                                     \
+    if (op == RG_REDUCE_SUM)                                                                     \
+      segment_stream_kernel<TS, TO, RG_REDUCE_SUM, VEC, G_, true, U_><<<grid_s, 256, 0, st>>>(   \
+          RG_STREAM_ARGS);                                                                       \
+    else if (op == RG_REDUCE_MEAN)                                                               \
+      segment_stream_kernel<TS, TO, RG_REDUCE_MEAN, VEC, G_, true, U_><<<grid_s, 256, 0, st>>>(  \
+          RG_STREAM_ARGS);                                                                       \
+    else                                                                                         \
+      segment_stream_kernel<TS, TO, RG_REDUCE_MAX, VEC, G_, true, U_><<<grid_s, 256, 0, st>>>(   \
+          RG_STREAM_ARGS);                                                                       \
+  }
+    if (G == 2 && U == 8)
+      RG_STREAM(2, 8)
+    else if (G == 1 && U == 4)
+      RG_STREAM(1, 4)
+    else if (G == 2 && U == 4)
+      RG_STREAM(2, 4)
+    else if (G == 4 && U == 8)
+      RG_STREAM(4, 8)
+    else if (G == 1 && U == 16)
+      RG_STREAM(1, 16)
+    else if (G == 1 && U == 12)
+      RG_STREAM(1, 12)
     else
-      segment_stream_kernel<TS, TO, RG_REDUCE_MAX, VEC, G, true><<<grid_s, 256, 0, st>>>(RG_STREAM_ARGS);
+      RG_STREAM(1, 8)
+#undef RG_STREAM
 #undef RG_STREAM_ARGS
   } else if (op == RG_REDUCE_SUM)
     segment_reduce_kernel<TS, TO, RG_REDUCE_SUM, VEC><<<grid, 256, 0, st>>>(RG_SEG_ARGS);
@@ -324,7 +350,10 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
              ld_out);
   if (n_seg <= 0) return RG_OK;
   const SegArgs g = {src, ld_src, seg_ptr, nullptr, idx, 0, 0, nullptr, 0, n_seg, C, out, ld_out};
-  return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out),
+  // RG_SEG_V4=1: 16-bit rows as 8-B lane loads (16 lanes per 64 channels) -- A/B knob
+  const char* v4 = getenv("RG_SEG_V4");
+  return launch_any(op, src_dtype, out_dtype,
+                    vec8(C, ld_src, out_dtype, ld_out, src, out) && !(v4 && atoi(v4)),
                     (hipStream_t)stream, g);
 }
 

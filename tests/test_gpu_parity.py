@@ -12,6 +12,10 @@ edge_index bit-exact):
                                                          per output k (bf16_bound), >= 99.5 %
                                                          argmax agreement of class logits
 """
+import contextlib
+import itertools
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -484,9 +488,27 @@ def _sequential_segment_sum(src32: torch.Tensor, counts: torch.Tensor) -> torch.
     return acc
 
 
+@contextlib.contextmanager
+def _env(name, value):
+    """Set (or, for None, unset) one environment variable for the duration of a block."""
+    old = os.environ.get(name)
+    if value is None:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = value
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop(name, None)
+        else:
+            os.environ[name] = old
+
+
 def test_segment_stream_bit_exact(cuda_device):
-    """rg_segment_reduce sum / mean / max over a plain CSR (the streaming kernel: two segments per
-    lane group as one row stream, restarting the sum at each boundary) equals the in-order
+    """rg_segment_reduce sum / mean / max over a plain CSR (the streaming kernel: one or two
+    segments per lane group as one row stream, restarting the sum at each boundary, 8 / 16 / 32
+    rows in flight -- every compiled RG_SEG_CFG variant) equals the in-order
     float32 sum bit for bit: empty segments at every position of a group, an odd segment
     count, short (kNN-like) and long row runs, f32 and bf16 messages, C = 64 and 128; max:
     empty segments 0, as PyG / scatter_reduce(include_self=False)."""
@@ -500,22 +522,25 @@ def test_segment_stream_bit_exact(cuda_device):
     counts[-1] = 0
     ptr = torch.cat([torch.zeros(1, dtype=torch.int64), counts.cumsum(0)]).to(torch.int32).to(dev)
     E, S = int(counts.sum()), len(counts)
-    for C in (64, 128):
+    # RG_SEG_CFG: (segments per lane group, rows in flight per lane); RG_SEG_V4: 8-B bf16 lanes
+    variants = [(None, None), ('2,8', None), ('1,4', None), ('2,4', None), ('4,8', None),
+                ('1,16', None), ('1,12', None), (None, '1'), ('2,8', '1')]
+    for C, sdt, v in itertools.product((64, 128), (torch.float32, torch.bfloat16), variants):
         src = torch.randn(E, C, generator=g)
-        for sdt in (torch.float32, torch.bfloat16):
+        with _env('RG_SEG_CFG', v[0]), _env('RG_SEG_V4', v[1]):
             s_dev = src.to(sdt).to(dev)
             ref = _sequential_segment_sum(src.to(sdt).float(), counts)
             out = torch.empty(S, C, device=dev)
             engine.segment_reduce(s_dev, ptr, S, 'add', out)
-            assert torch.equal(out.cpu(), ref), (C, sdt)
+            assert torch.equal(out.cpu(), ref), (C, sdt, v)
             engine.segment_reduce(s_dev, ptr, S, 'mean', out)
             mean = ref / counts.clamp(min=1).to(torch.float32).view(-1, 1)
-            assert torch.equal(out.cpu(), mean), (C, sdt)
+            assert torch.equal(out.cpu(), mean), (C, sdt, v)
             engine.segment_reduce(s_dev, ptr, S, 'max', out)
             seg = torch.repeat_interleave(torch.arange(S), counts)
             mx = torch.zeros(S, C).scatter_reduce(0, seg.view(-1, 1).expand(-1, C),
                                                   src.to(sdt).float(), 'amax', include_self=False)
-            assert torch.equal(out.cpu(), mx), (C, sdt)
+            assert torch.equal(out.cpu(), mx), (C, sdt, v)
 
 
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
