@@ -210,32 +210,42 @@ def rank_frame_seeds(rank: int, frames: int, seed0: int):
 
 
 def scatter_aggregate_bench(gb, E, N, steps):
-    """The north-star scatter-aggregate kernel on its own: rg_segment_reduce (PyG aggr 'add',
-    gnn_blocks.py:57/106 -> scatter_add_ at edge_index[1]) over the step's destination-major
-    CSR, messages E x 64 already in HBM (synthetic values).  It is the aggregation of the
-    unfused paths (fp32, and bf16 shapes the fused kernel does not take); the default bf16
-    step fuses it into rg_conv_layer_fused.  Algorithmic bytes per launch:
-    E*C*s_msg + N*C*s_out + (N+1)*4.  Timed with HIP events on the stream it runs on
-    (torch's current stream: engine.segment_reduce launches there)."""
+    """The north-star scatter-aggregate kernel on its own: rg_segment_reduce_ordered (PyG aggr
+    'add', gnn_blocks.py:57/106 -> scatter_add_ at edge_index[1]) over the step's
+    destination-major CSR with its longest-first segment order (rg_segment_order, computed
+    once per graph like the CSR itself and reused by every layer; its own time is reported as
+    `order_ms`), messages E x 64 already in HBM (synthetic values).  It is the aggregation of
+    the unfused paths (max / mean aggregation, residual projections, shapes the fused kernels
+    do not take); the default steps fuse it into the conv kernels.  Algorithmic bytes per
+    launch: E*C*s_msg + N*C*s_out + (N+1)*4 (+ N*4 for the order).  Timed with
+    HIP events on the stream it runs on (torch's current stream: engine launches there)."""
     from graph_neural_network_for_radar_perception_amd import engine
     C = 64
     out = {}
     seg = gb.graph.seg_ptr
+    order = engine.segment_order(seg, N)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        engine.segment_order(seg, N)
+    b.record()
+    torch.cuda.synchronize()
+    out['order_ms'] = round(a.elapsed_time(b) / steps, 4)
     for name, tdt, s in (('bf16', torch.bfloat16, 2), ('fp32', torch.float32, 4)):
         msg = torch.randn((E, C), device=seg.device).to(tdt)
         agg = torch.empty((N, C), dtype=tdt, device=seg.device)
         for _ in range(2):
-            engine.segment_reduce(msg, seg, N, 'add', agg)
+            engine.segment_reduce_ordered(msg, seg, order, N, 'add', agg)
         # one event pair around `steps` back-to-back launches (a pair per launch adds its
         # own stream gap to every timed launch), avg = span / steps
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(steps):
-            engine.segment_reduce(msg, seg, N, 'add', agg)
+            engine.segment_reduce_ordered(msg, seg, order, N, 'add', agg)
         b.record()
         torch.cuda.synchronize()
         ms = a.elapsed_time(b) / steps
-        nbytes = E * C * s + N * C * s + (N + 1) * 4
+        nbytes = E * C * s + N * C * s + (N + 1) * 4 + N * 4
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {'avg_ms': round(ms, 4), 'bytes_per_launch': nbytes,
                      'achieved_gbs': round(gbs, 1), 'hbm_frac': round(gbs / HBM_PEAK_GBS, 4)}
@@ -979,8 +989,8 @@ def main():
         'forward_only_frames_per_s': round(r['forward_fps'], 2),
         'forward_algorithmic_tflops': round(r['forward_tflops'], 2),
         'roofline': r['roof'],
-        'scatter_aggregate': dict(r['scatter'], kernel='rg_segment_reduce sum over the step\'s '
-                                  'destination-major CSR (standalone; fused into conv_fused in '
+        'scatter_aggregate': dict(r['scatter'], kernel='rg_segment_reduce_ordered sum over the step\'s '
+                                  'destination-major CSR, longest-first segment order (standalone; fused into the conv kernels in '
                                   'the step)', bound='hbm', peak_gbs=HBM_PEAK_GBS),
         'kernels': r['kern'],
     }

@@ -162,6 +162,9 @@ _SIGNATURES = {
     'rg_gather_i32': (_I, [_P, _P, _I, _P, _P]),
     'rg_lower_bound_i32': (_I, [_P, _P, _L, _P, _I, _P, _P]),
     'rg_segment_reduce': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+    'rg_segment_order_workspace_size': (_S, []),
+    'rg_segment_order': (_I, [_P, _I, _P, _P, _S, _P]),
+    'rg_segment_reduce_ordered': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
     'rg_segment_reduce_ranges_workspace_size': (_S, [_L, _I, _I]),
     'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P, _S,
                                       _P]),

@@ -159,18 +159,23 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const TS* __restric
 // each boundary (segment pointers held one per lane of the group, read by shuffle).  Each
 // segment is still summed from its first row in order: bit-identical to the kernel above.
 // Sum / mean / max, no row index, C a multiple of 64.
+//
+// order (G = 1 only, else null): group i reduces segment order[i] (rg_segment_order: longest
+// first), so the segments a wave holds have similar lengths -- a wave waits for its longest.
 template <typename TS, typename TO, int OP, int VEC, int G, bool NT, int U = 8>
 __global__ __launch_bounds__(256) void segment_stream_kernel(const TS* __restrict__ src, int ld_src,
                                                              const int* __restrict__ seg_ptr,
+                                                             const int* __restrict__ order,
                                                              int n_seg, int C, TO* __restrict__ out,
                                                              int ld_out) {
   constexpr int LPS = 64 / VEC;
   constexpr int GPB = 256 / LPS;
   static_assert(G <= LPS, "one segment pointer per lane of the group");
   const int g = threadIdx.x % LPS;
-  const int s0 = (blockIdx.x * GPB + threadIdx.x / LPS) * G;
-  if (s0 >= n_seg) return;
-  const int ns = min(G, n_seg - s0);
+  const int lin = (blockIdx.x * GPB + threadIdx.x / LPS) * G;
+  if (lin >= n_seg) return;
+  const int s0 = (G == 1 && order) ? order[lin] : lin;
+  const int ns = min(G, n_seg - lin);
   const int my_ptr = seg_ptr[s0 + min(g, ns)];
   const int p_end = seg_ptr[s0 + ns];
   // ptr_at(j) is called with j uniform over the lane group (all its lanes active)
@@ -226,6 +231,7 @@ struct SegArgs {
   const void* src;
   int ld_src;
   const int* seg_ptr;
+  const int* order;  // rg_segment_order permutation (streaming kernel, G = 1), or null
   const int* seg_end;
   const int* idx;
   int uni, n_uni;
@@ -255,12 +261,17 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
   // another compiled pair (A/B knob, read per launch: the parity test sweeps it).
   constexpr int GPB = 256 / (64 / VEC);
   if (stream_on && !g.idx && !g.seg_end && !g.bm && g.uni == 0 && g.C % 64 == 0) {
-    int G = 1, U = 8;
+    // longest-first order (C5 sorted: bf16 0.56 -> 0.67 of HBM with 12 rows in flight and
+    // 8-B lanes, scripts/seg_few.py)
+    int G = 1, U = g.order ? 12 : 8;
     if (const char* cfg = getenv("RG_SEG_CFG")) sscanf(cfg, "%d,%d", &G, &U);
-#define RG_STREAM_ARGS (const TS*)g.src, g.ld_src, g.seg_ptr, g.n_seg, g.C, (TO*)g.out, g.ld_out
+    if (g.order) G = 1;
+#define RG_STREAM_ARGS \
+  (const TS*)g.src, g.ld_src, g.seg_ptr, ord_, g.n_seg, g.C, (TO*)g.out, g.ld_out
 #define RG_STREAM(G_, U_)                                                                        \
   {                                                                                              \
     const int grid_s = ceil_div(ceil_div(g.n_seg, G_), GPB);                                     \
+    const int* ord_ = G_ == 1 ? g.order : nullptr;                                               \
     if (op == RG_REDUCE_SUM)                                                                     \
       segment_stream_kernel<TS, TO, RG_REDUCE_SUM, VEC, G_, true, U_><<<grid_s, 256, 0, st>>>(   \
           RG_STREAM_ARGS);                                                                       \
@@ -349,7 +360,7 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
              "rg_segment_reduce: C=%d ld_src=%d ld_out=%d must be multiples of 4", C, ld_src,
              ld_out);
   if (n_seg <= 0) return RG_OK;
-  const SegArgs g = {src, ld_src, seg_ptr, nullptr, idx, 0, 0, nullptr, 0, n_seg, C, out, ld_out};
+  const SegArgs g = {src, ld_src, seg_ptr, nullptr, nullptr, idx, 0, 0, nullptr, 0, n_seg, C, out, ld_out};
   // RG_SEG_V4=1: 16-bit rows as 8-B lane loads (16 lanes per 64 channels) -- A/B knob
   const char* v4 = getenv("RG_SEG_V4");
   return launch_any(op, src_dtype, out_dtype,
@@ -382,16 +393,109 @@ extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_s
     // pass 1: 32-row block maxima of src, in src's dtype (exact)
     void* w = (void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
     const int nb = (int)((n_rows + RANGE_BLOCK - 1) / RANGE_BLOCK);
-    const SegArgs g1 = {src, ld_src, nullptr, nullptr, nullptr, RANGE_BLOCK, (int)n_rows,
+    const SegArgs g1 = {src, ld_src, nullptr, nullptr, nullptr, nullptr, RANGE_BLOCK, (int)n_rows,
                         nullptr, 0, nb, C, w, ldb};
     const int rc = launch_any(op, src_dtype, src_dtype,
                               vec8(C, ld_src, src_dtype, ldb, src, w), st, g1);
     if (rc) return rc;
     bm = w;
   }
-  const SegArgs g = {src, ld_src, seg_begin, seg_end, nullptr, 0, 0, bm, ldb, n_seg, C, out,
-                     ld_out};
+  const SegArgs g = {src, ld_src, seg_begin, nullptr, seg_end, nullptr, 0, 0, bm, ldb, n_seg, C,
+                     out, ld_out};
   return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out) &&
                                                   (!bm || ldb % 8 == 0),
                     st, g);
+}
+
+// ---- longest-first segment order (rg_segment_order): a counting sort of the segments by
+//      length, descending, lengths capped at ORD_BINS - 1, in ONE workgroup (the order is
+//      used for graphs of a few ten thousand segments, where one launch beats three plus a
+//      memset): per-wave LDS histograms (contention only inside a wave), the cursors of bin b
+//      = the segments in longer bins + those of bin b in lower waves, then each wave places
+//      its segments at its cursors.  The order inside a bin depends on timing; no result
+//      does (every segment's reduction is independent of the schedule).
+namespace rg {
+static constexpr int ORD_BINS = 256;
+static constexpr int ORD_T = 1024;
+static constexpr int ORD_W = ORD_T / 64;
+
+__device__ __forceinline__ int ord_bin(const int* seg_ptr, int s) {
+  return min(seg_ptr[s + 1] - seg_ptr[s], ORD_BINS - 1);
+}
+
+__global__ __launch_bounds__(ORD_T) void seg_order_kernel(const int* __restrict__ seg_ptr,
+                                                          int n_seg, int* __restrict__ order) {
+  __shared__ int cnt[ORD_W][ORD_BINS];  // per-wave counts, then per-wave cursors
+  __shared__ int tot[ORD_BINS];
+  const int t = threadIdx.x, w = t >> 6;
+  for (int i = t; i < ORD_W * ORD_BINS; i += ORD_T) (&cnt[0][0])[i] = 0;
+  __syncthreads();
+  for (int s = t; s < n_seg; s += ORD_T) atomicAdd(&cnt[w][ord_bin(seg_ptr, s)], 1);
+  __syncthreads();
+  if (t < ORD_BINS) {  // thread t: bin ORD_BINS - 1 - t (longest first)
+    const int bn = ORD_BINS - 1 - t;
+    int run = 0;
+    for (int v = 0; v < ORD_W; ++v) {
+      const int c = cnt[v][bn];
+      cnt[v][bn] = run;  // offset of wave v inside the bin
+      run += c;
+    }
+    tot[t] = run;
+  }
+  __syncthreads();
+  // inclusive scan of tot over the descending bins (Hillis-Steele, 8 steps)
+  for (int o = 1; o < ORD_BINS; o <<= 1) {
+    const int v = t < ORD_BINS && t >= o ? tot[t - o] : 0;
+    __syncthreads();
+    if (t < ORD_BINS) tot[t] += v;
+    __syncthreads();
+  }
+  if (t < ORD_BINS) {
+    const int bn = ORD_BINS - 1 - t;
+    const int base = t > 0 ? tot[t - 1] : 0;
+    for (int v = 0; v < ORD_W; ++v) cnt[v][bn] += base;
+  }
+  __syncthreads();
+  for (int s = t; s < n_seg; s += ORD_T) order[atomicAdd(&cnt[w][ord_bin(seg_ptr, s)], 1)] = s;
+}
+}  // namespace rg
+
+extern "C" size_t rg_segment_order_workspace_size(void) { return 0; }
+
+extern "C" int rg_segment_order(const int* seg_ptr, int n_seg, int* order, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  if (n_seg <= 0) return RG_OK;
+  seg_order_kernel<<<1, ORD_T, 0, (hipStream_t)stream>>>(seg_ptr, n_seg, order);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// graphs with more segments than this keep the plain order in rg_segment_reduce_ordered:
+// M's 192 000 kNN segments (lengths 10..25, rows contiguous in node order) measured
+// 0.73 -> 0.61-0.66 of HBM in bf16 with the longest-first order (the groups' rows then lie
+// scattered), C5's 20 000 radius segments (20 rows on average, 63 at most) 0.55 -> 0.65
+#ifndef RG_SEG_ORDER_MAX
+#define RG_SEG_ORDER_MAX 65536
+#endif
+
+extern "C" int rg_segment_reduce_ordered(const void* src, int src_dtype, int ld_src,
+                                         const int* seg_ptr, const int* order, int n_seg, int C,
+                                         int op, void* out, int out_dtype, int ld_out,
+                                         void* stream) {
+  RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
+  RG_REQUIRE(check_shape(C, ld_src, ld_out) && C % 64 == 0, RG_ERR_UNSUPPORTED,
+             "rg_segment_reduce_ordered: C=%d must be a multiple of 64, ld_src=%d ld_out=%d of 4",
+             C, ld_src, ld_out);
+  RG_REQUIRE(order, RG_ERR_ARG, "rg_segment_reduce_ordered: order missing");
+  if (n_seg <= 0) return RG_OK;
+  const bool use = n_seg <= RG_SEG_ORDER_MAX;
+  const SegArgs g = {src, ld_src, seg_ptr, use ? order : nullptr, nullptr, nullptr, 0, 0, nullptr,
+                     0, n_seg, C, out, ld_out};
+  // with the order, 16-bit rows as 8-B lane loads (16 lanes per 64 channels: twice the lane
+  // groups; C5 bf16 0.57 -> 0.65); RG_SEG_V8=1 forces 16-B lanes (A/B knob)
+  const char* v8s = getenv("RG_SEG_V8");
+  const bool v8 = (!use || (v8s && atoi(v8s))) && vec8(C, ld_src, out_dtype, ld_out, src, out);
+  return launch_any(op, src_dtype, out_dtype, v8, (hipStream_t)stream, g);
 }

@@ -446,6 +446,32 @@ def segment_reduce(src: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int, op: str
     return out
 
 
+def segment_order(seg_ptr: torch.Tensor, n_seg: int) -> torch.Tensor:
+    """Longest-first permutation of the CSR's segments (rg_segment_order), int32 [n_seg]."""
+    lib = nat.lib()
+    order = torch.empty(max(int(n_seg), 1), dtype=torch.int32, device=seg_ptr.device)
+    ws = torch.empty(max(lib.rg_segment_order_workspace_size(), 1), dtype=torch.uint8,
+                     device=seg_ptr.device)
+    nat.check(lib.rg_segment_order(seg_ptr.data_ptr(), int(n_seg), order.data_ptr(),
+                                   ws.data_ptr(), ws.numel(), nat.stream_ptr(seg_ptr.device)),
+              'rg_segment_order')
+    return order[:int(n_seg)]
+
+
+def segment_reduce_ordered(src: torch.Tensor, seg_ptr: torch.Tensor, order: torch.Tensor,
+                           n_seg: int, op: str, out: torch.Tensor):
+    """rg_segment_reduce over a plain CSR with the longest-first schedule of `order`
+    (rg_segment_reduce_ordered): bit-identical to segment_reduce."""
+    lib = nat.lib()
+    C = src.shape[1]
+    nat.check(lib.rg_segment_reduce_ordered(src.data_ptr(), _dt_code(src), src.stride(0),
+                                            seg_ptr.data_ptr(), order.data_ptr(), int(n_seg), C,
+                                            nat.REDUCE[op], out.data_ptr(), _dt_code(out),
+                                            out.stride(0), nat.stream_ptr(src.device)),
+              'rg_segment_reduce_ordered')
+    return out
+
+
 # --------------------------------------------------------------------------- graphs
 class DeviceGraph:
     """Destination-major CSR of a (batched) graph plus its link pairs.

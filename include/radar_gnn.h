@@ -525,6 +525,24 @@ int rg_segment_reduce(const void* src, int src_dtype, int ld_src, const int* seg
                       const int* idx, int n_seg, int C, int op, void* out, int out_dtype,
                       int ld_out, void* stream);
 
+/* Longest-first schedule for rg_segment_reduce_ordered: order int32[n_seg] = a
+ * permutation of the segments by length (seg_ptr[s+1] - seg_ptr[s], capped at 255),
+ * descending (a counting sort in one workgroup; ties in timing order).  Computed once
+ * per graph, reused by every layer's aggregation.  workspace:
+ * rg_segment_order_workspace_size() bytes (currently 0; may be NULL). */
+size_t rg_segment_order_workspace_size(void);
+int rg_segment_order(const int* seg_ptr, int n_seg, int* order, void* workspace,
+                     size_t workspace_bytes, void* stream);
+/* rg_segment_reduce (no row index, C a multiple of 64) with lane group i reducing
+ * segment order[i]: the segments one wave holds then have similar lengths (a wave waits
+ * for its longest).  Graphs of more than 65 536 segments keep the plain order (their
+ * rows' locality is worth more: M's kNN CSR).  Same results as rg_segment_reduce, bit for bit: every segment is
+ * still summed from its first row in order.  Replaces the PyG aggregation scatter at
+ * edge_index[1] (gnn_blocks.py:57, 106) like rg_segment_reduce. */
+int rg_segment_reduce_ordered(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
+                              const int* order, int n_seg, int C, int op, void* out,
+                              int out_dtype, int ld_out, void* stream);
+
 /* The same reductions over explicit row ranges [seg_begin[s], seg_end[s]) of src
  * [n_rows] (ranges may overlap): the per-object max-pool of the classifier GNN, whose
  * reference ranges are not a CSR (classifier/classifier.py:60-68, see

@@ -45,32 +45,45 @@ def main():
     cfgs = [None, '2,8', '1,4', '1,16', '1,12']
     c5 = radius_ptr(20_000, 2.5)
     # C5 with its segments in descending length (the bound of a longest-first schedule)
-    for name_g, counts in (('C5', c5), ('C5_sorted', np.sort(c5)[::-1].copy()),
-                           ('M', knn_ptr(64, 3000, 10))):
+    for name_g, counts in (('C5', c5), ('M', knn_ptr(64, 3000, 10))):
         N = len(counts)
         ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)).to(dev)
         E = int(counts.sum())
         for name, tdt, s in (('bf16', torch.bfloat16, 2), ('fp32', torch.float32, 4)):
             msg = torch.randn((E, C), device=dev, generator=torch.Generator(dev).manual_seed(1)).to(tdt)
             agg = torch.empty((N, C), dtype=tdt, device=dev)
-            for cfg in cfgs:
-                for v4 in ((None, '1') if tdt == torch.bfloat16 else (None,)):
-                    for key, val in (('RG_SEG_CFG', cfg), ('RG_SEG_V4', v4)):
+            order = engine.segment_order(ptr, N)
+            runs = [(cfg, v4, False) for cfg in cfgs
+                    for v4 in ((None, '1') if tdt == torch.bfloat16 else (None,))]
+            runs += [(cfg, v8, True) for cfg in (None, '1,8', '1,16')
+                     for v8 in ((None, '1') if tdt == torch.bfloat16 else (None,))]
+            for cfg, v4, ordered in runs:
+                if True:
+                    key4 = 'RG_SEG_V8' if ordered else 'RG_SEG_V4'
+                    for key in ('RG_SEG_V4', 'RG_SEG_V8'):
+                        os.environ.pop(key, None)
+                    for key, val in (('RG_SEG_CFG', cfg), (key4, v4)):
                         if val is None:
                             os.environ.pop(key, None)
                         else:
                             os.environ[key] = val
+                    def run():
+                        if ordered:
+                            engine.segment_reduce_ordered(msg, ptr, order, N, 'add', agg)
+                        else:
+                            engine.segment_reduce(msg, ptr, N, 'add', agg)
                     for _ in range(3):
-                        engine.segment_reduce(msg, ptr, N, 'add', agg)
+                        run()
                     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     a.record()
                     for _ in range(R):
-                        engine.segment_reduce(msg, ptr, N, 'add', agg)
+                        run()
                     b.record()
                     torch.cuda.synchronize()
                     ms = a.elapsed_time(b) / R
                     nbytes = E * C * s + N * C * s + (N + 1) * 4
-                    print(json.dumps({'graph': name_g, 'cfg': cfg or 'default', 'v4': v4, 'dtype': name,
+                    print(json.dumps({'graph': name_g, 'cfg': cfg or 'default', 'ordered': ordered,
+                                      ('v8' if ordered else 'v4'): v4, 'dtype': name,
                                       'E': E, 'max_deg': int(counts.max()), 'ms': round(ms, 4),
                                       'hbm_frac': round(nbytes / ms / 1e6 / 8000, 4),
                                       'checksum': float(agg.float().double().sum())}), flush=True)
