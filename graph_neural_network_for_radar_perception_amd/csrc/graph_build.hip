@@ -921,6 +921,139 @@ __global__ __launch_bounds__(KNN_BLOCK) void knn_select_coop(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Pure radius graph (compute_ball_query + np.where, graph_features.py:11-22, 79) without
+// the N x N_f bitset: the ball relation is symmetric bit for bit (sqdist of (i, j) and
+// (j, i) square the same magnitudes), so row i's columns are exactly the points j != i
+// with d(i, j) <= eps^2, ascending.  A group of CL lanes per row walks the rings
+// cooperatively (ring_coop) twice: radius_count_coop counts the row (= its ball degree),
+// and after the scan radius_emit_coop gathers the row's columns in LDS (ballot-compacted)
+// and writes each at its rank among them -- ascending, the np.where order.  A row with
+// more than RAD_CAP columns instead sweeps the frame's index range in windows of
+// 32 x RAD_CAP indices, each an LDS bitmask emitted in bit order.  (The bitset path wrote
+// and scanned 4 x N x N_f / 32 bytes: 50 MB at C5's 20 000-point frame.)
+// ---------------------------------------------------------------------------------
+#ifndef RG_RADIUS_COOP
+#define RG_RADIUS_COOP 1
+#endif
+static constexpr int RAD_CAP = 128;
+
+template <typename F>
+__device__ __forceinline__ void radius_walk(const FrameGrid& g, const int* __restrict__ cs_r,
+                                            const float4* __restrict__ pts_r,
+                                            const int* __restrict__ cs_c,
+                                            const float4* __restrict__ pts_c, int cx, int cy,
+                                            float xi, float yi, int il, float eps2, int sl,
+                                            F&& in_ball) {
+  const int rmax = max(max(cx, g.gw - 1 - cx), max(cy, g.gh - 1 - cy));
+  for (int r = 0; r <= rmax; ++r) {
+    ring_coop(g, cs_r, pts_r, cs_c, pts_c, cx, cy, r, sl, [&](const float4& q, bool ok, int) {
+      const int j = __float_as_int(q.z);
+      in_ball(j, ok && (sqdist(xi, yi, q.x, q.y) <= eps2) && (j != il));
+    });
+    if (eps2 < ring_bound(g, r)) break;
+  }
+}
+
+__global__ __launch_bounds__(KNN_BLOCK) void radius_count_coop(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const float4* __restrict__ pts_t, const int* __restrict__ cell_start_t,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, float eps2, int* __restrict__ ball_deg,
+    int* __restrict__ cnt) {
+  const int sl = threadIdx.x & (CL - 1), grp = threadIdx.x / CL;
+  const int t = blockIdx.x * CO_ROWS + grp;
+  if (t >= n_nodes) return;  // group-uniform
+  const int f = row_frame[t];
+  const FrameGrid g = fg[f];
+  const float4 me = pts[t];
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  int ball = 0;
+  radius_walk(g, cell_start, pts, cell_start_t, pts_t, cme % g.gw, cme / g.gw, me.x, me.y, il,
+              eps2, sl, [&](int, bool in) { ball += in ? 1 : 0; });
+  ball = grp_sum(ball);
+  if (sl == 0) {
+    const int row = frame_ptr[f] + il;
+    ball_deg[row] = ball;
+    cnt[row] = ball;
+  }
+}
+
+__global__ __launch_bounds__(KNN_BLOCK) void radius_emit_coop(
+    const float4* __restrict__ pts, const int* __restrict__ cell_start,
+    const float4* __restrict__ pts_t, const int* __restrict__ cell_start_t,
+    const int* __restrict__ row_frame, const FrameGrid* __restrict__ fg,
+    const int* __restrict__ frame_ptr, int n_nodes, float eps2,
+    const int* __restrict__ row_ptr, int* __restrict__ col, long cap) {
+  __shared__ int buf_s[CO_ROWS][RAD_CAP];
+  const int sl = threadIdx.x & (CL - 1), grp = threadIdx.x / CL;
+  const int lane = __lane_id();
+  const uint64_t gm = ((1ull << CL) - 1ull) << (lane & ~(CL - 1));
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int t = blockIdx.x * CO_ROWS + grp;
+  if (t >= n_nodes) return;  // group-uniform
+  const int f = row_frame[t];
+  const FrameGrid g = fg[f];
+  const int base = frame_ptr[f];
+  const float4 me = pts[t];
+  const int il = __float_as_int(me.z);
+  const int cme = __float_as_int(me.w) - g.cell0;
+  const int cx = cme % g.gw, cy = cme / g.gw;
+  const int row = base + il;
+  const long p0 = row_ptr[row], p1 = row_ptr[row + 1];
+  if (p1 > cap) return;  // overflow: the caller sees n_edges > capacity (as row_emit)
+  const int n = (int)(p1 - p0);
+  int* B = buf_s[grp];
+  if (n <= RAD_CAP) {
+    int nb = 0;
+    radius_walk(g, cell_start, pts, cell_start_t, pts_t, cx, cy, me.x, me.y, il, eps2, sl,
+                [&](int j, bool in) {
+                  const uint64_t m = __ballot(in) & gm;
+                  if (in) B[nb + __popcll(m & lt)] = j;
+                  nb += __popcll(m);
+                });
+    grp_sync();
+    for (int e = sl; e < n; e += CL) {
+      const int je = B[e];
+      int rank = 0;
+      for (int e2 = 0; e2 < n; ++e2) rank += B[e2] < je ? 1 : 0;
+      col[p0 + rank] = base + je;
+    }
+    return;
+  }
+  // a long row: windows of 32 x RAD_CAP frame-local indices, one LDS bitmask each
+  const int nf = frame_ptr[f + 1] - base;
+  constexpr int WPL = RAD_CAP / CL;  // mask words per lane, contiguous
+  uint32_t* M = (uint32_t*)B;
+  long pos = p0;
+  for (int w0 = 0; w0 < nf; w0 += 32 * RAD_CAP) {
+    grp_sync();
+    for (int w = sl; w < RAD_CAP; w += CL) M[w] = 0u;
+    grp_sync();
+    radius_walk(g, cell_start, pts, cell_start_t, pts_t, cx, cy, me.x, me.y, il, eps2, sl,
+                [&](int j, bool in) {
+                  const int o = j - w0;
+                  if (in && o >= 0 && o < 32 * RAD_CAP) atomicOr(M + (o >> 5), 1u << (o & 31));
+                });
+    grp_sync();
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) c += __popc(M[WPL * sl + w]);
+    long p = pos + grp_incl_scan(c, sl) - c;
+#pragma unroll
+    for (int w = 0; w < WPL; ++w) {
+      uint32_t word = M[WPL * sl + w];
+      while (word) {
+        const int bit = __ffs(word) - 1;
+        word &= word - 1;
+        col[p++] = base + w0 + 32 * (WPL * sl + w) + bit;
+      }
+    }
+    pos += grp_sum(c);
+  }
+}
+
 // column-major copy of the grid (for_ring_rc): transposed cell counts, then points
 // scattered by transposed cell (cell index cell0 + cx * gh + cy)
 __global__ void grid_transpose_counts(const FrameGrid* __restrict__ fg, int cpf, long n_cells,
@@ -1283,8 +1416,9 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
     return RG_OK;
   }
   const int W = (max_frame_nodes + 31) / 32;
-  // the cooperative selection zeroes its own bitset rows
-  if (!(RG_KNN_COOP && mode == RG_GRAPH_KNN))
+  const bool rad_coop = RG_RADIUS_COOP && mode == RG_GRAPH_RADIUS;
+  // the cooperative selection zeroes its own bitset rows; the radius path has none
+  if (!(RG_KNN_COOP && mode == RG_GRAPH_KNN) && !rad_coop)
     RG_CHECK_HIP(hipMemsetAsync(ws.bits, 0, (size_t)n_nodes * W * sizeof(uint32_t), st));
   build_init<<<ceil_div(max((long)n_nodes, ws.n_cells), 256), 256, 0, st>>>(
       frame_ptr, n_frames, ws.row_base, ws.row_frame, n_nodes, ws.redo, ws.n_cells, ws.cell_cnt,
@@ -1312,6 +1446,19 @@ extern "C" int rg_build_graph(const float* px, const float* py, const int* frame
                                                          ws.cell_of, n_nodes, ws.cursor_t, ws.pts_t,
                                                          ws.cell_start_t);
   RG_LAUNCH_CHECK();
+  if (rad_coop) {
+    radius_count_coop<<<ceil_div(n_nodes, CO_ROWS), KNN_BLOCK, 0, st>>>(
+        ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr, n_nodes,
+        eps2, ball_degree, ws.cnt);
+    RG_LAUNCH_CHECK();
+    int rc = exclusive_scan(ws.cnt, n_nodes, row_ptr, n_edges_out, ws.scan_ws, st);
+    if (rc) return rc;
+    radius_emit_coop<<<ceil_div(n_nodes, CO_ROWS), KNN_BLOCK, 0, st>>>(
+        ws.pts, ws.cell_start, ws.pts_t, ws.cell_start_t, ws.row_frame, ws.fg, frame_ptr, n_nodes,
+        eps2, row_ptr, col, col_capacity);
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
   switch (K) {
     case 1: launch_knn<1>(st, px, py, frame_ptr, n_nodes, 1, eps2, mode, ws, ball_degree, W); break;
     case 2: launch_knn<2>(st, px, py, frame_ptr, n_nodes, kk, eps2, mode, ws, ball_degree, W); break;
