@@ -1318,7 +1318,9 @@ static size_t graph_ws_layout(int n_nodes, int n_frames, int max_frame_nodes, in
     off += align_up(bytes);
     return p;
   };
-  char* p_bits = take((size_t)n_nodes * W * sizeof(uint32_t));
+  // the pure radius graph builds its CSR without the bitset (radius_count / emit_coop)
+  const bool no_bits = RG_RADIUS_COOP && mode == RG_GRAPH_RADIUS;
+  char* p_bits = take(no_bits ? 0 : (size_t)n_nodes * W * sizeof(uint32_t));
   char* p_idx = take((size_t)n_nodes * (K > 0 ? K : 1) * sizeof(int));
   char* p_cnt = take((size_t)n_nodes * sizeof(int));
   char* p_rb = take((size_t)n_nodes * sizeof(int));

@@ -460,6 +460,61 @@ __global__ __launch_bounds__(256) void gather_segsum_kernel(
   }
 }
 
+// The same sums as a row stream per lane group (the streaming scatter-aggregate of
+// segment_reduce.hip): 16 lanes per node, one 16-B piece of 4 columns per lane and row, U
+// rows in flight per lane (their list indices first, then the rows), each node's rows
+// summed in list order -- the order of gather_segsum_kernel, whose wave per node walked its
+// rows one dependent load at a time (44 us per call on c4's 300 k edges).  Columns in
+// passes of 64; needs 16-B aligned rows (ld_src, col0, width, ld_out multiples of 4).
+template <bool SCALED, int U = 8>
+__global__ __launch_bounds__(256) void gather_segsum_stream(
+    const float* __restrict__ src, int ld_src, int col0, int width, const int* __restrict__ ptr,
+    const int* __restrict__ list, const float* __restrict__ scale, int n_nodes,
+    float* __restrict__ out, int ld_out, int accumulate) {
+  const int sl = threadIdx.x & 15;
+  const int v = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (v >= n_nodes) return;  // group-uniform
+  const int b = ptr[v], e = ptr[v + 1];
+  for (int c0 = 0; c0 < width; c0 += 64) {
+    const int c = c0 + 4 * sl;
+    const bool on = c < width;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int p = b; p < e; p += U) {
+      int row[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = p + u < e ? p + u : e - 1;
+        row[u] = list ? list[q] : q;
+      }
+      f32x4 x[U];
+      float sc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u] = on ? *(const f32x4*)(src + (size_t)row[u] * ld_src + col0 + c)
+                  : (f32x4){0.f, 0.f, 0.f, 0.f};
+        sc[u] = SCALED ? scale[row[u]] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (p + u < e) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i] = SCALED ? __fmaf_rn(x[u][i], sc[u], acc[i]) : __fadd_rn(acc[i], x[u][i]);
+        }
+      }
+    }
+    if (on) {
+      f32x4* o = (f32x4*)(out + (size_t)v * ld_out + c);
+      if (accumulate) {
+        const f32x4 old = *o;
+        acc = (f32x4){__fadd_rn(old[0], acc[0]), __fadd_rn(old[1], acc[1]),
+                      __fadd_rn(old[2], acc[2]), __fadd_rn(old[3], acc[3])};
+      }
+      *o = acc;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ segment max backward
 __global__ void segmax_backward_kernel(const float* __restrict__ h, int ld_h, int C,
                                        const int* __restrict__ cptr, const int* __restrict__ cidx,
@@ -785,6 +840,20 @@ extern "C" int rg_gather_segment_sum(const float* src, int ld_src, int col0, int
   RG_REQUIRE(width >= 1 && width <= 256, RG_ERR_UNSUPPORTED, "rg_gather_segment_sum: width %d",
              width);
   if (n_nodes <= 0) return RG_OK;
+  const char* gss = getenv("RG_GSS_STREAM");  // per call: the parity test compares both kernels
+  const bool stream_on = !gss || atoi(gss) != 0;
+  const bool al = ld_src % 4 == 0 && col0 % 4 == 0 && width % 4 == 0 && ld_out % 4 == 0 &&
+                  (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
+  if (stream_on && al) {
+    if (scale)
+      gather_segsum_stream<true><<<ceil_div(n_nodes, 16), 256, 0, (hipStream_t)stream>>>(
+          src, ld_src, col0, width, ptr, list, scale, n_nodes, out, ld_out, accumulate);
+    else
+      gather_segsum_stream<false><<<ceil_div(n_nodes, 16), 256, 0, (hipStream_t)stream>>>(
+          src, ld_src, col0, width, ptr, list, scale, n_nodes, out, ld_out, accumulate);
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
   int blocks = ceil_div(n_nodes, 4);
   if (blocks > 4096) blocks = 4096;
   gather_segsum_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(

@@ -339,3 +339,70 @@ def test_f32_tape_kernel_matches_generic(cuda_device, monkeypatch):
             close(t1.a[l], t0.a[l], f'{name} a{l}')
         for l, (a, b) in enumerate(zip(d1, d0)):
             close(a, b, f'{name} dX{l}')
+
+
+def test_gather_segment_sum_stream_matches_sequential(cuda_device):
+    """rg_gather_segment_sum's streaming kernel (16 lanes per node, 8 rows in flight) sums each
+    node's rows in list order: without a scale bit-identical to the float32 sequential sum (and
+    to the one-wave-per-node kernel, RG_GSS_STREAM=0); with a per-row scale within one rounding
+    per term of it.  Incidence lists (random rows), the identity CSR, column windows of a wider
+    row (col0 / width / ld_src as the message-input transposes use them), accumulate, empty
+    nodes and a 300-row node."""
+    import os
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    dev = cuda_device
+    lib = nat.lib()
+    g = torch.Generator().manual_seed(3)
+    n, E, ld = 3001, 40000, 192
+    counts = torch.randint(0, 27, (n,), generator=g)
+    counts[::11] = 0
+    counts[5] = 300
+    counts[-1] = E - int(counts[:-1].sum()) if int(counts[:-1].sum()) < E else 0
+    tot = int(counts.sum())
+    ptr = torch.cat([torch.zeros(1, dtype=torch.int64), counts.cumsum(0)]).to(torch.int32)
+    lst = torch.randint(0, E, (tot,), generator=g, dtype=torch.int32)
+    src = torch.randn(E, ld, generator=g)
+    scale = torch.rand(E, generator=g) + 0.5
+
+    def run(col0, width, use_list, use_scale, accumulate, stream):
+        out = torch.randn(n, 72, generator=torch.Generator().manual_seed(9)).to(dev)
+        os.environ['RG_GSS_STREAM'] = '1' if stream else '0'
+        try:
+            s_dev, p_dev = src.to(dev), ptr.to(dev)
+            l_dev, c_dev = lst.to(dev), scale.to(dev)
+            nat.check(lib.rg_gather_segment_sum(
+                s_dev.data_ptr(), ld, col0, width, p_dev.data_ptr(),
+                l_dev.data_ptr() if use_list else None, c_dev.data_ptr() if use_scale else None,
+                n, out.data_ptr(), 72, int(accumulate), nat.stream_ptr(dev)), 'gss')
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop('RG_GSS_STREAM', None)
+        return out.cpu()
+
+    for col0, width in ((0, 64), (64, 64), (128, 64), (4, 72)):
+        for use_list, use_scale, acc in ((True, False, False), (True, False, True),
+                                         (True, True, False), (False, False, True)):
+            if not use_list and tot > E:
+                continue
+            got = run(col0, width, use_list, use_scale, acc, True)
+            old = run(col0, width, use_list, use_scale, acc, False)
+            # float32 sequential reference
+            base = torch.randn(n, 72, generator=torch.Generator().manual_seed(9))
+            ref = base.clone() if acc else torch.zeros(n, 72)
+            a = torch.zeros(n, width)
+            rows = lst.long() if use_list else torch.arange(tot)
+            for j in range(int(counts.max())):
+                m = counts > j
+                r = rows[ptr[:-1].long()[m] + j]
+                term = src[r, col0:col0 + width]
+                if use_scale:
+                    term = (term.double() * scale[r].double().view(-1, 1))
+                    a[m] = (a[m].double() + term).float()
+                else:
+                    a[m] = a[m] + term
+            ref[:, :width] = (ref[:, :width] + a) if acc else a
+            if use_scale:
+                assert torch.allclose(got[:, :width], ref[:, :width], rtol=1e-5, atol=1e-5)
+            else:
+                assert torch.equal(got[:, :width], ref[:, :width]), (col0, width, use_list, acc)
+                assert torch.equal(got, old), (col0, width, use_list, acc)
