@@ -264,12 +264,30 @@ __global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restric
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  for (long rb = r_begin; rb < r_end; rb += GR) {
-    for (int t = threadIdx.x; t < GR * (OC / 4); t += 256) {
+  // staging: every dz / x load of a block (x gathered for the GATHER3 / PAIRADD modes) is
+  // issued before the first LDS store, so a thread's ~10 row pieces are in flight together
+  // (a store-per-load loop waited one gather round trip per piece).  Carrying the next
+  // block's pieces through the MFMAs instead (a register double buffer) took the 192-wide
+  // gathered tiles to 256 VGPRs + 192 AGPRs, one wave per SIMD: not kept
+  // x pieces: a thread keeps ONE column group for every row it stages (xc fixed, rows xr0,
+  // xr0 + XR, ...), so the segment test of the gathered input modes is decided once per
+  // thread, not per piece (IC = 192: 48 groups, 5 rows per pass, 240 threads busy)
+  constexpr int ZI = GR * (OC / 4);   // dz f32x4 items per staged block
+  constexpr int ZT = (ZI + 255) / 256;
+  constexpr int XG = IC / 4;                    // x column groups
+  constexpr int XR = 256 / XG < GR ? 256 / XG : GR;  // rows per pass
+  constexpr int XT = (GR + XR - 1) / XR;        // passes
+  const bool xon = (int)threadIdx.x < XR * XG;
+  const int xc = 4 * ((int)threadIdx.x % XG), xr0 = (int)threadIdx.x / XG;
+  f32x4 zr[ZT], xr[XT];
+  auto fetch = [&](long rb) {
+#pragma unroll
+    for (int j = 0; j < ZT; ++j) {
+      const int t = threadIdx.x + 256 * j;
       const int rr = t / (OC / 4), c = 4 * (t % (OC / 4));
       const long row = rb + rr;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row < r_end) {
+      if (t < ZI && row < r_end) {
         const float* pz = dz + (size_t)row * lddz + o0 + c;
         if (vec_z && o0 + c + 4 <= out_dim) {
           v = *(const f32x4*)pz;
@@ -278,15 +296,32 @@ __global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restric
           for (int e = 0; e < 4; ++e) v[e] = o0 + c + e < out_dim ? pz[e] : 0.f;
         }
       }
-      *(f32x4*)(sZ + rr * SZ + c) = v;
+      zr[j] = v;
     }
-    for (int t = threadIdx.x; t < GR * (IC / 4); t += 256) {
-      const int rr = t / (IC / 4), c = 4 * (t % (IC / 4));
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+      const int rr = xr0 + XR * j;
       const long row = rb + rr;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (row < r_end && i0 + c < in.in_dim) v = x_chunk(in, row, i0 + c, vec_x);
-      *(f32x4*)(sX + rr * SX + c) = v;
+      if (xon && rr < GR && row < r_end && i0 + xc < in.in_dim) v = x_chunk(in, row, i0 + xc, vec_x);
+      xr[j] = v;
     }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < ZT; ++j) {
+      const int t = threadIdx.x + 256 * j;
+      if (t < ZI) *(f32x4*)(sZ + (t / (OC / 4)) * SZ + 4 * (t % (OC / 4))) = zr[j];
+    }
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+      const int rr = xr0 + XR * j;
+      if (xon && rr < GR) *(f32x4*)(sX + rr * SX + xc) = xr[j];
+    }
+  };
+  for (long rb = r_begin; rb < r_end; rb += GR) {
+    fetch(rb);
+    put();
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < GR / 4; ++ks) {
@@ -355,14 +390,16 @@ static size_t grad_ws_bytes(const GradGeom& g) {
   return (grad_part_floats(g) + (size_t)g.nchunk * g.ot * 64 * g.ow) * sizeof(float);
 }
 
-// dW / db += the chunk partials, summed in chunk order: 64 consecutive (o, i) entries
-// per workgroup, wave w sums chunks w, w + 4, ... and the four wave sums combine in a
-// fixed order
-__global__ __launch_bounds__(256) void linear_grad_reduce(
+// dW / db += the chunk partials in a fixed order: 64 consecutive (o, i) entries per
+// workgroup, wave w of RW sums chunks w, w + RW, ... (eight loads in flight) and the RW wave
+// sums combine in a fixed pairwise tree.  (Four waves per workgroup left ~70 workgroups on
+// the chip for a 64 x 64 layer's 512 chunks: 16 dependent rounds per thread, 15 us.)
+static constexpr int RW = 16;
+__global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
     const float* __restrict__ part, const float* __restrict__ part_b, int nchunk, int ot_n,
     int it_n, int oc, int ic, int out_dim, int in_dim, float* __restrict__ dW,
     float* __restrict__ db) {
-  __shared__ float red[4][64];
+  __shared__ float red[RW][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long t = (long)blockIdx.x * 64 + lane;
   const long total = (long)out_dim * (in_dim + 1);
@@ -374,18 +411,23 @@ __global__ __launch_bounds__(256) void linear_grad_reduce(
     const int ot = o / oc, oo = o % oc;
     if (i < in_dim) {
       const int it = i / ic, ii = i % ic;
-#pragma unroll 8  // eight partial loads in flight; still added in chunk order
-      for (int c = wave; c < nchunk; c += 4)
+#pragma unroll 8
+      for (int c = wave; c < nchunk; c += RW)
         s += part[((size_t)(c * ot_n + ot) * it_n + it) * oc * ic + (size_t)oo * ic + ii];
     } else {
 #pragma unroll 8
-      for (int c = wave; c < nchunk; c += 4) s += part_b[((size_t)c * ot_n + ot) * oc + oo];
+      for (int c = wave; c < nchunk; c += RW) s += part_b[((size_t)c * ot_n + ot) * oc + oo];
     }
   }
   red[wave][lane] = s;
   __syncthreads();
+#pragma unroll
+  for (int h = RW / 2; h > 0; h >>= 1) {
+    if (wave < h) red[wave][lane] += red[wave + h][lane];
+    __syncthreads();
+  }
   if (wave == 0 && t < total) {
-    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    const float v = red[0][lane];
     if (i < in_dim) dW[(size_t)o * in_dim + i] += v;
     else if (db) db[o] += v;
   }
@@ -795,7 +837,7 @@ extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim,
 #undef RG_GRAD_CASE
   RG_LAUNCH_CHECK();
   const long total = (long)out_dim * (in_dim + 1);
-  linear_grad_reduce<<<ceil_div(total, 64), 256, 0, st>>>(part, part_b, g.nchunk, g.ot, g.it,
+  linear_grad_reduce<<<ceil_div(total, 64), 64 * RW, 0, st>>>(part, part_b, g.nchunk, g.ot, g.it,
                                                            64 * g.ow, 16 * g.nt, out_dim, in_dim,
                                                            dW, db);
   RG_LAUNCH_CHECK();
