@@ -406,3 +406,73 @@ def test_gather_segment_sum_stream_matches_sequential(cuda_device):
             else:
                 assert torch.equal(got[:, :width], ref[:, :width]), (col0, width, use_list, acc)
                 assert torch.equal(got, old), (col0, width, use_list, acc)
+
+
+@pytest.mark.parametrize('shape', [(128, 192, 'gather3'), (64, 128, 'concat2'), (64, 64, 'dense'),
+                                   (256, 7, 'dense'), (7, 64, 'dense'), (2, 64, 'pairadd')])
+def test_linear_grad_x3_matches_float64(cuda_device, shape):
+    """rg_linear_grad's weight gradient on the bf16 matrix cores with exact three-term splits
+    (RG_GRAD_X3=1; measured slower than the float32 kernel on c4 and kept as an option) against a float64 evaluation of dZ^T X and sum(dZ): every dW / db entry within
+    2e-5 of max|dW| (the float32 MFMA kernel, the default, is held to the same bound) and the
+    split kernel's error at most 4x the float32 kernel's, over
+    20 011 rows (a partial last block) in the gathered / concatenated / dense / pair-sum input
+    modes the training step uses, including 7- and 2-wide layers (padded tiles)."""
+    import os
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    out_dim, in_dim, mode = shape
+    dev = cuda_device
+    lib = nat.lib()
+    g = torch.Generator().manual_seed(out_dim * 1000 + in_dim)
+    rows, n_nodes = 20011, 3000
+    dz = torch.randn(rows, out_dim, generator=g)
+    idx0 = torch.randint(0, n_nodes, (rows,), generator=g, dtype=torch.int32)
+    idx1 = torch.randint(0, n_nodes, (rows,), generator=g, dtype=torch.int32)
+    if mode == 'gather3':
+        w0 = 64
+        x_nodes = torch.randn(n_nodes, w0, generator=g)
+        e = torch.randn(rows, in_dim - 2 * w0, generator=g)
+        X = torch.cat([x_nodes[idx0.long()], x_nodes[idx1.long()], e], 1)
+        args = (nat.IN_GATHER3, x_nodes, w0, None, 0, e, e.shape[1])
+    elif mode == 'concat2':
+        a = torch.randn(rows, in_dim // 2, generator=g)
+        b = torch.randn(rows, in_dim - in_dim // 2, generator=g)
+        X = torch.cat([a, b], 1)
+        args = (nat.IN_CONCAT2, a, a.shape[1], b, b.shape[1], None, 0)
+    elif mode == 'pairadd':
+        x_nodes = torch.randn(n_nodes, in_dim, generator=g)
+        X = x_nodes[idx0.long()] + x_nodes[idx1.long()]
+        args = (nat.IN_PAIRADD, x_nodes, in_dim, None, 0, None, 0)
+    else:
+        X = torch.randn(rows, in_dim, generator=g)
+        args = (nat.IN_DENSE, X, in_dim, None, 0, None, 0)
+    want_w = (dz.double().t() @ X.double())
+    want_b = dz.double().sum(0)
+    mode_c, in0, w0, in1, w1, in2, w2 = args
+    d = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in
+         dict(dz=dz, in0=in0, in1=in1, in2=in2, idx0=idx0, idx1=idx1).items()}
+    ws = torch.empty(lib.rg_linear_grad_workspace_size(rows, out_dim, in_dim), dtype=torch.uint8,
+                     device=dev)
+    scale = float(want_w.abs().max())
+    errs = {}
+    for x3 in ('1', '0'):
+        dW = torch.zeros(out_dim, in_dim, device=dev)
+        db = torch.zeros(out_dim, device=dev)
+        os.environ['RG_GRAD_X3'] = x3
+        try:
+            p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+            ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
+            nat.check(lib.rg_linear_grad(
+                d['dz'].data_ptr(), out_dim, rows, out_dim, in_dim, mode_c, p(d['in0']),
+                ld(d['in0']), w0, p(d['in1']), ld(d['in1']), w1, p(d['in2']), ld(d['in2']), w2,
+                d['idx0'].data_ptr(), d['idx1'].data_ptr(), dW.data_ptr(), db.data_ptr(),
+                ws.data_ptr(), ws.numel(), nat.stream_ptr(dev)), 'rg_linear_grad')
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop('RG_GRAD_X3', None)
+        err_w = float((dW.cpu().double() - want_w).abs().max())
+        err_b = float((db.cpu().double() - want_b).abs().max())
+        assert err_w <= 2e-5 * scale, (x3, err_w, scale)
+        assert err_b <= 2e-5 * float(want_b.abs().max()) + 1e-6, (x3, err_b)
+        errs[x3] = err_w
+    # the split products are float32-class: no worse than 4x the float32 MFMA kernel's error
+    assert errs['1'] <= 4 * errs['0'] + 1e-6 * scale, errs
