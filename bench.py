@@ -105,6 +105,10 @@ def parse():
                    help='time every launch with its own HIP event pair (adds ~10 us of stream '
                         'gap per pair to the timed steps)')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
+    p.add_argument('--streams', type=int, default=2,
+                   help='inference configs: batches in flight -- 2 builds step i\'s graph on a '
+                        'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
+                        '1: build and forward back to back on one stream')
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
         if getattr(a, key, None) is None:
@@ -777,7 +781,8 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     max over ranks), then the forward alone; per-kernel HIP-event durations and the
     roofline of the conv layer kernel."""
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
-    from graph_neural_network_for_radar_perception_amd.pipeline import RadarGNNPipeline
+    from graph_neural_network_for_radar_perception_amd.pipeline import (PipelinedSteps,
+                                                                         RadarGNNPipeline)
     from graph_neural_network_for_radar_perception_amd import _native as nat
     rank = dist.get_rank() if world > 1 else 0
     mode = nat.GRAPH_RADIUS if args.graph == 'radius' else nat.GRAPH_KNN
@@ -786,13 +791,19 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     frames = [synthetic.make_frame(args.nodes, s) for s in seeds]
     clusters = [synthetic.cluster_lists(args.nodes) for _ in seeds]
     batch = FrameBatch.from_frames(frames, clusters, device=dev)
-    pipe = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
+    if args.streams > 1:
+        stepper = PipelinedSteps(model, cfg, args.dtype, mode=mode, eps2=args.eps2,
+                                 depth=args.streams)
+    else:
+        stepper = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
     log(f'{args.config}: {args.frames} frames generated; warm-up')
 
     with torch.no_grad():
-        for _ in range(args.warmup):
-            gb, out = pipe.step(batch)
+        # every in-flight pipeline warms once (its workspaces, a radius graph's capacity)
+        for _ in range(max(args.warmup, args.streams)):
+            gb, out = stepper.step(batch)
         torch.cuda.synchronize()
+        pipe = stepper.pipes[(stepper.i - 1) % stepper.depth] if args.streams > 1 else stepper
         E = int(gb.n_edges_dev.item())
         log(f'{args.config}: warm-up done, E = {E}; timing {args.steps} steps')
         # ---- timed region: K full steps -----------------------------------------
@@ -804,10 +815,12 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            gb, out = pipe.step(batch, events=events)
+            gb, out = stepper.step(batch, events=events)
         torch.cuda.synchronize()
         barrier(world)
         elapsed = max_over_ranks(time.perf_counter() - t0, world)
+        if args.streams > 1:
+            pipe = stepper.pipes[(stepper.i - 1) % stepper.depth]
         durs = event_durations(events)
         if 'conv_stack' in durs:  # per-layer launch time = span / layers
             durs['conv_fused'] = [ms / args.layers for ms in durs.pop('conv_stack')]
@@ -815,11 +828,16 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         barrier(world)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        ev_iso = EventList(coarse=True)
         for _ in range(args.steps):
-            pipe.forward(batch, gb)
+            pipe.forward(batch, gb, ev_iso)
         torch.cuda.synchronize()
         barrier(world)
         fwd_elapsed = max_over_ranks(time.perf_counter() - t1, world)
+        # the conv stack without a concurrent graph build (the timed steps overlap step i's
+        # build with step i-1's forward when --streams > 1)
+        iso = event_durations(ev_iso).get('conv_stack')
+        iso_ms = float(np.mean(iso)) / args.layers if iso else None
         sc = (scatter_aggregate_bench(gb, E, args.frames * args.nodes, max(args.steps, 5))
               if scatter else None)
 
@@ -933,8 +951,14 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     roof.update(avg_ms=round(ms, 4),
                 timing=('HIP events on the launch stream, timed region: ' +
                         ('one pair per launch' if args.fine_events else
-                         'one pair around the conv stack per step, avg = span / layers')),
+                         'one pair around the conv stack per step, avg = span / layers') +
+                        (f'; {args.streams} batches in flight (the next step\'s graph build '
+                         'runs beside this conv stack)' if args.streams > 1 else '')),
                 flops_per_launch=flops)
+    if iso_ms:
+        # the same kernels timed in the forward-only loop (nothing runs beside them)
+        roof.update(avg_ms_isolated=round(iso_ms, 4),
+                    frac_isolated=round(roof['frac'] * ms / iso_ms, 4))
     if ref_tf is not None:
         roof['reference_form_tflops'] = round(ref_tf, 2)
     if traffic is not None:
@@ -985,6 +1009,7 @@ def main():
                    'edges_per_frame': round(r['E'] / args.frames, 1),
                    'parallelism': f'frame-parallel x{world} (no collective in the step)',
                    'frames_per_rank_timed': r['rank_frames'],
+                   'streams': args.streams,
                    'backend': dist.get_backend() if world > 1 else None},
         'forward_only_frames_per_s': round(r['forward_fps'], 2),
         'forward_algorithmic_tflops': round(r['forward_tflops'], 2),

@@ -56,3 +56,46 @@ class RadarGNNPipeline:
         gb.check_capacity()
         U = int(gb.graph.n_pairs_dev.item())
         return out.node_cls, out.node_reg, out.link_cls[:U], out.obj_cls
+
+
+class PipelinedSteps:
+    """Two batches in flight: the graph build + features of step i run on a side stream while
+    the GNN forward of step i - 1 runs on the caller's stream (the build's grid / selection
+    kernels are latency-bound and need little LDS, so they fill the CUs the persistent forward
+    kernels leave idle).  Every step still builds its own graph and runs the whole forward;
+    results are those of ``RadarGNNPipeline.step`` bit for bit.
+
+    ``depth`` pipelines (own workspaces and buffers: a build never overwrites arrays a forward
+    in flight reads) are used round robin; pipeline p's build waits for its previous forward
+    (an event), and its GraphBatch is kept alive until that point, so the caching allocator
+    cannot hand the build stream memory the forward stream still reads."""
+
+    def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
+                 eps2: Optional[float] = None, depth: int = 2):
+        self.pipes = [RadarGNNPipeline(model, cfg, dtype, mode=mode, eps2=eps2)
+                      for _ in range(depth)]
+        self.depth = depth
+        self.side = None
+        self.ev_fwd = [None] * depth
+        self.keep = [None] * depth
+        self.i = 0
+
+    def step(self, batch: FrameBatch, events=None):
+        main = torch.cuda.current_stream()
+        if self.side is None:
+            self.side = torch.cuda.Stream(device=main.device)
+        p = self.i % self.depth
+        self.i += 1
+        with torch.cuda.stream(self.side):
+            if self.ev_fwd[p] is not None:
+                self.side.wait_event(self.ev_fwd[p])
+            gb = self.pipes[p].build(batch)
+            ev_b = torch.cuda.Event()
+            ev_b.record(self.side)
+        main.wait_event(ev_b)
+        out = self.pipes[p].forward(batch, gb, events)
+        ev_f = torch.cuda.Event()
+        ev_f.record(main)
+        self.ev_fwd[p] = ev_f
+        self.keep[p] = (gb, out)
+        return gb, out

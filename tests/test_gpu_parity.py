@@ -1091,3 +1091,42 @@ def test_model_inference_proposals_match_reference(cuda_device, tag):
         for gw, ww in zip(got, want):
             np.testing.assert_array_equal(gw, ww)
         np.testing.assert_allclose(out[3].cpu().numpy(), d[f'{tag}/obj_cls'], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('mode_name', ['knn', 'radius'])
+def test_pipelined_steps_bit_identical(cuda_device, mode_name):
+    """pipeline.PipelinedSteps (graph build of step i on a side stream while step i-1's forward
+    runs, two pipelines round robin) gives every step exactly the outputs RadarGNNPipeline.step
+    gives the same batch: two different batches alternated over six steps, fp32, kNN and
+    radius graphs."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
+    from graph_neural_network_for_radar_perception_amd.pipeline import (PipelinedSteps,
+                                                                         RadarGNNPipeline)
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    dev = cuda_device
+    cfg = model_cfg('model_trained_N500')
+    mt = Model_Training(cfg, dev)
+    mt.load_state_dict(model_state_dict('model_trained_N500'))
+    m = mt.to(dev).pred.eval()
+    mode = nat.GRAPH_KNN if mode_name == 'knn' else nat.GRAPH_RADIUS
+    batches = []
+    for b in range(2):
+        frs = [synthetic.make_frame(700 + 50 * f, 4000 + 10 * b + f) for f in range(3)]
+        cls = [synthetic.cluster_lists(len(fr['meas_px'])) for fr in frs]
+        batches.append(FrameBatch.from_frames(frs, cls, device=dev))
+    ref = []
+    with torch.no_grad():
+        seq = RadarGNNPipeline(m, cfg, 'fp32', mode=mode, eps2=4.0)
+        for b in batches:
+            for _ in range(2):
+                gb, out = seq.step(b)
+            torch.cuda.synchronize()
+            ref.append([t.clone() for t in RadarGNNPipeline.trim(gb, out)])
+        run = PipelinedSteps(m, cfg, 'fp32', mode=mode, eps2=4.0)
+        for i in range(6):
+            gb, out = run.step(batches[i % 2])
+            got = [t.clone() for t in RadarGNNPipeline.trim(gb, out)]
+            for a, b in zip(got, ref[i % 2]):
+                assert torch.equal(a, b), (mode_name, i)
