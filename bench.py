@@ -50,15 +50,15 @@ PRESETS = {
     # the metric's configuration (BASELINE.json metric "N~3k nodes, E~30k edges"; yml k = 10,
     # L = 7, configuration_radarscenes_gnn.yml:14,58), fp32, trained weights
     'm': dict(frames=64, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=5,
-              cpu_warm=2, dtype='fp32', weights='trained'),
+              cpu_warm=2, dtype='fp32', weights='trained', streams=1),
     'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
-               cpu_warm=2, dtype='bf16', weights='random'),
+               cpu_warm=2, dtype='bf16', weights='random', streams=2),
     # BASELINE config 3: 512 frames of C2's shape frame-parallel over 8 GPUs, forward only --
     # 64 frames per rank (weak scaling: --gpus 8 processes 512), no collective in the step
     'c3': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
-               cpu_warm=2, dtype='bf16', weights='random'),
+               cpu_warm=2, dtype='bf16', weights='random', streams=2),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
-               cpu_warm=1, dtype='fp16', weights='random'),
+               cpu_warm=1, dtype='fp16', weights='random', streams=2),
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
     'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
                cpu_warm=1),
@@ -105,10 +105,12 @@ def parse():
                    help='time every launch with its own HIP event pair (adds ~10 us of stream '
                         'gap per pair to the timed steps)')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
-    p.add_argument('--streams', type=int, default=2,
+    p.add_argument('--streams', type=int, default=None,
                    help='inference configs: batches in flight -- 2 builds step i\'s graph on a '
                         'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
-                        '1: build and forward back to back on one stream')
+                        '1: build and forward back to back on one stream (default: the preset\'s, '
+                        '1 for m -- its build is ~5 %% of the step and the overlap blurs the conv '
+                        'roofline -- 2 for c2 / c3 / c5)')
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
         if getattr(a, key, None) is None:
@@ -117,6 +119,8 @@ def parse():
         a.dtype = {'c2': 'bf16', 'c3': 'bf16', 'c5': 'fp16'}.get(a.config, 'fp32')
     if a.weights is None:
         a.weights = 'random'
+    if a.streams is None:
+        a.streams = 1
     return a
 
 
