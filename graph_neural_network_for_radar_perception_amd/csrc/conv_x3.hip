@@ -143,7 +143,9 @@ static constexpr int TS = 68;     // LDS row stride (floats) of the message tile
 #define RG_CX3_EXP 0  // timing experiments only (wrong results): 1 no tile norm epilogues,
                       // 2 no segmented sum, 3 no P / Q gathers, 4 no B splits (one plane
                       // copied), 5 no tile MFMAs, 6 no update / projection phase,
-                      // 7 no P | Q stores
+                      // 7 no P | Q stores, 8 no P gathers (Q[src] only), 9 no P gathers and
+                      // no P half of the node launch's projection (the bound of computing P
+                      // per block inside the edge launch)
 #endif
 
 static constexpr int WE_OFF = 0;                                   // W_e 64 -> 128 (FAST_IN)
@@ -171,7 +173,7 @@ __device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WSrc& 
 #pragma unroll
   for (int s = 0; s < 4; ++s) b[s] = split_acc(xo[s >> 1], s & 1);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = RG_CX3_EXP == 9 ? 2 : 0; q < 4; ++q) {
     f32x16 acc[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) acc[m] = ld_bias_frag(bias, 2 * q + m, h);
@@ -493,7 +495,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       const float* pp = a.pq + (size_t)dq * PQW + 4 * h;
       const float* pqq = a.pq + (size_t)sq * PQW + HID + 4 * h;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) w.p[i] = *(const f32x4*)(pp + 8 * i);
+      for (int i = 0; i < 16; ++i)
+        w.p[i] = (RG_CX3_EXP == 8 || RG_CX3_EXP == 9) ? (f32x4){0.f, 0.f, 0.f, 0.f}
+                                                       : *(const f32x4*)(pp + 8 * i);
 #pragma unroll
       for (int i = 0; i < 16; ++i) w.q[i] = *(const f32x4*)(pqq + 8 * i);
     };
