@@ -59,6 +59,10 @@ PRESETS = {
                cpu_warm=2, dtype='bf16', weights='random', streams=2),
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
                cpu_warm=1, dtype='fp16', weights='random', streams=2),
+    # the same dense frames batched 8 per step (3.2 M edges per step): the throughput form of
+    # config 5 -- a 20 000-node frame alone leaves the persistent kernels ~1 block per wave
+    'c5b': dict(frames=8, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
+                cpu_warm=1, dtype='fp16', weights='random', streams=2),
     # training (yml: k = 10, L = 7), 8 frames per GPU, DDP gradient all-reduce over RCCL
     'c4': dict(frames=8, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=1,
                cpu_warm=1),
@@ -83,7 +87,8 @@ def parse():
                    help='m: the metric configuration (default; fp32, trained weights); '
                         'c2: BASELINE config 2 (bf16); c3: config 3 (C2 frames, 64 per GPU, '
                         'frame-parallel over --gpus, forward only); '
-                        'c5: config 5 radius-graph stress; '
+                        'c5: config 5 radius-graph stress (one frame per step); c5b: its frames '
+                        'batched 8 per step; '
                         'c4: config 4 training step (forward + backward + SGD, DDP); '
                         'cls: the cluster-level classifier GNN (SURVEY 8(f) rank 4); '
                         'frontend: the real-data front-end (SURVEY 8(f) rank 3)')
@@ -116,7 +121,7 @@ def parse():
         if getattr(a, key, None) is None:
             setattr(a, key, v)
     if a.dtype is None:
-        a.dtype = {'c2': 'bf16', 'c3': 'bf16', 'c5': 'fp16'}.get(a.config, 'fp32')
+        a.dtype = {'c2': 'bf16', 'c3': 'bf16', 'c5': 'fp16', 'c5b': 'fp16'}.get(a.config, 'fp32')
     if a.weights is None:
         a.weights = 'random'
     if a.streams is None:
@@ -772,6 +777,7 @@ def frontend_main(args, world, rank, local):
 def workload_name(args) -> str:
     head = {'m': 'M (the metric configuration, SURVEY §8(d))',
             'c2': 'BASELINE config 2', 'c5': 'BASELINE config 5',
+            'c5b': 'BASELINE config 5 frames batched',
             'c3': f'BASELINE config 3 ({args.frames * max(args.gpus, 1)} frames frame-parallel '
                   f'over {max(args.gpus, 1)} GPU(s), forward only, no collective in the step)'
             }.get(args.config, args.config)

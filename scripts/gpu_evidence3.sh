@@ -22,6 +22,8 @@ step bench_c4 600 python bench.py --config c4
 python scripts/bench_line.py $O/bench_c4.log c4
 step bench_c3 300 python bench.py --config c3 --no-cpu-baseline
 python scripts/bench_line.py $O/bench_c3.log c3
+step bench_c5b 300 python bench.py --config c5b --no-cpu-baseline
+python scripts/bench_line.py $O/bench_c5b.log c5b
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run \
   -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extra
 step trace_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o run \
