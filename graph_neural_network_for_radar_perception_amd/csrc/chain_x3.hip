@@ -517,6 +517,10 @@ static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<
 #ifndef RG_X3_ENC_RT
 #define RG_X3_ENC_RT 2  // row tiles per wave of the encoders (1 wave / SIMD at 2)
 #endif
+#ifndef RG_X3_ENC_FT
+#define RG_X3_ENC_FT 0  // encoder threads per workgroup (0: 256 at RT >= 2, else 512; RT 2 at 512,
+                        // two waves per SIMD: 1.2 KB of spills per lane, not run)
+#endif
 
 #ifndef RG_X3_HEAD_RT
 #define RG_X3_HEAD_RT 1  // row tiles per wave of the 5-layer task-head chains (two waves / SIMD at 1)
@@ -526,7 +530,7 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
 #define RG_X3C(MODE, K0, SP, LM, RT, FT, ...) \
   if (match(k, MODE, K0, SP, {__VA_ARGS__})) return launch<MODE, SP, LM, RT, FT, K0, __VA_ARGS__>(a, st);
   constexpr int ALL = 07777777;  // every plane of every layer in LDS
-  constexpr int EFT = RG_X3_ENC_RT >= 2 ? 256 : 512;
+  constexpr int EFT = RG_X3_ENC_FT ? RG_X3_ENC_FT : (RG_X3_ENC_RT >= 2 ? 256 : 512);
   // edge encoder 7 -> 256 -> 128 -> 128 -> 64 (gnn_blocks.py:19-42, block 0 without norm):
   // LDS = layer 0 + planes 0, 1 of layer 1
   // (each shape twice: normalised layers packed centred -- the engine's choice -- or not)
