@@ -470,9 +470,11 @@ __global__ __launch_bounds__(256) void linear_grad_x3_kernel(const float* __rest
   const long r_begin = (long)chunk * rpc;
   const long r_end = min(rows, r_begin + rpc);
   // padding input rows of the last N tile stay zero (IC = 16: half a tile)
-  for (int t = threadIdx.x; t < 3 * (ICP - IC) * RS; t += 256) {
-    const int p = t / ((ICP - IC) * RS), q = t % ((ICP - IC) * RS);
-    XT[p][IC * RS + q] = (__bf16)0.f;
+  if constexpr (ICP > IC) {
+    for (int t = threadIdx.x; t < 3 * (ICP - IC) * RS; t += 256) {
+      const int p = t / ((ICP - IC) * RS), q = t % ((ICP - IC) * RS);
+      XT[p][IC * RS + q] = (__bf16)0.f;
+    }
   }
   f32x16 acc[NTW];
 #pragma unroll

@@ -52,6 +52,9 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 #ifndef RG_X3_PIPE
 #define RG_X3_PIPE 1  // layer_x3 computes the B operand of k-step s + 1 beside step s's MFMAs
 #endif
+#ifndef RG_X3_LASTSB
+#define RG_X3_LASTSB 0  // 0: no fence after the last k-step (M edge encoder 1.41 -> 1.38 ms, conv flat)
+#endif
 #ifndef RG_X3_PKNORM
 #define RG_X3_PKNORM 0  // 1: row statistics and scale in v_pk_fma_f32 (M: no gain, conv 1% slower)
 #endif
@@ -233,7 +236,9 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
         for (int t = 0; t < RT; ++t) bq[t] = bn[t];
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    // RG_X3_LASTSB 0: no fence after the last k-step, so the caller's epilogue of row tile 0
+    // may interleave with the last MFMAs of the other row tiles
+    if (RG_X3_LASTSB || s + 1 < KS) __builtin_amdgcn_sched_barrier(0);
   }
 }
 // The same products in the same order per accumulator as layer_x3 (one row tile), issued
