@@ -289,6 +289,9 @@ __device__ __forceinline__ void run_pre(const Args& a, const char* lds, const fl
   run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
 }
 
+#ifndef RG_X3_FUSED_LASTSB
+#define RG_X3_FUSED_LASTSB 0  // (M edge encoder -0.7 %, interleaved A/B r03h_ab_fusedsb)
+#endif
 #ifndef RG_X3_K0SLOT
 #define RG_X3_K0SLOT 0  // encoders' layer 0 (<= 8 inputs) as 3 MFMAs instead of 6 (slot packing)
 #endif
@@ -386,7 +389,9 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
         for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    // (the last tile unfenced with RG_X3_LASTSB=0, as layer_x3: layer 1's epilogue of row
+    // tile 0 may interleave with tile 1's last MFMAs)
+    if (RG_X3_FUSED_LASTSB || m0 + 1 < MT0) __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (S::NL > 2) {
     Pend pn[RT];
