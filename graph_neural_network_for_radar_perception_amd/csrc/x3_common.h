@@ -52,6 +52,9 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 #ifndef RG_X3_PIPE
 #define RG_X3_PIPE 1  // layer_x3 computes the B operand of k-step s + 1 beside step s's MFMAs
 #endif
+#ifndef RG_X3_SGB
+#define RG_X3_SGB 0  // n > 0: (1 MFMA, n VALU) sched groups per k-step (M encoder 1.38 -> 1.41-1.44 ms: off)
+#endif
 #ifndef RG_X3_LASTSB
 #define RG_X3_LASTSB 0  // 0: no fence after the last k-step (M edge encoder 1.41 -> 1.38 ms, conv flat)
 #endif
@@ -236,6 +239,14 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
         for (int t = 0; t < RT; ++t) bq[t] = bn[t];
       }
     }
+#if RG_X3_SGB
+    // RG_X3_SGB = n: ask the scheduler for the pattern (1 MFMA, n VALU) over the step
+#pragma unroll
+    for (int i = 0; i < 6 * MT * RT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, RG_X3_SGB, 0);
+    }
+#endif
     // RG_X3_LASTSB 0: no fence after the last k-step, so the caller's epilogue of row tile 0
     // may interleave with the last MFMAs of the other row tiles
     if (RG_X3_LASTSB || s + 1 < KS) __builtin_amdgcn_sched_barrier(0);
