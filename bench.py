@@ -435,10 +435,14 @@ def cpu_baseline(args, cfg, sd):
     build_ms = float(np.median(tb)) * 1e3
     fwd_ms = float(np.median(tf)) * 1e3
     total_ms = float(np.median(np.array(tb) + np.array(tf))) * 1e3
-    f1 = None
+    f1, n1 = None, 0
     if args.graph == 'knn':  # (a 1-thread pass over a 20k-node frame would take minutes)
+        # median over >= 5 frames (the reference's CPU path per frame), the
+        # first frame of the sample warming the 1-thread pools
         torch.set_num_threads(1)
-        _, f1 = one(frames[0])
+        one(frames[0])
+        t1 = [one(frames[i % len(frames)])[1] for i in range(1, 6)]
+        f1, n1 = float(np.median(t1)), len(t1)
         torch.set_num_threads(threads)
     return {'value': round(1e3 / total_ms, 4), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
             'graph_build_ms': round(build_ms, 1), 'forward_ms': round(fwd_ms, 1),
@@ -451,7 +455,8 @@ def cpu_baseline(args, cfg, sd):
                       f'L={args.layers} after {warm} warm-up frame(s): oracle graph build (dense '
                       f'numpy, graph_features.py) + torch-fp32 forward (gnn_detector.py), median '
                       f'{total_ms:.0f} ms/frame at torch threads={threads}'
-                      + ('; the forward also timed on 1 thread (1 frame)' if f1 else '')}
+                      + (f'; the forward also timed on 1 thread (median of {n1} frames after '
+                         f'1 warm-up)' if f1 else '')}
 
 
 def batch_labels(frames, gb, cfg, device):
@@ -574,11 +579,12 @@ def train_main(args, world, rank, local):
         'last_losses': [round(float(x), 5) for x in losses.cpu()],
         'roofline': roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         line['cpu_baseline'] = cpu_train_baseline(args, cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
 
 
@@ -684,11 +690,12 @@ def cls_main(args, world, rank, local):
                      'frac': round(tf / peak, 4), 'traffic': None},
         'kernels': kern,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         line['cpu_baseline'] = cpu_classifier_baseline(args, cfg, sd_cpu)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
 
 
@@ -754,7 +761,7 @@ def frontend_main(args, world, rank, local):
                      'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
                      'avg_ms': round(ms, 4), 'bytes_per_launch': nbytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         from oracle import frontend_ref  # the CPU baseline leg only
         sample = wins[:args.cpu_frames]
         t = time.perf_counter()
@@ -771,6 +778,7 @@ def frontend_main(args, world, rank, local):
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
 
 
@@ -1043,7 +1051,7 @@ def main():
                            'workload': workload_name(a2), 'edges_per_gpu': r2['E'],
                            'forward_only_frames_per_s': round(r2['forward_fps'], 2),
                            'roofline': r2['roof'], 'kernels': r2['kern']}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         log('cpu baseline')
         cb = cpu_baseline(args, cfg, sd)
         line['cpu_baseline'] = cb
@@ -1051,6 +1059,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
 
 

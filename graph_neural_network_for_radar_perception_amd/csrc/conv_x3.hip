@@ -65,6 +65,15 @@ static constexpr int PQW = 2 * HID;
                           // gather / norm phases leave the matrix pipe idle
 #endif
 static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
+#ifndef RG_CX3_PP
+#define RG_CX3_PP 1  // the edge launch as a two-group ping-pong (conv_x3_pp_kernel)
+#endif
+#ifndef RG_CX3_PP_PQ
+#define RG_CX3_PP_PQ 2
+#endif
+#ifndef RG_CX3_PP_PRIO
+#define RG_CX3_PP_PRIO 0
+#endif
 #ifndef RG_CX3_STAMP
 #define RG_CX3_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_cx3_stamp
 #endif
@@ -702,6 +711,322 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The edge launch as a two-group ping-pong (RG_CX3_PP, the default).
+//
+// conv_x3_kernel's waves each run the whole tile program -- gathers, layer 1, norm 1,
+// layer 2, norm 2, segmented sum -- and the two waves of a SIMD drift freely, so their
+// matrix phases collide as often as they interleave: the tile MFMAs (0.22 ms of the M
+// layer) and everything else (0.36 ms) measured serial.  Here a tile is cut into
+//   M: h = P[dst] + Q[src] + W_e e (acc1 from V), norm 1's statistics, layer 2   (192 MFMAs)
+//   V: norm 2 + the segmented sum of the tile M just finished, then the NEXT tile's set-up:
+//      block fetch when the block is exhausted, P | Q gathers, destination mask, acc1 = P + Q
+// and the workgroup alternates them in lock-step slots separated by s_barrier: waves 0-3
+// (one per SIMD) run M while waves 4-7 (the other wave of each SIMD) run V, then the roles
+// swap.  The matrix pipe of every SIMD then always has one wave feeding it, and the other
+// wave's gathers, norms and LDS work issue in the MFMA shadow.  A slot lasts as long as
+// its longest M phase (one tile each, equal work); a V phase is a fraction of that.
+// Each destination still sums its edges in CSR order inside one block: bit-identical to
+// conv_x3_kernel.  The two groups run separate loops (V, M / M, V) so that every register
+// array has one producer phase and one consumer phase and is dead in between.
+// Termination: a wave with no work left sets its bit in a per-slot-parity LDS word; every
+// wave reads the word of the slot it just closed after the barrier, so all waves leave
+// after the same slot (the word of slot s is next written in slot s + 2, after the barrier
+// every reader of slot s must reach first).
+template <bool CENT>
+__global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float nrm[4];
+  __shared__ uint32_t done_w[2];
+  if (threadIdx.x < 2) {
+    nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
+    nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
+    done_w[threadIdx.x] = 0;
+  }
+  stage_lds<FT>(lds + WE_OFF, a.w[0], x3_bytes(C, HID));
+  stage_lds<FT>(lds + W2_OFF, a.w[1], x3_bytes(HID, C));
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  float* T = (float*)(lds + W_LDS + wave * T_BYTES);  // [TR][TS] message rows
+  const WLds wE{lds + WE_OFF + lane * 16, plane_bytes(C, HID)};
+  const WLds w2{lds + W2_OFF + lane * 16, plane_bytes(HID, C)};
+  const float* bias2 = (const float*)(lds + W2_OFF + 3 * plane_bytes(HID, C));
+  const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3];
+
+  const int xcd = blockIdx.x % NXCD;
+  auto xlo = [&](int x) { return a.table ? a.table[x] : (int)((long)a.n_blocks * x / NXCD); };
+  int blo = xlo(xcd), bhi = xlo(xcd + 1);
+  const int* pairs = a.table ? a.table + TBL_HDR : nullptr;
+  int* ctr = a.counters + CTR_STRIDE * xcd;
+  int steal = 0;
+
+  int n0 = 0, e1 = 0;  // current block: first node, edge end
+  int tn = 0;          // first edge of the next tile to set up (tn >= e1: block exhausted)
+  bool alive = true;   // blocks may remain
+  bool have = false;   // acc1 holds a set-up tile for the M phase
+  bool pend = false;   // acc2 holds a tile's layer-2 output for the V phase
+  int tc = 0;          // first edge of the tile in acc1 / acc2
+  uint32_t smask = 0;  // its destination-change mask
+  int d = 0;           // this lane's destination in it
+  float run = 0.f;     // lane = feature: running sum of the current destination
+  int cur = -1;        // its slot in the block (wave-uniform)
+  int p1 = 0, d1 = 0, s1 = 0;  // edge / destination / source of this lane in tile tn
+  f32x4 ev[8];         // e rows of tile tn (k order), in flight from the previous M phase
+  f32x16 acc1[4], acc2[2];
+  int slot = 0;
+#if RG_CX3_STAMP
+  // diagnostic build: [0] V work, [1] of it in block-fetch slots, [2] M work, [3] barrier
+  // wait after V, [4] after M, [5] V slots, [6] fetch slots, [7] M slots with a tile,
+  // [8] norm 2 + segmented sum, [9] the rest of V after it (gathers' waits, adds)
+  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+  auto tick = [&]() {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    const unsigned long long dlt = n - t_last;
+    t_last = n;
+    return dlt;
+  };
+  bool vlast = false;
+#endif
+
+  auto tile_idx = [&](int t) {
+    p1 = min(t + r, e1 - 1);  // past the block's last edge clamped: a re-read of a cached row
+    d1 = a.dst[p1];
+    s1 = a.src[p1];
+  };
+  auto load_e = [&]() {
+    const float* pe = a.e + (size_t)p1 * a.lde + 8 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ev[2 * i] = *(const f32x4*)(pe + 16 * i);
+      ev[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
+    }
+  };
+  // the next block with edges: its bounds, first tile indices and e rows
+  auto fetch = [&]() {
+    for (;;) {
+      int bi = 0;
+      if (lane == 0) bi = atomicAdd(ctr, 1);
+      const int blk = blo + __builtin_amdgcn_readfirstlane(bi);
+      if (blk >= bhi) {
+        if (!RG_CX3_STEAL || !a.steal || ++steal >= NXCD) {
+          alive = false;
+          return;
+        }
+        const int x2 = (xcd + steal) % NXCD;  // this XCD's queue is empty: the next one's tail
+        blo = xlo(x2);
+        bhi = xlo(x2 + 1);
+        ctr = a.counters + CTR_STRIDE * x2;
+        continue;
+      }
+      n0 = pairs ? pairs[2 * blk] : blk * NBLK;
+      const int nb1 = pairs ? pairs[2 * blk + 1] : min(n0 + NBLK, a.n_nodes);
+      const int e0 = a.seg_ptr[n0];
+      e1 = a.seg_ptr[nb1];
+      if (e0 < e1) {  // (a block without edges leaves its aggregate rows unwritten: degree 0)
+        tn = e0;
+        tile_idx(tn);
+        load_e();
+        return;
+      }
+    }
+  };
+  // P[dst] | Q[src] rows of M-tile m (accumulator order) of this lane's edge in tile tn
+  auto ld_pq = [&](int m, f32x4 (&pr)[4], f32x4 (&qr)[4]) {
+    const float* pp = a.pq + (size_t)d1 * PQW + 4 * h + 32 * m;
+    const float* pq = a.pq + (size_t)s1 * PQW + HID + 4 * h + 32 * m;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) pr[g] = *(const f32x4*)(pp + 8 * g);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) qr[g] = *(const f32x4*)(pq + 8 * g);
+  };
+  auto add_pq = [&](int m, const f32x4 (&pr)[4], const f32x4 (&qr)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc1[m][4 * g + t] = pr[g][t] + qr[g][t];
+  };
+
+  // ================= V phase: norm 2 + segmented sum of acc2, then the next tile into acc1
+  auto vphase = [&]() {
+    const int pn0 = n0, pe1 = e1;  // the pending tile's block
+    const bool fresh = alive && tn >= e1;
+#if RG_CX3_STAMP
+    vlast = true;
+    tick();
+    st[5] += 1;
+    st[6] += fresh;
+#endif
+    if (fresh) fetch();
+    // the first two M-tiles' P | Q rows (RG_CX3_PP_PQ 4: all four) fly behind norm 2 and
+    // the segmented sum
+    f32x4 pr0[4], qr0[4], pr1[4], qr1[4];
+#if RG_CX3_PP_PQ == 4
+    f32x4 pr2[4], qr2[4], pr3[4], qr3[4];
+#endif
+    if (alive) {
+      ld_pq(0, pr0, qr0);
+      ld_pq(1, pr1, qr1);
+#if RG_CX3_PP_PQ == 4
+      ld_pq(2, pr2, qr2);
+      ld_pq(3, pr3, qr3);
+#endif
+    }
+    if (pend) {
+      norm_leaky<2, CENT>(acc2, mu1, sd1);
+#pragma unroll
+      for (int c = 0; c < 32 / TR; ++c) {
+        if (tc + TR * c >= pe1) break;  // wave-uniform
+        if (r / TR == c) {
+          float* row = T + (r % TR) * TS + 4 * h;
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){acc2[m][4 * g], acc2[m][4 * g + 1],
+                                                        acc2[m][4 * g + 2], acc2[m][4 * g + 3]};
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        float v[TR];
+#pragma unroll
+        for (int j = 0; j < TR; ++j) v[j] = T[j * TS + lane];
+#pragma unroll
+        for (int j = 0; j < TR; ++j) {
+          const int eo = TR * c + j;
+          if (tc + eo < pe1) {
+            if ((smask >> eo) & 1u) {  // a new destination: flush the finished sum
+              if (cur >= 0) a.agg[(size_t)(pn0 + cur) * C + lane] = run;
+              run = v[j];
+              cur = __builtin_amdgcn_readlane(d, eo) - pn0;
+            } else {
+              run += v[j];
+            }
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+      pend = false;
+    }
+#if RG_CX3_STAMP
+    const unsigned long long dseg = tick();  // (+ the block fetch in fresh slots)
+    st[8] += dseg;
+#endif
+    if (fresh) {  // the previous block is done: its last destination's sum
+      if (cur >= 0) a.agg[(size_t)(pn0 + cur) * C + lane] = run;
+      cur = -1;
+      run = 0.f;
+    }
+    if (alive) {
+      d = d1;
+      tc = tn;
+      const int dprev = __shfl_up(d, 1, 64);
+      smask = (uint32_t)__ballot(r == 0 ? d - n0 != cur : d != dprev) &
+              (e1 - tc >= 32 ? 0xffffffffu : ((1u << (e1 - tc)) - 1u));
+#if RG_CX3_PP_PQ == 4
+      add_pq(0, pr0, qr0);
+      add_pq(1, pr1, qr1);
+      add_pq(2, pr2, qr2);
+      add_pq(3, pr3, qr3);
+      tn += 32;
+      if (tn < e1) tile_idx(tn);
+#else
+      f32x4 pr2[4], qr2[4];
+      add_pq(0, pr0, qr0);
+      ld_pq(2, pr2, qr2);
+      add_pq(1, pr1, qr1);
+      ld_pq(3, pr0, qr0);
+      tn += 32;
+      if (tn < e1) tile_idx(tn);
+      add_pq(2, pr2, qr2);
+      add_pq(3, pr0, qr0);
+#endif
+      have = true;
+    } else {
+      // nothing set up: acc1 defined on every path (else its old value counts as live here)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc1[m] = (f32x16){};
+    }
+#if RG_CX3_STAMP
+    const unsigned long long dv = tick();
+    st[9] += dv;
+    st[0] += dseg + dv;
+    if (fresh) st[1] += dseg + dv;
+#endif
+  };
+  // ================= M phase: layer 1, norm 1's statistics, layer 2 (acc1 -> acc2)
+  auto mphase = [&]() {
+#if RG_CX3_STAMP
+    vlast = false;
+    tick();
+    st[7] += have;
+#endif
+    if (have) {
+      if (RG_CX3_PP_PRIO) __builtin_amdgcn_s_setprio(1);
+      layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0, [&](int s) { return split8(ev[2 * s], ev[2 * s + 1]); });
+      const Pend pn1 = pend_norm_leaky<4, CENT>(acc1, mu0, sd0);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
+      layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0,
+                                    [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
+      // the next tile's e rows (the only rows streamed from HBM) arrive behind the slot
+      if (tn < e1) load_e();
+      if (RG_CX3_PP_PRIO) __builtin_amdgcn_s_setprio(0);
+      have = false;
+      pend = true;
+    } else {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc2[m] = (f32x16){};
+    }
+#if RG_CX3_STAMP
+    st[2] += tick();
+#endif
+  };
+  // close the slot: true when every wave of the workgroup is out of work
+  auto sync = [&]() {
+    if (!alive && !pend && !have) atomicOr(&done_w[slot & 1], 1u << wave);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the done word is visible past the barrier
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#if RG_CX3_STAMP
+    st[vlast ? 3 : 4] += tick();
+#endif
+    const bool all = done_w[slot & 1] == (1u << NW) - 1u;
+    ++slot;
+    return all;
+  };
+  if (wave < NW / 2) {  // waves 0-3: V first
+    for (;;) {
+      vphase();
+      if (sync()) break;
+      mphase();
+      if (sync()) break;
+    }
+  } else {              // waves 4-7: M first (the first one idle)
+    for (;;) {
+      mphase();
+      if (sync()) break;
+      vphase();
+      if (sync()) break;
+    }
+  }
+#if RG_CX3_STAMP
+  if (lane == 0)
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_cx3_stamp[i], st[i]);
+#endif
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.counters + CTR_STRIDE * NXCD, 1) == (int)gridDim.x - 1) {
+#pragma unroll
+      for (int i = 0; i <= NXCD; ++i) a.counters[CTR_STRIDE * i] = 0;
+    }
+  }
+}
+
 // The node phase as a launch of its own (RG_CX3_NODE_KERNEL): W_u and W'_pq both staged in
 // LDS (145 KB), one 32-node tile per wave and step; the aggregate rows come from the
 // edge launch's scratch.  In the single-launch layer the same phase runs at each block's
@@ -1031,6 +1356,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
   auto edge = cent ? (espl ? conv_x3_kernel<true, NODE, true> : conv_x3_kernel<true, NODE, false>)
                    : (espl ? conv_x3_kernel<false, NODE, true> : conv_x3_kernel<false, NODE, false>);
+  if (RG_CX3_PP && !NODE && !espl) edge = cent ? conv_x3_pp_kernel<true> : conv_x3_pp_kernel<false>;
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
   RG_LAUNCH_CHECK_ZERO(a.counters, CTR_BYTES, stream);

@@ -223,6 +223,10 @@ __global__ void bfinal_kernel(const double* __restrict__ gpart, const double* __
     const double n = (double)(seg_ptr[s + 1] - seg_ptr[s]) * (C / G);
     const double sdev = (double)stats[2 * t + 1];
     const double r = 1.0 / (double)(stats[2 * t + 1] + NORM_EPS);
+    // a constant segment / group (std = 0): torch's std backward masks its 1 / std to zero
+    // (FunctionsManual.cpp std_backward: masked_fill_(result == 0, 0)), so the reference's
+    // gradient is finite, r (gn - mean(gn)) -- k2 = 0 here gives exactly that; n = 1 makes
+    // std NaN in the forward (torch.std's 0 / 0), and r = NaN carries it into dz
     const double k2 = sdev > 0.0 ? r * r * b / ((n - 1.0) * sdev) : 0.0;
     // dz = r gn - k2 d - mean(r gn - k2 d) = r gn - k2 d - (r a - k2 c) / n
     coef[3 * t] = (float)r;

@@ -76,17 +76,27 @@ class _DetectorOutputs(torch.autograd.Function):
     forward in float32 with the training tape (training.TrainEngine.forward_tape: the same
     kernels Model_Training trains with) and back-propagates the incoming output gradients
     through it (TrainEngine.backward_outputs), i.e. recomputation instead of keeping a tape
-    alive for callers that never call backward (the reference's evaluation loops)."""
+    alive for callers that never call backward (the reference's evaluation loops).
+    Recomputation needs the weights of the forward: the parameters' version counters and the
+    model's weight generation (bumped by writes outside torch, e.g. FusedSGD) are saved, and
+    backward raises like autograd's in-place check when either moved in between."""
 
     @staticmethod
     def forward(ctx, rec, node_cls, node_reg, link_cls, obj_cls, *params):
         ctx.rec = rec
         ctx.n_params = len(params)
+        ctx.versions = tuple(p._version for p in params)
+        ctx.gen = rec.model._weights_gen
         return node_cls.clone(), node_reg.clone(), link_cls.clone(), obj_cls.clone()
 
     @staticmethod
     def backward(ctx, *grads):
         rec = ctx.rec
+        if (rec.model._weights_gen != ctx.gen or
+                tuple(p._version for p in rec.model.parameters()) != ctx.versions):
+            raise RuntimeError('one of the variables needed for gradient computation has been '
+                               'modified by an inplace operation: the detector\'s parameters '
+                               'changed between the grad-enabled forward and backward()')
         eng = rec.model.train_engine()
         outs, T = eng.forward_tape(*rec.batch)
         eng.backward_outputs(T, *eng.output_grad_buffers(T, grads))
@@ -129,6 +139,7 @@ class Model_Inference(nn.Module):
                                                    c.activation, c.norm_layer, c.num_groups)
         self.compute_dtype = 'fp32'
         self._plans: Dict[str, engine.ModelPlans] = {}
+        self._weights_gen = 0  # bumped by invalidate_plans (weights written outside torch)
         if extract_proposals:
             self.set_param_for_proposal_extraction(eps, compute_adj_mat_from_links)
 
@@ -153,6 +164,7 @@ class Model_Inference(nn.Module):
 
     def invalidate_plans(self):
         """Re-pack every plan on next use (weights written outside torch, FusedSGD)."""
+        self._weights_gen += 1
         for p in self._plans.values():
             p.invalidate()
         if getattr(self, '_train_engine', None) is not None:

@@ -143,6 +143,20 @@ class FrameBatch:
     cluster_ptr: torch.Tensor     # int32 [Ncl+1] object-head clusters (global node ids)
     cluster_idx: torch.Tensor     # int32 [sum |c|]
     n_clusters: int
+    # recorded on the producing stream once every array above is written (uploads, or device
+    # ops of the caller): consumers on other streams wait on it (pipeline.PipelinedSteps)
+    ready: Optional['torch.cuda.Event'] = None
+
+    def tensors(self) -> List[torch.Tensor]:
+        return list(self.arrays.values()) + [self.frame_ptr, self.cluster_ptr, self.cluster_idx]
+
+    def mark_ready(self, stream=None) -> 'FrameBatch':
+        """Record ``ready`` on ``stream`` (default: the current stream) after the caller's
+        last write to the batch's arrays."""
+        if self.frame_ptr.is_cuda:
+            self.ready = torch.cuda.Event()
+            self.ready.record(stream if stream is not None else torch.cuda.current_stream())
+        return self
 
     @property
     def n_nodes(self) -> int:
@@ -154,25 +168,35 @@ class FrameBatch:
 
     @staticmethod
     def from_frames(frames: List[dict], clusters: Optional[List[List[np.ndarray]]] = None,
-                    device=None) -> 'FrameBatch':
+                    device=None, pinned: bool = False) -> 'FrameBatch':
+        """Upload frames (and the object-head clusters) as one batch.  ``pinned``: stage the
+        host arrays in page-locked memory and copy them asynchronously on the current stream
+        (the ``ready`` event, recorded after the copies, orders every consumer)."""
         dev = torch.device(device) if device is not None else _device()
+        async_up = pinned and dev.type == 'cuda'
+
+        def up(a: np.ndarray) -> torch.Tensor:
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if async_up:
+                return t.pin_memory().to(dev, non_blocking=True)
+            return t.to(dev)
+
         sizes = [int(np.asarray(f['meas_px']).shape[0]) for f in frames]
         cat = {}
         for k in _FIELDS_F32 + ('meas_timestamp',):
             dt = np.int64 if k == 'meas_timestamp' else np.float32
-            cat[k] = torch.from_numpy(np.concatenate([np.asarray(f[k]).astype(dt) for f in frames])
-                                      ).to(dev)
+            cat[k] = up(np.concatenate([np.asarray(f[k]).astype(dt) for f in frames]))
         base = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-        fp = torch.from_numpy(base.astype(np.int32)).to(dev)
+        fp = up(base.astype(np.int32))
         lens, idx = [], []
         if clusters is not None:
             for b, cl in zip(base[:-1], clusters):
                 for c in cl:
                     lens.append(len(c))
                     idx.append(np.asarray(c, dtype=np.int64) + b)
-        cptr = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)).to(dev)
-        cidx = torch.from_numpy((np.concatenate(idx) if idx else np.zeros(1)).astype(np.int32)).to(dev)
-        return FrameBatch(cat, fp, sizes, cptr, cidx, len(lens))
+        cptr = up(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32))
+        cidx = up((np.concatenate(idx) if idx else np.zeros(1)).astype(np.int32))
+        return FrameBatch(cat, fp, sizes, cptr, cidx, len(lens)).mark_ready()
 
 
 @dataclass

@@ -68,7 +68,12 @@ class PipelinedSteps:
     ``depth`` pipelines (own workspaces and buffers: a build never overwrites arrays a forward
     in flight reads) are used round robin; pipeline p's build waits for its previous forward
     (an event), and its GraphBatch is kept alive until that point, so the caching allocator
-    cannot hand the build stream memory the forward stream still reads."""
+    cannot hand the build stream memory the forward stream still reads.  The build also waits
+    for the batch itself: ``FrameBatch.ready``, recorded on the stream that wrote its arrays
+    (``from_frames`` records it after its uploads, asynchronous ones included; a batch without
+    one makes the build wait for everything enqueued on the caller's stream so far), and the
+    batch's arrays are marked as in use on the side stream (``record_stream``), so freeing the
+    batch early cannot hand its memory to the caller's stream while the build reads it."""
 
     def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
                  eps2: Optional[float] = None, depth: int = 2):
@@ -89,6 +94,12 @@ class PipelinedSteps:
         with torch.cuda.stream(self.side):
             if self.ev_fwd[p] is not None:
                 self.side.wait_event(self.ev_fwd[p])
+            if batch.ready is not None:
+                self.side.wait_event(batch.ready)
+            else:
+                self.side.wait_stream(main)
+            for t in batch.tensors():
+                t.record_stream(self.side)
             gb = self.pipes[p].build(batch)
             ev_b = torch.cuda.Event()
             ev_b.record(self.side)

@@ -189,10 +189,15 @@ def _run_bench(args, timeout=240):
 def test_bench_gpus2_launches_two_ranks(cuda_device):
     """`python bench.py --gpus 2` (no launcher in the environment) starts two ranks itself:
     the line reports n_gpus 2 and the value counts both ranks' frames (weak scaling; gloo
-    for the timing collectives so both ranks can share the test box's one card)."""
+    for the timing collectives so both ranks can share the test box's one card), and rank 0
+    adds the CPU baseline after the timed region while the other rank waits."""
     line = _run_bench(['--gpus', '2', '--steps', '2', '--warmup', '1', '--frames', '4',
-                       '--no-cpu-baseline', '--no-extra'])
+                       '--nodes', '1000', '--cpu-frames', '1', '--no-extra'])
     assert line['n_gpus'] == 2
+    # multi-rank lines carry the CPU baseline too (rank 0, after the timed region)
+    cb = line['cpu_baseline']
+    assert cb['kind'] == 'port' and cb['value'] > 0 and cb['cores'] >= 1
+    assert cb['forward_1thread_ms'] > 0 and 'median of 5 frames' in cb['sample']
     assert line['config']['frames_per_rank_timed'] == [8, 8]
     assert line['config']['backend'] == 'gloo'
     # value = frames of all ranks / max-over-ranks elapsed = 16 / (steps * ms_per_step)

@@ -253,3 +253,27 @@ def test_no_grad_inference_has_no_graph(cuda_device):
     assert all(o.grad_fn is None for o in out2)
     for a, b in zip(out, out2):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('how', ['inplace', 'outside_torch'])
+def test_grad_enabled_backward_after_weight_update_raises(cuda_device, how):
+    """backward() recomputes the forward from the parameters: if they changed after the
+    grad-enabled call -- an in-place torch update (version counter) or a write torch does not
+    see (FusedSGD: the model's weight generation) -- it raises like autograd's in-place check
+    instead of returning the gradients of different weights."""
+    name = 'model_trained_N500'
+    d = golden(name)
+    dev = cuda_device
+    detector = _detector(name, dev)
+    ei = torch.from_numpy(d['edge_index'].astype(np.int64)).to(dev)
+    out = detector(torch.from_numpy(d['node_features']).to(dev),
+                   torch.from_numpy(d['edge_features']).to(dev), ei, None,
+                   [c.to(dev) for c in cluster_lists(d)])
+    p = next(detector.parameters())
+    if how == 'inplace':
+        with torch.no_grad():
+            p.mul_(1.0)            # bumps the version counter, same values
+    else:
+        detector.invalidate_plans()  # what FusedSGD's on_update does after a native write
+    with pytest.raises(RuntimeError, match='modified by an inplace operation'):
+        out[0].sum().backward()

@@ -130,3 +130,82 @@ def test_max_aggregation_training_matches_reference(cuda_device):
     sum(loss.values()).backward()
     for name, p in m.named_parameters():
         _grad_close(p.grad.cpu().numpy(), d['g1/' + name], name)
+
+
+@pytest.mark.parametrize('groups', [1, 4])
+def test_frame_norm_backward_degenerate_segments(cuda_device, groups):
+    """rg_frame_norm_backward (common.py:223-253 under loss.backward()) on segments the
+    fixtures do not cover, against torch autograd in float64: a constant-valued frame (std = 0:
+    torch's std backward masks 1 / std, so the gradient is finite, r (gn - mean gn)), a frame
+    with one constant group, a one-row frame and an ordinary frame; and a one-element group
+    (n = 1: torch.std is NaN, the forward and every gradient NaN)."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    dev = cuda_device
+    C = 8
+    gen = torch.Generator().manual_seed(7)
+    rows = [5, 3, 1, 6]
+    z = torch.randn(sum(rows), C, generator=gen, dtype=torch.float64)
+    z[0:5] = 2.0                                   # constant frame
+    z[5:8, 0:C // groups] = -1.5                   # first group of frame 1 constant
+    da = torch.randn(sum(rows), C, generator=gen, dtype=torch.float64)
+    mu_p, sd_p = torch.tensor([0.3], dtype=torch.float64), torch.tensor([1.7], dtype=torch.float64)
+    seg = torch.tensor(np.concatenate([[0], np.cumsum(rows)]), dtype=torch.int32)
+
+    def ref(zz, dd, sg):
+        zz = zz.clone().requires_grad_(True)
+        m, s = mu_p.clone().requires_grad_(True), sd_p.clone().requires_grad_(True)
+        loss = 0.0
+        for f in range(sg.numel() - 1):
+            x = zz[sg[f]:sg[f + 1]]
+            n_, dg = x.shape[0], C // groups
+            xg = x.reshape(n_, groups, dg)
+            mean = xg.mean(dim=(0, 2), keepdim=True)
+            std = xg.std(dim=(0, 2), keepdim=True)
+            y = (s * ((xg - mean) / (std + 1e-5)) + m).reshape(n_, C)
+            y = torch.nn.functional.leaky_relu(y, 0.01)
+            loss = loss + (y * dd[sg[f]:sg[f + 1]]).sum()
+        loss.backward()
+        return zz.grad, m.grad, s.grad
+
+    def run(zz, dd, sg):
+        n_seg = sg.numel() - 1
+        z32 = zz.float().to(dev).contiguous()
+        d32 = dd.float().to(dev).contiguous()
+        dz = torch.full_like(z32, float('nan'))
+        dmu = torch.zeros(1, device=dev)
+        dsd = torch.zeros(1, device=dev)
+        m32, s32 = mu_p.float().to(dev), sd_p.float().to(dev)
+        sgd = sg.to(dev)
+        lib = nat.lib()
+        ws = torch.empty(lib.rg_frame_norm_backward_workspace_size(n_seg, groups), dtype=torch.uint8,
+                         device=dev)
+        nat.check(lib.rg_frame_norm_backward(z32.data_ptr(), C, d32.data_ptr(), C, C, groups,
+                                             sgd.data_ptr(), n_seg, m32.data_ptr(), s32.data_ptr(),
+                                             nat.ACT['leakyrelu'], dz.data_ptr(), C, dmu.data_ptr(),
+                                             dsd.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             nat.stream_ptr(dev)), 'rg_frame_norm_backward')
+        torch.cuda.synchronize()
+        return dz.double().cpu(), dmu.double().cpu(), dsd.double().cpu()
+
+    want = ref(z, da, seg)
+    got = run(z, da, seg)
+    for g_, w_, name in zip(got, want, ('dz', 'd_mu', 'd_std')):
+        assert torch.isfinite(g_).all(), name
+        for f in range(len(rows)):
+            sl = slice(int(seg[f]), int(seg[f + 1])) if name == 'dz' else slice(None)
+            scale = float(w_[sl].abs().max()) + 1e-30
+            err = float((g_[sl] - w_[sl]).abs().max())
+            assert err <= 1e-4 * scale, (name, f, err, scale)
+    if groups == 1:
+        return
+    # n = 1: one row with one element per group
+    z1 = torch.randn(1, C, generator=gen, dtype=torch.float64)
+    seg1 = torch.tensor([0, 1], dtype=torch.int32)
+    old = groups
+    try:
+        groups = C                                 # one element per group: torch.std = NaN
+        want1 = ref(z1, da[:1], seg1)
+        got1 = run(z1, da[:1], seg1)
+    finally:
+        groups = old
+    assert torch.isnan(want1[0]).all() and torch.isnan(got1[0]).all()
