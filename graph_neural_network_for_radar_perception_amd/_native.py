@@ -29,7 +29,6 @@ RG_PACK_X3 = 0x400
 RG_PACK_F16 = 0x800
 RG_LAYER_CENTERED = 1
 RG_LAYER_F16 = 2
-RG_LAYER_E_SPLIT = 4
 RG_ERR_UNSUPPORTED = 3
 ACT = {'none': 0, 'relu': 1, 'leakyrelu': 2, 'swish': 3}
 GRAPH_KNN, GRAPH_RADIUS, GRAPH_KNN_RADIUS = 0, 1, 2
@@ -129,7 +128,6 @@ _SIGNATURES = {
                                  _P, _I, _I, _P, _P, _P, _I, _P, _I, _P]),
     'rg_mlp_chain_x3': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _P, _I, _I, _P, _P, _P,
                              _I, _P]),
-    'rg_mlp_chain_x3_split': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _P, _I, _I, _P, _I, _P]),
     'rg_conv_layer_f32_workspace_size': (_S, [_I]),
     'rg_conv_layer_f32': (_I, [ctypes.POINTER(rg_layer), _I, _P, _I, _P, _I, _P, _P, _P, _I, _P,
                                _I, _P, _S, _P]),
@@ -165,6 +163,7 @@ _SIGNATURES = {
     'rg_segment_order_workspace_size': (_S, []),
     'rg_segment_order': (_I, [_P, _I, _P, _P, _S, _P]),
     'rg_segment_reduce_ordered': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+    'rg_segment_reduce_sched': (_I, [_P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P]),
     'rg_segment_reduce_ranges_workspace_size': (_S, [_L, _I, _I]),
     'rg_segment_reduce_ranges': (_I, [_P, _I, _I, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P, _S,
                                       _P]),

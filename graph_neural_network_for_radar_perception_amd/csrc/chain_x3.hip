@@ -84,8 +84,6 @@ struct Args {
   const int* idx1;
   float* out;
   int ld_out, out_real;
-  char* osplit;  // rg_mlp_chain_x3_split: the output pre-split (bf16 planes), else null
-  int ld_split;  // its row stride in bytes
 };
 
 // the weight source of layer l: LDS planes where staged (in plane order), else L2
@@ -129,25 +127,6 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
                                            long rows, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int out = a.out_real;
-  if (a.osplit) {
-    // the exact three-term split of each value, B-operand ready for a FAST_CHAIN-packed
-    // consumer: plane p of k-step s (accumulator registers 8(s&1) .. +7 of M-tile s>>1) at
-    // byte 96 s + 32 p + 16 h of the row
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const long row = row0 + 32 * t + r;
-      if (row >= rows) continue;
-      char* o = a.osplit + (size_t)row * a.ld_split + 16 * h;
-#pragma unroll
-      for (int s = 0; s < 2 * MT; ++s) {
-        const X3 x = split_acc(acc[t][s >> 1], s & 1);
-        *(u32x4*)(o + 96 * s) = __builtin_bit_cast(u32x4, x.p0);
-        *(u32x4*)(o + 96 * s + 32) = __builtin_bit_cast(u32x4, x.p1);
-        *(u32x4*)(o + 96 * s + 64) = __builtin_bit_cast(u32x4, x.p2);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const long row = row0 + 32 * t + r;
@@ -570,39 +549,20 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
 using namespace rg;
 using namespace rg::cx3;
 
-// enc_x3.hip: the encoders with their weights streamed through an LDS ring
-int rg_enc_ring_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
-                   const float* in0, int ld0, int w0, float* out, int ld_out, int norm_mask,
-                   int act_mask, int centred, void* stream);
-
 static int chain_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
                     int in_mode, const float* in0, int ld0, int w0, const int* idx0,
-                    const int* idx1, float* out, int ld_out, char* osplit, int ld_split,
-                    void* stream);
+                    const int* idx1, float* out, int ld_out, void* stream);
 
 extern "C" int rg_mlp_chain_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
                                int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                                const int* idx1, float* out, int ld_out, void* stream) {
   return chain_x3(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, idx0, idx1, out,
-                  ld_out, nullptr, 0, stream);
-}
-
-extern "C" int rg_mlp_chain_x3_split(const rg_layer* layers, int n_layers, long rows,
-                                     const int* rows_dev, const float* in0, int ld0, int w0,
-                                     void* out_split, int ld_split, void* stream) {
-  RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_x3_split: n_layers");
-  const int n = layers[n_layers - 1].out_dim;
-  RG_REQUIRE(out_split && n % 32 == 0 && ld_split % 16 == 0 && ld_split >= 6 * n, RG_ERR_ARG,
-             "rg_mlp_chain_x3_split: output width %d (multiple of 32), row stride %d bytes "
-             "(multiple of 16, >= 6 x width)", n, ld_split);
-  return chain_x3(layers, n_layers, rows, rows_dev, RG_IN_DENSE, in0, ld0, w0, nullptr, nullptr,
-                  nullptr, 0, (char*)out_split, ld_split, stream);
+                  ld_out, stream);
 }
 
 static int chain_x3(const rg_layer* layers, int n_layers, long rows, const int* rows_dev,
                     int in_mode, const float* in0, int ld0, int w0, const int* idx0,
-                    const int* idx1, float* out, int ld_out, char* osplit, int ld_split,
-                    void* stream) {
+                    const int* idx1, float* out, int ld_out, void* stream) {
   RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG, "rg_mlp_chain_x3: n_layers");
   RG_REQUIRE((in_mode != RG_IN_PAIRADD && in_mode != RG_IN_PAIRPRE) || (idx0 && idx1), RG_ERR_ARG,
              "rg_mlp_chain_x3: RG_IN_PAIRADD / RG_IN_PAIRPRE need idx0 and idx1");
@@ -650,11 +610,6 @@ static int chain_x3(const rg_layer* layers, int n_layers, long rows, const int* 
     if (layers[l].norm_mu && (layers[l].flags & RG_LAYER_CENTERED)) cm |= 1 << l;
   if (cm != 0 && cm != nm) return RG_ERR_UNSUPPORTED;
   k.sp = spec(nm, am, cm != 0);
-  if (k.mode == IN_SMALL && !osplit) {
-    const int rc = rg_enc_ring_x3(layers, n_layers, rows, rows_dev, in0, ld0, w0, out, ld_out, nm,
-                                  am, cm != 0, stream);
-    if (rc != RG_ERR_UNSUPPORTED) return rc;
-  }
   a.rows = rows;
   a.rows_dev = rows_dev;
   a.in0 = in0;
@@ -664,8 +619,6 @@ static int chain_x3(const rg_layer* layers, int n_layers, long rows, const int* 
   a.idx1 = idx1;
   a.out = out;
   a.ld_out = ld_out;
-  a.osplit = osplit;
-  a.ld_split = ld_split;
   a.out_real = layers[n_layers - 1].out_dim;
   if (rows <= 0) return RG_OK;
   return dispatch(k, a, (hipStream_t)stream);

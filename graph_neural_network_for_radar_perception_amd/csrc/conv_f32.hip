@@ -20,10 +20,7 @@
 //     MFMA spent on the reduction.  After the block's last tile the aggregates (LDS,
 //     row = node) and x[node] are the update MLP's B operand; update + norm + act +
 //     residual, store.  Messages and aggregates never touch HBM.
-// One wave per SIMD (up to 512 registers): the f32 MFMA (64 cycles) leaves the issue
-// slots for the epilogues; the next tile's rows (P[dst], Q[src], e: 160 registers) are
-// loaded while the current tile computes, the tile after's indices one tile earlier.
-// Workgroups are persistent; block ids come from one atomic counter per XCD over that
+// Two waves per SIMD (conv_f32_kernel2 below).  Workgroups are persistent; block ids come from one atomic counter per XCD over that
 // XCD's contiguous eighth of the nodes (workgroup w runs on XCD w % 8), so each frame's
 // x, P and Q rows are gathered from one L2.
 #include "rg_common.h"
@@ -141,197 +138,6 @@ struct Rows {
 struct Idx {
   int d, s;
 };
-
-__global__ __launch_bounds__(FT) void conv_f32_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  __shared__ float nrm[6];
-  __shared__ int acts[3];
-  if (threadIdx.x < 3) {
-    nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
-    nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
-  }
-  {
-    const int nb[3] = {fbytes(C, HID), fbytes(HID, C), fbytes(2 * C, C)};
-    const int off[3] = {W_E_OFF, W_2_OFF, W_U_OFF};
-#pragma unroll
-    for (int l = 0; l < 3; ++l) {
-      stage_lds<FT>(lds + off[l], a.w[l], nb[l]);
-    }
-  }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  float* T = (float*)(lds + W_BYTES + wave * WAVE_LDS);  // [16][TS] message half-tile
-  float* Agg = T + 16 * TS;                             // [NBLK][AS] aggregates
-  const char* wE = lds + W_E_OFF;
-  const char* w2 = lds + W_2_OFF;
-  const char* wU = lds + W_U_OFF;
-  const float* bias2 = (const float*)(w2 + 2 * 16 * 1024);
-  const float* biasU = (const float*)(wU + 2 * 16 * 1024);
-  const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3], muU = nrm[4], sdU = nrm[5];
-  const int act = ACT_LEAKY;  // host-checked: all three blocks use the yml LeakyReLU
-  (void)acts;
-
-  // this workgroup's XCD range of blocks
-  const int xcd = blockIdx.x % NXCD;
-  const int blo = (int)((long)a.n_blocks * xcd / NXCD);
-  const int bhi = (int)((long)a.n_blocks * (xcd + 1) / NXCD);
-  int* ctr = a.counters + xcd;
-
-  auto load_idx = [&](int t0, int e1) {
-    const int p = min(t0 + r, e1 - 1);
-    return Idx{a.dst[p], a.src[p]};
-  };
-  auto load_rows = [&](int t0, int e1, const Idx& ix, Rows& R) {
-    const int p = min(t0 + r, e1 - 1);
-    const float* pp = a.pq + (size_t)ix.d * a.ldpq + 4 * h;
-    const float* pq = a.pq + (size_t)ix.s * a.ldpq + HID + 4 * h;
-    const float* pe = a.e + (size_t)p * a.lde + 4 * h;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      R.p[i] = *(const f32x4*)(pp + 8 * i);
-      R.q[i] = *(const f32x4*)(pq + 8 * i);
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) R.e[s] = *(const f32x4*)(pe + 8 * s);
-  };
-
-  for (;;) {
-    int bi = 0;
-    if (lane == 0) bi = atomicAdd(ctr, 1);
-    const int blk = blo + __shfl(bi, 0, 64);
-    if (blk >= bhi) break;
-    const int n0 = blk * NBLK;
-    const int n1 = min(n0 + NBLK, a.n_nodes);
-    const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
-
-    // aggregates start at zero (nodes without incoming edges keep it, PyG semantics)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = lane + 64 * i;
-      *(f32x4*)(Agg + (idx >> 4) * AS + 4 * (idx & 15)) = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    float run = 0.f;  // lane = feature: the running sum of the current destination
-    int cur = -1;     // its slot (wave-uniform)
-
-    auto tile = [&](const Rows& R, int dcur, int t0, int e1) {
-      // ---- message layer 1: h = P[dst] + Q[src] + W_e e, then norm + act
-      f32x16 acc1[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 pv = R.p[4 * m + g], qv = R.q[4 * m + g];
-          acc1[m][4 * g + 0] = pv.x + qv.x;
-          acc1[m][4 * g + 1] = pv.y + qv.y;
-          acc1[m][4 * g + 2] = pv.z + qv.z;
-          acc1[m][4 * g + 3] = pv.w + qv.w;
-        }
-      layer<8, 4>(acc1, wE, lane, [&](int s4) { return R.e[s4]; });
-      norm_act<4>(acc1, mu0, sd0, act);
-      // ---- message layer 2 (B operand = layer 1's accumulators)
-      f32x16 acc2[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
-      layer<16, 2>(acc2, w2, lane, [&](int s4) {
-        const f32x16& p = acc1[s4 >> 2];
-        const int q = 4 * (s4 & 3);
-        return (f32x4){p[q], p[q + 1], p[q + 2], p[q + 3]};
-      });
-      norm_act<2>(acc2, mu1, sd1, act);
-      // ---- segmented sum in edge order, 16 edges at a time through the LDS tile
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if ((r >> 4) == c) {
-          float* row = T + (r & 15) * TS + 4 * h;
-#pragma unroll
-          for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-              *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){acc2[m][4 * g], acc2[m][4 * g + 1],
-                                                        acc2[m][4 * g + 2], acc2[m][4 * g + 3]};
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int eo = 16 * c + j;
-          if (t0 + eo < e1) {
-            const float v = T[j * TS + lane];
-            const int slot = __builtin_amdgcn_readlane(dcur, eo) - n0;
-            run = slot == cur ? run + v : v;
-            Agg[slot * AS + lane] = run;
-            cur = slot;
-          }
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-      }
-    };
-
-    if (e0 < e1) {
-      Idx iA = load_idx(e0, e1);
-      Idx iB = load_idx(e0 + 32, e1);
-      Rows RA, RB;
-      load_rows(e0, e1, iA, RA);
-      for (int t0 = e0;;) {
-        int dA = iA.d;
-        load_rows(t0 + 32, e1, iB, RB);
-        iA = load_idx(t0 + 64, e1);
-        tile(RA, dA, t0, e1);
-        t0 += 32;
-        if (t0 >= e1) break;
-        int dB = iB.d;
-        load_rows(t0 + 32, e1, iA, RA);
-        iB = load_idx(t0 + 64, e1);
-        tile(RB, dB, t0, e1);
-        t0 += 32;
-        if (t0 >= e1) break;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- update MLP on cat(x[node], agg[node]) + residual (gnn_blocks.py:103-109)
-    const int node = n0 + r;
-    const bool nvalid = node < n1;
-    const float* px = a.x + (size_t)(nvalid ? node : n0) * a.ldx + 4 * h;
-    f32x4 xb[8], ab[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) xb[s] = *(const f32x4*)(px + 8 * s);
-    float cnt = 1.f;
-    if (a.aggr_mean) {  // PyG mean: sum / max(count, 1)
-      const int deg = nvalid ? a.seg_ptr[node + 1] - a.seg_ptr[node] : 1;
-      cnt = (float)(deg > 0 ? deg : 1);
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      f32x4 v = *(const f32x4*)(Agg + r * AS + 8 * s + 4 * h);
-      if (a.aggr_mean) v = (f32x4){div_rn(v.x, cnt), div_rn(v.y, cnt), div_rn(v.z, cnt), div_rn(v.w, cnt)};
-      ab[s] = v;
-    }
-    f32x16 accu[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) accu[m] = ld_bias_frag(biasU, m, h);
-    layer<16, 2>(accu, wU, lane, [&](int s4) { return s4 < 8 ? xb[s4] : ab[s4 - 8]; });
-    norm_act<2>(accu, muU, sdU, act);
-    if (nvalid) {
-      float* po = a.x_out + (size_t)node * a.ldo + 4 * h;
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 xr = xb[4 * m + g];  // x[node] features 32m + 8g + 4h .. +3
-          *(f32x4*)(po + 32 * m + 8 * g) =
-              (f32x4){__fadd_rn(xr.x, accu[m][4 * g]), __fadd_rn(xr.y, accu[m][4 * g + 1]),
-                      __fadd_rn(xr.z, accu[m][4 * g + 2]), __fadd_rn(xr.w, accu[m][4 * g + 3])};
-        }
-    }
-    // Agg / T are rewritten by the next block only after this wave's reads completed
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Two waves per SIMD (512-thread workgroups, <= 256 registers per wave): the second wave
@@ -698,21 +504,14 @@ extern "C" int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* 
   a.n_nodes = n_nodes;
   a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
-  // one workgroup per CU (LDS); at least one per XCD counter.  RG_CONV_F32_WAVES=1 selects
-  // the one-wave-per-SIMD variant (timing comparison)
-  static const bool one_wave = getenv("RG_CONV_F32_WAVES") && atoi(getenv("RG_CONV_F32_WAVES")) == 1;
-  const int nw = one_wave ? NW : NW2;
+  // one workgroup per CU (LDS); at least one per XCD counter.  (A one-wave-per-SIMD variant
+  // with the next tile's rows prefetched measured slower and was removed.)
   int blocks = 256;
-  const int need = (a.n_blocks + nw - 1) / nw;
+  const int need = (a.n_blocks + NW2 - 1) / NW2;
   if (blocks > need) blocks = need;
   if (blocks < NXCD) blocks = NXCD;
-  if (one_wave) {
-    RG_ENSURE_LDS(conv_f32_kernel, DYN_LDS_MAX);
-    conv_f32_kernel<<<blocks, FT, LDS_BYTES, st>>>(a);
-  } else {
-    RG_ENSURE_LDS(conv_f32_kernel2, DYN_LDS_MAX);
-    conv_f32_kernel2<<<blocks, FT2, LDS_BYTES2, st>>>(a);
-  }
+  RG_ENSURE_LDS(conv_f32_kernel2, DYN_LDS_MAX);
+  conv_f32_kernel2<<<blocks, FT2, LDS_BYTES2, st>>>(a);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -107,11 +107,10 @@ extern "C" int rg_conv_blocks(const int* seg_ptr, int n_nodes, int* blk_nodes, i
   int* off = (int*)((char*)workspace + arr);  // their exclusive scan
   int* bounds = (int*)((char*)workspace + 2 * arr);  // block boundaries in node order
   void* sws = (char*)workspace + 2 * arr + ((size_t)((n_nodes + 1) * sizeof(int)) + 255) / 256 * 256;
-  // block edge cap max(cap_min, E / cap_div); RG_CONV_CAP_MIN / RG_CONV_CAP_DIV are
-  // measurement knobs
-  static const int cap_min = getenv("RG_CONV_CAP_MIN") ? atoi(getenv("RG_CONV_CAP_MIN")) : CAP_MIN;
-  static const int cap_div = getenv("RG_CONV_CAP_DIV") ? atoi(getenv("RG_CONV_CAP_DIV")) : 4096;
-  RG_REQUIRE(cap_min >= 1 && cap_div >= 1, RG_ERR_ARG, "rg_conv_blocks: bad RG_CONV_CAP_*");
+  // block edge cap max(cap_min, E / cap_div): a same-box sweep (scripts/experiments/
+  // gpu_c5_cap.sh) put C5's conv at 0.055 ms here and at min 64; 0.061 at E / 2048, at min
+  // 256 and at (64, E / 8192); 0.080 at 32-edge blocks
+  constexpr int cap_min = CAP_MIN, cap_div = 4096;
   conv_blocks_kernel<false><<<(nb8 + 255) / 256, 256, 0, st>>>(seg_ptr, n_nodes, cnt, nullptr,
                                                                 nullptr, cap_min, cap_div);
   RG_LAUNCH_CHECK();
@@ -147,8 +146,7 @@ extern "C" int rg_conv_wave_nodes(const int* seg_ptr, int n_nodes, int n_waves, 
                                   void* stream) {
   RG_REQUIRE(seg_ptr && wave_nodes && n_nodes >= 1 && n_waves >= 1, RG_ERR_ARG,
              "rg_conv_wave_nodes: bad argument");
-  static const int cost = getenv("RG_CONV_NODE_COST") ? atoi(getenv("RG_CONV_NODE_COST"))
-                                                     : rg::conv::WAVE_NODE_COST;
+  constexpr int cost = rg::conv::WAVE_NODE_COST;  // (4, 7 or 10 edge units: same within noise)
   conv_wave_nodes_kernel<<<(n_waves + 1 + 255) / 256, 256, 0, (hipStream_t)stream>>>(
       seg_ptr, n_nodes, n_waves, cost, wave_nodes);
   RG_LAUNCH_CHECK();

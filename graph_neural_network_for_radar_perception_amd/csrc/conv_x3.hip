@@ -733,16 +733,18 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
 // wave reads the word of the slot it just closed after the barrier, so all waves leave
 // after the same slot (the word of slot s is next written in slot s + 2, after the barrier
 // every reader of slot s must reach first).
-template <bool CENT>
+template <bool CENT, int MODE>
 __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[4];
   __shared__ uint32_t done_w[2];
+  __shared__ int tok[NW / 2];  // MODE 2: per SIMD pair, the group whose M phase is next (2: free)
   if (threadIdx.x < 2) {
     nrm[2 * threadIdx.x] = *a.mu[threadIdx.x];
     nrm[2 * threadIdx.x + 1] = *a.sd[threadIdx.x];
     done_w[threadIdx.x] = 0;
   }
+  if (threadIdx.x < NW / 2) tok[threadIdx.x] = 0;
   stage_lds<FT>(lds + WE_OFF, a.w[0], x3_bytes(C, HID));
   stage_lds<FT>(lds + W2_OFF, a.w[1], x3_bytes(HID, C));
   __syncthreads();
@@ -998,7 +1000,33 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
     ++slot;
     return all;
   };
-  if (wave < NW / 2) {  // waves 0-3: V first
+  if constexpr (MODE == 2) {
+    // RG_CX3_PP 2: no workgroup lock-step -- each wave loops V, M on its own, and the two
+    // waves of a SIMD (w, w + 4) pass a matrix-pipe token: a wave starts its M phase only
+    // when the token is its group's (or free), and hands it over at the M phase's end.  The
+    // token orders nothing the results depend on (every wave computes its own tiles), so the
+    // wait is bounded and a wave leaving sets it free for good.
+    const int pair = wave & (NW / 2 - 1), g = wave >= NW / 2;
+    for (;;) {
+      vphase();
+      if (!have) break;  // no block left (the last V phase flushed the last sum)
+#if RG_CX3_STAMP
+      tick();
+#endif
+      for (int spin = 0; spin < (1 << 16); ++spin) {
+        const int t = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&tok[pair], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (t == g || t == 2) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+#if RG_CX3_STAMP
+      st[4] += tick();
+#endif
+      mphase();
+      if (lane == 0) atomicCAS(&tok[pair], g, 1 - g);
+    }
+    if (lane == 0) atomicExch(&tok[pair], 2);
+  } else if (wave < NW / 2) {  // waves 0-3: V first
     for (;;) {
       vphase();
       if (sync()) break;
@@ -1256,8 +1284,7 @@ extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
 
 extern "C" int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream) {
   RG_REQUIRE(seg_ptr && table && n_nodes >= 1, RG_ERR_ARG, "rg_conv_x3_blocks: bad argument");
-  static const int order = getenv("RG_CX3_ORDER") ? atoi(getenv("RG_CX3_ORDER")) : 0;
-  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table, order);
+  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table, 0);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -1311,7 +1338,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
                           next_pq->act == RG_ACT_NONE),
              RG_ERR_UNSUPPORTED, "rg_conv_layer_x3: next_pq must be the 64 -> 256 projection");
   // RG_LAYER_E_SPLIT: e = the pre-split planes (rg_mlp_chain_x3_split), lde in BYTES
-  const bool espl = (m0.flags & RG_LAYER_E_SPLIT) != 0;
+  const bool espl = false;  // (the pre-split e path of conv_x3_kernel is no longer reachable)
   RG_REQUIRE(ldx % 4 == 0 && ld_out % 4 == 0 && (espl ? lde % 16 == 0 && lde >= 384 : lde % 4 == 0),
              RG_ERR_UNSUPPORTED,
              "rg_conv_layer_x3: row strides must be multiples of 4 (pre-split e: 16 bytes, >= 384)");
@@ -1356,7 +1383,8 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
   auto edge = cent ? (espl ? conv_x3_kernel<true, NODE, true> : conv_x3_kernel<true, NODE, false>)
                    : (espl ? conv_x3_kernel<false, NODE, true> : conv_x3_kernel<false, NODE, false>);
-  if (RG_CX3_PP && !NODE && !espl) edge = cent ? conv_x3_pp_kernel<true> : conv_x3_pp_kernel<false>;
+  if (RG_CX3_PP && !NODE && !espl)
+    edge = cent ? conv_x3_pp_kernel<true, RG_CX3_PP> : conv_x3_pp_kernel<false, RG_CX3_PP>;
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
   RG_LAUNCH_CHECK_ZERO(a.counters, CTR_BYTES, stream);

@@ -825,10 +825,9 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
     for (int l = 0; l + 1 < n_layers; ++l) kmax = layers[l].out_dim > kmax ? layers[l].out_dim : kmax;
     a.sstride = kpad(kmax, 64) + 8;
     const size_t slabs = (size_t)CH_WAVES * TR * a.sstride * sizeof(float);
-    // RG_CHAIN_WLDS_MAX (measurement knob): weight images larger than this many bytes are
-    // read from L2 instead of staged in LDS (more resident workgroups per CU)
-    static const long wlds_max = getenv("RG_CHAIN_WLDS_MAX") ? atol(getenv("RG_CHAIN_WLDS_MAX")) : -1;
-    const bool fits = dbytes + woff + slabs <= LDS_LIMIT && (wlds_max < 0 || (long)woff <= wlds_max);
+    // (reading the weights from L2 instead of staging them, for more resident workgroups per
+    // CU, measured slower on the training tape: 9.8 -> 11.1-12.0 ms)
+    const bool fits = dbytes + woff + slabs <= LDS_LIMIT;
     if (x3) return fits ? launch_chain<float, true, true>(a, rows, st)
                         : launch_chain<float, false, true>(a, rows, st);
     if (fits) return launch_chain<float, true>(a, rows, st);

@@ -242,8 +242,19 @@ struct SegArgs {
   int ld_out;
 };
 
+// the streaming schedule of a plain CSR: G segments per lane group (0: the one-segment-per-
+// group kernel), U rows in flight per lane
+struct Sched {
+  int G, U;
+};
+// the compiled (G, U) pairs of the streaming kernel
+static bool sched_compiled(Sched s) {
+  return s.G == 0 || (s.G == 1 && (s.U == 4 || s.U == 8 || s.U == 12 || s.U == 16)) ||
+         (s.G == 2 && (s.U == 4 || s.U == 8)) || (s.G == 4 && s.U == 8);
+}
+
 template <typename TS, typename TO, int VEC>
-static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
+static void launch_seg(int op, hipStream_t st, const SegArgs& g, Sched sc) {
   constexpr int SPB = 256 / (64 / VEC);
   int grid = ceil_div(g.n_seg, SPB);
   if (grid > 16384) grid = 16384;
@@ -252,20 +263,10 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
       g.ld_bm, g.n_seg, g.C, (TO*)g.out, g.ld_out
   // sum / mean / max over a plain CSR: the streaming kernel, non-temporal row loads (M's
   // CSR, bf16: 0.56 -> 0.70 of HBM with two segments per group; scripts/seg_variants.py).
-  // RG_SEG_STREAM=0 selects the one-segment-per-group kernel (A/B measurement knob).
-  static const bool stream_on = !getenv("RG_SEG_STREAM") || atoi(getenv("RG_SEG_STREAM")) != 0;
-  // (segments per lane group G, rows in flight per lane U): measured on C5's radius CSR (one
-  // 20 000-node frame, 20 rows per segment on average, 63 at most) and on M's kNN CSR
-  // (192 000 segments of ~13 rows), scripts/seg_few.py: (1, 8) beat (2, 8) on both -- more
-  // waves, and a wave waits for its longest segment either way.  RG_SEG_CFG="G,U" selects
-  // another compiled pair (A/B knob, read per launch: the parity test sweeps it).
+  // The schedule comes from the caller (default_sched; rg_segment_reduce_sched for sweeps).
   constexpr int GPB = 256 / (64 / VEC);
-  if (stream_on && !g.idx && !g.seg_end && !g.bm && g.uni == 0 && g.C % 64 == 0) {
-    // longest-first order (C5 sorted: bf16 0.56 -> 0.67 of HBM with 12 rows in flight and
-    // 8-B lanes, scripts/seg_few.py)
-    int G = 1, U = g.order ? 12 : 8;
-    if (const char* cfg = getenv("RG_SEG_CFG")) sscanf(cfg, "%d,%d", &G, &U);
-    if (g.order) G = 1;
+  if (sc.G > 0 && !g.idx && !g.seg_end && !g.bm && g.uni == 0 && g.C % 64 == 0) {
+    int G = g.order ? 1 : sc.G, U = sc.U;
 #define RG_STREAM_ARGS \
   (const TS*)g.src, g.ld_src, g.seg_ptr, ord_, g.n_seg, g.C, (TO*)g.out, g.ld_out
 #define RG_STREAM(G_, U_)                                                                        \
@@ -309,29 +310,29 @@ static void launch_seg(int op, hipStream_t st, const SegArgs& g) {
 
 // dispatch on (src dtype, out dtype, 16-B / 8-B lanes)
 static int launch_any(int op, int src_dtype, int out_dtype, bool v8, hipStream_t st,
-                      const SegArgs& g) {
+                      const SegArgs& g, Sched sc) {
   if (src_dtype == RG_F32 && out_dtype == RG_F32)
-    launch_seg<float, float, 4>(op, st, g);
+    launch_seg<float, float, 4>(op, st, g, sc);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32 && v8)
-    launch_seg<uint16_t, float, 8>(op, st, g);
+    launch_seg<uint16_t, float, 8>(op, st, g, sc);
   else if (src_dtype == RG_BF16 && out_dtype == RG_F32)
-    launch_seg<uint16_t, float, 4>(op, st, g);
+    launch_seg<uint16_t, float, 4>(op, st, g, sc);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16 && v8)
-    launch_seg<uint16_t, uint16_t, 8>(op, st, g);
+    launch_seg<uint16_t, uint16_t, 8>(op, st, g, sc);
   else if (src_dtype == RG_BF16 && out_dtype == RG_BF16)
-    launch_seg<uint16_t, uint16_t, 4>(op, st, g);
+    launch_seg<uint16_t, uint16_t, 4>(op, st, g, sc);
   else if (src_dtype == RG_F32 && out_dtype == RG_BF16)
-    launch_seg<float, uint16_t, 4>(op, st, g);
+    launch_seg<float, uint16_t, 4>(op, st, g, sc);
   else if (src_dtype == RG_F16 && out_dtype == RG_F32 && v8)
-    launch_seg<_Float16, float, 8>(op, st, g);
+    launch_seg<_Float16, float, 8>(op, st, g, sc);
   else if (src_dtype == RG_F16 && out_dtype == RG_F32)
-    launch_seg<_Float16, float, 4>(op, st, g);
+    launch_seg<_Float16, float, 4>(op, st, g, sc);
   else if (src_dtype == RG_F16 && out_dtype == RG_F16 && v8)
-    launch_seg<_Float16, _Float16, 8>(op, st, g);
+    launch_seg<_Float16, _Float16, 8>(op, st, g, sc);
   else if (src_dtype == RG_F16 && out_dtype == RG_F16)
-    launch_seg<_Float16, _Float16, 4>(op, st, g);
+    launch_seg<_Float16, _Float16, 4>(op, st, g, sc);
   else if (src_dtype == RG_F32 && out_dtype == RG_F16)
-    launch_seg<float, _Float16, 4>(op, st, g);
+    launch_seg<float, _Float16, 4>(op, st, g, sc);
   else
     RG_REQUIRE(false, RG_ERR_ARG, "rg_segment_reduce: bad dtypes");
   RG_LAUNCH_CHECK();
@@ -341,6 +342,13 @@ static int launch_any(int op, int src_dtype, int out_dtype, bool v8, hipStream_t
 }  // namespace rg
 
 using namespace rg;
+
+// (segments per lane group, rows in flight per lane) measured on C5's radius CSR (one 20 000-
+// node frame, 20 rows per segment on average, 63 at most) and on M's kNN CSR (192 000
+// segments of ~13 rows), scripts/seg_few.py: (1, 8) beat (2, 8) on both -- more waves, and a
+// wave waits for its longest segment either way; with the longest-first order 12 rows in
+// flight and 8-B lanes (C5 sorted: bf16 0.56 -> 0.67 of HBM)
+static Sched default_sched(bool ordered) { return Sched{1, ordered ? 12 : 8}; }
 
 static bool check_shape(int C, int ld_src, int ld_out) {
   return C > 0 && C <= 256 && C % 4 == 0 && ld_src % 4 == 0 && ld_out % 4 == 0;
@@ -361,11 +369,28 @@ extern "C" int rg_segment_reduce(const void* src, int src_dtype, int ld_src, con
              ld_out);
   if (n_seg <= 0) return RG_OK;
   const SegArgs g = {src, ld_src, seg_ptr, nullptr, nullptr, idx, 0, 0, nullptr, 0, n_seg, C, out, ld_out};
-  // RG_SEG_V4=1: 16-bit rows as 8-B lane loads (16 lanes per 64 channels) -- A/B knob
-  const char* v4 = getenv("RG_SEG_V4");
+  return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out),
+                    (hipStream_t)stream, g, default_sched(false));
+}
+
+extern "C" int rg_segment_reduce_sched(const void* src, int src_dtype, int ld_src,
+                                       const int* seg_ptr, const int* order, int n_seg, int C,
+                                       int op, void* out, int out_dtype, int ld_out, int groups,
+                                       int rows_in_flight, int narrow_lanes, void* stream) {
+  RG_REQUIRE(op >= RG_REDUCE_SUM && op <= RG_REDUCE_MAX, RG_ERR_ARG, "bad reduce op %d", op);
+  RG_REQUIRE(check_shape(C, ld_src, ld_out), RG_ERR_UNSUPPORTED,
+             "rg_segment_reduce_sched: C=%d ld_src=%d ld_out=%d must be multiples of 4", C, ld_src,
+             ld_out);
+  const Sched sc{groups, rows_in_flight};
+  RG_REQUIRE(sched_compiled(sc) && (!order || groups == 1), RG_ERR_UNSUPPORTED,
+             "rg_segment_reduce_sched: (groups %d, rows %d%s) is not a compiled schedule", groups,
+             rows_in_flight, order ? ", ordered" : "");
+  if (n_seg <= 0) return RG_OK;
+  const SegArgs g = {src, ld_src, seg_ptr, order, nullptr, nullptr, 0, 0, nullptr, 0, n_seg, C,
+                     out, ld_out};
   return launch_any(op, src_dtype, out_dtype,
-                    vec8(C, ld_src, out_dtype, ld_out, src, out) && !(v4 && atoi(v4)),
-                    (hipStream_t)stream, g);
+                    !narrow_lanes && vec8(C, ld_src, out_dtype, ld_out, src, out),
+                    (hipStream_t)stream, g, sc);
 }
 
 static int bm_ld(int C) { return (C + 7) / 8 * 8; }
@@ -396,7 +421,7 @@ extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_s
     const SegArgs g1 = {src, ld_src, nullptr, nullptr, nullptr, nullptr, RANGE_BLOCK, (int)n_rows,
                         nullptr, 0, nb, C, w, ldb};
     const int rc = launch_any(op, src_dtype, src_dtype,
-                              vec8(C, ld_src, src_dtype, ldb, src, w), st, g1);
+                              vec8(C, ld_src, src_dtype, ldb, src, w), st, g1, default_sched(false));
     if (rc) return rc;
     bm = w;
   }
@@ -404,7 +429,7 @@ extern "C" int rg_segment_reduce_ranges(const void* src, int src_dtype, int ld_s
                      out, ld_out};
   return launch_any(op, src_dtype, out_dtype, vec8(C, ld_src, out_dtype, ld_out, src, out) &&
                                                   (!bm || ldb % 8 == 0),
-                    st, g);
+                    st, g, default_sched(false));
 }
 
 // ---- longest-first segment order (rg_segment_order): a counting sort of the segments by
@@ -494,8 +519,7 @@ extern "C" int rg_segment_reduce_ordered(const void* src, int src_dtype, int ld_
   const SegArgs g = {src, ld_src, seg_ptr, use ? order : nullptr, nullptr, nullptr, 0, 0, nullptr,
                      0, n_seg, C, out, ld_out};
   // with the order, 16-bit rows as 8-B lane loads (16 lanes per 64 channels: twice the lane
-  // groups; C5 bf16 0.57 -> 0.65); RG_SEG_V8=1 forces 16-B lanes (A/B knob)
-  const char* v8s = getenv("RG_SEG_V8");
-  const bool v8 = (!use || (v8s && atoi(v8s))) && vec8(C, ld_src, out_dtype, ld_out, src, out);
-  return launch_any(op, src_dtype, out_dtype, v8, (hipStream_t)stream, g);
+  // groups; C5 bf16 0.57 -> 0.65)
+  const bool v8 = !use && vec8(C, ld_src, out_dtype, ld_out, src, out);
+  return launch_any(op, src_dtype, out_dtype, v8, (hipStream_t)stream, g, default_sched(use));
 }

@@ -20,7 +20,6 @@
 // bit-reproducible.
 #include "rg_common.h"
 #include "scan.h"
-#include "x3_common.h"
 
 namespace rg {
 namespace train {
@@ -371,9 +370,9 @@ static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
   // two workgroups per CU (one's row staging overlaps another's MFMAs: the kernel stages
   // single-buffered) and chunks of >= 4 staged blocks of GR rows (the partials' reduction
   // keeps eight loads in flight) -- c4 backward 20.4 -> 15.5 ms against one workgroup per
-  // CU and >= 32 blocks; RG_GRAD_WG_PER_CU / RG_GRAD_MIN_BLOCKS are the measurement knobs
-  static const int wg_cu = getenv("RG_GRAD_WG_PER_CU") ? atoi(getenv("RG_GRAD_WG_PER_CU")) : 2;
-  static const int min_blk = getenv("RG_GRAD_MIN_BLOCKS") ? atoi(getenv("RG_GRAD_MIN_BLOCKS")) : 4;
+  // CU and >= 32 blocks (scripts/experiments/gpu_c4_grad.sh: 3 per CU 293, 4 per CU 278
+  // frames/s against 2 per CU 309)
+  constexpr int wg_cu = 2, min_blk = 4;
   long want = 256L * (wg_cu > 0 ? wg_cu : 1) / (g.ot * g.it);
   if (want < 1) want = 1;
   const long mb = min_blk > 0 ? min_blk : 1;
@@ -434,169 +433,15 @@ __global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
   }
 }
 
-// ------------------------------------------------------------------ x3 weight gradient
-// The same partial tiles (OC = 64 OW outputs x IC = 16 NT inputs per workgroup and row
-// chunk, the same partial layout and reduction) on the bf16 matrix cores with the exact
-// three-term splits of x3_common.h: dW += dZ^T X with every product dz * x formed from the
-// six bf16 terms of weight <= 2 (error below 2^-23 |dz x|, f32 accumulation) on
-// v_mfma_f32_32x32x16_bf16 -- six 32-cycle MFMAs per 32 x 32 x 16 block instead of sixteen
-// 32-cycle v_mfma_f32_16x16x4_f32.  The forward tape and dX keep the exact f32 MFMA; dW feeds
-// nothing downstream.  Staging: a thread takes 8 rows x 4 features of dz or x (x gathered by
-// the input mode), splits each feature's 8 values (split8) and writes the three 16-B plane
-// pieces feature-major (ZT[p][o][r], XT[p][i][r], row stride RS), which is the K-contiguous
-// layout both MFMA operands read (lane = output / input index, 8 consecutive rows).
-static constexpr int RS = GR + 8;  // bf16 per feature row in LDS (pad: 80 B between features)
-
-template <int OW, int NT>
-__global__ __launch_bounds__(256) void linear_grad_x3_kernel(const float* __restrict__ dz, int lddz,
-                                                             long rows, int out_dim, GradIn in,
-                                                             long rpc, int vec_x, int vec_z,
-                                                             float* __restrict__ part,
-                                                             float* __restrict__ part_b) {
-  using namespace ::rg::x3;
-  constexpr int OC = 64 * OW, IC = 16 * NT;
-  constexpr int ICP = (IC + 31) / 32 * 32;         // padded to whole 32-wide N tiles
-  constexpr int MW = OC / 32, NW = 4 / MW;         // wave grid: M tile, N phase
-  constexpr int NT32 = ICP / 32, NTW = (NT32 + NW - 1) / NW;
-  constexpr int ZI = (OC / 4) * (GR / 8), XI = (IC / 4) * (GR / 8);
-  static_assert(ZI <= 256 && XI <= 256, "one staging item per thread and operand");
-  __shared__ __attribute__((aligned(16))) __bf16 ZT[3][OC * RS];
-  __shared__ __attribute__((aligned(16))) __bf16 XT[3][ICP * RS];
-  __shared__ float sB[GR / 8][OC];
-  const int chunk = blockIdx.x, ot = blockIdx.y, it = blockIdx.z;
-  const int o0 = ot * OC, i0 = it * IC;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int m = wave % MW, nph = wave / MW;
-  const long r_begin = (long)chunk * rpc;
-  const long r_end = min(rows, r_begin + rpc);
-  // padding input rows of the last N tile stay zero (IC = 16: half a tile)
-  if constexpr (ICP > IC) {
-    for (int t = threadIdx.x; t < 3 * (ICP - IC) * RS; t += 256) {
-      const int p = t / ((ICP - IC) * RS), q = t % ((ICP - IC) * RS);
-      XT[p][IC * RS + q] = (__bf16)0.f;
-    }
-  }
-  f32x16 acc[NTW];
-#pragma unroll
-  for (int n = 0; n < NTW; ++n)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[n][q] = 0.f;
-  float bsum = 0.f;
-  // this thread's staging items: dz features zf .. zf + 3 of rows 8 zq .. 8 zq + 7, and
-  // x features xf .. xf + 3 of rows 8 xq .. 8 xq + 7
-  const bool zon = (int)threadIdx.x < ZI, xon = (int)threadIdx.x < XI;
-  const int zf = 4 * ((int)threadIdx.x % (OC / 4)), zq = (int)threadIdx.x / (OC / 4);
-  const int xf = 4 * ((int)threadIdx.x % (IC / 4)), xq = (int)threadIdx.x / (IC / 4);
-  for (long rb = r_begin; rb < r_end; rb += GR) {
-    f32x4 zv[8], xv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long row = rb + 8 * zq + u;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (zon && row < r_end) {
-        const float* pz = dz + (size_t)row * lddz + o0 + zf;
-        if (vec_z && o0 + zf + 4 <= out_dim) {
-          v = *(const f32x4*)pz;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = o0 + zf + e < out_dim ? pz[e] : 0.f;
-        }
-      }
-      zv[u] = v;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long row = rb + 8 * xq + u;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (xon && row < r_end && i0 + xf < in.in_dim) v = x_chunk(in, row, i0 + xf, vec_x);
-      xv[u] = v;
-    }
-    if (zon) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const X3 sp = split8((f32x4){zv[0][e], zv[1][e], zv[2][e], zv[3][e]},
-                             (f32x4){zv[4][e], zv[5][e], zv[6][e], zv[7][e]});
-        __bf16* d = &ZT[0][(zf + e) * RS + 8 * zq];
-        *(bf16x8_t*)d = sp.p0;
-        *(bf16x8_t*)(d + OC * RS) = sp.p1;
-        *(bf16x8_t*)(d + 2 * OC * RS) = sp.p2;
-        if (it == 0) {
-          float b = 0.f;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) b += zv[u][e];
-          sB[zq][zf + e] = b;
-        }
-      }
-    }
-    if (xon) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const X3 sp = split8((f32x4){xv[0][e], xv[1][e], xv[2][e], xv[3][e]},
-                             (f32x4){xv[4][e], xv[5][e], xv[6][e], xv[7][e]});
-        __bf16* d = &XT[0][(xf + e) * RS + 8 * xq];
-        *(bf16x8_t*)d = sp.p0;
-        *(bf16x8_t*)(d + ICP * RS) = sp.p1;
-        *(bf16x8_t*)(d + 2 * ICP * RS) = sp.p2;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < GR / 16; ++ks) {
-      const int kr = 16 * ks + 8 * (lane >> 5);
-      const __bf16* za = &ZT[0][(32 * m + (lane & 31)) * RS + kr];
-      const bf16x8_t a0 = *(const bf16x8_t*)za, a1 = *(const bf16x8_t*)(za + OC * RS),
-                     a2 = *(const bf16x8_t*)(za + 2 * OC * RS);
-#pragma unroll
-      for (int n = 0; n < NTW; ++n) {
-        const int nn = nph + NW * n;
-        if (nn < NT32) {
-          const __bf16* xb = &XT[0][(32 * nn + (lane & 31)) * RS + kr];
-          const bf16x8_t b0 = *(const bf16x8_t*)xb, b1 = *(const bf16x8_t*)(xb + ICP * RS),
-                         b2 = *(const bf16x8_t*)(xb + 2 * ICP * RS);
-          acc[n] = mf(a2, b0, acc[n]);
-          acc[n] = mf(a1, b1, acc[n]);
-          acc[n] = mf(a0, b2, acc[n]);
-          acc[n] = mf(a1, b0, acc[n]);
-          acc[n] = mf(a0, b1, acc[n]);
-          acc[n] = mf(a0, b0, acc[n]);
-        }
-      }
-    }
-    if (it == 0 && threadIdx.x < OC) {
-#pragma unroll
-      for (int q = 0; q < GR / 8; ++q) bsum += sB[q][threadIdx.x];
-    }
-    __syncthreads();
-  }
-  // lane holds D[o = 32 m + 8 (q >> 2) + 4 (lane >> 5) + (q & 3)][i = 32 nn + (lane & 31)]
-  float* P = part + ((size_t)(chunk * gridDim.y + ot) * gridDim.z + it) * OC * IC;
-#pragma unroll
-  for (int n = 0; n < NTW; ++n) {
-    const int nn = nph + NW * n;
-    const int i = 32 * nn + (lane & 31);
-    if (nn < NT32 && i < IC) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        P[(32 * m + 8 * (q >> 2) + 4 * (lane >> 5) + (q & 3)) * IC + i] = acc[n][q];
-    }
-  }
-  if (it == 0 && threadIdx.x < OC) part_b[((size_t)chunk * gridDim.y + ot) * OC + threadIdx.x] = bsum;
-}
-
 template <int OW, int NT>
 static void launch_grad(const GradGeom& g, const float* dz, int lddz, long rows, int out_dim,
                         const GradIn& in, int vec_x, int vec_z, float* part, float* part_b,
                         hipStream_t st) {
-  // RG_GRAD_X3=1: the split-bf16 kernel (A/B knob, read per call).  Measured on c4: 614 ->
-  // 574 frames/s -- its staging (a split8 per 8 values, transposed LDS stores) outweighs the
-  // 2.7x matrix rate at these 32-row blocks; the exact f32 kernel stays the default
-  const char* x3s = getenv("RG_GRAD_X3");
-  if (x3s && atoi(x3s) != 0)
-    linear_grad_x3_kernel<OW, NT><<<dim3(g.nchunk, g.ot, g.it), 256, 0, st>>>(
-        dz, lddz, rows, out_dim, in, g.rpc, vec_x, vec_z, part, part_b);
-  else
-    linear_grad_kernel<OW, NT><<<dim3(g.nchunk, g.ot, g.it), 256, 0, st>>>(
-        dz, lddz, rows, out_dim, in, g.rpc, vec_x, vec_z, part, part_b);
+  // (a split-bf16 x3 variant of this kernel measured slower on c4, 614 -> 574 frames/s: its
+  // staging -- a three-term split per 8 values, transposed LDS stores -- outweighed the 2.7x
+  // matrix rate at 32-row blocks, and was removed; the exact f32 MFMA kernel is the one)
+  linear_grad_kernel<OW, NT><<<dim3(g.nchunk, g.ot, g.it), 256, 0, st>>>(
+      dz, lddz, rows, out_dim, in, g.rpc, vec_x, vec_z, part, part_b);
 }
 
 // ------------------------------------------------------------------ incidence lists
@@ -928,10 +773,10 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)workspace;
   // 2048 workgroups (8 waves per SIMD: each 16-lane group's row loop is one dependent
-  // load -> compute -> store chain; 512 left it latency-bound, c4 backward -0.7 ms);
-  // RG_FFN_PARTS is the measurement knob
-  static const int parts_env = getenv("RG_FFN_PARTS") ? atoi(getenv("RG_FFN_PARTS")) : 2048;
-  const int parts = parts_env < 1 ? 1 : parts_env > FFN_PARTS_MAX ? FFN_PARTS_MAX : parts_env;
+  // load -> compute -> store chain; 512 left it latency-bound, c4 backward -0.7 ms; 1 024
+  // and 4 096 the same within noise)
+  constexpr int parts = 2048;
+  static_assert(parts <= FFN_PARTS_MAX, "ffn backward partials");
   if (C <= 16)
     ffn_backward_kernel<1><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
                                                   act, dz, lddz, part);
@@ -1040,11 +885,11 @@ extern "C" int rg_gather_segment_sum(const float* src, int ld_src, int col0, int
   RG_REQUIRE(width >= 1 && width <= 256, RG_ERR_UNSUPPORTED, "rg_gather_segment_sum: width %d",
              width);
   if (n_nodes <= 0) return RG_OK;
-  const char* gss = getenv("RG_GSS_STREAM");  // per call: the parity test compares both kernels
-  const bool stream_on = !gss || atoi(gss) != 0;
+  // the streaming kernel for 16-B aligned rows, the one-wave-per-node kernel otherwise (both
+  // sum in list order: the parity test checks each against the sequential float32 sum)
   const bool al = ld_src % 4 == 0 && col0 % 4 == 0 && width % 4 == 0 && ld_out % 4 == 0 &&
                   (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0;
-  if (stream_on && al) {
+  if (al) {
     if (scale)
       gather_segsum_stream<true><<<ceil_div(n_nodes, 16), 256, 0, (hipStream_t)stream>>>(
           src, ld_src, col0, width, ptr, list, scale, n_nodes, out, ld_out, accumulate);

@@ -23,7 +23,6 @@ float32.
 from __future__ import annotations
 
 import ctypes
-import os
 import weakref
 from dataclasses import dataclass
 from typing import List, Optional
@@ -48,18 +47,14 @@ def _half_flag(dtype: str) -> int:
 # Arithmetic of the fused fp32 conv layer: 'x3' = float32 products from exact three-term
 # bf16 splits on the bf16 matrix cores (rg_conv_layer_x3, one launch per layer, the next
 # layer's projections fused into the update); 'mfma_f32' = v_mfma_f32_32x32x2_f32
-# (rg_conv_layer_f32).  Both keep float32 accuracy (tests/test_gpu_f32.py runs both).
-F32_ARITH = os.environ.get('RG_F32_ARITH', 'x3')
-# fp32 link head with its first Linear per node (ModelPlans.link_pairs_pre); '0' = per pair
-LINK_PRE = os.environ.get('RG_LINK_PRE', '1') != '0'
-# fp32 x3 stack: '1' = the edge encoder writes e pre-split (rg_mlp_chain_x3_split, 384 B per
-# edge) and no conv layer re-splits it.  Measured slower on M (conv layer 0.592 -> 0.651 ms,
-# encoder 1.40 -> 1.49 ms: the e rows are the edge launch's only HBM stream and grow by half),
-# so float32 e by default
-E_SPLIT = os.environ.get('RG_E_SPLIT', '0') != '0'
+# (rg_conv_layer_f32).  Both keep float32 accuracy (tests/test_gpu_f32.py runs both by
+# setting this attribute; nothing reads the environment).
+F32_ARITH = 'x3'
+# fp32 link head with its first Linear per node (ModelPlans.link_pairs_pre); False = per pair
+LINK_PRE = True
 # x3 conv over the per-graph work-block table (rg_conv_x3_blocks: LPT order, 8-node tail);
-# '0' = plain 32-node runs (same results)
-CONV_X3_TABLE = os.environ.get('RG_CONV_X3_TABLE', '1') != '0'
+# False = plain 32-node runs (same results)
+CONV_X3_TABLE = True
 
 
 def _dt_code(t: torch.Tensor) -> int:
@@ -332,25 +327,6 @@ class ChainPlan:
             self._x3 = groups[0][0]
         return self._x3
 
-    def x3_split(self, rows: int, out_split: torch.Tensor, in0: torch.Tensor, w0: int,
-                 rows_dev=None) -> bool:
-        """The chain over dense float32 rows with its output pre-split
-        (rg_mlp_chain_x3_split: uint8 [rows][6 x out_dim]); False when no x3 kernel takes it."""
-        if (self.pieces is not None or not self.use_fast or self.dt != nat.RG_F32
-                or F32_ARITH != 'x3' or self.x3_ok.get('split', True) is False
-                or in0.dtype != torch.float32 or len(self.specs) > nat.MAX_LAYERS):
-            return False
-        rc = nat.lib().rg_mlp_chain_x3_split(self._x3_layers(), len(self.specs), int(rows),
-                                             nat.ptr(rows_dev), in0.data_ptr(), in0.stride(0), w0,
-                                             out_split.data_ptr(), out_split.stride(0),
-                                             nat.stream_ptr(self.device))
-        if rc == nat.RG_ERR_UNSUPPORTED:
-            self.x3_ok['split'] = False
-            return False
-        nat.check(rc, 'rg_mlp_chain_x3_split')
-        self.x3_ok['split'] = True
-        return True
-
     def _f32_layers(self):
         """The chain packed RG_PACK_F32_FAST for rg_mlp_chain_f32 (lazily: training chains
         never use it)."""
@@ -446,6 +422,22 @@ def segment_reduce(src: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int, op: str
     return out
 
 
+def segment_reduce_sched(src: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int, op: str,
+                         out: torch.Tensor, groups: int, rows_in_flight: int,
+                         narrow_lanes: bool = False, order: Optional[torch.Tensor] = None):
+    """segment_reduce / segment_reduce_ordered under an explicit schedule
+    (rg_segment_reduce_sched: the parity tests and scripts/seg_few.py sweep the compiled ones)."""
+    lib = nat.lib()
+    C = src.shape[1]
+    nat.check(lib.rg_segment_reduce_sched(src.data_ptr(), _dt_code(src), src.stride(0),
+                                          seg_ptr.data_ptr(), nat.ptr(order), int(n_seg), C,
+                                          nat.REDUCE[op], out.data_ptr(), _dt_code(out),
+                                          out.stride(0), int(groups), int(rows_in_flight),
+                                          int(bool(narrow_lanes)), nat.stream_ptr(src.device)),
+              'rg_segment_reduce_sched')
+    return out
+
+
 def segment_order(seg_ptr: torch.Tensor, n_seg: int) -> torch.Tensor:
     """Longest-first permutation of the CSR's segments (rg_segment_order), int32 [n_seg]."""
     lib = nat.lib()
@@ -537,7 +529,7 @@ class DeviceGraph:
 
     # few 8-node runs per wave of the fused conv's 2 048-wave grid: dynamic scheduling of
     # whole runs leaves a tail of the heaviest runs (dense radius frames, BASELINE config 5)
-    CONV_BLOCK_TABLE_MAX_RUNS = int(os.environ.get('RG_CONV_TABLE_MAX_RUNS', 4 * 2048))
+    CONV_BLOCK_TABLE_MAX_RUNS = 4 * 2048
 
     def conv_blocks(self):
         """(blk_nodes, n_blocks_dev) of rg_conv_blocks -- edge-balanced work blocks for
@@ -560,8 +552,8 @@ class DeviceGraph:
 
     # the 16-bit fused conv's static schedule (rg_conv_wave_nodes) for the same small graphs:
     # equal per-wave shares instead of dequeued blocks ('0': the block table)
-    CONV_WAVES = int(os.environ.get('RG_CONV_WAVES', 2048))
-    CONV_WAVES_MAX_RUNS = int(os.environ.get('RG_CONV_WAVES_MAX_RUNS', 4 * 2048))
+    CONV_WAVES = 2048
+    CONV_WAVES_MAX_RUNS = 4 * 2048
 
     def conv_waves(self):
         """wave_nodes [CONV_WAVES + 1] of rg_conv_wave_nodes for rg_conv_layer_fused_waves, or
@@ -771,12 +763,11 @@ class ConvPlan:
             we = LayerSpec(Wc[:, 2 * C:].contiguous(), None, m0.mu, m0.std, m0.act)
             w_pq, b_pq = pq.weight, pq.bias
             # [0] W_e, [1] msg1, [2] upd (cat(x, agg) read from memory), [3] P | Q from
-            # memory (first layer), [4] P | Q from the previous layer's registers, [5] W_e
-            # for the pre-split e rows (rg_mlp_chain_x3_split: FAST_CHAIN k order)
-            specs = [we, m1, u, pq, pq, we]
+            # memory (first layer), [4] P | Q from the previous layer's registers
+            specs = [we, m1, u, pq, pq]
             fmts = [nat.RG_PACK_FAST_IN | X3, nat.RG_PACK_FAST_CHAIN | X3 | CEN,
                     nat.RG_PACK_FAST_IN | X3 | CEN, nat.RG_PACK_FAST_IN | X3,
-                    nat.RG_PACK_FAST_CHAIN | X3, nat.RG_PACK_FAST_CHAIN | X3]
+                    nat.RG_PACK_FAST_CHAIN | X3]
         else:
             fmts = [nat.RG_PACK_F32_FAST] * 4
         try:
@@ -788,8 +779,6 @@ class ConvPlan:
         if self.f32_arith == 'x3':
             self.fused_layers = layer_array(specs[:3], base, offs[:3], fmts[:3])
             self.fused_layers[0].flags = nat.RG_LAYER_CENTERED   # centred on the host
-            self.fused_layers_esplit = layer_array(specs[:3], base, [offs[5]] + offs[1:3], fmts[:3])
-            self.fused_layers_esplit[0].flags = nat.RG_LAYER_CENTERED | nat.RG_LAYER_E_SPLIT
             self.x3_pq_in = layer_array(specs[3:4], base, offs[3:4], fmts[3:4])
             self.x3_pq_chain = layer_array(specs[4:5], base, offs[4:5], fmts[4:5])
             self._ws = {}
@@ -863,9 +852,8 @@ class ConvPlan:
         return bool(self.fused) and self.f32_arith == 'x3'
 
     def x3_ready(self, x, e) -> bool:
-        """e: float32 rows, or the pre-split rows of rg_mlp_chain_x3_split (uint8 [E][384])."""
         return (self.use_fused and self.x3 and self.fused_ok is not False
-                and x.dtype == torch.float32 and e.dtype in (torch.float32, torch.uint8))
+                and x.dtype == torch.float32 and e.dtype == torch.float32)
 
     def project_x3(self, x, pq) -> bool:
         """P | Q of the first x3 layer (rg_conv_proj_x3); False when the kernel does not
@@ -885,9 +873,7 @@ class ConvPlan:
         st = nat.stream_ptr(x.device)
         ws = self.workspace(lib.rg_conv_layer_x3_workspace_size(g.n_nodes), st)
         tbl = g.conv_x3_blocks()
-        # pre-split e (uint8 rows of rg_mlp_chain_x3_split): its W_e image, stride in bytes
-        layers = self.fused_layers_esplit if e.dtype == torch.uint8 else self.fused_layers
-        args = (layers, nxt.x3_pq_chain if nxt is not None else None,
+        args = (self.fused_layers, nxt.x3_pq_chain if nxt is not None else None,
                 nat.REDUCE[self.aggr], x.data_ptr(), x.stride(0), e.data_ptr(), e.stride(0),
                 pq.data_ptr(), g.seg_ptr.data_ptr(), g.src.data_ptr(), g.dst.data_ptr(), g.n_nodes,
                 x_out.data_ptr(), x_out.stride(0), nat.ptr(pq_out))
@@ -1118,28 +1104,11 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
     x = alloc('x0', (N, plans.node_enc.out_dim), T)
     plans.node_enc(N, x, node_feats, node_feats.shape[1], segs=segs('node'))
     mark('edge_encoder:start', True)
-    e = None
     Ce = plans.edge_enc.out_dim
-    if (E_SPLIT and T == torch.float32 and Ce == 64 and plans.convs
-            and all(cv.x3 and cv.use_fused and cv.fused_ok is not False for cv in plans.convs)):
-        # every layer on the x3 conv: the encoder writes e pre-split once (three bf16 planes
-        # per row) and no layer re-splits it
-        es = alloc('e_split', (Ecap, 6 * Ce), torch.uint8)
-        if plans.edge_enc.x3_split(Ecap, es, edge_feats_dst, edge_feats_dst.shape[1],
-                                   rows_dev=ne_dev):
-            e = es
-    if e is None:
-        e = alloc('e', (Ecap, Ce), T)
-        plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
-                       segs=segs('edge'))
+    e = alloc('e', (Ecap, Ce), T)
+    plans.edge_enc(Ecap, e, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
+                   segs=segs('edge'))
     mark('edge_encoder:end', True)
-
-    def e_f32():
-        """float32 e for a layer the x3 conv did not take (after a pre-split encode)."""
-        ef = alloc('e', (Ecap, Ce), T)
-        plans.edge_enc(Ecap, ef, edge_feats_dst, edge_feats_dst.shape[1], rows_dev=ne_dev,
-                       segs=segs('edge'))
-        return ef
     mark('conv_stack:start', True)
     n_fused = 0
     pq = None   # fp32 x3 layers: this layer's P | Q projections
@@ -1174,8 +1143,6 @@ def forward_batched(plans: ModelPlans, node_feats: torch.Tensor, edge_feats_dst:
             if events and not coarse:
                 events.pop()
             pq = None
-        if e.dtype == torch.uint8:
-            e = e_f32()
         mark('conv_fused:start')
         fused = cv.run_fused(x, e, g, xn)
         if fused:
@@ -1354,8 +1321,12 @@ def run_cluster_head(stem_mods, head_mods, x: torch.Tensor, cluster_node_idx,
     return run_blocks(head_mods, pooled, dtype)
 
 
-def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):
-    """residual_graph_conv_block.forward (gnn_blocks.py:96-110) on one graph."""
+def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32',
+                   extra_features=None):
+    """residual_graph_conv_block.forward (gnn_blocks.py:96-110) on one graph.  A block built
+    with in_extra_feature_dim updates on cat(x, extra, agg) (gnn_blocks.py:107): the aggregate
+    is reduced straight into the columns after the extra features of one [N][d + C_msg] buffer,
+    and the update chain reads cat(x, that buffer) (RG_IN_CONCAT2)."""
     _require_device(node_features, 'node_features')
     dev = node_features.device
     cp = cached_plan(blk, ('conv', dtype), lambda: ConvPlan(blk, dtype, dev))
@@ -1372,15 +1343,28 @@ def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32'):
     msg = torch.empty((max(E, 1), cp.c_msg), dtype=torch.float32, device=dev)
     cp.msg(E, msg, x, x.shape[1], mode=nat.IN_GATHER3, in2=e, w2=e.shape[1], idx0=g.dst,
            idx1=g.src)
-    agg = torch.empty((N, cp.c_msg), dtype=torch.float32, device=dev)
-    segment_reduce(msg, g.seg_ptr, N, cp.aggr, agg)
+    d_extra = 0
+    if blk.in_extra_feature_dim is not None:
+        if extra_features is None:
+            # reference: torch.concat((x, None, agg)) raises
+            raise TypeError('expected Tensor as element 1 in argument 0, but got NoneType')
+        _require_device(extra_features, 'extra_features')
+        d_extra = int(extra_features.shape[1])
+        if extra_features.shape[0] != N or d_extra != blk.in_extra_feature_dim:
+            raise RuntimeError(f'extra_features of shape {tuple(extra_features.shape)}: the block '
+                               f'was built for [{N}, {blk.in_extra_feature_dim}]')
+    xa = torch.empty((N, d_extra + cp.c_msg), dtype=torch.float32, device=dev)
+    if d_extra:
+        xa[:, :d_extra].copy_(extra_features)   # (plumbing: the columns ahead of agg)
+    segment_reduce(msg, g.seg_ptr, N, cp.aggr, xa[:, d_extra:])
     if cp.res is not None:
         ident = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
         cp.res(N, ident, x, x.shape[1])
     else:
         ident = x
     out = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
-    cp.upd(N, out, x, x.shape[1], mode=nat.IN_CONCAT2, in1=agg, w1=cp.c_msg, residual=ident)
+    cp.upd(N, out, x, x.shape[1], mode=nat.IN_CONCAT2, in1=xa, w1=d_extra + cp.c_msg,
+           residual=ident)
     return out
 
 

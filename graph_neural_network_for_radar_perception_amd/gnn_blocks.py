@@ -74,11 +74,11 @@ class residual_graph_conv_block(nn.Module):
             self.residual_connection = nn.Sequential(lin, make_norm(norm_layer, num_groups))
 
     def forward(self, node_features, edge_features, edge_index, extra_features=None):
+        """gnn_blocks.py:96-110; with in_extra_feature_dim the update runs on
+        cat(x, extra_features, agg) (:107)."""
         from . import engine
-        if self.in_extra_feature_dim is not None:
-            raise NotImplementedError('augmented (extra) node features are not used by '
-                                      'Model_Inference and are not supported')
-        return engine.run_conv_block(self, node_features, edge_features, edge_index)
+        return engine.run_conv_block(self, node_features, edge_features, edge_index,
+                                     extra_features=extra_features)
 
 
 class graph_convolution(nn.Module):

@@ -26,7 +26,6 @@ counts (loss.py:59-73 on the concatenated predictions), so batching is exact.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -38,12 +37,12 @@ from .engine import ChainPlan, LayerSpec, specs_from_modules
 
 
 # training forward on the register-resident f32 chains (rg_mlp_chain_f32_ex with tapes)
-# where the shape has an instantiation; '0' = the generic chain kernel for every chain
-TAPE_F32_FAST = os.environ.get('RG_TRAIN_F32FAST', '1') != '0'
-# the backward's data GEMMs dX = dZ W on the register-resident f32 kernel ('0': generic)
-DX_F32_FAST = os.environ.get('RG_TRAIN_DX_FAST', '1') != '0'
-# after an optimizer step, re-pack every f32 image in place in one launch ('0': per chain)
-REPACK_JOBS = os.environ.get('RG_TRAIN_REPACK_JOBS', '1') != '0'
+# where the shape has an instantiation; False = the generic chain kernel for every chain
+TAPE_F32_FAST = True
+# the backward's data GEMMs dX = dZ W on the register-resident f32 kernel (False: generic)
+DX_F32_FAST = True
+# after an optimizer step, re-pack every f32 image in place in one launch (False: per chain)
+REPACK_JOBS = True
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:

@@ -275,8 +275,6 @@ typedef struct rg_layer {
 #define RG_LAYER_CENTERED 1 /* w_packed was packed with RG_PACK_CENTERED */
 #define RG_LAYER_F16 2      /* w_packed holds fp16 fragments (RG_PACK_F16): the fast chain /
                                fused conv then read and write RG_F16 activations */
-#define RG_LAYER_E_SPLIT 4  /* rg_conv_layer_x3 layers[0]: W_e packed FAST_CHAIN | X3 and e
-                               given pre-split by rg_mlp_chain_x3_split (lde in bytes) */
 
 #define RG_MAX_LAYERS 8
 
@@ -343,19 +341,6 @@ int rg_mlp_chain_f32_ex(const rg_layer* layers_host, int n_layers, long rows, co
 int rg_mlp_chain_x3(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
                     int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                     const int* idx1, float* out, int ld_out, void* stream);
-/* The same chain over dense rows (RG_IN_DENSE) with its output written PRE-SPLIT for an x3
- * consumer instead of as float32: each value v as its exact three bf16 terms
- * v = p0 + p1 + p2 (the split the x3 kernels form in registers), row r at
- * out_split + r * ld_split bytes (ld_split % 16 == 0, >= 6 x width; width a multiple of
- * 32): per k-step s (16 features) 96 bytes, plane p (0..2) at byte 96 s + 32 p + 16 h + 2 j
- * of the row holding, for h in 0..1 and j in 0..7, feature 16 s + 8 (j >> 2) + 4 h + (j & 3)
- * (the RG_PACK_FAST_CHAIN k order).  The edge encoder writes e this way once and every
- * rg_conv_layer_x3 with
- * RG_LAYER_E_SPLIT reads it instead of re-splitting the rows per layer.
- * (gnn_blocks.py:19-42 graph_feature_encoding, its output consumed at gnn_blocks.py:159-163) */
-int rg_mlp_chain_x3_split(const rg_layer* layers_host, int n_layers, long rows,
-                          const int* rows_dev, const float* in0, int ld0, int w0,
-                          void* out_split, int ld_split, void* stream);
 
 /* One fused FLOAT32 residual_graph_conv_block (gnn_blocks.py:96-113, the reference
  * precision) for the shipped widths (C = 64, message MLP 192 -> 128 -> 64, update
@@ -390,8 +375,6 @@ int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx,
  *             [b_msg0'; 0]): then pq_out [n_nodes][256] receives it from x_out's registers
  *   workspace rg_conv_layer_x3_workspace_size(n_nodes) bytes, block counters ZEROED before
  *             the first call (every completed launch leaves them zero); one per stream.
- *   layers[0].flags & RG_LAYER_E_SPLIT: e is the pre-split output of rg_mlp_chain_x3_split
- *             (lde = its row stride in BYTES, >= 384) and W_e is packed FAST_CHAIN | X3.
  * Same results contract as rg_conv_layer_f32 (sum in edge order, mean = sum / max(deg, 1)). */
 size_t rg_conv_layer_x3_workspace_size(int n_nodes);
 int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, const float* x,
@@ -542,6 +525,17 @@ int rg_segment_order(const int* seg_ptr, int n_seg, int* order, void* workspace,
 int rg_segment_reduce_ordered(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
                               const int* order, int n_seg, int C, int op, void* out,
                               int out_dtype, int ld_out, void* stream);
+/* rg_segment_reduce / _ordered (order nullable) with an explicit schedule instead of the
+ * measured defaults: groups = segments per lane group of the streaming kernel (0: the
+ * one-segment-per-group kernel), rows_in_flight per lane, narrow_lanes = 1: 16-bit rows
+ * as 8-B lane loads.  Compiled schedules: groups 0; (1, 4 / 8 / 12 / 16); (2, 4 / 8);
+ * (4, 8); with an order, groups 1 only -- anything else returns RG_ERR_UNSUPPORTED.  Same
+ * results, bit for bit, under every schedule (the parity tests sweep them; the library's
+ * own entries never read the environment). */
+int rg_segment_reduce_sched(const void* src, int src_dtype, int ld_src, const int* seg_ptr,
+                            const int* order, int n_seg, int C, int op, void* out, int out_dtype,
+                            int ld_out, int groups, int rows_in_flight, int narrow_lanes,
+                            void* stream);
 
 /* The same reductions over explicit row ranges [seg_begin[s], seg_end[s]) of src
  * [n_rows] (ranges may overlap): the per-object max-pool of the classifier GNN, whose

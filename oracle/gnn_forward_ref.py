@@ -16,7 +16,8 @@ Functional, op-for-op restatement of ``Model_Inference.forward``
   residual_graph_conv_block gnn_blocks.py:45-113, with the PyG 2.5
       ``MessagePassing.propagate`` semantics restated (x_i = x[ei[1]],
       x_j = x[ei[0]], scatter at ei[1]: add / mean / max(include_self=False))
-  graph_convolution     gnn_blocks.py:116-164
+  graph_convolution     gnn_blocks.py:116-164 (with append_extra_features: the flagged
+      blocks update on cat(x, extra, agg), gnn_blocks.py:69-72, 107)
   FFN_TaskSpecificHead  gnn_blocks.py:167-197
   node_segmentation / node_offset_predictions gnn_blocks.py:200-271
   edge_formation + link_predictions gnn_blocks.py:274-344 (triu/nonzero pairs)
@@ -117,8 +118,10 @@ def propagate(ctx, p, x, e, edge_index):
     raise ValueError(ctx.aggr)
 
 
-def conv_block(ctx, p, x, e, edge_index):
-    """residual_graph_conv_block.forward gnn_blocks.py:96-110."""
+def conv_block(ctx, p, x, e, edge_index, extra=None):
+    """residual_graph_conv_block.forward gnn_blocks.py:96-110; ``extra``: the augmented node
+    features of a block built with in_extra_feature_dim (concatenated as (x, extra, agg),
+    gnn_blocks.py:107)."""
     if (p + '.residual_connection.0.weight') in ctx.sd:
         identity = F.linear(x, ctx.sd[p + '.residual_connection.0.weight'],
                             ctx.sd[p + '.residual_connection.0.bias'])
@@ -126,7 +129,19 @@ def conv_block(ctx, p, x, e, edge_index):
     else:
         identity = x
     agg = propagate(ctx, p, x, e, edge_index)
-    return identity + ctx.seq(torch.concat((x, agg), dim=-1), p + '.upd', ctx.count(p + '.upd'))
+    h = torch.concat((x, agg) if extra is None else (x, extra, agg), dim=-1)
+    return identity + ctx.seq(h, p + '.upd', ctx.count(p + '.upd'))
+
+
+def graph_convolution(ctx, p, x, e, edge_index, extra=None, flags=None):
+    """graph_convolution.forward gnn_blocks.py:154-164 (blocks at ``p.conv_blk.<l>``); block l
+    takes the extra features when flags[l] (append_extra_features, gnn_blocks.py:130-133)."""
+    l = 0
+    while f'{p}.conv_blk.{l}.upd.0.block.0.weight' in ctx.sd:
+        use = extra is not None and flags is not None and bool(flags[l])
+        x = conv_block(ctx, f'{p}.conv_blk.{l}', x, e, edge_index, extra if use else None)
+        l += 1
+    return x
 
 
 def link_pairs_from_adj(adj_matrix):

@@ -1,4 +1,5 @@
 import glob
+import json
 import os
 import sys
 
@@ -122,3 +123,30 @@ def grad_within_f32_bound(ours: float, orc: float) -> bool:
     worse (the norm mu / std parameter gradients are sums over every row and feature with
     heavy cancellation: the float32 oracle is 2e-2 .. 2e-1 off float64 on some of them)."""
     return ours <= max(10 * orc, 2e-4) and ours <= max(1e-2, 2 * orc)
+
+
+def grad_bound(orc: float) -> float:
+    """The per-tensor bound grad_within_f32_bound applies: ours <= grad_bound(orc)."""
+    return min(max(10 * orc, 2e-4), max(1e-2, 2 * orc))
+
+
+def grad_report(test: str, rows) -> float:
+    """Gradient headroom of one test: rows = (tensor, ours, orc, raw, env_share) with ours the
+    error max|g - g64| / max|g64| the bound is applied to (beyond the kink envelope where the
+    test has one), orc the float32 oracle's, raw the error before the envelope, env_share the
+    envelope's largest element / max|g64|.  Appends one JSON line per test to $RG_GRAD_REPORT
+    (when set) with every tensor's ours / bound; returns the worst ours / bound."""
+    out = []
+    worst = 0.0
+    for name, ours, orc, raw, env in rows:
+        b = grad_bound(orc)
+        r = ours / b
+        worst = max(worst, r)
+        out.append({'tensor': name, 'err': ours, 'err_before_envelope': raw, 'envelope': env,
+                    'f32_oracle_err': orc, 'bound': b, 'of_bound': r})
+    path = os.environ.get('RG_GRAD_REPORT')
+    if path:
+        out.sort(key=lambda x: -x['of_bound'])
+        with open(path, 'a') as fh:
+            fh.write(json.dumps({'test': test, 'worst_of_bound': worst, 'tensors': out}) + '\n')
+    return worst

@@ -20,7 +20,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import cluster_lists, golden, grad_within_f32_bound, model_cfg, model_state_dict
+from conftest import (cluster_lists, golden, grad_report, grad_within_f32_bound, model_cfg,
+                      model_state_dict)
 
 pytestmark = pytest.mark.gpu
 
@@ -114,7 +115,7 @@ def _kink_envelope(name, d, lists, weights):
         torch.set_default_dtype(prev)
 
 
-def _check_grads(model, name, d, lists, weights):
+def _check_grads(model, name, d, lists, weights, tag=''):
     """Every parameter gradient at least as close to the float64 oracle as float32 allows
     (conftest.grad_within_f32_bound: per tensor max|g - g64| / max|g64| <= max(10 x the
     float32 oracle's own error, 2e-4) and <= max(1e-2, 2 x that error)), |g - g64| taken
@@ -122,6 +123,7 @@ def _check_grads(model, name, d, lists, weights):
     g32 = _oracle_grads(name, d, lists, weights, torch.float32)
     g64 = _oracle_grads(name, d, lists, weights, torch.float64)
     env = _kink_envelope(name, d, lists, weights)
+    rows = []
     for pname, p in model.named_parameters():
         assert p.grad is not None, pname
         key = 'pred.' + pname
@@ -130,7 +132,11 @@ def _check_grads(model, name, d, lists, weights):
         diff = np.abs(p.grad.double().cpu().numpy() - ref)
         ours = float(np.max(np.maximum(diff - env[key], 0.0))) / scale
         orc = float(np.max(np.abs(g32[key].double().numpy() - ref))) / scale
+        rows.append((pname, ours, orc, float(diff.max()) / scale, float(env[key].max()) / scale))
+    worst = grad_report(f'grad_enabled_inference[{tag}]', rows)
+    for pname, ours, orc, _, _ in rows:
         assert grad_within_f32_bound(ours, orc), (pname, ours, orc)
+    print(f'worst gradient error / bound: {worst:.3f}')
 
 
 def _weights(out, seed):
@@ -162,7 +168,7 @@ def test_grad_enabled_cluster_lists_match_reference(cuda_device):
     w = _weights(out, 3)
     total = sum((o * wi.to(dev)).sum() for o, wi in zip(out, w))
     total.backward()
-    _check_grads(detector, name, d, cluster_lists(d), w)
+    _check_grads(detector, name, d, cluster_lists(d), w, 'cluster_lists')
 
 
 @pytest.mark.parametrize('tag', ['off', 'links'])
@@ -212,7 +218,7 @@ def test_grad_enabled_proposals_like_reference_callers(cuda_device, tag):
     w = _weights(outs, 5)
     total = sum((o * wi.to(dev)).sum() for o, wi in zip(outs, w))
     total.backward()
-    _check_grads(detector, name, d, [c.cpu() for c in cluster_members_list], w)
+    _check_grads(detector, name, d, [c.cpu() for c in cluster_members_list], w, f'proposals-{tag}')
 
 
 def test_grad_enabled_frozen_layers_only_object_head_gets_grads(cuda_device):

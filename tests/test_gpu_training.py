@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, grad_within_f32_bound
+from conftest import golden, grad_report, grad_within_f32_bound
 from oracle import train_ref
 
 pytestmark = pytest.mark.gpu
@@ -19,12 +19,27 @@ pytestmark = pytest.mark.gpu
 LOSS_NAMES = ('loss_node_cls', 'loss_node_reg', 'loss_edge_cls', 'loss_obj_cls')
 
 
-def _grad_close(got, want, name, rel=2e-4):
+def _grad_close(got, want, name, rel=2e-4, report=None):
     got = np.asarray(got, np.float64)
     want = np.asarray(want, np.float64)
     tol = rel * float(np.max(np.abs(want))) + (1e-6 if want.size == 1 else 1e-7)
     err = float(np.max(np.abs(got - want))) if want.size else 0.0
+    if report is not None:
+        report.append({'tensor': name, 'err': err, 'bound': tol, 'of_bound': err / tol})
     assert err <= tol, f'{name}: max |d| {err:.3e} > {tol:.3e}'
+
+
+def _fixture_report(test, rows):
+    """Headroom against the reference fixture's 2e-4 x max|g| bound, to $RG_GRAD_REPORT."""
+    import json
+    import os
+    path = os.environ.get('RG_GRAD_REPORT')
+    worst = max((r['of_bound'] for r in rows), default=0.0)
+    if path:
+        rows = sorted(rows, key=lambda x: -x['of_bound'])
+        with open(path, 'a') as fh:
+            fh.write(json.dumps({'test': test, 'worst_of_bound': worst, 'tensors': rows}) + '\n')
+    return worst
 
 
 def _fixture_frames(d, dev):
@@ -76,16 +91,20 @@ def test_training_steps_match_reference(cuda_device, optim):
         if optim == 'torch_sgd':
             total.backward()
             if step == 1:
+                rep = []
                 for name, p in m.named_parameters():
-                    _grad_close(p.grad.cpu().numpy(), d['g1/' + name], name)
+                    _grad_close(p.grad.cpu().numpy(), d['g1/' + name], name, report=rep)
+                _fixture_report(f'training_steps_match_reference[{optim}]', rep)
             opt.step()
             opt.zero_grad()
         else:
             eng = m.train_engine()
             total.backward()
             if step == 1:
+                rep = []
                 for name, p in m.named_parameters():
-                    _grad_close(eng.grads[id(p)].cpu().numpy(), d['g1/' + name], name)
+                    _grad_close(eng.grads[id(p)].cpu().numpy(), d['g1/' + name], name, report=rep)
+                _fixture_report(f'training_steps_match_reference[{optim}]', rep)
             m.zero_grad(set_to_none=True)
             opt.step(eng.flat_grad)
     sd = m.state_dict()
@@ -161,12 +180,17 @@ def test_training_grads_match_oracle_larger(cuda_device, L, aggr):
         assert abs(float(loss[k].detach()) - want_loss[k]) <= 1e-5 * max(1.0, abs(want_loss[k])), k
     for k, v in acc.items():
         assert abs(float(v) - want_acc[k]) <= 1e-6, k
+    rows = []
     for name, p in m.named_parameters():
         ref = g64[name].numpy()
         scale = float(np.max(np.abs(ref))) + 1e-30
         ours = float(np.max(np.abs(p.grad.double().cpu().numpy() - ref))) / scale
         orc = float(np.max(np.abs(g32[name].double().numpy() - ref))) / scale
+        rows.append((name, ours, orc, ours, 0.0))
+    worst = grad_report(f'training_grads_match_oracle_larger[{L}-{aggr}]', rows)
+    for name, ours, orc, _, _ in rows:
         assert grad_within_f32_bound(ours, orc), (name, ours, orc)
+    print(f'worst gradient error / bound: {worst:.3f}')
 
 
 def test_training_step_is_deterministic(cuda_device):
@@ -342,13 +366,12 @@ def test_f32_tape_kernel_matches_generic(cuda_device, monkeypatch):
 
 
 def test_gather_segment_sum_stream_matches_sequential(cuda_device):
-    """rg_gather_segment_sum's streaming kernel (16 lanes per node, 8 rows in flight) sums each
-    node's rows in list order: without a scale bit-identical to the float32 sequential sum (and
-    to the one-wave-per-node kernel, RG_GSS_STREAM=0); with a per-row scale within one rounding
-    per term of it.  Incidence lists (random rows), the identity CSR, column windows of a wider
-    row (col0 / width / ld_src as the message-input transposes use them), accumulate, empty
-    nodes and a 300-row node."""
-    import os
+    """rg_gather_segment_sum's streaming kernel (16 lanes per node, 8 rows in flight; 16-B
+    aligned windows) and its one-wave-per-node kernel (any other window) sum each node's rows
+    in list order: without a scale bit-identical to the float32 sequential sum; with a per-row
+    scale within one rounding per term of it.  Incidence lists (random rows), the identity
+    CSR, column windows of a wider row (col0 / width / ld_src as the message-input transposes
+    use them), accumulate, empty nodes and a 300-row node."""
     from graph_neural_network_for_radar_perception_amd import _native as nat
     dev = cuda_device
     lib = nat.lib()
@@ -364,28 +387,24 @@ def test_gather_segment_sum_stream_matches_sequential(cuda_device):
     src = torch.randn(E, ld, generator=g)
     scale = torch.rand(E, generator=g) + 0.5
 
-    def run(col0, width, use_list, use_scale, accumulate, stream):
+    def run(col0, width, use_list, use_scale, accumulate):
         out = torch.randn(n, 72, generator=torch.Generator().manual_seed(9)).to(dev)
-        os.environ['RG_GSS_STREAM'] = '1' if stream else '0'
-        try:
-            s_dev, p_dev = src.to(dev), ptr.to(dev)
-            l_dev, c_dev = lst.to(dev), scale.to(dev)
-            nat.check(lib.rg_gather_segment_sum(
-                s_dev.data_ptr(), ld, col0, width, p_dev.data_ptr(),
-                l_dev.data_ptr() if use_list else None, c_dev.data_ptr() if use_scale else None,
-                n, out.data_ptr(), 72, int(accumulate), nat.stream_ptr(dev)), 'gss')
-            torch.cuda.synchronize()
-        finally:
-            os.environ.pop('RG_GSS_STREAM', None)
+        s_dev, p_dev = src.to(dev), ptr.to(dev)
+        l_dev, c_dev = lst.to(dev), scale.to(dev)
+        nat.check(lib.rg_gather_segment_sum(
+            s_dev.data_ptr(), ld, col0, width, p_dev.data_ptr(),
+            l_dev.data_ptr() if use_list else None, c_dev.data_ptr() if use_scale else None,
+            n, out.data_ptr(), 72, int(accumulate), nat.stream_ptr(dev)), 'gss')
+        torch.cuda.synchronize()
         return out.cpu()
 
-    for col0, width in ((0, 64), (64, 64), (128, 64), (4, 72)):
+    # (2, 63): not 16-B aligned -> the one-wave-per-node kernel
+    for col0, width in ((0, 64), (64, 64), (128, 64), (4, 72), (2, 63)):
         for use_list, use_scale, acc in ((True, False, False), (True, False, True),
                                          (True, True, False), (False, False, True)):
             if not use_list and tot > E:
                 continue
-            got = run(col0, width, use_list, use_scale, acc, True)
-            old = run(col0, width, use_list, use_scale, acc, False)
+            got = run(col0, width, use_list, use_scale, acc)
             # float32 sequential reference
             base = torch.randn(n, 72, generator=torch.Generator().manual_seed(9))
             ref = base.clone() if acc else torch.zeros(n, 72)
@@ -405,19 +424,15 @@ def test_gather_segment_sum_stream_matches_sequential(cuda_device):
                 assert torch.allclose(got[:, :width], ref[:, :width], rtol=1e-5, atol=1e-5)
             else:
                 assert torch.equal(got[:, :width], ref[:, :width]), (col0, width, use_list, acc)
-                assert torch.equal(got, old), (col0, width, use_list, acc)
 
 
 @pytest.mark.parametrize('shape', [(128, 192, 'gather3'), (64, 128, 'concat2'), (64, 64, 'dense'),
                                    (256, 7, 'dense'), (7, 64, 'dense'), (2, 64, 'pairadd')])
-def test_linear_grad_x3_matches_float64(cuda_device, shape):
-    """rg_linear_grad's weight gradient on the bf16 matrix cores with exact three-term splits
-    (RG_GRAD_X3=1; measured slower than the float32 kernel on c4 and kept as an option) against a float64 evaluation of dZ^T X and sum(dZ): every dW / db entry within
-    2e-5 of max|dW| (the float32 MFMA kernel, the default, is held to the same bound) and the
-    split kernel's error at most 4x the float32 kernel's, over
+def test_linear_grad_matches_float64(cuda_device, shape):
+    """rg_linear_grad's weight gradient (v_mfma_f32_16x16x4_f32, exact f32 products) against a
+    float64 evaluation of dZ^T X and sum(dZ): every dW / db entry within 2e-5 of max|dW|, over
     20 011 rows (a partial last block) in the gathered / concatenated / dense / pair-sum input
     modes the training step uses, including 7- and 2-wide layers (padded tiles)."""
-    import os
     from graph_neural_network_for_radar_perception_amd import _native as nat
     out_dim, in_dim, mode = shape
     dev = cuda_device
@@ -453,26 +468,17 @@ def test_linear_grad_x3_matches_float64(cuda_device, shape):
     ws = torch.empty(lib.rg_linear_grad_workspace_size(rows, out_dim, in_dim), dtype=torch.uint8,
                      device=dev)
     scale = float(want_w.abs().max())
-    errs = {}
-    for x3 in ('1', '0'):
-        dW = torch.zeros(out_dim, in_dim, device=dev)
-        db = torch.zeros(out_dim, device=dev)
-        os.environ['RG_GRAD_X3'] = x3
-        try:
-            p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-            ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
-            nat.check(lib.rg_linear_grad(
-                d['dz'].data_ptr(), out_dim, rows, out_dim, in_dim, mode_c, p(d['in0']),
-                ld(d['in0']), w0, p(d['in1']), ld(d['in1']), w1, p(d['in2']), ld(d['in2']), w2,
-                d['idx0'].data_ptr(), d['idx1'].data_ptr(), dW.data_ptr(), db.data_ptr(),
-                ws.data_ptr(), ws.numel(), nat.stream_ptr(dev)), 'rg_linear_grad')
-            torch.cuda.synchronize()
-        finally:
-            os.environ.pop('RG_GRAD_X3', None)
-        err_w = float((dW.cpu().double() - want_w).abs().max())
-        err_b = float((db.cpu().double() - want_b).abs().max())
-        assert err_w <= 2e-5 * scale, (x3, err_w, scale)
-        assert err_b <= 2e-5 * float(want_b.abs().max()) + 1e-6, (x3, err_b)
-        errs[x3] = err_w
-    # the split products are float32-class: no worse than 4x the float32 MFMA kernel's error
-    assert errs['1'] <= 4 * errs['0'] + 1e-6 * scale, errs
+    dW = torch.zeros(out_dim, in_dim, device=dev)
+    db = torch.zeros(out_dim, device=dev)
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    ld = lambda t: t.stride(0) if t is not None else 0  # noqa: E731
+    nat.check(lib.rg_linear_grad(
+        d['dz'].data_ptr(), out_dim, rows, out_dim, in_dim, mode_c, p(d['in0']),
+        ld(d['in0']), w0, p(d['in1']), ld(d['in1']), w1, p(d['in2']), ld(d['in2']), w2,
+        d['idx0'].data_ptr(), d['idx1'].data_ptr(), dW.data_ptr(), db.data_ptr(),
+        ws.data_ptr(), ws.numel(), nat.stream_ptr(dev)), 'rg_linear_grad')
+    torch.cuda.synchronize()
+    err_w = float((dW.cpu().double() - want_w).abs().max())
+    err_b = float((db.cpu().double() - want_b).abs().max())
+    assert err_w <= 2e-5 * scale, (err_w, scale)
+    assert err_b <= 2e-5 * float(want_b.abs().max()) + 1e-6, err_b

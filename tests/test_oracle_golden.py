@@ -252,3 +252,23 @@ def test_max_aggregation_training_oracle_matches_reference():
         assert abs(v - float(d[f's1/{k}'])) <= 1e-7, (k, v)
     for k, g in grads.items():
         np.testing.assert_allclose(g.numpy(), d['g1/' + k], rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+@pytest.mark.parametrize('name', ['conv_extra_N300', 'conv_extra_proj_N200'])
+def test_extra_features_conv_oracle_matches_reference(name):
+    """graph_convolution with append_extra_features (gnn_blocks.py:116-164; the flagged blocks
+    update on cat(x, extra, agg), :69-72, 107): the oracle restatement against the reference
+    module's own output (tests/golden/conv_extra_*.npz, make_golden.py
+    make_extra_features_fixture)."""
+    from types import SimpleNamespace
+    d = golden(name)
+    sd = {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith('w/')}
+    cfg = SimpleNamespace(activation='leakyrelu', norm_layer='channel_normalization',
+                          num_groups=None, aggregation=str(d['aggregation']))
+    ctx = gnn_forward_ref._Ctx({'g.' + k: v for k, v in sd.items()}, cfg)
+    with torch.no_grad():
+        out = gnn_forward_ref.graph_convolution(ctx, 'g', torch.from_numpy(d['x']),
+                                                torch.from_numpy(d['e']),
+                                                torch.from_numpy(d['edge_index']),
+                                                torch.from_numpy(d['extra']), d['flags'])
+    np.testing.assert_allclose(out.numpy(), d['out'], rtol=1e-5, atol=1e-5)
