@@ -74,6 +74,9 @@ static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
 #ifndef RG_CX3_PP_PRIO
 #define RG_CX3_PP_PRIO 0
 #endif
+#ifndef RG_CX3_PP_PF
+#define RG_CX3_PP_PF 1  // dequeue the next block ahead (conv_x3_pp_kernel prefetch)
+#endif
 #ifndef RG_CX3_STAMP
 #define RG_CX3_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_cx3_stamp
 #endif
@@ -806,15 +809,18 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
     }
   };
   // the next block with edges: its bounds, first tile indices and e rows
-  auto fetch = [&]() {
-    for (;;) {
+  // the next block with edges from the queues (stealing from the other XCDs' tails once
+  // this one drained): its first node and edge range; false when every queue is empty
+  bool dry = false;
+  auto dequeue = [&](int& b0, int& be0, int& be1) {
+    while (!dry) {
       int bi = 0;
       if (lane == 0) bi = atomicAdd(ctr, 1);
       const int blk = blo + __builtin_amdgcn_readfirstlane(bi);
       if (blk >= bhi) {
         if (!RG_CX3_STEAL || !a.steal || ++steal >= NXCD) {
-          alive = false;
-          return;
+          dry = true;
+          break;
         }
         const int x2 = (xcd + steal) % NXCD;  // this XCD's queue is empty: the next one's tail
         blo = xlo(x2);
@@ -822,16 +828,49 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
         ctr = a.counters + CTR_STRIDE * x2;
         continue;
       }
-      n0 = pairs ? pairs[2 * blk] : blk * NBLK;
-      const int nb1 = pairs ? pairs[2 * blk + 1] : min(n0 + NBLK, a.n_nodes);
-      const int e0 = a.seg_ptr[n0];
-      e1 = a.seg_ptr[nb1];
-      if (e0 < e1) {  // (a block without edges leaves its aggregate rows unwritten: degree 0)
-        tn = e0;
-        tile_idx(tn);
-        load_e();
-        return;
-      }
+      b0 = pairs ? pairs[2 * blk] : blk * NBLK;
+      const int nb1 = pairs ? pairs[2 * blk + 1] : min(b0 + NBLK, a.n_nodes);
+      be0 = a.seg_ptr[b0];
+      be1 = a.seg_ptr[nb1];
+      if (be0 < be1) return true;  // (a block without edges leaves its aggregate rows unwritten: degree 0)
+    }
+    return false;
+  };
+  // RG_CX3_PP_PF: the next block is dequeued while the current one runs -- its bounds in the
+  // V phase of the current block's second tile, its first tile's indices in the third's --
+  // so a block switch costs one gather round trip like any other tile, not the dequeue ->
+  // bounds -> indices -> rows chain (pf: 0 nothing prefetched, 1 bounds, 2 and indices)
+  int pf = 0, pn0 = 0, pe0 = 0, pe1 = 0;
+  int pp1 = 0, pd1 = 0, ps1 = 0;
+  auto fetch = [&]() {
+    int e0 = 0;
+    if (pf > 0) {
+      n0 = pn0;
+      e0 = pe0;
+      e1 = pe1;
+    } else if (!dequeue(n0, e0, e1)) {
+      alive = false;
+      return;
+    }
+    tn = e0;
+    if (pf == 2) {
+      p1 = pp1;
+      d1 = pd1;
+      s1 = ps1;
+    } else {
+      tile_idx(tn);
+    }
+    pf = 0;
+    load_e();
+  };
+  auto prefetch = [&]() {
+    if (pf == 0 && !dry) {
+      if (dequeue(pn0, pe0, pe1)) pf = 1;
+    } else if (pf == 1) {
+      pp1 = min(pe0 + r, pe1 - 1);
+      pd1 = a.dst[pp1];
+      ps1 = a.src[pp1];
+      pf = 2;
     }
   };
   // P[dst] | Q[src] rows of M-tile m (accumulator order) of this lane's edge in tile tn
@@ -852,7 +891,7 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
 
   // ================= V phase: norm 2 + segmented sum of acc2, then the next tile into acc1
   auto vphase = [&]() {
-    const int pn0 = n0, pe1 = e1;  // the pending tile's block
+    const int bn0 = n0, be1 = e1;  // the pending tile's block
     const bool fresh = alive && tn >= e1;
 #if RG_CX3_STAMP
     vlast = true;
@@ -879,7 +918,7 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
       norm_leaky<2, CENT>(acc2, mu1, sd1);
 #pragma unroll
       for (int c = 0; c < 32 / TR; ++c) {
-        if (tc + TR * c >= pe1) break;  // wave-uniform
+        if (tc + TR * c >= be1) break;  // wave-uniform
         if (r / TR == c) {
           float* row = T + (r % TR) * TS + 4 * h;
 #pragma unroll
@@ -897,11 +936,11 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
 #pragma unroll
         for (int j = 0; j < TR; ++j) {
           const int eo = TR * c + j;
-          if (tc + eo < pe1) {
+          if (tc + eo < be1) {
             if ((smask >> eo) & 1u) {  // a new destination: flush the finished sum
-              if (cur >= 0) a.agg[(size_t)(pn0 + cur) * C + lane] = run;
+              if (cur >= 0) a.agg[(size_t)(bn0 + cur) * C + lane] = run;
               run = v[j];
-              cur = __builtin_amdgcn_readlane(d, eo) - pn0;
+              cur = __builtin_amdgcn_readlane(d, eo) - bn0;
             } else {
               run += v[j];
             }
@@ -917,7 +956,7 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
     st[8] += dseg;
 #endif
     if (fresh) {  // the previous block is done: its last destination's sum
-      if (cur >= 0) a.agg[(size_t)(pn0 + cur) * C + lane] = run;
+      if (cur >= 0) a.agg[(size_t)(bn0 + cur) * C + lane] = run;
       cur = -1;
       run = 0.f;
     }
@@ -945,6 +984,7 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
       add_pq(2, pr2, qr2);
       add_pq(3, pr0, qr0);
 #endif
+      if (RG_CX3_PP_PF && !fresh) prefetch();
       have = true;
     } else {
       // nothing set up: acc1 defined on every path (else its old value counts as live here)
