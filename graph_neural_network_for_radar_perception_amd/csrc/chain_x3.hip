@@ -271,6 +271,9 @@ __device__ __forceinline__ void run_pre(const Args& a, const char* lds, const fl
 #ifndef RG_X3_FUSED_LASTSB
 #define RG_X3_FUSED_LASTSB 0  // (M edge encoder -0.7 %, interleaved A/B r03h_ab_fusedsb)
 #endif
+#ifndef RG_X3_L0PIPE
+#define RG_X3_L0PIPE 0  // encoders: layer 0 of tile m0 + 1 pipelined under tile m0's layer 1
+#endif
 #ifndef RG_X3_K0SLOT
 #define RG_X3_K0SLOT 0  // encoders' layer 0 (<= 8 inputs) as 3 MFMAs instead of 6 (slot packing)
 #endif
@@ -316,6 +319,74 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
   // edge encoder 12 % slower)
   bf16x8_t A1[2][2][MT1][3];
   lda1(0, A1[0]);
+#if RG_X3_L0PIPE
+  // software pipeline over the layer-0 tiles: tile m0 + 1's layer-0 MFMAs issue ahead of tile
+  // m0's layer-1 MFMAs, and its activation + first split among them, so the layer-1 MFMAs
+  // never wait for a layer-0 result (same products, same order per accumulator).  Layer 1's
+  // A fragments as a ring over the (tile, half) k-steps: the current and the next one
+  auto lda1h = [&](int k, bf16x8_t (&d)[MT1][3]) {  // k = 2 m0 + hf
+#pragma unroll
+    for (int m = 0; m < MT1; ++m)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) d[m][p] = W1(p, (m * KS1 + k) * 1024);
+  };
+  auto l0 = [&](int m0, f32x16 (&y)[RT][1]) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
+    layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
+  };
+  auto actsplit = [&](f32x16 (&y)[RT][1], X3 (&b)[RT]) {
+    if constexpr (sp_act(SPEC, 0)) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) y[t][0][q] = act_t<ACT_LEAKY>(y[t][0][q]);
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) b[t] = split_acc(y[t][0], 0);
+  };
+  bf16x8_t Ak[2][MT1][3];
+  lda1h(0, Ak[0]);
+  f32x16 yn[RT][1];
+  X3 bn[RT];
+  l0(0, yn);
+  actsplit(yn, bn);
+#pragma unroll
+  for (int m0 = 0; m0 < MT0; ++m0) {
+    f32x16 y[RT][1];
+    X3 bh[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      y[t][0] = yn[t][0];
+      bh[t] = bn[t];
+    }
+    if (m0 + 1 < MT0) l0(m0 + 1, yn);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int k = 2 * m0 + hf;
+      if (k + 1 < 2 * MT0) lda1h(k + 1, Ak[(k + 1) & 1]);
+      const bf16x8_t(&A)[MT1][3] = Ak[k & 1];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const X3 b = hf == 0 ? bh[t] : split_acc(y[t][0], 1);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][2], b.p0, acc[t][m]);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][1], b.p1, acc[t][m]);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p2, acc[t][m]);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][1], b.p0, acc[t][m]);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p1, acc[t][m]);
+#pragma unroll
+        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
+      }
+      if (hf == 1 && m0 + 1 < MT0) actsplit(yn, bn);
+      if (RG_X3_FUSED_LASTSB || k + 1 < 2 * MT0) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#else
 #pragma unroll
   for (int m0 = 0; m0 < MT0; ++m0) {
     const int u = m0 & 1;
@@ -372,6 +443,7 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
     // tile 0 may interleave with tile 1's last MFMAs)
     if (RG_X3_FUSED_LASTSB || m0 + 1 < MT0) __builtin_amdgcn_sched_barrier(0);
   }
+#endif
   if constexpr (S::NL > 2) {
     Pend pn[RT];
     epilogue_pend<SPEC, 1, MT1, RT>(acc, nrm, pn);

@@ -66,7 +66,7 @@ static constexpr int PQW = 2 * HID;
 #endif
 static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
 #ifndef RG_CX3_PP
-#define RG_CX3_PP 1  // the edge launch as a two-group ping-pong (conv_x3_pp_kernel)
+#define RG_CX3_PP 0  // 1 / 2: the edge launch as a two-group ping-pong (conv_x3_pp_kernel, barrier / token; measured slower)
 #endif
 #ifndef RG_CX3_PP_PQ
 #define RG_CX3_PP_PQ 2
@@ -76,6 +76,9 @@ static constexpr int NBLK = RG_CX3_NBLK;   // destination nodes per work block
 #endif
 #ifndef RG_CX3_PP_PF
 #define RG_CX3_PP_PF 1  // dequeue the next block ahead (conv_x3_pp_kernel prefetch)
+#endif
+#ifndef RG_CX3_PP_N2M
+#define RG_CX3_PP_N2M 0  // 1: norm 2 at the end of the M phase instead of the start of V
 #endif
 #ifndef RG_CX3_STAMP
 #define RG_CX3_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_cx3_stamp
@@ -447,7 +450,9 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
     STAMP(0);  // block fetch
     float run = 0.f;  // lane = feature: running sum of the current destination
-    int cur = -1;     // its slot (wave-uniform)
+    // its aggregate row (wave-uniform); before the block's first destination a dummy row past
+    // the last node, so a flush never tests for "no destination yet"
+    int crow = a.n_nodes;
     // one tile's gathered rows: P[dst] and Q[src] in accumulator order (features
     // 32m + 8g + 4h .. +3 at [4m + g]), e[edge] in k order (16 s + 8 h .. +3, +4 .. +7 at
     // [2s], [2s + 1])
@@ -560,7 +565,7 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       // destination-change mask of this tile's edges (bit j: edge t0 + j starts a segment)
       const int dprev = __shfl_up(d, 1, 64);
       const uint32_t smask =
-          (uint32_t)__ballot(r == 0 ? d - n0 != cur : d != dprev) &
+          (uint32_t)__ballot(r == 0 ? d != crow : d != dprev) &
           (e1 - t0 >= 32 ? 0xffffffffu : ((1u << (e1 - t0)) - 1u));
       // ---- layer 1: h = P[dst] + Q[src] + W_e e
       const int qt = min(t0 + r, e1 - 1);  // this lane's edge (tile_idx)
@@ -644,13 +649,16 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int q = 0; q < 16; ++q) run += acc2[m][q];
-        cur = 0;
+        crow = n0;
         continue;
       }
-      // ---- segmented sum in edge order, TR edges per LDS pass
+      // ---- segmented sum in edge order, TR edges per LDS pass: a full pass runs without
+      //      bounds checks, each edge one add; a destination change (a set bit of smask,
+      //      wave-uniform, ~2.5 per tile) flushes the finished sum to its row out of line
+      const int nv = min(32, e1 - t0);
 #pragma unroll
       for (int c = 0; c < 32 / TR; ++c) {
-        if (t0 + TR * c >= e1) break;  // wave-uniform
+        if (TR * c >= nv) break;  // wave-uniform
         if (r / TR == c) {
           float* row = T + (r % TR) * TS + 4 * h;
 #pragma unroll
@@ -665,26 +673,37 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
         float v[TR];  // all rows of the pass in flight at once
 #pragma unroll
         for (int j = 0; j < TR; ++j) v[j] = T[j * TS + lane];
+        // branch-free scan: rv[j] = the running sum after edge TR c + j (a set bit restarts
+        // it: rv[j] = v[j]); edges past the block's end add nothing (v = 0, no bit)
+        const uint32_t pm = (smask >> (TR * c)) & ((1u << TR) - 1u);
+        if (TR * c + TR > nv) {
+#pragma unroll
+          for (int j = 0; j < TR; ++j) v[j] = TR * c + j < nv ? v[j] : 0.f;
+        }
+        float rv[TR];
 #pragma unroll
         for (int j = 0; j < TR; ++j) {
-          const int eo = TR * c + j;
-          if (t0 + eo < e1) {
-            if ((smask >> eo) & 1u) {  // a new destination: flush the finished sum
-              if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
-              run = v[j];
-              cur = __builtin_amdgcn_readlane(d, eo) - n0;
-            } else {
-              run += v[j];
-            }
-          }
+          const float prev = j == 0 ? run : rv[j - 1];
+          rv[j] = ((pm >> j) & 1u) ? v[j] : prev + v[j];
         }
+        // the finished sums (~2.5 per tile): at a set bit j the sum before it belongs to the
+        // destination that ended there (crow), then crow = the new edge's destination
+        for (uint32_t m = pm; m; m &= m - 1) {
+          const int j = __builtin_ctz(m);
+          float fin = run;
+#pragma unroll
+          for (int k = 0; k + 1 < TR; ++k) fin = (j == k + 1) ? rv[k] : fin;
+          a.agg[(size_t)crow * C + lane] = fin;
+          crow = __builtin_amdgcn_readlane(d, TR * c + j);
+        }
+        run = rv[TR - 1];
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
       }
       STAMP(5);  // segmented sum
     }
     STAMP(9);  // tile loop exit
-    if (cur >= 0) a.agg[(size_t)(n0 + cur) * C + lane] = run;
+    a.agg[(size_t)crow * C + lane] = run;  // (a block without edges: 0 to the dummy row)
     // the aggregate rows were written by this wave's lanes = features; read them back as
     // rows (lane = node) from L2: stores complete (vmcnt 0), loads bypass L1 (nt)
     if constexpr (NODE) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
@@ -784,7 +803,8 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
   // diagnostic build: [0] V work, [1] of it in block-fetch slots, [2] M work, [3] barrier
   // wait after V, [4] after M, [5] V slots, [6] fetch slots, [7] M slots with a tile,
   // [8] norm 2 + segmented sum, [9] the rest of V after it (gathers' waits, adds)
-  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // [10] norm 2 alone, [11] layer 1 (M), [12] norm 1's statistics (M), [13] M slots' stamps
+  unsigned long long st[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_last = __builtin_amdgcn_s_memtime();
   auto tick = [&]() {
     const unsigned long long n = __builtin_amdgcn_s_memtime();
@@ -915,7 +935,14 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
 #endif
     }
     if (pend) {
-      norm_leaky<2, CENT>(acc2, mu1, sd1);
+      if (!RG_CX3_PP_N2M) norm_leaky<2, CENT>(acc2, mu1, sd1);
+#if RG_CX3_STAMP
+      {
+        const unsigned long long d2 = tick();
+        st[10] += d2;
+        st[8] += d2;
+      }
+#endif
 #pragma unroll
       for (int c = 0; c < 32 / TR; ++c) {
         if (tc + TR * c >= be1) break;  // wave-uniform
@@ -933,19 +960,28 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
         float v[TR];
 #pragma unroll
         for (int j = 0; j < TR; ++j) v[j] = T[j * TS + lane];
+        // branch-free scan as in conv_x3_kernel, the finished sums out of line
+        const int nv = be1 - tc;
+        const uint32_t pm = (smask >> (TR * c)) & ((1u << TR) - 1u);
+        if (TR * c + TR > nv) {
+#pragma unroll
+          for (int j = 0; j < TR; ++j) v[j] = TR * c + j < nv ? v[j] : 0.f;
+        }
+        float rv[TR];
 #pragma unroll
         for (int j = 0; j < TR; ++j) {
-          const int eo = TR * c + j;
-          if (tc + eo < be1) {
-            if ((smask >> eo) & 1u) {  // a new destination: flush the finished sum
-              if (cur >= 0) a.agg[(size_t)(bn0 + cur) * C + lane] = run;
-              run = v[j];
-              cur = __builtin_amdgcn_readlane(d, eo) - bn0;
-            } else {
-              run += v[j];
-            }
-          }
+          const float prev = j == 0 ? run : rv[j - 1];
+          rv[j] = ((pm >> j) & 1u) ? v[j] : prev + v[j];
         }
+        for (uint32_t m = pm; m; m &= m - 1) {
+          const int j = __builtin_ctz(m);
+          float fin = run;
+#pragma unroll
+          for (int k = 0; k + 1 < TR; ++k) fin = (j == k + 1) ? rv[k] : fin;
+          if (cur >= 0) a.agg[(size_t)(bn0 + cur) * C + lane] = fin;
+          cur = __builtin_amdgcn_readlane(d, TR * c + j) - bn0;
+        }
+        run = rv[TR - 1];
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
       }
@@ -1008,13 +1044,28 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
     if (have) {
       if (RG_CX3_PP_PRIO) __builtin_amdgcn_s_setprio(1);
       layer_x3<4, 4, 4, RG_CX3_DB1>(acc1, wE, 0, [&](int s) { return split8(ev[2 * s], ev[2 * s + 1]); });
+#if RG_CX3_STAMP
+      {
+        const unsigned long long d1 = tick();
+        st[11] += d1;
+        st[2] += d1;
+      }
+#endif
       const Pend pn1 = pend_norm_leaky<4, CENT>(acc1, mu0, sd0);
+#if RG_CX3_STAMP
+      {
+        const unsigned long long d1 = tick();
+        st[12] += d1;
+        st[2] += d1;
+      }
+#endif
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias2, m, h);
       layer_x3<8, 2, 2, RG_CX3_DB2>(acc2, w2, 0,
                                     [&](int s) { return split_acc_pend<1>(acc1[s >> 1], s & 1, pn1); });
       // the next tile's e rows (the only rows streamed from HBM) arrive behind the slot
       if (tn < e1) load_e();
+      if (RG_CX3_PP_N2M) norm_leaky<2, CENT>(acc2, mu1, sd1);  // norm 2 here, not in V
       if (RG_CX3_PP_PRIO) __builtin_amdgcn_s_setprio(0);
       have = false;
       pend = true;
@@ -1083,7 +1134,7 @@ __global__ __launch_bounds__(FT) void conv_x3_pp_kernel(Args a) {
   }
 #if RG_CX3_STAMP
   if (lane == 0)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_cx3_stamp[i], st[i]);
+    for (int i = 0; i < 14; ++i) atomicAdd(&g_cx3_stamp[i], st[i]);
 #endif
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1218,7 +1269,9 @@ extern "C" int rg_debug_cx3_stamps(unsigned long long* out_host) {
 
 extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
   static_assert((CTR_STRIDE * NXCD + 1) * sizeof(int) <= CTR_BYTES, "counter area");
-  return CTR_BYTES + (size_t)(n_nodes > 0 ? n_nodes : 1) * C * sizeof(float);
+  // the aggregate rows and one dummy row (the edge launch's flush target before a block's
+  // first destination)
+  return CTR_BYTES + (size_t)((n_nodes > 0 ? n_nodes : 1) + 1) * C * sizeof(float);
 }
 
 extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes,

@@ -35,11 +35,14 @@ with torch.no_grad():
         pipe.forward(batch, gb)
     torch.cuda.synchronize()
     fn(buf)
-v = np.array(buf[:10], dtype=np.float64) / (R * 7 * 2048)   # per wave-launch
-names = ['V work', ' of it fetch slots', 'M work', 'barrier after V', 'barrier after M',
-         'V slots', 'fetch slots', 'M slots', 'V: norm2+segsum(+fetch)', 'V: gathers+adds']
+v = np.array(buf[:14], dtype=np.float64) / (R * 7 * 2048)   # per wave-launch
+names = ['V work', ' of it fetch slots', 'M work', 'barrier after V', 'barrier after M / token wait',
+         'V slots', 'fetch slots', 'M slots', 'V: norm2+segsum(+fetch)', 'V: gathers+adds',
+         'V: norm2 alone', 'M: layer 1', 'M: norm1 stats', '-']
 tot = v[0] + v[2] + v[3] + v[4]
 for i, (n, x) in enumerate(zip(names, v)):
+    if i == 13:
+        continue
     if i in (5, 6, 7):
         print(f'{n:26s} {x:9.2f} per wave-launch')
     else:

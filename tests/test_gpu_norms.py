@@ -153,7 +153,8 @@ def test_frame_norm_backward_degenerate_segments(cuda_device, groups):
 
     def ref(zz, dd, sg):
         zz = zz.clone().requires_grad_(True)
-        m, s = mu_p.clone().requires_grad_(True), sd_p.clone().requires_grad_(True)
+        m = mu_p.clone().to(zz.dtype).requires_grad_(True)
+        s = sd_p.clone().to(zz.dtype).requires_grad_(True)
         loss = 0.0
         for f in range(sg.numel() - 1):
             x = zz[sg[f]:sg[f + 1]]
@@ -188,14 +189,19 @@ def test_frame_norm_backward_degenerate_segments(cuda_device, groups):
         return dz.double().cpu(), dmu.double().cpu(), dsd.double().cpu()
 
     want = ref(z, da, seg)
+    # float32 autograd of the same expression: where cancellation makes dz tiny (a frame whose
+    # groups hold two elements each: the normalised pair is +-1 / sqrt(2) whatever the input,
+    # so dz ~ 0 up to eps), float32 itself is this far from float64
+    want32 = ref(z.float(), da.float(), seg)
     got = run(z, da, seg)
-    for g_, w_, name in zip(got, want, ('dz', 'd_mu', 'd_std')):
+    for g_, w_, w32, name in zip(got, want, want32, ('dz', 'd_mu', 'd_std')):
         assert torch.isfinite(g_).all(), name
         for f in range(len(rows)):
             sl = slice(int(seg[f]), int(seg[f + 1])) if name == 'dz' else slice(None)
             scale = float(w_[sl].abs().max()) + 1e-30
             err = float((g_[sl] - w_[sl]).abs().max())
-            assert err <= 1e-4 * scale, (name, f, err, scale)
+            orc = float((w32[sl].double() - w_[sl]).abs().max())
+            assert err <= max(1e-4 * scale, 10 * orc), (name, f, err, scale, orc)
     if groups == 1:
         return
     # n = 1: one row with one element per group
