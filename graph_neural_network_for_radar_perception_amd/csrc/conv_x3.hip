@@ -344,11 +344,7 @@ __device__ __forceinline__ void node_update(const Args& a, int n0, int n1, const
   node_compute<CENT>(a, w, n0, n1, wU, biasU, wPQ, biasPQ, muU, sdU, lane);
 }
 
-// ESPL: e is the edge encoder's output pre-split (RG_LAYER_E_SPLIT, rg_mlp_chain_x3_split):
-// row q at (char*)e + q lde holds, per k-step s, the three bf16 planes of its 16 features
-// (FAST_CHAIN k order) in 96 B, so layer 1's B operand is three plain 16-B loads per
-// k-step and W_e is packed FAST_CHAIN
-template <bool CENT, bool NODE, bool ESPL>
+template <bool CENT, bool NODE>
 __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[6];
@@ -456,47 +452,22 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
     // one tile's gathered rows: P[dst] and Q[src] in accumulator order (features
     // 32m + 8g + 4h .. +3 at [4m + g]), e[edge] in k order (16 s + 8 h .. +3, +4 .. +7 at
     // [2s], [2s + 1])
-    struct RowsF {
+    struct Rows {
       f32x4 p[16], q[16], e[8];
     };
-    struct RowsS {  // ESPL: e[2 s + plane] = the 16 B of k-step s, planes 0 and 1
-      f32x4 p[16], q[16];
-      u32x4 e[8];
-    };
-    using Rows = std::conditional_t<ESPL, RowsS, RowsF>;
-    // this lane's 16 B of row q, plane pl, k-step s in the pre-split layout
-    auto esp = [&](int q, int pl, int s) {
-      return (const u32x4*)((const char*)a.e + (size_t)q * a.lde + 96 * s + 32 * pl + 16 * h);
-    };
-    // layer 1's B operand of k-step s (ESPL: plane 2 loaded here, one k-step ahead of its
-    // MFMAs -- its lines came into L2 with planes 0 and 1 a tile earlier)
-    auto eop = [&](const Rows& w, int s, int q) {
-      if constexpr (ESPL)
-        return X3{__builtin_bit_cast(bf16x8_t, w.e[2 * s]), __builtin_bit_cast(bf16x8_t, w.e[2 * s + 1]),
-                  __builtin_bit_cast(bf16x8_t, *esp(q, 2, s))};
-      else
-        return split8(w.e[2 * s], w.e[2 * s + 1]);
-    };
-    // (ESPL: planes 0 and 1 -- as many registers as the float32 rows; plane 2 is read at
-    // layer 1, eop)
+    // layer 1's B operand of k-step s
+    auto eop = [&](const Rows& w, int s, int) { return split8(w.e[2 * s], w.e[2 * s + 1]); };
     auto load_e = [&](int q, Rows& w) {
-      if constexpr (ESPL) {
+      const float* pe = a.e + (size_t)q * a.lde + 8 * h;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int pl = 0; pl < 2; ++pl) w.e[2 * s + pl] = *esp(q, pl, s);
-      } else {
-        const float* pe = a.e + (size_t)q * a.lde + 8 * h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i) {
 #if RG_CX3_ENT  // streamed once per layer: non-temporal (keeps the reused P | Q rows in L2)
-          w.e[2 * i] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i));
-          w.e[2 * i + 1] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i + 4));
+        w.e[2 * i] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i));
+        w.e[2 * i + 1] = __builtin_nontemporal_load((const f32x4*)(pe + 16 * i + 4));
 #else
-          w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
-          w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
+        w.e[2 * i] = *(const f32x4*)(pe + 16 * i);
+        w.e[2 * i + 1] = *(const f32x4*)(pe + 16 * i + 4);
 #endif
-        }
       }
     };
     auto load_rows = [&](int q, int dq, int sq, Rows& w) {
@@ -1431,8 +1402,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
                           next_pq->act == RG_ACT_NONE),
              RG_ERR_UNSUPPORTED, "rg_conv_layer_x3: next_pq must be the 64 -> 256 projection");
   // RG_LAYER_E_SPLIT: e = the pre-split planes (rg_mlp_chain_x3_split), lde in BYTES
-  const bool espl = false;  // (the pre-split e path of conv_x3_kernel is no longer reachable)
-  RG_REQUIRE(ldx % 4 == 0 && ld_out % 4 == 0 && (espl ? lde % 16 == 0 && lde >= 384 : lde % 4 == 0),
+  RG_REQUIRE(ldx % 4 == 0 && ld_out % 4 == 0 && lde % 4 == 0,
              RG_ERR_UNSUPPORTED,
              "rg_conv_layer_x3: row strides must be multiples of 4 (pre-split e: 16 bytes, >= 384)");
   RG_REQUIRE(x != x_out, RG_ERR_ARG, "rg_conv_layer_x3: x_out must not alias x");
@@ -1474,9 +1444,8 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   if (blocks < NXCD) blocks = NXCD;
   a.steal = a.n_blocks >= 2 * blocks * NW;
   constexpr bool NODE = !RG_CX3_NODE_KERNEL;  // node phase inside the edge launch
-  auto edge = cent ? (espl ? conv_x3_kernel<true, NODE, true> : conv_x3_kernel<true, NODE, false>)
-                   : (espl ? conv_x3_kernel<false, NODE, true> : conv_x3_kernel<false, NODE, false>);
-  if (RG_CX3_PP && !NODE && !espl)
+  auto edge = cent ? conv_x3_kernel<true, NODE> : conv_x3_kernel<false, NODE>;
+  if constexpr (RG_CX3_PP != 0 && !NODE)  // (variant builds only)
     edge = cent ? conv_x3_pp_kernel<true, RG_CX3_PP> : conv_x3_pp_kernel<false, RG_CX3_PP>;
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
