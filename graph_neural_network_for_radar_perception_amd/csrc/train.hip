@@ -70,13 +70,15 @@ template <int J>  // features per lane = J (C <= 16 J)
 __global__ __launch_bounds__(256) void ffn_backward_kernel(
     const float* __restrict__ z, int ldz, const float* __restrict__ da, int ldda, long rows,
     int C, int has_norm, const float* __restrict__ mu, const float* __restrict__ sd, int act,
-    float* __restrict__ dz, int lddz, float* __restrict__ part) {
-  __shared__ float red[16][2];
+    float* __restrict__ dz, int lddz, double* __restrict__ part) {
+  __shared__ double red[16][2];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 4, q = lane & 15;
   const float s = has_norm ? *sd : 1.f;
   const float m = has_norm ? *mu : 0.f;
-  float acc_s = 0.f, acc_m = 0.f;  // per 16-lane group, rows in fixed order
+  // per 16-lane group, rows in fixed order; in float64: d_mu / d_std are sums over every
+  // element of the layer with heavy cancellation (each row's 16-lane sum stays float32)
+  double acc_s = 0.0, acc_m = 0.0;
   for (long row = ((long)blockIdx.x * 4 + wave) * 4 + grp; row < rows;
        row += (long)gridDim.x * 16) {
     float zv[J], gv[J];
@@ -114,8 +116,8 @@ __global__ __launch_bounds__(256) void ffn_backward_kernel(
       ps = group16_sum(ps);
       pm = group16_sum(pm);
       A = group16_sum(A);
-      acc_s += ps;
-      acc_m += pm;
+      acc_s += (double)ps;
+      acc_m += (double)pm;
       const float coef = stdv > 0.f ? r * r * A / ((float)(C - 1) * stdv) : 0.f;
       float gd[J], sg = 0.f;
 #pragma unroll
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void ffn_backward_kernel(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float ts = 0.f, tm = 0.f;
+    double ts = 0.0, tm = 0.0;
     for (int i = 0; i < 16; ++i) {
       ts += red[i][0];
       tm += red[i][1];
@@ -154,26 +156,29 @@ __global__ __launch_bounds__(256) void ffn_backward_kernel(
 }
 
 // sum of PARTS (s, m) partials in a fixed order, added to the parameter gradients
-__global__ __launch_bounds__(256) void ffn_param_reduce(const float* __restrict__ part, int parts,
+__global__ __launch_bounds__(256) void ffn_param_reduce(const double* __restrict__ part, int parts,
                                                         float* __restrict__ d_mu,
                                                         float* __restrict__ d_sd) {
-  __shared__ float red[4][2];
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  float s = 0.f, m = 0.f;
+  __shared__ double red[256][2];
+  const int t = threadIdx.x;
+  double s = 0.0, m = 0.0;
   for (int i = t; i < parts; i += 256) {
     s += part[2 * i];
     m += part[2 * i + 1];
   }
-  s = wave_sum(s);
-  m = wave_sum(m);
-  if (lane == 0) {
-    red[wave][0] = s;
-    red[wave][1] = m;
-  }
+  red[t][0] = s;
+  red[t][1] = m;
   __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {  // fixed tree order
+    if (t < w) {
+      red[t][0] += red[t + w][0];
+      red[t][1] += red[t + w][1];
+    }
+    __syncthreads();
+  }
   if (t == 0) {
-    *d_sd += (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
-    *d_mu += (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    *d_sd = (float)((double)*d_sd + red[0][0]);
+    *d_mu = (float)((double)*d_mu + red[0][1]);
   }
 }
 
@@ -491,7 +496,7 @@ __global__ __launch_bounds__(256) void gather_segsum_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int f = lane + 64 * j;
-        if (f < width) acc[j] += scale ? p[f] * sc : p[f];
+        if (f < width) acc[j] = scale ? __fmaf_rn(p[f], sc, acc[j]) : __fadd_rn(acc[j], p[f]);
       }
     }
 #pragma unroll
@@ -758,7 +763,7 @@ using namespace rg::train;
 
 // ----------------------------------------------------------------------------- C ABI
 extern "C" size_t rg_ffn_backward_workspace_size(void) {
-  return (size_t)FFN_PARTS_MAX * 2 * sizeof(float);
+  return (size_t)FFN_PARTS_MAX * 2 * sizeof(double);
 }
 
 extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
@@ -771,7 +776,7 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
   RG_REQUIRE(act >= ACT_NONE && act <= ACT_SWISH, RG_ERR_ARG, "rg_ffn_backward: act %d", act);
   if (rows <= 0) return RG_OK;
   hipStream_t st = (hipStream_t)stream;
-  float* part = (float*)workspace;
+  double* part = (double*)workspace;
   // 2048 workgroups (8 waves per SIMD: each 16-lane group's row loop is one dependent
   // load -> compute -> store chain; 512 left it latency-bound, c4 backward -0.7 ms; 1 024
   // and 4 096 the same within noise)

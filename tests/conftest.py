@@ -130,6 +130,9 @@ def grad_bound(orc: float) -> float:
     return min(max(10 * orc, 2e-4), max(1e-2, 2 * orc))
 
 
+GRAD_HEADROOM = 0.5  # the gradient tests' headroom assertion: worst tensor <= this x its bound
+
+
 def grad_report(test: str, rows) -> float:
     """Gradient headroom of one test: rows = (tensor, ours, orc, raw, env_share) with ours the
     error max|g - g64| / max|g64| the bound is applied to (beyond the kink envelope where the

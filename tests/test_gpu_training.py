@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, grad_report, grad_within_f32_bound
+from conftest import GRAD_HEADROOM, golden, grad_report, grad_within_f32_bound
 from oracle import train_ref
 
 pytestmark = pytest.mark.gpu
@@ -191,6 +191,8 @@ def test_training_grads_match_oracle_larger(cuda_device, L, aggr):
     for name, ours, orc, _, _ in rows:
         assert grad_within_f32_bound(ours, orc), (name, ours, orc)
     print(f'worst gradient error / bound: {worst:.3f}')
+    # headroom: every tensor at most half its bound
+    assert worst <= GRAD_HEADROOM, worst
 
 
 def test_training_step_is_deterministic(cuda_device):
