@@ -27,6 +27,14 @@ using namespace ::rg::x3;
 #define RG_X3_DB 1  // weight fragments read this many k-steps ahead in the chained layers
                     // (1 vs 0, M: edge encoder 1.52 -> 1.45 ms)
 #endif
+#ifndef RG_X3_DB_MT2
+#define RG_X3_DB_MT2 RG_X3_DB  // the same for layers of <= 2 M-tiles (a k-step of 6 MT RT MFMAs
+                               // is then shorter than an L2 round trip)
+#endif
+template <int MT>
+constexpr int x3_db() {
+  return MT <= 2 ? RG_X3_DB_MT2 : RG_X3_DB;
+}
 
 enum { IN_SMALL = 0,   // float32 rows of <= 8 features; layer 0 (no norm) fused into layer 1
        IN_DENSE = 1,   // float32 rows, K0 % 16 == 0
@@ -149,6 +157,11 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
   }
 }
 
+#ifndef RG_X3_SKEW
+#define RG_X3_SKEW 0  // row tile 1's epilogue issued under row tile 0's first k-step of the next
+                      // layer (layer_x3's pre1) when a wave holds two row tiles
+#endif
+
 #ifndef RG_X3_JIT
 #define RG_X3_JIT 1  // a normalised layer's scale + act applied in the next layer's B operand
 #endif
@@ -176,12 +189,39 @@ __device__ __forceinline__ void epilogue_pend(f32x16 (&acc)[RT][MT], const float
   }
 }
 
+// epilogue_pend of row tile t only
+template <int SPEC, int l, int MT>
+__device__ __forceinline__ void epilogue_pend_one(f32x16 (&acc)[MT], const float* nrm, Pend& pn) {
+  constexpr int K = pend_kind<SPEC, l>();
+  if constexpr (K == 1) {
+    pn = pend_norm_leaky<MT, sp_cent(SPEC)>(acc, nrm[2 * l], nrm[2 * l + 1]);
+  } else if constexpr (K == 2) {
+    pn = pend_norm_only<MT, sp_cent(SPEC)>(acc, nrm[2 * l], nrm[2 * l + 1]);
+  } else {
+    epilogue<SPEC, l, MT>(acc, nrm);
+    pn = Pend{0.f, 0.f};
+  }
+}
+// a layer's epilogue before the next layer: every row tile, or with RG_X3_SKEW at two row
+// tiles only tile 0 (tile 1's runs as the next layer_x3's pre1)
+template <int SPEC, int l, int MT, int RT>
+__device__ __forceinline__ void epilogue_next(f32x16 (&acc)[RT][MT], const float* nrm,
+                                              Pend (&pn)[RT]) {
+  if constexpr (RG_X3_SKEW && RT == 2) {
+    epilogue_pend_one<SPEC, l, MT>(acc[0], nrm, pn[0]);
+    pn[1] = Pend{0.f, 0.f};
+  } else {
+    epilogue_pend<SPEC, l, MT, RT>(acc, nrm, pn);
+  }
+}
+
 // layers l.. of the chain; prev = the previous layer's activations (RT row tiles), with
-// the previous layer's norm / act still pending (PEND) where pend_kind says so
+// the previous layer's norm / act still pending (PEND) where pend_kind says so (with
+// RG_X3_SKEW at RT = 2: row tile 1's epilogue of layer l - 1 not yet run at all)
 template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND>
-__device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[RT][PMT],
-                                         const Pend (&pend)[RT], const char* lds, const float* nrm,
-                                         long row0, long rows, int lane) {
+__device__ __forceinline__ void run_rest(const Args& a, f32x16 (&prev)[RT][PMT], Pend (&pend)[RT],
+                                         const char* lds, const float* nrm, long row0, long rows,
+                                         int lane) {
   constexpr int N = S::N[l], MT = N / 32, KS = S::K(l) / 16;
   static_assert(S::K(l) == 32 * PMT, "chained width");
   const int h = lane >> 5;
@@ -191,12 +231,17 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[RT]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
-  layer_x3<KS, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, l>(a, lds, lane), 0, [&](int s, int t) {
-    return split_acc_pend<PEND>(prev[t][s >> 1], s & 1, pend[t]);
-  });
+  auto bop = [&](int s, int t) { return split_acc_pend<PEND>(prev[t][s >> 1], s & 1, pend[t]); };
+  if constexpr (RG_X3_SKEW && RT == 2) {
+    layer_x3<KS, MT, MT, RT, x3_db<MT>()>(acc, src_of<S, LM, l>(a, lds, lane), 0, bop, [&]() {
+      epilogue_pend_one<SPEC, l - 1, PMT>(prev[1], nrm, pend[1]);
+    });
+  } else {
+    layer_x3<KS, MT, MT, RT, x3_db<MT>()>(acc, src_of<S, LM, l>(a, lds, lane), 0, bop);
+  }
   if constexpr (l + 1 < S::NL) {
     Pend pn[RT];
-    epilogue_pend<SPEC, l, MT, RT>(acc, nrm, pn);
+    epilogue_next<SPEC, l, MT, RT>(acc, nrm, pn);
     run_rest<S, SPEC, LM, l + 1, RT, MT, pend_kind<SPEC, l>()>(a, acc, pn, lds, nrm, row0, rows,
                                                               lane);
   } else {
@@ -218,11 +263,11 @@ __device__ __forceinline__ void run_first(const Args& a, const X3 (&b0)[RT][KS0]
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[t][m] = ld_bias_frag(bias, m, h);
-  layer_x3<KS0, MT, MT, RT, RG_X3_DB>(acc, src_of<S, LM, 0>(a, lds, lane), 0,
+  layer_x3<KS0, MT, MT, RT, x3_db<MT>()>(acc, src_of<S, LM, 0>(a, lds, lane), 0,
                                   [&](int s, int t) { return b0[t][s]; });
   if constexpr (S::NL > 1) {
     Pend pn[RT];
-    epilogue_pend<SPEC, 0, MT, RT>(acc, nrm, pn);
+    epilogue_next<SPEC, 0, MT, RT>(acc, nrm, pn);
     run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
   } else {
 #pragma unroll
@@ -264,7 +309,7 @@ __device__ __forceinline__ void run_pre(const Args& a, const char* lds, const fl
   }
   static_assert(S::NL > 1, "a pair chain continues after layer 0");
   Pend pn[RT];
-  epilogue_pend<SPEC, 0, MT, RT>(acc, nrm, pn);
+  epilogue_next<SPEC, 0, MT, RT>(acc, nrm, pn);
   run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
 }
 
@@ -446,7 +491,7 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
 #endif
   if constexpr (S::NL > 2) {
     Pend pn[RT];
-    epilogue_pend<SPEC, 1, MT1, RT>(acc, nrm, pn);
+    epilogue_next<SPEC, 1, MT1, RT>(acc, nrm, pn);
     run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>()>(a, acc, pn, lds, nrm, row0, rows, lane);
   } else {
 #pragma unroll

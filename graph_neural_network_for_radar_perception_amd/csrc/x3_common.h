@@ -174,14 +174,25 @@ struct WMix {
   }
 };
 
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // acc[t][m] += W[m-tile m0 + m] . B_t over KS k-steps for RT row tiles t; W an x3 image of
 // MTW M-tiles; bop(s, t) returns the split B operand of k-step s, row tile t.  Per k-step
 // the A fragments are issued first and the B operands are split while they arrive; the
 // small terms go first.
 // DB: the A fragments of k-step s + 1 are issued before the MFMAs of step s (double
 // buffer: MT * 12 more registers, no wait on the fragment loads between k-steps).
-template <int KS, int MT, int MTW, int RT, int DB = 0, typename WSrc, typename BOp>
-__device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, int m0, BOp&& bop) {
+// pre1 (RT = 2): the previous layer's epilogue of row tile 1, run after row tile 0's first
+// MFMAs are issued instead of before the layer -- a one-k-step skew of the two row tiles at
+// the layer boundary, so that epilogue (row statistics, a dependent reduction) issues while
+// the matrix pipe works on tile 0 rather than in front of an idle pipe.
+template <int KS, int MT, int MTW, int RT, int DB = 0, typename WSrc, typename BOp,
+          typename Hook = NoHook>
+__device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, int m0, BOp&& bop,
+                                         Hook&& pre1 = Hook{}) {
+  constexpr bool LAZY = RT == 2 && !std::is_same<std::decay_t<Hook>, NoHook>::value;
   // DB: A fragments read DB k-steps ahead (a ring of DB + 1 buffers); 0: at their step
   constexpr int NBUF = DB + 1;
   bf16x8_t Ab[NBUF][MT][3];
@@ -200,7 +211,9 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
   X3 bq[RG_X3_PIPE ? RT : 1];
   if constexpr (RG_X3_PIPE) {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) bq[t] = bop(0, t);
+    for (int t = 0; t < (LAZY ? 1 : RT); ++t) bq[t] = bop(0, t);
+  } else if constexpr (LAZY) {
+    static_assert(!LAZY, "pre1 needs the B-operand pipeline");
   }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -214,11 +227,19 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
     if constexpr (RG_X3_PIPE) {
       if (s + 1 < KS) {
 #pragma unroll
-        for (int t = 0; t < RT; ++t) bn[t] = bop(s + 1, t);
+        for (int t = 0; t < RT; ++t)
+          if (!(LAZY && s == 0 && t == 1)) bn[t] = bop(s + 1, t);
       }
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
+      if constexpr (LAZY) {
+        if (s == 0 && t == 1) {  // tile 0's first MFMAs are issued: tile 1's epilogue now
+          pre1();
+          bq[1] = bop(0, 1);
+          if (s + 1 < KS) bn[1] = bop(1, 1);
+        }
+      }
       const X3 b = RG_X3_PIPE ? bq[t] : bop(s, t);
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[t][m] = mf(A[m][2], b.p0, acc[t][m]);
@@ -247,6 +268,21 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
       __builtin_amdgcn_sched_group_barrier(0x002, RG_X3_SGB, 0);
     }
 #endif
+#ifndef RG_X3_SKEW_SGB
+#define RG_X3_SKEW_SGB 0  // > 0: (1 MFMA, n VALU) sched groups over pre1's k-step region (n = 3, 6, 10 left larger gaps)
+#endif
+    if constexpr (LAZY && RG_X3_SKEW_SGB > 0) {
+      // the region from the previous layer's last k-step to here holds both tiles' epilogues:
+      // ask the scheduler to spread their VALU between the MFMAs (in-order issue: VALU after an
+      // MFMA run in program order cannot use the pipe's shadow)
+      if (s == 0) {
+#pragma unroll
+        for (int i = 0; i < 12 * MT * RT; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, RG_X3_SKEW_SGB, 0);
+        }
+      }
+    }
     // RG_X3_LASTSB 0: no fence after the last k-step, so the caller's epilogue of row tile 0
     // may interleave with the last MFMAs of the other row tiles
     if (RG_X3_LASTSB || s + 1 < KS) __builtin_amdgcn_sched_barrier(0);
