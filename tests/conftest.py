@@ -141,10 +141,14 @@ def is_norm_scalar(name: str) -> bool:
 
 def grad_headroom(rows) -> float:
     """The worst ours / bound over the tensors the headroom assertion covers: every tensor but
-    the norm scalars.  On those (7-layer add model, 2 200 nodes) our error is a consistent
-    8.4x the float32 oracle's (0.84 of the bound; the oracle's error is the same over two
-    summation orders), so it is systematic in the backward, not summation noise: they keep
-    the bound itself (grad_within_f32_bound) and their ratio is in the report."""
+    the norm scalars.  On those (7-layer add model, 2 200 nodes) our error reaches 8.4x the
+    float32 oracle's (0.84 of the bound): they sum gy over every element of a layer, and a
+    LeakyReLU pre-activation within float32 rounding of 0 may take either slope in two valid
+    float32 evaluations -- 27 pre-activations of that batch lie within 1e-7 of their tensor's
+    max of 0, and flipping them moves encode_edge_feat.encoder.3.block.1.mu's gradient by up
+    to 1.3e-3 of its max, 5x our error (scripts/experiments/grad_kink_diag.py,
+    profiles/r04e_grad_kink_diag.log).  They keep the bound itself (grad_within_f32_bound)
+    and their ratio is in the report."""
     return max([ours / grad_bound(orc) for name, ours, orc, _, _ in rows
                 if not is_norm_scalar(name)] or [0.0])
 
