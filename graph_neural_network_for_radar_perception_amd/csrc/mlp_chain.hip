@@ -43,6 +43,7 @@ template <> struct Cfg<uint16_t> {
   static constexpr int KPAD = 32;
   static constexpr int STRIDE = MAXW + 16;  // 544 B rows
 };
+template <> struct Cfg<_Float16> : Cfg<uint16_t> {};  // IEEE fp16 slab (RG_F16), bf16's layout
 
 __host__ __device__ inline int kpad(int k, int p) { return (k + p - 1) / p * p; }
 
@@ -120,8 +121,9 @@ __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, in
 
 // plane p > 0: the p-th term of the exact three-term bf16 split (RG_PACK_X3 | RG_BF16, the
 // generic chain's f32 arithmetic on bf16 products); transpose: W holds the [in][out] matrix
+// f16: IEEE fp16 fragments (RG_BF16 | RG_PACK_F16, the generic chain's fp16 operands)
 __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out, int plane,
-                                 int transpose, uint16_t* __restrict__ P, long total) {
+                                 int transpose, uint16_t* __restrict__ P, long total, int f16 = 0) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S = kpad(in, 32) / 32;
@@ -135,7 +137,7 @@ __global__ void pack_bf16_kernel(const float* __restrict__ W, int in, int out, i
   float v = 0.f;
   if (o < out && k < in) v = transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k];
   for (int q = 0; q < plane; ++q) v -= bf16_to_f32(f32_to_bf16(v));  // exact residues
-  P[t] = f32_to_bf16(v);
+  P[t] = f16 ? f32_to_f16(v) : f32_to_bf16(v);
 }
 
 // 32x32x16 fragments: [m][s][lane][8] = W[32m + (lane&31)][k(s, lane>>5, j)] with
@@ -222,11 +224,13 @@ __global__ void pack_bias_frag_kernel(const float* __restrict__ b, int out, int 
 
 // ------------------------------------------------------------------ element access
 __device__ __forceinline__ float ld_elem(const void* p, int dt, size_t i) {
-  return dt == RG_F32 ? ((const float*)p)[i] : bf16_to_f32(((const uint16_t*)p)[i]);
+  if (dt == RG_F32) return ((const float*)p)[i];
+  const uint16_t h = ((const uint16_t*)p)[i];
+  return dt == RG_F16 ? f16_to_f32(h) : bf16_to_f32(h);
 }
 __device__ __forceinline__ void st_elem(void* p, int dt, size_t i, float v) {
   if (dt == RG_F32) ((float*)p)[i] = v;
-  else ((uint16_t*)p)[i] = f32_to_bf16(v);
+  else ((uint16_t*)p)[i] = dt == RG_F16 ? f32_to_f16(v) : f32_to_bf16(v);
 }
 
 // 4 consecutive elements of a row, as floats (vector load when aligned and complete)
@@ -235,6 +239,12 @@ __device__ __forceinline__ f32x4 ld4(const void* p, int dt, size_t i, int valid,
   if (vec && valid >= 4) {
     if (dt == RG_F32) {
       v = *(const f32x4*)((const float*)p + i);
+    } else if (dt == RG_F16) {
+      const uint2 u = *(const uint2*)((const uint16_t*)p + i);
+      v.x = f16_to_f32((uint16_t)(u.x & 0xffffu));
+      v.y = f16_to_f32((uint16_t)(u.x >> 16));
+      v.z = f16_to_f32((uint16_t)(u.y & 0xffffu));
+      v.w = f16_to_f32((uint16_t)(u.y >> 16));
     } else {
       const uint2 u = *(const uint2*)((const uint16_t*)p + i);
       v.x = __uint_as_float(u.x << 16);
@@ -257,6 +267,12 @@ template <> __device__ __forceinline__ void st4_slab<uint16_t>(uint16_t* p, f32x
   uint2 w;
   w.x = pack_bf16x2(v.x, v.y);
   w.y = pack_bf16x2(v.z, v.w);
+  *(uint2*)p = w;
+}
+template <> __device__ __forceinline__ void st4_slab<_Float16>(_Float16* p, f32x4 v) {
+  uint2 w;
+  w.x = pack_f16x2(v.x, v.y);
+  w.y = pack_f16x2(v.z, v.w);
   *(uint2*)p = w;
 }
 
@@ -384,6 +400,26 @@ template <> struct Mfma<uint16_t> {
   }
 };
 
+template <> struct Mfma<_Float16> {  // RG_F16: v_mfma_f32_16x16x32_f16, bf16's fragment layout
+  typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ void run(f32x4 (&acc)[16], const _Float16* slab,
+                                             const _Float16* P, int mt, int K, int lane, int SS) {
+    const int S = kpad(K, 32) / 32;
+    const _Float16* brow = slab + (lane & 15) * SS + 8 * (lane >> 4);
+    for (int s = 0; s < S; ++s) {
+      const f16x8_t b = __builtin_bit_cast(f16x8_t, *(const u32x4*)(brow + 32 * s));
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m < mt) {
+          const u32x4 av = *(const u32x4*)(P + (((size_t)m * S + s) * 64 + lane) * 8);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, av), b,
+                                                           acc[m], 0, 0, 0);
+        }
+      }
+    }
+  }
+};
+
 // float32 arithmetic on the bf16 matrix cores (RG_F32X3): the f32 slab's 8 k values per
 // lane split exactly into three bf16 terms (x3_common.h), weights pre-split into three
 // planes of the 16x16x32 fragment format; six products of weight <= 2 per k-step
@@ -478,6 +514,11 @@ __device__ __forceinline__ void store_rows(const f32x4 (&acc)[16], const ChainAr
       if (vec) {
         if (a.out_dtype == RG_F32) {
           *(f32x4*)((float*)a.out + (size_t)row * a.ld_out + f0) = v;
+        } else if (a.out_dtype == RG_F16) {
+          uint2 w;
+          w.x = pack_f16x2(v.x, v.y);
+          w.y = pack_f16x2(v.z, v.w);
+          *(uint2*)((uint16_t*)a.out + (size_t)row * a.ld_out + f0) = w;
         } else {
           uint2 w;
           w.x = pack_bf16x2(v.x, v.y);
@@ -650,9 +691,9 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   hipStream_t st = (hipStream_t)stream;
   const int f16 = (dtype & RG_PACK_F16) ? 1 : 0;
   dtype &= ~RG_PACK_F16;
-  RG_REQUIRE(!f16 || ((dtype & ~RG_PACK_CENTERED) >= RG_PACK_FAST_IN &&
-                      (dtype & ~RG_PACK_CENTERED) <= RG_PACK_FAST_UPD),
-             RG_ERR_ARG, "rg_pack_linear: RG_PACK_F16 applies to the RG_PACK_FAST_* formats");
+  RG_REQUIRE(!f16 || dtype == RG_BF16 || ((dtype & ~RG_PACK_CENTERED) >= RG_PACK_FAST_IN &&
+                                          (dtype & ~RG_PACK_CENTERED) <= RG_PACK_FAST_UPD),
+             RG_ERR_ARG, "rg_pack_linear: RG_PACK_F16 applies to RG_BF16 and the RG_PACK_FAST_* formats");
   if (dtype & RG_PACK_X3) {
     return pack_x3(weight, bias, in_dim, out_dim,
                    dtype & ~(RG_PACK_X3 | RG_PACK_CENTERED | RG_PACK_TRANSPOSE),
@@ -678,7 +719,7 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   if (dtype == RG_BF16) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     pack_bf16_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, 0, 0,
-                                                           (uint16_t*)packed, total);
+                                                           (uint16_t*)packed, total, f16);
   } else if (dtype == RG_PACK_FAST_IN || dtype == RG_PACK_FAST_CHAIN || dtype == RG_PACK_FAST_UPD) {
     long total = (long)frag_bytes(in_dim, out_dim, dtype) / sizeof(uint16_t);
     const int ks = (in_dim + 15) / 16;
@@ -763,12 +804,15 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
                             int ld_out, int out_dtype, void* stream) {
   RG_REQUIRE(n_layers >= 1 && n_layers <= RG_MAX_LAYERS, RG_ERR_ARG,
              "rg_mlp_chain: n_layers=%d outside 1..%d", n_layers, RG_MAX_LAYERS);
-  RG_REQUIRE(dtype == RG_F32 || dtype == RG_BF16 || dtype == RG_F32X3, RG_ERR_ARG,
+  RG_REQUIRE(dtype == RG_F32 || dtype == RG_BF16 || dtype == RG_F16 || dtype == RG_F32X3, RG_ERR_ARG,
              "rg_mlp_chain: bad dtype");
   const bool x3 = dtype == RG_F32X3;
-  const int wfmt = x3 ? (RG_BF16 | RG_PACK_X3) : dtype;  // the layers' packed format
-  RG_REQUIRE(in_dtype == RG_F32 || in_dtype == RG_BF16, RG_ERR_ARG, "rg_mlp_chain: bad in_dtype");
-  RG_REQUIRE(out_dtype == RG_F32 || out_dtype == RG_BF16, RG_ERR_ARG, "rg_mlp_chain: bad out_dtype");
+  // the layers' packed format (RG_F16: RG_BF16's fragments holding fp16, RG_PACK_F16)
+  const int wfmt = x3 ? (RG_BF16 | RG_PACK_X3) : dtype == RG_F16 ? RG_BF16 : dtype;
+  auto dt_ok = [&](int d) { return d == RG_F32 || d == RG_BF16 || d == RG_F16; };
+  RG_REQUIRE(dt_ok(in_dtype), RG_ERR_ARG, "rg_mlp_chain: bad in_dtype");
+  RG_REQUIRE(dt_ok(out_dtype), RG_ERR_ARG, "rg_mlp_chain: bad out_dtype");
+  RG_REQUIRE(!residual || dt_ok(res_dtype), RG_ERR_ARG, "rg_mlp_chain: bad res_dtype");
   RG_REQUIRE(in_mode >= RG_IN_DENSE && in_mode <= RG_IN_PAIRADD, RG_ERR_ARG, "bad in_mode");
   RG_REQUIRE((in_mode != RG_IN_GATHER3 && in_mode != RG_IN_PAIRADD) || (idx0 && idx1), RG_ERR_ARG,
              "rg_mlp_chain: gather modes need idx0 and idx1");
@@ -835,6 +879,9 @@ extern "C" int rg_mlp_chain(int dtype, const rg_layer* layers, int n_layers, lon
   }
   a.sstride = Cfg<uint16_t>::STRIDE;
   const size_t slabs = (size_t)CH_WAVES * TR * Cfg<uint16_t>::STRIDE * sizeof(uint16_t);
-  if (dbytes + woff + slabs <= LDS_LIMIT) return launch_chain<uint16_t, true>(a, rows, st);
+  const bool fits = dbytes + woff + slabs <= LDS_LIMIT;
+  if (dtype == RG_F16)
+    return fits ? launch_chain<_Float16, true>(a, rows, st) : launch_chain<_Float16, false>(a, rows, st);
+  if (fits) return launch_chain<uint16_t, true>(a, rows, st);
   return launch_chain<uint16_t, false>(a, rows, st);
 }

@@ -36,8 +36,9 @@ from .common import (Activation, channel_normalization, ffn_block, group_normali
 
 DTYPES = {'fp32': (nat.RG_F32, torch.float32), 'bf16': (nat.RG_BF16, torch.bfloat16),
           'fp16': (nat.RG_F16, torch.float16)}
-# the 16-bit compute dtypes: register-resident fast chains and the fused conv only (the yml
-# widths); 'fp16' = IEEE binary16 operands (BASELINE config 5), packed with RG_PACK_F16
+# the 16-bit compute dtypes: register-resident fast chains and the fused conv for the yml
+# widths, the generic chain + segment reduce for any other; 'fp16' = IEEE binary16 operands
+# (BASELINE config 5), packed with RG_PACK_F16
 HALF = ('bf16', 'fp16')
 
 
@@ -244,9 +245,10 @@ class ChainPlan:
             for t in (s.weight, s.bias, s.mu, s.std):
                 if t is not None:
                     _require_device(t, 'model parameter')
-        # the generic chain kernel (fp32 / bf16; fp16 runs on the fast chains only)
-        self.buf, self.groups = (self._pack_buffer(lambda i: self.dt) if self.dtype != 'fp16'
-                                 else (None, None))
+        # the generic chain kernel (any widths <= 512; fp16 in bf16's fragment layout with
+        # fp16 elements, RG_PACK_F16)
+        self.buf, self.groups = self._pack_buffer(
+            lambda i: (nat.RG_BF16 | nat.RG_PACK_F16) if self.dtype == 'fp16' else self.dt)
         # 16-bit: also the register-resident 32x32x16 formats of rg_mlp_chain_fast
         self.fast = None
         if self.dtype in HALF and len(self.specs) <= nat.MAX_LAYERS:

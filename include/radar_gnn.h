@@ -283,8 +283,10 @@ typedef struct rg_layer {
  * Covers graph_feature_encoding (gnn_blocks.py:19-42), the message and update
  * MLPs of residual_graph_conv_block (:104-113), the stems and
  * FFN_TaskSpecificHead of every task head (:167-389).
+ *   dtype    RG_F32 (f32 MFMA), RG_BF16 / RG_F16 (16-bit operands, f32 accumulation;
+ *            RG_F16's layers packed RG_BF16 | RG_PACK_F16), RG_F32X3
  *   in_mode  RG_IN_*: how row r's input vector is formed from in0/in1/in2
- *   in_dtype element type of in0/in1/in2 (RG_F32 or the chain dtype)
+ *   in_dtype element type of in0/in1/in2 (RG_F32, RG_BF16 or RG_F16)
  *   rows_dev optional device int32 row count (overrides `rows` when non-NULL;
  *            `rows` is then the capacity used for the grid)
  *   residual optional [rows][out_dim] added after the last layer (:109)

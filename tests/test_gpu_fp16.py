@@ -112,3 +112,45 @@ def test_c5_full_size_fp16_within_bound(cuda_device):
     for key, gt, rf in zip(('node_cls', 'node_reg', 'link_cls', 'obj_cls'), got, ref):
         assert gt.shape == tuple(rf.shape), key
         assert_fp16_close(pred, key, gt, rf.numpy())
+
+
+@pytest.mark.parametrize('over', [dict(node_feat_enc_stem_channels=[256, 128, 96],
+                                       graph_convolution_stem_channels=[96, 96]),
+                                  dict(graph_convolution_stem_channels=[64, 64],
+                                       msg_mlp_hidden_dim=96)])
+@pytest.mark.parametrize('dtype', ['fp16', 'bf16'])
+def test_half_non_yml_widths_match_oracle(cuda_device, over, dtype):
+    """16-bit models whose conv blocks are NOT the compiled fused shape (96-wide blocks, a
+    96-wide message hidden layer): the unfused path runs -- the generic chain kernel
+    (v_mfma_f32_16x16x32_f16 / _bf16 with fp16 / bf16 activations between launches) and
+    the fp16 / bf16 segment reduce -- and every output is within its 16-bit bound of the
+    fp32 oracle (fp16: 8 u S_k with u = 2^-11; bf16: u = 2^-8)."""
+    from graph_neural_network_for_radar_perception_amd import synthetic
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    dev = cuda_device
+    cfg = default_config(**over)
+    torch.manual_seed(31)
+    m = Model_Training(cfg, 'cpu')
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    m.pred.compute_dtype = dtype
+    pred = m.pred.eval().requires_grad_(False)
+    fr = synthetic.make_frame(400, 4242)
+    g = gref.build_frame_graph(fr, 25.0, 10, GRID_MAX_R)
+    cl = [torch.from_numpy(c) for c in synthetic.cluster_lists(400)]
+    args = (torch.from_numpy(g['node_features']), torch.from_numpy(g['edge_features']),
+            torch.from_numpy(g['edge_index']))
+    with torch.no_grad():
+        out = pred(*(a.to(dev) for a in args), None, [c.to(dev) for c in cl])
+        ref = gnn_forward_ref.forward(sd, cfg, *args, None, cl)
+    plans = pred.plans(dtype)
+    assert any(not cv.fused_ok for cv in plans.convs), 'expected an unfused conv layer'
+    u = FP16_U if dtype == 'fp16' else 2.0 ** -8
+    for key, o, r in zip(('node_cls', 'node_reg', 'link_cls', 'obj_cls'), out, ref):
+        got, rf = o.float().cpu().numpy(), r.numpy()
+        assert got.shape == rf.shape, key
+        assert np.isfinite(got).all(), key
+        bound = fp16_bound(key, rf, pred) * (u / FP16_U)
+        worst = float((np.abs(got - rf) / bound).max()) if got.size else 0.0
+        assert worst <= 1.0, (key, worst)

@@ -646,10 +646,10 @@ def test_segment_order_and_ordered_reduce_bit_exact(cuda_device):
         engine.segment_reduce_sched(src.to(dev), ptr, S, 'add', torch.empty(S, 128, device=dev), 3, 8)
 
 
-@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16', 'fp16'])
 def test_chain_kernel_vs_torch(cuda_device, dtype):
     """rg_mlp_chain against a plain torch fp32 evaluation (widths not multiples of 16,
-    norm on/off, every activation, residual)."""
+    norm on/off, every activation, residual); fp16 = the generic chain's IEEE fp16 operands."""
     from graph_neural_network_for_radar_perception_amd import engine
     from graph_neural_network_for_radar_perception_amd.common import ffn_block
     dev = cuda_device
@@ -681,7 +681,8 @@ def test_chain_kernel_vs_torch(cuda_device, dtype):
         out = torch.empty(1001, 3, device=dev)
         res = torch.randn(1001, 3, device=dev)
         plan(1001, out, x, 13, residual=res)
-    tol = FP32_TOL if dtype == 'fp32' else dict(rtol=0.05, atol=0.05)
+    tol = (FP32_TOL if dtype == 'fp32' else dict(rtol=0.01, atol=0.01) if dtype == 'fp16'
+           else dict(rtol=0.05, atol=0.05))
     torch.testing.assert_close(out, ref + res, **tol)
     del sd
 
