@@ -135,6 +135,24 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
                                            long rows, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int out = a.out_real;
+  // every feature of the tile stored whole in 16-B pieces (wave-uniform: the encoders' rows),
+  // else piece by piece below (padded head outputs; the per-lane test there costs a divergent
+  // branch and a saved mask per piece)
+  if (out >= 32 * MT && (a.ld_out & 3) == 0) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const long row = row0 + 32 * t + r;
+      if (row >= rows) continue;
+      float* o = a.out + (size_t)row * a.ld_out + 4 * h;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *(f32x4*)(o + 32 * m + 8 * g) = (f32x4){acc[t][m][4 * g], acc[t][m][4 * g + 1],
+                                                  acc[t][m][4 * g + 2], acc[t][m][4 * g + 3]};
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const long row = row0 + 32 * t + r;
