@@ -141,6 +141,41 @@ __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT],
   }
 }
 
+// the same k-steps with the B operand of step s formed by bop(s) one step ahead, beside the
+// MFMAs of step s - 1 (a normalised previous layer's scale + LeakyReLU + bf16 pack then issue
+// in the matrix pipe's shadow instead of between the layers)
+template <int KS, int MT, int KT, int S0, typename BOp>
+__device__ __forceinline__ void mfma_steps_jit(BOp&& bop, f32x16 (&acc)[MT], const char* w,
+                                               int lane) {
+  const char* wl = w + lane * 16;
+  constexpr int PD = MT <= 2 ? RG_CONV_PFD : RG_CONV_PFD4;
+  bf16x8_t f[KS][MT];
+#pragma unroll
+  for (int s = 0; s < PD && s < KS; ++s)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) f[s][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s) * 1024));
+  bf16x8_t bq = bop(0);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + PD < KS) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        f[s + PD][m] = ld_bf8((const uint16_t*)(wl + (size_t)(m * KT + S0 + s + PD) * 1024));
+    }
+    bf16x8_t bn = bq;
+    if (s + 1 < KS) bn = bop(s + 1);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = HT::mfma(f[s][m], bq, acc[m]);
+    bq = bn;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+#ifndef RG_CONV_JIT
+#define RG_CONV_JIT 1  // message layer 1's norm + LeakyReLU + pack inside layer 2's k-steps
+#endif
+
 // channel_normalization (common.py:208-220) + activation (rg_common.h)
 // (every block is normalised; with ACT >= 0 every block uses ACT and was packed
 // RG_PACK_CENTERED: host-checked)
@@ -340,13 +375,33 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       for (int m = 0; m < 4; ++m)
         acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * PST, m, h);
       mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
-      if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
-      bf16x8_t b2[8];
-      pack_acc<4>(acc1, b2);
       f32x16 acc2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias1, m, h);
-      mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
+#ifndef RG_NO_FUSED_LEAKY
+      if constexpr (RG_CONV_JIT && ACT == ACT_LEAKY && RG_CONV_EXP != 2) {
+        // the same values as norm_act + pack_acc (same fmas, same order), formed per k-step
+        const f32x2 sc = norm_leaky_scale<4>(acc1, nrm[0], nrm[1], NORM_EPS);
+        mfma_steps_jit<8, 2, 8, 0>([&](int s) {
+          const f32x16& t = acc1[s >> 1];
+          const int q = 8 * (s & 1);
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float y = fmaf(t[q + i], sc.x, sc.y);
+            v[i] = fmaf(fabsf(y), LEAKY_C, y);
+          }
+          return __builtin_bit_cast(bf16x8_t, (u32x4){bf2(v[0], v[1]), bf2(v[2], v[3]),
+                                                      bf2(v[4], v[5]), bf2(v[6], v[7])});
+        }, acc2, w1, lane);
+      } else
+#endif
+      {
+        if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
+        bf16x8_t b2[8];
+        pack_acc<4>(acc1, b2);
+        mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
+      }
       if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1], nrm[2], nrm[3]);
       if (RG_CONV_EXP == 3) {
 #pragma unroll

@@ -362,9 +362,10 @@ __device__ __forceinline__ void channel_norm_pk_centered(f32x16 (&acc)[MT], floa
 static constexpr float LEAKY_PRE = 0.505f;
 static constexpr float LEAKY_C = 0.495f / 0.505f;
 
+// the row statistics of channel_norm_leaky_centered: y' = x gs + gb then |y'| C + y'
 template <int MT>
-__device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], float mu, float sd,
-                                                            float eps) {
+__device__ __forceinline__ f32x2 norm_leaky_scale(const f32x16 (&acc)[MT], float mu, float sd,
+                                                  float eps) {
   constexpr int N = 32 * MT;
   f32x2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
 #pragma unroll
@@ -379,7 +380,14 @@ __device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], f
   float ss = qt.x + qt.y;
   ss = add_xor32(ss);
   const float inv = inv_std_bf16(ss, N, eps);
-  const float gs = LEAKY_PRE * (sd * inv);
+  return (f32x2){LEAKY_PRE * (sd * inv), LEAKY_PRE * mu};
+}
+
+template <int MT>
+__device__ __forceinline__ void channel_norm_leaky_centered(f32x16 (&acc)[MT], float mu, float sd,
+                                                            float eps) {
+  const f32x2 sc = norm_leaky_scale<MT>(acc, mu, sd, eps);
+  const float gs = sc.x;
   const f32x2 gs2 = {gs, gs}, mu2 = {LEAKY_PRE * mu, LEAKY_PRE * mu};
   // all of a tile's packed fmas first, then the scalar ones: a v_fma_f32 reading a
   // v_pk_fma_f32 result right after it costs an s_nop (gfx950 hazard) -- one per pair
