@@ -175,6 +175,9 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
   }
 }
 
+#ifndef RG_X3_INPF
+#define RG_X3_INPF 1  // encoders: the next tile's input rows loaded during this tile's last layer
+#endif
 #ifndef RG_X3_SKEW
 #define RG_X3_SKEW 0  // row tile 1's epilogue issued under row tile 0's first k-step of the next
                       // layer (layer_x3's pre1) when a wave holds two row tiles
@@ -236,10 +239,12 @@ __device__ __forceinline__ void epilogue_next(f32x16 (&acc)[RT][MT], const float
 // layers l.. of the chain; prev = the previous layer's activations (RT row tiles), with
 // the previous layer's norm / act still pending (PEND) where pend_kind says so (with
 // RG_X3_SKEW at RT = 2: row tile 1's epilogue of layer l - 1 not yet run at all)
-template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND>
+// pre: run after the last layer's MFMAs are issued, before its epilogue (the encoders' next-tile
+// input loads: the only loads then in flight, so no weight wait stalls behind them)
+template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND, typename Pre = NoHook>
 __device__ __forceinline__ void run_rest(const Args& a, f32x16 (&prev)[RT][PMT], Pend (&pend)[RT],
                                          const char* lds, const float* nrm, long row0, long rows,
-                                         int lane) {
+                                         int lane, Pre&& pre = Pre{}) {
   constexpr int N = S::N[l], MT = N / 32, KS = S::K(l) / 16;
   static_assert(S::K(l) == 32 * PMT, "chained width");
   const int h = lane >> 5;
@@ -261,8 +266,9 @@ __device__ __forceinline__ void run_rest(const Args& a, f32x16 (&prev)[RT][PMT],
     Pend pn[RT];
     epilogue_next<SPEC, l, MT, RT>(acc, nrm, pn);
     run_rest<S, SPEC, LM, l + 1, RT, MT, pend_kind<SPEC, l>()>(a, acc, pn, lds, nrm, row0, rows,
-                                                              lane);
+                                                              lane, pre);
   } else {
+    pre();
 #pragma unroll
     for (int t = 0; t < RT; ++t) epilogue<SPEC, l, MT>(acc[t], nrm);
     store_rows<RT, MT>(acc, a, row0, rows, lane);
@@ -353,9 +359,10 @@ __device__ __forceinline__ bf16x8_t k0slot_b(const X3& x, int f, int h) {
 
 // encoders: layer 0 (one k-step of <= 8 inputs, no normalisation) fused tile by tile into
 // layer 1: tile m0 of layer 0 is layer 1's k-steps 2 m0 and 2 m0 + 1
-template <typename S, int SPEC, int LM, int RT>
+template <typename S, int SPEC, int LM, int RT, typename Pre = NoHook>
 __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1], const char* lds,
-                                            const float* nrm, long row0, long rows, int lane) {
+                                            const float* nrm, long row0, long rows, int lane,
+                                            Pre&& pre = Pre{}) {
   constexpr int MT0 = S::N[0] / 32, MT1 = S::N[1] / 32, KS1 = S::N[0] / 16;
   static_assert(S::K(0) <= 16, "fused first layer takes one k-step");
   static_assert(!sp_norm(SPEC, 0), "fused first layer is not normalised");
@@ -510,8 +517,10 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
   if constexpr (S::NL > 2) {
     Pend pn[RT];
     epilogue_next<SPEC, 1, MT1, RT>(acc, nrm, pn);
-    run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>()>(a, acc, pn, lds, nrm, row0, rows, lane);
+    run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>()>(a, acc, pn, lds, nrm, row0, rows, lane,
+                                                          pre);
   } else {
+    pre();
 #pragma unroll
     for (int t = 0; t < RT; ++t) epilogue<SPEC, 1, MT1>(acc[t], nrm);
     store_rows<RT, MT1>(acc, a, row0, rows, lane);
@@ -555,6 +564,25 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
   constexpr int TROWS = 32 * RT;
   const long ntiles = (rows + TROWS - 1) / TROWS;
   const long tstride = (long)gridDim.x * (FT / 64);
+  // IN_SMALL (the encoders, <= 8 inputs per row): this tile's raw rows, loaded during the
+  // previous tile's last layer (RG_X3_INPF) instead of at the tile's start, where the HBM
+  // round trip stood in front of the first MFMA with nothing else to issue
+  float vin[RT][8];
+  auto load_in = [&](long tl) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const long row = tl * TROWS + 32 * t + r;
+      const bool ok = row < rows;
+      const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        vin[t][j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
+    }
+  };
+  if constexpr (MODE == IN_SMALL && RG_X3_INPF) {
+    const long t0 = (long)blockIdx.x * (FT / 64) + wave;
+    if (t0 < ntiles) load_in(t0);
+  }
   for (long tile = (long)blockIdx.x * (FT / 64) + wave; tile < ntiles; tile += tstride) {
     const long row0 = tile * TROWS;
     if constexpr (MODE == IN_PAIRPRE) {
@@ -566,11 +594,16 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
       const long row = row0 + 32 * t + r;
       const bool ok = row < rows;
       if constexpr (MODE == IN_SMALL) {
-        const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
         float v[8];
+        if constexpr (RG_X3_INPF) {
 #pragma unroll
-        // both lane halves hold the row with RG_X3_K0SLOT (each carries other split terms)
-        for (int j = 0; j < 8; ++j) v[j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
+          for (int j = 0; j < 8; ++j) v[j] = vin[t][j];
+        } else {
+          const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
+#pragma unroll
+          // both lane halves hold the row with RG_X3_K0SLOT (each carries other split terms)
+          for (int j = 0; j < 8; ++j) v[j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
+        }
         b0[t][0] = split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]});
       } else if constexpr (MODE == IN_DENSE) {
         const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 8 * h;
@@ -595,7 +628,11 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
         }
       }
     }
-    if constexpr (MODE == IN_SMALL)
+    if constexpr (MODE == IN_SMALL && RG_X3_INPF)
+      run_fused01<S, SPEC, LM, RT>(a, b0, lds, nrm, row0, rows, lane, [&]() {
+        if (tile + tstride < ntiles) load_in(tile + tstride);
+      });
+    else if constexpr (MODE == IN_SMALL)
       run_fused01<S, SPEC, LM, RT>(a, b0, lds, nrm, row0, rows, lane);
     else
       run_first<S, SPEC, LM, RT, KS0>(a, b0, lds, nrm, row0, rows, lane);
