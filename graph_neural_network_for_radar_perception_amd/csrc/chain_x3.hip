@@ -678,6 +678,9 @@ static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<
                         // two waves per SIMD: 1.2 KB of spills per lane, not run)
 #endif
 
+#ifndef RG_X3_PAIR_FT
+#define RG_X3_PAIR_FT 768  // link pair chain: 12 waves, 3 per SIMD (133 VGPRs; 238.7 -> 233.2 us, M)
+#endif
 #ifndef RG_X3_HEAD_RT
 #define RG_X3_HEAD_RT 1  // row tiles per wave of the 5-layer task-head chains (two waves / SIMD at 1)
 #endif
@@ -703,7 +706,8 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   // the same link chain from per-node pre-projections (layer 0's planes are not staged), and
   // the per-node rows t: the compute_edge stem block + the bare layer 0 of the pair chain, or
   // the bare layer alone (no stem)
-  RG_X3C2(IN_PAIRPRE, 64, 0b1111, 0b1111, ALL & ~07, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
+  RG_X3C2(IN_PAIRPRE, 64, 0b1111, 0b1111, ALL & ~07, RG_X3_HEAD_RT, RG_X3_PAIR_FT ? RG_X3_PAIR_FT : HFT,
+          64, 64, 64, 64, 32)
   RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, 512, 64, 64)
   RG_X3C2(IN_DENSE, 64, 0, 0, ALL, 1, 512, 64)
   // link edge_formation stem (1 block), object-class stem (3 blocks), object head
