@@ -307,12 +307,26 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   int blk = 0;
   int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
   int s_hi = 0;  // static schedule: the end of this wave's node range
+  // static schedule's dynamic tail: the nodes [wave_nodes[n_waves], n_nodes) after every
+  // static range, in NB-node blocks dealt round robin to the XCDs' counters (unused by the
+  // static schedule otherwise): a wave whose range is done takes the next block of its XCD
+  int t_lo = 0;
+  auto tail_next = [&](int& n0, int& n1) {
+    int b = 0;
+    if (lane == 0) b = atomicAdd(head, 1);
+    b = __shfl(b, 0, 64);
+    n0 = t_lo + NB * (xcd + NQ * b);
+    n1 = min(n0 + NB, a.n_nodes);
+    return n0 < a.n_nodes;
+  };
   if (a.wave_nodes) {
     const int rank = (blockIdx.x % NQ) * (int)(gridDim.x / NQ) * CW + (blockIdx.x / NQ) * CW + wave;
+    t_lo = a.wave_nodes[gridDim.x * CW];
     bn0 = a.wave_nodes[rank];
     s_hi = a.wave_nodes[rank + 1];
     bn1 = min(bn0 + NB, s_hi);
     blk = bn0 < s_hi ? 0 : -1;
+    if (blk < 0 && t_lo < a.n_nodes) blk = tail_next(bn0, bn1) ? 0 : -1;
   } else {
     if (lane == 0) blk = atomicAdd(head, 1);
     blk = blo + __shfl(blk, 0, 64);
@@ -521,6 +535,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       nn0 = n1;
       nn1 = min(n1 + NB, s_hi);
       nxt = nn0 < s_hi ? 0 : -1;
+      if (nxt < 0 && t_lo < a.n_nodes) nxt = tail_next(nn0, nn1) ? 0 : -1;
     } else {
       nxt = blo + __shfl(nxt_raw, 0, 64);
       if (nxt >= bhi) nxt = steal_next();
@@ -658,12 +673,17 @@ __device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes, int ca
 // the static schedule's per-node cost in edge units (the block head (P) and update of an
 // NB-node block, per node; RG_CONV_NODE_COST overrides it for measurement)
 static constexpr int WAVE_NODE_COST = 4;
+// percent of the cost left to the dynamic tail (fused_conv_kernel's tail_next)
+#ifndef RG_CONV_TAIL
+#define RG_CONV_TAIL 0
+#endif
 __global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_nodes, int n_waves,
                                        int node_cost, int* __restrict__ wave_nodes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n_waves) return;
-  // first node n with cost(n) = seg_ptr[n] + node_cost n >= total i / n_waves
-  const long total = (long)seg_ptr[n_nodes] + (long)node_cost * n_nodes;
+  // first node n with cost(n) = seg_ptr[n] + node_cost n >= (static total) i / n_waves; the
+  // static ranges cover (100 - RG_CONV_TAIL) % of the cost, wave_nodes[n_waves] = the tail start
+  const long total = ((long)seg_ptr[n_nodes] + (long)node_cost * n_nodes) * (100 - RG_CONV_TAIL) / 100;
   const long target = total * i / n_waves;
   int lo = 0, hi = n_nodes;
   while (lo < hi) {
@@ -671,7 +691,7 @@ __global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_no
     if ((long)seg_ptr[mid] + (long)node_cost * mid < target) lo = mid + 1;
     else hi = mid;
   }
-  wave_nodes[i] = i == n_waves ? n_nodes : lo;
+  wave_nodes[i] = (i == n_waves && RG_CONV_TAIL == 0) ? n_nodes : lo;
 }
 
 template <bool EMIT>
