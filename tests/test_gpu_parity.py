@@ -1011,9 +1011,13 @@ def test_fused_conv_wave_schedule(cuda_device, dtype):
         assert wn is not None and wn.numel() == g.CONV_WAVES + 1
         w = wn.cpu().numpy().astype(np.int64)
         seg = g.seg_ptr.cpu().numpy().astype(np.int64)
-        assert w[0] == 0 and w[-1] == N and np.all(np.diff(w) >= 0)
+        # w[-1]: the end of the static ranges -- N, or the start of the dynamic tail the
+        # waves take in NB-node blocks once their ranges are done (RG_CONV_TAIL % of the cost)
+        assert w[0] == 0 and w[-1] <= N and np.all(np.diff(w) >= 0)
         cost = seg[w] + 4 * w
-        share = (seg[N] + 4 * N) / g.CONV_WAVES
+        total = seg[N] + 4 * N
+        assert cost[-1] >= 0.7 * total - 1
+        share = cost[-1] / g.CONV_WAVES
         node_max = int(np.max(np.diff(seg))) + 4
         assert np.all(np.diff(cost) <= share + node_max + 1)
         gen = torch.Generator(device='cpu').manual_seed(3)
