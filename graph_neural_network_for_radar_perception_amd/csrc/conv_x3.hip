@@ -10,19 +10,22 @@
 // Six 32-cycle bf16 MFMAs replace eight 64-cycle f32 MFMAs per 16-deep k-step (2.7x the
 // matrix rate of v_mfma_f32_32x32x2_f32, conv_f32.hip).
 //
-// One layer = ONE launch (rg_conv_layer_x3):
-//  * work block = 32 destination nodes and their incoming edges (destination-major CSR);
-//    workgroups are persistent and take blocks from one counter per XCD over that XCD's
-//    contiguous eighth of the nodes; the last workgroup out re-zeroes the counters;
+// One layer = an edge launch and a node launch (rg_conv_layer_x3; RG_CX3_NODE_KERNEL = 0 runs
+// the node phase at each block's end inside the edge launch instead):
+//  * work block = 32 destination nodes and their incoming edges (destination-major CSR; with
+//    the block table, 8-node blocks for the launch tail); workgroups are persistent and take
+//    blocks from one counter per XCD over that XCD's share, stealing from the other XCDs'
+//    tails once theirs is empty; the last workgroup out re-zeroes the counters;
 //  * per 32-edge tile a wave computes
 //        h = act(norm(P[dst] + Q[src] + W_e e))     P | Q = the per-node projections of
 //                                                   msg0's x_i / x_j columns (+ b1)
 //        m = act(norm(W_2 h + b2))                   (h stays in registers: layer 2's B)
 //    then the segmented sum: the message tile is transposed through a wave-private LDS
 //    tile (lane = feature) and summed IN EDGE ORDER into a running sum that starts anew
-//    at each change of destination (wave-uniform), the reference scatter_add_ order; a
-//    finished destination's sum is stored as one 256-B row to the aggregate scratch;
-//  * after the block's last tile: update MLP on cat(x, agg) (agg read back from L2),
+//    at each change of destination (wave-uniform), the reference scatter_add_ order --
+//    branch-free, one add and one select per edge; a finished destination's sum is stored
+//    as one 256-B row to the aggregate scratch;
+//  * node launch (node_x3_kernel): update MLP on cat(x, agg) (agg read back from L2),
 //    norm + act + residual -> x_out, and -- when the next layer is also this kernel --
 //    the NEXT layer's projections P' | Q' = W'_pq x_out (+ [b1'; 0]) from the same
 //    registers, so x_out is never re-read for them.
