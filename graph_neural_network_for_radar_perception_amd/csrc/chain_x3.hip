@@ -678,6 +678,10 @@ static bool match(const Key& k, int mode, int k0, int sp, std::initializer_list<
                         // two waves per SIMD: 1.2 KB of spills per lane, not run)
 #endif
 
+#ifndef RG_X3_HEAD_FT
+#define RG_X3_HEAD_FT 512  // the task-head chains (768 = 3 waves per SIMD: node heads -4 %, the
+                           // small chains slower, the step flat -- kept at 2)
+#endif
 #ifndef RG_X3_PAIR_FT
 #define RG_X3_PAIR_FT 768  // link pair chain: 12 waves, 3 per SIMD (133 VGPRs; 238.7 -> 233.2 us, M)
 #endif
@@ -700,7 +704,7 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   // node encoder 6 -> 256 -> 128 -> 64
   RG_X3C2(IN_SMALL, 6, 0b110, 0b111, 07 | (03 << 3), RG_X3_ENC_RT, EFT, 256, 128, 64)
   // task heads: 3-block stem + FFN_TaskSpecificHead (ffn + bare Linear -> 7 / 2, padded)
-  constexpr int HFT = RG_X3_HEAD_RT == 1 ? 512 : 256;
+  constexpr int HFT = RG_X3_HEAD_RT == 1 ? RG_X3_HEAD_FT : 256;
   RG_X3C2(IN_DENSE, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
   RG_X3C2(IN_PAIR, 64, 0b1111, 0b1111, ALL, RG_X3_HEAD_RT, HFT, 64, 64, 64, 64, 32)
   // the same link chain from per-node pre-projections (layer 0's planes are not staged), and
@@ -708,12 +712,12 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   // the bare layer alone (no stem)
   RG_X3C2(IN_PAIRPRE, 64, 0b1111, 0b1111, ALL & ~07, RG_X3_HEAD_RT, RG_X3_PAIR_FT ? RG_X3_PAIR_FT : HFT,
           64, 64, 64, 64, 32)
-  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, 512, 64, 64)
-  RG_X3C2(IN_DENSE, 64, 0, 0, ALL, 1, 512, 64)
+  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, RG_X3_HEAD_FT, 64, 64)
+  RG_X3C2(IN_DENSE, 64, 0, 0, ALL, 1, RG_X3_HEAD_FT, 64)
   // link edge_formation stem (1 block), object-class stem (3 blocks), object head
-  RG_X3C2(IN_DENSE, 64, 0b1, 0b1, ALL, 1, 512, 64)
-  RG_X3C2(IN_DENSE, 64, 0b111, 0b111, ALL, 1, 512, 64, 64, 64)
-  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, 512, 64, 32)
+  RG_X3C2(IN_DENSE, 64, 0b1, 0b1, ALL, 1, RG_X3_HEAD_FT, 64)
+  RG_X3C2(IN_DENSE, 64, 0b111, 0b111, ALL, 1, 512, 64, 64, 64)  // (176 B of spills at 768)
+  RG_X3C2(IN_DENSE, 64, 0b01, 0b01, ALL, 1, RG_X3_HEAD_FT, 64, 32)
 #undef RG_X3C2
 #undef RG_X3C
   return RG_ERR_UNSUPPORTED;
