@@ -110,6 +110,12 @@ def parse():
                    help='time every launch with its own HIP event pair (adds ~10 us of stream '
                         'gap per pair to the timed steps)')
     p.add_argument('--seed', type=int, default=synthetic.SEED0)
+    p.add_argument('--save-outputs', default=None, metavar='DIR',
+                   help='inference configs: every rank writes the four outputs of its first '
+                        '--save-frames frames of the last timed step (and their seeds) to '
+                        'DIR/rank<r>.npz, for a parity check against the oracle outside the '
+                        'bench (tests/test_distributed.py)')
+    p.add_argument('--save-frames', type=int, default=2)
     p.add_argument('--streams', type=int, default=None,
                    help='inference configs: batches in flight -- 2 builds step i\'s graph on a '
                         'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
@@ -177,7 +183,10 @@ def setup_dist(expect_world=None):
     if world > 1:
         backend = os.environ.get('RG_BENCH_BACKEND') or ('nccl' if torch.cuda.is_available()
                                                           else 'gloo')
-        dist.init_process_group(backend)
+        # rank 0 times the CPU baseline after the timed region while the others wait in a
+        # barrier: the timeout covers its worst case (--cpu-frames of a dense frame) with room
+        import datetime
+        dist.init_process_group(backend, timeout=datetime.timedelta(minutes=60))
     return world, rank, local
 
 
@@ -794,6 +803,31 @@ def workload_name(args) -> str:
             'node/edge features + encoders + message passing + 4 heads')
 
 
+def save_rank_outputs(args, rank, seeds, gb, out):
+    """This rank's outputs of its first args.save_frames frames (the last timed step):
+    node_cls / node_reg rows, the link pairs (global node ids) whose source lies in those
+    frames with their logits, and the frames' cluster logits -- plus the frame seeds, so a
+    checker can rebuild the same frames and run the oracle on them (the bench itself never
+    touches oracle/ outside its CPU-baseline leg)."""
+    F = min(args.save_frames, args.frames)
+    N = args.nodes
+    ncl = len(synthetic.cluster_lists(N))
+    U = int(gb.graph.n_pairs_dev.item())
+    ps = gb.graph.pair_src[:U].cpu().numpy()
+    pd = gb.graph.pair_dst[:U].cpu().numpy()
+    sel = ps < F * N
+    os.makedirs(args.save_outputs, exist_ok=True)
+    np.savez(os.path.join(args.save_outputs, f'rank{rank}.npz'),
+             seeds=np.asarray(seeds[:F]), nodes=N, k=args.k, eps2=args.eps2,
+             layers=args.layers, dtype=args.dtype,
+             node_cls=out.node_cls[:F * N].float().cpu().numpy(),
+             node_reg=out.node_reg[:F * N].float().cpu().numpy(),
+             pair_src=ps[sel], pair_dst=pd[sel],
+             link_cls=out.link_cls[:U].float().cpu().numpy()[sel],
+             obj_cls=out.obj_cls[:F * ncl].float().cpu().numpy())
+    log(f'rank {rank}: outputs of {F} frame(s) saved to {args.save_outputs}')
+
+
 def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     """Warm up, then time args.steps full steps (barrier + synchronize on both sides,
     max over ranks), then the forward alone; per-kernel HIP-event durations and the
@@ -839,6 +873,8 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         elapsed = max_over_ranks(time.perf_counter() - t0, world)
         if args.streams > 1:
             pipe = stepper.pipes[(stepper.i - 1) % stepper.depth]
+        if args.save_outputs:
+            save_rank_outputs(args, rank, seeds, gb, out)
         durs = event_durations(events)
         if 'conv_stack' in durs:  # per-layer launch time = span / layers
             durs['conv_fused'] = [ms / args.layers for ms in durs.pop('conv_stack')]

@@ -91,5 +91,37 @@ def build_variant(name: str, defines, only=None) -> str:
     return out
 
 
+SAN_FLAGS = ['-Xarch_host', '-fsanitize=address', '-Xarch_host', '-fsanitize=undefined',
+             '-Xarch_host', '-fno-sanitize-recover=undefined', '-Xarch_host',
+             '-fno-omit-frame-pointer']
+
+
+def build_sanitized_driver(driver: str) -> str:
+    """The library's HOST code under AddressSanitizer + UndefinedBehaviorSanitizer, linked
+    with a C++ driver into an executable at lib/asan/<driver name> (device code is compiled
+    as usual: every -fsanitize= sits behind -Xarch_host, and the link line keeps the GPU side
+    unsanitised with -fno-gpu-sanitize).  Run by tests/test_native_lib.py on the CPU; objects
+    are rebuilt only when a source or header is newer."""
+    adir = os.path.join(LIBDIR, 'asan')
+    os.makedirs(adir, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, SAN_FLAGS + ['-O1'], adir), srcs))
+    exe = os.path.join(adir, os.path.splitext(os.path.basename(driver))[0])
+    if _stale(exe, objs + [driver] + _headers()):
+        dobj = exe + '.o'
+        steps = [[HIPCC, '-std=c++17', '-O1', '-g', '-fPIC', '-fsanitize=address,undefined',
+                  '-fno-omit-frame-pointer', '-I', os.path.join(REPO, 'include'), '-c', driver,
+                  '-o', dobj],
+                 [HIPCC, f'--offload-arch={ARCH}', '-fsanitize=address,undefined',
+                  '-fno-gpu-sanitize', '-o', exe, dobj] + objs]
+        for cmd in steps:
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f'sanitized build failed: {" ".join(cmd[:4])}...\n'
+                                   f'{r.stdout}\n{r.stderr[-4000:]}')
+    return exe
+
+
 if __name__ == '__main__':
     build_library(verbose=True)

@@ -1358,7 +1358,14 @@ def run_conv_block(blk, node_features, edge_features, edge_index, dtype='fp32',
     xa = torch.empty((N, d_extra + cp.c_msg), dtype=torch.float32, device=dev)
     if d_extra:
         xa[:, :d_extra].copy_(extra_features)   # (plumbing: the columns ahead of agg)
-    segment_reduce(msg, g.seg_ptr, N, cp.aggr, xa[:, d_extra:])
+    if d_extra % 4 == 0:
+        segment_reduce(msg, g.seg_ptr, N, cp.aggr, xa[:, d_extra:])
+    else:
+        # the reduction writes 16-B row pieces: with a width that is not a multiple of 4 the
+        # aggregate columns of xa are unaligned -- reduce into an aligned buffer, then place it
+        agg = torch.empty((N, cp.c_msg), dtype=torch.float32, device=dev)
+        segment_reduce(msg, g.seg_ptr, N, cp.aggr, agg)
+        xa[:, d_extra:].copy_(agg)   # (plumbing)
     if cp.res is not None:
         ident = torch.empty((N, cp.c_out), dtype=torch.float32, device=dev)
         cp.res(N, ident, x, x.shape[1])

@@ -627,11 +627,11 @@ def make_extra_features_fixture():
     the flag concatenate (x, extra, agg) before their update MLP, gnn_blocks.py:69-72, 107):
     the reference's own module, seeded init, on a reference-built kNN graph with random node,
     edge and extra features.  A second case adds a residual projection (48 -> 64 channels)
-    and mean aggregation."""
+    and mean aggregation, a third an extra width of 3."""
     from modules.neural_net.gnn.gnn_blocks import graph_convolution
     from modules.compute_features.graph_features import compute_adjacency_information
 
-    def case(name, n, in_c, stems, aggr, flags, seed):
+    def case(name, n, in_c, stems, aggr, flags, seed, d_extra=16):
         frame = synthetic.make_frame(n, 9100 + seed)
         adj = compute_adjacency_information(frame, 25.0, 10)
         ei = torch.from_numpy(np.asarray(adj['adj_list']).astype(np.int64))
@@ -639,22 +639,25 @@ def make_extra_features_fixture():
         m = graph_convolution(in_node_channels=in_c, in_edge_channels=64, stem_channels=stems,
                               msg_mlp_hidden_dim=128, activation='leakyrelu', aggregation=aggr,
                               norm_layer='channel_normalization', num_groups=None,
-                              append_extra_features=flags, in_extra_feature_dim=16)
+                              append_extra_features=flags, in_extra_feature_dim=d_extra)
         g = torch.Generator().manual_seed(seed + 1)
         x = torch.randn(n, in_c, generator=g)
         e = torch.randn(ei.shape[1], 64, generator=g)
-        extra = torch.randn(n, 16, generator=g)
+        extra = torch.randn(n, d_extra, generator=g)
         with torch.no_grad():
             out = m(x, e, ei, extra)
         data = {'w/' + k: v.detach().numpy() for k, v in m.state_dict().items()}
         data.update(x=x.numpy(), e=e.numpy(), edge_index=ei.numpy(), extra=extra.numpy(),
                     out=out.numpy(), in_c=np.int64(in_c), stems=np.asarray(stems, np.int64),
-                    flags=np.asarray(flags, np.int64), aggregation=np.asarray(aggr))
+                    flags=np.asarray(flags, np.int64), aggregation=np.asarray(aggr),
+                    d_extra=np.int64(d_extra))
         np.savez_compressed(os.path.join(HERE, name + '.npz'), **data)
         print('wrote', name, out.shape)
 
     case('conv_extra_N300', 300, 64, [64, 64, 64], 'add', [True, False, True], 31)
     case('conv_extra_proj_N200', 200, 48, [64, 64], 'mean', [False, True], 32)
+    # an extra width that is not a multiple of 4 (unaligned aggregate columns)
+    case('conv_extra_odd_N150', 150, 64, [64, 64], 'add', [True, True], 33, d_extra=3)
 
 
 def main():

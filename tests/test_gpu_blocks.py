@@ -131,13 +131,13 @@ def test_dense_pairs_match_torch_nonzero_triu(cuda_device, n):
     np.testing.assert_array_equal(pd[:U].cpu().numpy(), di.numpy())
 
 
-@pytest.mark.parametrize('name', ['conv_extra_N300', 'conv_extra_proj_N200'])
+@pytest.mark.parametrize('name', ['conv_extra_N300', 'conv_extra_proj_N200', 'conv_extra_odd_N150'])
 def test_graph_convolution_extra_features_matches_reference(cuda_device, name):
-    """graph_convolution(append_extra_features=..., in_extra_feature_dim=16) (gnn_blocks.py:
+    """graph_convolution(append_extra_features=..., in_extra_feature_dim=16 / 3) (gnn_blocks.py:
     116-164): the flagged blocks update on cat(x, extra, agg) (:69-72, 107) -- the reference
     module's own output (tests/golden/conv_extra_*.npz: [True, False, True] over three 64-wide
-    blocks with 'add'; [False, True] with a 48 -> 64 residual projection and 'mean') at the fp32
-    tolerance; a flagged block called without extra features raises like the reference."""
+    blocks with 'add'; [False, True] with a 48 -> 64 residual projection and 'mean'; an extra
+    width of 3, whose aggregate columns are unaligned) at the fp32 tolerance; a flagged block called without extra features raises like the reference."""
     from graph_neural_network_for_radar_perception_amd.gnn_blocks import graph_convolution
     dev = cuda_device
     d = golden(name)
@@ -146,7 +146,7 @@ def test_graph_convolution_extra_features_matches_reference(cuda_device, name):
                           activation='leakyrelu', aggregation=str(d['aggregation']),
                           norm_layer='channel_normalization', num_groups=None,
                           append_extra_features=[bool(f) for f in d['flags']],
-                          in_extra_feature_dim=16)
+                          in_extra_feature_dim=int(d['d_extra']))
     m.load_state_dict({k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith('w/')})
     m = m.to(dev).eval().requires_grad_(False)
     x = torch.from_numpy(d['x']).to(dev)

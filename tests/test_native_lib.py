@@ -77,3 +77,23 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(nat, 'LIB_PATH', str(tmp_path / 'nope.so'))
     with pytest.raises(nat.NativeLibraryError):
         nat.lib()
+
+
+@pytest.mark.timeout(1200)
+def test_abi_host_code_under_asan_ubsan():
+    """The C ABI's host code -- argument checks, workspace-size arithmetic at the BASELINE
+    configurations' sizes and past them, the null / negative / short-workspace /
+    unsupported-shape paths -- compiled with AddressSanitizer + UndefinedBehaviorSanitizer
+    (host side only) and driven by tests/abi_sanitize_main.cpp; any sanitizer report or failed
+    check fails the run.  CPU only: no path it takes reaches a kernel launch."""
+    import os
+    import subprocess
+    from graph_neural_network_for_radar_perception_amd import build
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = build.build_sanitized_driver(os.path.join(here, 'abi_sanitize_main.cpp'))
+    env = dict(os.environ, ASAN_OPTIONS='abort_on_error=1:detect_leaks=0',
+               UBSAN_OPTIONS='print_stacktrace=1:halt_on_error=1', HIP_VISIBLE_DEVICES='')
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    out = r.stdout + r.stderr
+    assert 'AddressSanitizer' not in out and 'runtime error' not in out, out[-4000:]
+    assert r.returncode == 0, out[-4000:]

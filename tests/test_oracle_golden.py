@@ -254,7 +254,7 @@ def test_max_aggregation_training_oracle_matches_reference():
         np.testing.assert_allclose(g.numpy(), d['g1/' + k], rtol=1e-5, atol=1e-7, err_msg=k)
 
 
-@pytest.mark.parametrize('name', ['conv_extra_N300', 'conv_extra_proj_N200'])
+@pytest.mark.parametrize('name', ['conv_extra_N300', 'conv_extra_proj_N200', 'conv_extra_odd_N150'])
 def test_extra_features_conv_oracle_matches_reference(name):
     """graph_convolution with append_extra_features (gnn_blocks.py:116-164; the flagged blocks
     update on cat(x, extra, agg), :69-72, 107): the oracle restatement against the reference
