@@ -27,7 +27,7 @@ FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-Wall',
 # beside MFMAs costs far more than two scalar ops, MI355X_MICROARCH.md "price of one
 # filler"); measured 3.5 % faster per conv layer than the packed build
 FILE_FLAGS = {'conv_fused.hip': ['-DRG_NO_PK', '-fno-slp-vectorize'],
-              'conv_x3.hip': ['-fno-slp-vectorize']}
+              'conv_x3.hip': ['-fno-slp-vectorize', '-mllvm', '-amdgpu-mfma-vgpr-form']}
 
 
 def _headers():

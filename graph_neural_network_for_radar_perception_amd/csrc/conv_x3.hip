@@ -31,6 +31,10 @@
 // The first layer's projections come from rg_conv_proj_x3.
 #include <type_traits>
 
+#ifndef RG_X3_SPLIT
+#define RG_X3_SPLIT 4  // builtin conversions in the splits: no inline-asm s_nop pads (M: the
+                       // one-wave edge launch 0.620 -> 0.606 ms per layer; the chains keep 0)
+#endif
 #include "x3_common.h"
 
 namespace rg {
@@ -469,17 +473,520 @@ __global__ __launch_bounds__(PFT) void proj_x3_kernel(const float* x, int ldx, i
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The edge launch with one wave per SIMD, software-pipelined (conv_x3_sp_kernel).
+//
+// conv_x3_kernel runs the whole tile program per wave, two waves per SIMD: its MFMA phases
+// (layers 1 and 2) and its vector / memory phases (gathers, e split, norms, segmented sum)
+// run back to back in each wave and overlap only as far as the SIMD's two waves happen to
+// interleave (MFMA busy ~57 %).  Here each SIMD holds ONE wave that keeps the matrix pipe fed
+// by itself: while tile i's MFMAs issue, the same instruction stream carries
+//   * during layer 1 of tile i: the split of tile i's e rows (its B operand), norm 2 of tile
+//     i - 1, its message transposes and the in-order running sums, and the loads of tile
+//     i + 1 (Q rows by LDS-DMA, e rows, the indices of tile i + 2, layer 2's bias);
+//   * between the layers: the flushes of tile i - 1's finished destinations, norm 1's
+//     statistics of tile i, the P rows of tile i + 1;
+//   * during layer 2 of tile i: its B operand (norm 1's scale + LeakyReLU + split), then
+//     tile i + 1's accumulator init P[dst] + Q[src].
+// Work: the destination-major CSR cut into one contiguous range of whole destinations per
+// wave with equal edge counts (rg_conv_x3_blocks / the workspace table; XCD-major ranks, so
+// an XCD's waves hold one contiguous node range), walked in 32-edge tiles that may span
+// destinations -- each destination's messages are still summed in CSR order by one wave.
+// Registers: the weight fragments are read from LDS into AGPRs (inline ds_read, the MFMA
+// takes its A operand from AGPRs), the rest stays in VGPRs; LDS = the W_e and W_2 planes
+// (96 KiB) + one 16 KiB buffer per wave that holds the next tile's Q rows (LDS-DMA) and,
+// between two uses, the message tile being transposed.
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+namespace sp {
+constexpr int FT = 256, NW = FT / 64;
+constexpr int PLE = plane_bytes(C, HID), PL2 = plane_bytes(HID, C);  // 16 KiB each
+constexpr int OFF_W2 = 3 * PLE;
+constexpr int OFF_BUF = OFF_W2 + 3 * PL2;
+constexpr int TS2 = 68;            // message transpose: row stride (floats)
+constexpr int BUF = 32 * TS2 * 4;  // per wave: one tile's messages while transposing
+constexpr int OFF_BIAS = OFF_BUF + NW * BUF;  // layer 2's bias, accumulator order
+constexpr int LDS = OFF_BIAS + C * 4;
+static_assert(LDS <= 160 * 1024, "conv_x3_sp LDS");
+constexpr int GMAX = 256;          // workgroups (one per CU)
+constexpr int WMAX = GMAX * NW;    // waves: the table holds WMAX + 1 node boundaries
+}  // namespace sp
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+// one weight fragment LDS -> AGPRs (the MFMA reads its A operand from there); completion is
+// not tracked by the compiler: wait_frags before use
+template <int OFF>
+__device__ __forceinline__ bf16x8_t dsa(uint32_t a) {
+  bf16x8_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=a"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+// every LDS read issued so far has landed; the fragments are tied to the wait so no MFMA
+// that reads them can be scheduled above it
+template <int N>
+__device__ __forceinline__ void wait_frags(bf16x8_t (&f)[N][3]);
+template <>
+__device__ __forceinline__ void wait_frags<4>(bf16x8_t (&f)[4][3]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+a"(f[0][0]), "+a"(f[0][1]), "+a"(f[0][2]), "+a"(f[1][0]), "+a"(f[1][1]),
+                 "+a"(f[1][2]), "+a"(f[2][0]), "+a"(f[2][1]), "+a"(f[2][2]), "+a"(f[3][0]),
+                 "+a"(f[3][1]), "+a"(f[3][2]));
+}
+template <>
+__device__ __forceinline__ void wait_frags<2>(bf16x8_t (&f)[2][3]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+a"(f[0][0]), "+a"(f[0][1]), "+a"(f[0][2]), "+a"(f[1][0]), "+a"(f[1][1]),
+                 "+a"(f[1][2]));
+}
+// layer 1's A fragments of k-step S (W_e FAST_IN x3: K = 64, four M-tiles)
+template <int S>
+__device__ __forceinline__ void lda1(uint32_t b, bf16x8_t (&f)[4][3]) {
+#define RG_SP_L1(M, P) f[M][P] = dsa<P * sp::PLE + (M * 4 + S) * 1024>(b)
+  RG_SP_L1(0, 0); RG_SP_L1(0, 1); RG_SP_L1(0, 2); RG_SP_L1(1, 0); RG_SP_L1(1, 1); RG_SP_L1(1, 2);
+  RG_SP_L1(2, 0); RG_SP_L1(2, 1); RG_SP_L1(2, 2); RG_SP_L1(3, 0); RG_SP_L1(3, 1); RG_SP_L1(3, 2);
+#undef RG_SP_L1
+}
+// layer 2's A fragments of k-step S (W_2 FAST_CHAIN x3: K = 128, two M-tiles); b = W_2's base
+template <int S>
+__device__ __forceinline__ void lda2(uint32_t b, bf16x8_t (&f)[2][3]) {
+#define RG_SP_L2(M, P) f[M][P] = dsa<P * sp::PL2 + (M * 8 + S) * 1024>(b)
+  RG_SP_L2(0, 0); RG_SP_L2(0, 1); RG_SP_L2(0, 2); RG_SP_L2(1, 0); RG_SP_L2(1, 1); RG_SP_L2(1, 2);
+#undef RG_SP_L2
+}
+// the six products of one k-step (weights of term <= 2, small terms first: layer_x3's order)
+// for M-tiles [0, MT); MMAJOR: tile by tile (its result complete early), else product-major
+template <int MT, bool MMAJOR>
+__device__ __forceinline__ void x3_step(f32x16 (&acc)[MT], const bf16x8_t (&A)[MT][3], const X3& b) {
+  if constexpr (MMAJOR) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      acc[m] = mf(A[m][2], b.p0, acc[m]);
+      acc[m] = mf(A[m][1], b.p1, acc[m]);
+      acc[m] = mf(A[m][0], b.p2, acc[m]);
+      acc[m] = mf(A[m][1], b.p0, acc[m]);
+      acc[m] = mf(A[m][0], b.p1, acc[m]);
+      acc[m] = mf(A[m][0], b.p0, acc[m]);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][2], b.p0, acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][1], b.p1, acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][0], b.p2, acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][1], b.p0, acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][0], b.p1, acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][0], b.p0, acc[m]);
+  }
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16 B per lane straight into AGPRs (a load the compiler does not track: wait_q retires it)
+__device__ __forceinline__ void ld_agpr(const float* p, f32x4& d) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(d) : "v"(p) : "memory");
+}
+// every vector-memory access issued so far has completed; the AGPR rows are tied to the wait
+// so that no copy of them can be scheduled above it
+__device__ __forceinline__ void wait_q(f32x4 (&q)[16]) {
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+a"(q[0]), "+a"(q[1]), "+a"(q[2]), "+a"(q[3]), "+a"(q[4]), "+a"(q[5]),
+                 "+a"(q[6]), "+a"(q[7]), "+a"(q[8]), "+a"(q[9]), "+a"(q[10]), "+a"(q[11]),
+                 "+a"(q[12]), "+a"(q[13]), "+a"(q[14]), "+a"(q[15])
+               :
+               : "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// `n` groups of (one MFMA, v VALU) in program order: the scheduler fills them from the
+// region's MFMAs and independent vector work (the region's other instructions float)
+template <int N, int V>
+__device__ __forceinline__ void interleave() {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+  }
+}
+__device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// sum of squares of one 16-value accumulator tile into eight partial sums (row_inv_std's
+// order: partial q & 7)
+__device__ __forceinline__ void sq_partial(const f32x16& t, float (&u)[8], bool first) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u[i] = first ? t[i] * t[i] : fmaf(t[i], t[i], u[i]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u[i] = fmaf(t[i + 8], t[i + 8], u[i]);
+}
+// channel_normalization's scale from the partial sums of a CENTRED layer of N features
+// (row_inv_std<MT, true>): 0.505 sd / (std + eps), the LeakyReLU prescale folded in
+template <int N>
+__device__ __forceinline__ Pend finish_norm(const float (&u)[8], float mu, float sd) {
+  const float ss = add_xor32(((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7])));
+  const float inv =
+      __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
+  return Pend{X3_LEAKY_PRE * (sd * inv), X3_LEAKY_PRE * mu};
+}
+
+#ifndef RG_CX3_SP_STAMP
+#define RG_CX3_SP_STAMP 0  // diagnostic build: per-region s_memtime sums (rg_debug_sp_stamps)
+#endif
+#if RG_CX3_SP_STAMP
+__device__ unsigned long long g_sp_stamp[16];
+#define SP_STAMP(i)                                               \
+  do {                                                            \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();   \
+    st_acc[i] += _n - st_last;                                    \
+    st_last = _n;                                                 \
+  } while (0)
+#else
+#define SP_STAMP(i) do {} while (0)
+#endif
+
+template <bool CENT>
+__global__ __launch_bounds__(sp::FT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
+  static_assert(CENT, "the one-wave edge launch takes centred layers");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  stage_lds<sp::FT>(lds, a.w[0], 3 * sp::PLE);
+  stage_lds<sp::FT>(lds + sp::OFF_W2, a.w[1], 3 * sp::PL2);
+  stage_lds<sp::FT>(lds + sp::OFF_BIAS, a.w[1] + 3 * sp::PL2, C * 4);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int xcd = blockIdx.x % NXCD, slot = blockIdx.x / NXCD;
+  const int rank = (xcd * ((int)gridDim.x / NXCD) + slot) * sp::NW + wave;
+  const int na = __builtin_amdgcn_readfirstlane(wtab[rank]);
+  const int nb = __builtin_amdgcn_readfirstlane(wtab[rank + 1]);
+  const int E0 = __builtin_amdgcn_readfirstlane(a.seg_ptr[na]);
+  const int E1 = __builtin_amdgcn_readfirstlane(a.seg_ptr[nb]);
+  const int T = (E1 - E0 + 31) >> 5;
+  if (T <= 0) return;
+  const float mu0 = *a.mu[0], sd0 = *a.sd[0], mu1 = *a.mu[1], sd1 = *a.sd[1];
+  const float* bias2 = (const float*)(lds + sp::OFF_BIAS);  // layer 2's bias
+  const uint32_t lb = lds_addr(lds);
+  const uint32_t aw = lb + lane * 16;  // + the fragment's immediate offset
+  const uint32_t aw2 = aw + sp::OFF_W2;
+  char* bufp = lds + sp::OFF_BUF + wave * sp::BUF;
+  float* Tm = (float*)bufp;  // [32][TS2] message rows while transposing
+
+  // ---- per-tile inputs
+  auto edge_of = [&](int t) { return min(E0 + 32 * t + r, E1 - 1); };
+  // Q[src] rows of a tile in accumulator order (features 32 m + 8 g + 4 h + t at [4 m + g])
+  // into AGPRs: a plain load's issue costs a fraction of an LDS-DMA piece's (~70 cycles
+  // each, measured: 16 per tile were ~1 150 cycles), and the buffer stays free
+  auto load_q = [&](int s, f32x4 (&q)[16]) {
+    const float* g = a.pq + (size_t)s * PQW + HID + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ld_agpr(g + 8 * i, q[i]);
+  };
+  auto load_p = [&](int d, f32x4 (&p)[16]) {  // P[dst] in accumulator order
+    const float* g = a.pq + (size_t)d * PQW + 4 * h;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = *(const f32x4*)(g + 8 * i);
+  };
+  auto load_e = [&](int q, f32x4 (&ev)[8]) {  // e[edge] in k order
+    const float* g = a.e + (size_t)q * a.lde + 8 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ev[2 * i] = *(const f32x4*)(g + 16 * i);
+      ev[2 * i + 1] = *(const f32x4*)(g + 16 * i + 4);
+    }
+  };
+  f32x4 qv[16];  // the next tile's Q rows (AGPRs)
+  auto init_tile = [&](const f32x4 (&p)[16], f32x16& acc, int m) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[4 * g + t] = p[4 * m + g][t] + qv[4 * m + g][t];
+  };
+  // destination-change mask of a tile (bit j: edge j starts a new destination; edges past
+  // the range's end carry no bit); dlast = the destination of the previous tile's last edge
+  auto tile_mask = [&](int t, int d, int dlast) {
+    const int dprev = __builtin_amdgcn_mov_dpp(d, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const int nv = min(32, E1 - E0 - 32 * t);  // (<= 0 past the range: no bits)
+    const uint32_t live = nv >= 32 ? 0xffffffffu : nv <= 0 ? 0u : ((1u << nv) - 1u);
+    return (uint32_t)__ballot(r == 0 ? d != dlast : d != dprev) & live;
+  };
+  // message rows of a tile (lane = edge) -> the buffer; its columns (lane = feature) back
+  auto write_msgs = [&](const f32x16 (&m2)[2]) {
+    float* row = Tm + r * sp::TS2 + 4 * h;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(f32x4*)(row + 32 * m + 8 * g) =
+            (f32x4){m2[m][4 * g], m2[m][4 * g + 1], m2[m][4 * g + 2], m2[m][4 * g + 3]};
+  };
+  // in-order running sums (lane = feature): rv[j] = the sum after edge j, a set mask bit
+  // restarting it (the reference scatter_add_ order of a destination-major CSR)
+  auto scan = [&](const float (&cv)[32], uint32_t mask, float run_in, f32x32& rv) {
+    float prev = run_in;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      // prev * keep + v: exactly v at a set bit (keep = 0), prev + v otherwise (keep = 1)
+      const float keep = ((mask >> j) & 1u) ? 0.f : 1.f;
+      prev = fmaf(prev, keep, cv[j]);
+      rv[j] = prev;
+    }
+  };
+  // the finished destinations of a tile: at a set bit j the sum before edge j belongs to the
+  // destination that ended there (crow); then crow = edge j's destination
+  auto flush = [&](uint32_t mask, const f32x32& rv, float run_in, int d, int& crow) {
+    for (uint32_t m = mask; m; m &= m - 1) {
+      const int j = __builtin_ctz(m);
+      a.agg[(size_t)crow * C + lane] = j == 0 ? run_in : rv[j - 1];
+      crow = __builtin_amdgcn_readlane(d, j);
+    }
+  };
+  // the first four of them without branches (a kNN tile has ~2.5): an unused slot stores to
+  // the wave's own dummy row; returns the bits left for flush()
+  const int dummy = a.n_nodes + 1 + rank;
+  auto flush4 = [&](uint32_t mask, const f32x32& rv, float run_in, int d, int& crow) {
+    uint32_t m = mask;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool any = m != 0;
+      const int j = __builtin_amdgcn_readfirstlane(any ? __builtin_ctz(m) : 0);
+      const int jm = __builtin_amdgcn_readfirstlane(j > 0 ? j - 1 : 0);
+      const float v = rv[jm];
+      const int row = __builtin_amdgcn_readfirstlane(any ? crow : dummy);
+      a.agg[(size_t)row * C + lane] = j == 0 ? run_in : v;
+      const int nc = __builtin_amdgcn_readlane(d, j);
+      crow = any ? nc : crow;
+      m &= m - 1;
+    }
+    return m;
+  };
+
+  // ---- prologue: tile 0's inputs, tile 1's indices
+  int q_n = edge_of(0);
+  const int d0 = a.dst[q_n], s0 = a.src[q_n];
+  f32x4 pn[16], en[8];
+  load_q(s0, qv);
+  load_p(d0, pn);
+  load_e(q_n, en);
+  int q_nn = edge_of(1);
+  int d_nn = a.dst[q_nn], s_nn = a.src[q_nn];
+  wait_q(qv);
+  f32x16 acc1[4];
+  init_tile(pn, acc1[0], 0);
+  X3 b1 = split8(en[0], en[1]);
+  uint32_t mask_c = tile_mask(0, d0, a.n_nodes);
+  int d_c = d0;
+  // the previous tile's state (none yet: no mask bits, zero messages)
+  f32x16 acc2p[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc2p[m][i] = 0.f;
+  uint32_t mask_p = 0;
+  int d_p = 0;
+  float run = 0.f;       // lane = feature: the running sum carried into the previous tile
+  f32x32 rv;             // the previous tile's running sums
+  int crow = a.n_nodes;  // the destination row of `run` (a dummy row before the first)
+  bf16x8_t A1[2][4][3], A2[2][2][3];
+  lda1<0>(aw, A1[0]);
+#if RG_CX3_SP_STAMP
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
+
+  for (int t = 0; t < T; ++t) {
+    SP_STAMP(0);  // (loop back edge)
+    f32x4 ev[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ev[i] = en[i];
+    float cv[32];
+    // ======== A0: layer 1 k-step 0 (M-tile by M-tile, so tiles 1-3 take their P + Q init
+    //          beside it); the split of k-step 1
+    wait_frags<4>(A1[0]);
+    lda1<1>(aw, A1[1]);
+    X3 b1n = split8(ev[2], ev[3]);
+#pragma unroll
+    for (int m = 1; m < 4; ++m) init_tile(pn, acc1[m], m);
+    x3_step<4, true>(acc1, A1[0], b1);
+    interleave<24, 4>();
+    fence();
+    SP_STAMP(7);  // A0
+    // ======== A1: k-step 1; the split of k-step 2; tile t - 1: norm 2's statistics
+    wait_frags<4>(A1[1]);
+    lda1<2>(aw, A1[0]);
+    b1 = split8(ev[4], ev[5]);
+    float u2[8];
+    sq_partial(acc2p[0], u2, true);
+    sq_partial(acc2p[1], u2, false);
+    const Pend pn2 = finish_norm<C>(u2, mu1, sd1);
+    x3_step<4, false>(acc1, A1[1], b1n);
+    interleave<24, 4>();
+    fence();
+    SP_STAMP(8);  // A1
+    // ======== A2: k-step 2; the split of k-step 3; tile t - 1: norm 2's scale + LeakyReLU,
+    //          its message rows to the buffer and its columns back
+    wait_frags<4>(A1[0]);
+    lda1<3>(aw, A1[1]);
+    b1n = split8(ev[6], ev[7]);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float y = fmaf(acc2p[m][i], pn2.ga, pn2.gb);
+        acc2p[m][i] = fmaf(fabsf(y), X3_LEAKY_C, y);
+      }
+    write_msgs(acc2p);
+    wait_lgkm0();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cv[j] = Tm[j * sp::TS2 + lane];
+    x3_step<4, false>(acc1, A1[0], b1);
+    interleave<24, 5>();
+    fence();
+    SP_STAMP(9);  // A2
+    // ======== A3: k-step 3 (M-tile by M-tile: norm 1's partial sums start on tiles 0-2);
+    //          tile t - 1's running sums; tile t + 1's loads (Q rows into AGPRs, e rows,
+    //          P rows, the indices of tile t + 2)
+    wait_frags<4>(A1[1]);  // (also: the transposed reads have landed)
+    lda2<0>(aw2, A2[0]);
+    load_q(s_nn, qv);
+    load_e(q_nn, en);
+    load_p(d_nn, pn);
+    const int q_3 = edge_of(t + 2);
+    const int d_3 = a.dst[q_3], s_3 = a.src[q_3];
+    const float run_in = run;
+    scan(cv, mask_p, run_in, rv);
+    const uint32_t mask_rest = flush4(mask_p, rv, run_in, d_p, crow);
+    x3_step<4, true>(acc1, A1[1], b1n);
+    float u1[8];
+    sq_partial(acc1[0], u1, true);
+    sq_partial(acc1[1], u1, false);
+    sq_partial(acc1[2], u1, false);
+    interleave<24, 5>();
+    fence();
+    SP_STAMP(1);  // region A
+    // ======== B: tile t - 1's finished destinations; norm 1's scale; layer 2's first B
+    flush(mask_rest, rv, run_in, d_p, crow);
+    run = rv[31];
+    sq_partial(acc1[3], u1, false);
+    const Pend pn1 = finish_norm<HID>(u1, mu0, sd0);
+    X3 b2 = split_acc_pend<1>(acc1[0], 0, pn1);
+    f32x16 acc2[2] = {ld_bias_frag(bias2, 0, h), ld_bias_frag(bias2, 1, h)};
+    fence();
+    SP_STAMP(2);  // region B
+    // ======== C: layer 2 of tile t, its B operand one k-step ahead; in the last k-step tile
+    //          t + 1's first B operand and first accumulator tile
+    X3 b2n;
+#define RG_SP_C(S, BUFI, NEXT)                                         \
+    wait_frags<2>(A2[BUFI]);                                           \
+    lda2<S + 1>(aw2, A2[BUFI ^ 1]);                                     \
+    NEXT = split_acc_pend<1>(acc1[(S + 1) >> 1], (S + 1) & 1, pn1);    \
+    x3_step<2, false>(acc2, A2[BUFI], S % 2 ? b2n : b2);               \
+    interleave<12, 5>();                                               \
+    fence();
+    RG_SP_C(0, 0, b2n)
+    RG_SP_C(1, 1, b2)
+    RG_SP_C(2, 0, b2n)
+    RG_SP_C(3, 1, b2)
+    RG_SP_C(4, 0, b2n)
+    RG_SP_C(5, 1, b2)
+    RG_SP_C(6, 0, b2n)
+#undef RG_SP_C
+    SP_STAMP(3);  // C0 - C6
+    wait_frags<2>(A2[1]);
+    lda1<0>(aw, A1[0]);  // the next tile's first layer-1 fragments
+    wait_q(qv);          // every load issued in A3 has landed
+    SP_STAMP(4);  // the vm wait
+    b1 = split8(en[0], en[1]);
+    x3_step<2, false>(acc2, A2[1], b2n);
+    init_tile(pn, acc1[0], 0);
+    const uint32_t mask_n = tile_mask(t + 1, d_nn, __builtin_amdgcn_readlane(d_c, 31));
+    interleave<12, 5>();
+    fence();
+    SP_STAMP(5);  // C7
+    // rotate the pipeline
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc2p[m] = acc2[m];
+    mask_p = mask_c;
+    d_p = d_c;
+    mask_c = mask_n;
+    d_c = d_nn;
+    q_nn = q_3;
+    d_nn = d_3;
+    s_nn = s_3;
+  }
+  // ---- epilogue: the last tile's norm 2, running sums and flushes; the final sum goes to
+  //      the destination of the range's last edge (edges past it carry no bit and are not
+  //      counted: the sum after edge nv - 1)
+  wait_lgkm0();
+  norm_leaky<2, CENT>(acc2p, mu1, sd1);
+  write_msgs(acc2p);
+  wait_lgkm0();
+  float cv[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) cv[j] = Tm[j * sp::TS2 + lane];
+  const float run_in = run;
+  scan(cv, mask_p, run_in, rv);
+  flush(mask_p, rv, run_in, d_p, crow);
+  const int nv = E1 - E0 - 32 * (T - 1);
+  a.agg[(size_t)crow * C + lane] = rv[nv - 1];
+#if RG_CX3_SP_STAMP
+  SP_STAMP(6);  // epilogue
+  if (lane == 0) {
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_sp_stamp[i], st_acc[i]);
+    atomicAdd(&g_sp_stamp[12], (unsigned long long)T);
+    atomicAdd(&g_sp_stamp[13], 1ull);
+  }
+#endif
+}
+
+// Node boundaries of the edge launch's waves: rank w takes the destinations
+// [wtab[w], wtab[w + 1]), the first node whose CSR start reaches E w / W (equal edge counts;
+// every destination whole in one wave)
+__global__ __launch_bounds__(256) void conv_x3_waves_kernel(const int* __restrict__ seg_ptr,
+                                                            int n, int W, int* __restrict__ wtab) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w > W) return;
+  const long E = seg_ptr[n];
+  const long target = E * w / W;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (seg_ptr[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  wtab[w] = w == W ? n : lo;
+}
+
 }  // namespace convx3
 }  // namespace rg
 
 using namespace rg;
 using namespace rg::convx3;
 
+#ifndef RG_CX3_SP
+#define RG_CX3_SP 1  // the one-wave-per-SIMD software-pipelined edge launch (conv_x3_sp_kernel)
+#endif
+static size_t x3_agg_bytes(int n_nodes) {
+  // the aggregate rows, one dummy row (the flush target before a block's / wave's first
+  // destination) and one per wave of the one-wave launch (its unused branch-free flushes)
+  return (size_t)((n_nodes > 0 ? n_nodes : 1) + 1 + sp::WMAX) * C * sizeof(float);
+}
+// workgroups of the one-wave-per-SIMD edge launch (a multiple of the 8 XCDs, one per CU at most)
+static int x3_sp_groups(int n_nodes) {
+  const int g = (n_nodes / 128 + NXCD - 1) / NXCD * NXCD;
+  return g < NXCD ? NXCD : g > sp::GMAX ? sp::GMAX : g;
+}
+#if RG_CX3_SP_STAMP
+// diagnostic builds only (not in radar_gnn.h): read and clear the region sums
+extern "C" int rg_debug_sp_stamps(unsigned long long* out_host) {
+  RG_CHECK_HIP(hipMemcpyFromSymbol(out_host, HIP_SYMBOL(g_sp_stamp), sizeof(g_sp_stamp)));
+  static const unsigned long long z[16] = {0};
+  RG_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sp_stamp), z, sizeof(z)));
+  return RG_OK;
+}
+#endif
 extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
   static_assert((CTR_STRIDE * NXCD + 1) * sizeof(int) <= CTR_BYTES, "counter area");
-  // the aggregate rows and one dummy row (the edge launch's flush target before a block's
-  // first destination)
-  return CTR_BYTES + (size_t)((n_nodes > 0 ? n_nodes : 1) + 1) * C * sizeof(float);
+  // + the wave table when the layer has to build it (no rg_conv_x3_blocks table)
+  return CTR_BYTES + x3_agg_bytes(n_nodes) + (size_t)(sp::WMAX + 1) * sizeof(int);
 }
 
 extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes,
@@ -580,11 +1087,20 @@ static int x3_total_blocks(int n) {
 }
 
 extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
+  if (RG_CX3_SP) return (size_t)(sp::WMAX + 1) * sizeof(int);
   return (size_t)(TBL_HDR + 2 * x3_total_blocks(n_nodes > 0 ? n_nodes : 1)) * sizeof(int);
+}
+
+static int x3_wave_table(const int* seg_ptr, int n_nodes, int* table, void* stream) {
+  const int W = x3_sp_groups(n_nodes) * sp::NW;
+  conv_x3_waves_kernel<<<(W + 256) / 256, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, W, table);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
 }
 
 extern "C" int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream) {
   RG_REQUIRE(seg_ptr && table && n_nodes >= 1, RG_ERR_ARG, "rg_conv_x3_blocks: bad argument");
+  if (RG_CX3_SP) return x3_wave_table(seg_ptr, n_nodes, table, stream);
   conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table, 0);
   RG_LAUNCH_CHECK();
   return RG_OK;
@@ -673,6 +1189,24 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   a.n_blocks = table ? x3_total_blocks(n_nodes) : (n_nodes + NBLK - 1) / NBLK;
   a.table = table;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
+  // (the one-wave launch addresses Q rows with 32-bit byte offsets: < 4 Mi nodes)
+  if (RG_CX3_SP && cent && n_nodes < (1 << 22)) {
+    const int* wtab = table;
+    if (!wtab) {  // no per-graph table: build the wave ranges into the workspace
+      int* ws_tab = (int*)((char*)workspace + CTR_BYTES + x3_agg_bytes(n_nodes));
+      const int rc = x3_wave_table(seg_ptr, n_nodes, ws_tab, stream);
+      if (rc != RG_OK) return rc;
+      wtab = ws_tab;
+    }
+    auto edge = conv_x3_sp_kernel<true>;
+    RG_ENSURE_LDS(edge, sp::LDS);
+    edge<<<x3_sp_groups(n_nodes), sp::FT, sp::LDS, (hipStream_t)stream>>>(a, wtab);
+    RG_LAUNCH_CHECK();
+  } else {
+  if (RG_CX3_SP) {  // the table holds the wave ranges: plain NBLK-node runs here
+    a.table = nullptr;
+    a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
+  }
   int blocks = 256;  // one workgroup per CU (LDS); a multiple of the 8 XCDs
   const int need = (a.n_blocks + NW - 1) / NW;
   if (blocks > need) blocks = (need + NXCD - 1) / NXCD * NXCD;
@@ -682,6 +1216,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   RG_ENSURE_LDS(edge, LDS_BYTES);
   edge<<<blocks, FT, LDS_BYTES, (hipStream_t)stream>>>(a);
   RG_LAUNCH_CHECK_ZERO(a.counters, CTR_BYTES, stream);
+  }
   auto node = cent ? node_x3_kernel<true> : node_x3_kernel<false>;
   RG_ENSURE_LDS(node, NODE_LDS);
   const int tiles = (n_nodes + 31) / 32;

@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 #define RG_X3_PKNORM 0  // 1: row statistics and scale in v_pk_fma_f32 (M: no gain, conv 1% slower)
 #endif
 #ifndef RG_X3_SPLIT
-#define RG_X3_SPLIT 0  // split8: 0 pair by pair, 3 stage by stage (no s_nop pads; measured flat),
+#define RG_X3_SPLIT 0  // split8: 0 pair by pair, 4 builtin conversions (no asm: no s_nop pads; conv_x3.hip), 3 stage by stage (no s_nop pads; measured flat),
                        // 1 f32x2 residues (compiler), 2 forced v_pk_add_f32 residues
 #endif
 
@@ -78,13 +78,38 @@ __device__ __forceinline__ f32x2 sub_pk(f32x2 a, f32x2 b) {
   return r;
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// v_cvt_pk_bf16_f32 through the generic conversion: the compiler takes each element's value
+// from the packed word (no inline asm: an asm result costs an s_nop before its first reader,
+// the hazard recognizer having to assume a transcendental)
+__device__ __forceinline__ uint32_t cvt_pk_bf16_c(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2_t));
+}
+__device__ __forceinline__ f32x2 unpk_c(uint32_t u) {
+  return __builtin_convertvector(__builtin_bit_cast(bf16x2_t, u), f32x2);
+}
+
 // 8 consecutive k values of one row -> the three exact bf16 terms (the residues of a
 // pair in one v_pk_add_f32)
 __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
   const f32x2 v[4] = {{lo.x, lo.y}, {lo.z, lo.w}, {hi.x, hi.y}, {hi.z, hi.w}};
   u32x4 w0, w1, w2;
+#if RG_X3_SPLIT == 4
+  // builtin conversions, scalar residues: 3 conversions + 4 unpacks + 4 subtractions per pair
 #pragma unroll
-  for (int i = 0; i < 4 && RG_X3_SPLIT != 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t u0 = cvt_pk_bf16_c(v[i].x, v[i].y);
+    const f32x2 u0f = unpk_c(u0);
+    const float rx = v[i].x - u0f.x, ry = v[i].y - u0f.y;
+    const uint32_t u1 = cvt_pk_bf16_c(rx, ry);
+    const f32x2 u1f = unpk_c(u1);
+    w0[i] = u0;
+    w1[i] = u1;
+    w2[i] = cvt_pk_bf16_c(rx - u1f.x, ry - u1f.y);
+  }
+#endif
+#pragma unroll
+  for (int i = 0; i < 4 && RG_X3_SPLIT != 3 && RG_X3_SPLIT != 4; ++i) {
     const uint32_t u0 = cvt_pk_bf16(v[i].x, v[i].y);
 #if RG_X3_SPLIT == 2
     const f32x2 r = sub_pk(v[i], unpk(u0));
@@ -101,7 +126,7 @@ __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
     const f32x2 u1f = unpk(u1);
     const f32x2 t = {r.x - u1f.x, r.y - u1f.y};
 #endif
-#if RG_X3_SPLIT != 3
+#if RG_X3_SPLIT != 3 && RG_X3_SPLIT != 4
     w0[i] = u0;
     w1[i] = u1;
     w2[i] = cvt_pk_bf16(t.x, t.y);

@@ -215,11 +215,13 @@ def test_f32_fused_conv_matches_unfused_and_oracle(cuda_device, aggr, arith):
 
 
 @pytest.mark.parametrize('sizes', [[700, 1, 33, 1500, 64], [3], [3000] * 8])
-def test_x3_conv_block_table_bit_identical(cuda_device, sizes):
-    """rg_conv_x3_blocks: per XCD share [N x / 8, N (x + 1) / 8) the (first, end) pairs
-    cover every node once in 32-node blocks then 8-node tail blocks, each share ordered by
-    edge tiles (largest first); rg_conv_layer_x3_blocks over it is bit-identical to the
-    plain 32-node schedule (each destination sums its edges in CSR order in one block)."""
+def test_x3_conv_wave_table_bit_identical(cuda_device, sizes):
+    """rg_conv_x3_blocks: the edge launch's per-wave node ranges -- wave w (XCD-major rank)
+    owns the destinations [wtab[w], wtab[w + 1]) whose CSR starts reach E w / W: ranges
+    ascending and covering every node once, edge counts within one destination's degree of
+    an equal share.  rg_conv_layer_x3_blocks over it is bit-identical to rg_conv_layer_x3,
+    which builds the same table in its workspace (every destination's messages summed in CSR
+    order by one wave)."""
     from graph_neural_network_for_radar_perception_amd import engine
     from graph_neural_network_for_radar_perception_amd import _native as nat
     from graph_neural_network_for_radar_perception_amd.config import default_config
@@ -234,27 +236,16 @@ def test_x3_conv_block_table_bit_identical(cuda_device, sizes):
     N = batch.n_nodes
     tbl = g.conv_x3_blocks()
     assert tbl is not None and tbl.numel() * 4 >= nat.lib().rg_conv_x3_blocks_bytes(N)
-    t = tbl.cpu().numpy()
-    off = t[:9]
-    nbk = int(off[8])
-    assert off[0] == 0 and np.all(np.diff(off) >= 0)
-    assert 16 + 2 * nbk <= t.size
-    pairs = t[16:16 + 2 * nbk].reshape(nbk, 2)
+    G = min(max((N // 128 + 7) // 8 * 8, 8), 256)      # workgroups (x3_sp_groups)
+    W = 4 * G
+    wt = tbl[:W + 1].cpu().numpy()
     seg = g.seg_ptr.cpu().numpy()
-    tiles = (seg[pairs[:, 1]] - seg[pairs[:, 0]] + 31) // 32
-    for x in range(8):
-        a0, b0 = N * x // 8, N * (x + 1) // 8
-        p = pairs[off[x]:off[x + 1]]
-        assert np.all(np.diff(np.minimum(tiles[off[x]:off[x + 1]], 63)) <= 0)
-        if b0 == a0:
-            assert p.shape[0] == 0
-            continue
-        o = p[np.argsort(p[:, 0])]
-        assert o[0, 0] == a0 and o[-1, 1] == b0 and np.all(o[1:, 0] == o[:-1, 1])
-        w = o[:, 1] - o[:, 0]
-        assert np.all((w >= 1) & (w <= 32))
-        k = int(np.sum(w == 32))                            # 32-node runs, then the tail
-        assert np.all(w[:k] == 32) and np.all(w[k:] <= 8)
+    E = int(seg[N])
+    assert wt[0] == 0 and wt[W] == N and np.all(np.diff(wt) >= 0)
+    per = seg[wt[1:]] - seg[wt[:-1]]
+    assert per.sum() == E
+    maxdeg = int(np.diff(seg).max())
+    assert np.all(per <= -(-E // W) + maxdeg), (per.max(), E / W, maxdeg)
     gen = torch.Generator(device='cpu').manual_seed(4)
     x = (torch.randn(N, 64, generator=gen) * 1.5).to(dev)
     e = (torch.randn(gb.capacity, 64, generator=gen) * 1.5).to(dev)
