@@ -503,7 +503,9 @@ constexpr int PLE = plane_bytes(C, HID), PL2 = plane_bytes(HID, C);  // 16 KiB e
 constexpr int OFF_W2 = 3 * PLE;
 constexpr int OFF_BUF = OFF_W2 + 3 * PL2;
 constexpr int TS2 = 68;            // message transpose: row stride (floats)
-constexpr int BUF = 32 * TS2 * 4;  // per wave: one tile's messages while transposing
+constexpr int TBUF = 32 * TS2 * 4;  // per wave: one tile's messages while transposing
+constexpr int RING = 8;             // per wave: P rows of the last RING destinations (slot = node & 7)
+constexpr int BUF = TBUF + RING * HID * 4;
 constexpr int OFF_BIAS = OFF_BUF + NW * BUF;  // layer 2's bias, accumulator order
 constexpr int LDS = OFF_BIAS + C * 4;
 static_assert(LDS <= 160 * 1024, "conv_x3_sp LDS");
@@ -521,21 +523,25 @@ __device__ __forceinline__ bf16x8_t dsa(uint32_t a) {
   return r;
 }
 // every LDS read issued so far has landed; the fragments are tied to the wait so no MFMA
-// that reads them can be scheduled above it
+// that reads them can be scheduled above it.  The wait itself is the s_waitcnt builtin, not
+// inline asm: the compiler's own counter model then knows every older LDS read is done (its
+// later waits for its own reads never stall on the untracked fragment reads issued after)
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0)
 template <int N>
 __device__ __forceinline__ void wait_frags(bf16x8_t (&f)[N][3]);
 template <>
 __device__ __forceinline__ void wait_frags<4>(bf16x8_t (&f)[4][3]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
+  wait_lgkm0();
+  asm volatile(""
                : "+a"(f[0][0]), "+a"(f[0][1]), "+a"(f[0][2]), "+a"(f[1][0]), "+a"(f[1][1]),
                  "+a"(f[1][2]), "+a"(f[2][0]), "+a"(f[2][1]), "+a"(f[2][2]), "+a"(f[3][0]),
                  "+a"(f[3][1]), "+a"(f[3][2]));
 }
 template <>
 __device__ __forceinline__ void wait_frags<2>(bf16x8_t (&f)[2][3]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+a"(f[0][0]), "+a"(f[0][1]), "+a"(f[0][2]), "+a"(f[1][0]), "+a"(f[1][1]),
-                 "+a"(f[1][2]));
+  wait_lgkm0();
+  asm volatile("" : "+a"(f[0][0]), "+a"(f[0][1]), "+a"(f[0][2]), "+a"(f[1][0]), "+a"(f[1][1]),
+                    "+a"(f[1][2]));
 }
 // layer 1's A fragments of k-step S (W_e FAST_IN x3: K = 64, four M-tiles)
 template <int S>
@@ -581,31 +587,41 @@ __device__ __forceinline__ void x3_step(f32x16 (&acc)[MT], const bf16x8_t (&A)[M
     for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][0], b.p0, acc[m]);
   }
 }
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// 16 B per lane straight into AGPRs (a load the compiler does not track: wait_q retires it)
-__device__ __forceinline__ void ld_agpr(const float* p, f32x4& d) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(d) : "v"(p) : "memory");
+// one product of a k-step (x3_step's order: P = 0 .. 5) on every M-tile
+template <int P, int MT>
+__device__ __forceinline__ void x3_prod(f32x16 (&acc)[MT], const bf16x8_t (&A)[MT][3], const X3& b) {
+  constexpr int ia = P == 0 ? 2 : (P == 1 || P == 3) ? 1 : 0;
+  constexpr int ib = (P == 0 || P == 3 || P == 5) ? 0 : (P == 1 || P == 4) ? 1 : 2;
+  const bf16x8_t bb = ib == 0 ? b.p0 : ib == 1 ? b.p1 : b.p2;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = mf(A[m][ia], bb, acc[m]);
 }
-// every vector-memory access issued so far has completed; the AGPR rows are tied to the wait
-// so that no copy of them can be scheduled above it
-__device__ __forceinline__ void wait_q(f32x4 (&q)[16]) {
-  asm volatile("s_waitcnt vmcnt(0)"
-               : "+a"(q[0]), "+a"(q[1]), "+a"(q[2]), "+a"(q[3]), "+a"(q[4]), "+a"(q[5]),
-                 "+a"(q[6]), "+a"(q[7]), "+a"(q[8]), "+a"(q[9]), "+a"(q[10]), "+a"(q[11]),
-                 "+a"(q[12]), "+a"(q[13]), "+a"(q[14]), "+a"(q[15])
-               :
-               : "memory");
+// the six products of a k-step on M-tile M alone (the same order per accumulator)
+template <int M, int MT>
+__device__ __forceinline__ void x3_tile(f32x16 (&acc)[MT], const bf16x8_t (&A)[MT][3], const X3& b) {
+  acc[M] = mf(A[M][2], b.p0, acc[M]);
+  acc[M] = mf(A[M][1], b.p1, acc[M]);
+  acc[M] = mf(A[M][0], b.p2, acc[M]);
+  acc[M] = mf(A[M][1], b.p0, acc[M]);
+  acc[M] = mf(A[M][0], b.p1, acc[M]);
+  acc[M] = mf(A[M][0], b.p0, acc[M]);
 }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
+// keeps a value computed where it stands (IR sinking would otherwise move work whose only
+// use lies past a branch into the block after it, out of the sub-chunk it was placed in)
+template <int N>
+__device__ __forceinline__ void pin(float (&u)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(u[i]));
+}
 // `n` groups of (one MFMA, v VALU) in program order: the scheduler fills them from the
 // region's MFMAs and independent vector work (the region's other instructions float)
-template <int N, int V>
+template <int N, int V, int M = 0>
 __device__ __forceinline__ void interleave() {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+    if (M > 0 && i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x010, M, 0);  // VMEM
   }
 }
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
@@ -673,14 +689,13 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   // ---- per-tile inputs
   auto edge_of = [&](int t) { return min(E0 + 32 * t + r, E1 - 1); };
   // Q[src] rows of a tile in accumulator order (features 32 m + 8 g + 4 h + t at [4 m + g])
-  // into AGPRs: a plain load's issue costs a fraction of an LDS-DMA piece's (~70 cycles
-  // each, measured: 16 per tile were ~1 150 cycles), and the buffer stays free
-  auto load_q = [&](int s, f32x4 (&q)[16]) {
+  auto load_q_part = [&](int s, f32x4 (&q)[16], int i0, int i1) {
     const float* g = a.pq + (size_t)s * PQW + HID + 4 * h;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ld_agpr(g + 8 * i, q[i]);
+    for (int i = i0; i < i1; ++i) q[i] = *(const f32x4*)(g + 8 * i);
   };
-  auto load_p = [&](int d, f32x4 (&p)[16]) {  // P[dst] in accumulator order
+  auto load_q = [&](int s, f32x4 (&q)[16]) { load_q_part(s, q, 0, 16); };
+  auto load_p = [&](int d, f32x4 (&p)[16]) {  // P[dst] in accumulator order (slow path)
     const float* g = a.pq + (size_t)d * PQW + 4 * h;
 #pragma unroll
     for (int i = 0; i < 16; ++i) p[i] = *(const f32x4*)(g + 8 * i);
@@ -693,12 +708,42 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
       ev[2 * i + 1] = *(const f32x4*)(g + 16 * i + 4);
     }
   };
-  f32x4 qv[16];  // the next tile's Q rows (AGPRs)
-  auto init_tile = [&](const f32x4 (&p)[16], f32x16& acc, int m) {
+  // P rows through a ring of the wave's last RING destinations in LDS (slot = node & 7): a
+  // tile's P[dst] is one row per DESTINATION (~4 per kNN tile), gathered per edge it was 16
+  // vector loads per tile.  Before tile t + 1 the rows dl - 3 .. dl of its last destination
+  // dl are loaded (two 16-B pieces per lane, half a wave per row); with at most four new
+  // destinations per tile the ring then holds every row the tile needs, and the rows it
+  // overwrites (dl - 11 .. dl - 8) belong to no tile still to be initialised.  A tile with
+  // more new destinations takes its P rows straight from memory (fastf = 0).
+  float* ring = (float*)(bufp + sp::TBUF);
+  auto ring_row = [&](int dl, int k) {  // the row loaded by piece k for a last destination dl
+    return min(max(dl - 3 + 2 * k + h, 0), a.n_nodes - 1);
+  };
+  auto ring_load = [&](int dl, f32x4 (&rp)[2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rp[k] = *(const f32x4*)(a.pq + (size_t)ring_row(dl, k) * PQW + 4 * r);
+  };
+  auto ring_store = [&](int dl, const f32x4 (&rp)[2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) *(f32x4*)(ring + (ring_row(dl, k) & (sp::RING - 1)) * HID + 4 * r) = rp[k];
+  };
+  // tile accumulator init: Q + P (P from the ring, scaled by fastf: 0 when the slow path has
+  // already added it into q)
+  auto ring_p = [&](int d, int m, f32x4 (&p)[4]) {  // M-tile m of P[d] from the ring
+    const float* rp = ring + (d & (sp::RING - 1)) * HID + 4 * h + 32 * m;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) p[g] = *(const f32x4*)(rp + 8 * g);
+  };
+  auto init_from = [&](const f32x4 (&p)[4], float fastf, const f32x4 (&q)[16], f32x16& acc, int m) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[4 * g + t] = p[4 * m + g][t] + qv[4 * m + g][t];
+      for (int t = 0; t < 4; ++t) acc[4 * g + t] = fmaf(p[g][t], fastf, q[4 * m + g][t]);
+  };
+  auto init_tile = [&](int d, float fastf, const f32x4 (&q)[16], f32x16& acc, int m) {
+    f32x4 p[4];
+    ring_p(d, m, p);
+    init_from(p, fastf, q, acc, m);
   };
   // destination-change mask of a tile (bit j: edge j starts a new destination; edges past
   // the range's end carry no bit); dlast = the destination of the previous tile's last edge
@@ -709,25 +754,38 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     return (uint32_t)__ballot(r == 0 ? d != dlast : d != dprev) & live;
   };
   // message rows of a tile (lane = edge) -> the buffer; its columns (lane = feature) back
-  auto write_msgs = [&](const f32x16 (&m2)[2]) {
+  auto write_msg = [&](const f32x16& m2, int m) {
     float* row = Tm + r * sp::TS2 + 4 * h;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *(f32x4*)(row + 32 * m + 8 * g) =
-            (f32x4){m2[m][4 * g], m2[m][4 * g + 1], m2[m][4 * g + 2], m2[m][4 * g + 3]};
+    for (int g = 0; g < 4; ++g)
+      *(f32x4*)(row + 32 * m + 8 * g) = (f32x4){m2[4 * g], m2[4 * g + 1], m2[4 * g + 2], m2[4 * g + 3]};
+  };
+  auto write_msgs = [&](const f32x16 (&m2)[2]) {
+    write_msg(m2[0], 0);
+    write_msg(m2[1], 1);
   };
   // in-order running sums (lane = feature): rv[j] = the sum after edge j, a set mask bit
-  // restarting it (the reference scatter_add_ order of a destination-major CSR)
-  auto scan = [&](const float (&cv)[32], uint32_t mask, float run_in, f32x32& rv) {
-    float prev = run_in;
+  // restarting it (the reference scatter_add_ order of a destination-major CSR); edges
+  // [j0, j1) continuing from prev
+  auto scan_part = [&](int j0, int j1, const float (&cv)[32], uint32_t mask, float& prev, f32x32& rv) {
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = j0; j < j1; ++j) {
       // prev * keep + v: exactly v at a set bit (keep = 0), prev + v otherwise (keep = 1)
       const float keep = ((mask >> j) & 1u) ? 0.f : 1.f;
       prev = fmaf(prev, keep, cv[j]);
       rv[j] = prev;
+    }
+  };
+  auto scan = [&](const float (&cv)[32], uint32_t mask, float run_in, f32x32& rv) {
+    float prev = run_in;
+    scan_part(0, 32, cv, mask, prev, rv);
+  };
+  // the norm 2 scale + LeakyReLU of one message tile
+  auto norm2_apply = [&](f32x16& m2, Pend pn, int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const float y = fmaf(m2[i], pn.ga, pn.gb);
+      m2[i] = fmaf(fabsf(y), X3_LEAKY_C, y);
     }
   };
   // the finished destinations of a tile: at a set bit j the sum before edge j belongs to the
@@ -739,38 +797,46 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
       crow = __builtin_amdgcn_readlane(d, j);
     }
   };
-  // the first four of them without branches (a kNN tile has ~2.5): an unused slot stores to
-  // the wave's own dummy row; returns the bits left for flush()
+  // one of them without branches (the first four go through slots, a kNN tile has ~2.5): an
+  // unused slot stores to the wave's own dummy row; clears the bit it took from m
   const int dummy = a.n_nodes + 1 + rank;
-  auto flush4 = [&](uint32_t mask, const f32x32& rv, float run_in, int d, int& crow) {
-    uint32_t m = mask;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool any = m != 0;
-      const int j = __builtin_amdgcn_readfirstlane(any ? __builtin_ctz(m) : 0);
-      const int jm = __builtin_amdgcn_readfirstlane(j > 0 ? j - 1 : 0);
-      const float v = rv[jm];
-      const int row = __builtin_amdgcn_readfirstlane(any ? crow : dummy);
-      a.agg[(size_t)row * C + lane] = j == 0 ? run_in : v;
-      const int nc = __builtin_amdgcn_readlane(d, j);
-      crow = any ? nc : crow;
-      m &= m - 1;
-    }
-    return m;
+  auto flush_slot = [&](uint32_t& m, const f32x32& rv, float run_in, int d, int& crow) {
+    const bool any = m != 0;
+    const int j = __builtin_amdgcn_readfirstlane(any ? __builtin_ctz(m) : 0);
+    const int jm = __builtin_amdgcn_readfirstlane(j > 0 ? j - 1 : 0);
+    const float v = rv[jm];
+    const int row = __builtin_amdgcn_readfirstlane(any ? crow : dummy);
+    a.agg[(size_t)row * C + lane] = j == 0 ? run_in : v;
+    const int nc = __builtin_amdgcn_readlane(d, j);
+    crow = any ? nc : crow;
+    m &= m - 1;
   };
 
-  // ---- prologue: tile 0's inputs, tile 1's indices
+  // ---- prologue: the ring zeroed (its stale slots are only ever multiplied by 0), tile
+  //      0's inputs (P straight from memory), tile 1's indices
+#pragma unroll
+  for (int k = 0; k < sp::RING * HID / 256; ++k) *(f32x4*)(ring + 256 * k + 4 * lane) = (f32x4){0.f, 0.f, 0.f, 0.f};
   int q_n = edge_of(0);
   const int d0 = a.dst[q_n], s0 = a.src[q_n];
-  f32x4 pn[16], en[8];
-  load_q(s0, qv);
-  load_p(d0, pn);
+  f32x4 qn[16], en[8], rp[2];
+  load_q(s0, qn);
   load_e(q_n, en);
+  const int dl0 = __builtin_amdgcn_readlane(d0, 31);
+  ring_load(dl0, rp);
+  {
+    f32x4 pg[16];
+    load_p(d0, pg);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) qn[i] += pg[i];
+  }
+  ring_store(dl0, rp);
   int q_nn = edge_of(1);
   int d_nn = a.dst[q_nn], s_nn = a.src[q_nn];
-  wait_q(qv);
+  float fastf = 0.f;  // tile 0's P is in qn
   f32x16 acc1[4];
-  init_tile(pn, acc1[0], 0);
+  init_tile(d0, fastf, qn, acc1[0], 0);
+  f32x4 pr[4];  // the ring rows of the next M-tile to initialise, read one sub-chunk ahead
+  ring_p(d0, 1, pr);
   X3 b1 = split8(en[0], en[1]);
   uint32_t mask_c = tile_mask(0, d0, a.n_nodes);
   int d_c = d0;
@@ -798,81 +864,152 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) ev[i] = en[i];
     float cv[32];
-    // ======== A0: layer 1 k-step 0 (M-tile by M-tile, so tiles 1-3 take their P + Q init
-    //          beside it); the split of k-step 1
+    // Region A = layer 1 of tile t, cut into sub-chunks of 4 - 8 MFMAs with the vector work
+    // each one carries placed beside it (a sched_barrier per sub-chunk: left to itself the
+    // scheduler bunches the MFMAs of a 24-MFMA region and leaves dependent runs -- the scan,
+    // the flushes, the transposes -- without any beside them)
+    // ======== A0: k-step 0 tile by tile; beside M-tile m the P + Q init of M-tile m + 1;
+    //          the split of k-step 1; norm 2's statistics of tile t - 1
     wait_frags<4>(A1[0]);
     lda1<1>(aw, A1[1]);
     X3 b1n = split8(ev[2], ev[3]);
-#pragma unroll
-    for (int m = 1; m < 4; ++m) init_tile(pn, acc1[m], m);
-    x3_step<4, true>(acc1, A1[0], b1);
-    interleave<24, 4>();
+    init_from(pr, fastf, qn, acc1[1], 1);
+    ring_p(d_c, 2, pr);
+    x3_tile<0>(acc1, A1[0], b1);
+    interleave<6, 5>();
+    fence();
+    float u2[8];
+    init_from(pr, fastf, qn, acc1[2], 2);
+    ring_p(d_c, 3, pr);
+    sq_partial(acc2p[0], u2, true);
+    x3_tile<1>(acc1, A1[0], b1);
+    interleave<6, 6>();
+    fence();
+    init_from(pr, fastf, qn, acc1[3], 3);
+    sq_partial(acc2p[1], u2, false);
+    x3_tile<2>(acc1, A1[0], b1);
+    interleave<6, 6>();
+    fence();
+    const Pend pn2 = finish_norm<C>(u2, mu1, sd1);
+    x3_tile<3>(acc1, A1[0], b1);
+    interleave<6, 4>();
     fence();
     SP_STAMP(7);  // A0
-    // ======== A1: k-step 1; the split of k-step 2; tile t - 1: norm 2's statistics
+    // ======== A1: k-step 1 product by product; the split of k-step 2; tile t - 1: norm 2's
+    //          scale + LeakyReLU, its message rows to the buffer and its columns back (one
+    //          wave's LDS operations complete in order: no wait between them)
     wait_frags<4>(A1[1]);
     lda1<2>(aw, A1[0]);
     b1 = split8(ev[4], ev[5]);
-    float u2[8];
-    sq_partial(acc2p[0], u2, true);
-    sq_partial(acc2p[1], u2, false);
-    const Pend pn2 = finish_norm<C>(u2, mu1, sd1);
-    x3_step<4, false>(acc1, A1[1], b1n);
-    interleave<24, 4>();
+    norm2_apply(acc2p[0], pn2, 0, 4);
+    x3_prod<0>(acc1, A1[1], b1n);
+    interleave<4, 5>();
+    fence();
+    norm2_apply(acc2p[0], pn2, 4, 12);
+    x3_prod<1>(acc1, A1[1], b1n);
+    interleave<4, 4>();
+    fence();
+    norm2_apply(acc2p[0], pn2, 12, 16);
+    write_msg(acc2p[0], 0);
+    x3_prod<2>(acc1, A1[1], b1n);
+    interleave<4, 4>();
+    fence();
+    norm2_apply(acc2p[1], pn2, 0, 8);
+    x3_prod<3>(acc1, A1[1], b1n);
+    interleave<4, 4>();
+    fence();
+    norm2_apply(acc2p[1], pn2, 8, 16);
+    x3_prod<4>(acc1, A1[1], b1n);
+    interleave<4, 4>();
+    fence();
+    write_msg(acc2p[1], 1);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cv[j] = Tm[j * sp::TS2 + lane];
+    x3_prod<5>(acc1, A1[1], b1n);
+    interleave<4, 2>();
     fence();
     SP_STAMP(8);  // A1
-    // ======== A2: k-step 2; the split of k-step 3; tile t - 1: norm 2's scale + LeakyReLU,
-    //          its message rows to the buffer and its columns back
+    // ======== A2: k-step 2 product by product; the split of k-step 3; tile t - 1's running
+    //          sums; tile t + 1's e rows
     wait_frags<4>(A1[0]);
     lda1<3>(aw, A1[1]);
     b1n = split8(ev[6], ev[7]);
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float y = fmaf(acc2p[m][i], pn2.ga, pn2.gb);
-        acc2p[m][i] = fmaf(fabsf(y), X3_LEAKY_C, y);
-      }
-    write_msgs(acc2p);
-    wait_lgkm0();
-#pragma unroll
-    for (int j = 0; j < 32; ++j) cv[j] = Tm[j * sp::TS2 + lane];
-    x3_step<4, false>(acc1, A1[0], b1);
-    interleave<24, 5>();
+    x3_prod<0>(acc1, A1[0], b1);
+    interleave<4, 3>();
+    fence();
+    const float run_in = run;
+    float prev = run_in;
+    scan_part(0, 8, cv, mask_p, prev, rv);
+    x3_prod<1>(acc1, A1[0], b1);
+    interleave<4, 2>();
+    fence();
+    scan_part(8, 16, cv, mask_p, prev, rv);
+    x3_prod<2>(acc1, A1[0], b1);
+    interleave<4, 2>();
+    fence();
+    scan_part(16, 24, cv, mask_p, prev, rv);
+    x3_prod<3>(acc1, A1[0], b1);
+    interleave<4, 2>();
+    fence();
+    scan_part(24, 32, cv, mask_p, prev, rv);
+    x3_prod<4>(acc1, A1[0], b1);
+    interleave<4, 2>();
+    fence();
+    load_e(q_nn, en);
+    x3_prod<5>(acc1, A1[0], b1);
+    interleave<4, 0, 2>();
     fence();
     SP_STAMP(9);  // A2
-    // ======== A3: k-step 3 (M-tile by M-tile: norm 1's partial sums start on tiles 0-2);
-    //          tile t - 1's running sums; tile t + 1's loads (Q rows into AGPRs, e rows,
-    //          P rows, the indices of tile t + 2)
-    wait_frags<4>(A1[1]);  // (also: the transposed reads have landed)
+    // ======== A3: k-step 3 tile by tile (norm 1's partial sums follow one tile behind);
+    //          tile t - 1's first four finished destinations, one per sub-chunk; tile t + 1's
+    //          Q rows and ring rows, the indices of tile t + 2 (a one-wave SIMD pays each
+    //          vector-memory instruction's issue in its own stream, so the loads are spread
+    //          over the sub-chunks)
+    wait_frags<4>(A1[1]);
     lda2<0>(aw2, A2[0]);
-    load_q(s_nn, qv);
-    load_e(q_nn, en);
-    load_p(d_nn, pn);
+    uint32_t mask_rest = mask_p;
+    const int dl_c = __builtin_amdgcn_readlane(d_c, 31);   // tile t's last destination
+    const int dl_n = __builtin_amdgcn_readlane(d_nn, 31);  // tile t + 1's
     const int q_3 = edge_of(t + 2);
     const int d_3 = a.dst[q_3], s_3 = a.src[q_3];
-    const float run_in = run;
-    scan(cv, mask_p, run_in, rv);
-    const uint32_t mask_rest = flush4(mask_p, rv, run_in, d_p, crow);
-    x3_step<4, true>(acc1, A1[1], b1n);
+    load_q_part(s_nn, qn, 0, 6);
+    flush_slot(mask_rest, rv, run_in, d_p, crow);
+    x3_tile<0>(acc1, A1[1], b1n);
+    interleave<6, 4, 2>();
+    fence();
     float u1[8];
+    load_q_part(s_nn, qn, 6, 12);
+    flush_slot(mask_rest, rv, run_in, d_p, crow);
     sq_partial(acc1[0], u1, true);
+    x3_tile<1>(acc1, A1[1], b1n);
+    interleave<6, 6, 2>();
+    fence();
+    load_q_part(s_nn, qn, 12, 16);
+    ring_load(dl_n, rp);
+    flush_slot(mask_rest, rv, run_in, d_p, crow);
     sq_partial(acc1[1], u1, false);
+    x3_tile<2>(acc1, A1[1], b1n);
+    interleave<6, 6, 2>();
+    fence();
+    flush_slot(mask_rest, rv, run_in, d_p, crow);
     sq_partial(acc1[2], u1, false);
-    interleave<24, 5>();
+    pin(u1);
+    x3_tile<3>(acc1, A1[1], b1n);
+    interleave<6, 6>();
     fence();
     SP_STAMP(1);  // region A
-    // ======== B: tile t - 1's finished destinations; norm 1's scale; layer 2's first B
+    // ======== B: tile t - 1's remaining finished destinations (a kNN tile has none); norm
+    //          1's scale; layer 2's bias
     flush(mask_rest, rv, run_in, d_p, crow);
     run = rv[31];
     sq_partial(acc1[3], u1, false);
     const Pend pn1 = finish_norm<HID>(u1, mu0, sd0);
-    X3 b2 = split_acc_pend<1>(acc1[0], 0, pn1);
     f32x16 acc2[2] = {ld_bias_frag(bias2, 0, h), ld_bias_frag(bias2, 1, h)};
     fence();
     SP_STAMP(2);  // region B
     // ======== C: layer 2 of tile t, its B operand one k-step ahead; in the last k-step tile
-    //          t + 1's first B operand and first accumulator tile
+    //          t + 1's ring rows, first B operand and first accumulator tile
+    X3 b2 = split_acc_pend<1>(acc1[0], 0, pn1);
     X3 b2n;
 #define RG_SP_C(S, BUFI, NEXT)                                         \
     wait_frags<2>(A2[BUFI]);                                           \
@@ -890,14 +1027,25 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     RG_SP_C(6, 0, b2n)
 #undef RG_SP_C
     SP_STAMP(3);  // C0 - C6
+    // the slow path: more than four new destinations in tile t + 1 (never on a kNN graph of
+    // degree >= 8): its P rows straight from memory, added into its Q rows
+    const bool fast = dl_n - dl_c <= 4;
+    if (!fast) {
+      f32x4 pg[16];
+      load_p(d_nn, pg);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) qn[i] += pg[i];
+    }
+    fastf = fast ? 1.f : 0.f;
+    SP_STAMP(4);  // the slow path
     wait_frags<2>(A2[1]);
     lda1<0>(aw, A1[0]);  // the next tile's first layer-1 fragments
-    wait_q(qv);          // every load issued in A3 has landed
-    SP_STAMP(4);  // the vm wait
+    ring_store(dl_n, rp);
     b1 = split8(en[0], en[1]);
     x3_step<2, false>(acc2, A2[1], b2n);
-    init_tile(pn, acc1[0], 0);
-    const uint32_t mask_n = tile_mask(t + 1, d_nn, __builtin_amdgcn_readlane(d_c, 31));
+    init_tile(d_nn, fastf, qn, acc1[0], 0);
+    ring_p(d_nn, 1, pr);
+    const uint32_t mask_n = tile_mask(t + 1, d_nn, dl_c);
     interleave<12, 5>();
     fence();
     SP_STAMP(5);  // C7
