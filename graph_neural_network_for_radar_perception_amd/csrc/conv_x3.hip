@@ -854,7 +854,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   bf16x8_t A1[2][4][3], A2[2][2][3];
   lda1<0>(aw, A1[0]);
 #if RG_CX3_SP_STAMP
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -977,6 +977,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     x3_tile<0>(acc1, A1[1], b1n);
     interleave<6, 4, 2>();
     fence();
+    SP_STAMP(10);  // A3.0
     float u1[8];
     load_q_part(s_nn, qn, 6, 12);
     flush_slot(mask_rest, rv, run_in, d_p, crow);
@@ -984,6 +985,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     x3_tile<1>(acc1, A1[1], b1n);
     interleave<6, 6, 2>();
     fence();
+    SP_STAMP(11);  // A3.1
     load_q_part(s_nn, qn, 12, 16);
     ring_load(dl_n, rp);
     flush_slot(mask_rest, rv, run_in, d_p, crow);
@@ -991,6 +993,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     x3_tile<2>(acc1, A1[1], b1n);
     interleave<6, 6, 2>();
     fence();
+    SP_STAMP(14);  // A3.2
     flush_slot(mask_rest, rv, run_in, d_p, crow);
     sq_partial(acc1[2], u1, false);
     pin(u1);
@@ -998,6 +1001,18 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     interleave<6, 6>();
     fence();
     SP_STAMP(1);  // region A
+    // the slow path: more than four new destinations in tile t + 1 (never on a kNN graph of
+    // degree >= 8): its P rows straight from memory, added into its Q rows
+    const bool fast = dl_n - dl_c <= 4;
+    if (!fast) {
+      asm volatile("");  // a real branch: the compiler would otherwise speculate the loads
+      f32x4 pg[16];
+      load_p(d_nn, pg);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) qn[i] += pg[i];
+    }
+    fastf = fast ? 1.f : 0.f;
+    SP_STAMP(4);  // the slow path
     // ======== B: tile t - 1's remaining finished destinations (a kNN tile has none); norm
     //          1's scale; layer 2's bias
     flush(mask_rest, rv, run_in, d_p, crow);
@@ -1007,46 +1022,37 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     f32x16 acc2[2] = {ld_bias_frag(bias2, 0, h), ld_bias_frag(bias2, 1, h)};
     fence();
     SP_STAMP(2);  // region B
-    // ======== C: layer 2 of tile t, its B operand one k-step ahead; in the last k-step tile
-    //          t + 1's ring rows, first B operand and first accumulator tile
+    // ======== C: layer 2 of tile t, its B operand one k-step ahead; beside k-step 3 tile
+    //          t + 1's ring rows go in (tile t's accumulators were all initialised in A0),
+    //          beside k-step 6 its first accumulator tile (acc1[0] is dead after k-step 1's
+    //          split; its ring rows read one k-step ahead), beside k-step 7 its first B
+    //          operand
     X3 b2 = split_acc_pend<1>(acc1[0], 0, pn1);
     X3 b2n;
-#define RG_SP_C(S, BUFI, NEXT)                                         \
+#define RG_SP_C(S, BUFI, NEXT, EXTRA)                                  \
     wait_frags<2>(A2[BUFI]);                                           \
     lda2<S + 1>(aw2, A2[BUFI ^ 1]);                                     \
     NEXT = split_acc_pend<1>(acc1[(S + 1) >> 1], (S + 1) & 1, pn1);    \
+    EXTRA;                                                             \
     x3_step<2, false>(acc2, A2[BUFI], S % 2 ? b2n : b2);               \
     interleave<12, 5>();                                               \
     fence();
-    RG_SP_C(0, 0, b2n)
-    RG_SP_C(1, 1, b2)
-    RG_SP_C(2, 0, b2n)
-    RG_SP_C(3, 1, b2)
-    RG_SP_C(4, 0, b2n)
-    RG_SP_C(5, 1, b2)
-    RG_SP_C(6, 0, b2n)
+    RG_SP_C(0, 0, b2n, (void)0)
+    RG_SP_C(1, 1, b2, (void)0)
+    RG_SP_C(2, 0, b2n, (void)0)
+    RG_SP_C(3, 1, b2, ring_store(dl_n, rp))
+    RG_SP_C(4, 0, b2n, (void)0)
+    RG_SP_C(5, 1, b2, ring_p(d_nn, 0, pr))
+    RG_SP_C(6, 0, b2n, init_from(pr, fastf, qn, acc1[0], 0))
 #undef RG_SP_C
     SP_STAMP(3);  // C0 - C6
-    // the slow path: more than four new destinations in tile t + 1 (never on a kNN graph of
-    // degree >= 8): its P rows straight from memory, added into its Q rows
-    const bool fast = dl_n - dl_c <= 4;
-    if (!fast) {
-      f32x4 pg[16];
-      load_p(d_nn, pg);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) qn[i] += pg[i];
-    }
-    fastf = fast ? 1.f : 0.f;
-    SP_STAMP(4);  // the slow path
     wait_frags<2>(A2[1]);
     lda1<0>(aw, A1[0]);  // the next tile's first layer-1 fragments
-    ring_store(dl_n, rp);
     b1 = split8(en[0], en[1]);
     x3_step<2, false>(acc2, A2[1], b2n);
-    init_tile(d_nn, fastf, qn, acc1[0], 0);
     ring_p(d_nn, 1, pr);
     const uint32_t mask_n = tile_mask(t + 1, d_nn, dl_c);
-    interleave<12, 5>();
+    interleave<12, 2>();
     fence();
     SP_STAMP(5);  // C7
     // rotate the pipeline
@@ -1078,7 +1084,8 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #if RG_CX3_SP_STAMP
   SP_STAMP(6);  // epilogue
   if (lane == 0) {
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_sp_stamp[i], st_acc[i]);
+    for (int i = 0; i < 16; ++i)
+      if (i != 12 && i != 13) atomicAdd(&g_sp_stamp[i], st_acc[i]);
     atomicAdd(&g_sp_stamp[12], (unsigned long long)T);
     atomicAdd(&g_sp_stamp[13], 1ull);
   }

@@ -35,10 +35,10 @@ with torch.no_grad():
         pipe.forward(batch, gb)
     torch.cuda.synchronize()
     fn(buf)
-v = np.array(buf[:10], dtype=np.float64)
+v = np.array([buf[i] for i in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 14)], dtype=np.float64)
 tiles, waves = float(buf[12]), float(buf[13])
-names = ['loop edge', 'A3 (layer 1 k-step 3)', 'B (DMA+flush+norm1)', 'C0-C6 (layer 2)', 'vm wait',
-         'C7', 'epilogue', 'A0', 'A1', 'A2']
+names = ['loop edge', 'A3.3', 'B (flush rest+norm1)', 'C0-C6 (layer 2)', 'slow path',
+         'C7', 'epilogue', 'A0', 'A1', 'A2', 'A3.0', 'A3.1', 'A3.2']
 print(f'tiles {tiles:.0f}, wave-launches {waves:.0f}, tiles per wave {tiles / waves:.1f}')
 for n, x in zip(names, v):
     print(f'{n:18s} {x / tiles:9.0f} cycles per tile  ({x / v.sum() * 100:5.1f} %)')
