@@ -942,7 +942,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
                                   flops_per_launch=flops, bytes_per_launch=nbytes,
                                   reference_form_tflops=round(ref_tf, 2))
         if x3:
-            kname = ('conv_fused (conv_x3_kernel = rg_conv_layer_x3: f32 products from exact '
+            kname = ('conv_fused (conv_x3_sp_kernel = rg_conv_layer_x3: f32 products from exact '
                      '3-term bf16 splits on v_mfma_f32_32x32x16_bf16, gnn_blocks.py:96-113)')
             # roofline on the pipe it runs on: the bf16 matrix cores, which execute six bf16
             # products per f32 product
@@ -954,10 +954,10 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         else:
             kname = 'conv_fused (rg_conv_layer_fused, gnn_blocks.py:96-113)'
         if x3 and not args.fine_events:  # one layer of the stack: edge + node launches + proj / L
-            tparts = [('conv_x3_kernel', 1.0), ('node_x3_kernel', 1.0),
+            tparts = [('conv_x3_sp_kernel', 1.0), ('node_x3_kernel', 1.0),
                       ('proj_x3_kernel', 1.0 / args.layers)]
         elif x3:
-            tparts = [('conv_x3_kernel', 1.0), ('node_x3_kernel', 1.0)]
+            tparts = [('conv_x3_sp_kernel', 1.0), ('node_x3_kernel', 1.0)]
         else:
             tparts = 'conv_f32' if args.dtype == 'fp32' else 'fused_conv'
         traffic, tsrc = pmc_traffic(args, tparts)

@@ -58,7 +58,8 @@ int main() {
     }
     const size_t x3 = rg_conv_layer_x3_workspace_size(s.nodes);
     CHECK(x3 >= (size_t)s.nodes * 64 * sizeof(float));
-    CHECK(rg_conv_x3_blocks_bytes(s.nodes) >= (size_t)(s.nodes + 31) / 32 * 2 * sizeof(int));
+    // the edge launch's wave table: one node boundary per wave + the end (a fixed size)
+    CHECK(rg_conv_x3_blocks_bytes(s.nodes) >= 2 * sizeof(int));
     CHECK(rg_conv_layer_f32_workspace_size(s.nodes) > 0);
     CHECK(rg_conv_blocks_workspace_size(s.nodes) > 0);
     CHECK(rg_csr_by_dst_workspace_size(s.nodes, s.edges) > 0);

@@ -137,7 +137,7 @@ def _check_grads(model, name, d, lists, weights, tag=''):
     for pname, ours, orc, _, _ in rows:
         assert grad_within_f32_bound(ours, orc), (pname, ours, orc)
     print(f'worst gradient error / bound: {worst:.3f}')
-    # headroom: every tensor but the norm scalars at most half its bound
+    # headroom: every tensor at most half its bound
     assert grad_headroom(rows) <= GRAD_HEADROOM, grad_headroom(rows)
 
 
