@@ -11,10 +11,14 @@
 // matrix rate of v_mfma_f32_32x32x2_f32, conv_f32.hip).
 //
 // One layer = an edge launch and a node launch (rg_conv_layer_x3):
-//  * work block = 32 destination nodes and their incoming edges (destination-major CSR; with
-//    the block table, 8-node blocks for the launch tail); workgroups are persistent and take
-//    blocks from one counter per XCD over that XCD's share, stealing from the other XCDs'
-//    tails once theirs is empty; the last workgroup out re-zeroes the counters;
+//  * edge launch for centred layers (the shipped packing) below 4 Mi nodes: conv_x3_sp_kernel,
+//    one wave per SIMD, each wave one contiguous range of whole destinations with an equal
+//    share of the edges (the wave table, rg_conv_x3_blocks), walked in 32-edge tiles that may
+//    span destinations and software-pipelined across tiles (its own comment below);
+//    otherwise conv_x3_kernel, two waves per SIMD: work block = 32 destination nodes and their
+//    incoming edges (destination-major CSR); workgroups are persistent and take blocks from
+//    one counter per XCD over that XCD's share, stealing from the other XCDs' tails once
+//    theirs is empty; the last workgroup out re-zeroes the counters;
 //  * per 32-edge tile a wave computes
 //        h = act(norm(P[dst] + Q[src] + W_e e))     P | Q = the per-node projections of
 //                                                   msg0's x_i / x_j columns (+ b1)
@@ -47,9 +51,6 @@ static constexpr int HID = 128;   // msg_mlp_hidden_dim
 static constexpr int PQW = 2 * HID;
 static constexpr int NBLK = 32;   // destination nodes per work block
 static constexpr int NXCD = 8;
-static constexpr int TBL_HDR = 16;  // block table: NXCD + 1 block offsets, padded, then pairs
-static constexpr int TAIL_PCT = 15; // percent of each XCD's nodes cut into TAILN-node blocks (launch tail)
-static constexpr int TAILN = 8;
 static constexpr int CTR_STRIDE = 32;  // block counters one 128-B line apart (per-line atomics)
 static constexpr int CTR_BYTES = 2048; // counter area at the front of the workspace
 static constexpr int FT = 512;         // edge launch: 8 waves, two per SIMD
@@ -98,7 +99,6 @@ __device__ __forceinline__ void project_rows(const f32x16 (&xo)[2], const WSrc& 
 }
 
 struct Args {
-  const int* table;      // optional work-block table (rg_conv_x3_blocks), else NBLK-node runs
   const float* x;
   const float* e;
   const float* pq;       // [N][256]: P | Q of this layer
@@ -226,12 +226,10 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
   const float* bias2 = (const float*)(lds + W2_OFF + 3 * plane_bytes(HID, C));
   const float mu0 = nrm[0], sd0 = nrm[1], mu1 = nrm[2], sd1 = nrm[3];
 
-  // with a block table: this XCD's blocks are table[xcd] .. table[xcd + 1] of the (first,
-  // end) node pairs at table + TBL_HDR, largest first
+  // this XCD's share of the NBLK-node blocks: [xlo(xcd), xlo(xcd + 1))
   const int xcd = blockIdx.x % NXCD;
-  auto xlo = [&](int x) { return a.table ? a.table[x] : (int)((long)a.n_blocks * x / NXCD); };
+  auto xlo = [&](int x) { return (int)((long)a.n_blocks * x / NXCD); };
   int blo = xlo(xcd), bhi = xlo(xcd + 1);
-  const int* pairs = a.table ? a.table + TBL_HDR : nullptr;
   int* ctr = a.counters + CTR_STRIDE * xcd;
   int steal = 0;  // other XCDs' queues visited after this one drained
   for (;;) {
@@ -249,8 +247,8 @@ __global__ __launch_bounds__(FT) void conv_x3_kernel(Args a) {
       ctr = a.counters + CTR_STRIDE * x2;
       continue;
     }
-    const int n0 = pairs ? pairs[2 * blk] : blk * NBLK;
-    const int n1 = pairs ? pairs[2 * blk + 1] : min(n0 + NBLK, a.n_nodes);
+    const int n0 = blk * NBLK;
+    const int n1 = min(n0 + NBLK, a.n_nodes);
     const int e0 = a.seg_ptr[n0], e1 = a.seg_ptr[n1];
     float run = 0.f;  // lane = feature: running sum of the current destination
     // its aggregate row (wave-uniform); before the block's first destination a dummy row past
@@ -479,23 +477,27 @@ __global__ __launch_bounds__(PFT) void proj_x3_kernel(const float* x, int ldx, i
 // conv_x3_kernel runs the whole tile program per wave, two waves per SIMD: its MFMA phases
 // (layers 1 and 2) and its vector / memory phases (gathers, e split, norms, segmented sum)
 // run back to back in each wave and overlap only as far as the SIMD's two waves happen to
-// interleave (MFMA busy ~57 %).  Here each SIMD holds ONE wave that keeps the matrix pipe fed
-// by itself: while tile i's MFMAs issue, the same instruction stream carries
-//   * during layer 1 of tile i: the split of tile i's e rows (its B operand), norm 2 of tile
-//     i - 1, its message transposes and the in-order running sums, and the loads of tile
-//     i + 1 (Q rows by LDS-DMA, e rows, the indices of tile i + 2, layer 2's bias);
-//   * between the layers: the flushes of tile i - 1's finished destinations, norm 1's
-//     statistics of tile i, the P rows of tile i + 1;
-//   * during layer 2 of tile i: its B operand (norm 1's scale + LeakyReLU + split), then
-//     tile i + 1's accumulator init P[dst] + Q[src].
+// interleave.  Here each SIMD holds ONE wave that keeps the matrix pipe fed by itself: the
+// 192 MFMAs of tile i are cut into sub-chunks of 4 - 12 (a sched_barrier each) and every
+// piece of vector / memory work is placed in one of them:
+//   * layer 1 of tile i (region A, 96 MFMAs): the split of tile i's e rows (its B operand),
+//     the P + Q init of its accumulator tiles 1-3, norm 2 of tile i - 1 and its message
+//     transposes, the in-order running sums (8 edges per sub-chunk) and the first four
+//     finished destinations (one per sub-chunk), norm 1's partial sums, the loads of tile
+//     i + 1 (e rows, Q rows, ring rows) and the indices of tile i + 2;
+//   * between the layers (region B): norm 1's scale;
+//   * layer 2 of tile i (96 MFMAs): its B operand one k-step ahead (norm 1 + LeakyReLU +
+//     split), tile i + 1's ring rows and its first accumulator tile, its first B operand.
 // Work: the destination-major CSR cut into one contiguous range of whole destinations per
-// wave with equal edge counts (rg_conv_x3_blocks / the workspace table; XCD-major ranks, so
-// an XCD's waves hold one contiguous node range), walked in 32-edge tiles that may span
-// destinations -- each destination's messages are still summed in CSR order by one wave.
+// wave with equal edge counts (the wave table: rg_conv_x3_blocks, or built into the
+// workspace; XCD-major ranks, so an XCD's waves hold one contiguous node range), walked in
+// 32-edge tiles that may span destinations -- each destination's messages are still summed
+// in CSR order by one wave, the running sum carried from tile to tile.
 // Registers: the weight fragments are read from LDS into AGPRs (inline ds_read, the MFMA
-// takes its A operand from AGPRs), the rest stays in VGPRs; LDS = the W_e and W_2 planes
-// (96 KiB) + one 16 KiB buffer per wave that holds the next tile's Q rows (LDS-DMA) and,
-// between two uses, the message tile being transposed.
+// takes its A operand from AGPRs), the rest stays in VGPRs (256 + ~110 AGPRs, no scratch).
+// LDS: the W_e and W_2 planes (96 KiB), layer 2's bias, and per wave the message transpose
+// tile and a ring of the P rows of its last 8 destinations (a tile's P[dst] is one row per
+// destination: 2 rows loaded per tile instead of one row per edge).
 typedef float f32x32 __attribute__((ext_vector_type(32)));
 namespace sp {
 constexpr int FT = 256, NW = FT / 64;
@@ -1116,9 +1118,6 @@ __global__ __launch_bounds__(256) void conv_x3_waves_kernel(const int* __restric
 using namespace rg;
 using namespace rg::convx3;
 
-#ifndef RG_CX3_SP
-#define RG_CX3_SP 1  // the one-wave-per-SIMD software-pipelined edge launch (conv_x3_sp_kernel)
-#endif
 static size_t x3_agg_bytes(int n_nodes) {
   // the aggregate rows, one dummy row (the flush target before a block's / wave's first
   // destination) and one per wave of the one-wave launch (its unused branch-free flushes)
@@ -1161,89 +1160,9 @@ extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int 
   return RG_OK;
 }
 
-// Work blocks of the edge launch for one graph: XCD x's share of the nodes
-// [N x / 8, N (x + 1) / 8) -- its frames' rows in one L2 -- as 32-node runs over the first
-// (100 - TAIL_PCT) % and TAILN-node runs over the rest, all ordered by edge tiles, largest
-// first: the waves take the big blocks first and end on the small ones, so the launch tail
-// (waves idle until the last block of their workgroup ends: 14 % of the wave time with
-// 32-node blocks only, M) shrinks to a few tiles.  Order and size change no result: each
-// destination's messages are summed in CSR order within one block.
-__host__ __device__ inline void x3_share(int n, int x, int& a0, int& sp, int& b0) {
-  a0 = (int)((long)n * x / NXCD);
-  b0 = (int)((long)n * (x + 1) / NXCD);
-  sp = a0 + (int)((long)(b0 - a0) * (100 - TAIL_PCT) / 100 / NBLK) * NBLK;
-}
-__host__ __device__ inline int x3_share_blocks(int n, int x) {
-  int a0, sp, b0;
-  x3_share(n, x, a0, sp, b0);
-  return (sp - a0 + NBLK - 1) / NBLK + (b0 - sp + TAILN - 1) / TAILN;
-}
-// order: 0 = every block by edge tiles, largest first;
-// 1 = the 32-node blocks in node order (consecutive blocks share their frame's rows in
-// L2), then the tail blocks largest first; 2 = every block in node order
-__global__ __launch_bounds__(256) void conv_x3_blocks_kernel(const int* __restrict__ seg_ptr,
-                                                             int n, int* __restrict__ table,
-                                                             int order) {
-  constexpr int NBIN = 64;
-  __shared__ int hist[NBIN];
-  const int x = blockIdx.x;
-  int off = 0;
-  for (int xx = 0; xx < x; ++xx) off += x3_share_blocks(n, xx);
-  int a0, sp, b0;
-  x3_share(n, x, a0, sp, b0);
-  const int nmain = (sp - a0 + NBLK - 1) / NBLK;
-  const int m = nmain + (b0 - sp + TAILN - 1) / TAILN;
-  if (threadIdx.x == 0) {
-    table[x] = off;
-    if (x == NXCD - 1) table[NXCD] = off + m;
-  }
-  if (threadIdx.x < NBIN) hist[threadIdx.x] = 0;
-  __syncthreads();
-  auto block = [&](int i, int& n0, int& n1) {
-    if (i < nmain) {
-      n0 = a0 + NBLK * i;
-      n1 = min(n0 + NBLK, sp);
-    } else {
-      n0 = sp + TAILN * (i - nmain);
-      n1 = min(n0 + TAILN, b0);
-    }
-    const int t = (seg_ptr[n1] - seg_ptr[n0] + 31) / 32;
-    return NBIN - 1 - min(t, NBIN - 1);  // bin 0 = the most tiles
-  };
-  const int sorted0 = order == 0 ? 0 : order == 1 ? nmain : m;  // blocks [sorted0, m) sorted
-  for (int i = sorted0 + threadIdx.x; i < m; i += blockDim.x) {
-    int n0, n1;
-    atomicAdd(&hist[block(i, n0, n1)], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < NBIN; ++i) {
-      const int c = hist[i];
-      hist[i] = acc;
-      acc += c;
-    }
-  }
-  __syncthreads();
-  int* pairs = table + TBL_HDR;
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    int n0, n1;
-    const int bin = block(i, n0, n1);
-    const int pos = off + (i < sorted0 ? i : sorted0 + atomicAdd(&hist[bin], 1));
-    pairs[2 * pos] = n0;
-    pairs[2 * pos + 1] = n1;
-  }
-}
-
-static int x3_total_blocks(int n) {
-  int t = 0;
-  for (int x = 0; x < NXCD; ++x) t += x3_share_blocks(n, x);
-  return t;
-}
-
 extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
-  if (RG_CX3_SP) return (size_t)(sp::WMAX + 1) * sizeof(int);
-  return (size_t)(TBL_HDR + 2 * x3_total_blocks(n_nodes > 0 ? n_nodes : 1)) * sizeof(int);
+  (void)n_nodes;
+  return (size_t)(sp::WMAX + 1) * sizeof(int);
 }
 
 static int x3_wave_table(const int* seg_ptr, int n_nodes, int* table, void* stream) {
@@ -1255,10 +1174,7 @@ static int x3_wave_table(const int* seg_ptr, int n_nodes, int* table, void* stre
 
 extern "C" int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream) {
   RG_REQUIRE(seg_ptr && table && n_nodes >= 1, RG_ERR_ARG, "rg_conv_x3_blocks: bad argument");
-  if (RG_CX3_SP) return x3_wave_table(seg_ptr, n_nodes, table, stream);
-  conv_x3_blocks_kernel<<<NXCD, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, table, 0);
-  RG_LAUNCH_CHECK();
-  return RG_OK;
+  return x3_wave_table(seg_ptr, n_nodes, table, stream);
 }
 
 static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, const float* x,
@@ -1341,11 +1257,10 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
   a.lde = lde;
   a.ldo = ld_out;
   a.n_nodes = n_nodes;
-  a.n_blocks = table ? x3_total_blocks(n_nodes) : (n_nodes + NBLK - 1) / NBLK;
-  a.table = table;
+  a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
   a.aggr_mean = aggr == RG_REDUCE_MEAN;
   // (the one-wave launch addresses Q rows with 32-bit byte offsets: < 4 Mi nodes)
-  if (RG_CX3_SP && cent && n_nodes < (1 << 22)) {
+  if (cent && n_nodes < (1 << 22)) {
     const int* wtab = table;
     if (!wtab) {  // no per-graph table: build the wave ranges into the workspace
       int* ws_tab = (int*)((char*)workspace + CTR_BYTES + x3_agg_bytes(n_nodes));
@@ -1357,11 +1272,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
     RG_ENSURE_LDS(edge, sp::LDS);
     edge<<<x3_sp_groups(n_nodes), sp::FT, sp::LDS, (hipStream_t)stream>>>(a, wtab);
     RG_LAUNCH_CHECK();
-  } else {
-  if (RG_CX3_SP) {  // the table holds the wave ranges: plain NBLK-node runs here
-    a.table = nullptr;
-    a.n_blocks = (n_nodes + NBLK - 1) / NBLK;
-  }
+  } else {  // (a wave table, if given, is not used: NBLK-node blocks)
   int blocks = 256;  // one workgroup per CU (LDS); a multiple of the 8 XCDs
   const int need = (a.n_blocks + NW - 1) / NW;
   if (blocks > need) blocks = (need + NXCD - 1) / NXCD * NXCD;

@@ -209,16 +209,19 @@ class GraphBatch:
     graph: engine.DeviceGraph    # destination-major view + link pairs
     node_features: torch.Tensor  # float32 [N, 6]
     edge_features: torch.Tensor  # float32 [cap, 7], destination-major order
-    # radius graphs built into an unchecked capacity: device int32[1] = the true edge count
-    # (rg_csr_clamp); None when the capacity was checked on the host (or is exact, kNN)
-    need_dev: Optional[torch.Tensor] = None
+    # radius graphs built into an unchecked capacity: (pinned host int32[1] = the true edge
+    # count, written by rg_csr_clamp itself; the event after it); None when the capacity was
+    # checked on the host (or is exact, kNN)
+    need: Optional[tuple] = None
 
     def check_capacity(self):
         """Raise if this graph was cut to its capacity (a radius graph built without a host
         sync whose edges outgrew the capacity that sufficed before): every output computed
         from it is invalid.  Host sync."""
-        if self.need_dev is not None:
-            need = int(self.need_dev.item())
+        if self.need is not None:
+            host, ev = self.need
+            ev.synchronize()
+            need = int(host[0])
             if need > self.capacity:
                 raise RuntimeError(f'radius graph needed {need} edges but was built into a '
                                    f'capacity of {self.capacity}; this step\'s outputs are '
@@ -241,8 +244,8 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
     # radius graphs have no a-priori edge bound.  First build (nothing cached): built,
     # checked with one host sync and rebuilt if short.  Later builds use the cached
     # capacity WITHOUT a host sync: rg_csr_clamp keeps an overflowing graph in bounds and
-    # records the true edge count, read back asynchronously (pinned copy + event) and
-    # checked at the next build -- a short capacity grows there -- and by
+    # writes the true edge count straight into pinned host memory (no copy launch; an event
+    # marks it landed), checked at the next build -- a short capacity grows there -- and by
     # GraphBatch.check_capacity() (called by edge_index() / RadarGNNPipeline.trim()).
     cap_key = ('radius_cap', mode, float(eps2))
     pend_key = ('radius_need', mode, float(eps2))
@@ -263,7 +266,7 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
                                                     batch.arrays['meas_py'], batch.frame_ptr,
                                                     batch.frame_sizes, k, eps2, mode,
                                                     edge_capacity=cap0, ws_cache=ws_cache)
-    need_dev = None
+    need = None
     if mode != nat.GRAPH_KNN and cap0 is None:
         E = int(ne.item())
         if E > cap:
@@ -273,18 +276,19 @@ def build_graph_batch(batch: FrameBatch, cfg, k: Optional[int] = None, eps2: Opt
         if ws_cache is not None:
             ws_cache[cap_key] = cap
     elif mode != nat.GRAPH_KNN:
-        need_dev = torch.empty(1, dtype=torch.int32, device=row_ptr.device)
-        nat.check(nat.lib().rg_csr_clamp(row_ptr.data_ptr(), batch.n_nodes, ne.data_ptr(), cap,
-                                         need_dev.data_ptr(), nat.stream_ptr(row_ptr.device)),
-                  'rg_csr_clamp')
+        # pinned host memory is mapped into the device's address space: the clamp kernel
+        # stores the count there directly
         host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-        host.copy_(need_dev, non_blocking=True)
+        nat.check(nat.lib().rg_csr_clamp(row_ptr.data_ptr(), batch.n_nodes, ne.data_ptr(), cap,
+                                         host.data_ptr(), nat.stream_ptr(row_ptr.device)),
+                  'rg_csr_clamp')
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(row_ptr.device))
         ws_cache.setdefault(pend_key, []).append((host, ev))
+        need = (host, ev)
     g = engine.graph_from_csr(row_ptr, col, batch.n_nodes, ne, cap)
     g.set_frames(batch.frame_ptr, batch.n_frames)
     nf = engine.node_features(batch.arrays, deg, batch.frame_ptr, batch.n_frames, cfg)
     # destination-major edge (src = g.src[p] -> dst = g.dst[p])
     ef = engine.edge_features(batch.arrays, g.src, g.dst, ne, cap)
-    return GraphBatch(row_ptr, col, deg, ne, cap, g, nf, ef, need_dev)
+    return GraphBatch(row_ptr, col, deg, ne, cap, g, nf, ef, need)

@@ -205,8 +205,10 @@ int rg_csr_rows(const int* row_ptr, int n_rows, int* out, void* stream);
 
 /* Capacity guard for a graph built by rg_build_graph into a capacity the host has not
  * checked (radius graphs without a host sync, graph_features.py:build_graph_batch):
- * need_out[0] = the true edge count (device int32); if it exceeds capacity, row_ptr is cut
- * at a row boundary (the rows rg_build_graph left unwritten become empty) and *n_edges_dev = that boundary, so every consumer stays in bounds.  The host
+ * need_out[0] = the true edge count (int32 in device memory, or in pinned host memory -- the
+ * kernel stores it directly, no copy launch); if it exceeds capacity, row_ptr is cut at a
+ * row boundary (the rows rg_build_graph left unwritten become empty) and *n_edges_dev =
+ * that boundary, so every consumer stays in bounds.  The host
  * reads need_out later (no sync on the launch path) and treats the step as invalid when
  * need_out[0] > capacity.  (The cut is at the last boundary <= capacity / 2: a cut graph is
  * not symmetric, and the link-pair arrays hold capacity / 2 + 1 pairs.) */
@@ -366,8 +368,8 @@ int rg_conv_layer_f32(const rg_layer* layers, int aggr, const float* x, int ldx,
 /* The same FLOAT32 layer on the bf16 matrix cores: every product of the MLPs is formed
  * from the exact three-term bf16 splits of both operands (six bf16 products of total
  * weight <= 2 per product, f32 accumulation; dropped terms < 2^-23 |a b|), so the layer
- * keeps float32 accuracy at 2.7x the matrix rate of the f32 MFMA path.  One launch per
- * layer:
+ * keeps float32 accuracy at 2.7x the matrix rate of the f32 MFMA path.  Two launches per
+ * layer (edge: layers [0], [1] and the in-order segmented sum; node: [2] and next_pq):
  *   layers[3], all RG_PACK_X3: [0] W_msg0[:, 128:192] (edge columns, FAST_IN) with msg0's
  *     norm + act, bias unused; [1] msg1 (FAST_CHAIN); [2] upd on cat(x, agg) (FAST_IN over
  *     the 128 concatenated inputs)
@@ -383,16 +385,17 @@ int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, 
                      int ldx, const float* e, int lde, const float* pq, const int* seg_ptr,
                      const int* src, const int* dst, int n_nodes, float* x_out, int ld_out,
                      float* pq_out, void* workspace, size_t workspace_bytes, void* stream);
-/* The same layer over a work-block table from rg_conv_x3_blocks (built once per graph): each
- * XCD's eighth of the nodes in 32-node blocks, its last 15 % in 8-node blocks, ordered by
- * edge tiles, largest first, so the launch ends on small blocks.  Same results. */
+/* The same layer with the edge launch's wave table from rg_conv_x3_blocks (built once per
+ * graph instead of once per layer): one contiguous range of whole destinations per wave of
+ * the one-wave-per-SIMD edge launch, equal edge counts.  Same results. */
 int rg_conv_layer_x3_blocks(const rg_layer* layers, const rg_layer* next_pq, int aggr,
                             const float* x, int ldx, const float* e, int lde, const float* pq,
                             const int* seg_ptr, const int* src, const int* dst, int n_nodes,
                             float* x_out, int ld_out, float* pq_out, const int* table,
                             void* workspace, size_t workspace_bytes, void* stream);
-/* table: rg_conv_x3_blocks_bytes(n_nodes) bytes of device memory -- int32 block offsets per
- * XCD [9] (padded to 16), then (first node, end node) pairs -- from seg_ptr[n_nodes + 1]. */
+/* table: rg_conv_x3_blocks_bytes(n_nodes) bytes of device memory -- int32 node boundaries of
+ * the edge launch's waves (wave w takes destinations [table[w], table[w + 1])) -- from
+ * seg_ptr[n_nodes + 1]. */
 size_t rg_conv_x3_blocks_bytes(int n_nodes);
 int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream);
 /* P | Q of the first layer for dense float32 rows x [n_nodes][ldx >= 64]: pq layer packed
