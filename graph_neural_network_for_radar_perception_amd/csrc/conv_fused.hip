@@ -27,12 +27,6 @@
 #include "rg_common.h"
 #include "scan.h"
 
-#ifndef RG_CONV_EXP
-#define RG_CONV_EXP 0  // timing experiments only (wrong results): 1 no row gathers after the
-                       // first tile, 2 no message norm/act, 3 no transpose/aggregation,
-                       // 4 accumulators start from zero instead of P (no LDS reads)
-#endif
-
 #define RG_HALF_F16 0
 #define RG_CONV_NS conv
 #include "conv_fused_impl.h"
@@ -48,9 +42,6 @@
 using namespace rg;
 using namespace rg::conv;
 
-#ifndef RG_CONV_LPT
-#define RG_CONV_LPT 1  // 0: blocks in node order (timing comparison)
-#endif
 // Each XCD's share of the blocks (the fused kernel's ranges [n*x/NQ, n*(x+1)/NQ) of the
 // dequeue order) sorted by tile count, largest first: the waves then finish on the
 // smallest blocks (greedy longest-first), instead of on whatever blocks come last in node
@@ -83,7 +74,7 @@ __global__ __launch_bounds__(256) void conv_blocks_lpt(const int* __restrict__ b
   }
   __syncthreads();
   for (int b = lo + threadIdx.x; b < hi; b += blockDim.x) {
-    const int pos = RG_CONV_LPT ? lo + atomicAdd(&hist[bin(b)], 1) : b;
+    const int pos = lo + atomicAdd(&hist[bin(b)], 1);
     pairs[2 * pos] = bounds[b];
     pairs[2 * pos + 1] = bounds[b + 1];
   }

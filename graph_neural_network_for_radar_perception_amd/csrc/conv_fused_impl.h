@@ -9,23 +9,16 @@ using HT = ::rg::H16<RG_HALF_F16 != 0>;  // the 16-bit operand type (bf16 / fp16
 typedef HT::v8 bf16x8_t;  // (named for the bf16 build; fp16 lanes in the fp16 build)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef RG_CONV_PFX
-#define RG_CONV_PFX 0  // 1: the next block's x rows for P are loaded one block ahead
-#endif
-
-#ifndef RG_CONV_CT
-#define RG_CONV_CT 512  // threads per workgroup (8 waves, 2 per SIMD)
-#endif
-static constexpr int CT = RG_CONV_CT;
+static constexpr int CT = 512;  // threads per workgroup (8 waves, 2 per SIMD)
 static constexpr int CW = CT / 64;
 static constexpr int NB = 8;         // destination nodes per work block
 static constexpr int C = 64;         // node / edge / message / output channels
 static constexpr int HID = 128;      // msg_mlp_hidden_dim
 // wave-private LDS: P (NB rows of HID f32, row stride PST: the 4-float pad puts the rows of
 // different nodes on different banks -- at HID they all mapped to the same four), message
-// tile (32 x C bf16), slots (32 int)
+// tile (32 x C bf16)
 static constexpr int PST = HID + 4;
-static constexpr int WAVE_LDS = NB * PST * 4 + 32 * C * 2 + 128;
+static constexpr int WAVE_LDS = NB * PST * 4 + 32 * C * 2;
 static constexpr float NORM_EPS = 1e-5f;
 // Work-block heads: one per XCD (workgroup b runs on XCD b % 8), each on a 128-B line of
 // its own.  One shared head saturates at ~88 dequeues/us (MI355X_MICROARCH.md, dequeue):
@@ -33,16 +26,9 @@ static constexpr float NORM_EPS = 1e-5f;
 static constexpr int NQ = 8;
 static constexpr int CTR_STRIDE = 32;
 
-#ifndef RG_CONV_STEAL
-#define RG_CONV_STEAL 0  // 1: a wave whose XCD queue drained takes blocks from the others
-                         // (C2 -0.5 %, C5 +23 %: stealers saturate the heads of small blocks)
-#endif
-
-#ifndef RG_CONV_LUT
-#define RG_CONV_LUT 1  // one-hot segment matrix from a 256-entry LDS table (0: per-edge compares)
-#endif
-// the one-hot table: entry b = eight 16-bit ONEs / zeros for the bits of b (4 KiB of LDS)
-static constexpr int LUT_BYTES = RG_CONV_LUT ? 256 * 16 : 0;
+// the one-hot segment matrix from a 256-entry LDS table: entry b = eight 16-bit ONEs / zeros
+// for the bits of b (4 KiB of LDS)
+static constexpr int LUT_BYTES = 256 * 16;
 
 #ifndef RG_CONV_STAMP
 #define RG_CONV_STAMP 0  // diagnostic build: per-phase s_memtime sums in g_conv_stamp
@@ -107,21 +93,12 @@ __device__ __forceinline__ bf16x8_t zero_bf8() {
 // Software pipelined: the A fragments of step s+1 are read from LDS while the MFMAs of
 // step s issue, so an MFMA never waits for the LDS read that feeds it; one scheduling
 // fence per step keeps the compiler from hoisting the whole layer's fragments.
-#ifndef RG_CONV_PFD
-#define RG_CONV_PFD 1  // A-fragment prefetch distance (k-steps) for layers with MT <= 2
-#endif
-
-#ifndef RG_CONV_PFD4
-#define RG_CONV_PFD4 1  // the same for the 4-tile first message layer
-#endif
+static constexpr int PD = 1;  // A-fragment prefetch distance (k-steps)
 
 template <int KS, int MT, int KT, int S0>
 __device__ __forceinline__ void mfma_steps(const bf16x8_t* b, f32x16 (&acc)[MT], const char* w,
                                            int lane) {
   const char* wl = w + lane * 16;
-  // narrow layers (MT <= 2) issue only MT MFMAs per k-step, less than an LDS round trip:
-  // their fragments are read PD steps ahead (registers: (PD + 1) * MT fragments)
-  constexpr int PD = MT <= 2 ? RG_CONV_PFD : RG_CONV_PFD4;
   bf16x8_t f[KS][MT];
 #pragma unroll
   for (int s = 0; s < PD && s < KS; ++s)
@@ -148,7 +125,6 @@ template <int KS, int MT, int KT, int S0, typename BOp>
 __device__ __forceinline__ void mfma_steps_jit(BOp&& bop, f32x16 (&acc)[MT], const char* w,
                                                int lane) {
   const char* wl = w + lane * 16;
-  constexpr int PD = MT <= 2 ? RG_CONV_PFD : RG_CONV_PFD4;
   bf16x8_t f[KS][MT];
 #pragma unroll
   for (int s = 0; s < PD && s < KS; ++s)
@@ -172,9 +148,6 @@ __device__ __forceinline__ void mfma_steps_jit(BOp&& bop, f32x16 (&acc)[MT], con
   }
 }
 
-#ifndef RG_CONV_JIT
-#define RG_CONV_JIT 1  // message layer 1's norm + LeakyReLU + pack inside layer 2's k-steps
-#endif
 
 // channel_normalization (common.py:208-220) + activation (rg_common.h)
 // (every block is normalised; with ACT >= 0 every block uses ACT and was packed
@@ -237,7 +210,6 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   for (int l = 0; l < 3; ++l) {
     stage_lds<CT>(lds + a.L[l].woff, a.L[l].src, a.L[l].bytes);
   }
-#if RG_CONV_LUT
   for (int b = threadIdx.x; b < 256; b += CT) {
     u32x4 e;
 #pragma unroll
@@ -245,22 +217,15 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       e[i] = (((b >> (2 * i)) & 1) ? HT::ONE : 0u) | ((((b >> (2 * i + 1)) & 1) ? HT::ONE : 0u) << 16);
     *(u32x4*)(lds + a.total_bytes + 16 * b) = e;
   }
-#endif
   __syncthreads();
   CSTAMP(0);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-#ifdef RG_CONV_PRIO
-  // static priority for the second-dispatched half of the waves (MI355X_MICROARCH.md,
-  // "two waves per SIMD", item 4)
-  if (wave >= CW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-  // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16, slots [32]
+  // wave-private: P [NB][MT=4][h][16] f32, message tile [32][64] bf16
   const u32x4* lut = (const u32x4*)(lds + a.total_bytes);
   char* wbase = lds + a.total_bytes + LUT_BYTES + wave * WAVE_LDS;
   float* P = (float*)wbase;
   uint16_t* tile = (uint16_t*)(wbase + NB * PST * 4);
-  int* slots = (int*)((char*)tile + 32 * C * 2);
   const char* w0 = lds + a.L[0].woff;
   const char* w1 = lds + a.L[1].woff;
   const char* w2 = lds + a.L[2].woff;
@@ -278,22 +243,6 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   int blo = (int)((long)n_blocks * xcd / NQ);
   int bhi = (int)((long)n_blocks * (xcd + 1) / NQ);
   int* head = a.counter + CTR_STRIDE * xcd;
-  // this XCD's queue drained: take blocks from the other XCDs' queues (their tails; the
-  // rows are cold in this L2, but the launch no longer waits on the slowest XCD); -1: done
-  int steal = 0;
-  auto steal_next = [&]() -> int {
-    while (RG_CONV_STEAL && ++steal < NQ) {
-      const int x2 = (xcd + steal) % NQ;
-      blo = (int)((long)n_blocks * x2 / NQ);
-      bhi = (int)((long)n_blocks * (x2 + 1) / NQ);
-      head = a.counter + CTR_STRIDE * x2;
-      int b = 0;
-      if (lane == 0) b = atomicAdd(head, 1);
-      b = blo + __shfl(b, 0, 64);
-      if (b < bhi) return b;
-    }
-    return -1;
-  };
   // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
   auto block_nodes = [&](int b, int& n0, int& n1) {
     if (a.blk_nodes) {
@@ -307,56 +256,30 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   int blk = 0;
   int e0 = 0, e1 = 0, bn0 = 0, bn1 = 0;
   int s_hi = 0;  // static schedule: the end of this wave's node range
-  // static schedule's dynamic tail: the nodes [wave_nodes[n_waves], n_nodes) after every
-  // static range, in NB-node blocks dealt round robin to the XCDs' counters (unused by the
-  // static schedule otherwise): a wave whose range is done takes the next block of its XCD
-  int t_lo = 0;
-  auto tail_next = [&](int& n0, int& n1) {
-    int b = 0;
-    if (lane == 0) b = atomicAdd(head, 1);
-    b = __shfl(b, 0, 64);
-    n0 = t_lo + NB * (xcd + NQ * b);
-    n1 = min(n0 + NB, a.n_nodes);
-    return n0 < a.n_nodes;
-  };
   if (a.wave_nodes) {
     const int rank = (blockIdx.x % NQ) * (int)(gridDim.x / NQ) * CW + (blockIdx.x / NQ) * CW + wave;
-    t_lo = a.wave_nodes[gridDim.x * CW];
     bn0 = a.wave_nodes[rank];
     s_hi = a.wave_nodes[rank + 1];
     bn1 = min(bn0 + NB, s_hi);
     blk = bn0 < s_hi ? 0 : -1;
-    if (blk < 0 && t_lo < a.n_nodes) blk = tail_next(bn0, bn1) ? 0 : -1;
   } else {
     if (lane == 0) blk = atomicAdd(head, 1);
     blk = blo + __shfl(blk, 0, 64);
-    if (blk >= bhi) blk = steal_next();
+    if (blk >= bhi) blk = -1;
     if (blk >= 0) block_nodes(blk, bn0, bn1);
   }
   if (blk >= 0) {
     e0 = a.seg_ptr[bn0];
     e1 = a.seg_ptr[bn1];
   }
-#if RG_CONV_PFX
-  // x rows of the block's nodes for P, loaded one block ahead (the block start otherwise
-  // waits a full global round trip before its first MFMA)
-  bf16x8_t bxn[4];
-  {
-    const uint16_t* px = a.x + (size_t)min(bn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
-  }
-#endif
   while (blk >= 0) {
     const int n0 = bn0;
     const int n1 = bn1;
     int nxt_raw = 0;
     if (!a.wave_nodes && lane == 0) nxt_raw = atomicAdd(head, 1);
-#if RG_CONV_LUT
     // the block's node r (= one-hot column / slot r) owns the CSR range [sst, sen); lanes
     // past the block's nodes get an empty range (clamped loads, no branch)
     const int sst = a.seg_ptr[min(n0 + r, n1)], sen = a.seg_ptr[min(n0 + r + 1, n1)];
-#endif
     f32x16 agg[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) agg[m] = (f32x16){0.f};
@@ -383,17 +306,16 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       }
     };
     auto compute = [&](const bf16x8_t (&b)[8], int slot, int t0) {
-      const bool valid = t0 + r < e1;
       f32x16 acc1[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        acc1[m] = RG_CONV_EXP == 4 ? (f32x16){0.f} : ld_bias_frag(P + slot * PST, m, h);
+        acc1[m] = ld_bias_frag(P + slot * PST, m, h);
       mfma_steps<8, 4, 12, 4>(b, acc1, w0, lane);  // k-steps 4..11: x[src], e
       f32x16 acc2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) acc2[m] = ld_bias_frag(bias1, m, h);
 #ifndef RG_NO_FUSED_LEAKY
-      if constexpr (RG_CONV_JIT && ACT == ACT_LEAKY && RG_CONV_EXP != 2) {
+      if constexpr (ACT == ACT_LEAKY) {
         // the same values as norm_act + pack_acc (same fmas, same order), formed per k-step
         const f32x2 sc = norm_leaky_scale<4>(acc1, nrm[0], nrm[1], NORM_EPS);
         mfma_steps_jit<8, 2, 8, 0>([&](int s) {
@@ -411,17 +333,12 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       } else
 #endif
       {
-        if (RG_CONV_EXP != 2) norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
+        norm_act<ACT, 4>(acc1, a.L[0], nrm[0], nrm[1]);
         bf16x8_t b2[8];
         pack_acc<4>(acc1, b2);
         mfma_steps<8, 2, 8, 0>(b2, acc2, w1, lane);
       }
-      if (RG_CONV_EXP != 2) norm_act<ACT, 2>(acc2, a.L[1], nrm[2], nrm[3]);
-      if (RG_CONV_EXP == 3) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) agg[m] += acc2[m];
-        return;
-      }
+      norm_act<ACT, 2>(acc2, a.L[1], nrm[2], nrm[3]);
       // ---- message tile M -> LDS rows [edge][feature] (8-B stores of 4 features)
       const int sr = swz(r);
 #pragma unroll
@@ -434,17 +351,12 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
           const int gr = (8 * m + 2 * g + h) ^ sr;
           *(uint2*)(tile + r * C + 4 * gr) = wv;
         }
-#if RG_CONV_LUT
       // slot r's edges in this tile: bits [sst - t0, sen - t0) of a 32-bit mask (edges past
       // the block's end belong to no slot)
       const int lo_b = min(max(sst - t0, 0), 32), hi_b = min(max(sen - t0, 0), 32);
       const uint32_t mhi = hi_b >= 32 ? 0xffffffffu : ((1u << hi_b) - 1u);
       const uint32_t mlo = lo_b >= 32 ? 0xffffffffu : ((1u << lo_b) - 1u);
       const uint32_t smask = mhi & ~mlo;
-      (void)valid;
-#else
-      if (h == 0) slots[r] = valid ? slot : 31;
-#endif
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       // ---- Agg[feature][slot] += sum_edges M[feature][edge] * S[edge][slot]
@@ -455,19 +367,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // B = S (k = edge 16s + 8h + j, col = slot r): one-hot bf16
-#if RG_CONV_LUT
         const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, lut[(smask >> (16 * s + 8 * h)) & 0xffu]);
-#else
-        const int4 sa = *(const int4*)(slots + 16 * s + 8 * h);
-        const int4 sb = *(const int4*)(slots + 16 * s + 8 * h + 4);
-        const uint32_t one = HT::ONE;
-        u32x4 sv;
-        sv[0] = (sa.x == r ? one : 0u) | ((sa.y == r ? one : 0u) << 16);
-        sv[1] = (sa.z == r ? one : 0u) | ((sa.w == r ? one : 0u) << 16);
-        sv[2] = (sb.x == r ? one : 0u) | ((sb.y == r ? one : 0u) << 16);
-        sv[3] = (sb.z == r ? one : 0u) | ((sb.w == r ? one : 0u) << 16);
-        const bf16x8_t sf = __builtin_bit_cast(bf16x8_t, sv);
-#endif
         const int row_lo = 16 * s + 8 * (G >> 1) + q4, row_hi = row_lo + 4;
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -498,17 +398,11 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     //      third of the message MLP's first layer is the same for every edge into a node,
     //      so it is computed once per node here instead of once per edge
     {
-#if RG_CONV_PFX
-      bf16x8_t bx[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) bx[s] = bxn[s];
-#else
       const int node = min(n0 + r, n1 - 1);
       const uint16_t* px = a.x + (size_t)node * a.ldx + 8 * h;
       bf16x8_t bx[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) bx[s] = ld_bf8(px + 16 * s);
-#endif
       f32x16 accp[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) accp[m] = ld_bias_frag(bias0, m, h);
@@ -535,23 +429,15 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       nn0 = n1;
       nn1 = min(n1 + NB, s_hi);
       nxt = nn0 < s_hi ? 0 : -1;
-      if (nxt < 0 && t_lo < a.n_nodes) nxt = tail_next(nn0, nn1) ? 0 : -1;
     } else {
       nxt = blo + __shfl(nxt_raw, 0, 64);
-      if (nxt >= bhi) nxt = steal_next();
+      if (nxt >= bhi) nxt = -1;
       if (nxt >= 0) block_nodes(nxt, nn0, nn1);
     }
     if (nxt >= 0) {
       ne0 = a.seg_ptr[nn0];
       ne1 = a.seg_ptr[nn1];
     }
-#if RG_CONV_PFX
-    {
-      const uint16_t* px = a.x + (size_t)min(nn0 + r, a.n_nodes - 1) * a.ldx + 8 * h;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) bxn[s] = ld_bf8(px + 16 * s);
-    }
-#endif
 
     // The next tile's rows and the tile after's indices are loaded UNCONDITIONALLY
     // (clamped to the block's last edge: past the end every lane reads one row): a load
@@ -560,15 +446,15 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     if (e0 < e1) {
       for (int t0 = e0;;) {
         const int slotA = iA.di - n0;
-        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iB, bB);
+        load_rows(t0 + 32, iB, bB);
         iA = load_idx(t0 + 64);
         compute(bA, slotA, t0);
         t0 += 32;
         if (t0 >= e1) break;
         const int slotB = iB.di - n0;
-        if (RG_CONV_EXP != 1) load_rows(t0 + 32, iA, bA);
+        load_rows(t0 + 32, iA, bA);
         iB = load_idx(t0 + 64);
-        compute(RG_CONV_EXP != 1 ? bB : bA, slotB, t0);
+        compute(bB, slotB, t0);
         t0 += 32;
         if (t0 >= e1) break;
       }
@@ -671,19 +557,14 @@ __device__ __forceinline__ int block_cap(const int* seg_ptr, int n_nodes, int ca
 }
 
 // the static schedule's per-node cost in edge units (the block head (P) and update of an
-// NB-node block, per node; RG_CONV_NODE_COST overrides it for measurement)
+// NB-node block, per node)
 static constexpr int WAVE_NODE_COST = 4;
-// percent of the cost left to the dynamic tail (fused_conv_kernel's tail_next)
-#ifndef RG_CONV_TAIL
-#define RG_CONV_TAIL 0
-#endif
 __global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_nodes, int n_waves,
                                        int node_cost, int* __restrict__ wave_nodes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n_waves) return;
-  // first node n with cost(n) = seg_ptr[n] + node_cost n >= (static total) i / n_waves; the
-  // static ranges cover (100 - RG_CONV_TAIL) % of the cost, wave_nodes[n_waves] = the tail start
-  const long total = ((long)seg_ptr[n_nodes] + (long)node_cost * n_nodes) * (100 - RG_CONV_TAIL) / 100;
+  // first node n with cost(n) = seg_ptr[n] + node_cost n >= total i / n_waves
+  const long total = (long)seg_ptr[n_nodes] + (long)node_cost * n_nodes;
   const long target = total * i / n_waves;
   int lo = 0, hi = n_nodes;
   while (lo < hi) {
@@ -691,7 +572,7 @@ __global__ void conv_wave_nodes_kernel(const int* __restrict__ seg_ptr, int n_no
     if ((long)seg_ptr[mid] + (long)node_cost * mid < target) lo = mid + 1;
     else hi = mid;
   }
-  wave_nodes[i] = (i == n_waves && RG_CONV_TAIL == 0) ? n_nodes : lo;
+  wave_nodes[i] = i == n_waves ? n_nodes : lo;
 }
 
 template <bool EMIT>
