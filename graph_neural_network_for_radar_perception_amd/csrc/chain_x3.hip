@@ -179,8 +179,9 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
 #define RG_X3_INPF 1  // encoders: the next tile's input rows loaded during this tile's last layer
 #endif
 #ifndef RG_X3_SKEW
-#define RG_X3_SKEW 0  // row tile 1's epilogue issued under row tile 0's first k-step of the next
-                      // layer (layer_x3's pre1) when a wave holds two row tiles
+#define RG_X3_SKEW 1  // row tile 1's epilogue issued under row tile 0's first k-step of the next
+                      // layer (layer_x3's pre1) when a wave holds two row tiles (M edge encoder
+                      // 1.362 -> 1.347 ms, three interleaved rounds, profiles/r05_enc_skew_ab.log)
 #endif
 
 #ifndef RG_X3_JIT

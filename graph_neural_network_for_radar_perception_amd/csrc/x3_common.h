@@ -52,30 +52,17 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 #ifndef RG_X3_PIPE
 #define RG_X3_PIPE 1  // layer_x3 computes the B operand of k-step s + 1 beside step s's MFMAs
 #endif
-#ifndef RG_X3_SGB
-#define RG_X3_SGB 0  // n > 0: (1 MFMA, n VALU) sched groups per k-step (M encoder 1.38 -> 1.41-1.44 ms: off)
-#endif
 #ifndef RG_X3_LASTSB
 #define RG_X3_LASTSB 0  // 0: no fence after the last k-step (M edge encoder 1.41 -> 1.38 ms, conv flat)
 #endif
-#ifndef RG_X3_PKNORM
-#define RG_X3_PKNORM 0  // 1: row statistics and scale in v_pk_fma_f32 (M: no gain, conv 1% slower)
-#endif
 #ifndef RG_X3_SPLIT
-#define RG_X3_SPLIT 0  // split8: 0 pair by pair, 4 builtin conversions (no asm: no s_nop pads; conv_x3.hip), 3 stage by stage (no s_nop pads; measured flat),
-                       // 1 f32x2 residues (compiler), 2 forced v_pk_add_f32 residues
+#define RG_X3_SPLIT 0  // split8: 0 pair by pair through the inline-asm conversion (the chains),
+                       // 4 builtin conversions (no asm: no s_nop pads; conv_x3.hip)
 #endif
 
 // the two f32 values of a packed bf16 pair
 __device__ __forceinline__ f32x2 unpk(uint32_t u) {
   return (f32x2){__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
-}
-// a - b on a register pair as ONE v_pk_add_f32 (the compiler otherwise keeps the
-// residues of split8 scalar: two v_add_f32 per pair)
-__device__ __forceinline__ f32x2 sub_pk(f32x2 a, f32x2 b) {
-  f32x2 r;
-  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-  return r;
 }
 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
@@ -107,52 +94,20 @@ __device__ __forceinline__ X3 split8(const f32x4 lo, const f32x4 hi) {
     w1[i] = u1;
     w2[i] = cvt_pk_bf16_c(rx - u1f.x, ry - u1f.y);
   }
-#endif
+#else
+  // the inline-asm conversion, scalar residues
 #pragma unroll
-  for (int i = 0; i < 4 && RG_X3_SPLIT != 3 && RG_X3_SPLIT != 4; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const uint32_t u0 = cvt_pk_bf16(v[i].x, v[i].y);
-#if RG_X3_SPLIT == 2
-    const f32x2 r = sub_pk(v[i], unpk(u0));
-    const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
-    const f32x2 t = sub_pk(r, unpk(u1));
-#elif RG_X3_SPLIT == 1
-    const f32x2 r = add2(v[i], -unpk(u0));
-    const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
-    const f32x2 t = add2(r, -unpk(u1));
-#elif RG_X3_SPLIT == 0
     const f32x2 u0f = unpk(u0);
     const f32x2 r = {v[i].x - u0f.x, v[i].y - u0f.y};
     const uint32_t u1 = cvt_pk_bf16(r.x, r.y);
     const f32x2 u1f = unpk(u1);
     const f32x2 t = {r.x - u1f.x, r.y - u1f.y};
-#endif
-#if RG_X3_SPLIT != 3 && RG_X3_SPLIT != 4
     w0[i] = u0;
     w1[i] = u1;
     w2[i] = cvt_pk_bf16(t.x, t.y);
-#endif
   }
-#if RG_X3_SPLIT == 3
-  // stage by stage over the four pairs: every read of a conversion result is three
-  // instructions after it (right after an inline-asm conversion the compiler pads an
-  // s_nop: 43 per conv tile)
-  f32x2 r[4], t[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w0[i] = cvt_pk_bf16(v[i].x, v[i].y);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x2 u = unpk(w0[i]);
-    r[i] = (f32x2){v[i].x - u.x, v[i].y - u.y};
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w1[i] = cvt_pk_bf16(r[i].x, r[i].y);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x2 u = unpk(w1[i]);
-    t[i] = (f32x2){r[i].x - u.x, r[i].y - u.y};
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w2[i] = cvt_pk_bf16(t[i].x, t[i].y);
 #endif
   return X3{__builtin_bit_cast(bf16x8_t, w0), __builtin_bit_cast(bf16x8_t, w1),
             __builtin_bit_cast(bf16x8_t, w2)};
@@ -285,29 +240,6 @@ __device__ __forceinline__ void layer_x3(f32x16 (&acc)[RT][MT], const WSrc& W, i
         for (int t = 0; t < RT; ++t) bq[t] = bn[t];
       }
     }
-#if RG_X3_SGB
-    // RG_X3_SGB = n: ask the scheduler for the pattern (1 MFMA, n VALU) over the step
-#pragma unroll
-    for (int i = 0; i < 6 * MT * RT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, RG_X3_SGB, 0);
-    }
-#endif
-#ifndef RG_X3_SKEW_SGB
-#define RG_X3_SKEW_SGB 0  // > 0: (1 MFMA, n VALU) sched groups over pre1's k-step region (n = 3, 6, 10 left larger gaps)
-#endif
-    if constexpr (LAZY && RG_X3_SKEW_SGB > 0) {
-      // the region from the previous layer's last k-step to here holds both tiles' epilogues:
-      // ask the scheduler to spread their VALU between the MFMAs (in-order issue: VALU after an
-      // MFMA run in program order cannot use the pipe's shadow)
-      if (s == 0) {
-#pragma unroll
-        for (int i = 0; i < 12 * MT * RT; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, RG_X3_SKEW_SGB, 0);
-        }
-      }
-    }
     // RG_X3_LASTSB 0: no fence after the last k-step, so the caller's epilogue of row tile 0
     // may interleave with the last MFMAs of the other row tiles
     if (RG_X3_LASTSB || s + 1 < KS) __builtin_amdgcn_sched_barrier(0);
@@ -384,7 +316,6 @@ __device__ __forceinline__ float row_inv_std(f32x16 (&acc)[MT]) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[m][q] -= mean;
   }
-#if !RG_X3_PKNORM
   float u[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) u[i] = acc[0][i] * acc[0][i];
@@ -395,20 +326,6 @@ __device__ __forceinline__ float row_inv_std(f32x16 (&acc)[MT]) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) u[q & 7] = fmaf(acc[m][q], acc[m][q], u[q & 7]);
   const float ss = add_xor32(((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7])));
-#else
-  // sum of squares in four packed partial sums (v_pk_fma_f32: two features per instruction)
-  f32x2 v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = mul2(pair(acc[0], i), pair(acc[0], i));
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = fma2(pair(acc[0], i + 4), pair(acc[0], i + 4), v[i]);
-#pragma unroll
-  for (int m = 1; m < MT; ++m)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i & 3] = fma2(pair(acc[m], i), pair(acc[m], i), v[i & 3]);
-  const f32x2 w = add2(add2(v[0], v[1]), add2(v[2], v[3]));
-  const float ss = add_xor32(w.x + w.y);
-#endif
   return __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(ss * (1.f / (float)(N - 1))) + X3_NORM_EPS);
 }
 
@@ -419,16 +336,11 @@ template <int MT, bool CENT = false>
 __device__ __forceinline__ void norm_leaky(f32x16 (&acc)[MT], float mu, float sd) {
   const float inv = row_inv_std<MT, CENT>(acc);  // acc now centred
   const float ga = X3_LEAKY_PRE * (sd * inv), gb = X3_LEAKY_PRE * mu;
-  const f32x2 ga2 = {ga, ga}, gb2 = {gb, gb};
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-#if RG_X3_PKNORM
-      const f32x2 y = fma2(pair(acc[m], i), ga2, gb2);
-#else
       const f32x2 y = {fmaf(acc[m][2 * i], ga, gb), fmaf(acc[m][2 * i + 1], ga, gb)};
-#endif
       set_pair(acc[m], i, (f32x2){fmaf(fabsf(y.x), X3_LEAKY_C, y.x), fmaf(fabsf(y.y), X3_LEAKY_C, y.y)});
     }
 }
