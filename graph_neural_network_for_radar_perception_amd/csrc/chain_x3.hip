@@ -338,26 +338,6 @@ __device__ __forceinline__ void run_pre(const Args& a, const char* lds, const fl
   run_rest<S, SPEC, LM, 1, RT, MT, pend_kind<SPEC, 0>()>(a, acc, pn, lds, nrm, row0, rows, lane);
 }
 
-#ifndef RG_X3_FUSED_LASTSB
-#define RG_X3_FUSED_LASTSB 0  // (M edge encoder -0.7 %, interleaved A/B r03h_ab_fusedsb)
-#endif
-#ifndef RG_X3_L0PIPE
-#define RG_X3_L0PIPE 0  // encoders: layer 0 of tile m0 + 1 pipelined under tile m0's layer 1
-#endif
-#ifndef RG_X3_K0SLOT
-#define RG_X3_K0SLOT 0  // encoders' layer 0 (<= 8 inputs) as 3 MFMAs instead of 6 (slot packing)
-#endif
-// Layer 0 of <= 8 inputs fills only half of a 16-deep k-step, so the six products of the
-// x3 form fit three MFMAs when the lane halves carry different terms: lanes h = 0 hold
-// (w_p, b_0) and lanes h = 1 (w_q, b_r) for k = 0..7 of the same row, with
-// (p | q, r) = (0 | 0, 1), (1 | 0, 2), (2 | 1, 1): a0 b0 + a0 b1, a1 b0 + a0 b2, a2 b0 + a1 b1.
-// A: plane P0[f] (h = 0) / P1[f] (h = 1) of the x3 image's k = 0..7 half (lane & 31 of the
-// fragment); B: the row's split, plane 0 (h = 0) / Q1[f] (h = 1).
-__device__ __forceinline__ bf16x8_t k0slot_b(const X3& x, int f, int h) {
-  const bf16x8_t hi = f == 1 ? x.p2 : x.p1;
-  return h ? hi : x.p0;
-}
-
 // encoders: layer 0 (one k-step of <= 8 inputs, no normalisation) fused tile by tile into
 // layer 1: tile m0 of layer 0 is layer 1's k-steps 2 m0 and 2 m0 + 1
 template <typename S, int SPEC, int LM, int RT, typename Pre = NoHook>
@@ -390,74 +370,6 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
   // edge encoder 12 % slower)
   bf16x8_t A1[2][2][MT1][3];
   lda1(0, A1[0]);
-#if RG_X3_L0PIPE
-  // software pipeline over the layer-0 tiles: tile m0 + 1's layer-0 MFMAs issue ahead of tile
-  // m0's layer-1 MFMAs, and its activation + first split among them, so the layer-1 MFMAs
-  // never wait for a layer-0 result (same products, same order per accumulator).  Layer 1's
-  // A fragments as a ring over the (tile, half) k-steps: the current and the next one
-  auto lda1h = [&](int k, bf16x8_t (&d)[MT1][3]) {  // k = 2 m0 + hf
-#pragma unroll
-    for (int m = 0; m < MT1; ++m)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) d[m][p] = W1(p, (m * KS1 + k) * 1024);
-  };
-  auto l0 = [&](int m0, f32x16 (&y)[RT][1]) {
-#pragma unroll
-    for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
-    layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
-  };
-  auto actsplit = [&](f32x16 (&y)[RT][1], X3 (&b)[RT]) {
-    if constexpr (sp_act(SPEC, 0)) {
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) y[t][0][q] = act_t<ACT_LEAKY>(y[t][0][q]);
-    }
-#pragma unroll
-    for (int t = 0; t < RT; ++t) b[t] = split_acc(y[t][0], 0);
-  };
-  bf16x8_t Ak[2][MT1][3];
-  lda1h(0, Ak[0]);
-  f32x16 yn[RT][1];
-  X3 bn[RT];
-  l0(0, yn);
-  actsplit(yn, bn);
-#pragma unroll
-  for (int m0 = 0; m0 < MT0; ++m0) {
-    f32x16 y[RT][1];
-    X3 bh[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      y[t][0] = yn[t][0];
-      bh[t] = bn[t];
-    }
-    if (m0 + 1 < MT0) l0(m0 + 1, yn);
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const int k = 2 * m0 + hf;
-      if (k + 1 < 2 * MT0) lda1h(k + 1, Ak[(k + 1) & 1]);
-      const bf16x8_t(&A)[MT1][3] = Ak[k & 1];
-#pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        const X3 b = hf == 0 ? bh[t] : split_acc(y[t][0], 1);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][2], b.p0, acc[t][m]);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][1], b.p1, acc[t][m]);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p2, acc[t][m]);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][1], b.p0, acc[t][m]);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p1, acc[t][m]);
-#pragma unroll
-        for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
-      }
-      if (hf == 1 && m0 + 1 < MT0) actsplit(yn, bn);
-      if (RG_X3_FUSED_LASTSB || k + 1 < 2 * MT0) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#else
 #pragma unroll
   for (int m0 = 0; m0 < MT0; ++m0) {
     const int u = m0 & 1;
@@ -465,24 +377,7 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
     f32x16 y[RT][1];
 #pragma unroll
     for (int t = 0; t < RT; ++t) y[t][0] = ld_bias_frag(bias0, m0, h);
-    if constexpr (RG_X3_K0SLOT) {
-      static_assert(lmask(LM, 0) == 7, "slot layer 0 reads every plane from LDS");
-      const char* w0l = lds + S::woff(LM, 0) + m0 * 1024 + (lane & 31) * 16;
-      bf16x8_t A0[3];
-#pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        const int pl = h ? (f == 2 ? 1 : 0) : f;
-        A0[f] = ld_bf8(w0l + pl * S::pl(0));
-      }
-#pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        y[t][0] = mf(A0[2], k0slot_b(b0[t][0], 2, h), y[t][0]);
-        y[t][0] = mf(A0[1], k0slot_b(b0[t][0], 1, h), y[t][0]);
-        y[t][0] = mf(A0[0], k0slot_b(b0[t][0], 0, h), y[t][0]);
-      }
-    } else {
-      layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
-    }
+    layer_x3<1, 1, MT0, RT>(y, W0, m0, [&](int, int t) { return b0[t][0]; });
     if constexpr (sp_act(SPEC, 0)) {
 #pragma unroll
       for (int t = 0; t < RT; ++t)
@@ -510,11 +405,10 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
         for (int m = 0; m < MT1; ++m) acc[t][m] = mf(A[m][0], b.p0, acc[t][m]);
       }
     }
-    // (the last tile unfenced with RG_X3_LASTSB=0, as layer_x3: layer 1's epilogue of row
-    // tile 0 may interleave with tile 1's last MFMAs)
-    if (RG_X3_FUSED_LASTSB || m0 + 1 < MT0) __builtin_amdgcn_sched_barrier(0);
+    // (the last tile unfenced, as layer_x3: layer 1's epilogue of row tile 0 may interleave
+    // with tile 1's last MFMAs)
+    if (m0 + 1 < MT0) __builtin_amdgcn_sched_barrier(0);
   }
-#endif
   if constexpr (S::NL > 2) {
     Pend pn[RT];
     epilogue_next<SPEC, 1, MT1, RT>(acc, nrm, pn);
@@ -577,7 +471,7 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
       const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        vin[t][j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
+        vin[t][j] = (ok && h == 0 && j < a.w0real) ? p[j] : 0.f;
     }
   };
   if constexpr (MODE == IN_SMALL && RG_X3_INPF) {
@@ -602,8 +496,7 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
         } else {
           const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
 #pragma unroll
-          // both lane halves hold the row with RG_X3_K0SLOT (each carries other split terms)
-          for (int j = 0; j < 8; ++j) v[j] = (ok && (RG_X3_K0SLOT || h == 0) && j < a.w0real) ? p[j] : 0.f;
+          for (int j = 0; j < 8; ++j) v[j] = (ok && h == 0 && j < a.w0real) ? p[j] : 0.f;
         }
         b0[t][0] = split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]});
       } else if constexpr (MODE == IN_DENSE) {
