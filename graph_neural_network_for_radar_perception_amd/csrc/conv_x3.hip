@@ -769,18 +769,31 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   // in-order running sums (lane = feature): rv[j] = the sum after edge j, a set mask bit
   // restarting it (the reference scatter_add_ order of a destination-major CSR); edges
   // [j0, j1) continuing from prev
-  auto scan_part = [&](int j0, int j1, const float (&cv)[32], uint32_t mask, float& prev, f32x32& rv) {
+  // the scan's factor for edge j: keep = 0 at a set mask bit, else 1 -- formed in scalar
+  // registers from the wave-uniform mask (bit j of ~mask times the bits of 1.0f), a scalar
+  // operand of the scan's fma (compiled from C the select is materialised per lane: one more
+  // VALU per edge), and a sub-chunk ahead of its use (a VALU read right behind an inline-asm
+  // result costs an s_nop)
+  auto keeps = [&](int j0, int j1, uint32_t mask, uint32_t (&kb)[32]) {
+#pragma unroll
+    for (int j = j0; j < j1; ++j)
+      asm("s_bfe_u32 %0, %1, %2\n\ts_mul_i32 %0, %0, 0x3f800000"
+          : "=s"(kb[j]) : "s"(~mask), "i"(j | (1 << 16)));
+  };
+  auto scan_part = [&](int j0, int j1, const float (&cv)[32], const uint32_t (&kb)[32],
+                       float& prev, f32x32& rv) {
 #pragma unroll
     for (int j = j0; j < j1; ++j) {
       // prev * keep + v: exactly v at a set bit (keep = 0), prev + v otherwise (keep = 1)
-      const float keep = ((mask >> j) & 1u) ? 0.f : 1.f;
-      prev = fmaf(prev, keep, cv[j]);
+      prev = fmaf(prev, __uint_as_float(kb[j]), cv[j]);
       rv[j] = prev;
     }
   };
   auto scan = [&](const float (&cv)[32], uint32_t mask, float run_in, f32x32& rv) {
     float prev = run_in;
-    scan_part(0, 32, cv, mask, prev, rv);
+    uint32_t kb[32];
+    keeps(0, 32, mask, kb);
+    scan_part(0, 32, cv, kb, prev, rv);
   };
   // the norm 2 scale + LeakyReLU of one message tile
   auto norm2_apply = [&](f32x16& m2, Pend pn, int i0, int i1) {
@@ -936,24 +949,27 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     wait_frags<4>(A1[0]);
     lda1<3>(aw, A1[1]);
     b1n = split8(ev[6], ev[7]);
+    uint32_t kb[32];
+    keeps(0, 16, mask_p, kb);
     x3_prod<0>(acc1, A1[0], b1);
     interleave<4, 3>();
     fence();
     const float run_in = run;
     float prev = run_in;
-    scan_part(0, 8, cv, mask_p, prev, rv);
+    keeps(16, 32, mask_p, kb);
+    scan_part(0, 8, cv, kb, prev, rv);
     x3_prod<1>(acc1, A1[0], b1);
     interleave<4, 2>();
     fence();
-    scan_part(8, 16, cv, mask_p, prev, rv);
+    scan_part(8, 16, cv, kb, prev, rv);
     x3_prod<2>(acc1, A1[0], b1);
     interleave<4, 2>();
     fence();
-    scan_part(16, 24, cv, mask_p, prev, rv);
+    scan_part(16, 24, cv, kb, prev, rv);
     x3_prod<3>(acc1, A1[0], b1);
     interleave<4, 2>();
     fence();
-    scan_part(24, 32, cv, mask_p, prev, rv);
+    scan_part(24, 32, cv, kb, prev, rv);
     x3_prod<4>(acc1, A1[0], b1);
     interleave<4, 2>();
     fence();
@@ -1031,13 +1047,21 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     //          operand
     X3 b2 = split_acc_pend<1>(acc1[0], 0, pn1);
     X3 b2n;
+    // the next k-step's fragment reads right behind the chunk's first product (two MFMAs):
+    // issued later in the chunk they are still in flight at the next chunk's wait
 #define RG_SP_C(S, BUFI, NEXT, EXTRA)                                  \
     wait_frags<2>(A2[BUFI]);                                           \
+    x3_prod<0>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
     lda2<S + 1>(aw2, A2[BUFI ^ 1]);                                     \
+    fence();                                                           \
     NEXT = split_acc_pend<1>(acc1[(S + 1) >> 1], (S + 1) & 1, pn1);    \
     EXTRA;                                                             \
-    x3_step<2, false>(acc2, A2[BUFI], S % 2 ? b2n : b2);               \
-    interleave<12, 5>();                                               \
+    x3_prod<1>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
+    x3_prod<2>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
+    x3_prod<3>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
+    x3_prod<4>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
+    x3_prod<5>(acc2, A2[BUFI], S % 2 ? b2n : b2);                      \
+    interleave<10, 6>();                                               \
     fence();
     RG_SP_C(0, 0, b2n, (void)0)
     RG_SP_C(1, 1, b2, (void)0)
@@ -1049,9 +1073,15 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #undef RG_SP_C
     SP_STAMP(3);  // C0 - C6
     wait_frags<2>(A2[1]);
+    x3_prod<0>(acc2, A2[1], b2n);
     lda1<0>(aw, A1[0]);  // the next tile's first layer-1 fragments
+    fence();
     b1 = split8(en[0], en[1]);
-    x3_step<2, false>(acc2, A2[1], b2n);
+    x3_prod<1>(acc2, A2[1], b2n);
+    x3_prod<2>(acc2, A2[1], b2n);
+    x3_prod<3>(acc2, A2[1], b2n);
+    x3_prod<4>(acc2, A2[1], b2n);
+    x3_prod<5>(acc2, A2[1], b2n);
     ring_p(d_nn, 1, pr);
     const uint32_t mask_n = tile_mask(t + 1, d_nn, dl_c);
     interleave<12, 2>();
