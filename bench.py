@@ -48,9 +48,10 @@ MFMA_PEAK_TFLOPS = {'bf16': 2500.0, 'fp16': 2500.0, 'fp32': 157.3}   # dense MFM
 # workloads; k is unused by the pure radius graph
 PRESETS = {
     # the metric's configuration (BASELINE.json metric "N~3k nodes, E~30k edges"; yml k = 10,
-    # L = 7, configuration_radarscenes_gnn.yml:14,58), fp32, trained weights
+    # L = 7, configuration_radarscenes_gnn.yml:14,58), fp32, trained weights, two batches in
+    # flight (the next step's graph build beside this forward: +2.9 %)
     'm': dict(frames=64, nodes=3000, k=10, layers=7, graph='knn', eps2=25.0, cpu_frames=5,
-              cpu_warm=2, dtype='fp32', weights='trained', streams=1),
+              cpu_warm=2, dtype='fp32', weights='trained', streams=2),
     'c2': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
                cpu_warm=2, dtype='bf16', weights='random', streams=2),
     # BASELINE config 3: 512 frames of C2's shape frame-parallel over 8 GPUs, forward only --
