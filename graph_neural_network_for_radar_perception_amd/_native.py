@@ -99,6 +99,8 @@ _SIGNATURES = {
     # real-data front-end (frontend.hip)
     'rg_frontend_sync': (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P,
                               _P, _P]),
+    'rg_frontend_gate_lists': (_I, [_P, _P, _I, _P, _P, _P]),
+    'rg_frontend_ransac': (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _D, _I, _D, _P, _P, _P, _P]),
     'rg_frontend_labels_workspace_size': (_S, [_I]),
     'rg_frontend_labels': (_I, [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _S, _P]),
     'rg_frontend_select_workspace_size': (_S, [_I]),

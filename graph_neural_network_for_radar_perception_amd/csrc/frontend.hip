@@ -158,9 +158,176 @@ __global__ void frontend_frame_ptr_kernel(const int* __restrict__ pos,
   if (w <= n_windows) frame_ptr[w] = pos[win_ptr[w]];
 }
 
+// ---- RANSAC stationary-measurement rejection (meas_selection.py:96-166, applied per scan to
+// the gated measurements by identify_stationary_measurements, :188-199)
+//
+// The gated measurements of each scan, in order: one workgroup per scan, 256 at a time,
+// positions from the waves' ballots.  gated_idx holds measurement indices at the scan's own
+// offset scan_ptr[s]; gated_cnt[s] their count.
+__global__ __launch_bounds__(256) void frontend_gate_lists_kernel(
+    const uint8_t* __restrict__ stationary, const int* __restrict__ scan_ptr,
+    int* __restrict__ gated_idx, int* __restrict__ gated_cnt) {
+  __shared__ int wsum[4];
+  const int s = blockIdx.x, a = scan_ptr[s], b = scan_ptr[s + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int base = 0;
+  for (int c = a; c < b; c += 256) {
+    const int i = c + threadIdx.x;
+    const bool g = i < b && stationary[i];
+    const uint64_t m = __ballot(g);
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    if (g) gated_idx[a + off + __popcll(m & ((1ull << lane) - 1ull))] = i;
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gated_cnt[s] = base;
+}
+
+// The least-squares sensor velocity of a consensus set (meas_selection.py:72-93): normal
+// equations summed in float64 over float32 cos / sin (numpy's float32 scalars: c ** 2,
+// sin(2 t), c * vr, s * vr in float32), then inv(A) @ b.  numpy's float32 cos / sin (and its
+// scalar c ** 2 in ~0.1 % of cases) are not correctly rounded and differ from cosf / sinf in
+// the last place for some inputs, so a fit can differ from numpy's by ~1e-7 relative: an
+// inlier decision then moves only for an error within ~1e-6 of the margin
+__device__ void ransac_fit(const float* __restrict__ az, const float* __restrict__ vr,
+                           const int* __restrict__ gi, const int* __restrict__ set, int k,
+                           double& vx, double& vy) {
+  double a00 = 0.0, a01 = 0.0, b0 = 0.0, b1 = 0.0;
+  for (int j = 0; j < k; ++j) {
+    const int m = gi[set[j]];
+    const float t = az[m], v = vr[m];
+    const float c = cosf(t), sn = sinf(t), s2 = sinf(2.f * t);
+    a00 += (double)(c * c);
+    a01 += (double)s2;
+    b0 -= (double)(c * v);
+    b1 -= (double)(sn * v);
+  }
+  a01 = 0.5 * a01;
+  const double a10 = a01, a11 = (double)k - a00;
+  // np.linalg.inv = LAPACK gesv against the identity: getrf (row pivot on |a10| > |a00|, the
+  // multiplier scaled by the pivot's reciprocal), getrs (L, then U: y0 - u01 x1 in one fused
+  // step, times the reciprocal); then numpy's matmul x_i = fma(inv_i0, b0, inv_i1 b1) --
+  // bit-identical to numpy on this image's OpenBLAS for the fits of two samples
+  const bool piv = fabs(a10) > fabs(a00);
+  const double u00 = piv ? a10 : a00, u01 = piv ? a11 : a01;
+  const double q0 = piv ? a00 : a10, q1 = piv ? a01 : a11;
+  const double r0 = 1.0 / u00, l = q0 * r0, u11 = q1 - l * u01, r1 = 1.0 / u11;
+  const double xa1 = (-l) * r1, xa0 = fma(-u01, xa1, 1.0) * r0;  // right-hand side (1, 0) / P
+  const double xb1 = r1, xb0 = (-u01 * r1) * r0;                  // (0, 1) / P
+  const double i00 = piv ? xb0 : xa0, i10 = piv ? xb1 : xa1;
+  const double i01 = piv ? xa0 : xb0, i11 = piv ? xa1 : xb1;
+  vx = fma(i00, b0, i01 * b1);
+  vy = fma(i10, b0, i11 * b1);
+}
+
+__device__ __forceinline__ bool ransac_inlier(float t, float v, double vx, double vy,
+                                              double margin) {
+  const double pred = -(vx * (double)cosf(t) + vy * (double)sinf(t));
+  return fabs((double)v - pred) <= margin;
+}
+
+// One workgroup per scan: every consensus set's fit and its inlier count over the test set
+// (all gated measurements but the set's own), the first best, then the flags of the gated
+// measurements from that fit.  Scans with <= min_meas gated measurements: no inliers.
+constexpr int RANSAC_MAX_ITERS = 256;
+__global__ __launch_bounds__(256) void frontend_ransac_kernel(
+    const float* __restrict__ az, const float* __restrict__ vr, const int* __restrict__ scan_ptr,
+    const int* __restrict__ gated_idx, const int* __restrict__ gated_cnt,
+    const int* __restrict__ sets, int n_iter, int k, double margin, int min_meas,
+    double ratio_thresh, uint8_t* __restrict__ stationary, double* __restrict__ in_ratio,
+    uint8_t* __restrict__ is_valid) {
+  __shared__ int cnt_it[RANSAC_MAX_ITERS];
+  __shared__ int part[4];
+  __shared__ double best_v[2];
+  const int s = blockIdx.x, a = scan_ptr[s], n = gated_cnt[s];
+  const int* gi = gated_idx + a;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (n <= min_meas) {
+    for (int j = threadIdx.x; j < n; j += 256) stationary[gi[j]] = 0;
+    if (threadIdx.x == 0) {
+      in_ratio[s] = 0.0;
+      is_valid[s] = 0;
+    }
+    return;
+  }
+  for (int it = 0; it < n_iter; ++it) {
+    const int* set = sets + ((size_t)s * n_iter + it) * k;
+    double vx, vy;
+    ransac_fit(az, vr, gi, set, k, vx, vy);
+    int c = 0;
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const int m = gi[j];
+      c += ransac_inlier(az[m], vr[m], vx, vy, margin) ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) part[wave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = part[0] + part[1] + part[2] + part[3];
+      for (int j = 0; j < k; ++j) {  // the consensus set is not in the test set
+        const int m = gi[set[j]];
+        tot -= ransac_inlier(az[m], vr[m], vx, vy, margin) ? 1 : 0;
+      }
+      cnt_it[it] = tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int it = 1; it < n_iter; ++it)
+      if (cnt_it[it] > cnt_it[best]) best = it;  // np.argmax: the first maximum
+    double vx, vy;
+    ransac_fit(az, vr, gi, sets + ((size_t)s * n_iter + best) * k, k, vx, vy);
+    best_v[0] = vx;
+    best_v[1] = vy;
+    const double r = ((double)cnt_it[best] + (double)k) / (double)n;
+    in_ratio[s] = r;
+    is_valid[s] = r >= ratio_thresh ? 1 : 0;
+  }
+  __syncthreads();
+  const double vx = best_v[0], vy = best_v[1];
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const int m = gi[j];
+    stationary[m] = ransac_inlier(az[m], vr[m], vx, vy, margin) ? 1 : 0;
+  }
+}
+
 }  // namespace rg
 
 using namespace rg;
+
+extern "C" int rg_frontend_gate_lists(const uint8_t* stationary, const int* scan_ptr, int n_scans,
+                                      int* gated_idx, int* gated_cnt, void* stream) {
+  RG_REQUIRE(n_scans >= 1 && stationary && scan_ptr && gated_idx && gated_cnt, RG_ERR_ARG,
+             "rg_frontend_gate_lists: bad argument");
+  frontend_gate_lists_kernel<<<n_scans, 256, 0, (hipStream_t)stream>>>(stationary, scan_ptr,
+                                                                       gated_idx, gated_cnt);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_frontend_ransac(const float* azimuth_sc, const float* vr, const int* scan_ptr,
+                                  int n_scans, const int* gated_idx, const int* gated_cnt,
+                                  const int* consensus_sets, int n_iter, int n_samples,
+                                  double error_margin, int min_num_meas, double ratio_threshold,
+                                  uint8_t* stationary, double* in_ratio, uint8_t* is_valid,
+                                  void* stream) {
+  RG_REQUIRE(n_scans >= 1 && n_iter >= 1 && n_iter <= RANSAC_MAX_ITERS && n_samples >= 1 &&
+                 n_samples <= min_num_meas + 1,
+             RG_ERR_ARG, "rg_frontend_ransac: n_iter %d (<= %d), n_samples %d", n_iter,
+             RANSAC_MAX_ITERS, n_samples);
+  RG_REQUIRE(azimuth_sc && vr && scan_ptr && gated_idx && gated_cnt && consensus_sets &&
+                 stationary && in_ratio && is_valid,
+             RG_ERR_ARG, "rg_frontend_ransac: null argument");
+  frontend_ransac_kernel<<<n_scans, 256, 0, (hipStream_t)stream>>>(
+      azimuth_sc, vr, scan_ptr, gated_idx, gated_cnt, consensus_sets, n_iter, n_samples,
+      error_margin, min_num_meas, ratio_threshold, stationary, in_ratio, is_valid);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
 
 extern "C" int rg_frontend_sync(const float* x_cc, const float* y_cc, const float* azimuth_sc,
                                 const float* vr, const float* vr_compensated,

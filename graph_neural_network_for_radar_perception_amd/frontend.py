@@ -10,10 +10,12 @@ host), the reference sequence
   graph_features.select_moving_data                       (graph_features.py:167-182)
 
 as three native launches (``rg_frontend_sync``, ``rg_frontend_labels``,
-``rg_frontend_select``, csrc/frontend.hip) plus one gather of the selected rows.  The
-stationary gate runs without RANSAC (configuration_radarscenes_gnn.yml:11 turns it off;
-its np.random.shuffle consensus sets are not reproducible by any other implementation),
-so ``reject_outlier_by_ransac=True`` raises.
+``rg_frontend_select``, csrc/frontend.hip) plus one gather of the selected rows.  With
+``reject_outlier_by_ransac=True`` (off in configuration_radarscenes_gnn.yml:11) the gate is
+followed by the RANSAC rejection of meas_selection.py:96-166: the host draws the consensus
+sets exactly as the reference does -- ``np.random.shuffle`` on numpy's global generator,
+scans in window order -- and ``rg_frontend_gate_lists`` / ``rg_frontend_ransac`` evaluate
+every set on the device, so a seeded generator reproduces the reference's flags.
 """
 from __future__ import annotations
 
@@ -28,6 +30,8 @@ from .engine import _require_device
 GAMMA_STATIONARY = 1.5            # data_utils/constants.py:15
 LABEL_STATIC = 7                  # labels.py:60-70
 GRID_LIMITS = (0.0, 100.0, -50.0, 50.0)   # configuration_radarscenes_gnn.yml:34-38
+RANSAC_MIN_SAMPLES, RANSAC_MARGIN, RANSAC_ITERS = 2, 0.25, 30   # data_utils/constants.py:8-10
+RANSAC_RATIO, RANSAC_MIN_MEAS = 0.6, 10                         # constants.py:11-12
 # labels.py:90-100: old label ids 0..11 -> new ids
 OLD_TO_NEW = np.array([0, 4, 4, 4, 4, 3, 3, 1, 2, 5, 5, 7], dtype=np.int32)
 
@@ -116,10 +120,6 @@ def extract_and_sync_radar_data(w: ScanWindow, reject_outlier_by_ransac: bool = 
     compensated into the last scan's frame), meas_vx / vy (vr_cartesian_vf), meas_vr
     (vr_compensated), meas_rcs, meas_timestamp, meas_sensorid, meas_label_id,
     stationary_meas_flag (bool)."""
-    if reject_outlier_by_ransac:
-        raise NotImplementedError('RANSAC outlier rejection (meas_selection.py:96-166) draws '
-                                  'np.random.shuffle consensus sets; the shipped configuration '
-                                  'turns it off (configuration_radarscenes_gnn.yml:11)')
     a = w.arrays
     _require_device(a['x_cc'], 'x_cc')
     dev = a['x_cc'].device
@@ -134,12 +134,53 @@ def extract_and_sync_radar_data(w: ScanWindow, reject_outlier_by_ransac: bool = 
         px.data_ptr(),
         py.data_ptr(), vx.data_ptr(), vy.data_ptr(), st.data_ptr(), nat.stream_ptr(dev)),
         'rg_frontend_sync')
+    ransac = _ransac(w, st) if reject_outlier_by_ransac and n > 0 else None
     return {'meas_px': px, 'meas_py': py, 'meas_vx': vx, 'meas_vy': vy,
             'meas_vr': a['vr_compensated'], 'meas_rcs': a['rcs'],
             'meas_timestamp': a['timestamp'], 'meas_sensorid': a['sensor_id'],
             'meas_label_id': a['label_id'], 'stationary_meas_flag': st.bool(),
             '_track_key': w.track_key, '_n_tracks': w.n_tracks, '_stationary_u8': st,
-            '_win_ptr': w.win_ptr, '_n_windows': w.n_windows}
+            '_win_ptr': w.win_ptr, '_n_windows': w.n_windows, '_ransac': ransac}
+
+
+def _ransac(w: ScanWindow, st: torch.Tensor):
+    """meas_selection.py:96-166 on every scan's gated measurements (st updated in place):
+    the device lists each scan's gated measurements, the host draws the consensus sets from
+    numpy's global generator in the reference's order (per scan with more than
+    RANSAC_MIN_MEAS gated, RANSAC_ITERS np.random.shuffle passes over arange(gated), the
+    first RANSAC_MIN_SAMPLES of each), the device fits and counts.  Returns the per-scan
+    (in_ratio f64, is_valid bool) device tensors.  Synchronises once (the draws need the
+    gated counts)."""
+    lib = nat.lib()
+    a = w.arrays
+    dev = a['x_cc'].device
+    S = w.n_scans
+    stream = nat.stream_ptr(dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    gidx = torch.empty(max(w.n_meas, 1), **i32)
+    gcnt = torch.empty(S, **i32)
+    nat.check(lib.rg_frontend_gate_lists(st.data_ptr(), w.scan_ptr.data_ptr(), S,
+                                         gidx.data_ptr(), gcnt.data_ptr(), stream),
+              'rg_frontend_gate_lists')
+    counts = gcnt.cpu().numpy()
+    sets = np.zeros((S, RANSAC_ITERS, RANSAC_MIN_SAMPLES), np.int32)
+    for s in range(S):
+        c = int(counts[s])
+        if c <= RANSAC_MIN_MEAS:
+            continue
+        order = np.arange(c)
+        for it in range(RANSAC_ITERS):
+            np.random.shuffle(order)
+            sets[s, it] = order[:RANSAC_MIN_SAMPLES]
+    sets_d = torch.from_numpy(sets).to(dev)
+    ratio = torch.empty(S, dtype=torch.float64, device=dev)
+    valid = torch.empty(S, dtype=torch.uint8, device=dev)
+    nat.check(lib.rg_frontend_ransac(
+        a['azimuth_sc'].data_ptr(), a['vr'].data_ptr(), w.scan_ptr.data_ptr(), S, gidx.data_ptr(),
+        gcnt.data_ptr(), sets_d.data_ptr(), RANSAC_ITERS, RANSAC_MIN_SAMPLES, RANSAC_MARGIN,
+        RANSAC_MIN_MEAS, RANSAC_RATIO, st.data_ptr(), ratio.data_ptr(), valid.data_ptr(), stream),
+        'rg_frontend_ransac')
+    return ratio, valid.bool()
 
 
 def compute_ground_truth(d: dict) -> dict:
@@ -193,9 +234,9 @@ def select_dynamic(d: dict, gt: dict, grid_limits=GRID_LIMITS) -> Tuple[dict, di
     return dd, gd
 
 
-def dynamic_frame(w: ScanWindow) -> Tuple[dict, dict]:
+def dynamic_frame(w: ScanWindow, reject_outlier_by_ransac: bool = False) -> Tuple[dict, dict]:
     """The whole front-end for one window: (data_dict_dyn, node_labels_dict_dyn) of
     datagen_gnn.RadarScenesDataset.__getitem__ (datagen_gnn.py:96-102)."""
-    d = extract_and_sync_radar_data(w)
+    d = extract_and_sync_radar_data(w, reject_outlier_by_ransac)
     gt = compute_ground_truth(d)
     return select_dynamic(d, gt)

@@ -608,8 +608,8 @@ int rg_segment_amax_backward(const float* msg, int ldm, int C, const int* seg_pt
 /* read_data.extract_and_sync_radar_data + extract_frame (read_data.py:227-303, 442-486)
  * for a window of n_scans scans already in device memory (measurements of scan s at
  * [scan_ptr[s], scan_ptr[s+1])): the stationary gate of identify_stationary_measurements
- * (meas_selection.py:22-70, 169-200, |predicted - measured range rate| <= gamma; ransac
- * not supported), vr_cartesian_vf (meas_sync.py:15-20) and the ego compensation into the
+ * (meas_selection.py:22-70, 169-200, |predicted - measured range rate| <= gamma; RANSAC
+ * below), vr_cartesian_vf (meas_sync.py:15-20) and the ego compensation into the
  * window's current scan (meas_sync.py:23-103), float32 outputs.  A batch of windows is
  * one call: scan_ref[s] = the current scan of scan s's window (NULL: one window whose
  * current scan is the last).  mount: f64 [n_scans][3] (x, y, yaw); odometry: f64
@@ -620,6 +620,30 @@ int rg_frontend_sync(const float* x_cc, const float* y_cc, const float* azimuth_
                      const double* odometry,
                      float gamma_stationary, int n_meas, float* px, float* py, float* vx,
                      float* vy, uint8_t* stationary, void* stream);
+/* RANSAC stationary-measurement rejection (meas_selection.py:96-166, applied by
+ * identify_stationary_measurements to each scan's gated measurements, :188-199), in two
+ * calls around the host's random draws (the reference draws np.random.shuffle consensus
+ * sets; the host draws the same from numpy's generator, so a seeded generator reproduces
+ * the reference):
+ *   rg_frontend_gate_lists: gated_idx [n_meas] receives, at each scan's offset scan_ptr[s],
+ *     the indices of the scan's measurements whose stationary flag is set, in order;
+ *     gated_cnt [n_scans] their count.
+ *   rg_frontend_ransac: for each scan with more than min_num_meas gated measurements,
+ *     consensus_sets [n_scans][n_iter][n_samples] (positions 0 .. gated_cnt[s) - 1 in the
+ *     scan's gated list) -> per set the least-squares sensor velocity (:72-93) and its
+ *     inliers (|vr - predicted| <= error_margin) among the other gated measurements; the
+ *     first set with the most inliers then sets the gated measurements' stationary flags
+ *     (float64 arithmetic over float32 cos / sin, as numpy).  Scans with <= min_num_meas
+ *     gated measurements: every flag 0 (the reference's empty inlier set).  in_ratio
+ *     [n_scans] f64 = (inliers + n_samples) / gated (0 when skipped), is_valid [n_scans] u8
+ *     = in_ratio >= ratio_threshold.  n_iter <= 256. */
+int rg_frontend_gate_lists(const uint8_t* stationary, const int* scan_ptr, int n_scans,
+                           int* gated_idx, int* gated_cnt, void* stream);
+int rg_frontend_ransac(const float* azimuth_sc, const float* vr, const int* scan_ptr, int n_scans,
+                       const int* gated_idx, const int* gated_cnt, const int* consensus_sets,
+                       int n_iter, int n_samples, double error_margin, int min_num_meas,
+                       double ratio_threshold, uint8_t* stationary, double* in_ratio,
+                       uint8_t* is_valid, void* stream);
 /* compute_ground_truth (compute_node_labels.py:50-105): class labels (tracked: the
  * old -> new label id map, labels.py:90-100; untracked: FALSE = 6 / STATIC = 7 by the
  * stationary flag) and offsets to each track's mean position (track_key int32, 0 = no

@@ -5,9 +5,10 @@ Only tests/ may import this module; the product path is csrc/frontend.hip.
 A numpy restatement, on a window of scans already in memory (the .h5 reading of
 read_data.py stays out of scope: h5py and the data are absent), of
   read_data.extract_and_sync_radar_data + extract_frame (read_data.py:227-303, 442-486):
-    identify_stationary_measurements, gating only (meas_selection.py:22-70, 169-200;
-    ransac off as configuration_radarscenes_gnn.yml:11 sets -- it draws np.random.shuffle
-    permutations, so no two implementations agree on it),
+    identify_stationary_measurements (meas_selection.py:22-70, 169-200): the gate, and
+    with ransac=True the RANSAC rejection (:72-166) -- its consensus sets are
+    np.random.shuffle draws from numpy's global generator, so a seeded generator makes it
+    reproducible (pinned by tests/golden/make_ransac_golden.py -> ransac_*.npz),
     vr_cartesian_vf (meas_sync.py:15-20),
     ego_compensate_radar_frames_list (meas_sync.py:23-103),
     the concatenation and float32 casts;
@@ -45,6 +46,55 @@ def stationary_flag(az: np.ndarray, vr: np.ndarray, tx: float, ty: float, theta:
     return np.abs(pred - vr) <= GAMMA_STATIONARY
 
 
+RANSAC_MIN_SAMPLES, RANSAC_MARGIN, RANSAC_ITERS = 2, 0.25, 30   # data_utils/constants.py:8-10
+RANSAC_RATIO, RANSAC_MIN_MEAS = 0.6, 10                         # constants.py:11-12
+
+
+def ego_vx_vy(theta: np.ndarray, vr: np.ndarray):
+    """Least-squares sensor velocity from (azimuth, range rate) pairs (meas_selection.py:72-
+    93): normal equations summed in float64 over float32 cos / sin, solved by inversion."""
+    A = np.zeros((2, 2))
+    rhs = np.zeros((2, 1))
+    for t, v in zip(theta, vr):
+        c, sn, s2 = np.cos(t), np.sin(t), np.sin(2 * t)
+        A[0, 0] += c ** 2
+        A[0, 1] += s2
+        rhs[0, 0] -= c * v
+        rhs[1, 0] -= sn * v
+    A[0, 1] *= 0.5
+    A[1, 0] = A[0, 1]
+    A[1, 1] = len(theta) - A[0, 0]
+    sol = np.linalg.inv(A) @ rhs
+    return sol[0, 0], sol[1, 0]
+
+
+def ransac(z: np.ndarray, with_fit: bool = False):
+    """meas_selection.py:96-166 on z = [azimuth, vr] rows (float32): (inlier flags, valid,
+    inlier ratio) -- with_fit: + the chosen (vx, vy) and every row's |vr - predicted| under
+    it.  Draws RANSAC_ITERS np.random.shuffle permutations (global generator) when there are
+    more than RANSAC_MIN_MEAS rows, none otherwise (all flags False)."""
+    n = z.shape[0]
+    if n <= RANSAC_MIN_MEAS:
+        out = (np.zeros(n, dtype=bool), False, 0)
+        return out + (None, None) if with_fit else out
+    order = np.arange(n)
+    fits, counts = [], np.zeros(RANSAC_ITERS)
+    for it in range(RANSAC_ITERS):
+        np.random.shuffle(order)
+        cons, test = z[order[:RANSAC_MIN_SAMPLES]], z[order[RANSAC_MIN_SAMPLES:]]
+        vx, vy = ego_vx_vy(cons[:, 0], cons[:, 1])
+        pred = -(vx * np.cos(test[:, 0]) + vy * np.sin(test[:, 0]))
+        counts[it] = np.sum(np.abs(test[:, 1] - pred) <= RANSAC_MARGIN)
+        fits.append((vx, vy))
+    best = int(np.argmax(counts))
+    vx, vy = fits[best]
+    ratio = (counts[best] + RANSAC_MIN_SAMPLES) / n
+    pred = -(vx * np.cos(z[:, 0]) + vy * np.sin(z[:, 0]))
+    err = np.abs(z[:, 1] - pred)
+    out = (err <= RANSAC_MARGIN, bool(ratio >= RANSAC_RATIO), ratio)
+    return out + ((vx, vy), err) if with_fit else out
+
+
 def se2(x, y, th) -> np.ndarray:
     T = np.eye(3)
     T[:2, :2] = [[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]]
@@ -52,9 +102,9 @@ def se2(x, y, th) -> np.ndarray:
     return T
 
 
-def sync_window(win: dict) -> dict:
+def sync_window(win: dict, reject_outlier_by_ransac: bool = False) -> dict:
     """Per-measurement arrays of extract_frame for a window (synthetic.make_scan_window
-    layout)."""
+    layout); with RANSAC the scans draw from numpy's global generator in window order."""
     ptr = win['scan_ptr']
     W = int(win['n_scans'])
     mount, odo = win['mount'], win['odometry']
@@ -65,8 +115,12 @@ def sync_window(win: dict) -> dict:
         a, b = int(ptr[s]), int(ptr[s + 1])
         tx, ty, yaw = (float(v) for v in mount[s])
         az, vr = win['azimuth_sc'][a:b], win['vr'][a:b]
-        cols['st'].append(stationary_flag(az, vr, tx, ty, yaw, np.float64(odo[s][3]),
-                                          np.float64(odo[s][4])))
+        gate = stationary_flag(az, vr, tx, ty, yaw, np.float64(odo[s][3]), np.float64(odo[s][4]))
+        if reject_outlier_by_ransac:   # meas_selection.py:188-199: inliers among the gated
+            inl = ransac(np.stack((az, vr), axis=1)[gate])[0]
+            gate = gate.copy()
+            gate[np.flatnonzero(gate)] = inl
+        cols['st'].append(gate)
         ang = az + yaw                                    # float32 (weak python scalar)
         vrc = win['vr_compensated'][a:b]
         cols['vx'].append(vrc * np.cos(ang))

@@ -1,0 +1,51 @@
+"""The RANSAC restatement (oracle/frontend_ref.ransac, meas_selection.py:96-166) against the
+reference's own outputs (tests/golden/ransac_*.npz, tests/golden/make_ransac_golden.py),
+CPU only: with numpy's global generator seeded as the fixture's was, every scan's flags,
+inlier ratio and validity are equal, and no gated measurement's error under the chosen fit
+lies within 1e-5 of the margin -- so the device's float32 cos / sin, which can differ from
+numpy's in the last place, cannot move a fixture decision (test_gpu_frontend.py)."""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_names
+from oracle import frontend_ref as F
+
+NAMES = golden_names('ransac_')
+
+
+def _window(d):
+    w = {k[3:]: d[k] for k in d.files if k.startswith('in/')}
+    w['n_scans'] = int(w['n_scans'])
+    return w
+
+
+@pytest.mark.parametrize('name', NAMES)
+def test_ransac_oracle_matches_reference(name):
+    d = golden(name)
+    w = _window(d)
+    np.random.seed(int(d['rng_seed']))
+    got = F.sync_window(w, reject_outlier_by_ransac=True)
+    np.testing.assert_array_equal(got['stationary_meas_flag'], d['stationary'])
+    # per scan: the same draws again, scan by scan, with the fit and the margin distance
+    np.random.seed(int(d['rng_seed']))
+    ptr, mount, odo = w['scan_ptr'], w['mount'], w['odometry']
+    for s in range(w['n_scans']):
+        a, b = int(ptr[s]), int(ptr[s + 1])
+        az, vr = w['azimuth_sc'][a:b], w['vr'][a:b]
+        gate = F.stationary_flag(az, vr, *(float(v) for v in mount[s]), np.float64(odo[s][3]),
+                                 np.float64(odo[s][4]))
+        assert int(gate.sum()) == int(d['n_gated'][s])
+        flags, ok, ratio, fit, err = F.ransac(np.stack((az, vr), axis=1)[gate], with_fit=True)
+        assert ratio == d['in_ratio'][s] and ok == bool(d['is_valid'][s])
+        if err is not None:
+            assert np.min(np.abs(err - F.RANSAC_MARGIN)) > 1e-5
+
+
+def test_ransac_small_scan_draws_nothing():
+    """<= RANSAC_MIN_MEAS gated rows: no inliers and no draws from the generator."""
+    np.random.seed(3)
+    before = np.random.get_state()[1].copy()
+    z = np.ones((F.RANSAC_MIN_MEAS, 2), np.float32)
+    flags, ok, ratio = F.ransac(z)
+    assert not flags.any() and not ok and ratio == 0
+    np.testing.assert_array_equal(np.random.get_state()[1], before)

@@ -79,12 +79,52 @@ def test_frontend_feeds_graph_build(cuda_device):
     np.testing.assert_array_equal(got['adj_list'], want['adj_list'])
 
 
-def test_frontend_ransac_refused(cuda_device):
+RANSAC = golden_names('ransac_')
+
+
+@pytest.mark.parametrize('name', RANSAC)
+def test_frontend_ransac_matches_reference(cuda_device, name):
+    """RANSAC stationary rejection (meas_selection.py:96-166) with numpy's global generator
+    seeded as the fixture's was (tests/golden/make_ransac_golden.py): the device flags, each
+    scan's inlier ratio and validity equal the reference's, and the host's draws leave the
+    generator exactly where the reference's left it.  Exact: the ratios are inlier counts,
+    and no fixture measurement's error lies within 1e-5 of the margin under the chosen fit
+    (tests/test_frontend_ransac_oracle.py), where a last-place cos / sin difference could
+    move a decision."""
     from graph_neural_network_for_radar_perception_amd import frontend
-    d = golden('frontend_w1')
-    win = frontend.ScanWindow.from_numpy(_window(d), cuda_device)
-    with pytest.raises(NotImplementedError):
-        frontend.extract_and_sync_radar_data(win, reject_outlier_by_ransac=True)
+    d = golden(name)
+    w = _window(d)
+    win = frontend.ScanWindow.from_numpy(w, cuda_device)
+    np.random.seed(int(d['rng_seed']))
+    full = frontend.extract_and_sync_radar_data(win, reject_outlier_by_ransac=True)
+    after = np.random.get_state()[1].copy()
+    np.random.seed(int(d['rng_seed']))
+    ref = frontend_ref.sync_window(w, reject_outlier_by_ransac=True)
+    np.testing.assert_array_equal(np.random.get_state()[1], after)
+    np.testing.assert_array_equal(ref['stationary_meas_flag'], d['stationary'])
+    np.testing.assert_array_equal(full['stationary_meas_flag'].cpu().numpy(), d['stationary'])
+    ratio, valid = full['_ransac']
+    np.testing.assert_array_equal(ratio.cpu().numpy(), d['in_ratio'])
+    np.testing.assert_array_equal(valid.cpu().numpy(), d['is_valid'])
+
+
+def test_frontend_ransac_batch_of_windows(cuda_device):
+    """Every RANSAC fixture's window in ONE batch, the generator seeded once: the draws run
+    window after window, scan after scan, as the reference's loop over windows would; the
+    flags equal the oracle's over the same seeded sequence (the oracle is pinned to the
+    fixtures above), and the whole dynamic frame follows."""
+    from graph_neural_network_for_radar_perception_amd import frontend
+    ws = [_window(golden(n)) for n in RANSAC]
+    win = frontend.scan_window_batch(ws, cuda_device)
+    np.random.seed(2024)
+    full = frontend.extract_and_sync_radar_data(win, reject_outlier_by_ransac=True)
+    np.random.seed(2024)
+    want = np.concatenate([frontend_ref.sync_window(w, reject_outlier_by_ransac=True)
+                           ['stationary_meas_flag'] for w in ws])
+    np.testing.assert_array_equal(full['stationary_meas_flag'].cpu().numpy(), want)
+    np.random.seed(2024)
+    dd, gd = frontend.dynamic_frame(win, reject_outlier_by_ransac=True)
+    assert int(dd['frame_ptr'][-1]) == len(dd['meas_px'])
 
 
 def test_frontend_batch_of_windows(cuda_device):
