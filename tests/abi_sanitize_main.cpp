@@ -156,6 +156,17 @@ int main() {
                "rg_conv_layer_x3 unsupported widths");
   conv[1].out_dim = 64;
   expect_error(rg_conv_x3_blocks(nullptr, 100, nullptr, nullptr), "rg_conv_x3_blocks null table");
+  // RANSAC: null lists, iteration count out of range
+  expect_error(rg_frontend_gate_lists(nullptr, nullptr, 4, nullptr, nullptr, nullptr),
+               "rg_frontend_gate_lists null arguments");
+  expect_error(rg_frontend_ransac(fake, fake, (const int*)fake, 4, (const int*)fake,
+                                  (const int*)fake, (const int*)fake, 0, 2, 0.25, 10, 0.6,
+                                  (uint8_t*)fake, (double*)fake, (uint8_t*)fake, nullptr),
+               "rg_frontend_ransac zero iterations");
+  expect_error(rg_frontend_ransac(fake, fake, (const int*)fake, 4, (const int*)fake,
+                                  (const int*)fake, (const int*)fake, 30, 2, 0.25, 10, 0.6,
+                                  nullptr, nullptr, nullptr, nullptr),
+               "rg_frontend_ransac null outputs");
   expect_error(rg_conv_layer_x3_blocks(conv, nullptr, RG_REDUCE_SUM, fake, 64, fake, 64, fake,
                                        nullptr, nullptr, nullptr, 100, fake + 64, 64, nullptr,
                                        nullptr, fake, 1 << 20, nullptr),
