@@ -58,8 +58,11 @@ PRESETS = {
     # 64 frames per rank (weak scaling: --gpus 8 processes 512), no collective in the step
     'c3': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
                cpu_warm=2, dtype='bf16', weights='random', streams=2),
+    # one 20 000-node frame per step leaves the persistent kernels a few tiles per wave: the
+    # in-flight batches run on streams of their own, so consecutive forwards overlap (+15 %,
+    # profiles/r05_concurrent_ab.log)
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
-               cpu_warm=1, dtype='fp16', weights='random', streams=2),
+               cpu_warm=1, dtype='fp16', weights='random', streams=2, concurrent=1),
     # the same dense frames batched 8 per step (3.2 M edges per step): the throughput form of
     # config 5 -- a 20 000-node frame alone leaves the persistent kernels ~1 block per wave
     'c5b': dict(frames=8, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
@@ -121,8 +124,11 @@ def parse():
                    help='inference configs: batches in flight -- 2 builds step i\'s graph on a '
                         'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
                         '1: build and forward back to back on one stream (default: the preset\'s, '
-                        '1 for m -- its build is ~5 %% of the step and the overlap blurs the conv '
-                        'roofline -- 2 for c2 / c3 / c5)')
+                        '2 for every inference preset)')
+    p.add_argument('--concurrent', type=int, default=None,
+                   help='with --streams > 1: 1 runs each in-flight batch\'s build AND forward on '
+                        'a stream of its own, so consecutive forwards overlap too '
+                        '(PipelinedSteps(concurrent=True); default: the preset\'s, else 0)')
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
         if getattr(a, key, None) is None:
@@ -133,6 +139,8 @@ def parse():
         a.weights = 'random'
     if a.streams is None:
         a.streams = 1
+    if a.concurrent is None:
+        a.concurrent = 0
     return a
 
 
@@ -846,7 +854,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     batch = FrameBatch.from_frames(frames, clusters, device=dev)
     if args.streams > 1:
         stepper = PipelinedSteps(model, cfg, args.dtype, mode=mode, eps2=args.eps2,
-                                 depth=args.streams)
+                                 depth=args.streams, concurrent=bool(args.concurrent))
     else:
         stepper = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
     log(f'{args.config}: {args.frames} frames generated; warm-up')
@@ -1008,7 +1016,12 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
                         ('one pair per launch' if args.fine_events else
                          'one pair around the conv stack per step, avg = span / layers') +
                         (f'; {args.streams} batches in flight (the next step\'s graph build '
-                         'runs beside this conv stack)' if args.streams > 1 else '')),
+                         'runs beside this conv stack)' if args.streams > 1 and not args.concurrent
+                         else '') +
+                        (f'; {args.streams} batches in flight on streams of their own (the next '
+                         'step\'s build AND forward overlap this conv stack, so a span holds both '
+                         'forwards\' kernels: avg_ms_isolated / frac_isolated are the kernel\'s own)'
+                         if args.streams > 1 and args.concurrent else '')),
                 flops_per_launch=flops)
     if iso_ms:
         # the same kernels timed in the forward-only loop (nothing runs beside them)
@@ -1064,7 +1077,7 @@ def main():
                    'edges_per_frame': round(r['E'] / args.frames, 1),
                    'parallelism': f'frame-parallel x{world} (no collective in the step)',
                    'frames_per_rank_timed': r['rank_frames'],
-                   'streams': args.streams,
+                   'streams': args.streams, 'concurrent_forwards': bool(args.concurrent and args.streams > 1),
                    'backend': dist.get_backend() if world > 1 else None},
         'forward_only_frames_per_s': round(r['forward_fps'], 2),
         'forward_algorithmic_tflops': round(r['forward_tflops'], 2),

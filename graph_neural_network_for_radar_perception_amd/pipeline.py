@@ -76,16 +76,51 @@ class PipelinedSteps:
     batch early cannot hand its memory to the caller's stream while the build reads it."""
 
     def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
-                 eps2: Optional[float] = None, depth: int = 2):
+                 eps2: Optional[float] = None, depth: int = 2, concurrent: bool = False):
+        """concurrent: each pipeline runs its build AND its forward on a stream of its own,
+        so the forwards of consecutive steps overlap too (latency-bound single-frame steps:
+        one 20 000-node frame leaves the persistent kernels a few tiles per wave); the
+        caller's stream then waits for nothing -- synchronise the device (or each step's
+        ``done`` event) before reading an output."""
         self.pipes = [RadarGNNPipeline(model, cfg, dtype, mode=mode, eps2=eps2)
                       for _ in range(depth)]
         self.depth = depth
+        self.concurrent = concurrent
+        self.streams = None
+        self.done = [None] * depth
+        self.last_done = None   # concurrent: the latest step's completion (wait on it to read)
         self.side = None
         self.ev_fwd = [None] * depth
         self.keep = [None] * depth
         self.i = 0
 
+    def _step_concurrent(self, batch: FrameBatch, events=None):
+        main = torch.cuda.current_stream()
+        if self.streams is None:
+            self.streams = [torch.cuda.Stream(device=main.device) for _ in range(self.depth)]
+        p = self.i % self.depth
+        self.i += 1
+        st = self.streams[p]
+        with torch.cuda.stream(st):
+            # the pipeline's previous step ran on this same stream: its arrays are free
+            if batch.ready is not None:
+                st.wait_event(batch.ready)
+            else:
+                st.wait_stream(main)
+            for t in batch.tensors():
+                t.record_stream(st)
+            gb = self.pipes[p].build(batch)
+            out = self.pipes[p].forward(batch, gb, events)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self.done[p] = ev
+        self.last_done = ev
+        self.keep[p] = (gb, out)
+        return gb, out
+
     def step(self, batch: FrameBatch, events=None):
+        if self.concurrent:
+            return self._step_concurrent(batch, events)
         main = torch.cuda.current_stream()
         if self.side is None:
             self.side = torch.cuda.Stream(device=main.device)
