@@ -1139,9 +1139,10 @@ def test_model_inference_proposals_match_reference(cuda_device, tag):
         np.testing.assert_allclose(out[3].cpu().numpy(), d[f'{tag}/obj_cls'], rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize('mode_name,concurrent', [('knn', False), ('radius', False),
-                                                   ('knn', True), ('radius', True)])
-def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent):
+@pytest.mark.parametrize('mode_name,concurrent,dtype', [
+    ('knn', False, 'fp32'), ('radius', False, 'fp32'), ('knn', True, 'fp32'),
+    ('radius', True, 'fp32'), ('radius', True, 'fp16')])
+def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent, dtype):
     """pipeline.PipelinedSteps (graph build of step i on a side stream while step i-1's forward
     runs, two pipelines round robin) gives every step exactly the outputs RadarGNNPipeline.step
     gives the same batch: two different batches alternated over six steps, fp32, kNN and
@@ -1151,7 +1152,8 @@ def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent):
     asynchronously from pinned memory on the caller's stream right before the step, so the
     build has to wait for that upload (FrameBatch.ready), not for the previous forward.
     concurrent: each in-flight batch's build and forward on a stream of its own (the caller
-    waits on the step's completion event before copying its outputs)."""
+    waits on the step's completion event before copying its outputs); also the fp16 path of
+    BASELINE config 5 (the preset that runs concurrent)."""
     from graph_neural_network_for_radar_perception_amd import _native as nat
     from graph_neural_network_for_radar_perception_amd import synthetic
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
@@ -1171,14 +1173,14 @@ def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent):
         host.append((frs, cls))
     ref = []
     with torch.no_grad():
-        seq = RadarGNNPipeline(m, cfg, 'fp32', mode=mode, eps2=4.0)
+        seq = RadarGNNPipeline(m, cfg, dtype, mode=mode, eps2=4.0)
         for frs, cls in host:
             b = FrameBatch.from_frames(frs, cls, device=dev)
             for _ in range(2):
                 gb, out = seq.step(b)
             torch.cuda.synchronize()
             ref.append([t.clone() for t in RadarGNNPipeline.trim(gb, out)])
-        run = PipelinedSteps(m, cfg, 'fp32', mode=mode, eps2=4.0, concurrent=concurrent)
+        run = PipelinedSteps(m, cfg, dtype, mode=mode, eps2=4.0, concurrent=concurrent)
         if mode == nat.GRAPH_RADIUS:
             # each pipeline's first radius build checks its capacity on the host (one sync);
             # warm both so the six steps below run without any
