@@ -59,10 +59,11 @@ PRESETS = {
     'c3': dict(frames=64, nodes=3000, k=32, layers=6, graph='knn', eps2=25.0, cpu_frames=5,
                cpu_warm=2, dtype='bf16', weights='random', streams=2),
     # one 20 000-node frame per step leaves the persistent kernels a few tiles per wave: the
-    # in-flight batches run on streams of their own, so consecutive forwards overlap (+15 %,
-    # profiles/r05_concurrent_ab.log)
+    # in-flight batches (three) run on streams of their own, so consecutive forwards overlap,
+    # each conv launch on 1536 waves (+15 % and +8 %, profiles/r05_concurrent_ab.log,
+    # r05_conv_waves_ab.log)
     'c5': dict(frames=1, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
-               cpu_warm=1, dtype='fp16', weights='random', streams=2, concurrent=1),
+               cpu_warm=1, dtype='fp16', weights='random', streams=3, concurrent=1),
     # the same dense frames batched 8 per step (3.2 M edges per step): the throughput form of
     # config 5 -- a 20 000-node frame alone leaves the persistent kernels ~1 block per wave
     'c5b': dict(frames=8, nodes=20000, k=10, layers=7, graph='radius', eps2=2.5, cpu_frames=1,
@@ -125,6 +126,9 @@ def parse():
                         'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
                         '1: build and forward back to back on one stream (default: the preset\'s, '
                         '2 for every inference preset)')
+    p.add_argument('--conv-waves', type=int, default=None,
+                   help='16-bit conv static schedule (small graphs): waves per launch, a '
+                        'multiple of 64 (default 2048, 1536 with --concurrent 1)')
     p.add_argument('--concurrent', type=int, default=None,
                    help='with --streams > 1: 1 runs each in-flight batch\'s build AND forward on '
                         'a stream of its own, so consecutive forwards overlap too '
@@ -142,6 +146,19 @@ def parse():
     if a.concurrent is None:
         a.concurrent = 0
     return a
+
+
+def conv_waves_of(args):
+    """The 16-bit conv's static-schedule wave count this run uses on small graphs (None:
+    fp32, or the dynamic schedule)."""
+    if args.dtype not in ('bf16', 'fp16'):
+        return None
+    from graph_neural_network_for_radar_perception_amd import engine as _eng
+    from graph_neural_network_for_radar_perception_amd import pipeline as _pl
+    if args.conv_waves:
+        return args.conv_waves
+    return (_pl.CONCURRENT_CONV_WAVES if args.concurrent and args.streams > 1
+            else _eng.DeviceGraph.CONV_WAVES)
 
 
 def launch_ranks(n: int) -> int:
@@ -854,9 +871,11 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     batch = FrameBatch.from_frames(frames, clusters, device=dev)
     if args.streams > 1:
         stepper = PipelinedSteps(model, cfg, args.dtype, mode=mode, eps2=args.eps2,
-                                 depth=args.streams, concurrent=bool(args.concurrent))
+                                 depth=args.streams, concurrent=bool(args.concurrent),
+                                 conv_waves=args.conv_waves)
     else:
-        stepper = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2)
+        stepper = RadarGNNPipeline(model, cfg, args.dtype, mode=mode, eps2=args.eps2,
+                                   conv_waves=args.conv_waves)
     log(f'{args.config}: {args.frames} frames generated; warm-up')
 
     with torch.no_grad():
@@ -1078,6 +1097,7 @@ def main():
                    'parallelism': f'frame-parallel x{world} (no collective in the step)',
                    'frames_per_rank_timed': r['rank_frames'],
                    'streams': args.streams, 'concurrent_forwards': bool(args.concurrent and args.streams > 1),
+                   'conv_waves': conv_waves_of(args),
                    'backend': dist.get_backend() if world > 1 else None},
         'forward_only_frames_per_s': round(r['forward_fps'], 2),
         'forward_algorithmic_tflops': round(r['forward_tflops'], 2),

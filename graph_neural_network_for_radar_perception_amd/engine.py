@@ -558,15 +558,18 @@ class DeviceGraph:
     CONV_WAVES_MAX_RUNS = 4 * 2048
 
     def conv_waves(self):
-        """wave_nodes [CONV_WAVES + 1] of rg_conv_wave_nodes for rg_conv_layer_fused_waves, or
-        None (large graphs: the dynamic 8-node schedule; or CONV_WAVES = 0)."""
+        """wave_nodes [W + 1] of rg_conv_wave_nodes for rg_conv_layer_fused_waves, or None
+        (large graphs: the dynamic 8-node schedule; or CONV_WAVES = 0).  W = this graph's
+        conv_wave_count when set (a multiple of 64: the pipeline sets fewer waves when
+        forwards overlap), else CONV_WAVES."""
         n = self.n_nodes
-        if n == 0 or self.CONV_WAVES <= 0 or (n + 7) // 8 >= self.CONV_WAVES_MAX_RUNS:
+        W = getattr(self, 'conv_wave_count', None) or self.CONV_WAVES
+        if n == 0 or W <= 0 or (n + 7) // 8 >= self.CONV_WAVES_MAX_RUNS:
             return None
         if self._conv_waves is None:
             dev = self.seg_ptr.device
-            wn = torch.empty(self.CONV_WAVES + 1, dtype=torch.int32, device=dev)
-            nat.check(nat.lib().rg_conv_wave_nodes(self.seg_ptr.data_ptr(), n, self.CONV_WAVES,
+            wn = torch.empty(W + 1, dtype=torch.int32, device=dev)
+            nat.check(nat.lib().rg_conv_wave_nodes(self.seg_ptr.data_ptr(), n, W,
                                                    wn.data_ptr(), nat.stream_ptr(dev)),
                       'rg_conv_wave_nodes')
             self._conv_waves = wn

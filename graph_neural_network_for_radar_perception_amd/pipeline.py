@@ -19,14 +19,22 @@ from . import engine
 from .graph_features import FrameBatch, GraphBatch, build_graph_batch
 
 
+# the 16-bit conv's static schedule (small graphs) while forwards overlap: fewer waves per
+# launch, so the launches of the in-flight forwards share the chip (C5, three in flight:
+# 2048 -> 1536 waves, +8 %, profiles/r05_conv_waves_ab.log)
+CONCURRENT_CONV_WAVES = 1536
+
+
 class RadarGNNPipeline:
     def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
-                 eps2: Optional[float] = None):
+                 eps2: Optional[float] = None, conv_waves: Optional[int] = None):
         """mode: nat.GRAPH_KNN (datagen_gnn.py:104-106, the default), nat.GRAPH_RADIUS (a pure
         ball-query graph, BASELINE config 5) or nat.GRAPH_KNN_RADIUS
         (compute_adjacency_information_v2); eps2: squared radius (default
-        cfg.ball_query_eps_square)."""
+        cfg.ball_query_eps_square); conv_waves: the built graphs' 16-bit conv wave count
+        (DeviceGraph.conv_waves; None: DeviceGraph.CONV_WAVES)."""
         self.model = model
+        self.conv_waves = conv_waves
         self.cfg = cfg
         self.dtype = dtype
         self.mode = mode
@@ -36,8 +44,11 @@ class RadarGNNPipeline:
         self.buffers: dict = {}
 
     def build(self, batch: FrameBatch) -> GraphBatch:
-        return build_graph_batch(batch, self.cfg, eps2=self.eps2, mode=self.mode,
-                                 ws_cache=self.ws_cache)
+        gb = build_graph_batch(batch, self.cfg, eps2=self.eps2, mode=self.mode,
+                               ws_cache=self.ws_cache)
+        if self.conv_waves:
+            gb.graph.conv_wave_count = self.conv_waves
+        return gb
 
     def forward(self, batch: FrameBatch, gb: GraphBatch, events=None) -> engine.ForwardOutputs:
         return engine.forward_batched(self.plans, gb.node_features, gb.edge_features, gb.graph,
@@ -76,14 +87,18 @@ class PipelinedSteps:
     batch early cannot hand its memory to the caller's stream while the build reads it."""
 
     def __init__(self, model, cfg, dtype: str = 'fp32', mode: int = nat.GRAPH_KNN,
-                 eps2: Optional[float] = None, depth: int = 2, concurrent: bool = False):
+                 eps2: Optional[float] = None, depth: int = 2, concurrent: bool = False,
+                 conv_waves: Optional[int] = None):
         """concurrent: each pipeline runs its build AND its forward on a stream of its own,
         so the forwards of consecutive steps overlap too (latency-bound single-frame steps:
         one 20 000-node frame leaves the persistent kernels a few tiles per wave); the
         caller's stream then waits for nothing -- synchronise the device (or each step's
-        ``done`` event) before reading an output."""
-        self.pipes = [RadarGNNPipeline(model, cfg, dtype, mode=mode, eps2=eps2)
-                      for _ in range(depth)]
+        ``done`` event) before reading an output.  conv_waves: as RadarGNNPipeline's (default
+        with concurrent: CONCURRENT_CONV_WAVES)."""
+        if conv_waves is None and concurrent:
+            conv_waves = CONCURRENT_CONV_WAVES
+        self.pipes = [RadarGNNPipeline(model, cfg, dtype, mode=mode, eps2=eps2,
+                                       conv_waves=conv_waves) for _ in range(depth)]
         self.depth = depth
         self.concurrent = concurrent
         self.streams = None

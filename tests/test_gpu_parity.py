@@ -1173,7 +1173,12 @@ def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent, dtype
         host.append((frs, cls))
     ref = []
     with torch.no_grad():
-        seq = RadarGNNPipeline(m, cfg, dtype, mode=mode, eps2=4.0)
+        # (the 16-bit conv's wave count is part of its schedule -- a different count moves
+        # some sums across its 16-edge aggregation groups -- so the sequential reference
+        # uses the one the overlapping pipeline sets)
+        from graph_neural_network_for_radar_perception_amd.pipeline import CONCURRENT_CONV_WAVES
+        seq = RadarGNNPipeline(m, cfg, dtype, mode=mode, eps2=4.0,
+                               conv_waves=CONCURRENT_CONV_WAVES if concurrent else None)
         for frs, cls in host:
             b = FrameBatch.from_frames(frs, cls, device=dev)
             for _ in range(2):
