@@ -126,6 +126,9 @@ def parse():
                         'side stream while step i-1\'s forward runs (pipeline.PipelinedSteps); '
                         '1: build and forward back to back on one stream (default: the preset\'s, '
                         '2 for every inference preset)')
+    p.add_argument('--ransac', type=int, default=0,
+                   help='frontend config: 1 adds the RANSAC stationary rejection (numpy\'s global '
+                        'generator seeded once with --seed; the host draws the consensus sets)')
     p.add_argument('--conv-waves', type=int, default=None,
                    help='16-bit conv static schedule (small graphs): waves per launch, a '
                         'multiple of 64 (default 2048, 1536 with --concurrent 1)')
@@ -752,7 +755,7 @@ def frontend_main(args, world, rank, local):
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             events.append(('sync:start', ev))
-        d = frontend.extract_and_sync_radar_data(batch)
+        d = frontend.extract_and_sync_radar_data(batch, reject_outlier_by_ransac=bool(args.ransac))
         if events is not None:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
@@ -760,6 +763,7 @@ def frontend_main(args, world, rank, local):
         gt = frontend.compute_ground_truth(d)
         return frontend.select_dynamic(d, gt)
 
+    np.random.seed(args.seed)   # the RANSAC draws (meas_selection.py:128)
     for _ in range(args.warmup):
         dd, _ = step()
     torch.cuda.synchronize()
@@ -787,7 +791,9 @@ def frontend_main(args, world, rank, local):
         'data': 'synthetic RadarScenes-shaped scan windows (synthetic.make_scan_window)',
         'config': {'workload': f'frontend: {args.frames} windows x {args.layers} scans x '
                                f'~{args.nodes} measurements per GPU; step = sync (gate, ego '
-                               'compensation) + labels + grid/moving selection',
+                               'compensation' + (', RANSAC: host draws + device fits' if args.ransac
+                                                 else '') + ') + labels + grid/moving selection',
+                   'ransac': bool(args.ransac),
                    'windows_per_gpu': args.frames, 'measurements_per_gpu': n_meas,
                    'dynamic_per_gpu': n_dyn,
                    'parallelism': f'window-parallel x{world} (no collective in the step)'},
@@ -803,7 +809,7 @@ def frontend_main(args, world, rank, local):
         for w in sample:
             w2 = dict(w)
             w2['track_key'] = frontend._host_track_keys(w)
-            full = frontend_ref.sync_window(w2)
+            full = frontend_ref.sync_window(w2, reject_outlier_by_ransac=bool(args.ransac))
             frontend_ref.select_dynamic(full, frontend_ref.ground_truth(full, w2['track_key']))
         dt = time.perf_counter() - t
         line['cpu_baseline'] = {'value': round(len(sample) / dt, 1), 'unit': 'windows/s',
