@@ -100,6 +100,7 @@ _SIGNATURES = {
     'rg_frontend_sync': (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P,
                               _P, _P]),
     'rg_frontend_gate_lists': (_I, [_P, _P, _I, _P, _P, _P]),
+    'rg_ransac_consensus_sets': (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     'rg_frontend_ransac': (_I, [_P, _P, _P, _I, _P, _P, _P, _I, _I, _D, _I, _D, _P, _P, _P, _P]),
     'rg_frontend_labels_workspace_size': (_S, [_I]),
     'rg_frontend_labels': (_I, [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _P, _S, _P]),

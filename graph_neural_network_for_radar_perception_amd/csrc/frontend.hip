@@ -15,6 +15,7 @@
 // promotion (comments at each step); transcendental functions of float32 arrays are
 // evaluated in float32 as numpy does.
 #include "rg_common.h"
+#include <vector>
 #include "scan.h"
 
 // numpy evaluates every product and sum separately
@@ -298,6 +299,86 @@ __global__ __launch_bounds__(256) void frontend_ransac_kernel(
 }  // namespace rg
 
 using namespace rg;
+
+// ---- the RANSAC consensus draws, host side (no device work): numpy's legacy generator
+// (RandomState: MT19937, mtrand.pyx shuffle -> _shuffle_raw + random_interval of
+// distributions.c) restated, so the draws numpy.random.shuffle would make -- and the state
+// it would leave -- come out of one native loop instead of one Python call per shuffle
+namespace {
+constexpr int MT_N = 624, MT_M = 397;
+void mt_refill(uint32_t* key) {
+  int i = 0;
+  for (; i < MT_N - MT_M; ++i) {
+    const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+    key[i] = key[i + MT_M] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  for (; i < MT_N - 1; ++i) {
+    const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+    key[i] = key[i + (MT_M - MT_N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  const uint32_t y = (key[MT_N - 1] & 0x80000000u) | (key[0] & 0x7fffffffu);
+  key[MT_N - 1] = key[MT_M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+}
+uint32_t mt_next32(uint32_t* key, int& pos) {
+  if (pos >= MT_N) {
+    mt_refill(key);
+    pos = 0;
+  }
+  uint32_t y = key[pos++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+// a uniform integer in [0, mx] by masked rejection (random_interval, mx < 2^32)
+uint32_t mt_interval(uint32_t* key, int& pos, uint32_t mx) {
+  if (mx == 0) return 0;
+  uint32_t mask = mx;
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  uint32_t v;
+  while ((v = (mt_next32(key, pos) & mask)) > mx) {
+  }
+  return v;
+}
+}  // namespace
+
+extern "C" int rg_ransac_consensus_sets(uint32_t* mt_key, int* mt_pos, const int* gated_cnt,
+                                        int n_scans, int n_iter, int n_samples, int min_num_meas,
+                                        int* consensus_sets) {
+  RG_REQUIRE(mt_key && mt_pos && gated_cnt && consensus_sets && n_scans >= 0 && n_iter >= 1 &&
+                 n_samples >= 1 && *mt_pos >= 0 && *mt_pos <= MT_N,
+             RG_ERR_ARG, "rg_ransac_consensus_sets: bad argument");
+  int pos = *mt_pos;
+  std::vector<int> order;
+  for (int s = 0; s < n_scans; ++s) {
+    const int c = gated_cnt[s];
+    int* out = consensus_sets + (size_t)s * n_iter * n_samples;
+    if (c <= min_num_meas) {  // no draws (ransac's size check), sets unused
+      for (int q = 0; q < n_iter * n_samples; ++q) out[q] = 0;
+      continue;
+    }
+    RG_REQUIRE(n_samples <= c, RG_ERR_ARG, "rg_ransac_consensus_sets: %d samples of %d",
+               n_samples, c);
+    order.resize(c);
+    for (int i = 0; i < c; ++i) order[i] = i;      // meas_idx = np.arange(n)
+    for (int it = 0; it < n_iter; ++it) {          // np.random.shuffle(meas_idx), in place
+      for (int i = c - 1; i >= 1; --i) {
+        const int j = (int)mt_interval(mt_key, pos, (uint32_t)i);
+        const int t = order[i];
+        order[i] = order[j];
+        order[j] = t;
+      }
+      for (int q = 0; q < n_samples; ++q) out[it * n_samples + q] = order[q];
+    }
+  }
+  *mt_pos = pos;
+  return RG_OK;
+}
 
 extern "C" int rg_frontend_gate_lists(const uint8_t* stationary, const int* scan_ptr, int n_scans,
                                       int* gated_idx, int* gated_cnt, void* stream) {

@@ -148,7 +148,8 @@ def _ransac(w: ScanWindow, st: torch.Tensor):
     the device lists each scan's gated measurements, the host draws the consensus sets from
     numpy's global generator in the reference's order (per scan with more than
     RANSAC_MIN_MEAS gated, RANSAC_ITERS np.random.shuffle passes over arange(gated), the
-    first RANSAC_MIN_SAMPLES of each), the device fits and counts.  Returns the per-scan
+    first RANSAC_MIN_SAMPLES of each -- natively, rg_ransac_consensus_sets, from and back into
+    numpy's generator state), the device fits and counts.  Returns the per-scan
     (in_ratio f64, is_valid bool) device tensors.  Synchronises once (the draws need the
     gated counts)."""
     lib = nat.lib()
@@ -162,16 +163,17 @@ def _ransac(w: ScanWindow, st: torch.Tensor):
     nat.check(lib.rg_frontend_gate_lists(st.data_ptr(), w.scan_ptr.data_ptr(), S,
                                          gidx.data_ptr(), gcnt.data_ptr(), stream),
               'rg_frontend_gate_lists')
-    counts = gcnt.cpu().numpy()
+    counts = np.ascontiguousarray(gcnt.cpu().numpy(), dtype=np.int32)
     sets = np.zeros((S, RANSAC_ITERS, RANSAC_MIN_SAMPLES), np.int32)
-    for s in range(S):
-        c = int(counts[s])
-        if c <= RANSAC_MIN_MEAS:
-            continue
-        order = np.arange(c)
-        for it in range(RANSAC_ITERS):
-            np.random.shuffle(order)
-            sets[s, it] = order[:RANSAC_MIN_SAMPLES]
+    # the draws np.random.shuffle would make, from numpy's own generator state, in one native
+    # loop (rg_ransac_consensus_sets); the advanced state goes back into numpy
+    kind, key, pos, has_gauss, gauss = np.random.get_state()
+    key = np.array(key, dtype=np.uint32)
+    posa = np.array([pos], dtype=np.int32)
+    nat.check(lib.rg_ransac_consensus_sets(key.ctypes.data, posa.ctypes.data, counts.ctypes.data,
+                                           S, RANSAC_ITERS, RANSAC_MIN_SAMPLES, RANSAC_MIN_MEAS,
+                                           sets.ctypes.data), 'rg_ransac_consensus_sets')
+    np.random.set_state((kind, key, int(posa[0]), has_gauss, gauss))
     sets_d = torch.from_numpy(sets).to(dev)
     ratio = torch.empty(S, dtype=torch.float64, device=dev)
     valid = torch.empty(S, dtype=torch.uint8, device=dev)

@@ -639,6 +639,15 @@ int rg_frontend_sync(const float* x_cc, const float* y_cc, const float* azimuth_
  *     = in_ratio >= ratio_threshold.  n_iter <= 256. */
 int rg_frontend_gate_lists(const uint8_t* stationary, const int* scan_ptr, int n_scans,
                            int* gated_idx, int* gated_cnt, void* stream);
+/* Host only (no device work): the consensus sets numpy's legacy generator would draw, for
+ * gated_cnt [n_scans] (host) -- per scan with more than min_num_meas, n_iter in-place
+ * np.random.shuffle passes over arange(count) (MT19937 + masked-rejection random_interval,
+ * numpy/random/mtrand.pyx, distributions.c), the first n_samples of each -- into
+ * consensus_sets [n_scans][n_iter][n_samples] (host).  mt_key [624] / *mt_pos: numpy's
+ * np.random.get_state()[1] / [2], advanced in place exactly as the shuffles would (write
+ * them back with np.random.set_state). */
+int rg_ransac_consensus_sets(uint32_t* mt_key, int* mt_pos, const int* gated_cnt, int n_scans,
+                             int n_iter, int n_samples, int min_num_meas, int* consensus_sets);
 int rg_frontend_ransac(const float* azimuth_sc, const float* vr, const int* scan_ptr, int n_scans,
                        const int* gated_idx, const int* gated_cnt, const int* consensus_sets,
                        int n_iter, int n_samples, double error_margin, int min_num_meas,

@@ -167,6 +167,16 @@ int main() {
                                   (const int*)fake, (const int*)fake, 30, 2, 0.25, 10, 0.6,
                                   nullptr, nullptr, nullptr, nullptr),
                "rg_frontend_ransac null outputs");
+  expect_error(rg_ransac_consensus_sets(nullptr, nullptr, nullptr, 4, 30, 2, 10, nullptr),
+               "rg_ransac_consensus_sets null arguments");
+  {  // a draw over a real state: 3 scans, the middle one below the minimum
+    uint32_t key[624];
+    for (int i = 0; i < 624; ++i) key[i] = 0x9e3779b9u * (uint32_t)(i + 1);
+    int pos = 624, cnt[3] = {40, 7, 13}, sets[3 * 30 * 2];
+    CHECK(rg_ransac_consensus_sets(key, &pos, cnt, 3, 30, 2, 10, sets) == RG_OK);
+    for (int i = 0; i < 3 * 30 * 2; ++i) CHECK(sets[i] >= 0 && sets[i] < 40);
+    CHECK(pos >= 0 && pos <= 624);
+  }
   expect_error(rg_conv_layer_x3_blocks(conv, nullptr, RG_REDUCE_SUM, fake, 64, fake, 64, fake,
                                        nullptr, nullptr, nullptr, 100, fake + 64, 64, nullptr,
                                        nullptr, fake, 1 << 20, nullptr),
