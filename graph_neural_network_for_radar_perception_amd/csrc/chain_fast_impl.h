@@ -19,20 +19,9 @@ static constexpr float NORM_EPS = 1e-5f;
 #endif
 static constexpr int FUSE01 = 0x100;  // kernel MODE flag: run_chain01 for layers 0+1
 
-#ifndef RG_CHAIN_EXP
-#define RG_CHAIN_EXP 0  // timing experiments only (wrong results): 1 no epilogue VALU,
-                        // 2 no MFMA (accumulators keep the bias),
-                        // 3 MFMAs without their A-fragment LDS reads
-#endif
-// MFMA wrapper for the timing experiments
+// the chains' MFMA (bf16 or fp16 by HT)
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
-  if constexpr (RG_CHAIN_EXP == 2) {
-    return c;
-  } else if constexpr (RG_CHAIN_EXP == 3) {  // no A-fragment LDS reads (A := B)
-    return HT::mfma(b, b, c);
-  } else {
-    return HT::mfma(a, b, c);
-  }
+  return HT::mfma(a, b, c);
 }
 
 struct FLayer {
@@ -263,7 +252,6 @@ constexpr int spec(int act, int norm_mask, int act_mask) {
 // nrm: the layers' channel_normalization (mu, sd) staged in LDS at kernel start
 template <int SPEC, int LI, int MT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const FLayer& L, const float* nrm) {
-  if constexpr (RG_CHAIN_EXP == 1) return;
   if constexpr (SPEC >= 0) {
     constexpr bool NORM = ((SPEC >> (8 + LI)) & 1) != 0, ACTV = ((SPEC >> (16 + LI)) & 1) != 0;
 #ifndef RG_NO_FUSED_LEAKY
