@@ -153,10 +153,6 @@ struct Idx {
 #ifndef RG_CF32_PRIO
 #define RG_CF32_PRIO 0
 #endif
-#ifndef RG_CF32_EXP
-#define RG_CF32_EXP 0  // timing experiments only (wrong results): 1 no norm/act epilogues,
-                       // 2 no segmented sum, 3 no P/Q gathers, 4 = 1 + 2 + 3
-#endif
 static constexpr int FT2 = 512;
 static constexpr int NW2 = FT2 / 64;
 static constexpr int TR2 = 8;   // message rows per LDS pass
@@ -319,10 +315,7 @@ __global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
         const float* pp = a.pq + (size_t)d * a.ldpq + 4 * h;
         const float* pq = a.pq + (size_t)sj * a.ldpq + HID + 4 * h;
         f32x4 pv[16], qv[16];
-        if (RG_CF32_EXP == 3 || RG_CF32_EXP == 4) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) pv[i] = qv[i] = (f32x4){1.f, 2.f, 3.f, (float)d};
-        } else {
+        {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             pv[i] = *(const f32x4*)(pp + 8 * i);
@@ -344,7 +337,7 @@ __global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
         layer<8, 4>(acc1, wE, lane, [&](int s4) { return eb[s4]; });
       }
 #endif
-      if (RG_CF32_EXP != 1 && RG_CF32_EXP != 4) norm_leaky5<4>(acc1, mu0, sd0);
+      norm_leaky5<4>(acc1, mu0, sd0);
       // ---- layer 2
       f32x16 acc2[2];
 #pragma unroll
@@ -354,15 +347,7 @@ __global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
         const int o = 4 * (s4 & 3);
         return (f32x4){q[o], q[o + 1], q[o + 2], q[o + 3]};
       });
-      if (RG_CF32_EXP != 1 && RG_CF32_EXP != 4) norm_leaky5<2>(acc2, mu1, sd1);
-      if (RG_CF32_EXP == 2 || RG_CF32_EXP == 4) {
-        // keep the messages live: fold them into the running sum without the LDS pass
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) run += acc2[m][q];
-        continue;
-      }
+      norm_leaky5<2>(acc2, mu1, sd1);
       // ---- segmented sum in edge order, 8 edges per LDS pass
 #pragma unroll
       for (int c = 0; c < 32 / TR2; ++c) {
@@ -393,7 +378,6 @@ __global__ __launch_bounds__(FT2) void conv_f32_kernel2(Args a) {
         __builtin_amdgcn_wave_barrier();
       }
     }
-    if (RG_CF32_EXP == 2 || RG_CF32_EXP == 4) Agg[lane] = run;  // keep the messages live
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 

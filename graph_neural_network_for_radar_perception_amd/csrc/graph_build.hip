@@ -55,10 +55,6 @@ hipError_t ensure_max_lds(const void* kernel, int bytes) {
 
 static constexpr int KNN_BLOCK = 256;
 
-#ifndef RG_KNN_EXP
-#define RG_KNN_EXP 0  // timing experiments only (wrong results): 1 no boundary pick,
-                      // 2 no selection pass (histogram pass only)
-#endif
 
 // fp32 squared distance exactly as numpy evaluates graph_features.py:72-73:
 // two products and one sum, each rounded, no fused multiply-add.
@@ -516,12 +512,7 @@ __device__ __forceinline__ void knn_select_row(
       sh = nsh;
     }
   }
-  const int need = RG_KNN_EXP == 1 ? 0 : cnt - below;
-  if (RG_KNN_EXP == 2) {
-    knn_cnt[row] = 0;
-    kth[row] = make_int2(0, 0);
-    return;
-  }
+  const int need = cnt - below;
   if (in_bs > BBUF) {  // exact ties beyond the buffer: exact insert path
     *redo_flag = 1;
     return;
