@@ -360,6 +360,134 @@ __global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restric
   if (it == 0 && threadIdx.x < OC) part_b[((size_t)chunk * gridDim.y + ot) * OC + threadIdx.x] = bsum;
 }
 
+#ifndef RG_GRAD_DMA
+#define RG_GRAD_DMA 1  // full row blocks staged by LDS DMA, double-buffered (below); 0 = the register-staged kernel only
+#endif
+#if RG_GRAD_DMA
+// the 16-B source of input features [f, f + 4) of row `row` (x_chunk's vector path); j0 / j1:
+// the row's gathered node indices (RG_IN_GATHER3)
+__device__ __forceinline__ const float* x_src(const GradIn& a, long row, int f, int j0, int j1) {
+  if (a.mode == RG_IN_GATHER3)
+    return f < a.w0 ? a.in0 + (size_t)j0 * a.ld0 + f
+         : f < 2 * a.w0 ? a.in0 + (size_t)j1 * a.ld0 + (f - a.w0)
+                        : a.in2 + (size_t)row * a.ld2 + (f - 2 * a.w0);
+  if (a.mode == RG_IN_CONCAT2 && f >= a.w0) return a.in1 + (size_t)row * a.ld1 + (f - a.w0);
+  return a.in0 + (size_t)row * a.ld0 + f;
+}
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// The same tile as linear_grad_kernel (same k-step order: bit-identical partials) for a tile
+// whose columns are all real features (no bias / padding column), 16-B aligned rows and a
+// non-PAIRADD input: the full 32-row blocks go through the LDS by DMA (global_load_lds, one
+// instruction per row and operand, no register round trip) into two buffers -- block b + 1
+// lands while block b's MFMAs run; the barrier closing block b waits for it.  A partial last
+// block is staged as in linear_grad_kernel.  One workgroup per CU (two 53-KB buffers).
+template <int OW, int NT>
+__global__ __launch_bounds__(256) void linear_grad_dma_kernel(const float* __restrict__ dz,
+                                                              int lddz, long rows, GradIn in,
+                                                              long rpc, float* __restrict__ part,
+                                                              float* __restrict__ part_b) {
+  constexpr int OC = 64 * OW, IC = 16 * NT;
+  constexpr int SZ = grad_stride(OC), SX = grad_stride(IC);
+  constexpr int BUF = GR * SZ + GR * SX;
+  static_assert(OC / 4 <= 64 && IC / 4 <= 64, "one DMA instruction per row");
+  extern __shared__ __attribute__((aligned(16))) float glds[];
+  const int chunk = blockIdx.x, ot = blockIdx.y, it = blockIdx.z;
+  const int o0 = ot * OC, i0 = it * IC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r_begin = (long)chunk * rpc;
+  const long r_end = min(rows, r_begin + rpc);
+  f32x4 acc[OW][NT];
+#pragma unroll
+  for (int m = 0; m < OW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  // rows wave, wave + 4, ... of the block: their dz and x rows by DMA into buffer b.  A
+  // gathered input's row indices come first, in one load (lanes 0-15) and one wait, then
+  // broadcast: a per-row index load would wait, in order, for every DMA issued before it
+  const int f = i0 + 4 * lane;
+  auto issue = [&](long rb, int b) {
+    float* sZ = glds + b * BUF;
+    float* sX = sZ + GR * SZ;
+    int iv = 0;
+    if (in.mode == RG_IN_GATHER3 && lane < 2 * (GR / 4)) {
+      const long row = rb + wave + 4 * (lane % (GR / 4));
+      iv = lane < GR / 4 ? in.idx0[row] : in.idx1[row];
+    }
+#pragma unroll
+    for (int j = 0; j < GR / 4; ++j) {
+      const int rr = wave + 4 * j;
+      const long row = rb + rr;
+      if (lane < OC / 4)
+        __builtin_amdgcn_global_load_lds((const void*)(dz + (size_t)row * lddz + o0 + 4 * lane),
+                                         (lds_ptr_t)(sZ + rr * SZ), 16, 0, 0);
+      const float* src = x_src(in, row, f, __builtin_amdgcn_readlane(iv, j),
+                               __builtin_amdgcn_readlane(iv, GR / 4 + j));
+      if (lane < IC / 4)
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(sX + rr * SX), 16, 0, 0);
+    }
+  };
+  auto compute = [&](int b) {
+    const float* sZ = glds + b * BUF;
+    const float* sX = sZ + GR * SZ;
+#pragma unroll
+    for (int ks = 0; ks < GR / 4; ++ks) {
+      const int kr = 4 * ks + (lane >> 4);
+      float av[OW], bv[NT];
+#pragma unroll
+      for (int m = 0; m < OW; ++m) av[m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bv[n] = sX[kr * SX + 16 * n + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < OW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+    if (it == 0 && threadIdx.x < OC) {
+#pragma unroll 8
+      for (int rr = 0; rr < GR; ++rr) bsum += sZ[rr * SZ + threadIdx.x];
+    }
+  };
+  const long nfull = (r_end - r_begin) / GR;
+  if (nfull > 0) issue(r_begin, 0);
+  __syncthreads();
+  for (long b = 0; b < nfull; ++b) {
+    if (b + 1 < nfull) issue(r_begin + (b + 1) * GR, (int)((b + 1) & 1));
+    compute((int)(b & 1));
+    __syncthreads();  // (waits for every wave's DMA of block b + 1; buffer b free again)
+  }
+  const long rb = r_begin + nfull * GR;
+  if (rb < r_end) {  // the partial last block, staged through registers with zero rows
+    float* sZ = glds;
+    float* sX = glds + GR * SZ;
+    for (int t = threadIdx.x; t < GR * (OC / 4); t += 256) {
+      const int rr = t / (OC / 4), c = 4 * (t % (OC / 4));
+      const long row = rb + rr;
+      *(f32x4*)(sZ + rr * SZ + c) = row < r_end ? *(const f32x4*)(dz + (size_t)row * lddz + o0 + c)
+                                                : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    for (int t = threadIdx.x; t < GR * (IC / 4); t += 256) {
+      const int rr = t / (IC / 4), c = 4 * (t % (IC / 4));
+      const long row = rb + rr;
+      *(f32x4*)(sX + rr * SX + c) = row < r_end ? x_chunk(in, row, i0 + c, true)
+                                                : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+    compute(0);
+  }
+  float* P = part + ((size_t)(chunk * gridDim.y + ot) * gridDim.z + it) * OC * IC;
+#pragma unroll
+  for (int m = 0; m < OW; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        P[(16 * (OW * wave + m) + 4 * (lane >> 4) + e) * IC + 16 * n + (lane & 15)] = acc[m][n][e];
+  if (it == 0 && threadIdx.x < OC) part_b[((size_t)chunk * gridDim.y + ot) * OC + threadIdx.x] = bsum;
+}
+#endif
+
 struct GradGeom {
   int ow, nt, ot, it, nchunk;
   long rpc;  // rows per chunk (multiple of GR)
@@ -439,14 +567,25 @@ __global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
 }
 
 template <int OW, int NT>
-static void launch_grad(const GradGeom& g, const float* dz, int lddz, long rows, int out_dim,
-                        const GradIn& in, int vec_x, int vec_z, float* part, float* part_b,
-                        hipStream_t st) {
+static int launch_grad(const GradGeom& g, const float* dz, int lddz, long rows, int out_dim,
+                       const GradIn& in, int vec_x, int vec_z, float* part, float* part_b,
+                       hipStream_t st) {
+#if RG_GRAD_DMA
+  if (vec_x && vec_z && in.mode != RG_IN_PAIRADD && out_dim % (64 * OW) == 0 &&
+      in.in_dim % (16 * NT) == 0 && g.rpc % GR == 0) {
+    constexpr int lds = 2 * (GR * grad_stride(64 * OW) + GR * grad_stride(16 * NT)) * 4;
+    auto kern = linear_grad_dma_kernel<OW, NT>;
+    RG_ENSURE_LDS(kern, lds);
+    kern<<<dim3(g.nchunk, g.ot, g.it), 256, lds, st>>>(dz, lddz, rows, in, g.rpc, part, part_b);
+    return RG_OK;
+  }
+#endif
   // (a split-bf16 x3 variant of this kernel measured slower on c4, 614 -> 574 frames/s: its
   // staging -- a three-term split per 8 values, transposed LDS stores -- outweighed the 2.7x
   // matrix rate at 32-row blocks, and was removed; the exact f32 MFMA kernel is the one)
   linear_grad_kernel<OW, NT><<<dim3(g.nchunk, g.ot, g.it), 256, 0, st>>>(
       dz, lddz, rows, out_dim, in, g.rpc, vec_x, vec_z, part, part_b);
+  return RG_OK;
 }
 
 // ------------------------------------------------------------------ incidence lists
@@ -838,8 +977,11 @@ extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim,
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)workspace;
   float* part_b = part + grad_part_floats(g);
-#define RG_GRAD_CASE(OW, NT) \
-  if (g.ow == OW && g.nt == NT) launch_grad<OW, NT>(g, dz, lddz, rows, out_dim, in, vec_x, vec_z, part, part_b, st);
+#define RG_GRAD_CASE(OW, NT)                                                                   \
+  if (g.ow == OW && g.nt == NT) {                                                              \
+    const int rc = launch_grad<OW, NT>(g, dz, lddz, rows, out_dim, in, vec_x, vec_z, part, part_b, st); \
+    if (rc != RG_OK) return rc;                                                                \
+  }
   RG_GRAD_CASE(1, 1) RG_GRAD_CASE(1, 4) RG_GRAD_CASE(1, 8) RG_GRAD_CASE(1, 12) RG_GRAD_CASE(1, 16)
   RG_GRAD_CASE(2, 1) RG_GRAD_CASE(2, 4) RG_GRAD_CASE(2, 8) RG_GRAD_CASE(2, 12) RG_GRAD_CASE(2, 16)
 #undef RG_GRAD_CASE
