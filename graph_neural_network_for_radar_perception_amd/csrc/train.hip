@@ -505,7 +505,13 @@ static GradGeom grad_geom(long rows, int out_dim, int in_dim) {
   // keeps eight loads in flight) -- c4 backward 20.4 -> 15.5 ms against one workgroup per
   // CU and >= 32 blocks (scripts/experiments/gpu_c4_grad.sh: 3 per CU 293, 4 per CU 278
   // frames/s against 2 per CU 309)
-  constexpr int wg_cu = 2, min_blk = 4;
+#ifndef RG_GRAD_WG_CU
+#define RG_GRAD_WG_CU 2
+#endif
+#ifndef RG_GRAD_MIN_BLK
+#define RG_GRAD_MIN_BLK 4
+#endif
+  constexpr int wg_cu = RG_GRAD_WG_CU, min_blk = RG_GRAD_MIN_BLK;
   long want = 256L * (wg_cu > 0 ? wg_cu : 1) / (g.ot * g.it);
   if (want < 1) want = 1;
   const long mb = min_blk > 0 ? min_blk : 1;
