@@ -443,18 +443,22 @@ def test_gather_segment_sum_stream_matches_sequential(cuda_device):
 
 
 @pytest.mark.parametrize('shape', [(128, 192, 'gather3'), (64, 128, 'concat2'), (64, 64, 'dense'),
-                                   (256, 7, 'dense'), (7, 64, 'dense'), (2, 64, 'pairadd')])
+                                   (256, 7, 'dense'), (7, 64, 'dense'), (2, 64, 'pairadd'),
+                                   (128, 192, 'gather3', 31), (128, 192, 'gather3', 4096),
+                                   (64, 128, 'concat2', 1), (128, 128, 'dense', 65)])
 def test_linear_grad_matches_float64(cuda_device, shape):
     """rg_linear_grad's weight gradient (v_mfma_f32_16x16x4_f32, exact f32 products) against a
     float64 evaluation of dZ^T X and sum(dZ): every dW / db entry within 2e-5 of max|dW|, over
     20 011 rows (a partial last block) in the gathered / concatenated / dense / pair-sum input
-    modes the training step uses, including 7- and 2-wide layers (padded tiles)."""
+    modes the training step uses, including 7- and 2-wide layers (padded tiles).  The 64-multiple
+    shapes run the LDS-DMA kernel (train.hip, RG_GRAD_DMA); the extra row counts cover a single
+    partial block (1, 31 rows), whole blocks only (4 096) and one row past a block (65)."""
     from graph_neural_network_for_radar_perception_amd import _native as nat
-    out_dim, in_dim, mode = shape
+    out_dim, in_dim, mode = shape[:3]
     dev = cuda_device
     lib = nat.lib()
     g = torch.Generator().manual_seed(out_dim * 1000 + in_dim)
-    rows, n_nodes = 20011, 3000
+    rows, n_nodes = (shape[3] if len(shape) > 3 else 20011), 3000
     dz = torch.randn(rows, out_dim, generator=g)
     idx0 = torch.randint(0, n_nodes, (rows,), generator=g, dtype=torch.int32)
     idx1 = torch.randint(0, n_nodes, (rows,), generator=g, dtype=torch.int32)
