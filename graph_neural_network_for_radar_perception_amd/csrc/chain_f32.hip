@@ -28,6 +28,9 @@ namespace f32c {
 
 static constexpr float NORM_EPS = 1e-5f;  // constants.py:9
 static constexpr int FT = 256;            // 4 waves, one per SIMD
+#ifndef RG_CF32_DIVR
+#define RG_CF32_DIVR 1  // the tape's channel-norm divides as reciprocal + one correction (0: __fdiv_rn)
+#endif
 
 // bytes of one RG_PACK_F32_FAST layer (fragments + accumulator-order bias)
 __host__ __device__ constexpr int fbytes(int K, int N) {
@@ -251,10 +254,26 @@ __device__ __forceinline__ void channel_norm_ref(f32x16 (&acc)[MT], float mu, fl
       q1 = fmaf(acc[m][q + 1], acc[m][q + 1], q1);
     }
   const float den = __fadd_rn(__fsqrt_rn(__fdiv_rn(add_xor32(q0 + q1), (float)(N - 1))), NORM_EPS);
+#if RG_CF32_DIVR
+  // x / den as RN(x * r) plus one fma residual correction with r = RN(1 / den): the
+  // correctly rounded quotient (scripts/experiments/div_check.hip: every x in [2^-100, 2^100)
+  // for 64 divisors); e == 0 keeps q itself (a signed zero stays signed)
+  const float rd = __fdiv_rn(1.f, den);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float x = acc[m][q];
+      const float y = __fmul_rn(x, rd);
+      const float e = fmaf(-y, den, x);
+      acc[m][q] = __fadd_rn(__fmul_rn(sd, e == 0.f ? y : fmaf(e, rd, y)), mu);
+    }
+#else
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[m][q] = __fadd_rn(__fmul_rn(sd, __fdiv_rn(acc[m][q], den)), mu);
+#endif
 }
 
 template <int SPEC, int LI, int MT, bool TAPE = false>
