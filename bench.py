@@ -375,6 +375,53 @@ class EventList(list):
         self.coarse = coarse
 
 
+def clock_probe(dev, n_mfma: int = 65536, blocks: int = 256) -> dict:
+    """The shader clock the chip holds now (rg_clock_probe, csrc/clock_probe.hip): every wave
+    runs a dependent chain of n_mfma v_mfma_f32_32x32x16_bf16 (32 cycles each on its SIMD,
+    MI355X_MICROARCH.md) stamped with s_memtime / s_memrealtime.  mhz = median over
+    workgroups of shader cycles / wall-clock ticks x the tick rate; mhz_fixed_work = the
+    chain's known cycle count / the launch's HIP-event time (a cross-check)."""
+    import ctypes
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    out = torch.zeros(2 * blocks, dtype=torch.int64, device=dev)
+    sink = torch.empty(4 * blocks, dtype=torch.float32, device=dev)
+    khz = ctypes.c_int(0)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    nat.check(nat.lib().rg_clock_probe(blocks, n_mfma, out.data_ptr(), sink.data_ptr(),
+                                       ctypes.byref(khz), nat.stream_ptr(dev)), 'rg_clock_probe')
+    b.record()
+    torch.cuda.synchronize()
+    o = out.view(blocks, 2).cpu().double()
+    ratio = float((o[:, 0] / o[:, 1].clamp(min=1)).median())
+    ms = a.elapsed_time(b)
+    return {'mhz': round(ratio * khz.value / 1e3, 1), 'wall_clock_khz': khz.value,
+            'mhz_fixed_work': round(n_mfma * 32 / (ms * 1e-3) / 1e6, 1), 'probe_ms': round(ms, 4)}
+
+
+def clock_record(before: dict, after: dict) -> dict:
+    return {'mhz_before': before['mhz'], 'mhz_after': after['mhz'],
+            'mhz_fixed_work_before': before['mhz_fixed_work'],
+            'mhz_fixed_work_after': after['mhz_fixed_work'],
+            'method': 'rg_clock_probe right before and right after the timed region: 256 '
+                      'workgroups x 4 waves, each a dependent chain of 65536 '
+                      'v_mfma_f32_32x32x16_bf16 on register operands; mhz = median s_memtime / '
+                      's_memrealtime x wall-clock rate; mhz_fixed_work = 32 cycles x 65536 / the '
+                      'probe\'s HIP-event time; kernels[*].kcycles = avg_ms x mean(mhz)'}
+
+
+def add_cycles(kern: dict, roof: dict, clock: dict):
+    """Per-kernel cycles at the measured clock (ms x MHz = thousands of cycles)."""
+    mhz = 0.5 * (clock['mhz_before'] + clock['mhz_after'])
+    for rec in kern.values():
+        if 'avg_ms' in rec:
+            rec['kcycles'] = round(rec['avg_ms'] * mhz, 1)
+    if 'avg_ms' in roof:
+        roof['kcycles'] = round(roof['avg_ms'] * mhz, 1)
+        if roof.get('avg_ms_isolated'):
+            roof['kcycles_isolated'] = round(roof['avg_ms_isolated'] * mhz, 1)
+
+
 def event_durations(events):
     """(name:start, name:end) event pairs -> {name: [ms, ...]}"""
     out, open_ = {}, {}
@@ -565,6 +612,7 @@ def train_main(args, world, rank, local):
         losses, acc, gb = trainer.step(batch, labels)
     torch.cuda.synchronize()
     E = int(gb.n_edges_dev.item())
+    clk0 = clock_probe(dev)
     barrier(world)
     torch.cuda.synchronize()
     events = []
@@ -574,6 +622,7 @@ def train_main(args, world, rank, local):
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    clock = clock_record(clk0, clock_probe(dev))
     frames_total = sum_over_ranks(args.frames * args.steps, world)
     rank_frames = per_rank_counts(args.frames * args.steps, world)
     durs = event_durations(events)
@@ -615,8 +664,11 @@ def train_main(args, world, rank, local):
                    'frames_per_rank_timed': rank_frames,
                    'backend': dist.get_backend() if world > 1 else None},
         'last_losses': [round(float(x), 5) for x in losses.cpu()],
+        'applied_steps': trainer.opt.applied_steps(),
         'roofline': roof,
+        'clock': clock,
     }
+    add_cycles({}, roof, clock)
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         line['cpu_baseline'] = cpu_train_baseline(args, cfg)
     if rank == 0:
@@ -897,6 +949,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         # per step (a pair per launch cost ~10 us of stream gap each); --fine-events
         # times every launch
         events = EventList(coarse=not args.fine_events)
+        clk0 = clock_probe(dev)
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -905,6 +958,7 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
         torch.cuda.synchronize()
         barrier(world)
         elapsed = max_over_ranks(time.perf_counter() - t0, world)
+        clock = clock_record(clk0, clock_probe(dev))
         if args.streams > 1:
             pipe = stepper.pipes[(stepper.i - 1) % stepper.depth]
         if args.save_outputs:
@@ -1060,10 +1114,11 @@ def gnn_measure(args, world, dev, cfg, sd, scatter=True):
     F = (84992.0 * N + 118272.0 * E + args.layers * (65536.0 * E + 16384.0 * N) + 99456.0 * N
          + 33024.0 * (E / 2) + 9088.0 * (N / 5))       # SURVEY §8(d) forward flops
     fwd_ms = fwd_elapsed / args.steps * 1e3
+    add_cycles(kern, roof, clock)
     return {'value': frames_total / elapsed, 'elapsed': elapsed, 'ms_step': elapsed / args.steps * 1e3,
             'forward_fps': frames_total / fwd_elapsed, 'forward_ms': fwd_ms, 'E': E,
             'forward_tflops': F / (fwd_ms * 1e-3) / 1e12, 'roof': roof, 'kern': kern,
-            'scatter': sc, 'rank_frames': rank_frames}
+            'scatter': sc, 'rank_frames': rank_frames, 'clock': clock}
 
 
 def main():
@@ -1112,6 +1167,7 @@ def main():
                                   'destination-major CSR, longest-first segment order (standalone; fused into the conv kernels in '
                                   'the step)', bound='hbm', peak_gbs=HBM_PEAK_GBS),
         'kernels': r['kern'],
+        'clock': r['clock'],
     }
     if args.config == 'm' and not args.no_extra:
         # the same run also times BASELINE config 2 (bf16, random init) as an extra key
@@ -1126,7 +1182,7 @@ def main():
                            'ms_per_step': round(r2['ms_step'], 3), 'dtype': 'bf16',
                            'workload': workload_name(a2), 'edges_per_gpu': r2['E'],
                            'forward_only_frames_per_s': round(r2['forward_fps'], 2),
-                           'roofline': r2['roof'], 'kernels': r2['kern']}
+                           'roofline': r2['roof'], 'kernels': r2['kern'], 'clock': r2['clock']}
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region, every world size
         log('cpu baseline')
         cb = cpu_baseline(args, cfg, sd)

@@ -68,6 +68,15 @@ class rg_loss_args(ctypes.Structure):
                 ('w_edge_cls', ctypes.c_float), ('w_obj_cls', ctypes.c_float)]
 
 
+LR_MILESTONES_MAX = 16
+
+
+class rg_lr_schedule(ctypes.Structure):
+    _fields_ = [('n_milestones', ctypes.c_int),
+                ('milestones', ctypes.c_int * LR_MILESTONES_MAX),
+                ('lr', ctypes.c_double * (LR_MILESTONES_MAX + 1))]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
@@ -192,6 +201,11 @@ _SIGNATURES = {
     'rg_loss_graph': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _S, _P]),
     'rg_loss_graph_backward': (_I, [ctypes.POINTER(rg_loss_args), _P, _P, _P, _P, _P, _P]),
     'rg_sgd_step': (_I, [_P, _P, _P, _L, _F, _F, _F, _I, _F, _P]),
+    'rg_clock_probe': (_I, [_I, _I, _P, _P, ctypes.POINTER(_I), _P]),
+    'rg_sgd_step_sched': (_I, [_P, _P, _P, _L, ctypes.POINTER(rg_lr_schedule), _F, _F, _F, _P, _I,
+                               _P, _I, _P]),
+    'rg_adamw_step_sched': (_I, [_P, _P, _P, _P, _L, ctypes.POINTER(rg_lr_schedule), _D, _D, _D,
+                                 _D, _F, _P, _I, _P, _I, _P]),
 }
 
 _lib = None

@@ -256,8 +256,24 @@ __device__ __forceinline__ void channel_norm_ref(f32x16 (&acc)[MT], float mu, fl
   const float den = __fadd_rn(__fsqrt_rn(__fdiv_rn(add_xor32(q0 + q1), (float)(N - 1))), NORM_EPS);
 #if RG_CF32_DIVR
   // x / den as RN(x * r) plus one fma residual correction with r = RN(1 / den): the
-  // correctly rounded quotient (scripts/experiments/div_check.hip: every x in [2^-100, 2^100)
-  // for 64 divisors); e == 0 keeps q itself (a signed zero stays signed)
+  // correctly rounded quotient while the quotient is a normal number (Markstein's result;
+  // scripts/experiments/div_check.hip checks it for 64 chosen divisors over x in
+  // [2^-100, 2^100), not exhaustively); e == 0 keeps q itself (a signed zero stays signed).
+  // A nonzero |x| < 2 FLT_MIN den can give a subnormal quotient, outside that result: a wave
+  // holding one divides with __fdiv_rn instead (wave-uniform branch, practically never taken)
+  bool tiny = false;
+  const float lim = __fmul_rn(2.f * 1.17549435e-38f, den);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tiny |= acc[m][q] != 0.f && fabsf(acc[m][q]) < lim;
+  if (__builtin_amdgcn_ballot_w64(tiny)) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = __fadd_rn(__fmul_rn(sd, __fdiv_rn(acc[m][q], den)), mu);
+    return;
+  }
   const float rd = __fdiv_rn(1.f, den);
 #pragma unroll
   for (int m = 0; m < MT; ++m)

@@ -509,7 +509,8 @@ constexpr int TBUF = 32 * TS2 * 4;  // per wave: one tile's messages while trans
 constexpr int RING = 8;             // per wave: P rows of the last RING destinations (slot = node & 7)
 constexpr int BUF = TBUF + RING * HID * 4;
 constexpr int OFF_BIAS = OFF_BUF + NW * BUF;  // layer 2's bias, accumulator order
-constexpr int LDS = OFF_BIAS + C * 4;
+constexpr int OFF_NZ = OFF_BIAS + C * 4;       // a row of -0.0: the "P" of a slow-path tile
+constexpr int LDS = OFF_NZ + HID * 4;
 static_assert(LDS <= 160 * 1024, "conv_x3_sp LDS");
 constexpr int GMAX = 256;          // workgroups (one per CU)
 constexpr int WMAX = GMAX * NW;    // waves: the table holds WMAX + 1 node boundaries
@@ -669,6 +670,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   stage_lds<sp::FT>(lds, a.w[0], 3 * sp::PLE);
   stage_lds<sp::FT>(lds + sp::OFF_W2, a.w[1], 3 * sp::PL2);
   stage_lds<sp::FT>(lds + sp::OFF_BIAS, a.w[1] + 3 * sp::PL2, C * 4);
+  if (threadIdx.x < HID) ((float*)(lds + sp::OFF_NZ))[threadIdx.x] = -0.f;
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -716,7 +718,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   // dl are loaded (two 16-B pieces per lane, half a wave per row); with at most four new
   // destinations per tile the ring then holds every row the tile needs, and the rows it
   // overwrites (dl - 11 .. dl - 8) belong to no tile still to be initialised.  A tile with
-  // more new destinations takes its P rows straight from memory (fastf = 0).
+  // more new destinations takes its P rows straight from memory (fast = false).
   float* ring = (float*)(bufp + sp::TBUF);
   auto ring_row = [&](int dl, int k) {  // the row loaded by piece k for a last destination dl
     return min(max(dl - 3 + 2 * k + h, 0), a.n_nodes - 1);
@@ -729,23 +731,27 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) *(f32x4*)(ring + (ring_row(dl, k) & (sp::RING - 1)) * HID + 4 * r) = rp[k];
   };
-  // tile accumulator init: Q + P (P from the ring, scaled by fastf: 0 when the slow path has
-  // already added it into q)
+  // tile accumulator init: Q + P with P from the ring -- or, when the slow path has already
+  // added P into q (fast = false: the tile being initialised), from a row of -0.0, which
+  // adds nothing (q + -0 = q, signed zeros included), so no ring row of another node
+  // reaches the sum
+  bool fast = false;  // tile 0's P is in qn
+  const float* nzrow = (const float*)(lds + sp::OFF_NZ);
   auto ring_p = [&](int d, int m, f32x4 (&p)[4]) {  // M-tile m of P[d] from the ring
-    const float* rp = ring + (d & (sp::RING - 1)) * HID + 4 * h + 32 * m;
+    const float* rp = (fast ? ring + (d & (sp::RING - 1)) * HID : nzrow) + 4 * h + 32 * m;
 #pragma unroll
     for (int g = 0; g < 4; ++g) p[g] = *(const f32x4*)(rp + 8 * g);
   };
-  auto init_from = [&](const f32x4 (&p)[4], float fastf, const f32x4 (&q)[16], f32x16& acc, int m) {
+  auto init_from = [&](const f32x4 (&p)[4], const f32x4 (&q)[16], f32x16& acc, int m) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[4 * g + t] = fmaf(p[g][t], fastf, q[4 * m + g][t]);
+      for (int t = 0; t < 4; ++t) acc[4 * g + t] = __fadd_rn(p[g][t], q[4 * m + g][t]);
   };
-  auto init_tile = [&](int d, float fastf, const f32x4 (&q)[16], f32x16& acc, int m) {
+  auto init_tile = [&](int d, const f32x4 (&q)[16], f32x16& acc, int m) {
     f32x4 p[4];
     ring_p(d, m, p);
-    init_from(p, fastf, q, acc, m);
+    init_from(p, q, acc, m);
   };
   // destination-change mask of a tile (bit j: edge j starts a new destination; edges past
   // the range's end carry no bit); dlast = the destination of the previous tile's last edge
@@ -847,9 +853,8 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   ring_store(dl0, rp);
   int q_nn = edge_of(1);
   int d_nn = a.dst[q_nn], s_nn = a.src[q_nn];
-  float fastf = 0.f;  // tile 0's P is in qn
   f32x16 acc1[4];
-  init_tile(d0, fastf, qn, acc1[0], 0);
+  init_tile(d0, qn, acc1[0], 0);
   f32x4 pr[4];  // the ring rows of the next M-tile to initialise, read one sub-chunk ahead
   ring_p(d0, 1, pr);
   X3 b1 = split8(en[0], en[1]);
@@ -888,19 +893,19 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     wait_frags<4>(A1[0]);
     lda1<1>(aw, A1[1]);
     X3 b1n = split8(ev[2], ev[3]);
-    init_from(pr, fastf, qn, acc1[1], 1);
+    init_from(pr, qn, acc1[1], 1);
     ring_p(d_c, 2, pr);
     x3_tile<0>(acc1, A1[0], b1);
     interleave<6, 5>();
     fence();
     float u2[8];
-    init_from(pr, fastf, qn, acc1[2], 2);
+    init_from(pr, qn, acc1[2], 2);
     ring_p(d_c, 3, pr);
     sq_partial(acc2p[0], u2, true);
     x3_tile<1>(acc1, A1[0], b1);
     interleave<6, 6>();
     fence();
-    init_from(pr, fastf, qn, acc1[3], 3);
+    init_from(pr, qn, acc1[3], 3);
     sq_partial(acc2p[1], u2, false);
     x3_tile<2>(acc1, A1[0], b1);
     interleave<6, 6>();
@@ -1021,7 +1026,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     SP_STAMP(1);  // region A
     // the slow path: more than four new destinations in tile t + 1 (never on a kNN graph of
     // degree >= 8): its P rows straight from memory, added into its Q rows
-    const bool fast = dl_n - dl_c <= 4;
+    fast = dl_n - dl_c <= 4;
     if (!fast) {
       asm volatile("");  // a real branch: the compiler would otherwise speculate the loads
       f32x4 pg[16];
@@ -1029,7 +1034,6 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) qn[i] += pg[i];
     }
-    fastf = fast ? 1.f : 0.f;
     SP_STAMP(4);  // the slow path
     // ======== B: tile t - 1's remaining finished destinations (a kNN tile has none); norm
     //          1's scale; layer 2's bias
@@ -1069,7 +1073,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
     RG_SP_C(3, 1, b2, ring_store(dl_n, rp))
     RG_SP_C(4, 0, b2n, (void)0)
     RG_SP_C(5, 1, b2, ring_p(d_nn, 0, pr))
-    RG_SP_C(6, 0, b2n, init_from(pr, fastf, qn, acc1[0], 0))
+    RG_SP_C(6, 0, b2n, init_from(pr, qn, acc1[0], 0))
 #undef RG_SP_C
     SP_STAMP(3);  // C0 - C6
     wait_frags<2>(A2[1]);

@@ -900,6 +900,79 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
   p[i] = fmaf(-lr, b, p[i]);                          // p.add_(buf, alpha=-lr)
 }
 
+// ------------------------------------------------------------------ scheduled steps
+// train_model's skip_batch + MultiStepLR on the device (rg_sgd_step_sched).  Every thread
+// reads the applied-step counter k = state[parity] and the (all-reduced) losses; thread 0
+// of block 0 writes k or k + 1 to state[parity ^ 1], a slot no thread of this launch reads.
+struct StepCtl {
+  bool skip;
+  int k;        // applied steps before this one
+  double lr;
+};
+
+__device__ __forceinline__ StepCtl step_control(const rg_lr_schedule& s, const float* losses,
+                                                int n_losses, int* state, int parity) {
+  StepCtl c;
+  c.k = state[parity];
+  c.skip = false;
+  if (losses) {
+    float t = losses[0];                      // total_loss = l0 + l1 + l2 + l3 (training.py:75)
+    for (int i = 1; i < n_losses; ++i) t = __fadd_rn(t, losses[i]);
+    c.skip = isnan(t);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) state[parity ^ 1] = c.k + (c.skip ? 0 : 1);
+  double lr = s.lr[0];
+#pragma unroll
+  for (int j = 0; j < RG_LR_MILESTONES_MAX; ++j)
+    if (j < s.n_milestones && s.milestones[j] <= c.k) lr = s.lr[j + 1];
+  c.lr = lr;
+  return c;
+}
+
+__global__ void sgd_sched_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                 float* __restrict__ buf, long n, rg_lr_schedule s,
+                                 float momentum, float wd, float gscale,
+                                 const float* __restrict__ losses, int n_losses, int* state,
+                                 int parity) {
+  const StepCtl c = step_control(s, losses, n_losses, state, parity);
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c.skip || i >= n) return;
+  const float lr = (float)c.lr;
+  const float d = fmaf(wd, p[i], __fmul_rn(g[i], gscale));
+  const float b = c.k == 0 ? d : __fadd_rn(__fmul_rn(momentum, buf[i]), d);
+  buf[i] = b;
+  p[i] = fmaf(-lr, b, p[i]);
+}
+
+// torch.optim.AdamW's foreach update (torch/optim/adam.py _multi_tensor_adam, decoupled
+// weight decay): the scalars are formed in double as Python forms them, the tensor ops in
+// float32 as the foreach kernels run them
+__global__ void adamw_sched_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                   rg_lr_schedule s, double beta1, double beta2, double eps,
+                                   double wd, float gscale, const float* __restrict__ losses,
+                                   int n_losses, int* state, int parity) {
+  const StepCtl c = step_control(s, losses, n_losses, state, parity);
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c.skip || i >= n) return;
+  const double t = (double)(c.k + 1);
+  const double bc1 = 1.0 - pow(beta1, t);
+  const double bc2 = 1.0 - pow(beta2, t);
+  const float step_size = (float)(-(c.lr / bc1));
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float decay = (float)(1.0 - c.lr * wd);
+  const float gi = __fmul_rn(g[i], gscale);
+  const float pi = __fmul_rn(p[i], decay);                    // p.mul_(1 - lr wd)
+  const float w1 = (float)(1.0 - beta1);
+  const float mi = m[i];
+  const float mn = fmaf(w1, __fsub_rn(gi, mi), mi);            // lerp_(g, 1 - beta1), w < 0.5
+  const float vn = fmaf(__fmul_rn((float)(1.0 - beta2), gi), gi, __fmul_rn(v[i], (float)beta2));
+  m[i] = mn;
+  v[i] = vn;
+  const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(vn), bc2_sqrt), (float)eps);
+  p[i] = fmaf(step_size, __fdiv_rn(mn, den), pi);              // addcdiv_(m, den, -step)
+}
+
 }  // namespace train
 }  // namespace rg
 
@@ -1112,6 +1185,50 @@ extern "C" int rg_sgd_step(float* param, const float* grad, float* momentum_buf,
   if (n <= 0) return RG_OK;
   sgd_kernel<<<ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(
       param, grad, momentum_buf, n, lr, momentum, weight_decay, first_step, grad_scale);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+static int check_sched(const rg_lr_schedule* s, const float* losses, int n_losses,
+                       const int* step_state, int parity) {
+  RG_REQUIRE(s && step_state, RG_ERR_ARG, "optimizer step: schedule and step_state required");
+  RG_REQUIRE(s->n_milestones >= 0 && s->n_milestones <= RG_LR_MILESTONES_MAX, RG_ERR_ARG,
+             "optimizer step: %d milestones (max %d)", s->n_milestones, RG_LR_MILESTONES_MAX);
+  for (int j = 0; j < s->n_milestones; ++j)
+    RG_REQUIRE(s->milestones[j] >= 0 && (j == 0 || s->milestones[j] > s->milestones[j - 1]),
+               RG_ERR_ARG, "optimizer step: milestones must be distinct, ascending, >= 0");
+  RG_REQUIRE(!losses || (n_losses >= 1 && n_losses <= 16), RG_ERR_ARG,
+             "optimizer step: n_losses %d", n_losses);
+  RG_REQUIRE(parity == 0 || parity == 1, RG_ERR_ARG, "optimizer step: parity %d", parity);
+  return RG_OK;
+}
+
+extern "C" int rg_sgd_step_sched(float* param, const float* grad, float* momentum_buf, long n,
+                                 const rg_lr_schedule* sched, float momentum, float weight_decay,
+                                 float grad_scale, const float* losses, int n_losses,
+                                 int* step_state, int parity, void* stream) {
+  const int rc = check_sched(sched, losses, n_losses, step_state, parity);
+  if (rc != RG_OK) return rc;
+  // one block even for n = 0: the counter still advances (an empty model's step counts)
+  sgd_sched_kernel<<<n > 0 ? ceil_div(n, 256) : 1, 256, 0, (hipStream_t)stream>>>(
+      param, grad, momentum_buf, n, *sched, momentum, weight_decay, grad_scale, losses,
+      n_losses, step_state, parity);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_adamw_step_sched(float* param, const float* grad, float* exp_avg,
+                                   float* exp_avg_sq, long n, const rg_lr_schedule* sched,
+                                   double beta1, double beta2, double eps, double weight_decay,
+                                   float grad_scale, const float* losses, int n_losses,
+                                   int* step_state, int parity, void* stream) {
+  const int rc = check_sched(sched, losses, n_losses, step_state, parity);
+  if (rc != RG_OK) return rc;
+  RG_REQUIRE(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0,
+             RG_ERR_ARG, "rg_adamw_step_sched: betas / eps");
+  adamw_sched_kernel<<<n > 0 ? ceil_div(n, 256) : 1, 256, 0, (hipStream_t)stream>>>(
+      param, grad, exp_avg, exp_avg_sq, n, *sched, beta1, beta2, eps, weight_decay, grad_scale,
+      losses, n_losses, step_state, parity);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -334,12 +334,28 @@ class Model_Training(nn.Module):
         if self._train_engine is not None:
             self._train_engine.invalidate()
 
-    def fused_sgd(self, lr: float, momentum: float = 0.9, weight_decay: float = 0.0):
+    def fused_sgd(self, lr: float, momentum: float = 0.9, weight_decay: float = 0.0,
+                  milestones=(), gamma: float = 0.1):
         """torch.optim.SGD(params, momentum, lr, weight_decay) (set_param_for_training_gnn.py:46)
-        as training.FusedSGD: one rg_sgd_step launch; step(flat_grad) after backward."""
+        as training.FusedSGD: one rg_sgd_step_sched launch; step(flat_grad) after backward
+        (optionally with MultiStepLR milestones, set_param_for_training_gnn.py:51-56)."""
         from .training import FusedSGD
         return FusedSGD([p for p in self.parameters()], lr, momentum, weight_decay,
-                        on_update=self.invalidate_plans)
+                        on_update=self.invalidate_plans, milestones=milestones, gamma=gamma)
+
+    def fused_optimizer(self, optim: str, lr: float, weight_decay: float, momentum: float = 0.9,
+                        milestones=(), gamma: float = 0.1):
+        """set_param_for_training_gnn.py:43-56: 'sgd' (momentum 0.9) or 'adamw', each with
+        the MultiStepLR schedule, as one native launch per step."""
+        from .training import FusedAdamW, FusedSGD
+        params = [p for p in self.parameters()]
+        if optim == 'sgd':
+            return FusedSGD(params, lr, momentum, weight_decay, on_update=self.invalidate_plans,
+                            milestones=milestones, gamma=gamma)
+        if optim == 'adamw':
+            return FusedAdamW(params, lr, weight_decay, on_update=self.invalidate_plans,
+                              milestones=milestones, gamma=gamma)
+        raise ValueError(f'optim {optim!r}: the reference configures sgd or adamw')
 
     def _labels(self, labels, dev):
         from .loss import check_class_labels

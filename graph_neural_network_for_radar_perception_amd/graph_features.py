@@ -213,11 +213,21 @@ class GraphBatch:
     # count, written by rg_csr_clamp itself; the event after it); None when the capacity was
     # checked on the host (or is exact, kNN)
     need: Optional[tuple] = None
+    # the completion event of the step that built this graph and ran its forward on a stream
+    # of its own (PipelinedSteps(concurrent=True)); readers wait on it (wait_ready)
+    done: Optional[object] = None
+
+    def wait_ready(self):
+        """Make the caller's current stream wait for this graph's step (concurrent pipelines
+        write the graph and the outputs on a private stream)."""
+        if self.done is not None:
+            torch.cuda.current_stream(self.row_ptr.device).wait_event(self.done)
 
     def check_capacity(self):
         """Raise if this graph was cut to its capacity (a radius graph built without a host
         sync whose edges outgrew the capacity that sufficed before): every output computed
         from it is invalid.  Host sync."""
+        self.wait_ready()
         if self.need is not None:
             host, ev = self.need
             ev.synchronize()

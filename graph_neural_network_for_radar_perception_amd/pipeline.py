@@ -63,7 +63,8 @@ class RadarGNNPipeline:
     @staticmethod
     def trim(gb: GraphBatch, out: engine.ForwardOutputs):
         """Host-synchronising view of the outputs at their true sizes (raises if a radius
-        graph built without a host sync outgrew its capacity: GraphBatch.check_capacity)."""
+        graph built without a host sync outgrew its capacity: GraphBatch.check_capacity).  A
+        concurrent pipeline's step is waited for first (GraphBatch.done)."""
         gb.check_capacity()
         U = int(gb.graph.n_pairs_dev.item())
         return out.node_cls, out.node_reg, out.link_cls[:U], out.obj_cls
@@ -92,9 +93,10 @@ class PipelinedSteps:
         """concurrent: each pipeline runs its build AND its forward on a stream of its own,
         so the forwards of consecutive steps overlap too (latency-bound single-frame steps:
         one 20 000-node frame leaves the persistent kernels a few tiles per wave); the
-        caller's stream then waits for nothing -- synchronise the device (or each step's
-        ``done`` event) before reading an output.  conv_waves: as RadarGNNPipeline's (default
-        with concurrent: CONCURRENT_CONV_WAVES)."""
+        caller's stream then waits for nothing -- the step's GraphBatch carries its completion
+        event (``gb.done``; trim / check_capacity / edge_index wait on it, and
+        ``gb.wait_ready()`` makes the current stream wait before reading an output).
+        conv_waves: as RadarGNNPipeline's (default with concurrent: CONCURRENT_CONV_WAVES)."""
         if conv_waves is None and concurrent:
             conv_waves = CONCURRENT_CONV_WAVES
         self.pipes = [RadarGNNPipeline(model, cfg, dtype, mode=mode, eps2=eps2,
@@ -128,6 +130,7 @@ class PipelinedSteps:
             out = self.pipes[p].forward(batch, gb, events)
             ev = torch.cuda.Event()
             ev.record(st)
+        gb.done = ev          # trim / check_capacity / edge_index wait on it before reading
         self.done[p] = ev
         self.last_done = ev
         self.keep[p] = (gb, out)

@@ -16,7 +16,8 @@ Everything runs in float32 (the reference trains in f32) on the HIP library:
             x_i = x[dst] is a segment sum over the destination-major CSR, x_j = x[src]
             and the link pairs' x[i] + x[j] are sums over incidence lists),
             rg_segment_max_backward (object head)
-  update    rg_sgd_step on the flat parameter / gradient buffers (FusedSGD)
+  update    rg_sgd_step_sched / rg_adamw_step_sched on the flat parameter / gradient buffers
+            (FusedSGD / FusedAdamW: skip_batch and MultiStepLR evaluated on the device)
 
 This module only sequences calls and owns buffers.  The batch of frames is one
 disjoint-union graph, as in the forward (engine.forward_batched): every operator is per
@@ -43,6 +44,8 @@ TAPE_F32_FAST = True
 DX_F32_FAST = True
 # after an optimizer step, re-pack every f32 image in place in one launch (False: per chain)
 REPACK_JOBS = True
+# loss values appended to the gradient bucket (loss_node_cls, _node_reg, _edge_cls, _obj_cls)
+N_LOSS_SLOTS = 4
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -409,10 +412,14 @@ class TrainEngine:
         self.cls_head = mk([pc.pred_cls.head[0], pc.pred_cls.head[1]])
         # layer / group normalisation anywhere: the tape needs each frame's row ranges
         self.frame_norm = any(c.frame_norm for c in self.chains())
-        # flat gradient buffer: one view per parameter (one bucket for the DDP all-reduce)
+        # flat gradient buffer: one view per parameter, then the step's four loss values --
+        # the ONE bucket of the DDP all-reduce, so every rank sees the summed losses and
+        # skips a NaN batch together (training.py:40-45)
         self.params = [p for p in model_training.parameters()]
         n = sum(p.numel() for p in self.params)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.flat_bucket = torch.zeros(n + N_LOSS_SLOTS, dtype=torch.float32, device=self.device)
+        self.flat_grad = self.flat_bucket[:n]
+        self.loss_slots = self.flat_bucket[n:]
         self.grads: Dict[int, torch.Tensor] = {}
         o = 0
         for p in self.params:
@@ -747,13 +754,41 @@ def train_step_losses(engine_: TrainEngine, batch) -> torch.Tensor:
     return _TrainStep.apply(engine_, batch, *engine_.params)
 
 
-class FusedSGD:
-    """torch.optim.SGD(params, lr, momentum, weight_decay) (set_param_for_training_gnn.py:46)
-    as one rg_sgd_step launch over a flat copy of the parameters.  The module's
-    parameters become views of the flat buffer, so the model sees every update."""
+def multistep_lr_table(base_lr: float, milestones, gamma: float = 0.1):
+    """torch.optim.lr_scheduler.MultiStepLR's learning rates as a table: (distinct milestones
+    >= 0 ascending, lr[j] = the lr after j of them).  Applied step k (0-based) uses
+    lr[bisect_right(ms, k)].  The values are chained in double exactly as the scheduler does
+    (group['lr'] * gamma ** multiplicity at each milestone; a milestone of 0 fires when the
+    scheduler is built, negative ones never fire)."""
+    from collections import Counter
+    cnt = Counter(int(m) for m in milestones)
+    ms = sorted(m for m in cnt if m >= 0)
+    if len(ms) > nat.LR_MILESTONES_MAX:
+        raise ValueError(f'{len(ms)} distinct milestones > {nat.LR_MILESTONES_MAX}')
+    lrs = [float(base_lr)]
+    for m in ms:
+        lrs.append(lrs[-1] * gamma ** cnt[m])
+    return ms, lrs
 
-    def __init__(self, params, lr: float, momentum: float = 0.9, weight_decay: float = 0.0,
-                 on_update=None):
+
+def reference_milestones(cfg, starting_iter_num: int = 0):
+    """set_param_for_training_gnn.py:51-56: decay x0.1 at 50 % and 80 % of max_train_iter,
+    shifted by the iteration training resumes from."""
+    return [int(0.5 * cfg.max_train_iter - starting_iter_num),
+            int(0.8 * cfg.max_train_iter - starting_iter_num)]
+
+
+class _FlatOptimizer:
+    """Parameters flattened into one float32 buffer (the module's parameters become views of
+    it, so the model sees every update) and stepped by one native launch, with
+    train_model's per-iteration rules on the device (rg_sgd_step_sched /
+    rg_adamw_step_sched): a step whose (all-reduced) total loss is NaN is skipped
+    (skip_batch, training.py:40-45, 79-85) and the learning rate follows MultiStepLR over the
+    APPLIED steps (set_param_for_training_gnn.py:51-56, stepped at training.py:83-84).  The
+    applied-step counter lives on the device, so no step synchronises the host."""
+
+    def __init__(self, params, lr: float, milestones=(), gamma: float = 0.1, on_update=None,
+                 n_state: int = 1):
         self.params = list(params)
         self.on_update = on_update
         dev = self.params[0].device
@@ -766,20 +801,90 @@ class FusedSGD:
                 self.flat[o:o + k].copy_(p.reshape(-1))
                 p.data = self.flat[o:o + k].view_as(p)
                 o += k
-        self.buf = torch.zeros_like(self.flat)
-        self.lr, self.momentum, self.weight_decay = lr, momentum, weight_decay
-        self.steps = 0
+        self.state_bufs = [torch.zeros_like(self.flat) for _ in range(n_state)]
+        self.lr = lr
+        self.milestones, self.gamma = list(milestones), gamma
+        self.step_state = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._parity = 0
+        self.steps = 0          # launches (applied + skipped)
 
-    def step(self, flat_grad: torch.Tensor, grad_scale: float = 1.0):
-        lib = nat.lib()
-        nat.check(lib.rg_sgd_step(self.flat.data_ptr(), flat_grad.data_ptr(), self.buf.data_ptr(),
-                                  self.flat.numel(), float(self.lr), float(self.momentum),
-                                  float(self.weight_decay), int(self.steps == 0),
-                                  float(grad_scale), nat.stream_ptr(self.flat.device)),
-                  'rg_sgd_step')
+    def schedule(self) -> 'nat.rg_lr_schedule':
+        ms, lrs = multistep_lr_table(self.lr, self.milestones, self.gamma)
+        s = nat.rg_lr_schedule()
+        s.n_milestones = len(ms)
+        for j, m in enumerate(ms):
+            s.milestones[j] = m
+        for j, v in enumerate(lrs):
+            s.lr[j] = v
+        return s
+
+    def lr_at(self, k: int) -> float:
+        """The lr applied step k runs with (MultiStepLR's value after k scheduler steps)."""
+        import bisect
+        ms, lrs = multistep_lr_table(self.lr, self.milestones, self.gamma)
+        return lrs[bisect.bisect_right(ms, int(k))]
+
+    def applied_steps(self) -> int:
+        """Steps applied so far (skipped ones excluded); reading it synchronises."""
+        return int(self.step_state[self._parity].item())
+
+    def _launch(self, flat_grad, grad_scale, losses):
+        raise NotImplementedError
+
+    def step(self, flat_grad: torch.Tensor, grad_scale: float = 1.0,
+             losses: Optional[torch.Tensor] = None):
+        """One update from flat_grad (x grad_scale); losses: device f32 [n] whose sum decides
+        skip_batch (None: never skip)."""
+        if flat_grad.numel() < self.flat.numel():
+            raise ValueError(f'flat_grad has {flat_grad.numel()} < {self.flat.numel()} entries')
+        if losses is not None and (losses.dtype != torch.float32 or not losses.is_contiguous()):
+            raise TypeError('losses must be a contiguous float32 device tensor')
+        self._launch(flat_grad, float(grad_scale), losses)
+        self._parity ^= 1
         if self.on_update is not None:   # weights changed outside torch: re-pack the plans
             self.on_update()
         self.steps += 1
+
+
+class FusedSGD(_FlatOptimizer):
+    """torch.optim.SGD(params, lr, momentum, weight_decay) (set_param_for_training_gnn.py:46)
+    + MultiStepLR(milestones, gamma) as one rg_sgd_step_sched launch per step."""
+
+    def __init__(self, params, lr: float, momentum: float = 0.9, weight_decay: float = 0.0,
+                 on_update=None, milestones=(), gamma: float = 0.1):
+        super().__init__(params, lr, milestones, gamma, on_update, n_state=1)
+        self.buf = self.state_bufs[0]
+        self.momentum, self.weight_decay = momentum, weight_decay
+
+    def _launch(self, flat_grad, grad_scale, losses):
+        s = self.schedule()
+        nat.check(nat.lib().rg_sgd_step_sched(
+            self.flat.data_ptr(), flat_grad.data_ptr(), self.buf.data_ptr(), self.flat.numel(),
+            ctypes.byref(s), float(self.momentum), float(self.weight_decay), grad_scale,
+            nat.ptr(losses), losses.numel() if losses is not None else 0,
+            self.step_state.data_ptr(), self._parity, nat.stream_ptr(self.flat.device)),
+            'rg_sgd_step_sched')
+
+
+class FusedAdamW(_FlatOptimizer):
+    """torch.optim.AdamW(params, lr, weight_decay) (set_param_for_training_gnn.py:47; betas,
+    eps at torch's defaults) + MultiStepLR as one rg_adamw_step_sched launch per step."""
+
+    def __init__(self, params, lr: float, weight_decay: float = 0.01, betas=(0.9, 0.999),
+                 eps: float = 1e-8, on_update=None, milestones=(), gamma: float = 0.1):
+        super().__init__(params, lr, milestones, gamma, on_update, n_state=2)
+        self.exp_avg, self.exp_avg_sq = self.state_bufs
+        self.betas, self.eps, self.weight_decay = tuple(betas), eps, weight_decay
+
+    def _launch(self, flat_grad, grad_scale, losses):
+        s = self.schedule()
+        nat.check(nat.lib().rg_adamw_step_sched(
+            self.flat.data_ptr(), flat_grad.data_ptr(), self.exp_avg.data_ptr(),
+            self.exp_avg_sq.data_ptr(), self.flat.numel(), ctypes.byref(s),
+            float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.weight_decay),
+            grad_scale, nat.ptr(losses), losses.numel() if losses is not None else 0,
+            self.step_state.data_ptr(), self._parity, nat.stream_ptr(self.flat.device)),
+            'rg_adamw_step_sched')
 
 
 # ------------------------------------------------------------------ data parallel
@@ -806,17 +911,29 @@ def broadcast_parameters(flat: torch.Tensor, world: int, src: int = 0):
 class RadarGNNTrainer:
     """One data-parallel training iteration (training.py:66-85 for one rank's batch):
     graph build + features (pipeline) -> forward tape + Loss_Graph -> backward ->
-    gradient all-reduce -> fused SGD.  Labels are per batch on the device (node_class,
-    node_offsets, edge_class in link-pair order, cluster_labels)."""
+    gradient all-reduce -> fused optimizer step.  Labels are per batch on the device
+    (node_class, node_offsets, edge_class in link-pair order, cluster_labels).
+
+    train_model's loop rules hold across ranks without a host sync: the step's losses ride
+    in the gradient bucket's tail, so after the all-reduce every rank holds their sum and
+    the optimizer kernel skips the update on every rank when it is NaN (skip_batch,
+    training.py:40-45, 79-85); the lr follows MultiStepLR at 50 % / 80 % of max_train_iter
+    (set_param_for_training_gnn.py:51-56) over the applied steps; cfg.optim picks SGD
+    (momentum 0.9) or AdamW (set_param_for_training_gnn.py:46-47)."""
 
     def __init__(self, model_training, cfg, world: int = 1, lr: Optional[float] = None,
-                 momentum: float = 0.9, weight_decay: Optional[float] = None):
+                 momentum: float = 0.9, weight_decay: Optional[float] = None,
+                 optim: Optional[str] = None, milestones=None, starting_iter_num: int = 0):
         self.model = model_training
         self.cfg = cfg
         self.world = world
         lr = cfg.learning_rate if lr is None else lr
         wd = cfg.weight_decay if weight_decay is None else weight_decay
-        self.opt = model_training.fused_sgd(lr, momentum, wd)
+        optim = getattr(cfg, 'optim', 'sgd') if optim is None else optim
+        if milestones is None:
+            milestones = reference_milestones(cfg, starting_iter_num)
+        self.opt = model_training.fused_optimizer(optim, lr, wd, momentum=momentum,
+                                                  milestones=milestones)
         broadcast_parameters(self.opt.flat, world)
         model_training.invalidate_plans()
         self.engine = model_training.train_engine()
@@ -843,6 +960,7 @@ class RadarGNNTrainer:
         mark('train_backward:start')
         self.engine.backward(tape, self.ones)
         mark('train_backward:end')
-        scale = allreduce_gradients(self.engine.flat_grad, self.world)
-        self.opt.step(self.engine.flat_grad, grad_scale=scale)
+        self.engine.loss_slots.copy_(losses)
+        scale = allreduce_gradients(self.engine.flat_bucket, self.world)
+        self.opt.step(self.engine.flat_grad, grad_scale=scale, losses=self.engine.loss_slots)
         return losses, acc, gb

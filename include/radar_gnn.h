@@ -789,6 +789,54 @@ int rg_sgd_step(float* param, const float* grad, float* momentum_buf, long n, fl
                 float momentum, float weight_decay, int first_step, float grad_scale,
                 void* stream);
 
+/* The optimizer step of the reference's train_model loop (training.py:66-85) with its two
+ * host-side rules evaluated on the device, so a data-parallel step needs no host sync:
+ *  - skip_batch (training.py:40-45, 79-85): when losses[0] + ... + losses[n_losses-1]
+ *    (float32, left to right) is NaN, param and the optimizer state are left untouched and
+ *    the step is not counted.  The DDP trainer all-reduces the losses in the same bucket as
+ *    the gradients, so a NaN on any rank reaches every rank and all ranks skip together.
+ *    losses = NULL: never skip.
+ *  - MultiStepLR (set_param_for_training_gnn.py:51-56, stepped only after an applied step,
+ *    training.py:83-84): applied step k (0-based) uses lr[j], j = the number of distinct
+ *    milestones ms[i] <= k.  The host fills lr[] exactly as the scheduler chains it (in
+ *    double: lr[j] = lr[j-1] * gamma ** multiplicity(ms[j-1])); milestones < 0 never fire
+ *    and are dropped by the host, milestone 0 fires before the first step.
+ * step_state: device int[2], the applied-step counter ping-ponged between launches: the
+ * launch reads step_state[parity] and writes step_state[parity ^ 1]; the caller flips
+ * parity every launch (both zero before the first).  The first applied step (k = 0)
+ * initialises the momentum buffer (torch's momentum_buffer = None). */
+#define RG_LR_MILESTONES_MAX 16
+typedef struct rg_lr_schedule {
+  int n_milestones;                        /* distinct, ascending, >= 0 */
+  int milestones[RG_LR_MILESTONES_MAX];
+  double lr[RG_LR_MILESTONES_MAX + 1];
+} rg_lr_schedule;
+int rg_sgd_step_sched(float* param, const float* grad, float* momentum_buf, long n,
+                      const rg_lr_schedule* sched, float momentum, float weight_decay,
+                      float grad_scale, const float* losses, int n_losses, int* step_state,
+                      int parity, void* stream);
+/* torch.optim.AdamW (set_param_for_training_gnn.py:47; amsgrad off, the foreach update
+ * order) with the same skip / schedule / step_state rules (the hyper-parameters are
+ * doubles, as Python holds them; each scalar is formed in double, then rounded): t = k + 1;
+ * p *= 1 - lr wd; m = lerp(m, g, 1 - beta1); v = beta2 v + (1 - beta2) g g;
+ * p += -(lr / (1 - beta1^t)) m / (sqrt(v) / sqrt(1 - beta2^t) + eps). */
+int rg_adamw_step_sched(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        long n, const rg_lr_schedule* sched, double beta1, double beta2,
+                        double eps, double weight_decay, float grad_scale, const float* losses,
+                        int n_losses,
+                        int* step_state, int parity, void* stream);
+
+/* ---------------------------------------------------------------- diagnostics */
+
+/* Shader-clock calibration (bench.py; no product path calls it): n_blocks workgroups of
+ * 256 threads, each wave one dependent chain of n_mfma v_mfma_f32_32x32x16_bf16 on register
+ * operands, stamped with s_memtime / s_memrealtime around the chain.  out: device u64
+ * [n_blocks][2] = (shader cycles, wall-clock ticks) of each workgroup's wave 0; sink: device
+ * f32 [n_blocks * 4] (the chains' results); *wall_clock_khz_host = the wall-clock tick rate
+ * (hipDeviceAttributeWallClockRate).  clock = cycles / ticks x rate. */
+int rg_clock_probe(int n_blocks, int n_mfma, unsigned long long* out, float* sink,
+                   int* wall_clock_khz_host, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1151,9 +1151,10 @@ def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent, dtype
     builds and forwards of different steps really overlap; every step's batch is uploaded
     asynchronously from pinned memory on the caller's stream right before the step, so the
     build has to wait for that upload (FrameBatch.ready), not for the previous forward.
-    concurrent: each in-flight batch's build and forward on a stream of its own (the caller
-    waits on the step's completion event before copying its outputs); also the fp16 path of
-    BASELINE config 5 (the preset that runs concurrent)."""
+    concurrent: each in-flight batch's build and forward on a stream of its own, three
+    pipelines (the C5 preset's depth), the caller's stream never waiting on a step, so up to
+    three builds + forwards run at once (each step's outputs are copied on its own stream);
+    also the fp16 path of BASELINE config 5 (the preset that runs concurrent)."""
     from graph_neural_network_for_radar_perception_amd import _native as nat
     from graph_neural_network_for_radar_perception_amd import synthetic
     from graph_neural_network_for_radar_perception_amd.graph_features import FrameBatch
@@ -1185,22 +1186,28 @@ def test_pipelined_steps_bit_identical(cuda_device, mode_name, concurrent, dtype
                 gb, out = seq.step(b)
             torch.cuda.synchronize()
             ref.append([t.clone() for t in RadarGNNPipeline.trim(gb, out)])
-        run = PipelinedSteps(m, cfg, dtype, mode=mode, eps2=4.0, concurrent=concurrent)
+        # concurrent: three pipelines (the C5 preset's depth), so three forwards overlap
+        run = PipelinedSteps(m, cfg, dtype, mode=mode, eps2=4.0, concurrent=concurrent,
+                             depth=3 if concurrent else 2)
         if mode == nat.GRAPH_RADIUS:
             # each pipeline's first radius build checks its capacity on the host (one sync);
-            # warm both so the six steps below run without any
-            for i in range(2):
-                run.step(FrameBatch.from_frames(*host[i], device=dev))
+            # warm every pipeline so the six steps below run without any
+            for i in range(run.depth):
+                run.step(FrameBatch.from_frames(*host[i % 2], device=dev))
             torch.cuda.synchronize()
         got, keep = [], []
         for i in range(6):
             batch = FrameBatch.from_frames(*host[i % 2], device=dev, pinned=True)
             gb, out = run.step(batch)
-            if concurrent:
-                torch.cuda.current_stream().wait_event(run.last_done)
             U = ref[i % 2][2].shape[0]
-            got.append([out.node_cls.clone(), out.node_reg.clone(), out.link_cls[:U].clone(),
-                        out.obj_cls.clone(), gb.graph.n_pairs_dev.clone()])
+            # concurrent: the copies are enqueued on the step's own stream right behind it
+            # (in order before that pipeline's next step overwrites its buffers); the caller's
+            # stream never waits, so the next upload and step start while this one runs
+            ctx = (torch.cuda.stream(run.streams[(run.i - 1) % run.depth]) if concurrent
+                   else torch.cuda.stream(torch.cuda.current_stream()))
+            with ctx:
+                got.append([out.node_cls.clone(), out.node_reg.clone(), out.link_cls[:U].clone(),
+                            out.obj_cls.clone(), gb.graph.n_pairs_dev.clone()])
             keep.append(gb)
             del batch                      # freed before its build ran: record_stream keeps it
         torch.cuda.synchronize()
