@@ -29,9 +29,12 @@ __global__ __launch_bounds__(256) void clock_probe_kernel(int n_mfma,
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_sched_barrier(0);
-  // (|a b| summed over 16 products per step stays ~2: 10^5 steps cannot overflow f32)
-#pragma unroll 16
-  for (int i = 0; i < n_mfma; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  // (|a b| summed over 16 products per step stays ~2: 10^5 steps cannot overflow f32); 64
+  // MFMAs per loop trip, so the loop's scalar compare and branch sit under the chain
+  for (int i = 0; i < n_mfma; i += 64) {
+#pragma unroll
+    for (int j = 0; j < 64; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
   __builtin_amdgcn_sched_barrier(0);
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -52,7 +55,8 @@ __global__ __launch_bounds__(256) void clock_probe_kernel(int n_mfma,
 
 extern "C" int rg_clock_probe(int n_blocks, int n_mfma, unsigned long long* out, float* sink,
                               int* wall_clock_khz_host, void* stream) {
-  RG_REQUIRE(n_blocks >= 1 && n_blocks <= 65536 && n_mfma >= 1 && out && sink, RG_ERR_ARG,
+  RG_REQUIRE(n_blocks >= 1 && n_blocks <= 65536 && n_mfma >= 64 && n_mfma % 64 == 0 && out && sink,
+             RG_ERR_ARG,
              "rg_clock_probe: n_blocks %d n_mfma %d", n_blocks, n_mfma);
   if (wall_clock_khz_host) {
     int dev = 0;

@@ -829,8 +829,9 @@ int rg_adamw_step_sched(float* param, const float* grad, float* exp_avg, float* 
 /* ---------------------------------------------------------------- diagnostics */
 
 /* Shader-clock calibration (bench.py; no product path calls it): n_blocks workgroups of
- * 256 threads, each wave one dependent chain of n_mfma v_mfma_f32_32x32x16_bf16 on register
- * operands, stamped with s_memtime / s_memrealtime around the chain.  out: device u64
+ * 256 threads, each wave one dependent chain of n_mfma (a multiple of 64)
+ * v_mfma_f32_32x32x16_bf16 on register operands, stamped with s_memtime / s_memrealtime
+ * around the chain.  out: device u64
  * [n_blocks][2] = (shader cycles, wall-clock ticks) of each workgroup's wave 0; sink: device
  * f32 [n_blocks * 4] (the chains' results); *wall_clock_khz_host = the wall-clock tick rate
  * (hipDeviceAttributeWallClockRate).  clock = cycles / ticks x rate. */

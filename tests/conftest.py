@@ -180,20 +180,27 @@ def grad_headroom(rows) -> float:
     return max([ours / grad_bound(orc) for name, ours, orc, _, _ in rows] or [0.0])
 
 
-def grad_report(test: str, rows) -> float:
+def grad_report(test: str, rows, as_given=None) -> float:
     """Gradient headroom of one test: rows = (tensor, ours, orc, raw, env_share) with ours the
     error max|g - g64| / max|g64| the bound is applied to (beyond the kink envelope where the
     test has one), orc the float32 oracle's, raw the error before the envelope, env_share the
-    envelope's largest element / max|g64|.  Appends one JSON line per test to $RG_GRAD_REPORT
-    (when set) with every tensor's ours / bound; returns the worst ours / bound."""
+    envelope's largest element / max|g64|.  as_given: {tensor: the error of the single
+    as-given float32 evaluation} where orc is a maximum over several (reported beside it with
+    ours over ITS bound).  Appends one JSON line per test to $RG_GRAD_REPORT (when set) with
+    every tensor's ours / bound; returns the worst ours / bound."""
     out = []
     worst = 0.0
     for name, ours, orc, raw, env in rows:
         b = grad_bound(orc)
         r = ours / b
         worst = max(worst, r)
-        out.append({'tensor': name, 'err': ours, 'err_before_envelope': raw, 'envelope': env,
-                    'f32_oracle_err': orc, 'bound': b, 'of_bound': r})
+        rec = {'tensor': name, 'err': ours, 'err_before_envelope': raw, 'envelope': env,
+               'f32_oracle_err': orc, 'bound': b, 'of_bound': r}
+        if as_given is not None:
+            bg = grad_bound(as_given[name])
+            rec.update(f32_oracle_err_as_given=as_given[name], bound_as_given=bg,
+                       of_bound_as_given=ours / bg)
+        out.append(rec)
     path = os.environ.get('RG_GRAD_REPORT')
     if path:
         out.sort(key=lambda x: -x['of_bound'])
