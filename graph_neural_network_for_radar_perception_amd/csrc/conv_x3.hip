@@ -117,6 +117,7 @@ struct Args {
   int n_nodes, n_blocks;
   int steal;  // STEAL and >= 2 blocks per wave (small graphs: the heads would saturate)
   int aggr_mean;
+  int slabs;  // one-wave edge launch: pieces per wave (x3_slabs)
 };
 
 // the rows the node phase of nodes n0 .. n1 - 1 reads first (lane r = node): the segment
@@ -513,7 +514,8 @@ constexpr int OFF_NZ = OFF_BIAS + C * 4;       // a row of -0.0: the "P" of a sl
 constexpr int LDS = OFF_NZ + HID * 4;
 static_assert(LDS <= 160 * 1024, "conv_x3_sp LDS");
 constexpr int GMAX = 256;          // workgroups (one per CU)
-constexpr int WMAX = GMAX * NW;    // waves: the table holds WMAX + 1 node boundaries
+constexpr int WMAX = GMAX * NW;    // waves
+constexpr int SMAX = 8;            // slabs: the table holds WMAX * SMAX + 1 node boundaries
 }  // namespace sp
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
@@ -675,12 +677,27 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int xcd = blockIdx.x % NXCD, slot = blockIdx.x / NXCD;
-  const int rank = (xcd * ((int)gridDim.x / NXCD) + slot) * sp::NW + wave;
-  const int na = __builtin_amdgcn_readfirstlane(wtab[rank]);
-  const int nb = __builtin_amdgcn_readfirstlane(wtab[rank + 1]);
-  const int E0 = __builtin_amdgcn_readfirstlane(a.seg_ptr[na]);
-  const int E1 = __builtin_amdgcn_readfirstlane(a.seg_ptr[nb]);
-  const int T = (E1 - E0 + 31) >> 5;
+  const int WX = ((int)gridDim.x / NXCD) * sp::NW;  // waves per XCD
+  const int j = slot * sp::NW + wave;
+  const int rank = xcd * WX + j;
+  // the wave's S pieces (one per slab of its XCD's node range, x3_slabs): piece k = table
+  // entry (xcd S + k) WX + j, whole destinations, walked as ONE virtual edge sequence --
+  // positions [vbase[k], vbase[k + 1]) are the real edges v + voff[k].  While the XCD's waves
+  // work through slab k together, their Q[src] gathers stay inside 1 / S of its nodes (L2).
+  const int S = a.slabs;
+  typedef int i8v __attribute__((ext_vector_type(sp::SMAX)));
+  i8v vbase, voff;  // (vectors, not arrays: the lambdas below capture them)
+  int V = 0;
+#pragma unroll
+  for (int k = 0; k < sp::SMAX; ++k) {
+    const int q = (xcd * S + min(k, S - 1)) * WX + j;
+    const int e0 = __builtin_amdgcn_readfirstlane(a.seg_ptr[__builtin_amdgcn_readfirstlane(wtab[q])]);
+    const int e1 = __builtin_amdgcn_readfirstlane(a.seg_ptr[__builtin_amdgcn_readfirstlane(wtab[q + 1])]);
+    vbase[k] = k < S ? V : 0x7fffffff;
+    voff[k] = e0 - V;
+    V += k < S ? e1 - e0 : 0;
+  }
+  const int T = (V + 31) >> 5;
   if (T <= 0) return;
   const float mu0 = *a.mu[0], sd0 = *a.sd[0], mu1 = *a.mu[1], sd1 = *a.sd[1];
   const float* bias2 = (const float*)(lds + sp::OFF_BIAS);  // layer 2's bias
@@ -691,7 +708,13 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   float* Tm = (float*)bufp;  // [32][TS2] message rows while transposing
 
   // ---- per-tile inputs
-  auto edge_of = [&](int t) { return min(E0 + 32 * t + r, E1 - 1); };
+  auto edge_of = [&](int t) {  // the real edge of lane r in tile t (past the end: the last)
+    const int v = min(32 * t + r, V - 1);
+    int off = voff[0];
+#pragma unroll
+    for (int k = 1; k < sp::SMAX; ++k) off = v >= vbase[k] ? voff[k] : off;
+    return v + off;
+  };
   // Q[src] rows of a tile in accumulator order (features 32 m + 8 g + 4 h + t at [4 m + g])
   auto load_q_part = [&](int s, f32x4 (&q)[16], int i0, int i1) {
     const float* g = a.pq + (size_t)s * PQW + HID + 4 * h;
@@ -757,7 +780,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   // the range's end carry no bit); dlast = the destination of the previous tile's last edge
   auto tile_mask = [&](int t, int d, int dlast) {
     const int dprev = __builtin_amdgcn_mov_dpp(d, 0x138, 0xf, 0xf, false);  // wave_shr:1
-    const int nv = min(32, E1 - E0 - 32 * t);  // (<= 0 past the range: no bits)
+    const int nv = min(32, V - 32 * t);  // (<= 0 past the range: no bits)
     const uint32_t live = nv >= 32 ? 0xffffffffu : nv <= 0 ? 0u : ((1u << nv) - 1u);
     return (uint32_t)__ballot(r == 0 ? d != dlast : d != dprev) & live;
   };
@@ -1115,7 +1138,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   const float run_in = run;
   scan(cv, mask_p, run_in, rv);
   flush(mask_p, rv, run_in, d_p, crow);
-  const int nv = E1 - E0 - 32 * (T - 1);
+  const int nv = V - 32 * (T - 1);
   a.agg[(size_t)crow * C + lane] = rv[nv - 1];
 #if RG_CX3_SP_STAMP
   SP_STAMP(6);  // epilogue
@@ -1128,9 +1151,9 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
 #endif
 }
 
-// Node boundaries of the edge launch's waves: rank w takes the destinations
-// [wtab[w], wtab[w + 1]), the first node whose CSR start reaches E w / W (equal edge counts;
-// every destination whole in one wave)
+// Node boundaries of the edge launch's pieces: piece w = the destinations [wtab[w], wtab[w + 1]),
+// wtab[w] the first node whose CSR start reaches E w / W (equal edge counts; every
+// destination whole in one piece); W = waves x slabs
 __global__ __launch_bounds__(256) void conv_x3_waves_kernel(const int* __restrict__ seg_ptr,
                                                             int n, int W, int* __restrict__ wtab) {
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1174,7 +1197,7 @@ extern "C" int rg_debug_sp_stamps(unsigned long long* out_host) {
 extern "C" size_t rg_conv_layer_x3_workspace_size(int n_nodes) {
   static_assert((CTR_STRIDE * NXCD + 1) * sizeof(int) <= CTR_BYTES, "counter area");
   // + the wave table when the layer has to build it (no rg_conv_x3_blocks table)
-  return CTR_BYTES + x3_agg_bytes(n_nodes) + (size_t)(sp::WMAX + 1) * sizeof(int);
+  return CTR_BYTES + x3_agg_bytes(n_nodes) + (size_t)(sp::WMAX * sp::SMAX + 1) * sizeof(int);
 }
 
 extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int n_nodes,
@@ -1196,11 +1219,22 @@ extern "C" int rg_conv_proj_x3(const rg_layer* pq, const float* x, int ldx, int 
 
 extern "C" size_t rg_conv_x3_blocks_bytes(int n_nodes) {
   (void)n_nodes;
-  return (size_t)(sp::WMAX + 1) * sizeof(int);
+  return (size_t)(sp::WMAX * sp::SMAX + 1) * sizeof(int);
 }
 
+// slabs per XCD node range for the one-wave launch: ~RG_CX3_SLAB_NODES nodes each, at most
+// sp::SMAX (M: 4 slabs of 6000 nodes, 3 MB of Q rows, against the XCD's 4 MB L2; the
+// launch's fetched bytes 1.77 -> 0.96 GB at 8 slabs, its time unchanged,
+// profiles/r06_slab_ab.log, r06_slab_fetch.json)
+#ifndef RG_CX3_SLAB_NODES
+#define RG_CX3_SLAB_NODES 6000
+#endif
+static int x3_slabs(int n_nodes) {
+  const int s = (n_nodes / NXCD + RG_CX3_SLAB_NODES / 2) / RG_CX3_SLAB_NODES;
+  return s < 1 ? 1 : s > sp::SMAX ? sp::SMAX : s;
+}
 static int x3_wave_table(const int* seg_ptr, int n_nodes, int* table, void* stream) {
-  const int W = x3_sp_groups(n_nodes) * sp::NW;
+  const int W = x3_sp_groups(n_nodes) * sp::NW * x3_slabs(n_nodes);
   conv_x3_waves_kernel<<<(W + 256) / 256, 256, 0, (hipStream_t)stream>>>(seg_ptr, n_nodes, W, table);
   RG_LAUNCH_CHECK();
   return RG_OK;
@@ -1302,6 +1336,7 @@ static int conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int ag
       if (rc != RG_OK) return rc;
       wtab = ws_tab;
     }
+    a.slabs = x3_slabs(n_nodes);
     auto edge = conv_x3_sp_kernel<true>;
     RG_ENSURE_LDS(edge, sp::LDS);
     edge<<<x3_sp_groups(n_nodes), sp::FT, sp::LDS, (hipStream_t)stream>>>(a, wtab);

@@ -386,15 +386,18 @@ int rg_conv_layer_x3(const rg_layer* layers, const rg_layer* next_pq, int aggr, 
                      const int* src, const int* dst, int n_nodes, float* x_out, int ld_out,
                      float* pq_out, void* workspace, size_t workspace_bytes, void* stream);
 /* The same layer with the edge launch's wave table from rg_conv_x3_blocks (built once per
- * graph instead of once per layer): one contiguous range of whole destinations per wave of
- * the one-wave-per-SIMD edge launch, equal edge counts.  Same results. */
+ * graph instead of once per layer): per wave of the one-wave-per-SIMD edge launch S pieces
+ * of whole destinations (one per slab of its XCD's node range), equal edge counts.  Same
+ * results. */
 int rg_conv_layer_x3_blocks(const rg_layer* layers, const rg_layer* next_pq, int aggr,
                             const float* x, int ldx, const float* e, int lde, const float* pq,
                             const int* seg_ptr, const int* src, const int* dst, int n_nodes,
                             float* x_out, int ld_out, float* pq_out, const int* table,
                             void* workspace, size_t workspace_bytes, void* stream);
-/* table: rg_conv_x3_blocks_bytes(n_nodes) bytes of device memory -- int32 node boundaries of
- * the edge launch's waves (wave w takes destinations [table[w], table[w + 1])) -- from
+/* table: rg_conv_x3_blocks_bytes(n_nodes) bytes of device memory -- int32 boundaries of
+ * W x S node pieces with equal edge counts in node order (piece q = destinations
+ * [table[q], table[q + 1])); wave j of XCD x (W / 8 waves per XCD) takes the pieces
+ * (x S + k) W / 8 + j, k = 0 .. S - 1, so the XCD's waves walk its slabs together -- from
  * seg_ptr[n_nodes + 1]. */
 size_t rg_conv_x3_blocks_bytes(int n_nodes);
 int rg_conv_x3_blocks(const int* seg_ptr, int n_nodes, int* table, void* stream);

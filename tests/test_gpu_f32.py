@@ -237,7 +237,7 @@ def test_x3_conv_wave_table_bit_identical(cuda_device, sizes):
     tbl = g.conv_x3_blocks()
     assert tbl is not None and tbl.numel() * 4 >= nat.lib().rg_conv_x3_blocks_bytes(N)
     G = min(max((N // 128 + 7) // 8 * 8, 8), 256)      # workgroups (x3_sp_groups)
-    W = 4 * G
+    W = 4 * G * _x3_slabs(N)                             # pieces: waves x slabs
     wt = tbl[:W + 1].cpu().numpy()
     seg = g.seg_ptr.cpu().numpy()
     E = int(seg[N])
@@ -262,6 +262,71 @@ def test_x3_conv_wave_table_bit_identical(cuda_device, sizes):
     finally:
         engine.CONV_X3_TABLE = old
     assert torch.equal(out_t, out_p)
+
+
+def _x3_slabs(N):
+    """conv_x3.hip x3_slabs: slabs per XCD node range of ~6000 nodes, 1 .. 8."""
+    return min(max((N // 8 + 3000) // 6000, 1), 8)
+
+
+@pytest.mark.parametrize('sizes', [[3000] * 24, [2999, 1, 40] * 24 + [500] * 2])
+def test_x3_conv_slab_schedule_bit_identical(cuda_device, sizes):
+    """The one-wave edge launch's slab schedule: each wave walks S pieces of whole
+    destinations (one per slab of its XCD's node range, so the XCD's waves gather Q rows from
+    one slab at a time) as one virtual edge sequence.  Bit-identical to one contiguous range
+    per wave -- the same launch over a table whose pieces 1 .. S - 1 are empty -- and the
+    table's pieces cover every node once with equal edge shares; the output also against
+    the oracle's residual_graph_conv_block."""
+    from graph_neural_network_for_radar_perception_amd.config import default_config
+    from graph_neural_network_for_radar_perception_amd.gnn_detector import Model_Training
+    dev = cuda_device
+    cfg = default_config(graph_convolution_stem_channels=[64], k_number_nearest_points=10)
+    torch.manual_seed(15)
+    m = Model_Training(cfg, dev).to(dev).eval().requires_grad_(False)
+    cv = _conv_plan(m, 'x3')
+    batch, gb = _graph(dev, sizes, 10, 92, cfg)
+    g = gb.graph
+    N = batch.n_nodes
+    S = _x3_slabs(N)
+    assert S > 1
+    G = min(max((N // 128 + 7) // 8 * 8, 8), 256)
+    WX = G // 8 * 4                                      # waves per XCD
+    W = 8 * WX
+    tbl = g.conv_x3_blocks()
+    seg = g.seg_ptr.cpu().numpy().astype(np.int64)
+    E = int(seg[N])
+    wt = tbl[:W * S + 1].cpu().numpy()
+    assert wt[0] == 0 and wt[W * S] == N and np.all(np.diff(wt) >= 0)
+    per = seg[wt[1:]] - seg[wt[:-1]]
+    assert per.sum() == E and np.all(per <= -(-E // (W * S)) + int(np.diff(seg).max()))
+    gen = torch.Generator(device='cpu').manual_seed(5)
+    x = (torch.randn(N, 64, generator=gen) * 1.5).to(dev)
+    e = (torch.randn(gb.capacity, 64, generator=gen) * 1.5).to(dev)
+    out_s = torch.full((N, 64), float('nan'), device=dev)
+    assert cv.run_fused(x, e, g, out_s)
+    # one contiguous range per wave: wave (x, j) = the single-slab table's range, as piece 0;
+    # its pieces 1 .. S - 1 empty at the end of the XCD's range
+    one = np.searchsorted(seg, (E * np.arange(W + 1)) // W, side='left')
+    one[W] = N
+    t2 = np.empty(W * S + 1, np.int32)
+    for xcd in range(8):
+        for k in range(S):
+            for j in range(WX):
+                q = (xcd * S + k) * WX + j
+                t2[q] = one[xcd * WX + j] if k == 0 else one[(xcd + 1) * WX]
+    t2[W * S] = N
+    assert np.all(np.diff(t2.astype(np.int64)) >= 0)
+    g._conv_x3_blocks = torch.from_numpy(t2).to(dev)
+    out_c = torch.full((N, 64), float('nan'), device=dev)
+    assert cv.run_fused(x, e, g, out_c)
+    g._conv_x3_blocks = tbl
+    assert torch.equal(out_s, out_c)
+    sd = {k: v.float().cpu() for k, v in m.state_dict().items()}
+    ei = torch.stack((g.src[:E], g.dst[:E])).long().cpu()
+    with torch.no_grad():
+        ctx = gnn_forward_ref._Ctx(sd, cfg)
+        ref = gnn_forward_ref.conv_block(ctx, 'pass_messages.conv_blk.0', x.cpu(), e[:E].cpu(), ei)
+    torch.testing.assert_close(out_s.cpu(), ref, **FP32_TOL)
 
 
 def test_f32_fused_conv_deterministic_and_isolated_nodes(cuda_device):
