@@ -51,7 +51,8 @@ class rg_layer(ctypes.Structure):
 class rg_pack_job(ctypes.Structure):
     _fields_ = [('weight', ctypes.c_void_p), ('bias', ctypes.c_void_p),
                 ('packed', ctypes.c_void_p), ('in_dim', ctypes.c_int),
-                ('out_dim', ctypes.c_int), ('fmt', ctypes.c_int), ('transpose', ctypes.c_int)]
+                ('out_dim', ctypes.c_int), ('fmt', ctypes.c_int), ('transpose', ctypes.c_int),
+                ('ld', ctypes.c_int)]
 
 
 class rg_loss_args(ctypes.Structure):
@@ -130,6 +131,7 @@ _SIGNATURES = {
     'rg_packed_linear_bytes': (_S, [_I, _I, _I]),
     'rg_pack_linear': (_I, [_P, _P, _I, _I, _I, _P, _P]),
     'rg_pack_linear_jobs': (_I, [_P, _I, _P]),
+    'rg_pack_linear_ld': (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     'rg_mlp_chain': (_I, [_I, ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,
                           _I, _P, _I, _I, _P, _P, _P, _I, _I, _P, _I, _I, _P]),
     'rg_mlp_chain_fast': (_I, [ctypes.POINTER(rg_layer), _I, _L, _P, _I, _I, _P, _I, _I, _P, _I,
@@ -193,6 +195,8 @@ _SIGNATURES = {
     'rg_linear_grad_workspace_size': (_S, [_L, _I, _I]),
     'rg_linear_grad': (_I, [_P, _I, _L, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P,
                             _P, _P, _P, _S, _P]),
+    'rg_linear_grad_ld': (_I, [_P, _I, _L, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P,
+                               _P, _I, _P, _P, _S, _P]),
     'rg_incidence_workspace_size': (_S, [_I, _L]),
     'rg_incidence': (_I, [_P, _P, _L, _I, _P, _P, _P, _S, _P]),
     'rg_gather_segment_sum': (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P, _I, _I, _P]),

@@ -100,7 +100,7 @@ struct ChainArgs {
 // one launch per packed f32 layer (the training step repacks every layer after each SGD step)
 __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, int transpose,
                                 float* __restrict__ P, long total,
-                                const float* __restrict__ bias = nullptr, int nb = 0) {
+                                const float* __restrict__ bias = nullptr, int nb = 0, int ld = 0) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) {
     const long i = t - total;
@@ -115,8 +115,10 @@ __global__ void pack_f32_kernel(const float* __restrict__ W, int in, int out, in
   const int m = (int)(ms / S4);
   const int o = 16 * m + (lane & 15);
   const int k = 16 * s4 + 4 * (lane >> 4) + e;
-  // transpose: W holds the [in][out] matrix whose transpose is the layer
-  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k]) : 0.f;
+  // transpose: W holds the [in][out] matrix whose transpose is the layer; ld: W's row stride
+  // (0: dense) -- a column block of a wider matrix
+  const int ldw = ld ? ld : (transpose ? out : in);
+  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * ldw + o] : W[(size_t)o * ldw + k]) : 0.f;
 }
 
 // plane p > 0: the p-th term of the exact three-term bf16 split (RG_PACK_X3 | RG_BF16, the
@@ -184,7 +186,7 @@ __global__ void pack_fast_kernel(const float* __restrict__ W, int in, int out, i
 // previous layer's 32x32 accumulators (register 4g + t of M-tile m' = k-step
 // 16 m' + 4g + t) supply, so one format serves every layer of an f32 chain
 __global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int out, int transpose,
-                                     float* __restrict__ P, long total) {
+                                     float* __restrict__ P, long total, int ld = 0) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int S4 = (in + 7) / 8;
@@ -195,8 +197,10 @@ __global__ void pack_f32_fast_kernel(const float* __restrict__ W, int in, int ou
   const int m = (int)(ms / S4);
   const int o = 32 * m + (lane & 31);
   const int k = 8 * s4 + 4 * (lane >> 5) + u;
-  // transpose: W is the [in][out] weight of the forward layer, packed as its transpose
-  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * out + o] : W[(size_t)o * in + k]) : 0.f;
+  // transpose: W is the [in][out] weight of the forward layer, packed as its transpose;
+  // ld: W's row stride (0: dense)
+  const int ldw = ld ? ld : (transpose ? out : in);
+  P[t] = (o < out && k < in) ? (transpose ? W[(size_t)k * ldw + o] : W[(size_t)o * ldw + k]) : 0.f;
 }
 
 __global__ void pack_bias_kernel(const float* __restrict__ b, int out, int n, float* __restrict__ P) {
@@ -746,6 +750,33 @@ extern "C" int rg_pack_linear(const float* weight, const float* bias, int in_dim
   return RG_OK;
 }
 
+extern "C" int rg_pack_linear_ld(const float* weight, const float* bias, int in_dim, int out_dim,
+                                 int dtype, int ld, void* packed, void* stream) {
+  const int transpose = (dtype & RG_PACK_TRANSPOSE) ? 1 : 0;
+  const int fmt = dtype & ~RG_PACK_TRANSPOSE;
+  RG_REQUIRE(fmt == RG_F32 || fmt == RG_PACK_F32_FAST, RG_ERR_ARG,
+             "rg_pack_linear_ld: RG_F32 or RG_PACK_F32_FAST (| RG_PACK_TRANSPOSE)");
+  RG_REQUIRE(in_dim > 0 && out_dim > 0 && in_dim <= MAXW && out_dim <= MAXW, RG_ERR_UNSUPPORTED,
+             "rg_pack_linear_ld: dims %dx%d outside 1..%d", out_dim, in_dim, MAXW);
+  RG_REQUIRE(ld == 0 || ld >= (transpose ? out_dim : in_dim), RG_ERR_ARG,
+             "rg_pack_linear_ld: ld %d shorter than a row", ld);
+  hipStream_t st = (hipStream_t)stream;
+  const long total = (long)frag_bytes(in_dim, out_dim, fmt) / sizeof(float);
+  if (fmt == RG_F32) {
+    const int nb = kpad(out_dim, 16);
+    pack_f32_kernel<<<ceil_div(total + nb, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
+                                                               (float*)packed, total, bias, nb, ld);
+  } else {
+    pack_f32_fast_kernel<<<ceil_div(total, 256), 256, 0, st>>>(weight, in_dim, out_dim, transpose,
+                                                               (float*)packed, total, ld);
+    const int nb = kpad(out_dim, 32);
+    pack_bias_frag_kernel<<<ceil_div(nb, 256), 256, 0, st>>>(
+        bias, out_dim, nb, 0, (float*)((char*)packed + frag_bytes(in_dim, out_dim, fmt)));
+  }
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 // rg_pack_linear_jobs: blockIdx.y = job, a grid-stride loop over its weights then its bias
 // (RG_F32: plain, padded to 16; RG_PACK_F32_FAST: accumulator order, padded to 32) -- the same
 // element formulas as pack_f32_kernel / pack_f32_fast_kernel / pack_bias_frag_kernel
@@ -780,8 +811,9 @@ __global__ void pack_jobs_kernel(const rg_pack_job* __restrict__ jobs) {
       o = 16 * (int)(ms / S4) + (lane & 15);
       k = 16 * (int)(ms % S4) + 4 * (lane >> 4) + e;
     }
+    const int ldw = j.ld ? j.ld : (j.transpose ? j.out_dim : j.in_dim);
     P[t] = (o < j.out_dim && k < j.in_dim)
-               ? (j.transpose ? j.weight[(size_t)k * j.out_dim + o] : j.weight[(size_t)o * j.in_dim + k])
+               ? (j.transpose ? j.weight[(size_t)k * ldw + o] : j.weight[(size_t)o * ldw + k])
                : 0.f;
   }
 }

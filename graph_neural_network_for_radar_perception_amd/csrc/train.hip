@@ -537,7 +537,7 @@ static constexpr int RW = 16;
 __global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
     const float* __restrict__ part, const float* __restrict__ part_b, int nchunk, int ot_n,
     int it_n, int oc, int ic, int out_dim, int in_dim, float* __restrict__ dW,
-    float* __restrict__ db) {
+    float* __restrict__ db, int ld_dw) {
   __shared__ float red[RW][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long t = (long)blockIdx.x * 64 + lane;
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
   }
   if (wave == 0 && t < total) {
     const float v = red[0][lane];
-    if (i < in_dim) dW[(size_t)o * in_dim + i] += v;
+    if (i < in_dim) dW[(size_t)o * ld_dw + i] += v;
     else if (db) db[o] += v;
   }
 }
@@ -1025,12 +1025,13 @@ extern "C" size_t rg_linear_grad_workspace_size(long rows, int out_dim, int in_d
   return grad_ws_bytes(grad_geom(rows, out_dim, in_dim));
 }
 
-extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim,
-                              int in_mode, const float* in0, int ld0, int w0, const float* in1,
-                              int ld1, int w1, const float* in2, int ld2, int w2, const int* idx0,
-                              const int* idx1, float* dW, float* db, void* workspace,
-                              size_t workspace_bytes, void* stream) {
+extern "C" int rg_linear_grad_ld(const float* dz, int lddz, long rows, int out_dim, int in_dim,
+                                 int in_mode, const float* in0, int ld0, int w0, const float* in1,
+                                 int ld1, int w1, const float* in2, int ld2, int w2,
+                                 const int* idx0, const int* idx1, float* dW, int ld_dw, float* db,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
   RG_REQUIRE(out_dim >= 1 && in_dim >= 1, RG_ERR_ARG, "rg_linear_grad: dims");
+  RG_REQUIRE(ld_dw >= in_dim, RG_ERR_ARG, "rg_linear_grad: ld_dw %d < in_dim %d", ld_dw, in_dim);
   RG_REQUIRE(in_mode >= RG_IN_DENSE && in_mode <= RG_IN_PAIRADD, RG_ERR_ARG, "bad in_mode");
   RG_REQUIRE((in_mode != RG_IN_GATHER3 && in_mode != RG_IN_PAIRADD) || (idx0 && idx1), RG_ERR_ARG,
              "rg_linear_grad: gather modes need idx0 and idx1");
@@ -1068,9 +1069,19 @@ extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim,
   const long total = (long)out_dim * (in_dim + 1);
   linear_grad_reduce<<<ceil_div(total, 64), 64 * RW, 0, st>>>(part, part_b, g.nchunk, g.ot, g.it,
                                                            64 * g.ow, 16 * g.nt, out_dim, in_dim,
-                                                           dW, db);
+                                                           dW, db, ld_dw);
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim,
+                              int in_mode, const float* in0, int ld0, int w0, const float* in1,
+                              int ld1, int w1, const float* in2, int ld2, int w2, const int* idx0,
+                              const int* idx1, float* dW, float* db, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  return rg_linear_grad_ld(dz, lddz, rows, out_dim, in_dim, in_mode, in0, ld0, w0, in1, ld1, w1,
+                           in2, ld2, w2, idx0, idx1, dW, in_dim, db, workspace, workspace_bytes,
+                           stream);
 }
 
 extern "C" size_t rg_incidence_workspace_size(int n_nodes, long n_items) {

@@ -46,6 +46,13 @@ DX_F32_FAST = True
 REPACK_JOBS = True
 # loss values appended to the gradient bucket (loss_node_cls, _node_reg, _edge_cls, _obj_cls)
 N_LOSS_SLOTS = 4
+# the message MLP's first layer backward factorised over its x_i / x_j / e column blocks
+# (gnn_blocks.py:100-101 is linear before its norm): dZ reduced per node first (destination /
+# source sums), so those blocks' weight and input gradients run over N rows, not E.  False:
+# one GATHER3 weight gradient and one 192-wide dX over the E rows.  (The forward keeps the
+# GATHER3 tape: a per-node P | Q form of it moved the reference fixture's norm-scale
+# gradients 3 % through LeakyReLU kink flips, profiles/r06_pqe_forward_diag.log.)
+FACTORED_MSG0 = True
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -104,6 +111,8 @@ class TrainChain:
         self.plan = ChainPlan(packed, 'fp32', device)
         self._fast_ok = {}   # input mode -> the register-resident tape kernel took the chain
         self._dx_ok = {}     # layer -> the register-resident kernel took its dX = dZ W
+        self._sub = {}       # (layer, col0, width) -> column-block images for dX (_block_images)
+        self._subsig = None
         self.device = torch.device(device)
         self.ws = ws
         self._tsig = None
@@ -116,6 +125,7 @@ class TrainChain:
     def invalidate(self):
         self.plan.sig = None
         self._tsig = None
+        self._subsig = None
 
     def pack_jobs(self):
         """rg_pack_job entries that re-write every packed image of this chain in place (the
@@ -147,6 +157,15 @@ class TrainChain:
                     job(s.weight.detach(), None, arr[0].w_packed, s.out_dim, s.in_dim, fmt, 1)
         else:
             self._tsig = None   # transposes not packed yet: packed on first use
+        if self._subsig is not None and self._subsig == p.sig:
+            for (l, c0, wd), pair in self._sub.items():
+                s = self.specs[l]
+                for fmt, arr in zip((nat.RG_F32, nat.RG_PACK_F32_FAST), pair):
+                    job(s.weight.detach(), None, arr[0].w_packed, s.out_dim, wd, fmt, 1)
+                    jobs[-1].weight = s.weight.data_ptr() + 4 * c0
+                    jobs[-1].ld = s.in_dim
+        else:
+            self._subsig = None
         return jobs
 
     def _transposed(self):
@@ -185,23 +204,66 @@ class TrainChain:
         self._tsig = sig
         return self._tarr
 
-    def _dx(self, l: int, rows: int, dZ, out, res):
-        """out = dZ W_l (+ res): the register-resident f32 kernel where it has the shape,
-        else the generic chain kernel."""
+    def _block_images(self, l: int, col0: int, width: int):
+        """Images of the column block W_l[:, col0:col0 + width] for the data GEMM
+        dX_block = dZ W_l[:, col0:col0 + width] (generic RG_F32 and register-resident
+        RG_PACK_F32_FAST, packed transposed straight from the block: rg_pack_linear_ld, row
+        stride in_dim), re-written in place with the other images after an optimizer step
+        (pack_jobs)."""
+        sig = self.plan.sig
+        key = (l, col0, width)
+        if self._subsig != sig:
+            self._sub_packed = {}
+            self._subsig = sig
+        if key in self._sub and key in self._sub_packed:
+            return self._sub[key]
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
-        gen, fast = self._transposed()[l]
-        if TAPE_F32_FAST and DX_F32_FAST and self._dx_ok.get(l, True):
+        s = self.specs[l]
+        w = s.weight.detach()
+        arrs = []
+        for f in (nat.RG_F32, nat.RG_PACK_F32_FAST):
+            bkey = ('blk', id(self), key, f)
+            buf = self.ws.bufs.get(bkey)
+            if buf is None:
+                buf = torch.empty(lib.rg_packed_linear_bytes(s.out_dim, width, f),
+                                  dtype=torch.uint8, device=self.device)
+                self.ws.bufs[bkey] = buf
+            nat.check(lib.rg_pack_linear_ld(w.data_ptr() + 4 * col0, None, s.out_dim, width,
+                                            f | nat.RG_PACK_TRANSPOSE, s.in_dim, buf.data_ptr(),
+                                            st), 'rg_pack_linear_ld')
+            arr = (nat.rg_layer * 1)()
+            arr[0].w_packed = buf.data_ptr()
+            arr[0].in_dim = s.out_dim
+            arr[0].out_dim = width
+            arr[0].act = nat.ACT['none']
+            arrs.append(arr)
+        self._sub[key] = tuple(arrs)
+        self._sub_packed[key] = True
+        return self._sub[key]
+
+    def _dx(self, l: int, rows: int, dZ, out, res, block=None):
+        """out = dZ W_l (+ res): the register-resident f32 kernel where it has the shape,
+        else the generic chain kernel.  block = (col0, width): dZ W_l[:, col0:col0 + width]."""
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        if block is None:
+            gen, fast = self._transposed()[l]
+            okey = l
+        else:
+            gen, fast = self._block_images(l, *block)
+            okey = (l,) + tuple(block)
+        if TAPE_F32_FAST and DX_F32_FAST and self._dx_ok.get(okey, True):
             rc = lib.rg_mlp_chain_f32_ex(fast, 1, rows, None, nat.IN_DENSE, dZ.data_ptr(),
                                          dZ.stride(0), dZ.shape[1], None, 0, 0, None, 0, 0, None,
                                          None, nat.ptr(res), res.stride(0) if res is not None else 0,
                                          out.data_ptr(), out.stride(0), st)
             if rc == 0:
-                self._dx_ok[l] = True
+                self._dx_ok[okey] = True
                 return
             if rc != nat.RG_ERR_UNSUPPORTED:
                 nat.check(rc, 'rg_mlp_chain_f32_ex (dX = dZ W)')
-            self._dx_ok[l] = False
+            self._dx_ok[okey] = False
         nat.check(lib.rg_mlp_chain(
             nat.RG_F32, gen, 1, rows, None, nat.IN_DENSE, nat.RG_F32, dZ.data_ptr(),
             dZ.stride(0), dZ.shape[1], None, 0, 0, None, 0, 0, None, None,
@@ -315,15 +377,18 @@ class TrainChain:
 
     # ------------------------------------------------------------------ backward
     def backward(self, tape: ChainTape, d_out: torch.Tensor, grads: Dict[int, torch.Tensor],
-                 din: Optional[torch.Tensor] = None, din_accumulate: bool = False):
+                 din: Optional[torch.Tensor] = None, din_accumulate: bool = False,
+                 stop_at_first_linear: bool = False):
         """d_out: f32 [rows][out_dim] gradient of the chain output (overwritten).
         Parameter gradients accumulate into grads[id(param)]; with ``din`` the gradient of
-        the chain input (dense [rows][in_dim]) is written (or added) there."""
+        the chain input (dense [rows][in_dim]) is written (or added) there.
+        stop_at_first_linear: return dZ of the first layer (its pre-activation gradient) and
+        leave that Linear's weight / input gradients to the caller."""
         lib = nat.lib()
         st = nat.stream_ptr(self.device)
         rows = tape.rows
         if rows <= 0:
-            return
+            return None
         dA = d_out
         for l in range(len(self.specs) - 1, -1, -1):
             sp = self.specs[l]
@@ -348,6 +413,8 @@ class TrainChain:
                     dA.stride(0), nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
                     ws.data_ptr(), st), 'rg_ffn_backward')
             dZ = dA
+            if l == 0 and stop_at_first_linear:
+                return dZ
             # dW, db over this layer's input rows
             if l == 0:
                 m, i0, w0, i1, w1, i2, w2 = (tape.mode, tape.in0, tape.w0, tape.in1, tape.w1,
@@ -642,14 +709,18 @@ class TrainEngine:
             else:
                 scale = self._mean_scale(g, N) if cv.aggr == 'mean' else None
                 self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
-            dG = torch.empty((max(E, 1), cv.msg.in_dim), **f32)
-            cv.msg.backward(ct['msg'], d_msg, G, din=dG)
-            # x_i = x[dst]: segment sums over the destination-major CSR
-            self._segsum(dG, 0, Cin, g.seg_ptr, None, None, dx_new, accumulate=True)
-            # x_j = x[src]: sums over each node's outgoing positions
-            self._segsum(dG, Cin, Cin, src_ptr, src_lst, None, dx_new, accumulate=True)
-            # e (the same encoded edges every layer, gnn_blocks.py:159-163)
-            self._segsum(dG, 2 * Cin, e_enc_out_dim, eptr, None, None, de, accumulate=True)
+            if FACTORED_MSG0 and E > 0:
+                dz0 = cv.msg.backward(ct['msg'], d_msg, G, stop_at_first_linear=True)
+                self._msg0_backward(cv.msg, ct['msg'], dz0, g, src_ptr, src_lst, dx_new, de)
+            else:
+                dG = torch.empty((max(E, 1), cv.msg.in_dim), **f32)
+                cv.msg.backward(ct['msg'], d_msg, G, din=dG)
+                # x_i = x[dst]: segment sums over the destination-major CSR
+                self._segsum(dG, 0, Cin, g.seg_ptr, None, None, dx_new, accumulate=True)
+                # x_j = x[src]: sums over each node's outgoing positions
+                self._segsum(dG, Cin, Cin, src_ptr, src_lst, None, dx_new, accumulate=True)
+                # e (the same encoded edges every layer, gnn_blocks.py:159-163)
+                self._segsum(dG, 2 * Cin, e_enc_out_dim, eptr, None, None, de, accumulate=True)
             dx = dx_new
         # encoders (gnn_blocks.py:19-42): inputs are data, no input gradient
         self.edge_enc.backward(T['edge_enc'], de, G)
@@ -680,7 +751,7 @@ class TrainEngine:
             if j is None:
                 return False
             jobs += j
-        key = tuple((j.weight, j.bias, j.packed, j.in_dim, j.out_dim, j.fmt, j.transpose)
+        key = tuple((j.weight, j.bias, j.packed, j.in_dim, j.out_dim, j.fmt, j.transpose, j.ld)
                     for j in jobs)
         if getattr(self, '_repack_key', None) != key:
             arr = (nat.rg_pack_job * len(jobs))(*jobs)
@@ -691,6 +762,46 @@ class TrainEngine:
                                                 nat.stream_ptr(self.device)),
                   'rg_pack_linear_jobs')
         return True
+
+    def _msg0_backward(self, chain, tape, dz0, g, src_ptr, src_lst, dx, de):
+        """Backward of the message MLP's first Linear, z0 = W0 cat(x[dst], x[src], e) + b0
+        (gnn_blocks.py:100-101, 113), over its three column blocks W0 = [W_i | W_j | W_e]:
+            dW_e += dZ0^T e, db0 += sum dZ0          (E rows, K = |e|)
+            S_i = sum over each node's incoming edges of dZ0, S_j = over its outgoing ones
+            dW_i += S_i^T x, dW_j += S_j^T x          (N rows)
+            dx += S_i W_i + S_j W_j, de += dZ0 W_e
+        -- the same sums as the GATHER3 weight gradient and the 192-wide dX + three transposed
+        gathers, grouped per node first (x[dst] / x[src] are the same row for every edge of a
+        node), so two of the three blocks run over N rows instead of E."""
+        lib = nat.lib()
+        st = nat.stream_ptr(self.device)
+        sp = chain.specs[0]
+        H, K = sp.out_dim, sp.in_dim
+        x, Cin, e, De = tape.in0, tape.w0, tape.in2, tape.w2
+        E, N = tape.rows, x.shape[0]
+        wg = self.grads[id(sp.weight)]
+        bg = self.grads.get(id(sp.bias)) if sp.bias is not None else None
+
+        def wgrad(dz, rows, inp, width, col0, db):
+            wsz = lib.rg_linear_grad_workspace_size(rows, H, width)
+            ws = self.ws.get('lgrad', wsz)
+            nat.check(lib.rg_linear_grad_ld(
+                dz.data_ptr(), dz.stride(0), rows, H, width, nat.IN_DENSE, inp.data_ptr(),
+                inp.stride(0), width, None, 0, 0, None, 0, 0, None, None,
+                wg.data_ptr() + 4 * col0, K, nat.ptr(db), ws.data_ptr(), ws.numel(), st),
+                'rg_linear_grad_ld')
+
+        f32 = dict(dtype=torch.float32, device=self.device)
+        wgrad(dz0, E, e, De, 2 * Cin, bg)
+        s_i = torch.empty((N, H), **f32)
+        s_j = torch.empty((N, H), **f32)
+        self._segsum(dz0, 0, H, g.seg_ptr, None, None, s_i, accumulate=False)
+        self._segsum(dz0, 0, H, src_ptr, src_lst, None, s_j, accumulate=False)
+        wgrad(s_i, N, x, Cin, 0, None)
+        wgrad(s_j, N, x, Cin, Cin, None)
+        chain._dx(0, N, s_i, dx, dx, block=(0, Cin))
+        chain._dx(0, N, s_j, dx, dx, block=(Cin, Cin))
+        chain._dx(0, E, dz0, de, de, block=(2 * Cin, De))
 
     # ------------------------------------------------------------------ helpers
     def _segsum(self, src, col0, width, ptr, lst, scale, out, accumulate):

@@ -255,8 +255,15 @@ typedef struct rg_pack_job {
   const float* bias;    /* [out] or NULL */
   void* packed;         /* rg_packed_linear_bytes(in_dim, out_dim, fmt) bytes */
   int in_dim, out_dim, fmt, transpose;
+  int ld;               /* weight's row stride in floats (0: dense rows) */
 } rg_pack_job;
 int rg_pack_linear_jobs(const rg_pack_job* jobs, int n_jobs, void* stream);
+/* rg_pack_linear for RG_F32 / RG_PACK_F32_FAST (| RG_PACK_TRANSPOSE) from a column block of a
+ * wider row-major matrix: rows ld floats apart (0: dense).  The training step packs the
+ * x_i / x_j / e column blocks of msg0 (gnn_blocks.py:100-101) this way for its factorised
+ * message backward. */
+int rg_pack_linear_ld(const float* weight, const float* bias, int in_dim, int out_dim, int dtype,
+                      int ld, void* packed, void* stream);
 
 /* One ffn_block (common.py:185-205): Linear -> [channel_normalization] -> activation. */
 typedef struct rg_layer {
@@ -739,6 +746,12 @@ int rg_linear_grad(const float* dz, int lddz, long rows, int out_dim, int in_dim
                    const float* in0, int ld0, int w0, const float* in1, int ld1, int w1,
                    const float* in2, int ld2, int w2, const int* idx0, const int* idx1,
                    float* dW, float* db, void* workspace, size_t workspace_bytes, void* stream);
+/* The same into a column block of a wider dW: rows ld_dw floats apart (>= in_dim). */
+int rg_linear_grad_ld(const float* dz, int lddz, long rows, int out_dim, int in_dim, int in_mode,
+                      const float* in0, int ld0, int w0, const float* in1, int ld1, int w1,
+                      const float* in2, int ld2, int w2, const int* idx0, const int* idx1,
+                      float* dW, int ld_dw, float* db, void* workspace, size_t workspace_bytes,
+                      void* stream);
 
 /* Incidence lists: for node n, every u < n_items with a[u] == n or b[u] == n (b may be
  * NULL), ascending: ptr int32 [n_nodes+1], list int32 [n_items * (b ? 2 : 1)].  The
