@@ -656,6 +656,7 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   RG_F32C(IN_DENSE, 64, spec(L, 0, 0, 0), false, 64)
   RG_F32C(IN_DENSE, 64, spec(L, 0, 0, 0), false, 128)
   RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 128)
+  RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 64)   // column blocks of msg0 (training.py)
   RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 192)
   RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 256)
 #undef RG_F32C

@@ -31,3 +31,5 @@ step trace_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   -- python bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline
 step trace_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run \
   -- python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline
+step trace_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4 -o run \
+  -- python bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline
