@@ -192,6 +192,10 @@ _SIGNATURES = {
     # training (train.hip)
     'rg_ffn_backward_workspace_size': (_S, []),
     'rg_ffn_backward': (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
+    'rg_dx_norm_backward_workspace_size': (_S, [_L]),
+    'rg_dx_norm_backward': (_I, [_P, _L, _P, _I, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _S, _P]),
+    'rg_ffn_backward_gather': (_I, [_P, _I, _P, _I, _P, _P, _L, _I, _I, _P, _P, _I, _P, _I, _P, _P,
+                                    _P, _P]),
     'rg_linear_grad_workspace_size': (_S, [_L, _I, _I]),
     'rg_linear_grad': (_I, [_P, _I, _L, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P,
                             _P, _P, _P, _S, _P]),

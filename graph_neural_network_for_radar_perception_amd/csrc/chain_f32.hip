@@ -664,6 +664,169 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   return RG_ERR_UNSUPPORTED;
 }
 
+// ---------------------------------------------------------------- dX + norm backward
+// The training backward's dA = dZ W (one transposed layer, as the dX chains above) with
+// the previous ffn_block's channel_normalization + activation backward applied in the same
+// registers (rg_dx_norm_backward): dz = ffn_backward(z, dA) without dA ever reaching
+// memory.  The arithmetic is rg_ffn_backward's (train.hip) with the row sums taken over
+// this layout (in-lane, then the lane pair):
+//   gy = dA act'(y);  ds += sum gy n;  dm += sum gy;  gn = s gy;
+//   gd = r gn - r^2 (sum gn d) d / ((C-1) std);  dz = gd - mean(gd)
+// with the d mu / d std sums of each row in float32 and over rows in float64, one partial
+// per workgroup (fixed order), reduced by the caller.
+struct NormBwd {
+  const float* z;  // the norm's input (pre-norm tape), [rows][C]
+  int ldz;
+  const float* mu;
+  const float* sd;
+  int act;
+  double* part;    // [gridDim.x][2]: (sum gy n, sum gy)
+};
+
+__device__ __forceinline__ float nb_act_grad(float y, int act) {
+  if (act == ACT_LEAKY) return y > 0.f ? 1.f : 0.01f;  // torch's leaky_relu backward
+  return 1.f;
+}
+
+template <int K0, int N>
+__global__ __launch_bounds__(FT) void dx_norm_bwd_kernel(Args a, NormBwd nb) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ double red[FT / 64][2];
+  constexpr int S40 = K0 / 8, MT = N / 32, C = N;
+  static_assert(K0 % 8 == 0 && N % 32 == 0, "dx_norm_bwd widths");
+  stage_lds<FT>(lds, a.L[0].src, fbytes(K0, N));
+  const float sp = *nb.sd, mp = *nb.mu;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const long rows = a.rows;
+  const long ntiles = (rows + 31) / 32;
+  const long tstride = (long)gridDim.x * (FT / 64);
+  const float* bias = (const float*)(lds + MT * S40 * 1024);
+  auto fetch = [&](long t, f32x4 (&b)[S40]) {
+    const long row = t * 32 + r;
+    const bool ok = t < ntiles && row < rows;
+    const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 4 * h;
+#pragma unroll
+    for (int s = 0; s < S40; ++s) b[s] = ok ? *(const f32x4*)(p + 8 * s) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  };
+  double acc_s = 0.0, acc_m = 0.0;
+  long tile = (long)blockIdx.x * (FT / 64) + wave;
+  f32x4 nbuf[S40];
+  fetch(tile, nbuf);
+  for (; tile < ntiles; tile += tstride) {
+    f32x4 b[S40];
+#pragma unroll
+    for (int s = 0; s < S40; ++s) b[s] = nbuf[s];
+    fetch(tile + tstride, nbuf);
+    const long row = tile * 32 + r;
+    const bool valid = row < rows;
+    // the row's z (issued before the MFMAs)
+    f32x4 zq[MT][4];
+    const float* zr = nb.z + (size_t)(valid ? row : 0) * nb.ldz + 4 * h;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        zq[m][g] = valid ? *(const f32x4*)(zr + 32 * m + 8 * g) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = bias_frag(bias, m, h);
+    layer<S40, MT, false>(acc, lds, lane, [&](int s4) { return b[s4]; });
+    // acc[m][4g + t] = dA of feature 32 m + 8 g + 4 h + t; zq the same features
+    float t0 = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) t0 += zq[m][g][t];
+    const float mean = add_xor32(t0) / (float)C;
+    float ss = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          zq[m][g][t] = zq[m][g][t] - mean;  // d
+          ss += zq[m][g][t] * zq[m][g][t];
+        }
+    ss = add_xor32(ss);
+    const float stdv = __fsqrt_rn(ss / (float)(C - 1));
+    const float rr = 1.f / (stdv + NORM_EPS);
+    float ps = 0.f, pm = 0.f, A = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float d = zq[m][g][t];
+          const float n = d * rr;
+          const float y = __fadd_rn(__fmul_rn(sp, n), mp);
+          const float gy = acc[m][4 * g + t] * nb_act_grad(y, nb.act);
+          ps += gy * n;
+          pm += gy;
+          const float gn = sp * gy;
+          acc[m][4 * g + t] = gn;
+          A += gn * d;
+        }
+    ps = add_xor32(ps);
+    pm = add_xor32(pm);
+    A = add_xor32(A);
+    if (valid && h == 0) {
+      acc_s += (double)ps;
+      acc_m += (double)pm;
+    }
+    const float coef = stdv > 0.f ? rr * rr * A / ((float)(C - 1) * stdv) : 0.f;
+    float sg = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        acc[m][q] = rr * acc[m][q] - coef * zq[m][q >> 2][q & 3];
+        sg += acc[m][q];
+      }
+    const float mg = add_xor32(sg) / (float)C;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] = acc[m][q] - mg;
+    if (valid) store_out<MT>(acc, a, row, h);
+  }
+  // per-workgroup partials: a fixed butterfly over the wave, the waves in order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    acc_s += __shfl_xor(acc_s, o, 64);
+    acc_m += __shfl_xor(acc_m, o, 64);
+  }
+  if (lane == 0) {
+    red[wave][0] = acc_s;
+    red[wave][1] = acc_m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ts = 0.0, tm = 0.0;
+#pragma unroll
+    for (int w = 0; w < FT / 64; ++w) {
+      ts += red[w][0];
+      tm += red[w][1];
+    }
+    nb.part[2 * blockIdx.x] = ts;
+    nb.part[2 * blockIdx.x + 1] = tm;
+  }
+}
+
+template <int K0, int N>
+static int launch_dxnb(const Args& a, const NormBwd& nb, long blocks, hipStream_t st) {
+  auto kern = dx_norm_bwd_kernel<K0, N>;
+  RG_ENSURE_LDS(kern, DYN_LDS_MAX);
+  kern<<<blocks, FT, fbytes(K0, N), st>>>(a, nb);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 }  // namespace f32c
 }  // namespace rg
 
@@ -790,4 +953,61 @@ extern "C" int rg_mlp_chain_f32_ex(const rg_layer* layers, int n_layers, long ro
              "rg_mlp_chain_f32_ex: gathered input modes need idx0 and idx1");
   return f32_chain_launch(layers, n_layers, rows, rows_dev, in_mode, in0, ld0, w0, in1, ld1, w1, in2,
                           ld2, w2, idx0, idx1, residual, ld_res, out, ld_out, nullptr, 0, stream);
+}
+
+// train.hip: sum of `parts` (s, m) float64 partials in a fixed order into *d_mu / *d_std
+int rg_train_param_reduce(const double* part, int parts, float* d_mu, float* d_std, void* stream);
+
+extern "C" size_t rg_dx_norm_backward_workspace_size(long rows) {
+  const long tiles = (rows + 31) / 32;
+  long blocks = (tiles + 3) / 4;
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  return (size_t)blocks * 2 * sizeof(double);
+}
+
+extern "C" int rg_dx_norm_backward(const rg_layer* layer, long rows, const float* dz_next,
+                                   int ld_dzn, const float* z, int ldz, const float* mu,
+                                   const float* std_, int act, float* dz, int lddz, float* d_mu,
+                                   float* d_std, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+  RG_REQUIRE(layer && layer->w_packed, RG_ERR_ARG, "rg_dx_norm_backward: layer");
+  RG_REQUIRE(mu && std_ && d_mu && d_std && z && dz_next && dz, RG_ERR_ARG,
+             "rg_dx_norm_backward: pointers");
+  RG_REQUIRE(act == ACT_NONE || act == ACT_LEAKY, RG_ERR_UNSUPPORTED, "rg_dx_norm_backward: act");
+  RG_REQUIRE(ld_dzn % 4 == 0 && ldz % 4 == 0 && lddz % 4 == 0, RG_ERR_UNSUPPORTED,
+             "rg_dx_norm_backward: strides must be multiples of 4");
+  RG_REQUIRE((const float*)dz != dz_next && (const float*)dz != z, RG_ERR_ARG,
+             "rg_dx_norm_backward: dz may not alias its inputs");
+  if (rows <= 0) return RG_OK;
+  const size_t need = rg_dx_norm_backward_workspace_size(rows);
+  RG_REQUIRE(workspace && workspace_bytes >= need, RG_ERR_ARG,
+             "rg_dx_norm_backward: workspace %zu < %zu", workspace_bytes, need);
+  const long blocks = (long)(need / (2 * sizeof(double)));
+  Args a;
+  memset(&a, 0, sizeof(a));
+  a.L[0].src = layer->w_packed;
+  a.nl = 1;
+  a.rows = rows;
+  a.in0 = dz_next;
+  a.ld0 = ld_dzn;
+  a.w0real = layer->in_dim;
+  a.out = dz;
+  a.ld_out = lddz;
+  a.out_real = layer->out_dim;
+  NormBwd nb;
+  nb.z = z;
+  nb.ldz = ldz;
+  nb.mu = mu;
+  nb.sd = std_;
+  nb.act = act;
+  nb.part = (double*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = RG_ERR_UNSUPPORTED;
+  const int K = layer->in_dim, N = layer->out_dim;
+  if (K == 64 && N == 128) rc = launch_dxnb<64, 128>(a, nb, blocks, st);
+  else if (K == 128 && N == 128) rc = launch_dxnb<128, 128>(a, nb, blocks, st);
+  else if (K == 64 && N == 64) rc = launch_dxnb<64, 64>(a, nb, blocks, st);
+  if (rc != RG_OK) return rc;
+  return rg_train_param_reduce((const double*)workspace, (int)blocks, d_mu, d_std, stream);
 }

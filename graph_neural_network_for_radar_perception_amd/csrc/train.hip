@@ -70,7 +70,8 @@ template <int J>  // features per lane = J (C <= 16 J)
 __global__ __launch_bounds__(256) void ffn_backward_kernel(
     const float* __restrict__ z, int ldz, const float* __restrict__ da, int ldda, long rows,
     int C, int has_norm, const float* __restrict__ mu, const float* __restrict__ sd, int act,
-    float* __restrict__ dz, int lddz, double* __restrict__ part) {
+    float* __restrict__ dz, int lddz, double* __restrict__ part, const int* __restrict__ gidx,
+    const float* __restrict__ gscale) {
   __shared__ double red[16][2];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 4, q = lane & 15;
@@ -82,11 +83,16 @@ __global__ __launch_bounds__(256) void ffn_backward_kernel(
   for (long row = ((long)blockIdx.x * 4 + wave) * 4 + grp; row < rows;
        row += (long)gridDim.x * 16) {
     float zv[J], gv[J];
+    // gathered input (rg_ffn_backward_gather): da row gidx[row], times gscale[gidx[row]]
+    // (the reference's mean aggregation), rounded as rg_gather_segment_sum forms it
+    const long arow = gidx ? (long)gidx[row] : row;
+    const float gsc = gscale ? gscale[arow] : 1.f;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int f = q + 16 * j;
       zv[j] = f < C ? z[(size_t)row * ldz + f] : 0.f;
-      gv[j] = f < C ? da[(size_t)row * ldda + f] : 0.f;
+      const float g = f < C ? da[(size_t)arow * ldda + f] : 0.f;
+      gv[j] = gscale ? __fmaf_rn(g, gsc, 0.f) : g;
     }
     if (has_norm) {
       float t = 0.f;
@@ -548,14 +554,25 @@ __global__ __launch_bounds__(64 * RW) void linear_grad_reduce(
     o = (int)(t / (in_dim + 1));
     i = (int)(t % (in_dim + 1));
     const int ot = o / oc, oo = o % oc;
-    if (i < in_dim) {
-      const int it = i / ic, ii = i % ic;
-#pragma unroll 8
-      for (int c = wave; c < nchunk; c += RW)
-        s += part[((size_t)(c * ot_n + ot) * it_n + it) * oc * ic + (size_t)oo * ic + ii];
-    } else {
-#pragma unroll 8
-      for (int c = wave; c < nchunk; c += RW) s += part_b[((size_t)c * ot_n + ot) * oc + oo];
+    // U chunks' loads in flight per wave, then summed in chunk order (c = wave, wave + RW,
+    // ...): a 512-chunk reduction is two load rounds per wave instead of four
+    constexpr int U = 16;
+    const bool w_ = i < in_dim;
+    const int it = i / ic, ii = i % ic;
+    const size_t base = w_ ? ((size_t)ot * it_n + it) * oc * ic + (size_t)oo * ic + ii
+                           : (size_t)ot * oc + oo;
+    const size_t cstride = w_ ? (size_t)ot_n * it_n * oc * ic : (size_t)ot_n * oc;
+    const float* src = w_ ? part : part_b;
+    for (int c0 = wave; c0 < nchunk; c0 += RW * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + RW * u;
+        v[u] = c < nchunk ? src[base + (size_t)c * cstride] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (c0 + RW * u < nchunk) s += v[u];
     }
   }
   red[wave][lane] = s;
@@ -984,14 +1001,17 @@ extern "C" size_t rg_ffn_backward_workspace_size(void) {
   return (size_t)FFN_PARTS_MAX * 2 * sizeof(double);
 }
 
-extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
-                               int has_norm, const float* mu, const float* std_, int act,
-                               float* dz, int lddz, float* d_mu, float* d_std, void* workspace,
-                               void* stream) {
+extern "C" int rg_ffn_backward_gather(const float* z, int ldz, const float* da, int ldda,
+                                      const int* gidx, const float* gscale, long rows, int C,
+                                      int has_norm, const float* mu, const float* std_, int act,
+                                      float* dz, int lddz, float* d_mu, float* d_std,
+                                      void* workspace, void* stream) {
   RG_REQUIRE(C >= 1 && C <= 256, RG_ERR_UNSUPPORTED, "rg_ffn_backward: C=%d outside 1..256", C);
   RG_REQUIRE(!has_norm || (mu && std_ && d_mu && d_std && C >= 2 && workspace), RG_ERR_ARG,
              "rg_ffn_backward: norm needs mu, std, their gradients, C >= 2 and a workspace");
   RG_REQUIRE(act >= ACT_NONE && act <= ACT_SWISH, RG_ERR_ARG, "rg_ffn_backward: act %d", act);
+  RG_REQUIRE(!gidx || (const float*)dz != da, RG_ERR_ARG,
+             "rg_ffn_backward_gather: dz may not alias a gathered da");
   if (rows <= 0) return RG_OK;
   hipStream_t st = (hipStream_t)stream;
   double* part = (double*)workspace;
@@ -1002,21 +1022,35 @@ extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldd
   static_assert(parts <= FFN_PARTS_MAX, "ffn backward partials");
   if (C <= 16)
     ffn_backward_kernel<1><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
-                                                  act, dz, lddz, part);
+                                                  act, dz, lddz, part, gidx, gscale);
   else if (C <= 64)
     ffn_backward_kernel<4><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
-                                                  act, dz, lddz, part);
+                                                  act, dz, lddz, part, gidx, gscale);
   else if (C <= 128)
     ffn_backward_kernel<8><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
-                                                  act, dz, lddz, part);
+                                                  act, dz, lddz, part, gidx, gscale);
   else
     ffn_backward_kernel<16><<<parts, 256, 0, st>>>(z, ldz, da, ldda, rows, C, has_norm, mu, std_,
-                                                   act, dz, lddz, part);
+                                                   act, dz, lddz, part, gidx, gscale);
   RG_LAUNCH_CHECK();
   if (has_norm) {
     ffn_param_reduce<<<1, 256, 0, st>>>(part, parts, d_mu, d_std);
     RG_LAUNCH_CHECK();
   }
+  return RG_OK;
+}
+
+extern "C" int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
+                               int has_norm, const float* mu, const float* std_, int act,
+                               float* dz, int lddz, float* d_mu, float* d_std, void* workspace,
+                               void* stream) {
+  return rg_ffn_backward_gather(z, ldz, da, ldda, nullptr, nullptr, rows, C, has_norm, mu, std_,
+                                act, dz, lddz, d_mu, d_std, workspace, stream);
+}
+
+int rg_train_param_reduce(const double* part, int parts, float* d_mu, float* d_std, void* stream) {
+  ffn_param_reduce<<<1, 256, 0, (hipStream_t)stream>>>(part, parts, d_mu, d_std);
+  RG_LAUNCH_CHECK();
   return RG_OK;
 }
 

@@ -53,6 +53,12 @@ N_LOSS_SLOTS = 4
 # GATHER3 tape: a per-node P | Q form of it moved the reference fixture's norm-scale
 # gradients 3 % through LeakyReLU kink flips, profiles/r06_pqe_forward_diag.log.)
 FACTORED_MSG0 = True
+# d msg = d agg[dst] read by the msg chain's last norm backward (rg_ffn_backward_gather)
+# instead of a gather kernel writing it first: the same values, one E-row pass less.
+GATHERED_DMSG = True
+# dX = dZ W fused with the previous ffn_block's norm backward (rg_dx_norm_backward): dA never
+# written; the row sums in the chain layout's order (not rg_ffn_backward's)
+DX_NORM_FUSED = False
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -376,10 +382,19 @@ class TrainChain:
         return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a, segs)
 
     # ------------------------------------------------------------------ backward
+    def accepts_gathered_dout(self) -> bool:
+        """backward(d_gather=...) applies: the last layer's norm / activation backward is
+        row-wise (rg_ffn_backward_gather reads the gathered gradient)."""
+        sp = self.specs[-1]
+        return not sp.frame_norm and (sp.mu is not None or nat.ACT[sp.act] != 0)
+
     def backward(self, tape: ChainTape, d_out: torch.Tensor, grads: Dict[int, torch.Tensor],
                  din: Optional[torch.Tensor] = None, din_accumulate: bool = False,
-                 stop_at_first_linear: bool = False):
+                 stop_at_first_linear: bool = False, d_gather=None):
         """d_out: f32 [rows][out_dim] gradient of the chain output (overwritten).
+        d_gather = (src, col0, idx, scale): the output gradient is src[idx[r]][col0:] (times
+        scale[idx[r]]) instead -- read straight by the last layer's norm backward
+        (rg_ffn_backward_gather), with d_out only its destination.
         Parameter gradients accumulate into grads[id(param)]; with ``din`` the gradient of
         the chain input (dense [rows][in_dim]) is written (or added) there.
         stop_at_first_linear: return dZ of the first layer (its pre-activation gradient) and
@@ -390,11 +405,26 @@ class TrainChain:
         if rows <= 0:
             return None
         dA = d_out
-        for l in range(len(self.specs) - 1, -1, -1):
+        last = len(self.specs) - 1
+        if d_gather is not None and not self.accepts_gathered_dout():
+            raise ValueError('d_gather: the last layer has no row-wise norm / activation')
+        fused = False   # dA already holds this layer's dZ (rg_dx_norm_backward)
+        for l in range(last, -1, -1):
             sp = self.specs[l]
             act = nat.ACT[sp.act]
             has_norm = sp.mu is not None
-            if sp.frame_norm:
+            if fused:
+                fused = False
+            elif l == last and d_gather is not None:
+                g_src, g_col0, g_idx, g_scale = d_gather
+                ws = self.ws.get('ffn', lib.rg_ffn_backward_workspace_size())
+                nat.check(lib.rg_ffn_backward_gather(
+                    tape.z[l].data_ptr(), tape.z[l].stride(0), g_src.data_ptr() + 4 * g_col0,
+                    g_src.stride(0), g_idx.data_ptr(), nat.ptr(g_scale), rows, sp.out_dim,
+                    int(has_norm), nat.ptr(sp.mu), nat.ptr(sp.std), act, dA.data_ptr(),
+                    dA.stride(0), nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
+                    ws.data_ptr(), st), 'rg_ffn_backward_gather')
+            elif sp.frame_norm:
                 seg_ptr, n_seg = tape.segs
                 groups_n = sp.groups if sp.norm == 'group' else 1
                 wsz = lib.rg_frame_norm_backward_workspace_size(n_seg, groups_n)
@@ -438,8 +468,36 @@ class TrainChain:
             else:
                 out = torch.empty((rows, sp.in_dim), dtype=torch.float32, device=self.device)
                 res = None
+                if self._dx_norm(l, rows, dZ, tape.z[l - 1], out, grads):
+                    dA, fused = out, True
+                    continue
             self._dx(l, rows, dZ, out, res)
             dA = out
+
+    def _dx_norm(self, l: int, rows: int, dZ, z_prev, out, grads) -> bool:
+        """out = dZ_{l-1} = the previous ffn_block's norm + activation backward of dZ W_l in
+        one launch (rg_dx_norm_backward) where the shapes allow; False: run the two steps."""
+        prev = self.specs[l - 1]
+        if not (DX_NORM_FUSED and TAPE_F32_FAST and DX_F32_FAST) or prev.mu is None \
+                or prev.frame_norm or nat.ACT[prev.act] not in (0, nat.ACT['leakyrelu']):
+            return False
+        key = ('nb', l)
+        if not self._dx_ok.get(key, True):
+            return False
+        lib = nat.lib()
+        _, fast = self._transposed()[l]
+        wsz = lib.rg_dx_norm_backward_workspace_size(rows)
+        ws = self.ws.get('dxnb', wsz)
+        rc = lib.rg_dx_norm_backward(
+            fast, rows, dZ.data_ptr(), dZ.stride(0), z_prev.data_ptr(), z_prev.stride(0),
+            prev.mu.data_ptr(), prev.std.data_ptr(), nat.ACT[prev.act], out.data_ptr(),
+            out.stride(0), grads[id(prev.mu)].data_ptr(), grads[id(prev.std)].data_ptr(),
+            ws.data_ptr(), ws.numel(), nat.stream_ptr(self.device))
+        if rc == nat.RG_ERR_UNSUPPORTED:
+            self._dx_ok[key] = False
+            return False
+        nat.check(rc, 'rg_dx_norm_backward')
+        return True
 
 
 class TrainConv:
@@ -706,15 +764,21 @@ class TrainEngine:
                         m.data_ptr(), m.stride(0), Cm, g.seg_ptr.data_ptr(), N,
                         d_updin[:, Cin:].data_ptr(), d_updin.stride(0), d_msg.data_ptr(),
                         d_msg.stride(0), st), 'rg_segment_amax_backward')
-            else:
+            gathered = None
+            if cv.aggr != 'max':
                 scale = self._mean_scale(g, N) if cv.aggr == 'mean' else None
-                self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
+                if GATHERED_DMSG and E > 0 and cv.msg.accepts_gathered_dout():
+                    # the msg chain's last norm backward reads d agg[dst] itself
+                    gathered = (d_updin, Cin, g.dst, scale)
+                else:
+                    self._segsum(d_updin, Cin, Cm, eptr, g.dst, scale, d_msg, accumulate=False)
             if FACTORED_MSG0 and E > 0:
-                dz0 = cv.msg.backward(ct['msg'], d_msg, G, stop_at_first_linear=True)
+                dz0 = cv.msg.backward(ct['msg'], d_msg, G, stop_at_first_linear=True,
+                                      d_gather=gathered)
                 self._msg0_backward(cv.msg, ct['msg'], dz0, g, src_ptr, src_lst, dx_new, de)
             else:
                 dG = torch.empty((max(E, 1), cv.msg.in_dim), **f32)
-                cv.msg.backward(ct['msg'], d_msg, G, din=dG)
+                cv.msg.backward(ct['msg'], d_msg, G, din=dG, d_gather=gathered)
                 # x_i = x[dst]: segment sums over the destination-major CSR
                 self._segsum(dG, 0, Cin, g.seg_ptr, None, None, dx_new, accumulate=True)
                 # x_j = x[src]: sums over each node's outgoing positions

@@ -736,6 +736,28 @@ size_t rg_ffn_backward_workspace_size(void);
 int rg_ffn_backward(const float* z, int ldz, const float* da, int ldda, long rows, int C,
                     int has_norm, const float* mu, const float* std_, int act, float* dz,
                     int lddz, float* d_mu, float* d_std, void* workspace, void* stream);
+/* The same with the activation gradient gathered: row r reads da[gidx[r]] (times
+ * gscale[gidx[r]] when gscale is non-NULL) -- d msg = d agg[dst] of the message MLP's last
+ * layer (sum / mean aggregation, gnn_blocks.py:104-113) without materialising d msg;
+ * the same values as rg_gather_segment_sum followed by rg_ffn_backward.  dz may not alias da. */
+int rg_ffn_backward_gather(const float* z, int ldz, const float* da, int ldda, const int* gidx,
+                           const float* gscale, long rows, int C, int has_norm, const float* mu,
+                           const float* std_, int act, float* dz, int lddz, float* d_mu,
+                           float* d_std, void* workspace, void* stream);
+
+/* dA = dz_next W (layer: ONE transposed RG_F32 | RG_PACK_F32_FAST image, in_dim = the width of
+ * dz_next, out_dim = C, as the backward's dX launches use) with the previous ffn_block's
+ * channel_normalization + activation backward (common.py:208-220, 256-267) applied in the
+ * same registers: dz = rg_ffn_backward(z, dA), d_mu / d_std ACCUMULATED -- dA never reaches
+ * memory.  has_norm is implied (mu / std required); act RG_ACT_NONE or RG_ACT_LEAKY; (in_dim,
+ * C) in {(64, 128), (128, 128), (64, 64)}, else RG_ERR_UNSUPPORTED (the caller runs the two
+ * steps).  Row sums in float32, their sums over rows in float64 in a fixed order:
+ * bit-reproducible.  workspace: rg_dx_norm_backward_workspace_size(rows) bytes. */
+size_t rg_dx_norm_backward_workspace_size(long rows);
+int rg_dx_norm_backward(const rg_layer* layer, long rows, const float* dz_next, int ld_dzn,
+                        const float* z, int ldz, const float* mu, const float* std_, int act,
+                        float* dz, int lddz, float* d_mu, float* d_std, void* workspace,
+                        size_t workspace_bytes, void* stream);
 
 /* Weight / bias gradient of nn.Linear (common.py:195): dW[out][in] += sum_r dz[r]^T x[r],
  * db[out] += sum_r dz[r] (db may be NULL), x[r] formed from in0/in1/in2 by in_mode as in

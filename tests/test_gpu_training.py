@@ -449,6 +449,140 @@ def test_gather_segment_sum_stream_matches_sequential(cuda_device):
                 assert torch.equal(got[:, :width], ref[:, :width]), (col0, width, use_list, acc)
 
 
+@pytest.mark.parametrize('K,C,act', [(64, 128, 'leakyrelu'), (128, 128, 'leakyrelu'),
+                                     (64, 64, 'leakyrelu'), (64, 128, 'none')])
+def test_dx_norm_backward_matches_two_steps(cuda_device, K, C, act):
+    """rg_dx_norm_backward (dX = dZ W with the previous ffn_block's channel_normalization +
+    activation backward in the same registers) against the two launches it replaces
+    (rg_mlp_chain_f32_ex on the transposed image, then rg_ffn_backward) and a float64
+    evaluation: dz and the accumulated d mu / d std no further from float64 than 2x the
+    two-step path's error (+ 1e-6 of the scale); 40 017 rows (a partial 32-row tile)."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    dev = cuda_device
+    lib = nat.lib()
+    g = torch.Generator().manual_seed(K + C)
+    rows = 40017
+    W = torch.randn(K, C, generator=g) / K ** 0.5        # the next Linear: C -> K
+    dzn = torch.randn(rows, K, generator=g)
+    z = torch.randn(rows, C, generator=g) * 2.0 + 0.3
+    mu_v, sd_v = 0.2, 1.3
+    st = nat.stream_ptr(dev)
+    fmt = nat.RG_PACK_F32_FAST
+    img = torch.empty(lib.rg_packed_linear_bytes(K, C, fmt), dtype=torch.uint8, device=dev)
+    Wd = W.to(dev)
+    nat.check(lib.rg_pack_linear(Wd.data_ptr(), None, K, C, fmt | nat.RG_PACK_TRANSPOSE,
+                                 img.data_ptr(), st), 'pack')
+    lay = (nat.rg_layer * 1)()
+    lay[0].w_packed = img.data_ptr()
+    lay[0].in_dim, lay[0].out_dim, lay[0].act = K, C, 0
+    dzn_d, z_d = dzn.to(dev), z.to(dev)
+    mu = torch.tensor([mu_v], device=dev)
+    sd = torch.tensor([sd_v], device=dev)
+    a = nat.ACT[act]
+
+    # two steps
+    dA = torch.empty(rows, C, device=dev)
+    nat.check(lib.rg_mlp_chain_f32_ex(lay, 1, rows, None, nat.IN_DENSE, dzn_d.data_ptr(), K, K,
+                                      None, 0, 0, None, 0, 0, None, None, None, 0,
+                                      dA.data_ptr(), C, st), 'dX')
+    ws = torch.empty(lib.rg_ffn_backward_workspace_size(), dtype=torch.uint8, device=dev)
+    gm2, gs2 = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+    nat.check(lib.rg_ffn_backward(z_d.data_ptr(), C, dA.data_ptr(), C, rows, C, 1, mu.data_ptr(),
+                                  sd.data_ptr(), a, dA.data_ptr(), C, gm2.data_ptr(),
+                                  gs2.data_ptr(), ws.data_ptr(), st), 'ffn')
+    # fused
+    dz = torch.empty(rows, C, device=dev)
+    wsz = lib.rg_dx_norm_backward_workspace_size(rows)
+    ws2 = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    gm1, gs1 = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+    nat.check(lib.rg_dx_norm_backward(lay, rows, dzn_d.data_ptr(), K, z_d.data_ptr(), C,
+                                      mu.data_ptr(), sd.data_ptr(), a, dz.data_ptr(), C,
+                                      gm1.data_ptr(), gs1.data_ptr(), ws2.data_ptr(), wsz, st),
+              'rg_dx_norm_backward')
+    torch.cuda.synchronize()
+
+    # float64
+    zz, dA64 = z.double(), dzn.double() @ W.double()
+    mean = zz.mean(1, keepdim=True)
+    d = zz - mean
+    std = (d.pow(2).sum(1, keepdim=True) / (C - 1)).sqrt()
+    r = 1.0 / (std + 1e-5)
+    n = d * r
+    y = sd_v * n + mu_v
+    gy = dA64 * (torch.where(y > 0, 1.0, 0.01) if act == 'leakyrelu' else 1.0)
+    ds, dm = (gy * n).sum(), gy.sum()
+    gn = sd_v * gy
+    A = (gn * d).sum(1, keepdim=True)
+    gd = r * gn - r * r * A * d / ((C - 1) * std)
+    want = gd - gd.mean(1, keepdim=True)
+    scale = float(want.abs().max())
+    e1 = float((dz.cpu().double() - want).abs().max())
+    e2 = float((dA.cpu().double() - want).abs().max())
+    assert e1 <= 2 * e2 + 1e-6 * scale, (e1, e2, scale)
+    for got, ref, two in ((gs1, ds, gs2), (gm1, dm, gm2)):
+        eg, et = abs(float(got) - float(ref)), abs(float(two) - float(ref))
+        assert eg <= 2 * et + 1e-6 * float((gy * n).abs().sum() + gy.abs().sum()), (eg, et)
+    # bit-reproducible
+    dz_b = torch.empty_like(dz)
+    gm3, gs3 = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+    nat.check(lib.rg_dx_norm_backward(lay, rows, dzn_d.data_ptr(), K, z_d.data_ptr(), C,
+                                      mu.data_ptr(), sd.data_ptr(), a, dz_b.data_ptr(), C,
+                                      gm3.data_ptr(), gs3.data_ptr(), ws2.data_ptr(), wsz, st),
+              'rg_dx_norm_backward')
+    torch.cuda.synchronize()
+    assert torch.equal(dz_b, dz) and torch.equal(gm3, gm1) and torch.equal(gs3, gs1)
+
+
+@pytest.mark.parametrize('C,mean', [(64, False), (64, True), (128, False), (5, True)])
+def test_ffn_backward_gather_matches_gather_then_ffn(cuda_device, C, mean):
+    """rg_ffn_backward_gather (d msg = d agg[dst] read inside the norm backward, the training
+    step's message-MLP last layer) against rg_gather_segment_sum writing d msg followed by
+    rg_ffn_backward: dz and the accumulated d mu / d std bit-identical, sum and mean
+    aggregation (the 1/deg scale), a 16-B aligned column window of the update-input gradient
+    and a 5-wide one."""
+    from graph_neural_network_for_radar_perception_amd import _native as nat
+    dev = cuda_device
+    lib = nat.lib()
+    g = torch.Generator().manual_seed(C + 7 * mean)
+    N, E, Cin = 2500, 31000, 64
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g, dtype=torch.int32)).values
+    deg = torch.bincount(dst.long(), minlength=N).clamp(min=1).float()
+    scale = (1.0 / deg).to(dev) if mean else None
+    d_upd = torch.randn(N, Cin + C, generator=g).to(dev)
+    z = torch.randn(E, C, generator=g).to(dev)
+    mu = torch.tensor([0.3], device=dev)
+    sd = torch.tensor([1.7], device=dev)
+    dst_d = dst.to(dev)
+    ws = torch.empty(lib.rg_ffn_backward_workspace_size(), dtype=torch.uint8, device=dev)
+    st = nat.stream_ptr(dev)
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+
+    # reference sequence: gather (identity CSR over the edges, list = dst), then in place
+    d_msg = torch.empty(E, C, device=dev)
+    iota = torch.arange(E + 1, dtype=torch.int32, device=dev)
+    nat.check(lib.rg_gather_segment_sum(d_upd.data_ptr(), d_upd.stride(0), Cin, C,
+                                        iota.data_ptr(), dst_d.data_ptr(), p(scale), E,
+                                        d_msg.data_ptr(), C, 0, st), 'gss')
+    gm0, gs0 = torch.full((1,), 0.25, device=dev), torch.full((1,), -0.5, device=dev)
+    nat.check(lib.rg_ffn_backward(z.data_ptr(), C, d_msg.data_ptr(), C, E, C, 1, mu.data_ptr(),
+                                  sd.data_ptr(), nat.ACT['leakyrelu'], d_msg.data_ptr(), C,
+                                  gm0.data_ptr(), gs0.data_ptr(), ws.data_ptr(), st), 'ffn')
+    dz1 = torch.empty(E, C, device=dev)
+    gm1, gs1 = torch.full((1,), 0.25, device=dev), torch.full((1,), -0.5, device=dev)
+    nat.check(lib.rg_ffn_backward_gather(
+        z.data_ptr(), C, d_upd.data_ptr() + 4 * Cin, d_upd.stride(0), dst_d.data_ptr(), p(scale),
+        E, C, 1, mu.data_ptr(), sd.data_ptr(), nat.ACT['leakyrelu'], dz1.data_ptr(), C,
+        gm1.data_ptr(), gs1.data_ptr(), ws.data_ptr(), st), 'ffn_gather')
+    torch.cuda.synchronize()
+    assert torch.equal(dz1, d_msg)
+    assert torch.equal(gm1, gm0) and torch.equal(gs1, gs0)
+    # aliasing a gathered input is refused
+    assert lib.rg_ffn_backward_gather(
+        z.data_ptr(), C, d_upd.data_ptr(), d_upd.stride(0), dst_d.data_ptr(), None, E, C, 1,
+        mu.data_ptr(), sd.data_ptr(), 1, d_upd.data_ptr(), C, gm1.data_ptr(), gs1.data_ptr(),
+        ws.data_ptr(), st) != 0
+
+
 @pytest.mark.parametrize('shape', [(128, 192, 'gather3'), (64, 128, 'concat2'), (64, 64, 'dense'),
                                    (256, 7, 'dense'), (7, 64, 'dense'), (2, 64, 'pairadd'),
                                    (128, 192, 'gather3', 31), (128, 192, 'gather3', 4096),
