@@ -58,7 +58,7 @@ FACTORED_MSG0 = True
 GATHERED_DMSG = True
 # dX = dZ W fused with the previous ffn_block's norm backward (rg_dx_norm_backward): dA never
 # written; the row sums in the chain layout's order (not rg_ffn_backward's)
-DX_NORM_FUSED = False
+DX_NORM_FUSED = True
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
