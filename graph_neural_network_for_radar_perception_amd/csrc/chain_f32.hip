@@ -375,7 +375,7 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT
   }
   epilogue<SPEC, LI, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
-    if (valid) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
+    if (valid && a.L[LI].as) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
   }
   if constexpr (sizeof...(Rest) > 0) {
     run_rest<SPEC, TAPE, LI + 1, N, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
@@ -400,7 +400,7 @@ __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 
   }
   epilogue<SPEC, 0, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
-    if (valid) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
+    if (valid && a.L[0].as) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
   }
   if constexpr (sizeof...(Rest) > 0) {
     run_rest<SPEC, TAPE, 1, N0, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
@@ -472,7 +472,7 @@ __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1]
   }
   epilogue<SPEC, 1, MT1, TAPE>(acc, nrm);
   if constexpr (TAPE) {
-    if (valid) tape_rows<MT1>(acc, a.L[1].as, a.L[1].out, row, h);
+    if (valid && a.L[1].as) tape_rows<MT1>(acc, a.L[1].as, a.L[1].out, row, h);
   }
   if constexpr (sizeof...(Rest) > 0) {
     run_rest<SPEC, TAPE, 2, N1, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
@@ -688,8 +688,14 @@ __device__ __forceinline__ float nb_act_grad(float y, int act) {
   return 1.f;
 }
 
+#ifndef RG_DXNB_WPS
+#define RG_DXNB_WPS 2  // waves per SIMD (<= 256 registers per lane): one wave's z / dZ loads
+                       // behind the other's MFMAs and epilogue (K0 = 128: one, 99 spills at two)
+#endif
+template <int K0>
+constexpr int dxnb_wps() { return K0 >= 128 ? 1 : RG_DXNB_WPS; }
 template <int K0, int N>
-__global__ __launch_bounds__(FT) void dx_norm_bwd_kernel(Args a, NormBwd nb) {
+__global__ __launch_bounds__(FT, dxnb_wps<K0>()) void dx_norm_bwd_kernel(Args a, NormBwd nb) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ double red[FT / 64][2];
   constexpr int S40 = K0 / 8, MT = N / 32, C = N;
@@ -880,7 +886,10 @@ static int f32_chain_launch(const rg_layer* layers, int n_layers, long rows, con
     const rg_layer& s = layers[l];
     RG_REQUIRE(s.w_packed, RG_ERR_ARG, "rg_mlp_chain_f32: layer %d weights", l);
     if (s.flags & RG_LAYER_CENTERED) return RG_ERR_UNSUPPORTED;
-    if ((s.save_pre != nullptr) != (bool)k.tape || (s.save_out != nullptr) != (bool)k.tape)
+    // (the last layer's save_out may be NULL: its activation is the chain output, which the
+    // backward never reads back -- one [rows][out] write less)
+    if ((s.save_pre != nullptr) != (bool)k.tape ||
+        ((s.save_out != nullptr) != (bool)k.tape && !(k.tape && l == n_layers - 1)))
       return RG_ERR_UNSUPPORTED;
     RG_REQUIRE(!s.norm_mu || (s.norm_std && s.out_dim >= 2), RG_ERR_ARG, "norm params");
     RG_REQUIRE(l == 0 ? s.in_dim == k0 : s.in_dim == layers[l - 1].out_dim, RG_ERR_ARG,

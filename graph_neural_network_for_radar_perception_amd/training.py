@@ -309,17 +309,20 @@ class TrainChain:
         for i in range(n):
             zi = torch.empty((max(rows, 1), self.specs[i].out_dim), dtype=torch.float32, device=dev)
             z.append(zi)
-            a.append(torch.empty_like(zi))
+            if i + 1 < n:
+                a.append(torch.empty_like(zi))
         st = nat.stream_ptr(dev)
         if not self.frame_norm and TAPE_F32_FAST and self._fast_ok.get(mode, True):
             # the register-resident f32 chain with its tape (rg_mlp_chain_f32_ex, exact f32
-            # products on v_mfma_f32_32x32x2_f32): one launch, activations in registers
+            # products on v_mfma_f32_32x32x2_f32): one launch, activations in registers.  The
+            # last layer's activation is not taped (the backward reads a[l - 1] only): the
+            # chain output stands for it when there is no residual
             src = self.plan._f32_layers()
             arr = (nat.rg_layer * n)()
             for i in range(n):
                 ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(src[i]), ctypes.sizeof(nat.rg_layer))
                 arr[i].save_pre = z[i].data_ptr()
-                arr[i].save_out = a[i].data_ptr()
+                arr[i].save_out = a[i].data_ptr() if i + 1 < n else None
             rc = lib.rg_mlp_chain_f32_ex(
                 arr, n, int(rows), None, mode, in0.data_ptr(), in0.stride(0), w0,
                 nat.ptr(in1), in1.stride(0) if in1 is not None else 0, w1,
@@ -328,10 +331,12 @@ class TrainChain:
                 residual.stride(0) if residual is not None else 0, out.data_ptr(), out.stride(0), st)
             if rc == 0:
                 self._fast_ok[mode] = True
+                a.append(out if residual is None else None)
                 return ChainTape(rows, mode, in0, w0, in1, w1, in2, w2, idx0, idx1, z, a, segs)
             if rc != nat.RG_ERR_UNSUPPORTED:
                 nat.check(rc, 'rg_mlp_chain_f32_ex (training tape)')
             self._fast_ok[mode] = False
+        a.append(torch.empty_like(z[-1]))
         if self.frame_norm:
             segs = self._segs(rows, segs)
             groups = [[i] for i in range(n)]

@@ -334,7 +334,8 @@ int rg_mlp_chain_f32(const rg_layer* layers_host, int n_layers, long rows, const
  * gnn_blocks.py:104-113) and RG_IN_CONCAT2 (cat(in0, in1), 64 + 64: the update MLP,
  * :108); optional residual (out = residual + chain, :109); when every layer's save_pre /
  * save_out is set, each layer's z and a rows are written as rg_mlp_chain writes them (the
- * training forward of training.py:66-85).  RG_ERR_UNSUPPORTED (launching nothing) for
+ * training forward of training.py:66-85); the LAST layer's save_out may be NULL (its
+ * activation is the chain output, never read back by the backward).  RG_ERR_UNSUPPORTED (launching nothing) for
  * shapes without an instantiation. */
 int rg_mlp_chain_f32_ex(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
                         int in_mode, const float* in0, int ld0, int w0, const float* in1, int ld1,

@@ -383,7 +383,10 @@ def test_f32_tape_kernel_matches_generic(cuda_device, monkeypatch):
         close(o1, o0, f'{name} out')
         for l in range(len(t1.z)):
             close(t1.z[l], t0.z[l], f'{name} z{l}')
-            close(t1.a[l], t0.a[l], f'{name} a{l}')
+            # (the fast tape leaves the last activation out: the chain output, or nothing
+            # behind a residual -- the backward never reads it)
+            if l + 1 < len(t1.z) or kw.get('residual') is None:
+                close(t1.a[l], t0.a[l], f'{name} a{l}')
         for l, (a, b) in enumerate(zip(d1, d0)):
             close(a, b, f'{name} dX{l}')
 
