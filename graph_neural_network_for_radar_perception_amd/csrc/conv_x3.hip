@@ -508,7 +508,14 @@ constexpr int OFF_BUF = OFF_W2 + 3 * PL2;
 constexpr int TS2 = 68;            // message transpose: row stride (floats)
 constexpr int TBUF = 32 * TS2 * 4;  // per wave: one tile's messages while transposing
 constexpr int RING = 8;             // per wave: P rows of the last RING destinations (slot = node & 7)
-constexpr int BUF = TBUF + RING * HID * 4;
+// ring row stride: a row plus 4 floats, so the rows of two destinations read by one lane group
+// of a ds_read_b128 (bank = dword mod 64) start 4 banks apart instead of on the same banks
+// (at 128 floats every edge group spanning two destinations was a 2-way conflict)
+#ifndef RG_SP_RING_PAD
+#define RG_SP_RING_PAD 4
+#endif
+constexpr int RS = HID + RG_SP_RING_PAD;
+constexpr int BUF = TBUF + RING * RS * 4;
 constexpr int OFF_BIAS = OFF_BUF + NW * BUF;  // layer 2's bias, accumulator order
 constexpr int OFF_NZ = OFF_BIAS + C * 4;       // a row of -0.0: the "P" of a slow-path tile
 constexpr int LDS = OFF_NZ + HID * 4;
@@ -752,7 +759,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   };
   auto ring_store = [&](int dl, const f32x4 (&rp)[2]) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) *(f32x4*)(ring + (ring_row(dl, k) & (sp::RING - 1)) * HID + 4 * r) = rp[k];
+    for (int k = 0; k < 2; ++k) *(f32x4*)(ring + (ring_row(dl, k) & (sp::RING - 1)) * sp::RS + 4 * r) = rp[k];
   };
   // tile accumulator init: Q + P with P from the ring -- or, when the slow path has already
   // added P into q (fast = false: the tile being initialised), from a row of -0.0, which
@@ -761,7 +768,7 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   bool fast = false;  // tile 0's P is in qn
   const float* nzrow = (const float*)(lds + sp::OFF_NZ);
   auto ring_p = [&](int d, int m, f32x4 (&p)[4]) {  // M-tile m of P[d] from the ring
-    const float* rp = (fast ? ring + (d & (sp::RING - 1)) * HID : nzrow) + 4 * h + 32 * m;
+    const float* rp = (fast ? ring + (d & (sp::RING - 1)) * sp::RS : nzrow) + 4 * h + 32 * m;
 #pragma unroll
     for (int g = 0; g < 4; ++g) p[g] = *(const f32x4*)(rp + 8 * g);
   };
@@ -859,7 +866,10 @@ void conv_x3_sp_kernel(Args a, const int* __restrict__ wtab) {
   // ---- prologue: the ring zeroed (its stale slots are only ever multiplied by 0), tile
   //      0's inputs (P straight from memory), tile 1's indices
 #pragma unroll
-  for (int k = 0; k < sp::RING * HID / 256; ++k) *(f32x4*)(ring + 256 * k + 4 * lane) = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < sp::RING * HID / 256; ++k) {
+    const int i = 64 * k + lane;  // piece i % 32 of row i / 32
+    *(f32x4*)(ring + (i >> 5) * sp::RS + 4 * (i & 31)) = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   int q_n = edge_of(0);
   const int d0 = a.dst[q_n], s0 = a.src[q_n];
   f32x4 qn[16], en[8], rp[2];
