@@ -481,8 +481,13 @@ __device__ __forceinline__ void run_chain01(const Args& a, const f32x4 (&bin)[1]
   }
 }
 
-template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int... Ns>
-__global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
+// NT threads per workgroup: 256 = one wave per SIMD, the next tile's input rows prefetched
+// into registers; 512 = two waves per SIMD within 256 registers, no register prefetch (the
+// other wave's work covers the row loads)
+template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int NT, int... Ns>
+__global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
+  static_assert(NT == FT || NT == 2 * FT, "chain_f32: 256 or 512 threads");
+  constexpr bool PF = NT == FT;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ float nrm[2 * RG_MAX_LAYERS];
   using Off = LdsOff<SPEC, 0, K0, Ns...>;
@@ -504,7 +509,7 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
     for (int l = 0; l < NL; ++l) {
       if (!spec_glob(SPEC, l)) {
         const int K = l == 0 ? K0 : Ks[l - 1];
-        stage_lds<FT>(lds + Off::get(l), a.L[l].src, fbytes(K, Ks[l]));
+        stage_lds<NT>(lds + Off::get(l), a.L[l].src, fbytes(K, Ks[l]));
       }
     }
   }
@@ -513,8 +518,8 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
   const int r = lane & 31, h = lane >> 5;
   const long rows = a.rows_dev ? min((long)*a.rows_dev, a.rows) : a.rows;
   const long ntiles = (rows + 31) / 32;
-  const long tstride = (long)gridDim.x * (FT / 64);
-  // layer-0 operands of tile t (prefetched one tile ahead)
+  const long tstride = (long)gridDim.x * (NT / 64);
+  // layer-0 operands of tile t (prefetched one tile ahead at NT = 256)
   auto fetch = [&](long t, f32x4 (&b)[S40]) {
     const long row = t * 32 + r;
     const bool ok = t < ntiles && row < rows;
@@ -567,14 +572,18 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
       }
     }
   };
-  long tile = (long)blockIdx.x * (FT / 64) + wave;
+  long tile = (long)blockIdx.x * (NT / 64) + wave;
   f32x4 nb[S40];
-  fetch(tile, nb);
+  if constexpr (PF) fetch(tile, nb);
   for (; tile < ntiles; tile += tstride) {
     f32x4 b[S40];
+    if constexpr (PF) {
 #pragma unroll
-    for (int s = 0; s < S40; ++s) b[s] = nb[s];
-    fetch(tile + tstride, nb);
+      for (int s = 0; s < S40; ++s) b[s] = nb[s];
+      fetch(tile + tstride, nb);
+    } else {
+      fetch(tile, b);
+    }
     const long row = tile * 32 + r;
     const bool valid = row < rows;
     if constexpr (FUSE01) run_chain01<SPEC, TAPE, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
@@ -582,19 +591,20 @@ __global__ __launch_bounds__(FT) void chain_f32_kernel(Args a) {
   }
 }
 
-template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int... Ns>
+template <int MODE, int K0, int SPEC, bool FUSE01, bool TAPE, int NT, int... Ns>
 static int launch(const Args& a, hipStream_t st) {
   using Off = LdsOff<SPEC, 0, K0, Ns...>;
   constexpr int lds = Off::total();
   static_assert(lds <= DYN_LDS_MAX, "LDS image too large: read more layers from global memory");
-  auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, TAPE, Ns...>;
+  auto kern = chain_f32_kernel<MODE, K0, SPEC, FUSE01, TAPE, NT, Ns...>;
   RG_ENSURE_LDS(kern, DYN_LDS_MAX);
   const long tiles = (a.rows + 31) / 32;
-  long blocks = (tiles + 3) / 4;
+  constexpr int WPG = NT / 64;
+  long blocks = (tiles + WPG - 1) / WPG;
   const long cap = lds <= 76 * 1024 ? 512 : 256;  // persistent: workgroups that fit at once
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  kern<<<blocks, FT, lds, st>>>(a);
+  kern<<<blocks, NT, lds, st>>>(a);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -618,10 +628,13 @@ static bool match(const Key& k, int mode, int k0, int sp, bool tape, std::initia
 static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   constexpr int L = ACT_LEAKY;
 #define RG_F32C(MODE, K0, SP, F01, ...) \
-  if (match(k, MODE, K0, SP, false, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, false, __VA_ARGS__>(a, st);
+  if (match(k, MODE, K0, SP, false, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, false, FT, __VA_ARGS__>(a, st);
   // training forward (rg_mlp_chain_f32_ex with every layer's save_pre / save_out set)
 #define RG_F32T(MODE, K0, SP, F01, ...) \
-  if (match(k, MODE, K0, SP, true, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, true, __VA_ARGS__>(a, st);
+  if (match(k, MODE, K0, SP, true, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, true, FT, __VA_ARGS__>(a, st);
+  // the same at two waves per SIMD (512 threads, no register prefetch)
+#define RG_F32T2(MODE, K0, SP, F01, ...) \
+  if (match(k, MODE, K0, SP, true, {__VA_ARGS__})) return launch<MODE, K0, (SP), F01, true, 2 * FT, __VA_ARGS__>(a, st);
   // edge encoder 7 -> 256 -> 128 -> 128 -> 64 (gnn_blocks.py:19-42, block 0 without norm):
   // layers 0 + 1 (136 KiB) in LDS, layers 2 + 3 (96 KiB) from L2
   RG_F32C(IN_SMALL, 7, spec(L, 0b1110, 0b1111, 0b1100), true, 256, 128, 128, 64)
@@ -638,7 +651,14 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   RG_F32C(IN_DENSE, 64, spec(L, 0b01, 0b01, 0), false, 64, 32)
   // ---- training tapes of the yml architecture (Model_Training.forward, training.py)
   // message MLP 192 -> 128 -> 64 on cat(x_i, x_j, e) (gnn_blocks.py:104-113), 131 KiB in LDS
+#ifndef RG_CF32_MSG_WPS
+#define RG_CF32_MSG_WPS 1  // 2: the 512-thread form (232 VGPRs, no register prefetch): c4 800.8 vs 800.4 frames/s, flat (profiles/r06_c4_msg_wps_ab.log)
+#endif
+#if RG_CF32_MSG_WPS == 2
+  RG_F32T2(IN_GATHER3, 192, spec(L, 0b11, 0b11, 0), false, 128, 64)
+#else
   RG_F32T(IN_GATHER3, 192, spec(L, 0b11, 0b11, 0), false, 128, 64)
+#endif
   // update MLP 128 -> 64 on cat(x, agg), + identity
   RG_F32T(IN_CONCAT2, 128, spec(L, 0b1, 0b1, 0), false, 64)
   // encoders (layer 0's tape written one 32-feature tile at a time)
@@ -661,6 +681,7 @@ static int dispatch(const Key& k, const Args& a, hipStream_t st) {
   RG_F32C(IN_DENSE, 128, spec(L, 0, 0, 0), false, 256)
 #undef RG_F32C
 #undef RG_F32T
+#undef RG_F32T2
   return RG_ERR_UNSUPPORTED;
 }
 
