@@ -64,6 +64,40 @@ def test_segment_reduce_rejects_bad_widths(lib):
     assert rc == 3
 
 
+def test_training_backward_argument_errors(lib):
+    """The round-6 training entries validate before touching the device: an unsupported
+    activation, a dz aliasing its input, a short workspace, and rows <= 0 as a no-op."""
+    arr = (nat.rg_layer * 1)()
+    arr[0].w_packed = 16
+    arr[0].in_dim, arr[0].out_dim = 64, 128
+    f = 4096  # any non-null address: nothing is dereferenced before the checks fail
+    # relu is not fused (the caller runs the two steps)
+    rc = lib.rg_dx_norm_backward(arr, 100, f, 64, f + 64, 128, f, f, nat.ACT['relu'], f + 128,
+                                 128, f, f, f, 1 << 20, None)
+    assert rc == 3 and b'act' in lib.rg_last_error()
+    # dz may not alias dz_next / z
+    rc = lib.rg_dx_norm_backward(arr, 100, f, 64, f + 64, 128, f, f, nat.ACT['leakyrelu'], f,
+                                 128, f, f, f, 1 << 20, None)
+    assert rc == 1 and b'alias' in lib.rg_last_error()
+    # workspace shorter than rg_dx_norm_backward_workspace_size(rows)
+    need = lib.rg_dx_norm_backward_workspace_size(100000)
+    assert need >= 16
+    rc = lib.rg_dx_norm_backward(arr, 100000, f, 64, f + 64, 128, f, f, nat.ACT['leakyrelu'],
+                                 f + 128, 128, f, f, f, need - 8, None)
+    assert rc == 1 and b'workspace' in lib.rg_last_error()
+    # no rows: nothing to do
+    assert lib.rg_dx_norm_backward(arr, 0, f, 64, f + 64, 128, f, f, nat.ACT['leakyrelu'],
+                                   f + 128, 128, f, f, f, 0, None) == 0
+    # a gathered ffn backward may not write over the rows it gathers
+    rc = lib.rg_ffn_backward_gather(f, 64, f + 64, 64, f, None, 10, 64, 1, f, f, 2, f + 64, 64, f,
+                                    f, f, None)
+    assert rc == 1 and b'alias' in lib.rg_last_error()
+    # a column block of dW narrower than the gradient's input width
+    rc = lib.rg_linear_grad_ld(f, 64, 10, 64, 64, nat.IN_DENSE, f, 64, 64, None, 0, 0, None, 0,
+                               0, None, None, f, 32, None, f, 1 << 20, None)
+    assert rc == 1 and b'ld_dw' in lib.rg_last_error()
+
+
 def test_workspace_queries(lib):
     assert lib.rg_build_graph_workspace_size(3000, 1, 3000, 10, 0) > 3000 * 94 * 4
     assert lib.rg_link_pairs_workspace_size(100) > 0
