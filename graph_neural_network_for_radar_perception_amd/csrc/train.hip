@@ -334,19 +334,27 @@ __global__ __launch_bounds__(256) void linear_grad_kernel(const float* __restric
     fetch(rb);
     put();
     __syncthreads();
+    // operands one k-step ahead, as linear_grad_dma_kernel's compute
+    float av[2][OW], bv[2][NT];
+    auto ld = [&](int ks, int u) {
+      const int kr = 4 * ks + (lane >> 4);
+#pragma unroll
+      for (int m = 0; m < OW; ++m) av[u][m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bv[u][n] = sX[kr * SX + 16 * n + (lane & 15)];
+    };
+    ld(0, 0);
 #pragma unroll
     for (int ks = 0; ks < GR / 4; ++ks) {
-      const int kr = 4 * ks + (lane >> 4);
-      float av[OW], bv[NT];
-#pragma unroll
-      for (int m = 0; m < OW; ++m) av[m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
-#pragma unroll
-      for (int n = 0; n < NT; ++n) bv[n] = sX[kr * SX + 16 * n + (lane & 15)];
+      const int u = ks & 1;
+      if (ks + 1 < GR / 4) ld(ks + 1, u ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < OW; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][m], bv[u][n], acc[m][n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (it == 0 && threadIdx.x < OC) {
 #pragma unroll 8
@@ -387,7 +395,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // instruction per row and operand, no register round trip) into two buffers -- block b + 1
 // lands while block b's MFMAs run; the barrier closing block b waits for it.  A partial last
 // block is staged as in linear_grad_kernel.  One workgroup per CU (two 53-KB buffers).
-template <int OW, int NT>
+template <int OW, int NT, bool G3>
 __global__ __launch_bounds__(256) void linear_grad_dma_kernel(const float* __restrict__ dz,
                                                               int lddz, long rows, GradIn in,
                                                               long rpc, float* __restrict__ part,
@@ -411,14 +419,20 @@ __global__ __launch_bounds__(256) void linear_grad_dma_kernel(const float* __res
   // rows wave, wave + 4, ... of the block: their dz and x rows by DMA into buffer b.  A
   // gathered input's row indices come first, in one load (lanes 0-15) and one wait, then
   // broadcast: a per-row index load would wait, in order, for every DMA issued before it
+  // (G3 is a template flag, not the runtime mode: with the index load on any path, the
+  // compiler waits for every load in flight -- this block's DMA included -- at its first
+  // readlane, and each block's issue then cost a full memory round trip before the MFMAs of
+  // the block before it)
   const int f = i0 + 4 * lane;
   auto issue = [&](long rb, int b) {
     float* sZ = glds + b * BUF;
     float* sX = sZ + GR * SZ;
     int iv = 0;
-    if (in.mode == RG_IN_GATHER3 && lane < 2 * (GR / 4)) {
-      const long row = rb + wave + 4 * (lane % (GR / 4));
-      iv = lane < GR / 4 ? in.idx0[row] : in.idx1[row];
+    if constexpr (G3) {
+      if (lane < 2 * (GR / 4)) {
+        const long row = rb + wave + 4 * (lane % (GR / 4));
+        iv = lane < GR / 4 ? in.idx0[row] : in.idx1[row];
+      }
     }
 #pragma unroll
     for (int j = 0; j < GR / 4; ++j) {
@@ -427,8 +441,9 @@ __global__ __launch_bounds__(256) void linear_grad_dma_kernel(const float* __res
       if (lane < OC / 4)
         __builtin_amdgcn_global_load_lds((const void*)(dz + (size_t)row * lddz + o0 + 4 * lane),
                                          (lds_ptr_t)(sZ + rr * SZ), 16, 0, 0);
-      const float* src = x_src(in, row, f, __builtin_amdgcn_readlane(iv, j),
-                               __builtin_amdgcn_readlane(iv, GR / 4 + j));
+      const float* src = G3 ? x_src(in, row, f, __builtin_amdgcn_readlane(iv, j),
+                                    __builtin_amdgcn_readlane(iv, GR / 4 + j))
+                            : x_src(in, row, f, 0, 0);
       if (lane < IC / 4)
         __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(sX + rr * SX), 16, 0, 0);
     }
@@ -436,19 +451,28 @@ __global__ __launch_bounds__(256) void linear_grad_dma_kernel(const float* __res
   auto compute = [&](int b) {
     const float* sZ = glds + b * BUF;
     const float* sX = sZ + GR * SZ;
+    // operands read one k-step ahead (fenced): left to itself the compiler re-used two
+    // registers for the B operands and waited for each LDS read before its two MFMAs
+    float av[2][OW], bv[2][NT];
+    auto ld = [&](int ks, int u) {
+      const int kr = 4 * ks + (lane >> 4);
+#pragma unroll
+      for (int m = 0; m < OW; ++m) av[u][m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bv[u][n] = sX[kr * SX + 16 * n + (lane & 15)];
+    };
+    ld(0, 0);
 #pragma unroll
     for (int ks = 0; ks < GR / 4; ++ks) {
-      const int kr = 4 * ks + (lane >> 4);
-      float av[OW], bv[NT];
-#pragma unroll
-      for (int m = 0; m < OW; ++m) av[m] = sZ[kr * SZ + 16 * (OW * wave + m) + (lane & 15)];
-#pragma unroll
-      for (int n = 0; n < NT; ++n) bv[n] = sX[kr * SX + 16 * n + (lane & 15)];
+      const int u = ks & 1;
+      if (ks + 1 < GR / 4) ld(ks + 1, u ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < OW; ++m)
 #pragma unroll
         for (int n = 0; n < NT; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][m], bv[u][n], acc[m][n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (it == 0 && threadIdx.x < OC) {
 #pragma unroll 8
@@ -597,7 +621,8 @@ static int launch_grad(const GradGeom& g, const float* dz, int lddz, long rows, 
   if (vec_x && vec_z && in.mode != RG_IN_PAIRADD && out_dim % (64 * OW) == 0 &&
       in.in_dim % (16 * NT) == 0 && g.rpc % GR == 0) {
     constexpr int lds = 2 * (GR * grad_stride(64 * OW) + GR * grad_stride(16 * NT)) * 4;
-    auto kern = linear_grad_dma_kernel<OW, NT>;
+    auto kern = in.mode == RG_IN_GATHER3 ? linear_grad_dma_kernel<OW, NT, true>
+                                         : linear_grad_dma_kernel<OW, NT, false>;
     RG_ENSURE_LDS(kern, lds);
     kern<<<dim3(g.nchunk, g.ot, g.it), 256, lds, st>>>(dz, lddz, rows, in, g.rpc, part, part_b);
     return RG_OK;
