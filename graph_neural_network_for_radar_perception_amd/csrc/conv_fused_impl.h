@@ -240,8 +240,8 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
   // this XCD's share of the blocks: contiguous destination ranges (its L2 then holds the
   // neighbourhoods it gathers), dequeued from its own head
   const int xcd = blockIdx.x % NQ;
-  int blo = (int)((long)n_blocks * xcd / NQ);
-  int bhi = (int)((long)n_blocks * (xcd + 1) / NQ);
+  const int blo = __builtin_amdgcn_readfirstlane((int)((long)n_blocks * xcd / NQ));
+  const int bhi = __builtin_amdgcn_readfirstlane((int)((long)n_blocks * (xcd + 1) / NQ));
   int* head = a.counter + CTR_STRIDE * xcd;
   // node range of work block b (its edges are the CSR range seg_ptr[n0] .. seg_ptr[n1])
   auto block_nodes = [&](int b, int& n0, int& n1) {
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     blk = bn0 < s_hi ? 0 : -1;
   } else {
     if (lane == 0) blk = atomicAdd(head, 1);
-    blk = blo + __shfl(blk, 0, 64);
+    blk = blo + __builtin_amdgcn_readfirstlane(blk);  // (lane 0's value: every lane is active)
     if (blk >= bhi) blk = -1;
     if (blk >= 0) block_nodes(blk, bn0, bn1);
   }
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
       nn1 = min(n1 + NB, s_hi);
       nxt = nn0 < s_hi ? 0 : -1;
     } else {
-      nxt = blo + __shfl(nxt_raw, 0, 64);
+      nxt = blo + __builtin_amdgcn_readfirstlane(nxt_raw);
       if (nxt >= bhi) nxt = -1;
       if (nxt >= 0) block_nodes(nxt, nn0, nn1);
     }
@@ -487,15 +487,17 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
     mfma_steps<8, 2, 8, 0>(bu, accu, w2, lane);
     norm_act<ACT, 2>(accu, a.L[2], nrm[4], nrm[5]);
     if (nvalid) {
-      uint16_t* po = a.x_out + (size_t)node * a.ldo;
-      const uint16_t* pr = a.x + (size_t)node * a.ldx;
+      // (row offsets with the lane's 4 h folded in: pointer + lane-offset pairs hoisted out of
+      //  the block loop were the kernel's spilled 64-bit values)
+      uint16_t* po = a.x_out + ((size_t)node * a.ldo + 4 * h);
+      const uint16_t* pr = a.x + ((size_t)node * a.ldx + 4 * h);
       // all residual loads first: interleaved with the stores, each load would wait
       // for the previous store (possible aliasing) -- eight serial round trips
       uint2 rv[2][4];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) rv[m][g] = *(const uint2*)(pr + 32 * m + 8 * g + 4 * h);
+        for (int g = 0; g < 4; ++g) rv[m][g] = *(const uint2*)(pr + 32 * m + 8 * g);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -509,7 +511,7 @@ __global__ __launch_bounds__(CT) void fused_conv_kernel(CArgs a) {
           uint2 o;
           o.x = bf2(v0, v1);
           o.y = bf2(v2, v3);
-          *(uint2*)(po + f0) = o;
+          *(uint2*)(po + (f0 - 4 * h)) = o;
         }
     }
 #if RG_CONV_STAMP
