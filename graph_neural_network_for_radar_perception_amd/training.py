@@ -395,8 +395,10 @@ class TrainChain:
 
     def backward(self, tape: ChainTape, d_out: torch.Tensor, grads: Dict[int, torch.Tensor],
                  din: Optional[torch.Tensor] = None, din_accumulate: bool = False,
-                 stop_at_first_linear: bool = False, d_gather=None):
-        """d_out: f32 [rows][out_dim] gradient of the chain output (overwritten).
+                 stop_at_first_linear: bool = False, d_gather=None, keep_dout: bool = False):
+        """d_out: f32 [rows][out_dim] gradient of the chain output (overwritten unless
+        keep_dout: the last norm backward then writes a buffer of its own instead of a copy
+        being taken by the caller).
         d_gather = (src, col0, idx, scale): the output gradient is src[idx[r]][col0:] (times
         scale[idx[r]]) instead -- read straight by the last layer's norm backward
         (rg_ffn_backward_gather), with d_out only its destination.
@@ -429,24 +431,29 @@ class TrainChain:
                     int(has_norm), nat.ptr(sp.mu), nat.ptr(sp.std), act, dA.data_ptr(),
                     dA.stride(0), nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
                     ws.data_ptr(), st), 'rg_ffn_backward_gather')
-            elif sp.frame_norm:
-                seg_ptr, n_seg = tape.segs
-                groups_n = sp.groups if sp.norm == 'group' else 1
-                wsz = lib.rg_frame_norm_backward_workspace_size(n_seg, groups_n)
-                wsb = self.ws.get('fnorm_bwd', wsz)
-                nat.check(lib.rg_frame_norm_backward(
-                    tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0),
-                    sp.out_dim, groups_n, seg_ptr.data_ptr(), n_seg, sp.mu.data_ptr(),
-                    sp.std.data_ptr(), act, dA.data_ptr(), dA.stride(0),
-                    nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))), wsb.data_ptr(),
-                    wsz, st), 'rg_frame_norm_backward')
-            elif has_norm or act != 0:
-                ws = self.ws.get('ffn', lib.rg_ffn_backward_workspace_size())
-                nat.check(lib.rg_ffn_backward(
-                    tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0), rows,
-                    sp.out_dim, int(has_norm), nat.ptr(sp.mu), nat.ptr(sp.std), act, dA.data_ptr(),
-                    dA.stride(0), nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
-                    ws.data_ptr(), st), 'rg_ffn_backward')
+            elif sp.frame_norm or has_norm or act != 0:
+                # in place, or -- the caller's d_out kept -- into a buffer of its own
+                dst = torch.empty((rows, sp.out_dim), dtype=torch.float32, device=self.device) \
+                    if (keep_dout and l == last) else dA
+                if sp.frame_norm:
+                    seg_ptr, n_seg = tape.segs
+                    groups_n = sp.groups if sp.norm == 'group' else 1
+                    wsz = lib.rg_frame_norm_backward_workspace_size(n_seg, groups_n)
+                    wsb = self.ws.get('fnorm_bwd', wsz)
+                    nat.check(lib.rg_frame_norm_backward(
+                        tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0),
+                        sp.out_dim, groups_n, seg_ptr.data_ptr(), n_seg, sp.mu.data_ptr(),
+                        sp.std.data_ptr(), act, dst.data_ptr(), dst.stride(0),
+                        nat.ptr(grads.get(id(sp.mu))), nat.ptr(grads.get(id(sp.std))),
+                        wsb.data_ptr(), wsz, st), 'rg_frame_norm_backward')
+                else:
+                    ws = self.ws.get('ffn', lib.rg_ffn_backward_workspace_size())
+                    nat.check(lib.rg_ffn_backward(
+                        tape.z[l].data_ptr(), tape.z[l].stride(0), dA.data_ptr(), dA.stride(0),
+                        rows, sp.out_dim, int(has_norm), nat.ptr(sp.mu), nat.ptr(sp.std), act,
+                        dst.data_ptr(), dst.stride(0), nat.ptr(grads.get(id(sp.mu))),
+                        nat.ptr(grads.get(id(sp.std))), ws.data_ptr(), st), 'rg_ffn_backward')
+                dA = dst
             dZ = dA
             if l == 0 and stop_at_first_linear:
                 return dZ
@@ -751,7 +758,7 @@ class TrainEngine:
             Cm = cv.msg.out_dim
             # x_out = ident + upd(cat(x, agg))
             d_updin = torch.empty((N, Cin + Cm), **f32)
-            cv.upd.backward(ct['upd'], dx.clone(), G, din=d_updin)   # (d_out is consumed)
+            cv.upd.backward(ct['upd'], dx, G, din=d_updin, keep_dout=True)
             if cv.res is not None:
                 dx_new = torch.empty((N, Cin), **f32)
                 cv.res.backward(ct['res'], dx, G, din=dx_new)
