@@ -520,61 +520,70 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
   const long ntiles = (rows + 31) / 32;
   const long tstride = (long)gridDim.x * (NT / 64);
   // layer-0 operands of tile t (prefetched one tile ahead at NT = 256)
+  // layer-0 operands of tile t (prefetched one tile ahead at NT = 256).  Every load is
+  // unconditional -- rows past the end read row 0, whose results are never stored -- so the
+  // compiler counts the loads in flight: a load under a branch (or a select of its result)
+  // made it wait for the prefetch it had just issued, every tile.  IN_SMALL's padding
+  // columns are zeroed when the tile is taken (take), not when its loads are issued.
   auto fetch = [&](long t, f32x4 (&b)[S40]) {
     const long row = t * 32 + r;
-    const bool ok = t < ntiles && row < rows;
+    const long rr = (t < ntiles && row < rows) ? row : 0;
     if constexpr (MODE == IN_SMALL) {
-      const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
+      const float* p = a.in0 + (size_t)rr * a.ld0;
       float v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = (ok && 4 * h + u < a.w0real) ? p[4 * h + u] : 0.f;
+      for (int u = 0; u < 4; ++u) v[u] = p[min(4 * h + u, a.w0real - 1)];
       b[0] = (f32x4){v[0], v[1], v[2], v[3]};
     } else if constexpr (MODE == IN_DENSE) {
-      const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 4 * h;
+      const float* p = a.in0 + (size_t)rr * a.ld0 + 4 * h;
 #pragma unroll
-      for (int s = 0; s < S40; ++s) b[s] = ok ? *(const f32x4*)(p + 8 * s) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S40; ++s) b[s] = *(const f32x4*)(p + 8 * s);
     } else if constexpr (MODE == IN_GATHER3) {
       // k-quad s: x[idx0] features 8 s + 4 h (s < 8), x[idx1] (8 <= s < 16), e (s >= 16)
       static_assert(K0 == 3 * GW, "gather3 width");
-      const long rr = ok ? row : 0;
-      const float* pi = a.in0 + (size_t)(ok ? a.idx0[rr] : 0) * a.ld0 + 4 * h;
-      const float* pj = a.in0 + (size_t)(ok ? a.idx1[rr] : 0) * a.ld0 + 4 * h;
+      const float* pi = a.in0 + (size_t)a.idx0[rr] * a.ld0 + 4 * h;
+      const float* pj = a.in0 + (size_t)a.idx1[rr] * a.ld0 + 4 * h;
       const float* pe = a.in2 + (size_t)rr * a.ld2 + 4 * h;
 #pragma unroll
       for (int s = 0; s < S40; ++s) {
         const float* p = s < GW / 8 ? pi + 8 * s : s < GW / 4 ? pj + 8 * (s - GW / 8) : pe + 8 * (s - GW / 4);
         b[s] = *(const f32x4*)p;
       }
-      if (!ok) {
-#pragma unroll
-        for (int s = 0; s < S40; ++s) b[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
     } else if constexpr (MODE == IN_CONCAT2) {
       static_assert(K0 == 2 * GW, "concat2 width");
-      const long rr = ok ? row : 0;
       const float* p0 = a.in0 + (size_t)rr * a.ld0 + 4 * h;
       const float* p1 = a.in1 + (size_t)rr * a.ld1 + 4 * h;
 #pragma unroll
-      for (int s = 0; s < S40; ++s) {
-        const f32x4 v = *(const f32x4*)(s < GW / 8 ? p0 + 8 * s : p1 + 8 * (s - GW / 8));
-        b[s] = ok ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
+      for (int s = 0; s < S40; ++s)
+        b[s] = *(const f32x4*)(s < GW / 8 ? p0 + 8 * s : p1 + 8 * (s - GW / 8));
     } else {
-      const int i = ok ? a.idx0[row] : 0, j = ok ? a.idx1[row] : 0;
-      const float* pi = a.in0 + (size_t)i * a.ld0 + 4 * h;
-      const float* pj = a.in0 + (size_t)j * a.ld0 + 4 * h;
+      const float* pi = a.in0 + (size_t)a.idx0[rr] * a.ld0 + 4 * h;
+      const float* pj = a.in0 + (size_t)a.idx1[rr] * a.ld0 + 4 * h;
 #pragma unroll
       for (int s = 0; s < S40; ++s) {
         const f32x4 xi = *(const f32x4*)(pi + 8 * s), xj = *(const f32x4*)(pj + 8 * s);
-        b[s] = ok ? (f32x4){__fadd_rn(xi.x, xj.x), __fadd_rn(xi.y, xj.y), __fadd_rn(xi.z, xj.z),
-                            __fadd_rn(xi.w, xj.w)}
-                  : (f32x4){0.f, 0.f, 0.f, 0.f};
+        b[s] = (f32x4){__fadd_rn(xi.x, xj.x), __fadd_rn(xi.y, xj.y), __fadd_rn(xi.z, xj.z),
+                       __fadd_rn(xi.w, xj.w)};
       }
+    }
+  };
+  // the operands of a fetched tile as layer 0 takes them (IN_SMALL: padding columns zero)
+  auto take = [&](f32x4 (&b)[S40]) {
+    if constexpr (MODE == IN_SMALL) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (4 * h + u >= a.w0real) b[0][u] = 0.f;
     }
   };
   long tile = (long)blockIdx.x * (NT / 64) + wave;
   f32x4 nb[S40];
-  if constexpr (PF) fetch(tile, nb);
+  if constexpr (PF) {
+    fetch(tile, nb);
+    // the first tile's loads complete before the loop: with them still pending on the way
+    // in, the compiler's wait at the loop top (for the tile fetched one iteration earlier)
+    // could not count past the previous tile's stores and waited for them all (vmcnt(0))
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  }
   for (; tile < ntiles; tile += tstride) {
     f32x4 b[S40];
     if constexpr (PF) {
@@ -584,6 +593,7 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
     } else {
       fetch(tile, b);
     }
+    take(b);
     const long row = tile * 32 + r;
     const bool valid = row < rows;
     if constexpr (FUSE01) run_chain01<SPEC, TAPE, K0, Ns...>(a, b, lds, nrm, row, valid, lane, Off{});
@@ -730,17 +740,17 @@ __global__ __launch_bounds__(FT, dxnb_wps<K0>()) void dx_norm_bwd_kernel(Args a,
   const long ntiles = (rows + 31) / 32;
   const long tstride = (long)gridDim.x * (FT / 64);
   const float* bias = (const float*)(lds + MT * S40 * 1024);
-  auto fetch = [&](long t, f32x4 (&b)[S40]) {
+  auto fetch = [&](long t, f32x4 (&b)[S40]) {  // unconditional loads (chain_f32_kernel's fetch)
     const long row = t * 32 + r;
-    const bool ok = t < ntiles && row < rows;
-    const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0 + 4 * h;
+    const float* p = a.in0 + (size_t)((t < ntiles && row < rows) ? row : 0) * a.ld0 + 4 * h;
 #pragma unroll
-    for (int s = 0; s < S40; ++s) b[s] = ok ? *(const f32x4*)(p + 8 * s) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S40; ++s) b[s] = *(const f32x4*)(p + 8 * s);
   };
   double acc_s = 0.0, acc_m = 0.0;
   long tile = (long)blockIdx.x * (FT / 64) + wave;
   f32x4 nbuf[S40];
   fetch(tile, nbuf);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): see chain_f32_kernel
   for (; tile < ntiles; tile += tstride) {
     f32x4 b[S40];
 #pragma unroll
