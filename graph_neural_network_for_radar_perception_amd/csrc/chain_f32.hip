@@ -100,6 +100,31 @@ __device__ __forceinline__ void tape_rows(const f32x16 (&acc)[MT], float* base, 
     }
 }
 
+#ifndef RG_CF32_TAPE_BUF
+#define RG_CF32_TAPE_BUF 1
+#endif
+// the same rows through a buffer resource for a full-width layer (out = 32 MT): one store per
+// 16 B, issued for every row -- a row past the end gets an offset past the buffer's size and
+// the hardware drops it.  With no branch around them the compiler counts these stores exactly,
+// so the next tile's wait for its prefetched rows does not wait for them as well.
+template <int MT>
+__device__ __forceinline__ void tape_rows_buf(const f32x16 (&acc)[MT], float* base, long rows,
+                                              long row, bool valid, int h) {
+  constexpr int OUT = 32 * MT;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(rows * OUT * 4), 0x00020000);
+  const int off = valid ? (int)(row * OUT * 4) : 0x7ffff000;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+      const u32x4_t v = {__float_as_uint(acc[m][4 * g]), __float_as_uint(acc[m][4 * g + 1]),
+                         __float_as_uint(acc[m][4 * g + 2]), __float_as_uint(acc[m][4 * g + 3])};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + (32 * m + 8 * g + 4 * h) * 4, 0, 0);
+    }
+}
+
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -371,11 +396,13 @@ __device__ __forceinline__ void run_rest(const Args& a, const f32x16 (&prev)[PMT
     return (f32x4){p[q], p[q + 1], p[q + 2], p[q + 3]};
   });
   if constexpr (TAPE) {
-    if (valid) tape_rows<MT>(acc, a.L[LI].zs, a.L[LI].out, row, h);
+    if constexpr (RG_CF32_TAPE_BUF && sizeof...(Rest) > 0) tape_rows_buf<MT>(acc, a.L[LI].zs, a.rows, row, valid, h);
+    else if (valid) tape_rows<MT>(acc, a.L[LI].zs, a.L[LI].out, row, h);
   }
   epilogue<SPEC, LI, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
-    if (valid && a.L[LI].as) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
+    if constexpr (RG_CF32_TAPE_BUF && sizeof...(Rest) > 0) tape_rows_buf<MT>(acc, a.L[LI].as, a.rows, row, valid, h);
+    else if (valid && a.L[LI].as) tape_rows<MT>(acc, a.L[LI].as, a.L[LI].out, row, h);
   }
   if constexpr (sizeof...(Rest) > 0) {
     run_rest<SPEC, TAPE, LI + 1, N, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
@@ -396,11 +423,13 @@ __device__ __forceinline__ void run_chain(const Args& a, const f32x4 (&bin)[(K0 
   for (int m = 0; m < MT; ++m) acc[m] = bias_frag(bias, m, h);
   layer<S4, MT, spec_glob(SPEC, 0)>(acc, w, lane, [&](int s4) { return bin[s4]; });
   if constexpr (TAPE) {
-    if (valid) tape_rows<MT>(acc, a.L[0].zs, a.L[0].out, row, h);
+    if constexpr (RG_CF32_TAPE_BUF && sizeof...(Rest) > 0) tape_rows_buf<MT>(acc, a.L[0].zs, a.rows, row, valid, h);
+    else if (valid) tape_rows<MT>(acc, a.L[0].zs, a.L[0].out, row, h);
   }
   epilogue<SPEC, 0, MT, TAPE>(acc, nrm);
   if constexpr (TAPE) {
-    if (valid && a.L[0].as) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
+    if constexpr (RG_CF32_TAPE_BUF && sizeof...(Rest) > 0) tape_rows_buf<MT>(acc, a.L[0].as, a.rows, row, valid, h);
+    else if (valid && a.L[0].as) tape_rows<MT>(acc, a.L[0].as, a.L[0].out, row, h);
   }
   if constexpr (sizeof...(Rest) > 0) {
     run_rest<SPEC, TAPE, 1, N0, Rest...>(a, acc, lds, nrm, row, valid, lane, Off{});
@@ -520,6 +549,13 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
   const long ntiles = (rows + 31) / 32;
   const long tstride = (long)gridDim.x * (NT / 64);
   // layer-0 operands of tile t (prefetched one tile ahead at NT = 256)
+  // IN_GATHER3: the two row indices of the tile fetch() is called for next
+  int2 gi = {0, 0};
+  auto fetch_idx = [&](long t) {
+    const long row = t * 32 + r;
+    const long rr = (t < ntiles && row < rows) ? row : 0;
+    return int2{a.idx0[rr], a.idx1[rr]};
+  };
   // layer-0 operands of tile t (prefetched one tile ahead at NT = 256).  Every load is
   // unconditional -- rows past the end read row 0, whose results are never stored -- so the
   // compiler counts the loads in flight: a load under a branch (or a select of its result)
@@ -539,10 +575,12 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
 #pragma unroll
       for (int s = 0; s < S40; ++s) b[s] = *(const f32x4*)(p + 8 * s);
     } else if constexpr (MODE == IN_GATHER3) {
-      // k-quad s: x[idx0] features 8 s + 4 h (s < 8), x[idx1] (8 <= s < 16), e (s >= 16)
+      // k-quad s: x[idx0] features 8 s + 4 h (s < 8), x[idx1] (8 <= s < 16), e (s >= 16);
+      // the indices come from gi, loaded one tile earlier (a load used right after its
+      // issue waits for every older memory operation: the previous tile's tape stores)
       static_assert(K0 == 3 * GW, "gather3 width");
-      const float* pi = a.in0 + (size_t)a.idx0[rr] * a.ld0 + 4 * h;
-      const float* pj = a.in0 + (size_t)a.idx1[rr] * a.ld0 + 4 * h;
+      const float* pi = a.in0 + (size_t)gi.x * a.ld0 + 4 * h;
+      const float* pj = a.in0 + (size_t)gi.y * a.ld0 + 4 * h;
       const float* pe = a.in2 + (size_t)rr * a.ld2 + 4 * h;
 #pragma unroll
       for (int s = 0; s < S40; ++s) {
@@ -578,7 +616,9 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
   long tile = (long)blockIdx.x * (NT / 64) + wave;
   f32x4 nb[S40];
   if constexpr (PF) {
+    if constexpr (MODE == IN_GATHER3) gi = fetch_idx(tile);
     fetch(tile, nb);
+    if constexpr (MODE == IN_GATHER3) gi = fetch_idx(tile + tstride);
     // the first tile's loads complete before the loop: with them still pending on the way
     // in, the compiler's wait at the loop top (for the tile fetched one iteration earlier)
     // could not count past the previous tile's stores and waited for them all (vmcnt(0))
@@ -590,7 +630,9 @@ __global__ __launch_bounds__(NT) void chain_f32_kernel(Args a) {
 #pragma unroll
       for (int s = 0; s < S40; ++s) b[s] = nb[s];
       fetch(tile + tstride, nb);
+      if constexpr (MODE == IN_GATHER3) gi = fetch_idx(tile + 2 * tstride);
     } else {
+      if constexpr (MODE == IN_GATHER3) gi = fetch_idx(tile);
       fetch(tile, b);
     }
     take(b);
@@ -939,6 +981,10 @@ static int f32_chain_launch(const rg_layer* layers, int n_layers, long rows, con
     a.L[l].zs = s.save_pre;
     a.L[l].as = s.save_out;
   }
+  // (tape_rows_buf: a non-last layer's tape is a 32-bit-addressed buffer resource)
+  if (k.tape)
+    for (int l = 0; l + 1 < n_layers; ++l)
+      if ((double)rows * k.n[l] * 4 >= 2147483648.0 || layers[l].out_dim != k.n[l]) return RG_ERR_UNSUPPORTED;
   k.spec_lo = spec(ACT_LEAKY, nm, am, 0);
   a.nl = n_layers;
   a.rows = rows;
