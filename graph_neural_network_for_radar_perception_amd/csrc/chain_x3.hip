@@ -130,11 +130,33 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[MT], const float* nrm) {
   }
 }
 
-template <int RT, int MT>
+template <int RT, int MT, bool FULL = false>
 __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Args& a, long row0,
                                            long rows, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int out = a.out_real;
+  if constexpr (FULL) {
+    // full-width, 16-B aligned rows (host-checked): branch-free buffer stores, a row past the
+    // end dropped by the hardware (offset past the buffer) -- the compiler then counts these
+    // stores, and the next tile's wait for its prefetched inputs does not wait for them too
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.out, 0, (int)(((rows - 1) * a.ld_out + 32 * MT) * 4), 0x00020000);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const long row = row0 + 32 * t + r;
+      const int off = row < rows ? (int)((row * a.ld_out + 4 * h) * 4) : 0x7ffff000;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          const u32x4_t v = {__float_as_uint(acc[t][m][4 * g]), __float_as_uint(acc[t][m][4 * g + 1]),
+                             __float_as_uint(acc[t][m][4 * g + 2]), __float_as_uint(acc[t][m][4 * g + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + (32 * m + 8 * g) * 4, 0, 0);
+        }
+    }
+    return;
+  }
   // every feature of the tile stored whole in 16-B pieces (wave-uniform: the encoders' rows),
   // else piece by piece below (padded head outputs; the per-lane test there costs a divergent
   // branch and a saved mask per piece)
@@ -177,6 +199,10 @@ __device__ __forceinline__ void store_rows(const f32x16 (&acc)[RT][MT], const Ar
 
 #ifndef RG_X3_INPF
 #define RG_X3_INPF 1  // encoders: the next tile's input rows loaded during this tile's last layer
+#endif
+#ifndef RG_X3_ENC_BUF
+#define RG_X3_ENC_BUF 1  // encoders: output rows by branch-free buffer stores, next-tile inputs loaded
+                         // unconditionally and masked at use (counted waits; host-checked sizes)
 #endif
 #ifndef RG_X3_SKEW
 #define RG_X3_SKEW 1  // row tile 1's epilogue issued under row tile 0's first k-step of the next
@@ -242,7 +268,8 @@ __device__ __forceinline__ void epilogue_next(f32x16 (&acc)[RT][MT], const float
 // RG_X3_SKEW at RT = 2: row tile 1's epilogue of layer l - 1 not yet run at all)
 // pre: run after the last layer's MFMAs are issued, before its epilogue (the encoders' next-tile
 // input loads: the only loads then in flight, so no weight wait stalls behind them)
-template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND, typename Pre = NoHook>
+template <typename S, int SPEC, int LM, int l, int RT, int PMT, int PEND, bool FULL = false,
+          typename Pre = NoHook>
 __device__ __forceinline__ void run_rest(const Args& a, f32x16 (&prev)[RT][PMT], Pend (&pend)[RT],
                                          const char* lds, const float* nrm, long row0, long rows,
                                          int lane, Pre&& pre = Pre{}) {
@@ -266,13 +293,13 @@ __device__ __forceinline__ void run_rest(const Args& a, f32x16 (&prev)[RT][PMT],
   if constexpr (l + 1 < S::NL) {
     Pend pn[RT];
     epilogue_next<SPEC, l, MT, RT>(acc, nrm, pn);
-    run_rest<S, SPEC, LM, l + 1, RT, MT, pend_kind<SPEC, l>()>(a, acc, pn, lds, nrm, row0, rows,
-                                                              lane, pre);
+    run_rest<S, SPEC, LM, l + 1, RT, MT, pend_kind<SPEC, l>(), FULL>(a, acc, pn, lds, nrm, row0,
+                                                                    rows, lane, pre);
   } else {
     pre();
 #pragma unroll
     for (int t = 0; t < RT; ++t) epilogue<SPEC, l, MT>(acc[t], nrm);
-    store_rows<RT, MT>(acc, a, row0, rows, lane);
+    store_rows<RT, MT, FULL>(acc, a, row0, rows, lane);
   }
 }
 
@@ -412,13 +439,13 @@ __device__ __forceinline__ void run_fused01(const Args& a, const X3 (&b0)[RT][1]
   if constexpr (S::NL > 2) {
     Pend pn[RT];
     epilogue_next<SPEC, 1, MT1, RT>(acc, nrm, pn);
-    run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>()>(a, acc, pn, lds, nrm, row0, rows, lane,
-                                                          pre);
+    run_rest<S, SPEC, LM, 2, RT, MT1, pend_kind<SPEC, 1>(), RG_X3_ENC_BUF>(a, acc, pn, lds, nrm, row0,
+                                                                         rows, lane, pre);
   } else {
     pre();
 #pragma unroll
     for (int t = 0; t < RT; ++t) epilogue<SPEC, 1, MT1>(acc[t], nrm);
-    store_rows<RT, MT1>(acc, a, row0, rows, lane);
+    store_rows<RT, MT1, RG_X3_ENC_BUF>(acc, a, row0, rows, lane);
   }
 }
 
@@ -470,13 +497,19 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
       const bool ok = row < rows;
       const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        vin[t][j] = (ok && h == 0 && j < a.w0real) ? p[j] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (RG_X3_ENC_BUF)
+          vin[t][j] = p[min(j, a.w0real - 1)];  // unconditional (masked at use)
+        else
+          vin[t][j] = (ok && h == 0 && j < a.w0real) ? p[j] : 0.f;
+      }
     }
   };
   if constexpr (MODE == IN_SMALL && RG_X3_INPF) {
     const long t0 = (long)blockIdx.x * (FT / 64) + wave;
     if (t0 < ntiles) load_in(t0);
+    // nothing in flight at the loop entry: the loop-top wait for the prefetched rows is counted
+    if constexpr (RG_X3_ENC_BUF) __builtin_amdgcn_s_waitcnt(0x0f70);
   }
   for (long tile = (long)blockIdx.x * (FT / 64) + wave; tile < ntiles; tile += tstride) {
     const long row0 = tile * TROWS;
@@ -492,7 +525,8 @@ __global__ __launch_bounds__(FT) void chain_x3_kernel(Args a) {
         float v[8];
         if constexpr (RG_X3_INPF) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = vin[t][j];
+          for (int j = 0; j < 8; ++j)
+            v[j] = (!RG_X3_ENC_BUF || (ok && h == 0 && j < a.w0real)) ? vin[t][j] : 0.f;
         } else {
           const float* p = a.in0 + (size_t)(ok ? row : 0) * a.ld0;
 #pragma unroll
@@ -695,5 +729,9 @@ static int chain_x3(const rg_layer* layers, int n_layers, long rows, const int* 
   a.ld_out = ld_out;
   a.out_real = layers[n_layers - 1].out_dim;
   if (rows <= 0) return RG_OK;
+  // encoders' buffer stores (RG_X3_ENC_BUF): full-width 16-B aligned rows, 32-bit byte offsets
+  if (RG_X3_ENC_BUF && k.mode == IN_SMALL &&
+      (a.out_real != k.n[n_layers - 1] || ld_out % 4 != 0 || (double)rows * ld_out * 4 > 0x7ff00000))
+    return RG_ERR_UNSUPPORTED;
   return dispatch(k, a, (hipStream_t)stream);
 }

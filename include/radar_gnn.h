@@ -349,7 +349,10 @@ int rg_mlp_chain_f32_ex(const rg_layer* layers_host, int n_layers, long rows, co
  * RG_PACK_FAST_IN | RG_PACK_X3, later layers RG_PACK_FAST_CHAIN | RG_PACK_X3, no
  * RG_LAYER_CENTERED; in_mode and the rest as rg_mlp_chain_f32 (dense inputs of <= 8 features
  * with an un-normalised first layer, or widths that are multiples of 16).  Returns
- * RG_ERR_UNSUPPORTED (launching nothing) for shapes without an instantiation. */
+ * RG_ERR_UNSUPPORTED (launching nothing) for shapes without an instantiation, and for the
+ * <= 8-input (encoder) shapes also unless the output rows are full width (last out_dim a
+ * multiple of 32), ld_out % 4 == 0 and rows * ld_out * 4 <= 0x7ff00000 (their rows are
+ * written by buffer stores with 32-bit byte offsets). */
 int rg_mlp_chain_x3(const rg_layer* layers_host, int n_layers, long rows, const int* rows_dev,
                     int in_mode, const float* in0, int ld0, int w0, const int* idx0,
                     const int* idx1, float* out, int ld_out, void* stream);
