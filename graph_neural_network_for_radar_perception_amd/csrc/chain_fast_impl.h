@@ -287,6 +287,13 @@ __device__ __forceinline__ void pack_next(const f32x16 (&acc)[MT], bf16x8_t (&nb
 // plain packed stores -- no run-time branches or kernel arguments live across the tile
 static constexpr int SPEC_PLAIN_OUT = 1 << 30;
 
+#ifndef RG_FAST_ENC_BUF
+#define RG_FAST_ENC_BUF 1  // plain outputs by branch-free buffer stores (a row past the end dropped
+                           // by the hardware) and the encoders' next-tile rows loaded
+                           // unconditionally, masked at use: the compiler counts these stores, so
+                           // the loop-top wait for the prefetched rows does not also drain them
+#endif
+
 template <int MT, bool PLAIN = false>
 __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& a, long row,
                                           int h) {
@@ -351,6 +358,28 @@ __device__ __forceinline__ void store_out(const f32x16 (&acc)[MT], const FArgs& 
     }
 }
 
+// a finished tile's rows: plain outputs (host-checked 32-bit byte offsets, plain_out) by buffer
+// stores for every lane, an invalid row's offset past the buffer; else store_out per valid row
+template <int MT, bool PLAIN>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[MT], const FArgs& a, long row,
+                                           bool valid, int h) {
+  if constexpr (PLAIN && RG_FAST_ENC_BUF) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.out, 0, (int)(((a.rows - 1) * a.ld_out + 32 * MT) * 2), 0x00020000);
+    const int off = valid ? (int)((row * a.ld_out + 4 * h) * 2) : 0x7ffff000;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t w = {bf2(acc[m][4 * g], acc[m][4 * g + 1]), bf2(acc[m][4 * g + 2], acc[m][4 * g + 3])};
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs, off + (32 * m + 8 * g) * 2, 0, 0);
+      }
+  } else {
+    if (valid) store_out<MT, PLAIN>(acc, a, row, h);
+  }
+}
+
 template <int SPEC, int OFF, int LI, int K, int N, int... Rest>
 __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K + 15) / 16],
                                           const char* lds, const float* nrm, long row, bool valid,
@@ -367,7 +396,7 @@ __device__ __forceinline__ void run_chain(const FArgs& a, const bf16x8_t (&b)[(K
     run_chain<SPEC, OFF + ((fast_bytes(K, N) + 15) & ~15), LI + 1, N, Rest...>(a, nb, lds, nrm,
                                                                              row, valid, lane);
   } else {
-    if (valid) store_out<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, lane >> 5);
+    store_tile<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, valid, lane >> 5);
   }
 }
 
@@ -398,7 +427,7 @@ __device__ __forceinline__ void run_chain_pair(const FArgs& a,
     run_chain<SPEC, ((fast_bytes(K, N) + 15) & ~15), 1, N, Rest...>(a, nb, lds, nrm, row, valid,
                                                                     lane);
   } else {
-    if (valid) store_out<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, lane >> 5);
+    store_tile<MT, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, valid, lane >> 5);
   }
 }
 
@@ -501,7 +530,7 @@ __device__ __forceinline__ void run_chain01(const FArgs& a, const bf16x8_t (&b)[
     pack_next<MT1>(acc, nb);
     run_chain<SPEC, OFF2, 2, N1, Rest...>(a, nb, lds, nrm, row, valid, lane);
   } else {
-    if (valid) store_out<MT1, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, h);
+    store_tile<MT1, SPEC >= 0 && (SPEC & SPEC_PLAIN_OUT) != 0>(acc, a, row, valid, h);
   }
 }
 
@@ -558,15 +587,32 @@ __global__ __launch_bounds__(FT) void fast_chain_kernel(FArgs a) {
     float nx[8];
     auto fetch = [&](long t, float (&v)[8]) {
       const long r = t * 32 + (lane & 31);
-      const float* p = (const float*)a.in0 + (size_t)r * a.ld0;
-      const bool ok = h == 0 && t < ntiles && r < rows;
+      if constexpr (RG_FAST_ENC_BUF) {  // unconditional: a row past the end reads row 0
+        const float* p = (const float*)a.in0 + (size_t)(r < rows ? r : 0) * a.ld0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ok && j < a.w0real ? p[j] : 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = p[min(j, a.w0real - 1)];
+      } else {
+        const float* p = (const float*)a.in0 + (size_t)r * a.ld0;
+        const bool ok = h == 0 && t < ntiles && r < rows;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ok && j < a.w0real ? p[j] : 0.f;
+      }
     };
     long tile = (long)blockIdx.x * FW + wave;
-    fetch(tile, nx);
+    if constexpr (RG_FAST_ENC_BUF) {
+      if (tile < ntiles) fetch(tile, nx);
+      // nothing in flight at the loop entry: the loop-top wait for the prefetched rows is counted
+      __builtin_amdgcn_s_waitcnt(0x0f70);
+    } else {
+      fetch(tile, nx);
+    }
     for (; tile < ntiles; tile += tstride) {
       bf16x8_t b[1];
+      if constexpr (RG_FAST_ENC_BUF) {  // the mask of this tile's prefetched rows
+        const bool ok = h == 0 && tile * 32 + (lane & 31) < rows;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nx[j] = ok && j < a.w0real ? nx[j] : 0.f;
+      }
       if constexpr (PRE0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx[j] *= LEAKY_PRE;
@@ -630,7 +676,8 @@ static bool match(const Key& k, int mode, int in_f32, int w0, int w1,
 #endif
 // output of width nl written as bf16 rows of 4-wide vectors, no residual
 static bool plain_out(const FArgs& a, int nl) {
-  return !a.res && !a.out_f32 && a.out_vec && a.out_real == nl;
+  return !a.res && !a.out_f32 && a.out_vec && a.out_real == nl &&
+         (!RG_FAST_ENC_BUF || (double)a.rows * a.ld_out * 2 <= 0x7ff00000);  // 32-bit offsets
 }
 
 // instantiations: the yml / BASELINE architecture (C = 64, encoders 256/128, heads 7 / 2)
